@@ -1,0 +1,117 @@
+"""ctypes loader for the C oracle — TEST INFRASTRUCTURE ONLY.
+
+Imported only by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+leg.  Builds oracle/build/liboracle.so on demand with the committed Makefile.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "liboracle.so")
+
+POINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("z", "<f4"), ("rgba", "u1", (4,))])
+
+
+class OrcConfig(C.Structure):
+    _fields_ = [("cell_point_overflow_limit", C.c_uint32), ("sub_grid_dimension", C.c_uint32),
+                ("max_cell_size", C.c_float)]
+
+
+_lib = None
+
+
+def build() -> str:
+    src = os.path.join(HERE, "pcc_oracle.c")
+    if not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < os.path.getmtime(src):
+        subprocess.check_call(["make", "-s", "-C", HERE, "build/liboracle.so"])
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        L.orc_new.restype = C.c_void_p
+        L.orc_new.argtypes = [C.POINTER(OrcConfig)]
+        L.orc_free.argtypes = [C.c_void_p]
+        L.orc_add_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
+        L.orc_add_file.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32]
+        L.orc_write.argtypes = [C.c_void_p, C.c_char_p]
+        L.orc_write.restype = C.c_int
+        L.orc_error.argtypes = [C.c_void_p]
+        L.orc_error.restype = C.c_int
+        L.orc_arrivals.argtypes = [C.c_void_p]
+        L.orc_arrivals.restype = C.c_uint64
+        L.orc_num_cells.argtypes = [C.c_void_p]
+        L.orc_num_cells.restype = C.c_uint64
+        L.orc_hierarchies.argtypes = [C.c_void_p]
+        L.orc_hierarchies.restype = C.c_uint32
+        L.orc_synth.argtypes = [C.c_uint64, C.c_int, C.c_uint64, C.c_uint64, C.c_float, C.c_float, C.c_void_p]
+        _lib = L
+    return _lib
+
+
+def synth(seed: int, kind: int, n: int, first: int = 0, lo: float = -1000.0, ext: float = 2000.0) -> np.ndarray:
+    out = np.empty(n, dtype=POINT_DTYPE)
+    lib().orc_synth(seed, kind, first, n, lo, ext, out.ctypes.data)
+    return out
+
+
+DEFAULT = dict(cell_point_overflow_limit=5000, sub_grid_dimension=96, max_cell_size=1000.0)
+
+
+class Oracle:
+    """Sequential reference restatement (pcc_oracle.c)."""
+
+    def __init__(self, cfg: dict | None = None):
+        cfg = dict(DEFAULT, **(cfg or {}))
+        self.cfg = cfg
+        c = OrcConfig(cfg["cell_point_overflow_limit"], cfg["sub_grid_dimension"], cfg["max_cell_size"])
+        self._h = lib().orc_new(C.byref(c))
+
+    def add_file(self, pts: np.ndarray, batch: int = 10_000):
+        pts = np.ascontiguousarray(pts, dtype=POINT_DTYPE)
+        lib().orc_add_file(self._h, pts.ctypes.data, len(pts), batch)
+
+    def add_batch(self, pts: np.ndarray):
+        pts = np.ascontiguousarray(pts, dtype=POINT_DTYPE)
+        lib().orc_add_batch(self._h, pts.ctypes.data, len(pts))
+
+    def write(self, out_dir: str):
+        r = lib().orc_write(self._h, out_dir.encode())
+        if r:
+            raise OSError(-r, "oracle write failed", out_dir)
+
+    @property
+    def error(self) -> int:
+        return lib().orc_error(self._h)
+
+    @property
+    def arrivals(self) -> int:
+        return lib().orc_arrivals(self._h)
+
+    @property
+    def num_cells(self) -> int:
+        return lib().orc_num_cells(self._h)
+
+    @property
+    def hierarchies(self) -> int:
+        return lib().orc_hierarchies(self._h)
+
+    def close(self):
+        if self._h:
+            lib().orc_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

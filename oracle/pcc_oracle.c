@@ -1,0 +1,534 @@
+/*
+ * pcc_oracle.c — TEST INFRASTRUCTURE ONLY.  Sequential CPU restatement of the
+ * reference `point-converter` hierarchy/LOD build (Seiichi-Yahiro/point-cloud
+ * @ 2024-08-07).  It is the parity checker for the HIP build and the timed
+ * `cpu_baseline` ("port") leg of bench.py.  Nothing in the product
+ * (point-cloud_amd/, include/) links, loads or calls this file.
+ *
+ * PARITY UNPINNED: the reference is Rust and cannot be built in this image
+ * (no cargo/rustc, crates not vendored), and it ships no tests, golden vectors
+ * or fixtures for this path.  This restatement is
+ * pinned instead by (a) an independent pure-Python restatement
+ * (oracle/pyref.py) that must agree with it on every committed fixture, and
+ * (b) hand-derived known-answer tests of the hex/cell arithmetic
+ * (tests/test_oracle_kat.py).
+ *
+ * It follows the reference operation by operation (file:line relative to
+ * /root/reference):
+ *   - hex math              point-converter/src/hex.rs:3-85
+ *   - config formulas       point-converter/src/metadata.rs:80-112
+ *   - Aabb                  bounding-volume/src/lib.rs:23-52
+ *   - Cell::add_point(s)    point-converter/src/cell.rs:70-106
+ *   - add_points_in_overflow cell.rs:108-153
+ *   - group_points / merge  converter.rs:32-60
+ *   - add_points_batch / add_points_in_hierarchy converter.rs:96-139
+ *   - hierarchy folders     converter.rs:141-158
+ *   - new cell header       converter.rs:187-207, cell.rs:43-49, 264-274
+ *   - cell file layout      cell.rs:155-181, 280-298 ; point.rs:26-37
+ *   - metadata.json         metadata.rs:9-57 (serde_json pretty printer)
+ * Cells are kept in memory (mode "(B) in-memory" of BASELINE.md); the LRU(100)
+ * write-back cache of converter.rs:92,160-216 changes only timing, not results.
+ *
+ * Float semantics: compile with -O2 -ffp-contract=off (no FMA contraction, no
+ * fast-math) so every f32 op rounds exactly like the Rust code (rustc never
+ * contracts a*b+c).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/stat.h>
+#include <errno.h>
+
+#define ORC_SQRT_3 1.73205080757f /* hex.rs:3 */
+
+typedef struct { float x, y, z; uint8_t rgba[4]; } orc_point;
+typedef struct { int32_t x, y, z; } ivec3;
+typedef struct { uint32_t cell_point_overflow_limit, sub_grid_dimension; float max_cell_size; } orc_config;
+
+/* ---------------------------------------------------------------- f32 helpers */
+/* Rust `f32 as i32`: saturating, NaN -> 0 */
+static int32_t sat_i32(float v) {
+    if (v != v) return 0;
+    if (v >= 2147483648.0f) return INT32_MAX;
+    if (v <= -2147483648.0f) return INT32_MIN;
+    return (int32_t)v; /* truncation toward zero */
+}
+
+/* metadata.rs:91-93 */
+float orc_cell_size(const orc_config* c, uint32_t h) {
+    uint32_t p = (h >= 32) ? 0u : (1u << h); /* 2u32.pow(h) (wraps to 0 at 32 in release) */
+    return c->max_cell_size / (float)p;
+}
+/* metadata.rs:95-97 */
+float orc_sub_cell_size(const orc_config* c, float cs) { return cs / (float)c->sub_grid_dimension; }
+/* metadata.rs:100-102 : (pos / cell_size).floor().as_ivec3() */
+ivec3 orc_cell_index(float px, float py, float pz, float cs) {
+    ivec3 r = { sat_i32(floorf(px / cs)), sat_i32(floorf(py / cs)), sat_i32(floorf(pz / cs)) };
+    return r;
+}
+/* metadata.rs:104-106 : cell_index.as_vec3() * cell_size + cell_size / 2.0 */
+void orc_cell_pos(ivec3 i, float cs, float out[3]) {
+    float half = cs / 2.0f;
+    out[0] = ((float)i.x * cs) + half;
+    out[1] = ((float)i.y * cs) + half;
+    out[2] = ((float)i.z * cs) + half;
+}
+
+/* hex.rs:67-85 AxialIndex::from_world followed by hex.rs:45-51 to_offset */
+ivec3 orc_hex_from_world(float px, float py, float pz, float cr) {
+    float x = px / (cr * ORC_SQRT_3);
+    float y = py / ((-cr) * ORC_SQRT_3);
+    float t = (ORC_SQRT_3 * y) + 1.0f;
+    float temp1 = floorf(t + x);
+    float temp2 = t - x;
+    float temp3 = (2.0f * x) + 1.0f;
+    float qf = (temp1 + temp3) / 3.0f;
+    float rf = (temp1 + temp2) / 3.0f;
+    int32_t q = sat_i32(floorf(qf));
+    int32_t r = (int32_t)(0u - (uint32_t)sat_i32(floorf(rf))); /* -(x as i32), wrapping */
+    int32_t h = sat_i32(pz / cr);
+    ivec3 o = { q + (r - (r & 1)) / 2, r, h };
+    return o;
+}
+
+/* hex.rs:18-24 to_axial then hex.rs:55-65 AxialIndex::to_world */
+void orc_hex_to_world(ivec3 o, float cr, float out[3]) {
+    int32_t q = o.x - (o.y - (o.y & 1)) / 2;
+    int32_t r = o.y;
+    int32_t h = o.z;
+    float qf = (float)q, rf = (float)r, hf = (float)h;
+    out[0] = cr * ((ORC_SQRT_3 * qf) + ((ORC_SQRT_3 / 2.0f) * rf));
+    out[1] = ((cr * 3.0f) / 2.0f) * rf;
+    out[2] = hf * cr;
+}
+
+/* glam 0.27 Vec3::distance_squared = (a-b).dot(a-b), evaluated left to right */
+static float dist2(const float c[3], float px, float py, float pz) {
+    float dx = c[0] - px, dy = c[1] - py, dz = c[2] - pz;
+    return ((dx * dx) + (dy * dy)) + (dz * dz);
+}
+
+/* ---------------------------------------------------------------- hash map */
+/* open addressing map from up to 4 x int32 keys to uint32 values */
+typedef struct {
+    int32_t* keys;  /* cap * kw */
+    uint32_t* vals;
+    uint8_t* used;
+    size_t cap, count;
+    int kw;
+} hmap;
+
+static uint64_t hkey(const int32_t* k, int kw) {
+    uint64_t h = 0x9E3779B97F4A7C15ull;
+    for (int i = 0; i < kw; i++) {
+        h ^= (uint64_t)(uint32_t)k[i];
+        h *= 0xBF58476D1CE4E5B9ull;
+        h ^= h >> 31;
+    }
+    return h;
+}
+
+static void hm_init(hmap* m, int kw, size_t cap) {
+    size_t c = 16;
+    while (c < cap * 2) c <<= 1;
+    m->kw = kw; m->cap = c; m->count = 0;
+    m->keys = (int32_t*)malloc(c * kw * sizeof(int32_t));
+    m->vals = (uint32_t*)malloc(c * sizeof(uint32_t));
+    m->used = (uint8_t*)calloc(c, 1);
+}
+static void hm_free(hmap* m) { free(m->keys); free(m->vals); free(m->used); memset(m, 0, sizeof(*m)); }
+
+static size_t hm_slot(const hmap* m, const int32_t* k) {
+    size_t mask = m->cap - 1, i = (size_t)hkey(k, m->kw) & mask;
+    while (m->used[i] && memcmp(&m->keys[i * m->kw], k, m->kw * sizeof(int32_t)) != 0) i = (i + 1) & mask;
+    return i;
+}
+static void hm_grow(hmap* m) {
+    hmap n;
+    hm_init(&n, m->kw, m->cap);
+    for (size_t i = 0; i < m->cap; i++)
+        if (m->used[i]) {
+            size_t s = hm_slot(&n, &m->keys[i * m->kw]);
+            n.used[s] = 1; memcpy(&n.keys[s * n.kw], &m->keys[i * m->kw], m->kw * sizeof(int32_t));
+            n.vals[s] = m->vals[i]; n.count++;
+        }
+    hm_free(m); *m = n;
+}
+/* returns pointer to value; *inserted = 1 if new */
+static uint32_t* hm_get_or_insert(hmap* m, const int32_t* k, int* inserted) {
+    if ((m->count + 1) * 2 > m->cap) hm_grow(m);
+    size_t s = hm_slot(m, k);
+    *inserted = !m->used[s];
+    if (!m->used[s]) {
+        m->used[s] = 1; memcpy(&m->keys[s * m->kw], k, m->kw * sizeof(int32_t));
+        m->vals[s] = 0; m->count++;
+    }
+    return &m->vals[s];
+}
+
+/* ---------------------------------------------------------------- point lists */
+typedef struct { orc_point* p; size_t len, cap; } plist;
+static void pl_push(plist* l, orc_point p) {
+    if (l->len == l->cap) { l->cap = l->cap ? l->cap * 2 : 16; l->p = (orc_point*)realloc(l->p, l->cap * sizeof(orc_point)); }
+    l->p[l->len++] = p;
+}
+static void pl_free(plist* l) { free(l->p); memset(l, 0, sizeof(*l)); }
+
+/* ---------------------------------------------------------------- cells */
+typedef struct {
+    ivec3 idx;
+    int state; /* 1 = Some(list), 2 = None (forwarded) ; cell.rs:36-37 */
+    plist pts;
+} bucket;
+
+typedef struct {
+    uint32_t h; ivec3 idx;                 /* CellId cell.rs:14-18 */
+    uint32_t total, number, overflow;      /* Header cell.rs:238-261 */
+    float size, sub, pos[3];
+    hmap grid;                             /* OffsetIndex -> index into gpts */
+    plist gpts;
+    bucket b[8]; int nb;
+} cell;
+
+typedef struct {
+    orc_config cfg;
+    uint64_t number_of_points;
+    uint32_t hierarchies;
+    float bmin[3], bmax[3];
+    hmap cells;        /* (h, x, y, z) -> index into cellv */
+    cell** cellv; size_t ncells, capcells;
+    int error;         /* 1 = hierarchy depth limit reached */
+    uint64_t arrivals; /* sum over levels of points handed to cells (W) */
+} orc_conv;
+
+orc_conv* orc_new(const orc_config* cfg) {
+    orc_conv* c = (orc_conv*)calloc(1, sizeof(orc_conv));
+    c->cfg = *cfg;
+    hm_init(&c->cells, 4, 64);
+    return c;
+}
+
+void orc_free(orc_conv* c) {
+    for (size_t i = 0; i < c->ncells; i++) {
+        cell* k = c->cellv[i];
+        hm_free(&k->grid); pl_free(&k->gpts);
+        for (int j = 0; j < k->nb; j++) pl_free(&k->b[j].pts);
+        free(k);
+    }
+    free(c->cellv); hm_free(&c->cells); free(c);
+}
+
+/* converter.rs:187-207 (create branch) + cell.rs:43-49 + Header::new cell.rs:264-274 */
+static cell* get_cell(orc_conv* c, uint32_t h, ivec3 idx) {
+    int32_t k[4] = { (int32_t)h, idx.x, idx.y, idx.z };
+    int ins;
+    uint32_t* v = hm_get_or_insert(&c->cells, k, &ins);
+    if (!ins) return c->cellv[*v];
+    cell* n = (cell*)calloc(1, sizeof(cell));
+    n->h = h; n->idx = idx;
+    n->size = orc_cell_size(&c->cfg, h);
+    orc_cell_pos(idx, n->size, n->pos);
+    n->sub = orc_sub_cell_size(&c->cfg, n->size);
+    hm_init(&n->grid, 3, 1024);
+    if (c->ncells == c->capcells) {
+        c->capcells = c->capcells ? c->capcells * 2 : 64;
+        c->cellv = (cell**)realloc(c->cellv, c->capcells * sizeof(cell*));
+    }
+    *v = (uint32_t)c->ncells;
+    c->cellv[c->ncells++] = n;
+    return n;
+}
+
+/* cell.rs:70-94 Cell::add_point ; returns 1 and sets *out when a point overflows */
+static int cell_add_point(cell* k, orc_point p, orc_point* out) {
+    float cr = k->sub / 2.0f; /* cell.rs:276-278 */
+    ivec3 s = orc_hex_from_world(p.x, p.y, p.z, cr);
+    int ins;
+    uint32_t* v = hm_get_or_insert(&k->grid, &s.x, &ins);
+    if (ins) {
+        *v = (uint32_t)k->gpts.len;
+        pl_push(&k->gpts, p);
+        k->total += 1; k->number += 1;
+        return 0;
+    }
+    float c[3];
+    orc_hex_to_world(s, k->sub / 2.0f, c);
+    orc_point* old = &k->gpts.p[*v];
+    float od = dist2(c, old->x, old->y, old->z);
+    float nd = dist2(c, p.x, p.y, p.z);
+    if (nd < od) { *out = *old; *old = p; }
+    else *out = p;
+    return 1;
+}
+
+/* group_points converter.rs:32-47: ordered groups keyed by cell index */
+typedef struct { ivec3 idx; plist pts; } group;
+typedef struct { group* g; size_t n, cap; hmap m; } groups;
+
+static void groups_init(groups* G) { memset(G, 0, sizeof(*G)); hm_init(&G->m, 3, 16); }
+static void groups_free(groups* G) {
+    for (size_t i = 0; i < G->n; i++) pl_free(&G->g[i].pts);
+    free(G->g); hm_free(&G->m);
+}
+static plist* groups_entry(groups* G, ivec3 idx) {
+    int ins;
+    uint32_t* v = hm_get_or_insert(&G->m, &idx.x, &ins);
+    if (ins) {
+        if (G->n == G->cap) { G->cap = G->cap ? G->cap * 2 : 8; G->g = (group*)realloc(G->g, G->cap * sizeof(group)); }
+        memset(&G->g[G->n], 0, sizeof(group));
+        G->g[G->n].idx = idx;
+        *v = (uint32_t)G->n++;
+    }
+    return &G->g[*v].pts;
+}
+static void group_points(groups* G, const orc_point* p, size_t n, float cs) {
+    for (size_t i = 0; i < n; i++) pl_push(groups_entry(G, orc_cell_index(p[i].x, p[i].y, p[i].z, cs)), p[i]);
+}
+
+/* cell.rs:108-153 Cell::add_points_in_overflow ; forwarded lists go to `next` */
+static void cell_add_overflow(orc_conv* c, cell* k, groups* og, groups* next) {
+    uint32_t L = c->cfg.cell_point_overflow_limit;
+    for (size_t gi = 0; gi < og->n; gi++) {
+        group* g = &og->g[gi];
+        bucket* b = NULL;
+        for (int j = 0; j < k->nb; j++)
+            if (k->b[j].idx.x == g->idx.x && k->b[j].idx.y == g->idx.y && k->b[j].idx.z == g->idx.z) b = &k->b[j];
+        if (!b) { /* Entry::Vacant */
+            b = &k->b[k->nb++];
+            b->idx = g->idx;
+            if (g->pts.len <= L) {
+                k->total += (uint32_t)g->pts.len; k->overflow += (uint32_t)g->pts.len;
+                b->state = 1; b->pts = g->pts; memset(&g->pts, 0, sizeof(plist));
+            } else {
+                b->state = 2;
+                plist* dst = groups_entry(next, g->idx);
+                for (size_t i = 0; i < g->pts.len; i++) pl_push(dst, g->pts.p[i]);
+            }
+        } else if (b->state == 2) { /* Occupied None */
+            plist* dst = groups_entry(next, g->idx);
+            for (size_t i = 0; i < g->pts.len; i++) pl_push(dst, g->pts.p[i]);
+        } else { /* Occupied Some */
+            uint32_t old_len = (uint32_t)b->pts.len, add = (uint32_t)g->pts.len;
+            for (size_t i = 0; i < g->pts.len; i++) pl_push(&b->pts, g->pts.p[i]);
+            if (b->pts.len < L) {
+                k->total += add; k->overflow += add;
+            } else {
+                k->total -= old_len; k->overflow -= old_len;
+                b->state = 2;
+                plist* dst = groups_entry(next, g->idx);
+                for (size_t i = 0; i < b->pts.len; i++) pl_push(dst, b->pts.p[i]);
+                pl_free(&b->pts);
+            }
+        }
+    }
+}
+
+/* converter.rs:114-139 add_points_in_hierarchy (iterative over levels) */
+static void add_points_in_hierarchy(orc_conv* c, uint32_t h, groups* cur) {
+    for (;;) {
+        if (h >= 31) { c->error = 1; return; } /* reference overflows 2u32.pow(h) at h=32 */
+        if (c->hierarchies <= h) c->hierarchies += 1; /* converter.rs:141-145 */
+        groups next; groups_init(&next);
+        float ccs = orc_cell_size(&c->cfg, h + 1);
+        for (size_t gi = 0; gi < cur->n; gi++) {
+            group* g = &cur->g[gi];
+            cell* k = get_cell(c, h, g->idx);
+            c->arrivals += g->pts.len;
+            plist over = {0};
+            for (size_t i = 0; i < g->pts.len; i++) { /* cell.rs:96-106 */
+                orc_point o;
+                if (cell_add_point(k, g->pts.p[i], &o)) pl_push(&over, o);
+            }
+            groups og; groups_init(&og);
+            group_points(&og, over.p, over.len, ccs); /* converter.rs:67 */
+            pl_free(&over);
+            cell_add_overflow(c, k, &og, &next);      /* converter.rs:68 */
+            groups_free(&og);
+        }
+        groups_free(cur);
+        *cur = next;
+        if (cur->n == 0) { groups_free(cur); return; }
+        h += 1;
+    }
+}
+
+/* converter.rs:96-112 update_bounding_box + add_points_batch */
+void orc_add_batch(orc_conv* c, const orc_point* p, uint64_t n) {
+    if (n > 0) { /* Aabb::from bounding-volume/src/lib.rs:38-52 ; f32::min/max */
+        float mn[3] = { p[0].x, p[0].y, p[0].z }, mx[3] = { p[0].x, p[0].y, p[0].z };
+        for (uint64_t i = 1; i < n; i++) {
+            float v[3] = { p[i].x, p[i].y, p[i].z };
+            for (int a = 0; a < 3; a++) { mn[a] = fminf(mn[a], v[a]); mx[a] = fmaxf(mx[a], v[a]); }
+        }
+        if (c->number_of_points == 0) { memcpy(c->bmin, mn, sizeof mn); memcpy(c->bmax, mx, sizeof mx); }
+        else for (int a = 0; a < 3; a++) { c->bmin[a] = fminf(c->bmin[a], mn[a]); c->bmax[a] = fmaxf(c->bmax[a], mx[a]); }
+    }
+    c->number_of_points += n;
+    groups g; groups_init(&g);
+    group_points(&g, p, (size_t)n, orc_cell_size(&c->cfg, 0));
+    add_points_in_hierarchy(c, 0, &g);
+}
+
+/* lib.rs:31-52: one input file = consecutive get_batch(batch) calls until empty */
+void orc_add_file(orc_conv* c, const orc_point* p, uint64_t n, uint32_t batch) {
+    uint64_t off = 0;
+    do {
+        uint64_t m = n - off < batch ? n - off : batch;
+        orc_add_batch(c, p + off, m);
+        off += m;
+    } while (off < n);
+}
+
+int orc_error(const orc_conv* c) { return c->error; }
+uint64_t orc_arrivals(const orc_conv* c) { return c->arrivals; }
+uint64_t orc_num_cells(const orc_conv* c) { return c->ncells; }
+uint32_t orc_hierarchies(const orc_conv* c) { return c->hierarchies; }
+
+/* ---------------------------------------------------------------- writers */
+static void put_u32(FILE* f, uint32_t v) { fwrite(&v, 4, 1, f); } /* little-endian host */
+static void put_i32(FILE* f, int32_t v) { fwrite(&v, 4, 1, f); }
+static void put_f32(FILE* f, float v) { fwrite(&v, 4, 1, f); }
+
+/* cell.rs:155-181 + Header::write_to cell.rs:280-298 + Point::write_to point.rs:26-37 */
+static int write_cell(const cell* k, const char* path) {
+    FILE* f = fopen(path, "wb");
+    if (!f) return -errno;
+    put_u32(f, k->h); put_i32(f, k->idx.x); put_i32(f, k->idx.y); put_i32(f, k->idx.z);
+    put_u32(f, k->total); put_u32(f, k->number); put_u32(f, k->overflow);
+    put_f32(f, k->size); put_f32(f, k->sub);
+    put_f32(f, k->pos[0]); put_f32(f, k->pos[1]); put_f32(f, k->pos[2]);
+    fwrite(k->gpts.p, sizeof(orc_point), k->gpts.len, f);
+    uint8_t nb = (uint8_t)k->nb;
+    fwrite(&nb, 1, 1, f);
+    for (int j = 0; j < k->nb; j++) {
+        put_i32(f, k->b[j].idx.x); put_i32(f, k->b[j].idx.y); put_i32(f, k->b[j].idx.z);
+        if (k->b[j].state == 1) {
+            put_u32(f, (uint32_t)k->b[j].pts.len);
+            fwrite(k->b[j].pts.p, sizeof(orc_point), k->b[j].pts.len, f);
+        } else put_u32(f, 0);
+    }
+    return fclose(f) == 0 ? 0 : -errno;
+}
+
+/* Shortest round-trip f32 text laid out like ryu::Buffer::format (serde_json
+ * 1.0.114 -> ryu 1.0.17, [dep], Cargo.lock:2657).  Byte layout parity is
+ * unpinned; tests compare parsed values. */
+static void fmt_f32(char* buf, float v) {
+    if (v == 0.0f) { strcpy(buf, signbit(v) ? "-0.0" : "0.0"); return; }
+    if (isinf(v)) { strcpy(buf, v < 0 ? "-inf" : "inf"); return; }
+    if (isnan(v)) { strcpy(buf, "NaN"); return; }
+    char e[48];
+    int p = 1;
+    for (; p <= 9; p++) {
+        snprintf(e, sizeof e, "%.*e", p - 1, (double)v);
+        if (strtof(e, NULL) == v) break;
+    }
+    /* e = [-]d[.ddd]e[+-]xx  -> digits + exponent */
+    char digits[16]; int nd = 0, neg = 0; const char* s = e;
+    if (*s == '-') { neg = 1; s++; }
+    for (; *s && *s != 'e'; s++) if (*s != '.') digits[nd++] = *s;
+    digits[nd] = 0;
+    int ex = atoi(s + 1);             /* value = d.ddd * 10^ex */
+    while (nd > 1 && digits[nd - 1] == '0') digits[--nd] = 0;
+    int k = ex - (nd - 1);            /* value = digits * 10^k */
+    int kk = nd + k;
+    char* o = buf;
+    if (neg) *o++ = '-';
+    if (0 <= k && kk <= 13) {
+        memcpy(o, digits, nd); o += nd;
+        for (int i = 0; i < k; i++) *o++ = '0';
+        strcpy(o, ".0");
+    } else if (0 < kk && kk <= 13) {
+        memcpy(o, digits, kk); o += kk; *o++ = '.';
+        memcpy(o, digits + kk, nd - kk); o += nd - kk; *o = 0;
+    } else if (-6 < kk && kk <= 0) {
+        *o++ = '0'; *o++ = '.';
+        for (int i = 0; i < -kk; i++) *o++ = '0';
+        memcpy(o, digits, nd); o += nd; *o = 0;
+    } else if (nd == 1) {
+        sprintf(o, "%ce%d", digits[0], kk - 1);
+    } else {
+        *o++ = digits[0]; *o++ = '.';
+        memcpy(o, digits + 1, nd - 1); o += nd - 1;
+        sprintf(o, "e%d", kk - 1);
+    }
+}
+
+/* metadata.rs:51-53 serde_json::to_writer_pretty */
+static int write_metadata(const orc_conv* c, const char* path) {
+    FILE* f = fopen(path, "wb");
+    if (!f) return -errno;
+    char b[6][48], ms[48];
+    for (int a = 0; a < 3; a++) { fmt_f32(b[a], c->bmin[a]); fmt_f32(b[3 + a], c->bmax[a]); }
+    fmt_f32(ms, c->cfg.max_cell_size);
+    fprintf(f,
+            "{\n  \"version\": \"1.0\",\n  \"name\": \"Unknown\",\n  \"number_of_points\": %llu,\n"
+            "  \"hierarchies\": %u,\n  \"bounding_box\": {\n    \"min\": [\n      %s,\n      %s,\n      %s\n    ],\n"
+            "    \"max\": [\n      %s,\n      %s,\n      %s\n    ]\n  },\n  \"config\": {\n"
+            "    \"cell_point_overflow_limit\": %u,\n    \"sub_grid_dimension\": %u,\n    \"max_cell_size\": %s\n  }\n}",
+            (unsigned long long)c->number_of_points, c->hierarchies, b[0], b[1], b[2], b[3], b[4], b[5],
+            c->cfg.cell_point_overflow_limit, c->cfg.sub_grid_dimension, ms);
+    return fclose(f) == 0 ? 0 : -errno;
+}
+
+/* converter.rs:141-158, 218-238 : h_{h} folders, every cell, then metadata.json */
+int orc_write(const orc_conv* c, const char* dir) {
+    char path[4096];
+    mkdir(dir, 0755);
+    for (uint32_t h = 0; h < c->hierarchies; h++) {
+        snprintf(path, sizeof path, "%s/h_%u", dir, h);
+        if (mkdir(path, 0755) != 0 && errno != EEXIST) return -errno;
+    }
+    for (size_t i = 0; i < c->ncells; i++) {
+        const cell* k = c->cellv[i];
+        snprintf(path, sizeof path, "%s/h_%u/c_%d_%d_%d.bin", dir, k->h, k->idx.x, k->idx.y, k->idx.z);
+        int r = write_cell(k, path);
+        if (r) return r;
+    }
+    snprintf(path, sizeof path, "%s/metadata.json", dir);
+    return write_metadata(c, path);
+}
+
+/* ---------------------------------------------------------------- synthetic input */
+/* Same generator as the product (point-cloud_amd/csrc/synth.h), restated here so
+ * the oracle never depends on product code.  SURVEY.md §8d. */
+static uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+static uint64_t synth_hash(uint64_t seed, uint64_t i, uint32_t a) {
+    return splitmix64(splitmix64(seed) ^ (i * 4u + a));
+}
+static float synth_unit(uint64_t h) { return (float)(uint32_t)(h >> 40) * (1.0f / 16777216.0f); }
+
+/* kind 0: uniform in [lo, lo+ext)^3 ; kind 1: clustered (32 Irwin-Hall(4) blobs) */
+void orc_synth(uint64_t seed, int kind, uint64_t first, uint64_t n, float lo, float ext, orc_point* out) {
+    for (uint64_t j = 0; j < n; j++) {
+        uint64_t i = first + j;
+        uint64_t hc = synth_hash(seed, i, 3);
+        orc_point p;
+        if (kind == 0) {
+            p.x = lo + ext * synth_unit(synth_hash(seed, i, 0));
+            p.y = lo + ext * synth_unit(synth_hash(seed, i, 1));
+            p.z = lo + ext * synth_unit(synth_hash(seed, i, 2));
+        } else {
+            uint32_t k = (uint32_t)(hc >> 59); /* cluster 0..31 */
+            float c[3], sig;
+            for (int a = 0; a < 3; a++) c[a] = (lo + 0.05f * ext) + (0.9f * ext) * synth_unit(synth_hash(seed ^ 0xC1u, k, (uint32_t)a));
+            sig = 10.0f * (1.0f + 7.0f * synth_unit(synth_hash(seed ^ 0xC2u, k, 0)));
+            float v[3];
+            for (int a = 0; a < 3; a++) {
+                uint64_t h = synth_hash(seed, i, (uint32_t)a);
+                float s = synth_unit(h) + synth_unit(h << 24) + synth_unit(splitmix64(h)) + synth_unit(splitmix64(h) << 24);
+                v[a] = c[a] + sig * (s - 2.0f);
+            }
+            p.x = v[0]; p.y = v[1]; p.z = v[2];
+        }
+        p.rgba[0] = (uint8_t)hc; p.rgba[1] = (uint8_t)(hc >> 8); p.rgba[2] = (uint8_t)(hc >> 16); p.rgba[3] = (uint8_t)(hc >> 24);
+        out[j] = p;
+    }
+}

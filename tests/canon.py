@@ -1,0 +1,115 @@
+"""Canonical form of a converted point cloud directory.
+
+The reference writes grid points in FxHashMap order (cell.rs:158-160) and
+overflow entries in FxHashMap order (cell.rs:164); neither is reproducible, so
+parity is defined on:
+  * per cell: header values (bit-exact f32), grid points keyed by their slot
+    OffsetIndex (recomputed exactly like Cell::read_from, cell.rs:197-203),
+  * overflow entries sorted by child index, each list in STORED order,
+  * metadata.json compared as parsed values.
+"""
+from __future__ import annotations
+
+import json
+import os
+import struct
+
+import numpy as np
+
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "oracle"))
+from pyref import _bits, _pt, hex_from_world  # noqa: E402
+
+F = np.float32
+PT = np.dtype([("x", "<f4"), ("y", "<f4"), ("z", "<f4"), ("rgba", "u1", (4,))])
+
+
+def read_cell(path: str, slots: bool = True) -> dict:
+    with open(path, "rb") as f:
+        data = f.read()
+    h, x, y, z, total, number, overflow = struct.unpack_from("<IiiiIII", data, 0)
+    size, sub, px, py, pz = struct.unpack_from("<5f", data, 28)
+    off = 48
+    grid = np.frombuffer(data, dtype=PT, count=number, offset=off)
+    off += 16 * number
+    nb = data[off]
+    off += 1
+    buckets = []
+    for _ in range(nb):
+        cx, cy, cz, n = struct.unpack_from("<iiiI", data, off)
+        off += 16
+        if n == 0:
+            buckets.append(((cx, cy, cz), None))
+        else:
+            lst = np.frombuffer(data, dtype=PT, count=n, offset=off)
+            off += 16 * n
+            buckets.append(((cx, cy, cz), [_pt((p["x"], p["y"], p["z"], p["rgba"])) for p in lst]))
+    assert off == len(data), f"{path}: trailing bytes"
+    cr = F(F(sub) / F(2.0))
+    if slots:
+        g = sorted((hex_from_world((p["x"], p["y"], p["z"]), cr), _pt((p["x"], p["y"], p["z"], p["rgba"])))
+                   for p in grid)
+    else:
+        g = sorted(_pt((p["x"], p["y"], p["z"], p["rgba"])) for p in grid)
+    return dict(id=(h, x, y, z),
+                header=(total, number, overflow, _bits(F(size)), _bits(F(sub)),
+                        (_bits(F(px)), _bits(F(py)), _bits(F(pz)))),
+                grid=g, buckets=sorted(buckets, key=lambda t: t[0]))
+
+
+def read_dir(out_dir: str, slots: bool = True):
+    cells = {}
+    with open(os.path.join(out_dir, "metadata.json")) as f:
+        meta = json.load(f)
+    for name in sorted(os.listdir(out_dir)):
+        if not name.startswith("h_"):
+            continue
+        hdir = os.path.join(out_dir, name)
+        for fn in os.listdir(hdir):
+            c = read_cell(os.path.join(hdir, fn), slots=slots)
+            assert fn == "c_%d_%d_%d.bin" % c["id"][1:], fn
+            assert name == "h_%d" % c["id"][0]
+            cells[c["id"]] = dict(header=c["header"], grid=c["grid"], buckets=c["buckets"])
+    m = dict(number_of_points=meta["number_of_points"], hierarchies=meta["hierarchies"],
+             bmin=[float(F(v)) for v in meta["bounding_box"]["min"]],
+             bmax=[float(F(v)) for v in meta["bounding_box"]["max"]],
+             config=dict(meta["config"]))
+    return cells, m
+
+
+def diff(a, b, limit: int = 10) -> list[str]:
+    """Human-readable differences between two canonical cell dicts."""
+    out = []
+    for k in sorted(set(a) | set(b)):
+        if k not in a or k not in b:
+            out.append(f"cell {k} only in {'b' if k not in a else 'a'}")
+        else:
+            ca, cb = a[k], b[k]
+            for f in ("header", "grid", "buckets"):
+                if ca[f] != cb[f]:
+                    if f == "grid":
+                        sa, sb = set(ca[f]), set(cb[f])
+                        out.append(f"cell {k} grid: {len(sa - sb)} only-a, {len(sb - sa)} only-b")
+                    elif f == "buckets":
+                        for (ia, la), (ib, lb) in zip(ca[f], cb[f]):
+                            if ia != ib or la != lb:
+                                out.append(f"cell {k} bucket {ia}/{ib}: "
+                                           f"{'None' if la is None else len(la)} vs {'None' if lb is None else len(lb)}")
+                        if len(ca[f]) != len(cb[f]):
+                            out.append(f"cell {k} #buckets {len(ca[f])} vs {len(cb[f])}")
+                    else:
+                        out.append(f"cell {k} {f}: {ca[f]} vs {cb[f]}")
+        if len(out) >= limit:
+            break
+    return out
+
+
+def digest(cells) -> str:
+    """Order-independent digest of canonical cells (for large-config fixtures)."""
+    import hashlib
+    h = hashlib.sha256()
+    for k in sorted(cells):
+        c = cells[k]
+        h.update(repr((k, c["header"], c["grid"], c["buckets"])).encode())
+    return h.hexdigest()
