@@ -1,0 +1,295 @@
+// capi.cpp — extern "C" boundary (include/pcconv.h) over pcc::Engine.
+#include <sys/stat.h>
+
+#include <cerrno>
+#include <chrono>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <ctime>
+#include <fstream>
+#include <memory>
+#include <sstream>
+#include <string>
+
+#include "../../include/pcconv.h"
+#include "engine.h"
+#include "format.h"
+#include "hip_check.h"
+
+using namespace pcc;
+
+static_assert(sizeof(pcc_point) == sizeof(Point), "pcc_point layout");
+
+namespace {
+thread_local std::string g_err;
+
+int set_err(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+// env_logger default format: [<rfc3339 utc> <LEVEL> <target>] msg  (main.rs:29)
+void log_line(const char* level, const char* fmt, ...) {
+    char ts[32];
+    std::time_t t = std::time(nullptr);
+    std::strftime(ts, sizeof ts, "%Y-%m-%dT%H:%M:%SZ", std::gmtime(&t));
+    char msg[2048];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(msg, sizeof msg, fmt, ap);
+    va_end(ap);
+    fprintf(stderr, "[%s %-5s point_converter] %s\n", ts, level, msg);
+}
+
+bool mkdirs(const std::string& d) {
+    if (d.empty()) return true;
+    struct stat st;
+    if (stat(d.c_str(), &st) == 0) return S_ISDIR(st.st_mode);
+    size_t p = d.find_last_of('/');
+    if (p != std::string::npos && p > 0 && !mkdirs(d.substr(0, p))) return false;
+    return mkdir(d.c_str(), 0755) == 0 || errno == EEXIST;
+}
+}  // namespace
+
+struct pcc_converter {
+    std::string out_dir;
+    pcc_options opt;
+    Metadata meta;
+    std::unique_ptr<Engine> eng;
+    bool built = false;
+    double build_ms = 0;
+};
+
+#define GUARD_BEGIN try {
+#define GUARD_END                                            \
+    }                                                        \
+    catch (const std::exception& e) {                        \
+        return set_err(-EIO, std::string("HIP/host error: ") + e.what()); \
+    }
+
+extern "C" {
+
+uint32_t pcc_abi_version(void) { return 1; }
+
+const char* pcc_last_error(void) { return g_err.c_str(); }
+
+int pcc_options_default(pcc_options* o) {
+    if (!o) return set_err(-EINVAL, "null options");
+    o->batch_size = 10000;
+    o->device = 0;
+    o->cell_point_overflow_limit = 5000;
+    o->sub_grid_dimension = 96;
+    o->max_cell_size = 1000.0f;
+    o->reserved = 0;
+    return 0;
+}
+
+int pcc_open(const char* out_dir, const pcc_options* opt, pcc_converter** out) {
+    if (!out_dir || !out) return set_err(-EINVAL, "null argument");
+    GUARD_BEGIN
+    auto c = std::make_unique<pcc_converter>();
+    c->out_dir = out_dir;
+    if (opt) c->opt = *opt; else pcc_options_default(&c->opt);
+    if (c->opt.batch_size == 0) return set_err(-EINVAL, "batch_size must be >= 1");
+    c->meta.config.cell_point_overflow_limit = c->opt.cell_point_overflow_limit;
+    c->meta.config.sub_grid_dimension = c->opt.sub_grid_dimension;
+    c->meta.config.max_cell_size = c->opt.max_cell_size;
+    // lib.rs:86-101 load_metadata
+    const std::string mp = c->out_dir + "/metadata.json";
+    std::ifstream f(mp);
+    if (f) {
+        std::stringstream ss;
+        ss << f.rdbuf();
+        std::string err;
+        Metadata m;
+        if (!parse_metadata_json(ss.str(), m, err)) return set_err(-EINVAL, err);
+        if (m.number_of_points > 0)
+            return set_err(-ENOTSUP, "incremental merge into an existing point cloud is not supported by the GPU build yet");
+        c->meta.config = m.config;
+    }
+    // converter.rs:79-94 create_dir_all
+    if (!mkdirs(c->out_dir)) return set_err(-EIO, "cannot create output directory " + c->out_dir);
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+        return set_err(-ENODEV, "no HIP device available: the MI355X build needs a GPU (there is no CPU fallback)");
+    if (c->opt.device < 0 || c->opt.device >= ndev) return set_err(-ENODEV, "invalid HIP device ordinal");
+    c->eng = std::make_unique<Engine>(c->meta.config, c->opt.device);
+    *out = c.release();
+    return 0;
+    GUARD_END
+}
+
+int pcc_add_points(pcc_converter* c, const pcc_point* pts, uint64_t n) {
+    if (!c || (!pts && n)) return set_err(-EINVAL, "null argument");
+    if (c->built) return set_err(-EINVAL, "points added after build");
+    GUARD_BEGIN
+    c->eng->add_file_host(reinterpret_cast<const Point*>(pts), n, c->opt.batch_size);
+    return 0;
+    GUARD_END
+}
+
+int pcc_add_points_device(pcc_converter* c, const pcc_point* pts, uint64_t n) {
+    if (!c || (!pts && n)) return set_err(-EINVAL, "null argument");
+    if (c->built) return set_err(-EINVAL, "points added after build");
+    GUARD_BEGIN
+    c->eng->add_file_device(reinterpret_cast<const Point*>(pts), n, c->opt.batch_size);
+    return 0;
+    GUARD_END
+}
+
+int pcc_add_empty_batches(pcc_converter* c, uint32_t k) {
+    if (!c) return set_err(-EINVAL, "null argument");
+    if (c->built) return set_err(-EINVAL, "points added after build");
+    c->eng->add_empty_batches(k);
+    return 0;
+}
+
+int pcc_add_synthetic(pcc_converter* c, uint64_t seed, int kind, uint64_t n, float lo, float extent) {
+    if (!c) return set_err(-EINVAL, "null argument");
+    if (c->built) return set_err(-EINVAL, "points added after build");
+    if (kind != 0 && kind != 1) return set_err(-EINVAL, "kind must be 0 (uniform) or 1 (clustered)");
+    GUARD_BEGIN
+    c->eng->add_file_synth(seed, kind, n, c->opt.batch_size, lo, extent);
+    HIP_CHECK(hipStreamSynchronize(c->eng->stream()));
+    return 0;
+    GUARD_END
+}
+
+int pcc_build(pcc_converter* c) {
+    if (!c) return set_err(-EINVAL, "null argument");
+    GUARD_BEGIN
+    const auto t0 = std::chrono::steady_clock::now();
+    const int rc = c->eng->build();
+    HIP_CHECK(hipStreamSynchronize(c->eng->stream()));
+    c->build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (rc) return set_err(rc, c->eng->last_error());
+    c->built = true;
+    Metadata& m = c->meta;   // converter.rs:96-112 + 141-145
+    m.number_of_points = c->eng->num_points();
+    m.hierarchies = c->eng->hierarchies();
+    if (m.number_of_points > 0)
+        for (int a = 0; a < 3; a++) { m.bmin[a] = c->eng->bbox_min()[a]; m.bmax[a] = c->eng->bbox_max()[a]; }
+    return 0;
+    GUARD_END
+}
+
+int pcc_write(pcc_converter* c) {
+    if (!c) return set_err(-EINVAL, "null argument");
+    if (!c->built) {
+        int rc = pcc_build(c);
+        if (rc) return rc;
+    }
+    GUARD_BEGIN
+    std::vector<LevelHost> levels;
+    std::vector<Point> arena, unused;
+    int rc = c->eng->download(levels, arena, unused);
+    if (rc) return set_err(rc, c->eng->last_error());
+    std::string err;
+    rc = write_output(c->out_dir, c->meta, levels, arena, err);
+    if (rc) return set_err(rc, err);
+    return 0;
+    GUARD_END
+}
+
+int pcc_finish(pcc_converter* c) {
+    if (!c) return set_err(-EINVAL, "null argument");
+    const int rc = pcc_write(c);
+    delete c;
+    return rc;
+}
+
+int pcc_close(pcc_converter* c) {
+    delete c;
+    return 0;
+}
+
+int pcc_get_stats(const pcc_converter* c, pcc_stats* s) {
+    if (!c || !s) return set_err(-EINVAL, "null argument");
+    memset(s, 0, sizeof *s);
+    const BuildStats& b = c->eng->stats();
+    s->number_of_points = c->eng->num_points();
+    s->hierarchies = c->eng->hierarchies();
+    s->levels = b.levels;
+    s->cells = b.cells;
+    s->slabs = b.slabs;
+    s->arrivals = b.arrivals;
+    s->grid_points = b.grid_points;
+    s->kept_points = b.kept_points;
+    s->build_ms = c->build_ms;
+    for (int a = 0; a < 3; a++) { s->bbox_min[a] = c->meta.bmin[a]; s->bbox_max[a] = c->meta.bmax[a]; }
+    return 0;
+}
+
+int pcc_set_profiling(pcc_converter* c, int on) {
+    if (!c) return set_err(-EINVAL, "null argument");
+    c->eng->set_profiling(on != 0);
+    return 0;
+}
+
+int pcc_get_profile(const pcc_converter* c, pcc_profile* out) {
+    if (!c || !out) return set_err(-EINVAL, "null argument");
+    const StageProfile& p = c->eng->profile();
+    out->level0_ms = p.level0_ms;
+    out->dense_ms = p.dense_ms;
+    out->small_ms = p.small_ms;
+    out->bucket_ms = p.bucket_ms;
+    out->next_ms = p.next_ms;
+    out->dense_arrivals = p.dense_arrivals;
+    out->small_arrivals = p.small_arrivals;
+    out->dense_launches = p.dense_launches;
+    out->small_launches = p.small_launches;
+    return 0;
+}
+
+const pcc_point* pcc_device_input(const pcc_converter* c) {
+    return c ? reinterpret_cast<const pcc_point*>(c->eng->device_input()) : nullptr;
+}
+
+// lib.rs:11-60 convert_from_paths
+int pcc_convert_files(const char* out_dir, const char* const* paths, size_t npaths, const pcc_options* opt) {
+    pcc_converter* c = nullptr;
+    {
+        std::ifstream f(std::string(out_dir) + "/metadata.json");
+        if (f) log_line("INFO", "Found an existing metadata file.");
+        else log_line("INFO", "Found no metadata file. A new one will be created.");
+    }
+    int rc = pcc_open(out_dir, opt, &c);
+    if (rc) return rc;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (size_t i = 0; i < npaths; i++) {
+        const std::string p = paths[i];
+        log_line("INFO", "Converting file %zu/%zu, \"%s\"", i + 1, npaths, p.c_str());
+        const size_t dot = p.find_last_of('.');
+        const size_t slash = p.find_last_of('/');
+        std::string ext = (dot == std::string::npos || (slash != std::string::npos && dot < slash)) ? "" : p.substr(dot + 1);
+        if (ext == "ply") {
+            PlyResult r;
+            std::string err;
+            if (!read_ply(p, r, err)) {
+                pcc_close(c);
+                return set_err(-EIO, err);   // the reference unwraps reader construction (ply.rs:20-21)
+            }
+            log_line("INFO", "Converting %llu points", (unsigned long long)r.vertex_count);
+            if (r.ascii) {
+                const uint64_t b = c->opt.batch_size;
+                rc = pcc_add_empty_batches(c, (uint32_t)std::max<uint64_t>(1, (r.vertex_count + b - 1) / b));
+            } else {
+                rc = pcc_add_points(c, reinterpret_cast<const pcc_point*>(r.points.data()), r.points.size());
+            }
+            if (rc) { pcc_close(c); return rc; }
+        } else if (ext == "las" || ext == "laz" || ext == "json") {
+            log_line("ERROR", "'%s' input is not supported by this build yet (LAS/LAZ and point-cloud merge are "
+                     "listed as next steps in DESIGN.md)", ext.c_str());
+        } else {
+            log_line("WARN", "Unsupported file format '%s'", ext.c_str());   // lib.rs:78-81
+        }
+    }
+    rc = pcc_build(c);
+    if (rc) { pcc_close(c); return rc; }
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    log_line("INFO", "Finished converting after %llu ms", (unsigned long long)ms);   // lib.rs:56-59
+    return pcc_finish(c);
+}
+
+}  // extern "C"

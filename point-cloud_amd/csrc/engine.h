@@ -1,0 +1,123 @@
+// engine.h — device-resident hierarchy/LOD build for MI355X (gfx950).
+//
+// Reference path replaced: point-converter/src/converter.rs:96-139
+// (add_points_batch -> add_points_in_hierarchy, per batch, per level) together
+// with cell.rs:70-153 (grid LOD + overflow buckets).  The engine runs the
+// SURVEY.md Appendix C level-synchronous restatement: all batches at once,
+// one pass per level over "slabs" = (cell, hex z-layer), each slab processed
+// by one workgroup with its slot table in LDS.  See DESIGN.md.
+#pragma once
+#include <stdint.h>
+#include <stddef.h>
+#include <string>
+#include <vector>
+
+#include <hip/hip_runtime.h>
+
+namespace pcc {
+
+struct Point { float x, y, z; uint8_t rgba[4]; };  // == point.rs:8-14 on-disk record (16 B)
+static_assert(sizeof(Point) == 16, "Point must be 16 bytes");
+
+struct Config {                     // metadata.rs:67-88
+    uint32_t cell_point_overflow_limit = 5000;
+    uint32_t sub_grid_dimension = 96;
+    float max_cell_size = 1000.0f;
+};
+
+// Host copy of one level's results (filled by Engine::download()).
+struct LevelHost {
+    uint32_t h = 0;
+    std::vector<int32_t> cell_idx;      // 3 per cell
+    std::vector<uint32_t> cell_slab0;   // ncells + 1
+    std::vector<uint32_t> slab_grid_off, slab_grid_n;
+    std::vector<uint32_t> bkt_state;    // 8 per cell: 0 absent, 1 kept (Some), 2 spilled (None)
+    std::vector<uint32_t> bkt_off, bkt_n;
+};
+
+struct StageProfile {
+    double level0_ms = 0, dense_ms = 0, small_ms = 0, bucket_ms = 0, next_ms = 0;
+    uint64_t dense_arrivals = 0, small_arrivals = 0;
+    uint32_t dense_launches = 0, small_launches = 0;
+};
+
+struct BuildStats {
+    uint32_t levels = 0;
+    uint64_t cells = 0, slabs = 0, arrivals = 0;   // arrivals = W
+    uint64_t grid_points = 0, kept_points = 0;
+    double ms_total = 0, ms_level0_bin = 0;
+    std::vector<double> ms_level;                  // per level (slab + bucket kernels)
+};
+
+class Engine {
+public:
+    Engine(const Config& cfg, int device, hipStream_t stream = nullptr);
+    ~Engine();
+    Engine(const Engine&) = delete;
+    Engine& operator=(const Engine&) = delete;
+
+    // Reserve device input capacity for n points (also sizes the arenas).
+    void reserve(uint64_t n);
+    // Append a "file": n points (host or device pointer) = ceil(n/batch) batches
+    // (lib.rs:31-52: a file end is a batch boundary).  batch >= 1.
+    void add_file_host(const Point* pts, uint64_t n, uint32_t batch);
+    void add_file_device(const Point* dpts, uint64_t n, uint32_t batch);
+    // A file whose reader yields k empty batches (ASCII PLY quirk, ply.rs:43-51).
+    void add_empty_batches(uint32_t k) { nbatches_ += k; }
+    // Synthetic input generated straight into HBM (bench / tests).
+    void add_file_synth(uint64_t seed, int kind, uint64_t n, uint32_t batch, float lo, float ext);
+
+    // Run the whole build on the device.  Returns 0 or a negative error code
+    // (message in last_error()).  Input must already be resident.
+    int build();
+    int download(std::vector<LevelHost>& levels, std::vector<Point>& grid, std::vector<Point>& kept);
+
+    uint64_t num_points() const { return n_; }
+    uint32_t num_batches() const { return nbatches_; }
+    const float* bbox_min() const { return bmin_; }
+    const float* bbox_max() const { return bmax_; }
+    uint32_t hierarchies() const { return hierarchies_; }
+    const BuildStats& stats() const { return stats_; }
+    void set_profiling(bool on) { profiling_ = on; }
+    const StageProfile& profile() const { return prof_; }
+    const std::string& last_error() const { return err_; }
+    hipStream_t stream() const { return stream_; }
+
+    // device pointer of the input (16 B AoS points), for benchmarking
+    Point* device_input() { return d_in_; }
+
+private:
+    struct Level;     // device tables of one level
+    struct Dev;       // device buffers
+    int fail(int code, const std::string& msg);
+    void ev_begin(int stage);
+    void ev_end(int stage);
+    void ev_collect();
+    int level0_bin();
+    int run_level(uint32_t h);
+    void free_all();
+
+    Config cfg_;
+    int device_;
+    hipStream_t stream_;
+    bool own_stream_ = false;
+    uint64_t n_ = 0, cap_ = 0;
+    uint32_t nbatches_ = 0;
+    std::vector<uint64_t> file_start_;   // first point index per file
+    std::vector<uint32_t> file_eb0_;     // first batch index per file
+    std::vector<uint32_t> file_batch_;   // batch size per file
+    Point* d_in_ = nullptr;
+    Dev* dev_ = nullptr;
+    std::vector<Level*> levels_;
+    float bmin_[3] = {0, 0, 0}, bmax_[3] = {0, 0, 0};
+    uint32_t hierarchies_ = 0;
+    BuildStats stats_;
+    bool profiling_ = false;
+    StageProfile prof_;
+    std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> ev_used_;
+    std::vector<hipEvent_t> ev_pool_;
+    std::string err_;
+    bool built_ = false;
+};
+
+}  // namespace pcc

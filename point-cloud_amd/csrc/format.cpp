@@ -1,0 +1,431 @@
+// format.cpp — cell / metadata writers and the PLY reader (see format.h).
+#include "format.h"
+
+#include <sys/stat.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <charconv>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+
+#include "pcc_math.h"
+
+namespace pcc {
+
+// ------------------------------------------------------------------ floats
+// Shortest round-trip digits (std::to_chars) laid out like ryu::Buffer::format
+// for f32 (serde_json 1.0.114 -> ryu 1.0.17 [dep]).  Byte parity unpinned:
+// tests compare parsed values.
+std::string format_f32(float v) {
+    if (v == 0.0f) return std::signbit(v) ? "-0.0" : "0.0";
+    if (std::isnan(v)) return "NaN";
+    if (std::isinf(v)) return v < 0 ? "-inf" : "inf";
+    char buf[64];
+    auto r = std::to_chars(buf, buf + sizeof buf, v, std::chars_format::scientific);
+    std::string s(buf, r.ptr);   // [-]d[.ddd]e[+-]xx
+    bool neg = false;
+    size_t i = 0;
+    if (s[0] == '-') { neg = true; i = 1; }
+    std::string digits;
+    for (; i < s.size() && s[i] != 'e'; i++)
+        if (s[i] != '.') digits += s[i];
+    int ex = std::atoi(s.c_str() + i + 1);
+    while (digits.size() > 1 && digits.back() == '0') digits.pop_back();
+    const int nd = (int)digits.size();
+    const int k = ex - (nd - 1), kk = nd + k;
+    std::string o = neg ? "-" : "";
+    if (0 <= k && kk <= 13) {
+        o += digits + std::string(k, '0') + ".0";
+    } else if (0 < kk && kk <= 13) {
+        o += digits.substr(0, kk) + "." + digits.substr(kk);
+    } else if (-6 < kk && kk <= 0) {
+        o += "0." + std::string(-kk, '0') + digits;
+    } else if (nd == 1) {
+        o += digits + "e" + std::to_string(kk - 1);
+    } else {
+        o += digits.substr(0, 1) + "." + digits.substr(1) + "e" + std::to_string(kk - 1);
+    }
+    return o;
+}
+
+std::string metadata_json(const Metadata& m) {
+    std::ostringstream o;
+    o << "{\n  \"version\": \"" << m.version << "\",\n  \"name\": \"" << m.name << "\",\n"
+      << "  \"number_of_points\": " << m.number_of_points << ",\n  \"hierarchies\": " << m.hierarchies << ",\n"
+      << "  \"bounding_box\": {\n    \"min\": [\n      " << format_f32(m.bmin[0]) << ",\n      " << format_f32(m.bmin[1])
+      << ",\n      " << format_f32(m.bmin[2]) << "\n    ],\n    \"max\": [\n      " << format_f32(m.bmax[0]) << ",\n      "
+      << format_f32(m.bmax[1]) << ",\n      " << format_f32(m.bmax[2]) << "\n    ]\n  },\n  \"config\": {\n"
+      << "    \"cell_point_overflow_limit\": " << m.config.cell_point_overflow_limit << ",\n"
+      << "    \"sub_grid_dimension\": " << m.config.sub_grid_dimension << ",\n"
+      << "    \"max_cell_size\": " << format_f32(m.config.max_cell_size) << "\n  }\n}";
+    return o.str();
+}
+
+// Minimal JSON reader for the metadata schema (metadata.rs:9-28).
+namespace {
+struct J {
+    const std::string& s;
+    size_t i = 0;
+    std::string err;
+    explicit J(const std::string& t) : s(t) {}
+    void ws() { while (i < s.size() && isspace((unsigned char)s[i])) i++; }
+    bool eat(char c) { ws(); if (i < s.size() && s[i] == c) { i++; return true; } return false; }
+    bool str(std::string& out) {
+        ws();
+        if (i >= s.size() || s[i] != '"') return false;
+        i++;
+        out.clear();
+        while (i < s.size() && s[i] != '"') {
+            if (s[i] == '\\' && i + 1 < s.size()) i++;
+            out += s[i++];
+        }
+        if (i >= s.size()) return false;
+        i++;
+        return true;
+    }
+    bool num(double& v) {
+        ws();
+        size_t j = i;
+        while (j < s.size() && (isdigit((unsigned char)s[j]) || strchr("+-.eE", s[j]))) j++;
+        if (j == i) return false;
+        v = strtod(s.substr(i, j - i).c_str(), nullptr);
+        i = j;
+        return true;
+    }
+    bool f32num(float& v) {   // parse as f32 directly (serde_json parses f32 fields via f64 then `as f32`)
+        double d;
+        if (!num(d)) return false;
+        v = (float)d;
+        return true;
+    }
+    bool vec3(float* v) {
+        if (!eat('[')) return false;
+        for (int a = 0; a < 3; a++) {
+            if (!f32num(v[a])) return false;
+            if (a < 2 && !eat(',')) return false;
+        }
+        return eat(']');
+    }
+    bool skip() {   // skip any value
+        ws();
+        if (i >= s.size()) return false;
+        if (s[i] == '"') { std::string t; return str(t); }
+        if (s[i] == '{' || s[i] == '[') {
+            char open = s[i], close = open == '{' ? '}' : ']';
+            int depth = 0;
+            bool instr = false;
+            for (; i < s.size(); i++) {
+                if (instr) { if (s[i] == '\\') i++; else if (s[i] == '"') instr = false; continue; }
+                if (s[i] == '"') instr = true;
+                else if (s[i] == open) depth++;
+                else if (s[i] == close && --depth == 0) { i++; return true; }
+            }
+            return false;
+        }
+        double d;
+        if (num(d)) return true;
+        for (const char* w : {"true", "false", "null"})
+            if (s.compare(i, strlen(w), w) == 0) { i += strlen(w); return true; }
+        return false;
+    }
+};
+}  // namespace
+
+bool parse_metadata_json(const std::string& text, Metadata& m, std::string& err) {
+    J j(text);
+    if (!j.eat('{')) { err = "metadata.json: expected object"; return false; }
+    bool first = true;
+    while (!j.eat('}')) {
+        if (!first && !j.eat(',')) { err = "metadata.json: expected ,"; return false; }
+        first = false;
+        std::string key;
+        if (!j.str(key) || !j.eat(':')) { err = "metadata.json: bad key"; return false; }
+        double d;
+        bool ok = true;
+        if (key == "version") ok = j.str(m.version);
+        else if (key == "name") ok = j.str(m.name);
+        else if (key == "number_of_points") { ok = j.num(d); m.number_of_points = (uint64_t)d; }
+        else if (key == "hierarchies") { ok = j.num(d); m.hierarchies = (uint32_t)d; }
+        else if (key == "bounding_box") {
+            ok = j.eat('{');
+            bool f2 = true;
+            while (ok && !j.eat('}')) {
+                if (!f2 && !j.eat(',')) { ok = false; break; }
+                f2 = false;
+                std::string k2;
+                ok = j.str(k2) && j.eat(':');
+                if (!ok) break;
+                if (k2 == "min") ok = j.vec3(m.bmin);
+                else if (k2 == "max") ok = j.vec3(m.bmax);
+                else ok = j.skip();
+            }
+        } else if (key == "config") {
+            ok = j.eat('{');
+            bool f2 = true;
+            while (ok && !j.eat('}')) {
+                if (!f2 && !j.eat(',')) { ok = false; break; }
+                f2 = false;
+                std::string k2;
+                ok = j.str(k2) && j.eat(':');
+                if (!ok) break;
+                if (k2 == "cell_point_overflow_limit") { ok = j.num(d); m.config.cell_point_overflow_limit = (uint32_t)d; }
+                else if (k2 == "sub_grid_dimension") { ok = j.num(d); m.config.sub_grid_dimension = (uint32_t)d; }
+                else if (k2 == "max_cell_size") ok = j.f32num(m.config.max_cell_size);
+                else ok = j.skip();
+            }
+        } else ok = j.skip();
+        if (!ok) { err = "metadata.json: bad value for " + key; return false; }
+    }
+    return true;
+}
+
+// ------------------------------------------------------------------ cells
+static void put32(std::string& b, uint32_t v) { b.append(reinterpret_cast<const char*>(&v), 4); }
+static void putf(std::string& b, float v) { b.append(reinterpret_cast<const char*>(&v), 4); }
+
+int write_output(const std::string& dir, const Metadata& meta, const std::vector<LevelHost>& levels,
+                 const std::vector<Point>& arena, std::string& err) {
+    if (mkdir(dir.c_str(), 0755) != 0 && errno != EEXIST) { err = "cannot create " + dir; return -errno; }
+    for (uint32_t h = 0; h < meta.hierarchies; h++) {   // converter.rs:141-158
+        std::string hd = dir + "/h_" + std::to_string(h);
+        if (mkdir(hd.c_str(), 0755) != 0 && errno != EEXIST) { err = "cannot create " + hd; return -errno; }
+    }
+    const Config& cfg = meta.config;
+    std::string buf;
+    for (const LevelHost& L : levels) {
+        const uint32_t h = L.h;
+        const float size = cell_size(cfg.max_cell_size, h);                 // converter.rs:197-199
+        const float sub = sub_cell_size(size, cfg.sub_grid_dimension);
+        const uint32_t ncells = (uint32_t)(L.cell_idx.size() / 3);
+        for (uint32_t c = 0; c < ncells; c++) {
+            const int32_t ix = L.cell_idx[3 * c], iy = L.cell_idx[3 * c + 1], iz = L.cell_idx[3 * c + 2];
+            uint32_t number = 0, overflow = 0, nb = 0;
+            for (uint32_t s = L.cell_slab0[c]; s < L.cell_slab0[c + 1]; s++) number += L.slab_grid_n[s];
+            for (int o = 0; o < 8; o++) {
+                const uint32_t st = L.bkt_state[8 * c + o];
+                if (st) nb++;
+                if (st == 1) overflow += L.bkt_n[8 * c + o];
+            }
+            buf.clear();
+            buf.reserve(48 + 16ull * (number + overflow) + 1 + 16 * nb);
+            // Header::write_to cell.rs:280-298
+            put32(buf, h);
+            put32(buf, (uint32_t)ix); put32(buf, (uint32_t)iy); put32(buf, (uint32_t)iz);
+            put32(buf, number + overflow);
+            put32(buf, number);
+            put32(buf, overflow);
+            putf(buf, size);
+            putf(buf, sub);
+            putf(buf, cell_pos1(ix, size)); putf(buf, cell_pos1(iy, size)); putf(buf, cell_pos1(iz, size));
+            // grid points (cell.rs:158-160; order free)
+            for (uint32_t s = L.cell_slab0[c]; s < L.cell_slab0[c + 1]; s++)
+                buf.append(reinterpret_cast<const char*>(arena.data() + L.slab_grid_off[s]), 16ull * L.slab_grid_n[s]);
+            buf.push_back((char)(uint8_t)nb);   // cell.rs:162
+            for (int o = 0; o < 8; o++) {
+                const uint32_t st = L.bkt_state[8 * c + o];
+                if (!st) continue;
+                put32(buf, (uint32_t)(2 * ix + (o & 1)));
+                put32(buf, (uint32_t)(2 * iy + ((o >> 1) & 1)));
+                put32(buf, (uint32_t)(2 * iz + ((o >> 2) & 1)));
+                if (st == 1) {
+                    put32(buf, L.bkt_n[8 * c + o]);
+                    buf.append(reinterpret_cast<const char*>(arena.data() + L.bkt_off[8 * c + o]), 16ull * L.bkt_n[8 * c + o]);
+                } else {
+                    put32(buf, 0);
+                }
+            }
+            char name[96];
+            snprintf(name, sizeof name, "/h_%u/c_%d_%d_%d.bin", h, ix, iy, iz);
+            const std::string path = dir + name;
+            FILE* f = fopen(path.c_str(), "wb");
+            if (!f) { err = "cannot write " + path; return -errno; }
+            const bool ok = fwrite(buf.data(), 1, buf.size(), f) == buf.size();
+            if (fclose(f) != 0 || !ok) { err = "write failed: " + path; return -EIO; }
+        }
+    }
+    const std::string mp = dir + "/metadata.json";
+    FILE* f = fopen(mp.c_str(), "wb");
+    if (!f) { err = "cannot write " + mp; return -errno; }
+    const std::string js = metadata_json(meta);
+    const bool ok = fwrite(js.data(), 1, js.size(), f) == js.size();
+    if (fclose(f) != 0 || !ok) { err = "write failed: " + mp; return -EIO; }
+    return 0;
+}
+
+// ------------------------------------------------------------------ PLY
+namespace {
+enum PType { P_I8, P_U8, P_I16, P_U16, P_I32, P_U32, P_F32, P_F64, P_BAD };
+PType ptype(const std::string& t) {
+    if (t == "char" || t == "int8") return P_I8;
+    if (t == "uchar" || t == "uint8") return P_U8;
+    if (t == "short" || t == "int16") return P_I16;
+    if (t == "ushort" || t == "uint16") return P_U16;
+    if (t == "int" || t == "int32") return P_I32;
+    if (t == "uint" || t == "uint32") return P_U32;
+    if (t == "float" || t == "float32") return P_F32;
+    if (t == "double" || t == "float64") return P_F64;
+    return P_BAD;
+}
+int psize(PType t) {
+    static const int s[] = {1, 1, 2, 2, 4, 4, 4, 8, 0};
+    return s[t];
+}
+struct Prop {
+    std::string name;
+    PType type;
+    bool list = false;
+    PType count_type = P_U8;
+};
+template <class T>
+T rd(const uint8_t* p, bool swap) {
+    T v;
+    uint8_t b[sizeof(T)];
+    memcpy(b, p, sizeof(T));
+    if (swap) std::reverse(b, b + sizeof(T));
+    memcpy(&v, b, sizeof(T));
+    return v;
+}
+double rdnum(const uint8_t* p, PType t, bool sw) {
+    switch (t) {
+        case P_I8: return (double)(int8_t)p[0];
+        case P_U8: return (double)p[0];
+        case P_I16: return rd<int16_t>(p, sw);
+        case P_U16: return rd<uint16_t>(p, sw);
+        case P_I32: return rd<int32_t>(p, sw);
+        case P_U32: return rd<uint32_t>(p, sw);
+        case P_F32: return rd<float>(p, sw);
+        case P_F64: return rd<double>(p, sw);
+        default: return 0;
+    }
+}
+// Rust `f32 as u8`: saturating, NaN -> 0
+uint8_t sat_u8(float v) {
+    if (!(v == v)) return 0;
+    if (v <= 0.0f) return 0;
+    if (v >= 255.0f) return 255;
+    return (uint8_t)v;
+}
+}  // namespace
+
+bool read_ply(const std::string& path, PlyResult& out, std::string& err) {
+    std::ifstream f(path, std::ios::binary);
+    if (!f) { err = "cannot open " + path; return false; }
+    std::string line;
+    if (!std::getline(f, line) || line.rfind("ply", 0) != 0) { err = path + ": not a PLY file"; return false; }
+    enum { ASCII, LE, BE } enc = LE;
+    std::vector<Prop> vprops;
+    bool in_vertex = false, seen_vertex = false, vertex_first = true;
+    uint64_t nvert = 0;
+    while (std::getline(f, line)) {
+        if (!line.empty() && line.back() == '\r') line.pop_back();
+        std::istringstream ls(line);
+        std::string kw;
+        ls >> kw;
+        if (kw == "format") {
+            std::string e;
+            ls >> e;
+            enc = e == "ascii" ? ASCII : e == "binary_big_endian" ? BE : LE;
+            if (e != "ascii" && e != "binary_big_endian" && e != "binary_little_endian") { err = "bad PLY format " + e; return false; }
+        } else if (kw == "element") {
+            std::string name;
+            uint64_t cnt;
+            ls >> name >> cnt;
+            in_vertex = name == "vertex";
+            if (in_vertex) { nvert = cnt; seen_vertex = true; }
+            else if (!seen_vertex) vertex_first = false;
+        } else if (kw == "property" && in_vertex) {
+            std::string t;
+            ls >> t;
+            Prop p;
+            if (t == "list") {
+                std::string ct, it;
+                ls >> ct >> it >> p.name;
+                p.list = true;
+                p.count_type = ptype(ct);
+                p.type = ptype(it);
+            } else {
+                ls >> p.name;
+                p.type = ptype(t);
+            }
+            if (p.type == P_BAD || p.count_type == P_BAD) { err = "unsupported PLY property type in " + line; return false; }
+            vprops.push_back(p);
+        } else if (kw == "end_header") {
+            break;
+        }
+    }
+    if (!seen_vertex) { err = path + ": no vertex element"; return false; }   // ply.rs:37 unwraps this
+    if (!vertex_first) { err = path + ": vertex must be the first PLY element"; return false; }
+    out.vertex_count = nvert;
+    out.points.clear();
+    if (enc == ASCII) {   // ply.rs:43-51: lines are parsed but never pushed into the batch
+        out.ascii = true;
+        return true;
+    }
+    const bool sw = enc == BE;
+    // fixed-size fast path
+    bool fixed = true;
+    int rec = 0;
+    for (auto& p : vprops) { if (p.list) fixed = false; rec += psize(p.type); }
+    out.points.resize(nvert);
+    std::vector<uint8_t> buf;
+    auto apply = [&](Point& pt, const Prop& p, const uint8_t* q) {
+        // point.rs:61-130
+        const std::string& nm = p.name;
+        if (nm == "x" || nm == "y" || nm == "z") {
+            float v;
+            if (p.type == P_F32) v = rd<float>(q, sw);
+            else if (p.type == P_F64) v = (float)rd<double>(q, sw);
+            else return;
+            (nm == "x" ? pt.x : nm == "y" ? pt.y : pt.z) = v;
+        } else {
+            int ch = (nm == "red" || nm == "r") ? 0 : (nm == "green" || nm == "g") ? 1 : (nm == "blue" || nm == "b") ? 2
+                   : (nm == "alpha" || nm == "a") ? 3 : -1;
+            if (ch < 0) return;
+            if (p.type == P_U8) pt.rgba[ch] = q[0];
+            else if (p.type == P_F32) pt.rgba[ch] = sat_u8(rd<float>(q, sw) / 255.0f);
+        }
+    };
+    if (fixed) {
+        const uint64_t chunk = 1 << 16;
+        buf.resize(chunk * rec);
+        for (uint64_t base = 0; base < nvert; base += chunk) {
+            const uint64_t m = std::min(chunk, nvert - base);
+            f.read(reinterpret_cast<char*>(buf.data()), (std::streamsize)(m * rec));
+            if ((uint64_t)f.gcount() != m * rec) { err = path + ": truncated vertex data"; return false; }
+            for (uint64_t i = 0; i < m; i++) {
+                Point& pt = out.points[base + i];
+                pt.x = pt.y = pt.z = 0;
+                pt.rgba[0] = pt.rgba[1] = pt.rgba[2] = 0;
+                pt.rgba[3] = 255;   // point.rs:16-23
+                const uint8_t* q = buf.data() + i * rec;
+                for (auto& p : vprops) { apply(pt, p, q); q += psize(p.type); }
+            }
+        }
+    } else {
+        for (uint64_t i = 0; i < nvert; i++) {
+            Point& pt = out.points[i];
+            pt.x = pt.y = pt.z = 0;
+            pt.rgba[0] = pt.rgba[1] = pt.rgba[2] = 0;
+            pt.rgba[3] = 255;
+            for (auto& p : vprops) {
+                uint8_t tmp[8];
+                if (p.list) {
+                    f.read(reinterpret_cast<char*>(tmp), psize(p.count_type));
+                    const uint64_t cnt = (uint64_t)rdnum(tmp, p.count_type, sw);
+                    f.seekg((std::streamoff)(cnt * psize(p.type)), std::ios::cur);
+                } else {
+                    f.read(reinterpret_cast<char*>(tmp), psize(p.type));
+                    apply(pt, p, tmp);
+                }
+                if (!f) { err = path + ": truncated vertex data"; return false; }
+            }
+        }
+    }
+    return true;
+}
+
+}  // namespace pcc

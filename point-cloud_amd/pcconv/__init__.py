@@ -1,0 +1,205 @@
+"""pcconv — Python host mirror of the reference `point-converter` library API
+(point-converter/src/lib.rs, converter.rs) over the MI355X C ABI
+(include/pcconv.h, libpcconv.so).
+
+There is no CPU fallback: every call goes through the HIP build, and importing
+this module fails loudly if libpcconv.so has not been built
+(`make -C point-cloud_amd`, or `python -c "import __graft_entry__ as g; g.build()"`).
+
+Reference-to-mirror map:
+  convert_from_paths(paths, output)   lib.rs:11-60
+  Converter(out_dir, ...)             lib.rs:86-101 load_metadata + converter.rs:79-94
+  Converter.add_points(points)        converter.rs:106-112 (one call == one input file,
+                                      ceil(n / batch_size) batches, lib.rs:31-52)
+  Converter.finish()                  converter.rs:241-246 Drop (cells, then metadata.json)
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "..", "build", "libpcconv.so")
+
+POINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("z", "<f4"), ("rgba", "u1", (4,))])  # point.rs:8-14
+
+# every symbol include/pcconv.h declares
+EXPORTS = ["pcc_abi_version", "pcc_last_error", "pcc_options_default", "pcc_open", "pcc_add_points",
+           "pcc_add_points_device", "pcc_add_empty_batches", "pcc_add_synthetic", "pcc_build", "pcc_write",
+           "pcc_finish", "pcc_close", "pcc_get_stats", "pcc_set_profiling", "pcc_get_profile", "pcc_device_input",
+           "pcc_convert_files"]
+
+
+class Options(C.Structure):
+    _fields_ = [("batch_size", C.c_uint32), ("device", C.c_int32), ("cell_point_overflow_limit", C.c_uint32),
+                ("sub_grid_dimension", C.c_uint32), ("max_cell_size", C.c_float), ("reserved", C.c_uint32)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("number_of_points", C.c_uint64), ("hierarchies", C.c_uint32), ("levels", C.c_uint32),
+                ("cells", C.c_uint64), ("slabs", C.c_uint64), ("arrivals", C.c_uint64),
+                ("grid_points", C.c_uint64), ("kept_points", C.c_uint64), ("build_ms", C.c_double),
+                ("bbox_min", C.c_float * 3), ("bbox_max", C.c_float * 3)]
+
+    def as_dict(self) -> dict:
+        d = {k: getattr(self, k) for k, _ in self._fields_ if not k.startswith("bbox")}
+        d["bbox_min"] = list(self.bbox_min)
+        d["bbox_max"] = list(self.bbox_max)
+        return d
+
+
+class Profile(C.Structure):
+    _fields_ = [("level0_ms", C.c_double), ("dense_ms", C.c_double), ("small_ms", C.c_double),
+                ("bucket_ms", C.c_double), ("next_ms", C.c_double), ("dense_arrivals", C.c_uint64),
+                ("small_arrivals", C.c_uint64), ("dense_launches", C.c_uint32), ("small_launches", C.c_uint32)]
+
+
+class PccError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"pcconv error {code}: {msg}")
+        self.code = code
+
+
+_lib = None
+
+
+def lib():
+    """Load libpcconv.so (no fallback: raises if the HIP library is missing)."""
+    global _lib
+    if _lib is None:
+        path = os.path.abspath(LIB_PATH)
+        if not os.path.exists(path):
+            raise ImportError(f"libpcconv.so not built at {path}; run `make -C point-cloud_amd`")
+        L = C.CDLL(path)
+        vp = C.c_void_p
+        L.pcc_abi_version.restype = C.c_uint32
+        L.pcc_last_error.restype = C.c_char_p
+        L.pcc_options_default.argtypes = [C.POINTER(Options)]
+        L.pcc_open.argtypes = [C.c_char_p, C.POINTER(Options), C.POINTER(vp)]
+        L.pcc_add_points.argtypes = [vp, vp, C.c_uint64]
+        L.pcc_add_points_device.argtypes = [vp, vp, C.c_uint64]
+        L.pcc_add_empty_batches.argtypes = [vp, C.c_uint32]
+        L.pcc_add_synthetic.argtypes = [vp, C.c_uint64, C.c_int, C.c_uint64, C.c_float, C.c_float]
+        L.pcc_build.argtypes = [vp]
+        L.pcc_write.argtypes = [vp]
+        L.pcc_finish.argtypes = [vp]
+        L.pcc_close.argtypes = [vp]
+        L.pcc_get_stats.argtypes = [vp, C.POINTER(Stats)]
+        L.pcc_set_profiling.argtypes = [vp, C.c_int]
+        L.pcc_get_profile.argtypes = [vp, C.POINTER(Profile)]
+        L.pcc_device_input.argtypes = [vp]
+        L.pcc_device_input.restype = vp
+        L.pcc_convert_files.argtypes = [C.c_char_p, C.POINTER(C.c_char_p), C.c_size_t, C.POINTER(Options)]
+        _lib = L
+    return _lib
+
+
+def _check(rc: int):
+    if rc != 0:
+        raise PccError(rc, lib().pcc_last_error().decode(errors="replace"))
+
+
+def default_options(**kw) -> Options:
+    o = Options()
+    _check(lib().pcc_options_default(C.byref(o)))
+    for k, v in kw.items():
+        setattr(o, k, v)
+    return o
+
+
+class Converter:
+    """converter.rs:72-94 Converter, built on the GPU at finish()/build()."""
+
+    def __init__(self, out_dir: str, batch_size: int = 10_000, device: int = 0, config: dict | None = None):
+        opt = default_options(batch_size=batch_size, device=device, **(config or {}))
+        h = C.c_void_p()
+        _check(lib().pcc_open(os.fsencode(out_dir), C.byref(opt), C.byref(h)))
+        self._h = h
+        self.out_dir = out_dir
+
+    def add_points(self, pts: np.ndarray):
+        """One input file (host array of POINT_DTYPE)."""
+        pts = np.ascontiguousarray(pts, dtype=POINT_DTYPE)
+        _check(lib().pcc_add_points(self._h, pts.ctypes.data, len(pts)))
+
+    def add_points_device(self, dev_ptr: int, n: int):
+        _check(lib().pcc_add_points_device(self._h, C.c_void_p(dev_ptr), n))
+
+    def add_empty_batches(self, k: int):
+        _check(lib().pcc_add_empty_batches(self._h, k))
+
+    def add_synthetic(self, seed: int, kind: int, n: int, lo: float = -1000.0, extent: float = 2000.0):
+        _check(lib().pcc_add_synthetic(self._h, seed, kind, n, lo, extent))
+
+    def build(self) -> dict:
+        _check(lib().pcc_build(self._h))
+        return self.stats()
+
+    def write(self):
+        _check(lib().pcc_write(self._h))
+
+    def stats(self) -> dict:
+        s = Stats()
+        _check(lib().pcc_get_stats(self._h, C.byref(s)))
+        return s.as_dict()
+
+    def set_profiling(self, on: bool = True):
+        _check(lib().pcc_set_profiling(self._h, 1 if on else 0))
+
+    def kernel_times(self) -> dict:
+        p = Profile()
+        _check(lib().pcc_get_profile(self._h, C.byref(p)))
+        return {k: getattr(p, k) for k, _ in p._fields_}
+
+    def device_input(self) -> int:
+        return lib().pcc_device_input(self._h)
+
+    def finish(self):
+        """converter.rs:241-246 Drop: build if needed, write cells then metadata.json."""
+        h, self._h = self._h, None
+        if h:
+            _check(lib().pcc_finish(h))
+
+    def close(self):
+        h, self._h = self._h, None
+        if h:
+            lib().pcc_close(h)
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, exc_type, exc, tb):
+        if exc_type is None:
+            self.finish()
+        else:
+            self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def convert_from_paths(paths, output: str, batch_size: int = 10_000, device: int = 0):
+    """lib.rs:11-60 convert_from_paths (PLY inputs)."""
+    arr = (C.c_char_p * len(paths))(*[os.fsencode(p) for p in paths])
+    opt = default_options(batch_size=batch_size, device=device)
+    _check(lib().pcc_convert_files(os.fsencode(output), arr, len(paths), C.byref(opt)))
+
+
+def write_ply(path: str, pts: np.ndarray, ascii: bool = False):
+    """Binary little-endian (or ASCII) PLY with x,y,z float + red,green,blue,alpha uchar."""
+    pts = np.ascontiguousarray(pts, dtype=POINT_DTYPE)
+    hdr = ("ply\nformat %s 1.0\nelement vertex %d\nproperty float x\nproperty float y\nproperty float z\n"
+           "property uchar red\nproperty uchar green\nproperty uchar blue\nproperty uchar alpha\nend_header\n"
+           % ("ascii" if ascii else "binary_little_endian", len(pts)))
+    with open(path, "wb") as f:
+        f.write(hdr.encode())
+        if ascii:
+            for p in pts:
+                f.write(("%r %r %r %d %d %d %d\n" % (float(p["x"]), float(p["y"]), float(p["z"]), *p["rgba"])).encode())
+        else:
+            f.write(pts.tobytes())

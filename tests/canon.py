@@ -113,3 +113,61 @@ def digest(cells) -> str:
         c = cells[k]
         h.update(repr((k, c["header"], c["grid"], c["buckets"])).encode())
     return h.hexdigest()
+
+
+def read_dir_fast(out_dir: str):
+    """Vectorised canonical form for large outputs: per cell the header, the
+    sorted multiset of grid point records (slots are a function of the point
+    and the header's sub_cell_size, so equal multisets imply equal slot maps)
+    and the overflow entries (child index, None | stored-order bytes)."""
+    cells = {}
+    with open(os.path.join(out_dir, "metadata.json")) as f:
+        meta = json.load(f)
+    for name in os.listdir(out_dir):
+        if not name.startswith("h_"):
+            continue
+        hdir = os.path.join(out_dir, name)
+        for fn in os.listdir(hdir):
+            with open(os.path.join(hdir, fn), "rb") as f:
+                data = f.read()
+            h, x, y, z, total, number, overflow = struct.unpack_from("<IiiiIII", data, 0)
+            hdr = data[16:48]
+            grid = np.frombuffer(data, dtype="V16", count=number, offset=48)
+            off = 48 + 16 * number
+            nb = data[off]
+            off += 1
+            buckets = []
+            for _ in range(nb):
+                cx, cy, cz, n = struct.unpack_from("<iiiI", data, off)
+                off += 16
+                buckets.append(((cx, cy, cz), None if n == 0 else data[off:off + 16 * n]))
+                off += 16 * n
+            assert off == len(data)
+            cells[(h, x, y, z)] = (hdr, np.sort(grid).tobytes(), tuple(sorted(buckets, key=lambda t: t[0])))
+    m = dict(number_of_points=meta["number_of_points"], hierarchies=meta["hierarchies"],
+             bmin=[float(F(v)) for v in meta["bounding_box"]["min"]],
+             bmax=[float(F(v)) for v in meta["bounding_box"]["max"]],
+             config=dict(meta["config"]))
+    return cells, m
+
+
+def diff_fast(a, b, limit: int = 10) -> list[str]:
+    out = []
+    for k in sorted(set(a) | set(b)):
+        if k not in a or k not in b:
+            out.append(f"cell {k} only in {'b' if k not in a else 'a'}")
+        elif a[k] != b[k]:
+            ha, ga, ba = a[k]
+            hb, gb, bb = b[k]
+            what = []
+            if ha != hb:
+                what.append(f"header {struct.unpack('<III5f', ha)} vs {struct.unpack('<III5f', hb)}")
+            if ga != gb:
+                what.append(f"grid {len(ga) // 16} vs {len(gb) // 16} pts")
+            if ba != bb:
+                what.append("buckets " + str([(i, None if l is None else len(l) // 16) for i, l in ba]) + " vs "
+                            + str([(i, None if l is None else len(l) // 16) for i, l in bb]))
+            out.append(f"cell {k}: " + "; ".join(what))
+        if len(out) >= limit:
+            break
+    return out

@@ -1,0 +1,134 @@
+"""GPU parity: the HIP build (through the C ABI, libpcconv.so) against the C
+oracle on identical inputs, compared on the canonical form of the output
+directory (tests/canon.py: headers bit-exact, grid membership, overflow lists
+in stored order, metadata values).  Oracle parity is unpinned against the Rust
+reference itself; see tests/test_oracle_xcheck.py."""
+import os
+import tempfile
+
+import numpy as np
+import pytest
+
+from gpu_util import compare_dirs, run_gpu, run_oracle  # noqa: E402
+from oracle_ctypes import POINT_DTYPE, synth  # noqa: E402
+from test_oracle_xcheck import _case, _to_np  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def _check(files, cfg=None, batch=10_000, fast=False, synth_files=None):
+    with tempfile.TemporaryDirectory() as tg, tempfile.TemporaryDirectory() as to:
+        st = run_gpu(tg, files if not synth_files else [], cfg=cfg, batch=batch, synth=synth_files)
+        err, arrivals = run_oracle(to, files, cfg=cfg, batch=batch)
+        assert err == 0
+        d, mg, mo = compare_dirs(tg, to, fast=fast)
+        assert d == [], d
+        assert mg == mo
+        assert st["arrivals"] == arrivals
+        assert st["grid_points"] + st["kept_points"] == st["number_of_points"]
+        return st
+
+
+@pytest.mark.parametrize("seed", range(60))
+def test_adversarial_small(seed):
+    """Tiny sub-grids, limits 1-7, batches 1-40, ties and duplicates, 1-3 files."""
+    files, cfg, batch = _case(seed)
+    _check([_to_np(f) for f in files], cfg=cfg, batch=batch)
+
+
+def test_config1_uniform_100k():
+    pts = synth(1, 0, 100_000)
+    st = _check([pts])
+    assert st["hierarchies"] == 1 and st["cells"] == 8
+
+
+def test_ragged_files_and_empty_file():
+    pts = synth(11, 0, 123_457)
+    files = [pts[:1], pts[1:1], pts[1:50_001], pts[50_001:]]
+    _check(files)
+
+
+def test_batch_size_one_and_tiny_limit():
+    pts = synth(12, 0, 3000, lo=-10.0, ext=20.0)
+    _check([pts], cfg=dict(cell_point_overflow_limit=3, sub_grid_dimension=4, max_cell_size=8.0), batch=1)
+
+
+def test_clustered_1m():
+    pts = synth(3, 1, 1_000_000)
+    st = _check([pts], fast=True)
+    assert st["levels"] >= 3
+
+
+def test_config2_uniform_10m_synthetic_on_device():
+    """Config 2: 10M uniform points generated in HBM; the oracle generates the same
+    points on the host with its own copy of the generator."""
+    n = 10_000_000
+    pts = synth(2, 0, n)
+    st = _check([pts], fast=True, synth_files=[(2, 0, n)])
+    assert st["levels"] == 2 and st["cells"] == 72
+
+
+def test_duplicates_exact_limit_chains():
+    """Thousands of exact duplicates (ties everywhere, multi-level spill chains)."""
+    base = synth(13, 0, 20_000)
+    dup = np.repeat(base[:3], 3000)
+    files = [np.concatenate([base, dup]), np.repeat(base[:1], 1000)]
+    _check(files, batch=10_000, fast=True)
+
+
+def test_depth_limit_is_an_error():
+    """More than L identical points never terminate in the reference (metadata.rs:92
+    overflows 2u32.pow(h) at h = 32); the GPU build reports it instead of hanging."""
+    import pcconv
+    p = np.zeros(6000, dtype=POINT_DTYPE)
+    p["x"], p["y"], p["z"] = 1.0, 2.0, 3.0
+    with tempfile.TemporaryDirectory() as tg:
+        c = pcconv.Converter(tg)
+        c.add_points(p)
+        with pytest.raises(pcconv.PccError) as ei:
+            c.build()
+        assert "depth" in str(ei.value)
+        c.close()
+
+
+def test_nonfinite_input_rejected():
+    import pcconv
+    p = synth(1, 0, 100)
+    p["x"][7] = np.nan
+    with tempfile.TemporaryDirectory() as tg:
+        c = pcconv.Converter(tg)
+        c.add_points(p)
+        with pytest.raises(pcconv.PccError):
+            c.build()
+        c.close()
+
+
+def test_ply_cli_roundtrip():
+    """Config 1 through the CLI binary with a binary-LE PLY, plus an ASCII PLY whose
+    points the reference drops (ply.rs:43-51) but whose batches still count."""
+    import subprocess
+    import pcconv
+    pts = synth(1, 0, 100_000)
+    with tempfile.TemporaryDirectory() as td:
+        a = os.path.join(td, "a.ply")
+        b = os.path.join(td, "b.ply")
+        pcconv.write_ply(a, pts[:60_000])
+        pcconv.write_ply(b, pts[:25_000], ascii=True)
+        c = os.path.join(td, "c.ply")
+        pcconv.write_ply(c, pts[60_000:])
+        out = os.path.join(td, "out")
+        exe = os.path.join(os.path.dirname(pcconv.LIB_PATH), "point_converter")
+        r = subprocess.run([exe, "-o", out, "-f", a, "-f", b, "-f", c], capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr
+        assert "Finished converting after" in r.stderr
+        ref = os.path.join(td, "ref")
+        from oracle_ctypes import Oracle
+        o = Oracle()
+        o.add_file(pts[:60_000])
+        for _ in range(3):   # 25 000 ASCII points -> 3 empty batches
+            o.add_batch(pts[:0])
+        o.add_file(pts[60_000:])
+        o.write(ref)
+        o.close()
+        d, mg, mo = compare_dirs(out, ref)
+        assert d == [] and mg == mo
