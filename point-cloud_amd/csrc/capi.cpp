@@ -182,11 +182,11 @@ int pcc_write(pcc_converter* c) {
     }
     GUARD_BEGIN
     std::vector<LevelHost> levels;
-    std::vector<Point> arena, unused;
-    int rc = c->eng->download(levels, arena, unused);
+    std::vector<Point> grid, kept;
+    int rc = c->eng->download(levels, grid, kept);
     if (rc) return set_err(rc, c->eng->last_error());
     std::string err;
-    rc = write_output(c->out_dir, c->meta, levels, arena, err);
+    rc = write_output(c->out_dir, c->meta, levels, grid, kept, err);
     if (rc) return set_err(rc, err);
     return 0;
     GUARD_END

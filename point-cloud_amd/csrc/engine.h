@@ -33,6 +33,8 @@ struct LevelHost {
     std::vector<uint32_t> slab_grid_off, slab_grid_n;
     std::vector<uint32_t> bkt_state;    // 8 per cell: 0 absent, 1 kept (Some), 2 spilled (None)
     std::vector<uint32_t> bkt_off, bkt_n;
+    uint64_t grid_base = 0;             // offset of this level's winner region in the downloaded grid array
+    uint64_t kept_base = 0;             // offset of this level's kept lists in the downloaded kept array
 };
 
 struct StageProfile {

@@ -4,16 +4,24 @@
 // and cell.rs:70-153 with the level-synchronous restatement of SURVEY.md
 // Appendix C (validated in oracle/pyref.py::convert_keyed):
 //
-//   level 0 binning  : input points -> slabs (cell, hex z-layer), stable in key
-//                      order (LSD radix sort on the slab id + gather)
-//   per level h      : one workgroup per slab, slot table in LDS
-//      sweep 1       : winners = argmin(dist2, key) per slot (ds_min_u64)
-//      sweep 2       : key-ordered replay -> one emission per non-first arrival,
-//                      written straight into the child slab it belongs to
+//   level-0 binning  : input points -> slabs (cell, hex z-layer), stable in key
+//                      order: LSD radix sort whose keys are recomputed from the
+//                      positions in every pass and which carries the payload
+//                      (no key array, no random gather)
+//   per level h      : one workgroup per slab, slot table in LDS, ONE pass in
+//                      key order: per chunk, the earliest pending arrival of
+//                      every slot is applied (cell.rs:70-94), the loser is
+//                      emitted at the arrival's key straight into its child
+//                      slab; winners are written at the end
 //   bucket resolve   : per (cell, octant) bucket: keep (Some) or spill (None),
-//                      spill batch via counting over key-ordered child slabs
+//                      spill batch by counting over key-ordered child slabs
 //   next level       : spilled buckets become the next level's cells; their
 //                      child slabs are already laid out contiguously.
+//
+// Every output range is known before the kernel that fills it: the parent
+// level counts, per child slab, how many of its arrivals go to each of ITS
+// child slabs ("capacities"), so emission and winner regions come from
+// exclusive scans, not from same-address atomics.
 //
 // Key facts this relies on:
 //   * child hex z-layer u comes from parent layer t = u/2 (truncating) because
@@ -38,15 +46,15 @@ namespace pcc {
 constexpr uint64_t kEmpty64 = ~0ull;
 constexpr uint32_t kEmpty32 = 0xFFFFFFFFu;
 constexpr int kDenseBS = 1024;
-constexpr int kDenseTab = 16560;     // 120 x 138 slots: one z-layer of a dim-96 cell
+constexpr int kDenseTab = 116 * 132;  // one z-layer of a dim-96 cell (slab_geom)
 constexpr int kDenseClaim = 2048;
 constexpr int kSmallBS = 256;
-constexpr uint32_t kSmallMax = 1024; // slabs with fewer arrivals use the hashed kernel
+constexpr uint32_t kSmallMax = 1024;  // slabs with fewer arrivals use the hashed kernel
 constexpr int kSmallTab = 2048;
 constexpr int kSmallClaim = 512;
-constexpr int kKeptMax = 8192;       // LDS sort capacity for kept (Some) buckets
-constexpr int kDests = 24;           // 8 octants x 3 child layers per slab
-constexpr uint32_t kMaxDepth = 31;   // 2u32.pow(h) overflows at h = 32 (metadata.rs:92)
+constexpr int kKeptMax = 8192;        // LDS sort capacity for kept (Some) buckets
+constexpr int kDests = 24;            // 8 octants x 3 child layers per slab
+constexpr uint32_t kMaxDepth = 31;    // 2u32.pow(h) overflows at h = 32 (metadata.rs:92)
 
 enum ErrBits : uint32_t {
     ERR_SLOT_RANGE = 1u << 0,
@@ -55,18 +63,17 @@ enum ErrBits : uint32_t {
     ERR_SEL = 1u << 3,
     ERR_KEPT_CAP = 1u << 4,
     ERR_L0_RANGE = 1u << 5,
-    ERR_NONFINITE = 1u << 6,
+    ERR_CAPACITY = 1u << 6,
+    ERR_CLAIM = 1u << 7,
 };
 
 struct Counters {
-    uint32_t arena_cur;   // next-level arena allocation cursor
-    uint32_t out_cur;     // grid + kept output arena cursor
+    uint32_t kept_cur;    // kept-list cursor inside the level's kept region
     uint32_t err;
     uint32_t nbig, nsmall;
-    uint32_t ncells_next, nslabs_next;
-    uint32_t pad;
     unsigned long long arrivals_next;  // sum of next-level slab sizes
-    unsigned long long grid_total;     // grid winners written so far
+    unsigned long long grid_total;     // grid winners written so far (all levels)
+    unsigned long long kept_total;
     unsigned long long dense_arrivals, small_arrivals;
 };
 
@@ -77,15 +84,14 @@ struct Arena {
 
 struct Engine::Dev {
     Arena ar[2] = {};
-    Point* out = nullptr;           // grid winners + kept bucket lists (== N points total)
     Counters* ctr = nullptr;
     float* bbox_part = nullptr;     // per-block min/max partials
     uint32_t* bbox_flag = nullptr;
     uint32_t* files = nullptr;      // per file: start_lo, start_hi, eb0, batch
     ScanTemp scan;
-    SortTemp sort;
     uint64_t cap = 0;
-    // chunked bump allocator for per-build tables (reset at every build, chunks kept)
+    // chunked bump allocator for per-build tables and output regions (reset at
+    // every build, chunks kept for the next build)
     std::vector<std::pair<uint8_t*, uint64_t>> chunks;
     size_t chunk_i = 0;
     uint64_t chunk_used = 0;
@@ -108,7 +114,9 @@ struct Engine::Dev {
 
 struct Engine::Level {
     uint32_t h = 0, ncells = 0, nslabs = 0, nbig = 0, nsmall = 0;
+    uint64_t arrivals = 0;           // sum of slab_n
     int arena = 0;
+    Engine::Dev* dev = nullptr;
     int32_t* cell_idx = nullptr;     // 3 * ncells
     uint32_t* cell_sb = nullptr;     // spill batch of the parent bucket (eb' = max(eb, sb))
     uint32_t* cell_slab0 = nullptr;  // ncells + 1
@@ -118,16 +126,21 @@ struct Engine::Level {
     uint32_t* slab_n = nullptr;
     uint32_t* big_list = nullptr;
     uint32_t* small_list = nullptr;
-    uint32_t* slab_grid_off = nullptr;
+    uint32_t* dcap = nullptr;        // 24 * nslabs: arrivals of this slab per child slab (capacity)
+    uint32_t* dest_off = nullptr;    // 24 * nslabs: exclusive scan of dcap = emission regions (next arena)
+    uint32_t* dest_n = nullptr;      // 24 * nslabs: emissions actually written
+    uint32_t* gcap = nullptr;        // 24 * 24 * nslabs: capacities of the child slabs' own child slabs
+    uint32_t* grid_off = nullptr;    // exclusive scan of slab_n = winner regions (capacity n)
     uint32_t* slab_grid_n = nullptr;
-    uint32_t* dest_off = nullptr;    // 24 * nslabs
-    uint32_t* dest_n = nullptr;
+    Point* grid = nullptr;           // this level's winner region (arrivals entries)
+    Point* kept = nullptr;           // this level's kept-list region
+    uint64_t kept_cap = 0;
+    uint32_t kept_used = 0;
     uint32_t* bkt_state = nullptr;   // 8 * ncells
     uint32_t* bkt_off = nullptr;
     uint32_t* bkt_n = nullptr;
     uint32_t* bkt_sb = nullptr;
     uint32_t* bkt_nd = nullptr;
-    Dev* dev = nullptr;
     template <class T>
     void alloc(T*& p, uint64_t n) { p = static_cast<T*>(dev->get(n * sizeof(T))); }
 };
@@ -149,16 +162,33 @@ __device__ __forceinline__ uint32_t event_batch(const uint32_t* files, uint32_t 
     return files[4 * lo + 2] + (uint32_t)((i - s) / files[4 * lo + 3]);
 }
 
+// Child slab of a point living in slab (cell c, layer t) at the current level:
+// octant from cell_index at the next level (metadata.rs:100-102; child index =
+// 2*parent + bit since floor(2q) = 2 floor(q) + {0,1}) and child layer
+// u = trunc(z / r_child) in {2t-1, 2t, 2t+1} -> sel = u - 2t + 1.
+// Returns 0..23 or -1 (sets err); also returns the child cell index and layer.
+__device__ __forceinline__ int route(float csc, float crc, int32_t cx, int32_t cy, int32_t cz, int32_t t, float x,
+                                     float y, float z, int32_t& ix, int32_t& iy, int32_t& iz, int32_t& u,
+                                     uint32_t& err) {
+    ix = cell_index1(x, csc);
+    iy = cell_index1(y, csc);
+    iz = cell_index1(z, csc);
+    u = sat_i32(z / crc);
+    const int32_t bx = ix - 2 * cx, by = iy - 2 * cy, bz = iz - 2 * cz;
+    const int32_t sel = u - 2 * t + 1;
+    if ((bx | by | bz) & ~1) { err |= ERR_OCTANT; return -1; }
+    if (sel < 0 || sel > 2) { err |= ERR_SEL; return -1; }
+    return (bx | (by << 1) | (bz << 2)) * 3 + sel;
+}
+
 // ------------------------------------------------------------------ input kernels
 __global__ void k_synth(Point* out, uint64_t first, uint64_t n, uint64_t seed, int kind, float lo, float ext) {
     for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < n; j += (uint64_t)gridDim.x * blockDim.x) {
         float x, y, z;
         uint32_t c;
         synth_point(seed, kind, j, lo, ext, x, y, z, c);
-        Point p;
-        p.x = x; p.y = y; p.z = z;
-        memcpy(p.rgba, &c, 4);
-        out[first + j] = p;
+        float4 v = make_float4(x, y, z, __uint_as_float(c));
+        reinterpret_cast<float4*>(out)[first + j] = v;
     }
 }
 
@@ -204,14 +234,15 @@ __global__ void k_bbox_final(float* part, uint32_t nb) {
 
 // ------------------------------------------------------------------ level-0 binning
 struct L0Params {
-    float cs, cr;
+    float cs, cr, csc, crc;   // level 0 and level 1 cell size / hex radius
     int32_t lo[3];
     int32_t g[3];
     int32_t nl;
     int32_t dim2;   // 2 * sub_grid_dimension
 };
 
-// dense slab id of a point: ((cell - lo) linearised) * nl + (layer - (dim2*iz - 2))
+// dense slab id of a point: ((cell - lo) linearised) * nl + (layer - (dim2*iz - 2));
+// ordered by (cell, layer) exactly like the compact slab ids.
 __device__ __forceinline__ int64_t l0_dense(const L0Params& P, float x, float y, float z) {
     int32_t ix = cell_index1(x, P.cs), iy = cell_index1(y, P.cs), iz = cell_index1(z, P.cs);
     int32_t gx = ix - P.lo[0], gy = iy - P.lo[1], gz = iz - P.lo[2];
@@ -221,26 +252,148 @@ __device__ __forceinline__ int64_t l0_dense(const L0Params& P, float x, float y,
     return (((int64_t)gz * P.g[1] + gy) * P.g[0] + gx) * P.nl + ll;
 }
 
-constexpr int kHistLds = 12288;
-__global__ __launch_bounds__(256) void k_l0_hist(const Point* __restrict__ in, uint64_t n, L0Params P, uint32_t* hist,
-                                                 uint32_t D, Counters* ctr) {
+constexpr int kL0BS = 256, kL0IPT = 8, kL0Tile = kL0BS * kL0IPT, kL0W = kL0BS / 64;
+constexpr int kHistLds = 8192;
+
+// pass-0 upsweep from the AoS input: per-tile digit histogram + full dense-slab histogram
+template <int BITS>
+__global__ __launch_bounds__(kL0BS) void k_l0_up0(const Point* __restrict__ in, uint64_t n, L0Params P, int shift,
+                                                  uint32_t* __restrict__ counts, uint32_t ntiles, uint32_t* hist,
+                                                  uint32_t D, Counters* ctr) {
+    constexpr int R = 1 << BITS;
+    __shared__ uint32_t dh[R];
     __shared__ uint32_t h[kHistLds];
     const bool lds = D <= (uint32_t)kHistLds;
-    if (lds) {
-        for (uint32_t i = threadIdx.x; i < D; i += 256) h[i] = 0;
-        __syncthreads();
-    }
+    for (int i = threadIdx.x; i < R; i += kL0BS) dh[i] = 0;
+    if (lds) for (uint32_t i = threadIdx.x; i < D; i += kL0BS) h[i] = 0;
+    __syncthreads();
+    const uint64_t base = (uint64_t)blockIdx.x * kL0Tile;
     const float4* p4 = reinterpret_cast<const float4*>(in);
-    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
-        float4 v = p4[i];
-        int64_t d = l0_dense(P, v.x, v.y, v.z);
-        if (d < 0) { set_err(ctr, ERR_L0_RANGE); continue; }
-        if (lds) atomicAdd(&h[d], 1u); else atomicAdd(&hist[d], 1u);
+#pragma unroll 4
+    for (int r = 0; r < kL0IPT; r++) {
+        const uint64_t i = base + (uint64_t)r * kL0BS + threadIdx.x;
+        if (i < n) {
+            const float4 v = p4[i];
+            const int64_t d = l0_dense(P, v.x, v.y, v.z);
+            if (d < 0) { set_err(ctr, ERR_L0_RANGE); continue; }
+            atomicAdd(&dh[((uint64_t)d >> shift) & (R - 1)], 1u);
+            if (lds) atomicAdd(&h[d], 1u); else atomicAdd(&hist[d], 1u);
+        }
     }
-    if (lds) {
-        __syncthreads();
-        for (uint32_t i = threadIdx.x; i < D; i += 256)
+    __syncthreads();
+    for (int d = threadIdx.x; d < R; d += kL0BS) counts[(uint64_t)d * ntiles + blockIdx.x] = dh[d];
+    if (lds)
+        for (uint32_t i = threadIdx.x; i < D; i += kL0BS)
             if (h[i]) atomicAdd(&hist[i], h[i]);
+}
+
+// later-pass upsweep from a SoA arena
+template <int BITS>
+__global__ __launch_bounds__(kL0BS) void k_l0_up(Arena A, uint64_t n, L0Params P, int shift,
+                                                 uint32_t* __restrict__ counts, uint32_t ntiles) {
+    constexpr int R = 1 << BITS;
+    __shared__ uint32_t dh[R];
+    for (int i = threadIdx.x; i < R; i += kL0BS) dh[i] = 0;
+    __syncthreads();
+    const uint64_t base = (uint64_t)blockIdx.x * kL0Tile;
+#pragma unroll 4
+    for (int r = 0; r < kL0IPT; r++) {
+        const uint64_t i = base + (uint64_t)r * kL0BS + threadIdx.x;
+        if (i < n) {
+            const int64_t d = l0_dense(P, A.x[i], A.y[i], A.z[i]);
+            atomicAdd(&dh[((uint64_t)(d < 0 ? 0 : d) >> shift) & (R - 1)], 1u);
+        }
+    }
+    __syncthreads();
+    for (int d = threadIdx.x; d < R; d += kL0BS) counts[(uint64_t)d * ntiles + blockIdx.x] = dh[d];
+}
+
+// Stable downsweep carrying the payload (x, y, z, rgba, input index); the key is
+// recomputed from the position.  SRC_AOS: read the 16-B input records (index =
+// position); FINAL: also write the event batch of every point.
+template <int BITS, bool SRC_AOS, bool FINAL>
+__global__ __launch_bounds__(kL0BS) void k_l0_down(const Point* __restrict__ in, Arena S, Arena O, uint64_t n,
+                                                   L0Params P, int shift, const uint32_t* __restrict__ offs,
+                                                   uint32_t ntiles, const uint32_t* files, uint32_t nfiles) {
+    constexpr int R = 1 << BITS;
+    __shared__ float sx[kL0Tile], sy[kL0Tile], sz[kL0Tile];
+    __shared__ uint32_t sc[kL0Tile], sk[kL0Tile];
+    __shared__ uint16_t sd[kL0Tile];
+    __shared__ uint32_t wcnt[kL0W][R], wpre[kL0W][R];
+    __shared__ uint32_t run[R], dbase[R], goff[R];
+    __shared__ uint32_t lds[kL0W + 1];
+    const uint32_t w = threadIdx.x / 64;
+    for (int i = threadIdx.x; i < R; i += kL0BS) {
+        run[i] = 0;
+        goff[i] = offs[(uint64_t)i * ntiles + blockIdx.x];
+        for (int q = 0; q < kL0W; q++) wcnt[q][i] = 0;
+    }
+    const uint64_t base = (uint64_t)blockIdx.x * kL0Tile;
+    float x[kL0IPT], y[kL0IPT], z[kL0IPT];
+    uint32_t c[kL0IPT], k[kL0IPT], rank[kL0IPT];
+    uint16_t dg[kL0IPT];
+#pragma unroll
+    for (int r = 0; r < kL0IPT; r++) {
+        const uint64_t i = base + (uint64_t)r * kL0BS + threadIdx.x;
+        dg[r] = 0;
+        if (i < n) {
+            if constexpr (SRC_AOS) {
+                const float4 v = reinterpret_cast<const float4*>(in)[i];
+                x[r] = v.x; y[r] = v.y; z[r] = v.z; c[r] = __float_as_uint(v.w); k[r] = (uint32_t)i;
+            } else {
+                x[r] = S.x[i]; y[r] = S.y[i]; z[r] = S.z[i]; c[r] = S.c[i]; k[r] = S.k[i];
+            }
+            const int64_t d = l0_dense(P, x[r], y[r], z[r]);
+            dg[r] = (uint16_t)(((uint64_t)(d < 0 ? 0 : d) >> shift) & (R - 1));
+        }
+    }
+    __syncthreads();
+    const uint64_t lt = lanemask_lt();
+#pragma unroll
+    for (int r = 0; r < kL0IPT; r++) {
+        const uint64_t i = base + (uint64_t)r * kL0BS + threadIdx.x;
+        const bool valid = i < n;
+        const uint32_t d = dg[r];
+        uint64_t same = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < BITS; b++) {
+            const uint64_t bb = __ballot(valid && ((d >> b) & 1));
+            same &= ((d >> b) & 1) ? bb : ~bb;
+        }
+        const uint32_t rw = __popcll(same & lt);
+        if (valid && rw == 0) wcnt[w][d] = (uint32_t)__popcll(same);
+        __syncthreads();
+        for (int t = threadIdx.x; t < R; t += kL0BS) {
+            uint32_t acc = run[t];
+#pragma unroll
+            for (int q = 0; q < kL0W; q++) { const uint32_t cc = wcnt[q][t]; wpre[q][t] = acc; acc += cc; wcnt[q][t] = 0; }
+            run[t] = acc;
+        }
+        __syncthreads();
+        rank[r] = valid ? wpre[w][d] + rw : 0;
+    }
+    {
+        uint32_t tot;
+        const uint32_t cc = threadIdx.x < (uint32_t)R ? run[threadIdx.x] : 0;
+        const uint32_t e = block_excl_scan<kL0BS>(cc, lds, &tot);
+        if (threadIdx.x < (uint32_t)R) dbase[threadIdx.x] = e;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kL0IPT; r++) {
+        const uint64_t i = base + (uint64_t)r * kL0BS + threadIdx.x;
+        if (i < n) {
+            const uint32_t p = dbase[dg[r]] + rank[r];
+            sx[p] = x[r]; sy[p] = y[r]; sz[p] = z[r]; sc[p] = c[r]; sk[p] = k[r]; sd[p] = dg[r];
+        }
+    }
+    __syncthreads();
+    const uint32_t tn = (uint32_t)((n - base) < (uint64_t)kL0Tile ? (n - base) : (uint64_t)kL0Tile);
+    for (uint32_t j = threadIdx.x; j < tn; j += kL0BS) {
+        const uint32_t d = sd[j];
+        const uint32_t dst = goff[d] + (j - dbase[d]);
+        O.x[dst] = sx[j]; O.y[dst] = sy[j]; O.z[dst] = sz[j]; O.c[dst] = sc[j]; O.k[dst] = sk[j];
+        if constexpr (FINAL) O.e[dst] = event_batch(files, nfiles, sk[j]);
     }
 }
 
@@ -258,8 +411,7 @@ __global__ void k_l0_flags(const uint32_t* hist, uint32_t D, int32_t nl, uint32_
 __global__ void k_l0_tables(const uint32_t* hist, const uint32_t* cnt_scan, const uint32_t* sflag_scan,
                             const uint32_t* cflag, const uint32_t* cflag_scan, uint32_t D, uint32_t G, L0Params P,
                             int32_t* cell_idx, uint32_t* cell_sb, uint32_t* cell_slab0, uint32_t* slab_cell,
-                            int32_t* slab_layer, uint32_t* slab_off, uint32_t* slab_n, uint32_t* big_list,
-                            uint32_t* small_list, Counters* ctr) {
+                            int32_t* slab_layer, uint32_t* slab_off, uint32_t* slab_n) {
     const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
     if (d < G && cflag[d]) {
         const uint32_t r = cflag_scan[d];
@@ -282,38 +434,46 @@ __global__ void k_l0_tables(const uint32_t* hist, const uint32_t* cnt_scan, cons
         slab_layer[sid] = ll + (P.dim2 * iz - 2);
         slab_off[sid] = cnt_scan[d];
         slab_n[sid] = hist[d];
-        if (hist[d] >= kSmallMax) big_list[atomicAdd(&ctr->nbig, 1u)] = sid;
-        else small_list[atomicAdd(&ctr->nsmall, 1u)] = sid;
     }
 }
 
-__global__ void k_l0_keys(const Point* __restrict__ in, uint64_t n, L0Params P, const uint32_t* sflag_scan,
-                          uint32_t* keys, uint32_t* vals) {
-    const float4* p4 = reinterpret_cast<const float4*>(in);
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-        float4 v = p4[i];
-        int64_t d = l0_dense(P, v.x, v.y, v.z);
-        keys[i] = d < 0 ? 0 : sflag_scan[d];
-        vals[i] = (uint32_t)i;
+// capacities of the level-0 slabs: arrivals per child slab
+__global__ __launch_bounds__(256) void k_l0_dcap(Arena A, L0Params P, const int32_t* cell_idx,
+                                                 const uint32_t* slab_cell, const int32_t* slab_layer,
+                                                 const uint32_t* slab_off, const uint32_t* slab_n, uint32_t* dcap,
+                                                 Counters* ctr) {
+    __shared__ uint32_t cnt[kDests];
+    const uint32_t s = blockIdx.x;
+    if (threadIdx.x < kDests) cnt[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t cr_ = slab_cell[s], off = slab_off[s], n = slab_n[s];
+    const int32_t t = slab_layer[s];
+    const int32_t cx = cell_idx[3 * cr_], cy = cell_idx[3 * cr_ + 1], cz = cell_idx[3 * cr_ + 2];
+    uint32_t err = 0;
+    uint32_t loc[kDests] = {};
+    for (uint32_t j = threadIdx.x; j < n; j += 256) {
+        int32_t ix, iy, iz, u;
+        const int d = route(P.csc, P.crc, cx, cy, cz, t, A.x[off + j], A.y[off + j], A.z[off + j], ix, iy, iz, u, err);
+        if (d >= 0) {
+#pragma unroll
+            for (int q = 0; q < kDests; q++) loc[q] += (q == d);
+        }
     }
-}
-
-__global__ void k_l0_gather(const Point* __restrict__ in, const uint32_t* __restrict__ perm, uint64_t n, Arena A,
-                            const uint32_t* files, uint32_t nfiles) {
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-        uint32_t src = perm[i];
-        float4 v = reinterpret_cast<const float4*>(in)[src];
-        A.x[i] = v.x; A.y[i] = v.y; A.z[i] = v.z;
-        A.c[i] = __float_as_uint(v.w);
-        A.k[i] = src;
-        A.e[i] = event_batch(files, nfiles, src);
+#pragma unroll
+    for (int q = 0; q < kDests; q++) {
+        uint32_t v = loc[q];
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+        if ((threadIdx.x & 63) == 0 && v) atomicAdd(&cnt[q], v);
     }
+    if (err) set_err(ctr, err);
+    __syncthreads();
+    if (threadIdx.x < kDests) dcap[s * kDests + threadIdx.x] = cnt[threadIdx.x];
 }
 
 // ------------------------------------------------------------------ slab kernels
 struct SlabParams {
     Arena in, nx;
-    Point* out;
+    Point* grid;
     const int32_t* cell_idx;
     const uint32_t* cell_sb;
     const uint32_t* slab_cell;
@@ -321,31 +481,17 @@ struct SlabParams {
     const uint32_t* slab_off;
     const uint32_t* slab_n;
     const uint32_t* list;
-    uint32_t* slab_grid_off;
+    const uint32_t* grid_off;
+    const uint32_t* dcap;
+    const uint32_t* dest_off;
     uint32_t* slab_grid_n;
-    uint32_t* dest_off;
     uint32_t* dest_n;
+    uint32_t* gcap;
     Counters* ctr;
-    float cs, cr, cs_child, cr_child;
+    float cs, cr, cs_child, cr_child, cs_gchild, cr_gchild;
     int32_t tx, ty;
+    int32_t check_gchild;
 };
-
-// Routing of a point from slab (cell c, layer t) to its child slab:
-// octant from cell_index at h+1 (metadata.rs:100-102; child = 2*parent + bit),
-// child layer u = trunc(z / r_{h+1}) in {2t-1, 2t, 2t+1} -> sel = u - 2t + 1.
-__device__ __forceinline__ int dest_of(const SlabParams& P, int32_t cx, int32_t cy, int32_t cz, int32_t t, float x,
-                                       float y, float z, uint32_t& err) {
-    int32_t bx = cell_index1(x, P.cs_child) - 2 * cx;
-    int32_t by = cell_index1(y, P.cs_child) - 2 * cy;
-    int32_t bz = cell_index1(z, P.cs_child) - 2 * cz;
-    int32_t u = sat_i32(z / P.cr_child);
-    int32_t sel = u - 2 * t + 1;
-    if ((bx | by | bz) & ~1) { err |= ERR_OCTANT; return -1; }
-    if (sel < 0 || sel > 2) { err |= ERR_SEL; return -1; }
-    return (bx | (by << 1) | (bz << 2)) * 3 + sel;
-}
-
-__device__ __forceinline__ uint32_t hash_slot(uint32_t k) { return (k * 2654435761u) >> 16; }
 
 template <bool DENSE>
 struct SlabLds;
@@ -354,42 +500,66 @@ template <>
 struct SlabLds<true> {
     static constexpr int BS = kDenseBS, TAB = kDenseTab, CLAIM = kDenseClaim, NW = BS / 64;
     unsigned long long tab[TAB];
-    uint32_t claim[CLAIM];
+    unsigned long long claim[CLAIM];
     uint32_t tkey[1];
-    uint32_t dcnt[kDests], doff[kDests], dcur[kDests];
+    uint32_t gcnt[kDests * kDests];
+    uint32_t doff[kDests], dcap[kDests], dcur[kDests];
     uint32_t wcnt[NW][kDests], wpre[NW][kDests];
-    uint32_t nwin, wbase, wctr, err;
+    uint32_t npend, nwin, err;
 };
 template <>
 struct SlabLds<false> {
     static constexpr int BS = kSmallBS, TAB = kSmallTab, CLAIM = kSmallClaim, NW = BS / 64;
     unsigned long long tab[TAB];
-    uint32_t claim[CLAIM];
+    unsigned long long claim[CLAIM];
     uint32_t tkey[TAB];
-    uint32_t dcnt[kDests], doff[kDests], dcur[kDests];
+    uint32_t gcnt[kDests * kDests];
+    uint32_t doff[kDests], dcap[kDests], dcur[kDests];
     uint32_t wcnt[NW][kDests], wpre[NW][kDests];
-    uint32_t nwin, wbase, wctr, err;
+    uint32_t npend, nwin, err;
 };
+
+__device__ __forceinline__ uint32_t hash_slot(uint32_t k) { return (k * 2654435761u) >> 15; }
 
 // slot -> table entry (DENSE: direct; otherwise LDS open addressing on the local slot id)
 template <bool DENSE>
-__device__ __forceinline__ int slot_entry(SlabLds<DENSE>& S, uint32_t local, bool insert) {
+__device__ __forceinline__ int slot_entry(SlabLds<DENSE>& S, uint32_t local) {
     if constexpr (DENSE) {
         return (int)local;
     } else {
         uint32_t h = hash_slot(local) & (SlabLds<false>::TAB - 1);
         for (int probe = 0; probe < SlabLds<false>::TAB; probe++) {
-            uint32_t k = S.tkey[h];
+            const uint32_t k = S.tkey[h];
             if (k == local) return (int)h;
             if (k == kEmpty32) {
-                if (!insert) return -1;
-                uint32_t old = atomicCAS(&S.tkey[h], kEmpty32, local);
+                const uint32_t old = atomicCAS(&S.tkey[h], kEmpty32, local);
                 if (old == kEmpty32 || old == local) return (int)h;
             }
             h = (h + 1) & (SlabLds<false>::TAB - 1);
         }
         return -1;
     }
+}
+
+// Per-chunk claim table keyed by slot: entry = (slot << 32) | min pending thread.
+template <int CLAIM>
+__device__ __forceinline__ int claim_insert(unsigned long long* H, uint32_t local, uint32_t tid) {
+    const unsigned long long mine = ((unsigned long long)local << 32) | tid;
+    uint32_t h = hash_slot(local) & (CLAIM - 1);
+    for (int probe = 0; probe < CLAIM; probe++) {
+        unsigned long long e = H[h];
+        if (e == kEmpty64) {
+            const unsigned long long old = atomicCAS(&H[h], kEmpty64, mine);
+            if (old == kEmpty64) return (int)h;
+            e = old;
+        }
+        if ((uint32_t)(e >> 32) == local) {
+            atomicMin(&H[h], mine);
+            return (int)h;
+        }
+        h = (h + 1) & (CLAIM - 1);
+    }
+    return -1;
 }
 
 template <bool DENSE>
@@ -414,102 +584,71 @@ __global__ __launch_bounds__(SlabLds<DENSE>::BS) void k_slab(SlabParams P) {
         S.tab[i] = kEmpty64;
         if constexpr (!DENSE) S.tkey[i] = kEmpty32;
     }
-    for (int i = tid; i < CLAIM; i += BS) S.claim[i] = kEmpty32;
-    if (tid < kDests) { S.dcnt[tid] = 0; S.dcur[tid] = 0; }
-    if (tid < NW * kDests) { (&S.wcnt[0][0])[tid] = 0; }
-    if (tid == 0) { S.nwin = 0; S.wctr = 0; S.err = 0; }
+    for (int i = tid; i < CLAIM; i += BS) S.claim[i] = kEmpty64;
+    for (int i = tid; i < kDests * kDests; i += BS) S.gcnt[i] = 0;
+    if (tid < kDests) {
+        S.dcur[tid] = 0;
+        S.doff[tid] = P.dest_off[s * kDests + tid];
+        S.dcap[tid] = P.dcap[s * kDests + tid];
+    }
+    if (tid < NW * kDests) (&S.wcnt[0][0])[tid] = 0;
+    if (tid == 0) { S.npend = 0; S.nwin = 0; S.err = 0; }
     __syncthreads();
 
-    // ---------------------------------------------------------------- sweep 1
+    // prefetch of the first chunk
+    float nxx = 0, nxy = 0, nxz = 0;
+    uint32_t nxc = 0, nxk = 0, nxe = 0;
+    if (tid < n) {
+        nxx = P.in.x[off + tid]; nxy = P.in.y[off + tid]; nxz = P.in.z[off + tid];
+        nxc = P.in.c[off + tid]; nxk = P.in.k[off + tid]; nxe = P.in.e[off + tid];
+    }
+    const uint64_t lt = lanemask_lt();
     for (uint32_t base = 0; base < n; base += BS) {
         const uint32_t j = base + tid;
-        if (j < n) {
-            const float x = P.in.x[off + j], y = P.in.y[off + j], z = P.in.z[off + j];
+        const bool valid = j < n;
+        const float x = nxx, y = nxy, z = nxz;
+        const uint32_t c = nxc, k = nxk, eb = max(nxe, sb);
+        // issue the next chunk's loads now; they stay in flight across the LDS barriers below
+        const uint32_t jn = j + BS;
+        if (jn < n) {
+            nxx = P.in.x[off + jn]; nxy = P.in.y[off + jn]; nxz = P.in.z[off + jn];
+            nxc = P.in.c[off + jn]; nxk = P.in.k[off + jn]; nxe = P.in.e[off + jn];
+        }
+        bool pending = false;
+        float d2 = 0;
+        int e = 0, hc = 0;
+        uint32_t local = 0;
+        if (valid) {
             const I3 sl = hex_from_world(x, y, z, P.cr);
             const int32_t lx = sl.x - rx, ly = sl.y - ry;
             if (sl.z != t) err |= ERR_LAYER;
             else if (lx < 0 || ly < 0 || lx >= P.tx || ly >= P.ty) err |= ERR_SLOT_RANGE;
             else {
-                const int e = slot_entry<DENSE>(S, (uint32_t)(ly * P.tx + lx), true);
-                float X, Y, Z;
-                hex_to_world(sl, P.cr, X, Y, Z);
-                const float d2 = dist2(X, Y, Z, x, y, z);
-                const unsigned long long pk = ((unsigned long long)f2u(d2) << 32) | j;
-                const unsigned long long old = atomicMin(&S.tab[e], pk);
-                if (old == kEmpty64) atomicAdd(&S.nwin, 1u);
-                const int d = dest_of(P, cx, cy, cz, t, x, y, z, err);
-                if (d >= 0) atomicAdd(&S.dcnt[d], 1u);
-            }
-        }
-    }
-    __syncthreads();
-    if (tid == 0) {
-        const uint32_t wb = atomicAdd(&P.ctr->out_cur, S.nwin);
-        S.wbase = wb;
-        P.slab_grid_off[s] = wb;
-        P.slab_grid_n[s] = S.nwin;
-        atomicAdd(&P.ctr->grid_total, (unsigned long long)S.nwin);
-    }
-    __syncthreads();
-    // winners -> output arena (grid points; order inside a cell is free: cell.rs:158-160 HashMap order)
-    for (int i = tid; i < TAB; i += BS) {
-        const unsigned long long e = S.tab[i];
-        if (e != kEmpty64) {
-            const uint32_t j = (uint32_t)e;
-            const float x = P.in.x[off + j], y = P.in.y[off + j], z = P.in.z[off + j];
-            const uint32_t c = P.in.c[off + j];
-            const int d = dest_of(P, cx, cy, cz, t, x, y, z, err);
-            if (d >= 0) atomicSub(&S.dcnt[d], 1u);
-            const uint32_t r = atomicAdd(&S.wctr, 1u);
-            Point p;
-            p.x = x; p.y = y; p.z = z;
-            memcpy(p.rgba, &c, 4);
-            P.out[S.wbase + r] = p;
-            S.tab[i] = kEmpty64;
-        }
-    }
-    __syncthreads();
-    if (tid < kDests) {
-        const uint32_t c = S.dcnt[tid];
-        const uint32_t o = c ? atomicAdd(&P.ctr->arena_cur, c) : 0u;
-        S.doff[tid] = o;
-        P.dest_off[s * kDests + tid] = o;
-        P.dest_n[s * kDests + tid] = c;
-    }
-    __syncthreads();
-
-    // ---------------------------------------------------------------- sweep 2
-    const uint64_t lt = lanemask_lt();
-    for (uint32_t base = 0; base < n; base += BS) {
-        const uint32_t j = base + tid;
-        bool pending = false;
-        float x = 0, y = 0, z = 0, d2 = 0;
-        uint32_t c = 0, k = 0, eb = 0, ch = 0;
-        int e = 0;
-        if (j < n) {
-            x = P.in.x[off + j]; y = P.in.y[off + j]; z = P.in.z[off + j];
-            c = P.in.c[off + j]; k = P.in.k[off + j]; eb = max(P.in.e[off + j], sb);
-            const I3 sl = hex_from_world(x, y, z, P.cr);
-            const int32_t lx = sl.x - rx, ly = sl.y - ry;
-            if (sl.z == t && lx >= 0 && ly >= 0 && lx < P.tx && ly < P.ty) {
-                e = slot_entry<DENSE>(S, (uint32_t)(ly * P.tx + lx), false);
-                if (e >= 0) {
+                local = (uint32_t)(ly * P.tx + lx);
+                e = slot_entry<DENSE>(S, local);
+                if (e < 0) err |= ERR_CLAIM;
+                else {
                     float X, Y, Z;
                     hex_to_world(sl, P.cr, X, Y, Z);
                     d2 = dist2(X, Y, Z, x, y, z);
                     pending = true;
-                    ch = (uint32_t)e & (CLAIM - 1);
                 }
             }
         }
         // cell.rs:70-94 replayed in key order: per round, the earliest pending
-        // arrival of every slot (claim = min thread index) is applied.
+        // arrival of every slot (min thread index = min key) is applied.
+        {
+            const uint32_t np = (uint32_t)__popcll(__ballot(pending));
+            if ((tid & 63) == 0 && np) atomicAdd(&S.npend, np);
+        }
+        if (pending) {
+            hc = claim_insert<CLAIM>(S.claim, local, tid);
+            if (hc < 0) { err |= ERR_CLAIM; pending = false; atomicSub(&S.npend, 1u); }
+        }
         int32_t em = -1;
+        lds_barrier();
         for (;;) {
-            if (pending) atomicMin(&S.claim[ch], tid);
-            __syncthreads();
-            bool won = false;
-            if (pending && S.claim[ch] == tid) {
+            if (pending && (uint32_t)S.claim[hc] == tid) {
                 const unsigned long long occ = S.tab[e];
                 const unsigned long long mine = ((unsigned long long)f2u(d2) << 32) | j;
                 if (occ == kEmpty64) {
@@ -521,56 +660,96 @@ __global__ __launch_bounds__(SlabLds<DENSE>::BS) void k_slab(SlabParams P) {
                     em = (int32_t)j;               // the arrival itself overflows
                 }
                 pending = false;
-                won = true;
+                S.claim[hc] = ((unsigned long long)local << 32) | 0xFFFFFFFFull;
+                atomicSub(&S.npend, 1u);
             }
-            __syncthreads();
-            if (won) S.claim[ch] = kEmpty32;
-            if (!__syncthreads_or(pending)) break;
+            lds_barrier();
+            if (S.npend == 0) break;
+            if (pending) atomicMin(&S.claim[hc], ((unsigned long long)local << 32) | tid);
+            lds_barrier();
         }
-        // emission: point (self or displaced), key/eb of this arrival
-        int d = -1;
+        if (valid && hc >= 0 && e >= 0 && local != 0xFFFFFFFFu && (err & (ERR_LAYER | ERR_SLOT_RANGE)) == 0)
+            S.claim[hc] = kEmpty64;   // all rounds done: clear for the next chunk
+        // emission: point (self or displaced), key/eb of this arrival, routed to its child slab
+        int d = -1, d2i = -1;
         float ex = x, ey = y, ez = z;
         uint32_t ec = c;
         if (em >= 0) {
             if ((uint32_t)em != j) {
                 ex = P.in.x[off + em]; ey = P.in.y[off + em]; ez = P.in.z[off + em]; ec = P.in.c[off + em];
             }
-            d = dest_of(P, cx, cy, cz, t, ex, ey, ez, err);
+            int32_t ix, iy, iz, u;
+            d = route(P.cs_child, P.cr_child, cx, cy, cz, t, ex, ey, ez, ix, iy, iz, u, err);
+            if (d >= 0) {
+                int32_t jx, jy, jz, v;
+                uint32_t gerr = 0;
+                d2i = route(P.cs_gchild, P.cr_gchild, ix, iy, iz, u, ex, ey, ez, jx, jy, jz, v, gerr);
+                if (P.check_gchild) err |= gerr;
+            }
         }
-        const bool v = d >= 0;
-        uint64_t same = __ballot(v);
+        const bool vd = d >= 0;
+        uint64_t same = __ballot(vd);
 #pragma unroll
         for (int b = 0; b < 5; b++) {
-            const uint64_t bb = __ballot(v && ((d >> b) & 1));
+            const uint64_t bb = __ballot(vd && ((d >> b) & 1));
             same &= ((d >> b) & 1) ? bb : ~bb;
         }
         const uint32_t rw = __popcll(same & lt);
-        if (v && rw == 0) S.wcnt[wv][d] = (uint32_t)__popcll(same);
-        __syncthreads();
+        if (vd && rw == 0) S.wcnt[wv][d] = (uint32_t)__popcll(same);
+        lds_barrier();
         if (tid < kDests) {
             uint32_t acc = S.dcur[tid];
 #pragma unroll
             for (int q = 0; q < NW; q++) { const uint32_t cc = S.wcnt[q][tid]; S.wpre[q][tid] = acc; acc += cc; S.wcnt[q][tid] = 0; }
             S.dcur[tid] = acc;
         }
-        __syncthreads();
-        if (v) {
-            const uint32_t pos = S.doff[d] + S.wpre[wv][d] + rw;
-            P.nx.x[pos] = ex; P.nx.y[pos] = ey; P.nx.z[pos] = ez;
-            P.nx.c[pos] = ec; P.nx.k[pos] = k; P.nx.e[pos] = eb;
+        lds_barrier();
+        if (vd) {
+            const uint32_t r = S.wpre[wv][d] + rw;
+            if (r < S.dcap[d]) {
+                const uint32_t pos = S.doff[d] + r;
+                P.nx.x[pos] = ex; P.nx.y[pos] = ey; P.nx.z[pos] = ez;
+                P.nx.c[pos] = ec; P.nx.k[pos] = k; P.nx.e[pos] = eb;
+            } else {
+                err |= ERR_CAPACITY;
+            }
+            if (d2i >= 0) atomicAdd(&S.gcnt[d * kDests + d2i], 1u);
+        }
+    }
+    __syncthreads();
+    // winners -> this slab's grid region (capacity n; order inside a cell is free:
+    // cell.rs:158-160 HashMap order)
+    const uint32_t gbase = P.grid_off[s];
+    for (int i = tid; i < TAB; i += BS) {
+        const unsigned long long en = S.tab[i];
+        if (en != kEmpty64) {
+            const uint32_t j = (uint32_t)en;
+            const uint32_t r = atomicAdd(&S.nwin, 1u);
+            const float4 v = make_float4(P.in.x[off + j], P.in.y[off + j], P.in.z[off + j], __uint_as_float(P.in.c[off + j]));
+            reinterpret_cast<float4*>(P.grid)[gbase + r] = v;
         }
     }
     if (err) atomicOr(&S.err, err);
     __syncthreads();
-    if (tid == 0 && S.err) set_err(P.ctr, S.err);
+    if (tid == 0) {
+        P.slab_grid_n[s] = S.nwin;
+        atomicAdd(&P.ctr->grid_total, (unsigned long long)S.nwin);
+        if (S.err) set_err(P.ctr, S.err);
+    }
+    if (tid < kDests) P.dest_n[s * kDests + tid] = S.dcur[tid] < S.dcap[tid] ? S.dcur[tid] : S.dcap[tid];
+    // capacities of the child slabs' own child slabs (only rows that will exist)
+    for (int i = tid; i < kDests * kDests; i += BS) {
+        const int dd = i / kDests;
+        if (S.dcur[dd]) P.gcap[(uint64_t)s * kDests * kDests + i] = S.gcnt[i];
+    }
 }
 
 // ------------------------------------------------------------------ bucket resolution
 struct BucketParams {
     Arena nx;          // arrivals of level h+1 (== emissions of level h)
-    Point* out;
+    Point* kept;
+    uint64_t kept_cap;
     const uint32_t* cell_slab0;
-    const int32_t* slab_layer;
     const uint32_t* dest_off;
     const uint32_t* dest_n;
     uint32_t* bkt_state;
@@ -637,8 +816,14 @@ __global__ __launch_bounds__(kBktBS) void k_bucket(BucketParams B) {
             if (threadIdx.x == 0) { set_err(B.ctr, ERR_KEPT_CAP); B.bkt_state[b] = 0; }
             return;
         }
-        if (threadIdx.x == 0) { s_cnt = 0; s_off = atomicAdd(&B.ctr->out_cur, tot); }
+        if (threadIdx.x == 0) {
+            s_cnt = 0;
+            s_off = atomicAdd(&B.ctr->kept_cur, tot);
+            atomicAdd(&B.ctr->kept_total, (unsigned long long)tot);
+            if ((uint64_t)s_off + tot > B.kept_cap) set_err(B.ctr, ERR_KEPT_CAP);
+        }
         __syncthreads();
+        if ((uint64_t)s_off + tot > B.kept_cap) return;
         for (uint32_t i = threadIdx.x; i < nd; i += kBktBS) {
             const uint32_t di = (s0 + i / 3) * kDests + oct * 3 + i % 3;
             const uint32_t n = B.dest_n[di];
@@ -671,11 +856,8 @@ __global__ __launch_bounds__(kBktBS) void k_bucket(BucketParams B) {
             }
         for (uint32_t i = threadIdx.x; i < tot; i += kBktBS) {
             const uint32_t o = spos[i];
-            Point p;
-            p.x = B.nx.x[o]; p.y = B.nx.y[o]; p.z = B.nx.z[o];
-            const uint32_t c = B.nx.c[o];
-            memcpy(p.rgba, &c, 4);
-            B.out[s_off + i] = p;
+            const float4 v = make_float4(B.nx.x[o], B.nx.y[o], B.nx.z[o], __uint_as_float(B.nx.c[o]));
+            reinterpret_cast<float4*>(B.kept)[s_off + i] = v;
         }
         if (threadIdx.x == 0) { B.bkt_state[b] = 1; B.bkt_off[b] = s_off; B.bkt_n[b] = tot; B.bkt_nd[b] = 0; B.bkt_sb[b] = 0; }
         return;
@@ -721,6 +903,7 @@ struct NextParams {
     const int32_t* slab_layer;
     const uint32_t* dest_off;
     const uint32_t* dest_n;
+    const uint32_t* gcap;
     int32_t* ncell_idx;
     uint32_t* ncell_sb;
     uint32_t* ncell_slab0;
@@ -728,6 +911,7 @@ struct NextParams {
     int32_t* nslab_layer;
     uint32_t* nslab_off;
     uint32_t* nslab_n;
+    uint32_t* ndcap;
     uint32_t* nbig_list;
     uint32_t* nsmall_list;
     Counters* ctr;
@@ -735,7 +919,8 @@ struct NextParams {
 
 __global__ __launch_bounds__(256) void k_next_emit(NextParams Q) {
     __shared__ uint32_t lds[256 / 64 + 1];
-    __shared__ uint32_t carry;
+    __shared__ uint32_t carry, s_big, s_small, s_bigbase, s_smallbase;
+    __shared__ unsigned long long s_arr;
     const uint32_t b = blockIdx.x;
     if (Q.bkt_state[b] != 2) return;
     const uint32_t cell = b >> 3, oct = b & 7;
@@ -748,10 +933,31 @@ __global__ __launch_bounds__(256) void k_next_emit(NextParams Q) {
         Q.ncell_sb[r] = Q.bkt_sb[b];
         Q.ncell_slab0[r] = base;
         carry = 0;
+        s_big = 0;
+        s_small = 0;
+        s_arr = 0;
     }
     __syncthreads();
     const uint32_t s0 = Q.cell_slab0[cell], s1 = Q.cell_slab0[cell + 1];
     const uint32_t nd = (s1 - s0) * 3;
+    // pass 1: count big / small slabs of this cell (one global atomic per block)
+    for (uint32_t i = threadIdx.x; i < nd; i += 256) {
+        const uint32_t di = (s0 + i / 3) * kDests + oct * 3 + i % 3;
+        const uint32_t n = Q.dest_n[di];
+        if (n) {
+            atomicAdd(n >= kSmallMax ? &s_big : &s_small, 1u);
+            atomicAdd(&s_arr, (unsigned long long)n);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        s_bigbase = s_big ? atomicAdd(&Q.ctr->nbig, s_big) : 0;
+        s_smallbase = s_small ? atomicAdd(&Q.ctr->nsmall, s_small) : 0;
+        if (s_arr) atomicAdd(&Q.ctr->arrivals_next, s_arr);
+        s_big = 0;
+        s_small = 0;
+    }
+    __syncthreads();
     for (uint32_t i0 = 0; i0 < nd; i0 += 256) {
         const uint32_t i = i0 + threadIdx.x;
         uint32_t n = 0, di = 0;
@@ -768,14 +974,32 @@ __global__ __launch_bounds__(256) void k_next_emit(NextParams Q) {
             Q.nslab_layer[sid] = 2 * t + (int32_t)(i % 3) - 1;
             Q.nslab_off[sid] = Q.dest_off[di];
             Q.nslab_n[sid] = n;
-            atomicAdd(&Q.ctr->arrivals_next, (unsigned long long)n);
-            if (n >= kSmallMax) Q.nbig_list[atomicAdd(&Q.ctr->nbig, 1u)] = sid;
-            else Q.nsmall_list[atomicAdd(&Q.ctr->nsmall, 1u)] = sid;
+            const uint32_t* g = Q.gcap + (uint64_t)di * kDests;
+            for (int q = 0; q < kDests; q++) Q.ndcap[(uint64_t)sid * kDests + q] = g[q];
+            if (n >= kSmallMax) Q.nbig_list[s_bigbase + atomicAdd(&s_big, 1u)] = sid;
+            else Q.nsmall_list[s_smallbase + atomicAdd(&s_small, 1u)] = sid;
         }
         __syncthreads();
         if (threadIdx.x == 0) carry += tot;
         __syncthreads();
     }
+}
+
+// big / small slab lists at level 0 (block-aggregated atomics)
+__global__ __launch_bounds__(256) void k_l0_lists(const uint32_t* slab_n, uint32_t nslabs, uint32_t* big,
+                                                  uint32_t* small, Counters* ctr) {
+    __shared__ uint32_t nb, ns, bb, bs;
+    if (threadIdx.x == 0) { nb = 0; ns = 0; }
+    __syncthreads();
+    const uint32_t s = blockIdx.x * 256 + threadIdx.x;
+    uint32_t rb = 0, rs = 0;
+    const bool v = s < nslabs;
+    const bool isbig = v && slab_n[s] >= kSmallMax;
+    if (v) { if (isbig) rb = atomicAdd(&nb, 1u); else rs = atomicAdd(&ns, 1u); }
+    __syncthreads();
+    if (threadIdx.x == 0) { bb = nb ? atomicAdd(&ctr->nbig, nb) : 0; bs = ns ? atomicAdd(&ctr->nsmall, ns) : 0; }
+    __syncthreads();
+    if (v) { if (isbig) big[bb + rb] = s; else small[bs + rs] = s; }
 }
 
 __global__ void k_set_u32(uint32_t* p, uint32_t v) { *p = v; }
@@ -804,33 +1028,6 @@ Engine::~Engine() {
     } catch (...) {
     }
     if (own_stream_) (void)hipStreamDestroy(stream_);
-}
-
-void Engine::free_all() {
-    for (auto& u : ev_used_) { ev_pool_.push_back(u.second.first); ev_pool_.push_back(u.second.second); }
-    ev_used_.clear();
-    for (hipEvent_t e : ev_pool_) (void)hipEventDestroy(e);
-    ev_pool_.clear();
-    for (Level* l : levels_) delete l;
-    levels_.clear();
-    if (dev_) {
-        for (int a = 0; a < 2; a++) {
-            (void)hipFree(dev_->ar[a].x); (void)hipFree(dev_->ar[a].y); (void)hipFree(dev_->ar[a].z);
-            (void)hipFree(dev_->ar[a].c); (void)hipFree(dev_->ar[a].k); (void)hipFree(dev_->ar[a].e);
-        }
-        (void)hipFree(dev_->out);
-        (void)hipFree(dev_->ctr);
-        (void)hipFree(dev_->bbox_part);
-        (void)hipFree(dev_->bbox_flag);
-        (void)hipFree(dev_->scan.bsums);
-        (void)hipFree(dev_->sort.counts);
-        (void)hipFree(dev_->sort.scan.bsums);
-        for (auto& c : dev_->chunks) (void)hipFree(c.first);
-        delete dev_;
-        dev_ = nullptr;
-    }
-    (void)hipFree(d_in_);
-    d_in_ = nullptr;
 }
 
 enum Stage { ST_L0 = 0, ST_DENSE, ST_SMALL, ST_BUCKET, ST_NEXT };
@@ -872,6 +1069,30 @@ void Engine::ev_collect() {
     ev_used_.clear();
 }
 
+void Engine::free_all() {
+    for (auto& u : ev_used_) { ev_pool_.push_back(u.second.first); ev_pool_.push_back(u.second.second); }
+    ev_used_.clear();
+    for (hipEvent_t e : ev_pool_) (void)hipEventDestroy(e);
+    ev_pool_.clear();
+    for (Level* l : levels_) delete l;
+    levels_.clear();
+    if (dev_) {
+        for (int a = 0; a < 2; a++) {
+            (void)hipFree(dev_->ar[a].x); (void)hipFree(dev_->ar[a].y); (void)hipFree(dev_->ar[a].z);
+            (void)hipFree(dev_->ar[a].c); (void)hipFree(dev_->ar[a].k); (void)hipFree(dev_->ar[a].e);
+        }
+        (void)hipFree(dev_->ctr);
+        (void)hipFree(dev_->bbox_part);
+        (void)hipFree(dev_->bbox_flag);
+        (void)hipFree(dev_->scan.bsums);
+        for (auto& c : dev_->chunks) (void)hipFree(c.first);
+        delete dev_;
+        dev_ = nullptr;
+    }
+    (void)hipFree(d_in_);
+    d_in_ = nullptr;
+}
+
 int Engine::fail(int code, const std::string& msg) {
     err_ = msg;
     return code;
@@ -889,31 +1110,33 @@ void Engine::reserve(uint64_t n) {
     cap_ = n;
 }
 
+static uint32_t batches_of(uint64_t n, uint32_t batch) {
+    const uint64_t b = std::max<uint32_t>(batch, 1);
+    return (uint32_t)std::max<uint64_t>(1, (n + b - 1) / b);
+}
+
 void Engine::add_file_host(const Point* pts, uint64_t n, uint32_t batch) {
-    if (built_) throw std::runtime_error("engine already built");
     reserve(n_ + n);
     if (n) HIP_CHECK(hipMemcpyAsync(d_in_ + n_, pts, n * sizeof(Point), hipMemcpyHostToDevice, stream_));
     file_start_.push_back(n_);
     file_eb0_.push_back(nbatches_);
     file_batch_.push_back(std::max<uint32_t>(batch, 1));
     n_ += n;
-    nbatches_ += (uint32_t)std::max<uint64_t>(1, (n + std::max<uint32_t>(batch, 1) - 1) / std::max<uint32_t>(batch, 1));
+    nbatches_ += batches_of(n, batch);
     HIP_CHECK(hipStreamSynchronize(stream_));
 }
 
 void Engine::add_file_device(const Point* dpts, uint64_t n, uint32_t batch) {
-    if (built_) throw std::runtime_error("engine already built");
     reserve(n_ + n);
     if (n) HIP_CHECK(hipMemcpyAsync(d_in_ + n_, dpts, n * sizeof(Point), hipMemcpyDeviceToDevice, stream_));
     file_start_.push_back(n_);
     file_eb0_.push_back(nbatches_);
     file_batch_.push_back(std::max<uint32_t>(batch, 1));
     n_ += n;
-    nbatches_ += (uint32_t)std::max<uint64_t>(1, (n + std::max<uint32_t>(batch, 1) - 1) / std::max<uint32_t>(batch, 1));
+    nbatches_ += batches_of(n, batch);
 }
 
 void Engine::add_file_synth(uint64_t seed, int kind, uint64_t n, uint32_t batch, float lo, float ext) {
-    if (built_) throw std::runtime_error("engine already built");
     reserve(n_ + n);
     if (n) k_synth<<<grid_for(n, 256, 1 << 20), 256, 0, stream_>>>(d_in_, n_, n, seed, kind, lo, ext);
     HIP_CHECK(hipGetLastError());
@@ -921,7 +1144,7 @@ void Engine::add_file_synth(uint64_t seed, int kind, uint64_t n, uint32_t batch,
     file_eb0_.push_back(nbatches_);
     file_batch_.push_back(std::max<uint32_t>(batch, 1));
     n_ += n;
-    nbatches_ += (uint32_t)std::max<uint64_t>(1, (n + std::max<uint32_t>(batch, 1) - 1) / std::max<uint32_t>(batch, 1));
+    nbatches_ += batches_of(n, batch);
 }
 
 int Engine::build() {
@@ -942,7 +1165,7 @@ int Engine::build() {
     stats_ = BuildStats();
     if (n_ == 0) return 0;
 
-    // allocate arenas (SoA, N entries each) + output arena (N points: grid + kept == N)
+    // arenas: SoA, N entries each (ping-pong between levels)
     if (dev_->cap < n_) {
         for (int a = 0; a < 2; a++) {
             Arena& A = dev_->ar[a];
@@ -950,8 +1173,6 @@ int Engine::build() {
             HIP_CHECK(hipMalloc(&A.x, n_ * 4)); HIP_CHECK(hipMalloc(&A.y, n_ * 4)); HIP_CHECK(hipMalloc(&A.z, n_ * 4));
             HIP_CHECK(hipMalloc(&A.c, n_ * 4)); HIP_CHECK(hipMalloc(&A.k, n_ * 4)); HIP_CHECK(hipMalloc(&A.e, n_ * 4));
         }
-        (void)hipFree(dev_->out);
-        HIP_CHECK(hipMalloc(&dev_->out, n_ * sizeof(Point)));
         dev_->cap = n_;
     }
     // file table for event batches
@@ -1007,13 +1228,30 @@ int Engine::build() {
     return 0;
 }
 
+template <int BITS>
+static void l0_pass(int p, int passes, const Point* in, Arena src, Arena dst, uint64_t n, const L0Params& P, int shift,
+                    uint32_t* counts, uint32_t ntiles, uint32_t* hist, uint32_t D, Counters* ctr, const uint32_t* files,
+                    uint32_t nfiles, ScanTemp& scan, hipStream_t st) {
+    const uint64_t nc = (uint64_t)ntiles << BITS;
+    if (p == 0) k_l0_up0<BITS><<<ntiles, kL0BS, 0, st>>>(in, n, P, shift, counts, ntiles, hist, D, ctr);
+    else k_l0_up<BITS><<<ntiles, kL0BS, 0, st>>>(src, n, P, shift, counts, ntiles);
+    scan_excl_u32(counts, counts, (uint32_t)nc, nullptr, scan, st);
+    const bool fin = p == passes - 1;
+    if (p == 0 && fin) k_l0_down<BITS, true, true><<<ntiles, kL0BS, 0, st>>>(in, src, dst, n, P, shift, counts, ntiles, files, nfiles);
+    else if (p == 0) k_l0_down<BITS, true, false><<<ntiles, kL0BS, 0, st>>>(in, src, dst, n, P, shift, counts, ntiles, files, nfiles);
+    else if (fin) k_l0_down<BITS, false, true><<<ntiles, kL0BS, 0, st>>>(in, src, dst, n, P, shift, counts, ntiles, files, nfiles);
+    else k_l0_down<BITS, false, false><<<ntiles, kL0BS, 0, st>>>(in, src, dst, n, P, shift, counts, ntiles, files, nfiles);
+    HIP_CHECK(hipGetLastError());
+}
+
 int Engine::level0_bin() {
     const uint32_t dim = cfg_.sub_grid_dimension;
-    const float cs = cell_size(cfg_.max_cell_size, 0);
-    const float cr = hex_radius(sub_cell_size(cs, dim));
+    const float cs = cell_size(cfg_.max_cell_size, 0), csc = cell_size(cfg_.max_cell_size, 1);
     L0Params P;
     P.cs = cs;
-    P.cr = cr;
+    P.cr = hex_radius(sub_cell_size(cs, dim));
+    P.csc = csc;
+    P.crc = hex_radius(sub_cell_size(csc, dim));
     const SlabGeom g = slab_geom(dim);
     P.nl = g.nl;
     P.dim2 = 2 * (int32_t)dim;
@@ -1027,7 +1265,6 @@ int Engine::level0_bin() {
     const uint64_t D = G * (uint64_t)P.nl;
     if (G > (1u << 20))
         return fail(-27, "level-0 cell grid too large (bounding box spans > 2^20 cells of max_cell_size)");
-    // scratch: hist, flags and scans over D and G (reuse arena B's arrays)
     uint32_t* hist = static_cast<uint32_t*>(dev_->get(D * 4));
     uint32_t* cnt_scan = static_cast<uint32_t*>(dev_->get(D * 4));
     uint32_t* sflag = static_cast<uint32_t*>(dev_->get(D * 4));
@@ -1035,8 +1272,31 @@ int Engine::level0_bin() {
     uint32_t* cscan = static_cast<uint32_t*>(dev_->get(G * 4));
     uint32_t* d_tot = static_cast<uint32_t*>(dev_->get(16));
     HIP_CHECK(hipMemsetAsync(hist, 0, D * 4, stream_));
-    k_l0_hist<<<grid_for(n_, 256, 4096), 256, 0, stream_>>>(d_in_, n_, P, hist, (uint32_t)D, dev_->ctr);
-    k_l0_flags<<<grid_for(std::max<uint64_t>(D, G), 256), 256, 0, stream_>>>(hist, (uint32_t)D, P.nl, sflag, cflag, (uint32_t)G);
+    // LSD passes over the dense slab id (key recomputed from positions every pass)
+    int bits = 0;
+    while ((1ull << bits) < D) bits++;
+    const int passes = std::max(1, (bits + 7) / 8);
+    const int per = std::max(1, (bits + passes - 1) / passes);
+    const uint32_t ntiles = (uint32_t)((n_ + kL0Tile - 1) / kL0Tile);
+    uint32_t* counts = static_cast<uint32_t*>(dev_->get(((uint64_t)ntiles << per) * 4 + 64));
+    Arena A0 = dev_->ar[0], A1 = dev_->ar[1];
+    Arena src = A1, dst = (passes % 2) ? A0 : A1;
+    for (int p = 0, shift = 0; p < passes; p++, shift += per) {
+        switch (per) {
+            case 1: l0_pass<1>(p, passes, d_in_, src, dst, n_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, (uint32_t)file_start_.size(), dev_->scan, stream_); break;
+            case 2: l0_pass<2>(p, passes, d_in_, src, dst, n_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, (uint32_t)file_start_.size(), dev_->scan, stream_); break;
+            case 3: l0_pass<3>(p, passes, d_in_, src, dst, n_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, (uint32_t)file_start_.size(), dev_->scan, stream_); break;
+            case 4: l0_pass<4>(p, passes, d_in_, src, dst, n_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, (uint32_t)file_start_.size(), dev_->scan, stream_); break;
+            case 5: l0_pass<5>(p, passes, d_in_, src, dst, n_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, (uint32_t)file_start_.size(), dev_->scan, stream_); break;
+            case 6: l0_pass<6>(p, passes, d_in_, src, dst, n_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, (uint32_t)file_start_.size(), dev_->scan, stream_); break;
+            case 7: l0_pass<7>(p, passes, d_in_, src, dst, n_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, (uint32_t)file_start_.size(), dev_->scan, stream_); break;
+            default: l0_pass<8>(p, passes, d_in_, src, dst, n_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, (uint32_t)file_start_.size(), dev_->scan, stream_); break;
+        }
+        src = dst;
+        dst = (dst.x == A0.x) ? A1 : A0;
+    }
+    // slab / cell tables from the dense histogram
+    k_l0_flags<<<grid_for(std::max<uint64_t>(D, G), 256, 1u << 30), 256, 0, stream_>>>(hist, (uint32_t)D, P.nl, sflag, cflag, (uint32_t)G);
     scan_excl_u32(hist, cnt_scan, (uint32_t)D, d_tot + 0, dev_->scan, stream_);
     scan_excl_u32(sflag, sflag, (uint32_t)D, d_tot + 1, dev_->scan, stream_);
     scan_excl_u32(cflag, cscan, (uint32_t)G, d_tot + 2, dev_->scan, stream_);
@@ -1054,6 +1314,7 @@ int Engine::level0_bin() {
     L->ncells = tots[2];
     L->nslabs = tots[1];
     L->arena = 0;
+    L->arrivals = n_;
     L->alloc(L->cell_idx, 3ull * L->ncells);
     L->alloc(L->cell_sb, L->ncells);
     L->alloc(L->cell_slab0, L->ncells + 1ull);
@@ -1063,25 +1324,18 @@ int Engine::level0_bin() {
     L->alloc(L->slab_n, L->nslabs);
     L->alloc(L->big_list, L->nslabs);
     L->alloc(L->small_list, L->nslabs);
+    L->alloc(L->dcap, (uint64_t)L->nslabs * kDests);
     k_l0_tables<<<grid_for(std::max<uint64_t>(D, G), 256, 1u << 30), 256, 0, stream_>>>(
-        hist, cnt_scan, sflag, cflag, cscan, (uint32_t)D, (uint32_t)G, P, L->cell_idx, L->cell_sb, L->cell_slab0, L->slab_cell,
-        L->slab_layer, L->slab_off, L->slab_n, L->big_list, L->small_list, dev_->ctr);
+        hist, cnt_scan, sflag, cflag, cscan, (uint32_t)D, (uint32_t)G, P, L->cell_idx, L->cell_sb, L->cell_slab0,
+        L->slab_cell, L->slab_layer, L->slab_off, L->slab_n);
     k_set_u32<<<1, 1, 0, stream_>>>(L->cell_slab0 + L->ncells, L->nslabs);
-    // keys = slab id (ordered by (cell, layer)), stable radix sort, gather into arena 0
-    Arena& A0 = dev_->ar[0];
-    Arena& A1 = dev_->ar[1];
-    k_l0_keys<<<grid_for(n_, 256, 1 << 20), 256, 0, stream_>>>(d_in_, n_, P, sflag, A1.k, A1.e);
-    int bits = 0;
-    while ((1ull << bits) < L->nslabs) bits++;
-    const int where = radix_sort_pairs(A1.k, A1.e, A1.x ? reinterpret_cast<uint32_t*>(A1.x) : nullptr,
-                                       reinterpret_cast<uint32_t*>(A1.y), (uint32_t)n_, bits, dev_->sort, stream_);
-    const uint32_t* perm = where ? reinterpret_cast<uint32_t*>(A1.y) : A1.e;
-    k_l0_gather<<<grid_for(n_, 256, 1 << 20), 256, 0, stream_>>>(d_in_, perm, n_, A0, dev_->files,
-                                                                   (uint32_t)file_start_.size());
+    k_l0_lists<<<grid_for(L->nslabs, 256, 1u << 30), 256, 0, stream_>>>(L->slab_n, L->nslabs, L->big_list, L->small_list, dev_->ctr);
+    k_l0_dcap<<<L->nslabs, 256, 0, stream_>>>(A0, P, L->cell_idx, L->slab_cell, L->slab_layer, L->slab_off, L->slab_n, L->dcap, dev_->ctr);
     HIP_CHECK(hipGetLastError());
     ev_end(ST_L0);
     HIP_CHECK(hipMemcpyAsync(&hc, dev_->ctr, sizeof hc, hipMemcpyDeviceToHost, stream_));
     HIP_CHECK(hipStreamSynchronize(stream_));
+    if (hc.err) return fail(-34, "level-0 capacities: routing error (internal error)");
     L->nbig = hc.nbig;
     L->nsmall = hc.nsmall;
     stats_.cells += L->ncells;
@@ -1094,24 +1348,34 @@ int Engine::run_level(uint32_t h) {
     Level* L = levels_[h];
     const uint32_t dim = cfg_.sub_grid_dimension;
     const SlabGeom g = slab_geom(dim);
-    const float cs = cell_size(cfg_.max_cell_size, h), csc = cell_size(cfg_.max_cell_size, h + 1);
+    const float cs = cell_size(cfg_.max_cell_size, h), csc = cell_size(cfg_.max_cell_size, h + 1),
+                csg = cell_size(cfg_.max_cell_size, h + 2);
     const Arena& in = dev_->ar[L->arena];
     const Arena& nx = dev_->ar[1 - L->arena];
-    L->alloc(L->slab_grid_off, L->nslabs);
+    const uint64_t ND = (uint64_t)L->nslabs * kDests;
+    L->alloc(L->dest_off, ND);
+    L->alloc(L->dest_n, ND);
+    L->alloc(L->gcap, ND * kDests);
+    L->alloc(L->grid_off, L->nslabs);
     L->alloc(L->slab_grid_n, L->nslabs);
-    L->alloc(L->dest_off, (uint64_t)L->nslabs * kDests);
-    L->alloc(L->dest_n, (uint64_t)L->nslabs * kDests);
     L->alloc(L->bkt_state, 8ull * L->ncells);
     L->alloc(L->bkt_off, 8ull * L->ncells);
     L->alloc(L->bkt_n, 8ull * L->ncells);
     L->alloc(L->bkt_sb, 8ull * L->ncells);
     L->alloc(L->bkt_nd, 8ull * L->ncells);
-    // reset the next-arena cursor and the next-level counters (keep out_cur)
+    L->alloc(L->grid, L->arrivals);
+    L->kept_cap = std::min<uint64_t>(L->arrivals, 8ull * L->ncells * cfg_.cell_point_overflow_limit);
+    L->alloc(L->kept, L->kept_cap);
+    uint32_t* scratch = static_cast<uint32_t*>(dev_->get(16));
+    // output regions from exclusive scans (no allocation atomics in the slab kernels)
+    scan_excl_u32(L->dcap, L->dest_off, (uint32_t)ND, scratch, dev_->scan, stream_);
+    scan_excl_u32(L->slab_n, L->grid_off, L->nslabs, scratch + 1, dev_->scan, stream_);
+    // per-level counters
     {
         Counters hc;
         HIP_CHECK(hipMemcpyAsync(&hc, dev_->ctr, sizeof hc, hipMemcpyDeviceToHost, stream_));
         HIP_CHECK(hipStreamSynchronize(stream_));
-        hc.arena_cur = 0;
+        hc.kept_cur = 0;
         hc.nbig = hc.nsmall = 0;
         hc.arrivals_next = 0;
         HIP_CHECK(hipMemcpyAsync(dev_->ctr, &hc, sizeof hc, hipMemcpyHostToDevice, stream_));
@@ -1119,24 +1383,29 @@ int Engine::run_level(uint32_t h) {
     SlabParams SP;
     SP.in = in;
     SP.nx = nx;
-    SP.out = dev_->out;
+    SP.grid = L->grid;
     SP.cell_idx = L->cell_idx;
     SP.cell_sb = L->cell_sb;
     SP.slab_cell = L->slab_cell;
     SP.slab_layer = L->slab_layer;
     SP.slab_off = L->slab_off;
     SP.slab_n = L->slab_n;
-    SP.slab_grid_off = L->slab_grid_off;
-    SP.slab_grid_n = L->slab_grid_n;
+    SP.grid_off = L->grid_off;
+    SP.dcap = L->dcap;
     SP.dest_off = L->dest_off;
+    SP.slab_grid_n = L->slab_grid_n;
     SP.dest_n = L->dest_n;
+    SP.gcap = L->gcap;
     SP.ctr = dev_->ctr;
     SP.cs = cs;
     SP.cr = hex_radius(sub_cell_size(cs, dim));
     SP.cs_child = csc;
     SP.cr_child = hex_radius(sub_cell_size(csc, dim));
+    SP.cs_gchild = csg;
+    SP.cr_gchild = hex_radius(sub_cell_size(csg, dim));
     SP.tx = g.tx;
     SP.ty = g.ty;
+    SP.check_gchild = (h + 2 < kMaxDepth) ? 1 : 0;
     if (L->nbig) {
         SP.list = L->big_list;
         ev_begin(ST_DENSE);
@@ -1152,9 +1421,9 @@ int Engine::run_level(uint32_t h) {
     HIP_CHECK(hipGetLastError());
     BucketParams BP;
     BP.nx = nx;
-    BP.out = dev_->out;
+    BP.kept = L->kept;
+    BP.kept_cap = L->kept_cap;
     BP.cell_slab0 = L->cell_slab0;
-    BP.slab_layer = L->slab_layer;
     BP.dest_off = L->dest_off;
     BP.dest_n = L->dest_n;
     BP.bkt_state = L->bkt_state;
@@ -1170,7 +1439,6 @@ int Engine::run_level(uint32_t h) {
     ev_end(ST_BUCKET);
     HIP_CHECK(hipGetLastError());
     ev_begin(ST_NEXT);
-    // next level
     uint32_t* flag = static_cast<uint32_t*>(dev_->get(nb * 4ull));
     uint32_t* ndv = static_cast<uint32_t*>(dev_->get(nb * 4ull));
     uint32_t* tots = static_cast<uint32_t*>(dev_->get(16));
@@ -1183,11 +1451,14 @@ int Engine::run_level(uint32_t h) {
     HIP_CHECK(hipMemcpyAsync(ht, tots, 8, hipMemcpyDeviceToHost, stream_));
     HIP_CHECK(hipMemcpyAsync(&hc, dev_->ctr, sizeof hc, hipMemcpyDeviceToHost, stream_));
     HIP_CHECK(hipStreamSynchronize(stream_));
+    L->kept_used = hc.kept_cur;
     stats_.grid_points = hc.grid_total;
-    stats_.kept_points = hc.out_cur - hc.grid_total;
+    stats_.kept_points = hc.kept_total;
     if (hc.err) {
-        char buf[160];
-        snprintf(buf, sizeof buf, "device error flags 0x%x at level %u (slot range/layer/octant/sel/kept-cap)", hc.err, h);
+        char buf[200];
+        snprintf(buf, sizeof buf,
+                 "device error flags 0x%x at level %u (1 slot range, 2 layer, 4 octant, 8 sel, 16 kept cap, 64 capacity, 128 claim)",
+                 hc.err, h);
         return fail(-5, buf);
     }
     if (ht[0] > 0) {
@@ -1207,11 +1478,7 @@ int Engine::run_level(uint32_t h) {
         N->alloc(N->slab_n, N->nslabs);
         N->alloc(N->big_list, N->nslabs);
         N->alloc(N->small_list, N->nslabs);
-        {
-            Counters z = hc;
-            z.nbig = z.nsmall = 0;
-            HIP_CHECK(hipMemcpyAsync(dev_->ctr, &z, sizeof z, hipMemcpyHostToDevice, stream_));
-        }
+        N->alloc(N->dcap, (uint64_t)N->nslabs * kDests);
         NextParams Q;
         Q.bkt_state = L->bkt_state;
         Q.bkt_sb = L->bkt_sb;
@@ -1222,6 +1489,7 @@ int Engine::run_level(uint32_t h) {
         Q.slab_layer = L->slab_layer;
         Q.dest_off = L->dest_off;
         Q.dest_n = L->dest_n;
+        Q.gcap = L->gcap;
         Q.ncell_idx = N->cell_idx;
         Q.ncell_sb = N->cell_sb;
         Q.ncell_slab0 = N->cell_slab0;
@@ -1229,16 +1497,20 @@ int Engine::run_level(uint32_t h) {
         Q.nslab_layer = N->slab_layer;
         Q.nslab_off = N->slab_off;
         Q.nslab_n = N->slab_n;
+        Q.ndcap = N->dcap;
         Q.nbig_list = N->big_list;
         Q.nsmall_list = N->small_list;
         Q.ctr = dev_->ctr;
+        ev_begin(ST_NEXT);
         k_next_emit<<<nb, 256, 0, stream_>>>(Q);
         k_set_u32<<<1, 1, 0, stream_>>>(N->cell_slab0 + N->ncells, N->nslabs);
+        ev_end(ST_NEXT);
         HIP_CHECK(hipGetLastError());
         HIP_CHECK(hipMemcpyAsync(&hc, dev_->ctr, sizeof hc, hipMemcpyDeviceToHost, stream_));
         HIP_CHECK(hipStreamSynchronize(stream_));
         N->nbig = hc.nbig;
         N->nsmall = hc.nsmall;
+        N->arrivals = hc.arrivals_next;
         stats_.arrivals += hc.arrivals_next;
         stats_.cells += N->ncells;
         stats_.slabs += N->nslabs;
@@ -1248,12 +1520,13 @@ int Engine::run_level(uint32_t h) {
 
 int Engine::download(std::vector<LevelHost>& out, std::vector<Point>& grid, std::vector<Point>& kept) {
     out.clear();
-    Counters hc;
-    HIP_CHECK(hipMemcpyAsync(&hc, dev_->ctr, sizeof hc, hipMemcpyDeviceToHost, stream_));
-    HIP_CHECK(hipStreamSynchronize(stream_));
-    grid.resize(hc.out_cur);
-    if (hc.out_cur) HIP_CHECK(hipMemcpyAsync(grid.data(), dev_->out, (uint64_t)hc.out_cur * sizeof(Point), hipMemcpyDeviceToHost, stream_));
-    kept.clear();   // kept lists share the output arena with the grid points
+    grid.clear();
+    kept.clear();
+    uint64_t gsz = 0, ksz = 0;
+    for (Level* L : levels_) { gsz += L->arrivals; ksz += L->kept_used; }
+    grid.resize(gsz);
+    kept.resize(ksz);
+    uint64_t go = 0, ko = 0;
     for (Level* L : levels_) {
         LevelHost H;
         H.h = L->h;
@@ -1263,12 +1536,18 @@ int Engine::download(std::vector<LevelHost>& out, std::vector<Point>& grid, std:
         };
         cp(H.cell_idx, L->cell_idx, 3ull * L->ncells);
         cp(H.cell_slab0, L->cell_slab0, L->ncells + 1ull);
-        cp(H.slab_grid_off, L->slab_grid_off, L->nslabs);
+        cp(H.slab_grid_off, L->grid_off, L->nslabs);
         cp(H.slab_grid_n, L->slab_grid_n, L->nslabs);
         cp(H.bkt_state, L->bkt_state, 8ull * L->ncells);
         cp(H.bkt_off, L->bkt_off, 8ull * L->ncells);
         cp(H.bkt_n, L->bkt_n, 8ull * L->ncells);
+        if (L->arrivals) HIP_CHECK(hipMemcpyAsync(grid.data() + go, L->grid, L->arrivals * sizeof(Point), hipMemcpyDeviceToHost, stream_));
+        if (L->kept_used) HIP_CHECK(hipMemcpyAsync(kept.data() + ko, L->kept, (uint64_t)L->kept_used * sizeof(Point), hipMemcpyDeviceToHost, stream_));
         HIP_CHECK(hipStreamSynchronize(stream_));
+        H.grid_base = go;
+        H.kept_base = ko;
+        go += L->arrivals;
+        ko += L->kept_used;
         out.push_back(std::move(H));
     }
     return 0;

@@ -188,7 +188,7 @@ static void put32(std::string& b, uint32_t v) { b.append(reinterpret_cast<const 
 static void putf(std::string& b, float v) { b.append(reinterpret_cast<const char*>(&v), 4); }
 
 int write_output(const std::string& dir, const Metadata& meta, const std::vector<LevelHost>& levels,
-                 const std::vector<Point>& arena, std::string& err) {
+                 const std::vector<Point>& grid, const std::vector<Point>& kept, std::string& err) {
     if (mkdir(dir.c_str(), 0755) != 0 && errno != EEXIST) { err = "cannot create " + dir; return -errno; }
     for (uint32_t h = 0; h < meta.hierarchies; h++) {   // converter.rs:141-158
         std::string hd = dir + "/h_" + std::to_string(h);
@@ -223,7 +223,7 @@ int write_output(const std::string& dir, const Metadata& meta, const std::vector
             putf(buf, cell_pos1(ix, size)); putf(buf, cell_pos1(iy, size)); putf(buf, cell_pos1(iz, size));
             // grid points (cell.rs:158-160; order free)
             for (uint32_t s = L.cell_slab0[c]; s < L.cell_slab0[c + 1]; s++)
-                buf.append(reinterpret_cast<const char*>(arena.data() + L.slab_grid_off[s]), 16ull * L.slab_grid_n[s]);
+                buf.append(reinterpret_cast<const char*>(grid.data() + L.grid_base + L.slab_grid_off[s]), 16ull * L.slab_grid_n[s]);
             buf.push_back((char)(uint8_t)nb);   // cell.rs:162
             for (int o = 0; o < 8; o++) {
                 const uint32_t st = L.bkt_state[8 * c + o];
@@ -233,7 +233,7 @@ int write_output(const std::string& dir, const Metadata& meta, const std::vector
                 put32(buf, (uint32_t)(2 * iz + ((o >> 2) & 1)));
                 if (st == 1) {
                     put32(buf, L.bkt_n[8 * c + o]);
-                    buf.append(reinterpret_cast<const char*>(arena.data() + L.bkt_off[8 * c + o]), 16ull * L.bkt_n[8 * c + o]);
+                    buf.append(reinterpret_cast<const char*>(kept.data() + L.kept_base + L.bkt_off[8 * c + o]), 16ull * L.bkt_n[8 * c + o]);
                 } else {
                     put32(buf, 0);
                 }

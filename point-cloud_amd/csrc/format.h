@@ -27,7 +27,7 @@ bool parse_metadata_json(const std::string& text, Metadata& m, std::string& err)
 // Writes h_{h}/c_{x}_{y}_{z}.bin for every cell of every level, then metadata.json
 // (converter.rs:218-238 order: cells first, metadata last).
 int write_output(const std::string& dir, const Metadata& meta, const std::vector<LevelHost>& levels,
-                 const std::vector<Point>& arena, std::string& err);
+                 const std::vector<Point>& grid, const std::vector<Point>& kept, std::string& err);
 
 // PLY reader.  Returns points of the `vertex` element.  `ascii` is set when the
 // file is ASCII-encoded: the reference's ASCII branch parses but never stores

@@ -83,8 +83,8 @@ struct SlabGeom {
 };
 PCC_HD SlabGeom slab_geom(uint32_t dim) {
     SlabGeom g;
-    g.tx = 2 * ((int32_t)(dim * 577u / 1000u) + 5);   // dim/sqrt3 + margin
-    g.ty = 2 * ((int32_t)(dim * 2u / 3u) + 5);        // 2*dim/3 + margin
+    g.tx = 2 * ((int32_t)(dim * 577u / 1000u) + 3);   // dim/sqrt3 + margin (dim 96: 116, observed |dx| <= 56)
+    g.ty = 2 * ((int32_t)(dim * 2u / 3u) + 2);        // 2*dim/3 + margin  (dim 96: 132, observed |dy| <= 64)
     g.nl = 2 * (int32_t)dim + 5;                      // layers [2*dim*iz - 2, 2*dim*(iz+1) + 2]
     return g;
 }

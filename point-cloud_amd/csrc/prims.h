@@ -16,6 +16,14 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
     return l == 0 ? 0ull : (~0ull >> (64 - l));
 }
 
+// Workgroup barrier that orders LDS only: waits lgkmcnt(0) but leaves global
+// loads in flight (a plain __syncthreads() drains vmcnt and kills prefetch).
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // ---------------------------------------------------------------- block scan
 // Exclusive scan of one u32 per thread across a BS-thread block; returns the
 // exclusive prefix and writes the block total to *total (all threads).
