@@ -33,6 +33,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 
 #include "hip_check.h"
@@ -71,6 +72,7 @@ struct Counters {
     uint32_t kept_cur;    // kept-list cursor inside the level's kept region
     uint32_t err;
     uint32_t nbig, nsmall;
+    uint32_t max_slab, pad0;
     unsigned long long arrivals_next;  // sum of next-level slab sizes
     unsigned long long grid_total;     // grid winners written so far (all levels)
     unsigned long long kept_total;
@@ -145,6 +147,21 @@ struct Engine::Level {
     void alloc(T*& p, uint64_t n) { p = static_cast<T*>(dev->get(n * sizeof(T))); }
 };
 
+// ------------------------------------------------------------------ diagnostics
+// Diagnostic build only (-DPCC_STAMPS): per-wave s_memtime phase sums of the
+// slab kernel, added into P.stamps[phase]; never compiled into the product.
+#ifdef PCC_STAMPS
+#define STAMP_DECL unsigned long long st_t0 = __builtin_amdgcn_s_memtime(), st_acc[12] = {};
+#define STAMP(ph) do { const unsigned long long st_n = __builtin_amdgcn_s_memtime(); st_acc[ph] += st_n - st_t0; st_t0 = st_n; } while (0)
+#define STAMP_COUNT(ph, v) do { st_acc[ph] += (v); } while (0)
+#define STAMP_FLUSH(ptr) do { if ((threadIdx.x & 63) == 0) for (int q_ = 0; q_ < 12; q_++) atomicAdd((ptr) + q_, st_acc[q_]); } while (0)
+#else
+#define STAMP_DECL
+#define STAMP(ph) do {} while (0)
+#define STAMP_COUNT(ph, v) do {} while (0)
+#define STAMP_FLUSH(ptr) do {} while (0)
+#endif
+
 // ------------------------------------------------------------------ small helpers
 __device__ __forceinline__ void set_err(Counters* c, uint32_t bit) { atomicOr(&c->err, bit); }
 
@@ -176,9 +193,92 @@ __device__ __forceinline__ int route(float csc, float crc, int32_t cx, int32_t c
     u = sat_i32(z / crc);
     const int32_t bx = ix - 2 * cx, by = iy - 2 * cy, bz = iz - 2 * cz;
     const int32_t sel = u - 2 * t + 1;
-    if ((bx | by | bz) & ~1) { err |= ERR_OCTANT; return -1; }
-    if (sel < 0 || sel > 2) { err |= ERR_SEL; return -1; }
-    return (bx | (by << 1) | (bz << 2)) * 3 + sel;
+    const bool bad_oct = ((bx | by | bz) & ~1) != 0;
+    const bool bad_sel = sel < 0 || sel > 2;
+    err |= bad_oct ? (uint32_t)ERR_OCTANT : (bad_sel ? (uint32_t)ERR_SEL : 0u);
+    return (bad_oct || bad_sel) ? -1 : (bx | (by << 1) | (bz << 2)) * 3 + sel;
+}
+
+// floorf(fl(a / b)) and truncf(fl(a / b)) without a full division in the common
+// case: the product with the correctly rounded reciprocal differs from the
+// correctly rounded quotient by at most ~4 ulp, so unless it lies within a
+// (16x wider) margin of an integer, both have the same floor/trunc.  Lanes near
+// an integer fall back to the exact IEEE division (wave-uniform branch guard).
+__device__ __forceinline__ float floor_div(float a, float b, float inv_b) {
+    const float q = a * inv_b;
+    const float m = (fabsf(q) * 0x1p-20f) + 0x1p-126f;
+    const bool amb = floorf(q - m) != floorf(q + m);
+    float r = floorf(q);
+    if (__ballot(amb)) {
+        if (amb) r = floorf(a / b);
+    }
+    return r;
+}
+__device__ __forceinline__ float trunc_div(float a, float b, float inv_b) {
+    const float q = a * inv_b;
+    const float m = (fabsf(q) * 0x1p-20f) + 0x1p-126f;
+    const bool amb = truncf(q - m) != truncf(q + m);
+    float r = truncf(q);
+    if (__ballot(amb)) {
+        if (amb) r = truncf(a / b);
+    }
+    return r;
+}
+
+// Per-level constants for the slot / routing arithmetic (all computed on the
+// host with the reference's own f32 formulas; see pcc_math.h).
+struct LevelGeo {
+    float cr, crx, cry, inv_cr;          // hex radius, cr*S3, (-cr)*S3 (hex.rs:69-70), 1/cr
+    float csc, inv_csc, crc, inv_crc;    // child level cell size / hex radius
+    float csg, inv_csg, crg, inv_crg;    // grandchild level
+};
+
+// hex.rs:67-85 + 45-51 with the floor/trunc-only divisions done by floor_div.
+__device__ __forceinline__ I3 hex_from_world_fast(float px, float py, float pz, const LevelGeo& G) {
+    const float x = px / G.crx;
+    const float y = py / G.cry;
+    const float t = (kSqrt3 * y) + 1.0f;
+    const float t1 = floorf(t + x);
+    const float t2 = t - x;
+    const float t3 = (2.0f * x) + 1.0f;
+    const int32_t q = sat_i32(floor_div(t1 + t3, 3.0f, 0x1.555556p-2f));
+    const int32_t r = (int32_t)(0u - (uint32_t)sat_i32(floor_div(t1 + t2, 3.0f, 0x1.555556p-2f)));
+    const int32_t h = sat_i32(trunc_div(pz, G.cr, G.inv_cr));
+    I3 o = {q + (r - (r & 1)) / 2, r, h};
+    return o;
+}
+
+__device__ __forceinline__ int route_fast(float cs, float inv_cs, float cr, float inv_cr, int32_t cx, int32_t cy,
+                                          int32_t cz, int32_t t, float x, float y, float z, int32_t& ix,
+                                          int32_t& iy, int32_t& iz, int32_t& u, uint32_t& err) {
+    ix = sat_i32(floor_div(x, cs, inv_cs));
+    iy = sat_i32(floor_div(y, cs, inv_cs));
+    iz = sat_i32(floor_div(z, cs, inv_cs));
+    u = sat_i32(trunc_div(z, cr, inv_cr));
+    const int32_t bx = ix - 2 * cx, by = iy - 2 * cy, bz = iz - 2 * cz;
+    const int32_t sel = u - 2 * t + 1;
+    const bool bad_oct = ((bx | by | bz) & ~1) != 0;
+    const bool bad_sel = sel < 0 || sel > 2;
+    err |= bad_oct ? (uint32_t)ERR_OCTANT : (bad_sel ? (uint32_t)ERR_SEL : 0u);
+    return (bad_oct || bad_sel) ? -1 : (bx | (by << 1) | (bz << 2)) * 3 + sel;
+}
+
+// Buffer descriptor of a wave-uniform range.  Base and size are forced into
+// SGPRs (readfirstlane): values loaded from global memory are otherwise kept
+// in VGPRs and every buffer op becomes a readfirstlane "waterfall" loop.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t srd(const void* base, uint64_t bytes) {
+    const uint64_t a = (uint64_t)base;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    const uint32_t nr = __builtin_amdgcn_readfirstlane((uint32_t)(bytes > 0xFFFFFFFFull ? 0xFFFFFFFFull : bytes));
+    void* p = (void*)(((uint64_t)hi << 32) | lo);
+    return __builtin_amdgcn_make_buffer_rsrc(p, 0, (int)nr, 0x00020000);
+}
+__device__ __forceinline__ uint32_t bld(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
+}
+__device__ __forceinline__ void bst(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t v) {
+    __builtin_amdgcn_raw_buffer_store_b32(v, r, off, 0, 0);
 }
 
 // ------------------------------------------------------------------ input kernels
@@ -256,6 +356,7 @@ constexpr int kL0BS = 256, kL0IPT = 8, kL0Tile = kL0BS * kL0IPT, kL0W = kL0BS / 
 constexpr int kHistLds = 8192;
 
 // pass-0 upsweep from the AoS input: per-tile digit histogram + full dense-slab histogram
+// (grid-stride over tiles so the dense histogram is flushed once per workgroup)
 template <int BITS>
 __global__ __launch_bounds__(kL0BS) void k_l0_up0(const Point* __restrict__ in, uint64_t n, L0Params P, int shift,
                                                   uint32_t* __restrict__ counts, uint32_t ntiles, uint32_t* hist,
@@ -264,24 +365,34 @@ __global__ __launch_bounds__(kL0BS) void k_l0_up0(const Point* __restrict__ in, 
     __shared__ uint32_t dh[R];
     __shared__ uint32_t h[kHistLds];
     const bool lds = D <= (uint32_t)kHistLds;
-    for (int i = threadIdx.x; i < R; i += kL0BS) dh[i] = 0;
     if (lds) for (uint32_t i = threadIdx.x; i < D; i += kL0BS) h[i] = 0;
-    __syncthreads();
-    const uint64_t base = (uint64_t)blockIdx.x * kL0Tile;
     const float4* p4 = reinterpret_cast<const float4*>(in);
-#pragma unroll 4
-    for (int r = 0; r < kL0IPT; r++) {
-        const uint64_t i = base + (uint64_t)r * kL0BS + threadIdx.x;
-        if (i < n) {
-            const float4 v = p4[i];
-            const int64_t d = l0_dense(P, v.x, v.y, v.z);
-            if (d < 0) { set_err(ctr, ERR_L0_RANGE); continue; }
-            atomicAdd(&dh[((uint64_t)d >> shift) & (R - 1)], 1u);
-            if (lds) atomicAdd(&h[d], 1u); else atomicAdd(&hist[d], 1u);
+    uint32_t err = 0;
+    for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        for (int i = threadIdx.x; i < R; i += kL0BS) dh[i] = 0;
+        __syncthreads();
+        const uint64_t base = (uint64_t)tile * kL0Tile;
+        float4 v[kL0IPT];
+#pragma unroll
+        for (int r = 0; r < kL0IPT; r++) {
+            const uint64_t i = base + (uint64_t)r * kL0BS + threadIdx.x;
+            if (i < n) v[r] = p4[i];
         }
+#pragma unroll
+        for (int r = 0; r < kL0IPT; r++) {
+            const uint64_t i = base + (uint64_t)r * kL0BS + threadIdx.x;
+            if (i < n) {
+                const int64_t d = l0_dense(P, v[r].x, v[r].y, v[r].z);
+                if (d < 0) { err = ERR_L0_RANGE; continue; }
+                atomicAdd(&dh[((uint64_t)d >> shift) & (R - 1)], 1u);
+                if (lds) atomicAdd(&h[d], 1u); else atomicAdd(&hist[d], 1u);
+            }
+        }
+        __syncthreads();
+        for (int d = threadIdx.x; d < R; d += kL0BS) counts[(uint64_t)d * ntiles + tile] = dh[d];
     }
+    if (err) set_err(ctr, err);
     __syncthreads();
-    for (int d = threadIdx.x; d < R; d += kL0BS) counts[(uint64_t)d * ntiles + blockIdx.x] = dh[d];
     if (lds)
         for (uint32_t i = threadIdx.x; i < D; i += kL0BS)
             if (h[i]) atomicAdd(&hist[i], h[i]);
@@ -438,20 +549,23 @@ __global__ void k_l0_tables(const uint32_t* hist, const uint32_t* cnt_scan, cons
 }
 
 // capacities of the level-0 slabs: arrivals per child slab
+constexpr uint32_t kDcapChunk = 32768;
 __global__ __launch_bounds__(256) void k_l0_dcap(Arena A, L0Params P, const int32_t* cell_idx,
                                                  const uint32_t* slab_cell, const int32_t* slab_layer,
                                                  const uint32_t* slab_off, const uint32_t* slab_n, uint32_t* dcap,
                                                  Counters* ctr) {
     __shared__ uint32_t cnt[kDests];
-    const uint32_t s = blockIdx.x;
+    const uint32_t s = blockIdx.x, j0 = blockIdx.y * kDcapChunk;
+    const uint32_t cr_ = slab_cell[s], off = slab_off[s], n = slab_n[s];
+    if (j0 >= n) return;
+    const uint32_t j1 = min(n, j0 + kDcapChunk);
     if (threadIdx.x < kDests) cnt[threadIdx.x] = 0;
     __syncthreads();
-    const uint32_t cr_ = slab_cell[s], off = slab_off[s], n = slab_n[s];
     const int32_t t = slab_layer[s];
     const int32_t cx = cell_idx[3 * cr_], cy = cell_idx[3 * cr_ + 1], cz = cell_idx[3 * cr_ + 2];
     uint32_t err = 0;
     uint32_t loc[kDests] = {};
-    for (uint32_t j = threadIdx.x; j < n; j += 256) {
+    for (uint32_t j = j0 + threadIdx.x; j < j1; j += 256) {
         int32_t ix, iy, iz, u;
         const int d = route(P.csc, P.crc, cx, cy, cz, t, A.x[off + j], A.y[off + j], A.z[off + j], ix, iy, iz, u, err);
         if (d >= 0) {
@@ -467,7 +581,7 @@ __global__ __launch_bounds__(256) void k_l0_dcap(Arena A, L0Params P, const int3
     }
     if (err) set_err(ctr, err);
     __syncthreads();
-    if (threadIdx.x < kDests) dcap[s * kDests + threadIdx.x] = cnt[threadIdx.x];
+    if (threadIdx.x < kDests && cnt[threadIdx.x]) atomicAdd(&dcap[s * kDests + threadIdx.x], cnt[threadIdx.x]);
 }
 
 // ------------------------------------------------------------------ slab kernels
@@ -488,9 +602,12 @@ struct SlabParams {
     uint32_t* dest_n;
     uint32_t* gcap;
     Counters* ctr;
-    float cs, cr, cs_child, cr_child, cs_gchild, cr_gchild;
+    float cs;
+    LevelGeo G;
     int32_t tx, ty;
     int32_t check_gchild;
+    int32_t ablate;   // timing-only diagnostics (PCC_ABLATE): 1 no emission, 2 no claim rounds, 4 no occupant loads
+    unsigned long long* stamps;   // diagnostic build only
 };
 
 template <bool DENSE>
@@ -500,23 +617,23 @@ template <>
 struct SlabLds<true> {
     static constexpr int BS = kDenseBS, TAB = kDenseTab, CLAIM = kDenseClaim, NW = BS / 64;
     unsigned long long tab[TAB];
-    unsigned long long claim[CLAIM];
+    uint32_t claim[2][CLAIM];   // double-buffered by chunk parity: no clearing barrier
     uint32_t tkey[1];
     uint32_t gcnt[kDests * kDests];
     uint32_t doff[kDests], dcap[kDests], dcur[kDests];
     uint32_t wcnt[NW][kDests], wpre[NW][kDests];
-    uint32_t npend, nwin, err;
+    uint32_t npend[2], nwin, err;
 };
 template <>
 struct SlabLds<false> {
     static constexpr int BS = kSmallBS, TAB = kSmallTab, CLAIM = kSmallClaim, NW = BS / 64;
     unsigned long long tab[TAB];
-    unsigned long long claim[CLAIM];
+    uint32_t claim[2][CLAIM];
     uint32_t tkey[TAB];
     uint32_t gcnt[kDests * kDests];
     uint32_t doff[kDests], dcap[kDests], dcur[kDests];
     uint32_t wcnt[NW][kDests], wpre[NW][kDests];
-    uint32_t npend, nwin, err;
+    uint32_t npend[2], nwin, err;
 };
 
 __device__ __forceinline__ uint32_t hash_slot(uint32_t k) { return (k * 2654435761u) >> 15; }
@@ -541,19 +658,21 @@ __device__ __forceinline__ int slot_entry(SlabLds<DENSE>& S, uint32_t local) {
     }
 }
 
-// Per-chunk claim table keyed by slot: entry = (slot << 32) | min pending thread.
+// Per-chunk claim table keyed by slot: entry = (slot << 11) | min pending thread
+// (0x7FF once that thread has been applied).  Slots < 2^14, threads < 2^10.
+constexpr uint32_t kClaimDone = 0x7FFu;
 template <int CLAIM>
-__device__ __forceinline__ int claim_insert(unsigned long long* H, uint32_t local, uint32_t tid) {
-    const unsigned long long mine = ((unsigned long long)local << 32) | tid;
+__device__ __forceinline__ int claim_insert(uint32_t* H, uint32_t local, uint32_t tid) {
+    const uint32_t mine = (local << 11) | tid;
     uint32_t h = hash_slot(local) & (CLAIM - 1);
     for (int probe = 0; probe < CLAIM; probe++) {
-        unsigned long long e = H[h];
-        if (e == kEmpty64) {
-            const unsigned long long old = atomicCAS(&H[h], kEmpty64, mine);
-            if (old == kEmpty64) return (int)h;
+        uint32_t e = H[h];
+        if (e == kEmpty32) {
+            const uint32_t old = atomicCAS(&H[h], kEmpty32, mine);
+            if (old == kEmpty32) return (int)h;
             e = old;
         }
-        if ((uint32_t)(e >> 32) == local) {
+        if ((e >> 11) == local) {
             atomicMin(&H[h], mine);
             return (int)h;
         }
@@ -567,88 +686,152 @@ __global__ __launch_bounds__(SlabLds<DENSE>::BS) void k_slab(SlabParams P) {
     using L = SlabLds<DENSE>;
     constexpr int BS = L::BS, TAB = L::TAB, CLAIM = L::CLAIM, NW = L::NW;
     __shared__ L S;
+    STAMP_DECL
     const uint32_t tid = threadIdx.x, wv = tid / 64;
     const uint32_t s = P.list[blockIdx.x];
     const uint32_t cr_ = P.slab_cell[s];
     const int32_t t = P.slab_layer[s];
-    const uint32_t off = P.slab_off[s], n = P.slab_n[s];
+    const uint32_t off = P.slab_off[s], n = P.slab_n[s], nm1 = n - 1;
     const int32_t cx = P.cell_idx[3 * cr_], cy = P.cell_idx[3 * cr_ + 1], cz = P.cell_idx[3 * cr_ + 2];
     const uint32_t sb = P.cell_sb[cr_];
+    const LevelGeo& G = P.G;
     // reference slot: the one holding the cell centre (metadata.rs:104-106)
-    const I3 c0 = hex_from_world(cell_pos1(cx, P.cs), cell_pos1(cy, P.cs), cell_pos1(cz, P.cs), P.cr);
+    const I3 c0 = hex_from_world_fast(cell_pos1(cx, P.cs), cell_pos1(cy, P.cs), cell_pos1(cz, P.cs), G);
     const int32_t rx = c0.x - P.tx / 2, ry = c0.y - P.ty / 2;
     uint32_t err = 0;
     if (tid == 0) atomicAdd(DENSE ? &P.ctr->dense_arrivals : &P.ctr->small_arrivals, (unsigned long long)n);
+    // buffer descriptors: this slab's arrivals, and the contiguous region of its
+    // 24 child slabs in the next arena (out-of-range offsets drop a store)
+    const uint64_t nb = (uint64_t)n * 4;
+    const __amdgpu_buffer_rsrc_t rX = srd(P.in.x + off, nb), rY = srd(P.in.y + off, nb), rZ = srd(P.in.z + off, nb);
+    const __amdgpu_buffer_rsrc_t rC = srd(P.in.c + off, nb), rK = srd(P.in.k + off, nb), rE = srd(P.in.e + off, nb);
+    const uint32_t dbase = P.dest_off[s * kDests];
+    const uint64_t db = (uint64_t)(P.dest_off[s * kDests + kDests - 1] + P.dcap[s * kDests + kDests - 1] - dbase) * 4;
+    const __amdgpu_buffer_rsrc_t oX = srd(P.nx.x + dbase, db), oY = srd(P.nx.y + dbase, db), oZ = srd(P.nx.z + dbase, db);
+    const __amdgpu_buffer_rsrc_t oC = srd(P.nx.c + dbase, db), oK = srd(P.nx.k + dbase, db), oE = srd(P.nx.e + dbase, db);
 
     for (int i = tid; i < TAB; i += BS) {
         S.tab[i] = kEmpty64;
         if constexpr (!DENSE) S.tkey[i] = kEmpty32;
     }
-    for (int i = tid; i < CLAIM; i += BS) S.claim[i] = kEmpty64;
+    for (int i = tid; i < 2 * CLAIM; i += BS) (&S.claim[0][0])[i] = kEmpty32;
     for (int i = tid; i < kDests * kDests; i += BS) S.gcnt[i] = 0;
     if (tid < kDests) {
         S.dcur[tid] = 0;
-        S.doff[tid] = P.dest_off[s * kDests + tid];
+        S.doff[tid] = P.dest_off[s * kDests + tid] - dbase;
         S.dcap[tid] = P.dcap[s * kDests + tid];
     }
     if (tid < NW * kDests) (&S.wcnt[0][0])[tid] = 0;
-    if (tid == 0) { S.npend = 0; S.nwin = 0; S.err = 0; }
+    if (tid == 0) { S.npend[0] = 0; S.npend[1] = 0; S.nwin = 0; S.err = 0; }
     __syncthreads();
+    STAMP(0);
 
-    // prefetch of the first chunk
-    float nxx = 0, nxy = 0, nxz = 0;
-    uint32_t nxc = 0, nxk = 0, nxe = 0;
-    if (tid < n) {
-        nxx = P.in.x[off + tid]; nxy = P.in.y[off + tid]; nxz = P.in.z[off + tid];
-        nxc = P.in.c[off + tid]; nxk = P.in.k[off + tid]; nxe = P.in.e[off + tid];
-    }
+    // Software pipeline, one chunk of BS arrivals (key order) per step:
+    //   phase A : slot/d2 of chunk i, claim inserts; routing + wave ranks of chunk i-1
+    //   barrier : then per round: apply claim winners | barrier | (round 1: chunk i-1
+    //             stores) check remaining | re-claim | barrier ...
+    // Chunk i-1's occupant loads were issued one step earlier.  A/B stages
+    // alternate so the loop carries no register copies of loaded values.
+    struct Stage {
+        int32_t em;
+        uint32_t j, k, e, c, oc;
+        float x, y, z, ox, oy, oz;
+    };
+    Stage A = {-1, 0, 0, 0, 0, 0, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    Stage B = A;
+    uint32_t jo = min(tid, nm1) * 4;
+    float nxx = __uint_as_float(bld(rX, jo)), nxy = __uint_as_float(bld(rY, jo)), nxz = __uint_as_float(bld(rZ, jo));
+    uint32_t nxc = bld(rC, jo), nxk = bld(rK, jo), nxe = bld(rE, jo);
     const uint64_t lt = lanemask_lt();
-    for (uint32_t base = 0; base < n; base += BS) {
-        const uint32_t j = base + tid;
+    const uint32_t nchunks = (n + BS - 1) / BS;
+    auto step = [&](uint32_t ci, Stage& cur, Stage& prv) {
+        const uint32_t par = ci & 1;
+        uint32_t* claim = S.claim[par];
+        const uint32_t j = ci * BS + tid;
         const bool valid = j < n;
         const float x = nxx, y = nxy, z = nxz;
         const uint32_t c = nxc, k = nxk, eb = max(nxe, sb);
-        // issue the next chunk's loads now; they stay in flight across the LDS barriers below
-        const uint32_t jn = j + BS;
-        if (jn < n) {
-            nxx = P.in.x[off + jn]; nxy = P.in.y[off + jn]; nxz = P.in.z[off + jn];
-            nxc = P.in.c[off + jn]; nxk = P.in.k[off + jn]; nxe = P.in.e[off + jn];
+        jo = min(j + BS, nm1) * 4;   // prefetch chunk i+1 (clamped)
+        nxx = __uint_as_float(bld(rX, jo)); nxy = __uint_as_float(bld(rY, jo)); nxz = __uint_as_float(bld(rZ, jo));
+        nxc = bld(rC, jo); nxk = bld(rK, jo); nxe = bld(rE, jo);
+        // ---- phase A (1): slot + distance of chunk i (hex.rs:67-85, 55-65)
+        const I3 sl = hex_from_world_fast(x, y, z, G);
+        const int32_t lx = sl.x - rx, ly = sl.y - ry;
+        const bool layer_ok = sl.z == t;
+        const bool range_ok = lx >= 0 && ly >= 0 && lx < P.tx && ly < P.ty;
+        err |= (valid && !layer_ok) ? (uint32_t)ERR_LAYER : ((valid && !range_ok) ? (uint32_t)ERR_SLOT_RANGE : 0u);
+        bool pending = valid && layer_ok && range_ok && !(P.ablate & 2);
+        const uint32_t local = pending ? (uint32_t)(ly * P.tx + lx) : 0u;
+        float X, Y, Z;
+        hex_to_world(sl, G.cr, X, Y, Z);
+        const float d2 = dist2(X, Y, Z, x, y, z);
+        int e = 0, hc = -1;
+        if (pending) {
+            e = slot_entry<DENSE>(S, local);
+            if (e >= 0) hc = claim_insert<CLAIM>(claim, local, tid);
+            if (e < 0 || hc < 0) { err |= ERR_CLAIM; pending = false; }
         }
-        bool pending = false;
-        float d2 = 0;
-        int e = 0, hc = 0;
-        uint32_t local = 0;
-        if (valid) {
-            const I3 sl = hex_from_world(x, y, z, P.cr);
-            const int32_t lx = sl.x - rx, ly = sl.y - ry;
-            if (sl.z != t) err |= ERR_LAYER;
-            else if (lx < 0 || ly < 0 || lx >= P.tx || ly >= P.ty) err |= ERR_SLOT_RANGE;
-            else {
-                local = (uint32_t)(ly * P.tx + lx);
-                e = slot_entry<DENSE>(S, local);
-                if (e < 0) err |= ERR_CLAIM;
-                else {
-                    float X, Y, Z;
-                    hex_to_world(sl, P.cr, X, Y, Z);
-                    d2 = dist2(X, Y, Z, x, y, z);
-                    pending = true;
-                }
+        {
+            const uint32_t np = (uint32_t)__popcll(__ballot(pending));
+            if ((tid & 63) == 0 && np) atomicAdd(&S.npend[par], np);
+        }
+        STAMP(1);
+        // ---- phase A (2): routing + wave ranks of chunk i-1 (stage prv)
+        const bool disp = prv.em >= 0 && (uint32_t)prv.em != prv.j;
+        const float ex = disp ? prv.ox : prv.x, ey = disp ? prv.oy : prv.y, ez = disp ? prv.oz : prv.z;
+        const uint32_t ec = disp ? prv.oc : prv.c;
+        int d, d2i;
+        {
+            int32_t ix, iy, iz, u;
+            uint32_t rerr = 0;
+            d = route_fast(G.csc, G.inv_csc, G.crc, G.inv_crc, cx, cy, cz, t, ex, ey, ez, ix, iy, iz, u, rerr);
+            int32_t jx, jy, jz, v;
+            uint32_t gerr = 0;
+            d2i = route_fast(G.csg, G.inv_csg, G.crg, G.inv_crg, ix, iy, iz, u, ex, ey, ez, jx, jy, jz, v, gerr);
+            if (prv.em >= 0) {
+                err |= rerr;
+                if (P.check_gchild && d >= 0) err |= gerr;
+            } else {
+                d = -1;
             }
+            if (d < 0) d2i = -1;
+        }
+        const bool vd = d >= 0;
+        uint64_t same = __ballot(vd);
+#pragma unroll
+        for (int b = 0; b < 5; b++) {
+            const uint64_t bb = __ballot(vd && ((d >> b) & 1));
+            same &= ((d >> b) & 1) ? bb : ~bb;
+        }
+        const uint32_t rw = __popcll(same & lt);
+        if (vd && rw == 0) S.wcnt[wv][d] = (uint32_t)__popcll(same);
+        {   // grandchild capacities: one LDS add per distinct (d, d2i) in the wave
+            const bool vg = vd && d2i >= 0;
+            uint64_t sg = same & __ballot(vg);
+#pragma unroll
+            for (int b = 0; b < 5; b++) {
+                const uint64_t bb = __ballot(vg && ((d2i >> b) & 1));
+                sg &= ((d2i >> b) & 1) ? bb : ~bb;
+            }
+            if (vg && __popcll(sg & lt) == 0) atomicAdd(&S.gcnt[d * kDests + d2i], (uint32_t)__popcll(sg));
+        }
+        STAMP(2);
+        lds_barrier();
+        STAMP(3);
+        // ---- phase B: ranks of chunk i-1 -> positions (wave 0), claim rounds of chunk i
+        if (tid < kDests) {
+            uint32_t acc = S.dcur[tid];
+#pragma unroll
+            for (int q = 0; q < NW; q++) { const uint32_t cc = S.wcnt[q][tid]; S.wpre[q][tid] = acc; acc += cc; S.wcnt[q][tid] = 0; }
+            S.dcur[tid] = acc;
         }
         // cell.rs:70-94 replayed in key order: per round, the earliest pending
         // arrival of every slot (min thread index = min key) is applied.
-        {
-            const uint32_t np = (uint32_t)__popcll(__ballot(pending));
-            if ((tid & 63) == 0 && np) atomicAdd(&S.npend, np);
-        }
-        if (pending) {
-            hc = claim_insert<CLAIM>(S.claim, local, tid);
-            if (hc < 0) { err |= ERR_CLAIM; pending = false; atomicSub(&S.npend, 1u); }
-        }
         int32_t em = -1;
-        lds_barrier();
+        bool first = true;
         for (;;) {
-            if (pending && (uint32_t)S.claim[hc] == tid) {
+            bool won = false;
+            if (pending && (claim[hc] & kClaimDone) == tid) {
                 const unsigned long long occ = S.tab[e];
                 const unsigned long long mine = ((unsigned long long)f2u(d2) << 32) | j;
                 if (occ == kEmpty64) {
@@ -660,75 +843,84 @@ __global__ __launch_bounds__(SlabLds<DENSE>::BS) void k_slab(SlabParams P) {
                     em = (int32_t)j;               // the arrival itself overflows
                 }
                 pending = false;
-                S.claim[hc] = ((unsigned long long)local << 32) | 0xFFFFFFFFull;
-                atomicSub(&S.npend, 1u);
+                won = true;
+                claim[hc] = (local << 11) | kClaimDone;
             }
+            {   // one LDS atomic per wave (same-address LDS atomics serialise per lane)
+                const uint64_t wm = __ballot(won);
+                if ((tid & 63) == 0 && wm) atomicSub(&S.npend[par], (uint32_t)__popcll(wm));
+            }
+            STAMP(4);
+            STAMP_COUNT(9, 1);
             lds_barrier();
-            if (S.npend == 0) break;
-            if (pending) atomicMin(&S.claim[hc], ((unsigned long long)local << 32) | tid);
+            STAMP(5);
+            if (first) {   // chunk i-1: stores into its child slabs (positions from phase B)
+                first = false;
+                const int dd = vd ? d : 0;
+                const uint32_t r = S.wpre[wv][dd] + rw;
+                const bool ok = vd && r < S.dcap[dd];
+                err |= (vd && !ok) ? (uint32_t)ERR_CAPACITY : 0u;
+                const uint32_t po = ok ? (S.doff[dd] + r) * 4 : 0xFFFFFFFFu;
+                bst(oX, po, __float_as_uint(ex)); bst(oY, po, __float_as_uint(ey)); bst(oZ, po, __float_as_uint(ez));
+                bst(oC, po, ec); bst(oK, po, prv.k); bst(oE, po, prv.e);
+                STAMP(6);
+            }
+            if (S.npend[par] == 0) break;
+            if (pending) atomicMin(&claim[hc], (local << 11) | tid);
+            STAMP(4);
             lds_barrier();
+            STAMP(5);
         }
-        if (valid && hc >= 0 && e >= 0 && local != 0xFFFFFFFFu && (err & (ERR_LAYER | ERR_SLOT_RANGE)) == 0)
-            S.claim[hc] = kEmpty64;   // all rounds done: clear for the next chunk
-        // emission: point (self or displaced), key/eb of this arrival, routed to its child slab
-        int d = -1, d2i = -1;
-        float ex = x, ey = y, ez = z;
-        uint32_t ec = c;
-        if (em >= 0) {
-            if ((uint32_t)em != j) {
-                ex = P.in.x[off + em]; ey = P.in.y[off + em]; ez = P.in.z[off + em]; ec = P.in.c[off + em];
-            }
-            int32_t ix, iy, iz, u;
-            d = route(P.cs_child, P.cr_child, cx, cy, cz, t, ex, ey, ez, ix, iy, iz, u, err);
-            if (d >= 0) {
-                int32_t jx, jy, jz, v;
-                uint32_t gerr = 0;
-                d2i = route(P.cs_gchild, P.cr_gchild, ix, iy, iz, u, ex, ey, ez, jx, jy, jz, v, gerr);
-                if (P.check_gchild) err |= gerr;
-            }
-        }
-        const bool vd = d >= 0;
-        uint64_t same = __ballot(vd);
-#pragma unroll
-        for (int b = 0; b < 5; b++) {
-            const uint64_t bb = __ballot(vd && ((d >> b) & 1));
-            same &= ((d >> b) & 1) ? bb : ~bb;
-        }
-        const uint32_t rw = __popcll(same & lt);
-        if (vd && rw == 0) S.wcnt[wv][d] = (uint32_t)__popcll(same);
-        lds_barrier();
-        if (tid < kDests) {
-            uint32_t acc = S.dcur[tid];
-#pragma unroll
-            for (int q = 0; q < NW; q++) { const uint32_t cc = S.wcnt[q][tid]; S.wpre[q][tid] = acc; acc += cc; S.wcnt[q][tid] = 0; }
-            S.dcur[tid] = acc;
-        }
-        lds_barrier();
-        if (vd) {
-            const uint32_t r = S.wpre[wv][d] + rw;
-            if (r < S.dcap[d]) {
-                const uint32_t pos = S.doff[d] + r;
-                P.nx.x[pos] = ex; P.nx.y[pos] = ey; P.nx.z[pos] = ez;
-                P.nx.c[pos] = ec; P.nx.k[pos] = k; P.nx.e[pos] = eb;
-            } else {
-                err |= ERR_CAPACITY;
-            }
-            if (d2i >= 0) atomicAdd(&S.gcnt[d * kDests + d2i], 1u);
-        }
+        if (hc >= 0) claim[hc] = kEmpty32;   // this buffer is next used two chunks later
+        if (P.ablate & 1) em = -1;
+        if (P.ablate & 4) em = em >= 0 ? (int32_t)j : em;
+        // chunk i -> stage `cur`; its occupant loads are consumed one step later
+        cur.em = em; cur.j = j; cur.k = k; cur.e = eb; cur.c = c; cur.x = x; cur.y = y; cur.z = z;
+        const uint32_t so = ((em >= 0 && (uint32_t)em != j) ? (uint32_t)em : min(j, nm1)) * 4;
+        cur.ox = __uint_as_float(bld(rX, so)); cur.oy = __uint_as_float(bld(rY, so));
+        cur.oz = __uint_as_float(bld(rZ, so)); cur.oc = bld(rC, so);
+        STAMP(7);
+        STAMP_COUNT(10, 1);
+    };
+    // nchunks + 1 steps (the last one only emits), rounded up to an even count
+    for (uint32_t ci = 0; ci <= nchunks; ci += 2) {
+        step(ci, A, B);
+        step(ci + 1, B, A);
     }
     __syncthreads();
     // winners -> this slab's grid region (capacity n; order inside a cell is free:
-    // cell.rs:158-160 HashMap order)
-    const uint32_t gbase = P.grid_off[s];
-    for (int i = tid; i < TAB; i += BS) {
-        const unsigned long long en = S.tab[i];
-        if (en != kEmpty64) {
-            const uint32_t j = (uint32_t)en;
-            const uint32_t r = atomicAdd(&S.nwin, 1u);
-            const float4 v = make_float4(P.in.x[off + j], P.in.y[off + j], P.in.z[off + j], __uint_as_float(P.in.c[off + j]));
-            reinterpret_cast<float4*>(P.grid)[gbase + r] = v;
-        }
+    // cell.rs:158-160 HashMap order).  All gathers of a thread are issued before
+    // any store so their latencies overlap.
+    constexpr int WPT = (TAB + BS - 1) / BS;
+    const __amdgpu_buffer_rsrc_t rG = srd(P.grid + P.grid_off[s], (uint64_t)n * 16);
+    uint32_t wj[WPT], wpos[WPT];
+#pragma unroll
+    for (int r = 0; r < WPT; r++) {
+        const int i = r * BS + (int)tid;
+        const unsigned long long en = i < TAB ? S.tab[i] : kEmpty64;
+        const bool occ = en != kEmpty64;
+        wj[r] = occ ? (uint32_t)en : 0u;
+        const uint64_t m = __ballot(occ);
+        uint32_t wb = 0;
+        if ((tid & 63) == 0 && m) wb = atomicAdd(&S.nwin, (uint32_t)__popcll(m));
+        wb = __shfl(wb, 0, 64);
+        wpos[r] = occ ? (wb + (uint32_t)__popcll(m & lt)) * 16 : 0xFFFFFFFFu;
     }
+    uint32_t wx[WPT], wy[WPT], wz[WPT], wc[WPT];
+#pragma unroll
+    for (int r = 0; r < WPT; r++) {
+        const uint32_t jo2 = min(wj[r], nm1) * 4;
+        wx[r] = bld(rX, jo2); wy[r] = bld(rY, jo2); wz[r] = bld(rZ, jo2); wc[r] = bld(rC, jo2);
+    }
+#pragma unroll
+    for (int r = 0; r < WPT; r++) {
+        __builtin_amdgcn_raw_buffer_store_b32(wx[r], rG, wpos[r], 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(wy[r], rG, wpos[r] == 0xFFFFFFFFu ? wpos[r] : wpos[r] + 4, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(wz[r], rG, wpos[r] == 0xFFFFFFFFu ? wpos[r] : wpos[r] + 8, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(wc[r], rG, wpos[r] == 0xFFFFFFFFu ? wpos[r] : wpos[r] + 12, 0, 0);
+    }
+    STAMP(8);
+    STAMP_FLUSH(P.stamps);
     if (err) atomicOr(&S.err, err);
     __syncthreads();
     if (tid == 0) {
@@ -996,6 +1188,9 @@ __global__ __launch_bounds__(256) void k_l0_lists(const uint32_t* slab_n, uint32
     const bool v = s < nslabs;
     const bool isbig = v && slab_n[s] >= kSmallMax;
     if (v) { if (isbig) rb = atomicAdd(&nb, 1u); else rs = atomicAdd(&ns, 1u); }
+    uint32_t mx = v ? slab_n[s] : 0;
+    for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o, 64));
+    if ((threadIdx.x & 63) == 0 && mx) atomicMax(&ctr->max_slab, mx);
     __syncthreads();
     if (threadIdx.x == 0) { bb = nb ? atomicAdd(&ctr->nbig, nb) : 0; bs = ns ? atomicAdd(&ctr->nsmall, ns) : 0; }
     __syncthreads();
@@ -1233,7 +1428,7 @@ static void l0_pass(int p, int passes, const Point* in, Arena src, Arena dst, ui
                     uint32_t* counts, uint32_t ntiles, uint32_t* hist, uint32_t D, Counters* ctr, const uint32_t* files,
                     uint32_t nfiles, ScanTemp& scan, hipStream_t st) {
     const uint64_t nc = (uint64_t)ntiles << BITS;
-    if (p == 0) k_l0_up0<BITS><<<ntiles, kL0BS, 0, st>>>(in, n, P, shift, counts, ntiles, hist, D, ctr);
+    if (p == 0) k_l0_up0<BITS><<<std::min<uint32_t>(ntiles, 2048), kL0BS, 0, st>>>(in, n, P, shift, counts, ntiles, hist, D, ctr);
     else k_l0_up<BITS><<<ntiles, kL0BS, 0, st>>>(src, n, P, shift, counts, ntiles);
     scan_excl_u32(counts, counts, (uint32_t)nc, nullptr, scan, st);
     const bool fin = p == passes - 1;
@@ -1330,7 +1525,14 @@ int Engine::level0_bin() {
         L->slab_cell, L->slab_layer, L->slab_off, L->slab_n);
     k_set_u32<<<1, 1, 0, stream_>>>(L->cell_slab0 + L->ncells, L->nslabs);
     k_l0_lists<<<grid_for(L->nslabs, 256, 1u << 30), 256, 0, stream_>>>(L->slab_n, L->nslabs, L->big_list, L->small_list, dev_->ctr);
-    k_l0_dcap<<<L->nslabs, 256, 0, stream_>>>(A0, P, L->cell_idx, L->slab_cell, L->slab_layer, L->slab_off, L->slab_n, L->dcap, dev_->ctr);
+    {
+        HIP_CHECK(hipMemcpyAsync(&hc, dev_->ctr, sizeof hc, hipMemcpyDeviceToHost, stream_));
+        HIP_CHECK(hipStreamSynchronize(stream_));
+        const uint32_t maxn = hc.max_slab;   // largest level-0 slab bounds the chunk grid
+        HIP_CHECK(hipMemsetAsync(L->dcap, 0, (uint64_t)L->nslabs * kDests * 4, stream_));
+        dim3 gd(L->nslabs, (maxn + kDcapChunk - 1) / kDcapChunk);
+        k_l0_dcap<<<gd, 256, 0, stream_>>>(A0, P, L->cell_idx, L->slab_cell, L->slab_layer, L->slab_off, L->slab_n, L->dcap, dev_->ctr);
+    }
     HIP_CHECK(hipGetLastError());
     ev_end(ST_L0);
     HIP_CHECK(hipMemcpyAsync(&hc, dev_->ctr, sizeof hc, hipMemcpyDeviceToHost, stream_));
@@ -1398,22 +1600,44 @@ int Engine::run_level(uint32_t h) {
     SP.gcap = L->gcap;
     SP.ctr = dev_->ctr;
     SP.cs = cs;
-    SP.cr = hex_radius(sub_cell_size(cs, dim));
-    SP.cs_child = csc;
-    SP.cr_child = hex_radius(sub_cell_size(csc, dim));
-    SP.cs_gchild = csg;
-    SP.cr_gchild = hex_radius(sub_cell_size(csg, dim));
+    {
+        LevelGeo& G = SP.G;
+        G.cr = hex_radius(sub_cell_size(cs, dim));
+        G.crx = G.cr * kSqrt3;
+        G.cry = (-G.cr) * kSqrt3;
+        G.inv_cr = 1.0f / G.cr;
+        G.csc = csc;
+        G.inv_csc = 1.0f / csc;
+        G.crc = hex_radius(sub_cell_size(csc, dim));
+        G.inv_crc = 1.0f / G.crc;
+        G.csg = csg;
+        G.inv_csg = 1.0f / csg;
+        G.crg = hex_radius(sub_cell_size(csg, dim));
+        G.inv_crg = 1.0f / G.crg;
+    }
     SP.tx = g.tx;
     SP.ty = g.ty;
     SP.check_gchild = (h + 2 < kMaxDepth) ? 1 : 0;
+    SP.ablate = getenv("PCC_ABLATE") ? atoi(getenv("PCC_ABLATE")) : 0;
+    SP.stamps = nullptr;
+#ifdef PCC_STAMPS
+    unsigned long long* stamps = static_cast<unsigned long long*>(dev_->get(2 * 12 * 8));
+    HIP_CHECK(hipMemsetAsync(stamps, 0, 2 * 12 * 8, stream_));
+#endif
     if (L->nbig) {
         SP.list = L->big_list;
+#ifdef PCC_STAMPS
+        SP.stamps = stamps;
+#endif
         ev_begin(ST_DENSE);
         k_slab<true><<<L->nbig, kDenseBS, 0, stream_>>>(SP);
         ev_end(ST_DENSE);
     }
     if (L->nsmall) {
         SP.list = L->small_list;
+#ifdef PCC_STAMPS
+        SP.stamps = stamps + 12;
+#endif
         ev_begin(ST_SMALL);
         k_slab<false><<<L->nsmall, kSmallBS, 0, stream_>>>(SP);
         ev_end(ST_SMALL);
@@ -1446,6 +1670,20 @@ int Engine::run_level(uint32_t h) {
     scan_excl_u32(flag, flag, nb, tots + 0, dev_->scan, stream_);
     scan_excl_u32(ndv, ndv, nb, tots + 1, dev_->scan, stream_);
     ev_end(ST_NEXT);
+#ifdef PCC_STAMPS
+    {
+        unsigned long long hs[24];
+        HIP_CHECK(hipMemcpy(hs, stamps, sizeof hs, hipMemcpyDeviceToHost));
+        const char* nm[12] = {"prologue", "slotA", "routeA", "B0wait", "rounds", "rndwait", "stores", "occload",
+                              "winners", "#rounds", "#steps", "-"};
+        for (int v = 0; v < 2; v++) {
+            if (!hs[12 * v + 10]) continue;
+            fprintf(stderr, "[stamps] level %u %s waves*steps=%llu  cycles/step:", h, v ? "small" : "dense", hs[12 * v + 10]);
+            for (int q = 0; q < 9; q++) fprintf(stderr, " %s=%.0f", nm[q], (double)hs[12 * v + q] / hs[12 * v + 10]);
+            fprintf(stderr, " rounds/step=%.2f\n", (double)hs[12 * v + 9] / hs[12 * v + 10]);
+        }
+    }
+#endif
     uint32_t ht[2];
     Counters hc;
     HIP_CHECK(hipMemcpyAsync(ht, tots, 8, hipMemcpyDeviceToHost, stream_));

@@ -20,12 +20,13 @@ constexpr float kSqrt3 = 1.73205080757f;  // hex.rs:3
 
 struct I3 { int32_t x, y, z; };
 
-// Rust `f32 as i32`: saturating, NaN -> 0.
+// Rust `f32 as i32`: saturating, NaN -> 0.  Branch-free (selects only) so it
+// does not split wavefront control flow on the GPU.
 PCC_HD int32_t sat_i32(float v) {
-    if (v != v) return 0;
-    if (v >= 2147483648.0f) return INT32_MAX;
-    if (v <= -2147483648.0f) return INT32_MIN;
-    return (int32_t)v;
+    const float c = fminf(fmaxf(v, -2147483648.0f), 2147483520.0f);  // 2147483520 = largest f32 < 2^31
+    int32_t r = (int32_t)c;
+    r = (v >= 2147483648.0f) ? INT32_MAX : r;
+    return (v != v) ? 0 : r;
 }
 
 // metadata.rs:91-93  max_cell_size / 2u32.pow(h) as f32

@@ -21,7 +21,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "..", "build", "libpcconv.so")
+LIB_PATH = os.environ.get("PCC_LIB") or os.path.join(HERE, "..", "build", "libpcconv.so")
 
 POINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("z", "<f4"), ("rgba", "u1", (4,))])  # point.rs:8-14
 
