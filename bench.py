@@ -55,26 +55,103 @@ def cpu_baseline(args):
                       f"(oracle/pcc_oracle.c, in-memory cells, 10 000-point batches), {dt:.1f} s"}
 
 
+METRIC = "points/sec converted (octree+LOD build), 1B synthetic pts, 1/2/4/8 MI355X"
+
+
+def record(args, n_gpus, ms, st_levels, st_cells, st_slabs, arrivals, k, dense_ms, parallelism):
+    """The one JSON line (rank 0).  roofline: dense slab kernel k_slab<true>,
+    algorithmic bytes = 32 B per arrival it processed over its
+    HIP-event time on the engine stream (rank 0's engine when N > 1)."""
+    dense_arr = k["dense_arrivals"]
+    achieved = 32.0 * dense_arr / (dense_ms / 1e3) / 1e9 if dense_ms > 0 else 0.0
+    whole = 32.0 * arrivals / (ms / 1e3) / 1e9
+    return {
+        "metric": METRIC,
+        "value": args.points / (ms / 1e3),
+        "unit": "points/s",
+        "n_gpus": n_gpus,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (counter-hash generator in HBM, SURVEY.md §8d)",
+        "config": {"workload": ("config4: %d uniform points in [-1000,1000)^3, seed %d" if args.kind == 0 else
+                                "config3-shape: %d clustered points, seed %d") % (args.points, args.seed),
+                   "batch": 10000, "levels": st_levels, "cells": st_cells, "slabs": st_slabs,
+                   "arrivals_W": arrivals, "parallelism": parallelism},
+        "roofline": {"bound": "hbm", "kernel": "k_slab<dense>", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "alg_bytes_per_arrival": 32, "kernel_ms_per_step": dense_ms,
+                     "whole_build_alg_GBs": whole, "whole_build_frac": whole / HBM_PEAK_GBS},
+        "stage_ms": k,
+    }
+
+
+def main_sharded(args, rank, world):
+    """N > 1: one rank per GPU (torchrun), level-0 cells sharded, RCCL exchange."""
+    import torch
+    import torch.distributed as dist
+    from pcconv.dist import HipShardOps, TorchComm, key_range, shard_build
+    import pcconv
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", device_id=dev)
+    comm = TorchComm(dev)
+    a, b = key_range(args.points, rank, world)
+    pts = torch.empty((b - a, 4), dtype=torch.int32, device=dev)
+    pcconv.synth_device(pts.data_ptr(), a, b - a, args.seed, args.kind, -1000.0, 2000.0, local)
+    torch.cuda.synchronize()
+    ops = HipShardOps(local, batch_size=10_000)
+    ops.conv.set_profiling(True)
+    files = [args.points]
+    for _ in range(args.warmup):
+        shard_build(comm, ops, pts, a, files)
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    prof = []
+    for _ in range(args.steps):
+        res = shard_build(comm, ops, pts, a, files)
+        prof.append(ops.conv.kernel_times())
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    ms = 1000.0 * float(el.item()) / args.steps
+    st = res.local
+    tot = torch.tensor([st["levels"], st["cells"], st["slabs"], st["arrivals"], res.recv_points], dtype=torch.int64,
+                       device=dev)
+    per = [torch.zeros_like(tot) for _ in range(world)]
+    dist.all_gather(per, tot)
+    stage = shard_build(comm, ops, pts, a, files, sync=torch.cuda.synchronize).ms   # untimed split
+    ops.close()
+    if rank == 0:
+        per = [p.tolist() for p in per]
+        k = prof[-1]
+        dense_ms = sum(p["dense_ms"] for p in prof) / len(prof)
+        rec = record(args, world, ms, max(p[0] for p in per), sum(p[1] for p in per), sum(p[2] for p in per),
+                     sum(p[3] for p in per), k, dense_ms, f"level-0 cell sharding over {world} ranks (RCCL all-to-all-v)")
+        rec["sharding"] = {"points_per_rank": [p[4] for p in per], "stage_ms_rank0": stage,
+                           "hierarchies": res.summary["hierarchies"]}
+        print(json.dumps(rec), flush=True)
+    dist.destroy_process_group()
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    if world != args.gpus:
-        args.gpus = world if world > 1 else args.gpus
-    import pcconv
     if world > 1:
-        import torch
-        import torch.distributed as dist
-        dist.init_process_group("nccl")
-        local = int(os.environ.get("LOCAL_RANK", "0"))
-        torch.cuda.set_device(local)
-        from pcconv.dist import run_sharded  # noqa: WPS433
-        res = run_sharded(args, rank, world, local)
-        if rank == 0:
-            print(json.dumps(res), flush=True)
-        dist.destroy_process_group()
+        args.gpus = world
+        main_sharded(args, rank, world)
         return
-
+    import pcconv
     import tempfile
     tmp = tempfile.mkdtemp(prefix="pcc_bench_")
     conv = pcconv.Converter(tmp, batch_size=10_000, device=0)
@@ -90,35 +167,9 @@ def main():
         prof.append(conv.kernel_times())
     conv.close()
     ms = 1000.0 * sum(times) / len(times)
-    # dominant kernel: the dense slab kernel; algorithmic bytes = 32 B per arrival it processed
-    k = prof[-1]
     dense_ms = sum(p["dense_ms"] for p in prof) / len(prof)
-    dense_arr = k["dense_arrivals"]
-    achieved = 32.0 * dense_arr / (dense_ms / 1e3) / 1e9 if dense_ms > 0 else 0.0
-    whole = 32.0 * st["arrivals"] / (ms / 1e3) / 1e9
-    res = {
-        "metric": "points/sec converted (octree+LOD build), 1B synthetic pts, 1/2/4/8 MI355X",
-        "value": args.points / (ms / 1e3),
-        "unit": "points/s",
-        "n_gpus": 1,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": ms,
-        "higher_is_better": True,
-        "scaling": "strong",
-        "vs_baseline": None,
-        "dtype": "f32",
-        "data": "synthetic (counter-hash generator in HBM, SURVEY.md §8d)",
-        "config": {"workload": ("config4: %d uniform points in [-1000,1000)^3, seed %d" if args.kind == 0 else
-                                "config3-shape: %d clustered points, seed %d") % (args.points, args.seed),
-                   "batch": 10000, "levels": st["levels"], "cells": st["cells"], "slabs": st["slabs"],
-                   "arrivals_W": st["arrivals"], "parallelism": "single GPU"},
-        "roofline": {"bound": "hbm", "kernel": "k_slab<dense>", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "alg_bytes_per_arrival": 32, "kernel_ms_per_step": dense_ms,
-                     "whole_build_alg_GBs": whole, "whole_build_frac": whole / HBM_PEAK_GBS},
-        "stage_ms": k,
-    }
+    res = record(args, 1, ms, st["levels"], st["cells"], st["slabs"], st["arrivals"], prof[-1], dense_ms,
+                 "single GPU")
     if args.cpu_sample > 0:
         res["cpu_baseline"] = cpu_baseline(args)
         res["speedup_vs_cpu"] = res["value"] / res["cpu_baseline"]["value"]

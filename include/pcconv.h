@@ -122,6 +122,61 @@ const pcc_point* pcc_device_input(const pcc_converter* c);
  * then finish.  Logs like the reference CLI. */
 int pcc_convert_files(const char* out_dir, const char* const* paths, size_t npaths, const pcc_options* opt);
 
+/* ---- Sharded multi-GPU build -------------------------------
+ * The reference converter is single-threaded (converter.rs:72-139) and has no
+ * multi-device notion; these entry points split ONE conversion across ranks by
+ * level-0 cell.  Every level-h cell has a unique level-0 ancestor
+ * (converter.rs:32-47 group_points at h+1 of a point of cell c lands in a child
+ * of c), so level-0 subtrees are independent and each rank builds the cells it
+ * owns, in global key order, with the global batch structure.  The collectives
+ * (bbox/histogram all-reduce, all-to-all-v of points) belong to the caller
+ * (pcconv/dist.py over RCCL).  All calls are synchronous. */
+typedef struct pcc_shard_grid {
+    int32_t lo[3];        /* level-0 cell index of the global bbox minimum (metadata.rs:100-102) */
+    uint32_t dims[3];     /* cells per axis spanned by the global bbox */
+    float cell_size;      /* metadata.rs:91-93 cell_size(0) */
+} pcc_shard_grid;
+
+/* Level-0 grid spanned by the global bounding box (host only, no device). */
+int pcc_shard_grid_from_bbox(const float gmin[3], const float gmax[3], float max_cell_size, pcc_shard_grid* out);
+
+/* Points first .. first+n-1 of the synthetic stream of pcc_add_synthetic,
+ * written to dst[0 .. n) in device memory (each rank generates its key range). */
+int pcc_synth_device(pcc_point* dst, uint64_t first, uint64_t n, uint64_t seed, int kind, float lo, float extent,
+                     int device);
+
+/* Local bounding box of n device points (bounding-volume/src/lib.rs:23-52). */
+int pcc_shard_bbox(const pcc_point* dev_pts, uint64_t n, float bmin[3], float bmax[3], int device);
+
+/* Points per level-0 cell of the grid (dev_hist: dims.x*dims.y*dims.z u32). */
+int pcc_shard_histogram(const pcc_point* dev_pts, uint64_t n, const pcc_shard_grid* g, uint32_t* dev_hist, int device);
+
+/* Stable partition of this rank's points by owner rank (owner = dev_owner[cell]):
+ * dev_send holds rank 0's points, then rank 1's, ... each in input order, and
+ * dev_keys the global key (key0 + local index) of each; counts[r] = points for
+ * rank r (host array of nranks, nranks <= 64). */
+int pcc_shard_route(const pcc_point* dev_pts, uint64_t n, uint32_t key0, const pcc_shard_grid* g,
+                    const uint32_t* dev_owner, uint32_t nranks, pcc_point* dev_send, uint32_t* dev_keys,
+                    uint64_t* counts, int device);
+
+/* Global file structure (points per input file, CLI order; lib.rs:31-52
+ * batching) without points.  Switches the converter to keyed input. */
+int pcc_declare_files(pcc_converter* c, const uint64_t* file_points, uint64_t nfiles);
+
+/* This rank's points (device memory) with their global keys, ascending. */
+int pcc_add_keyed_points_device(pcc_converter* c, const pcc_point* dev_pts, const uint32_t* dev_keys, uint64_t n);
+
+/* Global metadata values after the ranks' all-reduce (converter.rs:96-112,141-158). */
+int pcc_set_summary(pcc_converter* c, uint64_t number_of_points, const float bmin[3], const float bmax[3],
+                    uint32_t hierarchies);
+
+/* converter.rs:218-225 save_cache only (this rank's cells) / save_metadata only. */
+int pcc_write_cells(pcc_converter* c);
+int pcc_write_metadata(pcc_converter* c);
+
+/* Drop all added input (and build results) but keep device allocations. */
+int pcc_clear_input(pcc_converter* c);
+
 /* Thread-local message of the last failing call ("" if none). */
 const char* pcc_last_error(void);
 

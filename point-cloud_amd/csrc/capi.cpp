@@ -16,6 +16,7 @@
 #include "engine.h"
 #include "format.h"
 #include "hip_check.h"
+#include "pcc_math.h"
 
 using namespace pcc;
 
@@ -58,6 +59,8 @@ struct pcc_converter {
     Metadata meta;
     std::unique_ptr<Engine> eng;
     bool built = false;
+    bool keyed = false;         // pcc_declare_files: sharded input
+    bool summary_set = false;   // pcc_set_summary: global metadata values
     double build_ms = 0;
 };
 
@@ -121,6 +124,7 @@ int pcc_open(const char* out_dir, const pcc_options* opt, pcc_converter** out) {
 }
 
 int pcc_add_points(pcc_converter* c, const pcc_point* pts, uint64_t n) {
+    if (c && c->keyed) return set_err(-EINVAL, "converter takes keyed (sharded) input after pcc_declare_files");
     if (!c || (!pts && n)) return set_err(-EINVAL, "null argument");
     if (c->built) return set_err(-EINVAL, "points added after build");
     GUARD_BEGIN
@@ -130,6 +134,7 @@ int pcc_add_points(pcc_converter* c, const pcc_point* pts, uint64_t n) {
 }
 
 int pcc_add_points_device(pcc_converter* c, const pcc_point* pts, uint64_t n) {
+    if (c && c->keyed) return set_err(-EINVAL, "converter takes keyed (sharded) input after pcc_declare_files");
     if (!c || (!pts && n)) return set_err(-EINVAL, "null argument");
     if (c->built) return set_err(-EINVAL, "points added after build");
     GUARD_BEGIN
@@ -165,6 +170,7 @@ int pcc_build(pcc_converter* c) {
     c->build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     if (rc) return set_err(rc, c->eng->last_error());
     c->built = true;
+    if (c->summary_set) return 0;
     Metadata& m = c->meta;   // converter.rs:96-112 + 141-145
     m.number_of_points = c->eng->num_points();
     m.hierarchies = c->eng->hierarchies();
@@ -174,7 +180,7 @@ int pcc_build(pcc_converter* c) {
     GUARD_END
 }
 
-int pcc_write(pcc_converter* c) {
+static int write_impl(pcc_converter* c, bool with_metadata) {
     if (!c) return set_err(-EINVAL, "null argument");
     if (!c->built) {
         int rc = pcc_build(c);
@@ -186,8 +192,130 @@ int pcc_write(pcc_converter* c) {
     int rc = c->eng->download(levels, grid, kept);
     if (rc) return set_err(rc, c->eng->last_error());
     std::string err;
-    rc = write_output(c->out_dir, c->meta, levels, grid, kept, err);
+    rc = write_output(c->out_dir, c->meta, levels, grid, kept, err, with_metadata);
     if (rc) return set_err(rc, err);
+    return 0;
+    GUARD_END
+}
+
+int pcc_write(pcc_converter* c) { return write_impl(c, true); }
+int pcc_write_cells(pcc_converter* c) { return write_impl(c, false); }
+
+int pcc_write_metadata(pcc_converter* c) {
+    if (!c) return set_err(-EINVAL, "null argument");
+    if (!c->built && !c->summary_set) return set_err(-EINVAL, "nothing built and no summary set");
+    std::string err;
+    if (!mkdirs(c->out_dir)) return set_err(-EIO, "cannot create output directory " + c->out_dir);
+    for (uint32_t h = 0; h < c->meta.hierarchies; h++)   // converter.rs:141-158 (folders exist on every rank's disk view)
+        if (!mkdirs(c->out_dir + "/h_" + std::to_string(h))) return set_err(-EIO, "cannot create hierarchy folder");
+    const int rc = write_metadata(c->out_dir, c->meta, err);
+    return rc ? set_err(rc, err) : 0;
+}
+
+int pcc_shard_grid_from_bbox(const float gmin[3], const float gmax[3], float max_cell_size, pcc_shard_grid* out) {
+    if (!gmin || !gmax || !out) return set_err(-EINVAL, "null argument");
+    const float cs = cell_size(max_cell_size, 0);
+    uint64_t nc = 1;
+    for (int a = 0; a < 3; a++) {
+        if (!(gmin[a] <= gmax[a])) return set_err(-EINVAL, "empty or non-finite bounding box");
+        out->lo[a] = cell_index1(gmin[a], cs);
+        const int64_t d = (int64_t)cell_index1(gmax[a], cs) - out->lo[a] + 1;
+        out->dims[a] = (uint32_t)d;
+        nc *= (uint64_t)d;
+    }
+    out->cell_size = cs;
+    if (nc > (1ull << 22)) return set_err(-EFBIG, "level-0 grid of the bounding box exceeds 2^22 cells");
+    return 0;
+}
+
+static ShardGrid to_grid(const pcc_shard_grid* g) {
+    ShardGrid s;
+    for (int a = 0; a < 3; a++) { s.lo[a] = g->lo[a]; s.dims[a] = g->dims[a]; }
+    s.cs = g->cell_size;
+    return s;
+}
+
+int pcc_synth_device(pcc_point* dst, uint64_t first, uint64_t n, uint64_t seed, int kind, float lo, float extent,
+                     int device) {
+    if (!dst && n) return set_err(-EINVAL, "null argument");
+    if (kind != 0 && kind != 1) return set_err(-EINVAL, "kind must be 0 (uniform) or 1 (clustered)");
+    GUARD_BEGIN
+    return shard_synth(reinterpret_cast<Point*>(dst), first, n, seed, kind, lo, extent, device);
+    GUARD_END
+}
+
+int pcc_shard_bbox(const pcc_point* d, uint64_t n, float bmin[3], float bmax[3], int device) {
+    if ((!d && n) || !bmin || !bmax) return set_err(-EINVAL, "null argument");
+    GUARD_BEGIN
+    const int rc = shard_bbox(reinterpret_cast<const Point*>(d), n, bmin, bmax, device);
+    return rc ? set_err(rc, "input contains NaN or infinite coordinates (unsupported)") : 0;
+    GUARD_END
+}
+
+int pcc_shard_histogram(const pcc_point* d, uint64_t n, const pcc_shard_grid* g, uint32_t* dhist, int device) {
+    if ((!d && n) || !g || !dhist) return set_err(-EINVAL, "null argument");
+    GUARD_BEGIN
+    const int rc = shard_histogram(reinterpret_cast<const Point*>(d), n, to_grid(g), dhist, device);
+    return rc ? set_err(rc, "point outside the shard grid (grid not spanned by the global bbox?)") : 0;
+    GUARD_END
+}
+
+int pcc_shard_route(const pcc_point* d, uint64_t n, uint32_t key0, const pcc_shard_grid* g, const uint32_t* downer,
+                    uint32_t nranks, pcc_point* dsend, uint32_t* dkeys, uint64_t* counts, int device) {
+    if ((!d || !dsend || !dkeys) && n) return set_err(-EINVAL, "null argument");
+    if (!g || !downer || !counts) return set_err(-EINVAL, "null argument");
+    if ((uint64_t)key0 + n > (1ull << 32)) return set_err(-EOVERFLOW, "global keys must fit in 32 bits");
+    GUARD_BEGIN
+    const int rc = shard_route(reinterpret_cast<const Point*>(d), n, key0, to_grid(g), downer, nranks,
+                               reinterpret_cast<Point*>(dsend), dkeys, counts, device);
+    return rc ? set_err(rc, "routing failed (nranks > 64, point outside grid, or owner >= nranks)") : 0;
+    GUARD_END
+}
+
+int pcc_declare_files(pcc_converter* c, const uint64_t* file_points, uint64_t nfiles) {
+    if (!c || (!file_points && nfiles)) return set_err(-EINVAL, "null argument");
+    if (c->built) return set_err(-EINVAL, "files declared after build");
+    uint64_t tot = 0;
+    for (uint64_t f = 0; f < nfiles; f++) tot += file_points[f];
+    if (tot > (1ull << 32)) return set_err(-EOVERFLOW, "global keys must fit in 32 bits");
+    GUARD_BEGIN
+    c->eng->declare_files(file_points, nfiles, c->opt.batch_size);
+    c->keyed = true;
+    return 0;
+    GUARD_END
+}
+
+int pcc_add_keyed_points_device(pcc_converter* c, const pcc_point* d, const uint32_t* keys, uint64_t n) {
+    if (!c || ((!d || !keys) && n)) return set_err(-EINVAL, "null argument");
+    if (!c->keyed) return set_err(-EINVAL, "pcc_declare_files must come first");
+    if (c->built) return set_err(-EINVAL, "points added after build");
+    GUARD_BEGIN
+    c->eng->add_keyed_device(reinterpret_cast<const Point*>(d), keys, n);
+    return 0;
+    GUARD_END
+}
+
+int pcc_set_summary(pcc_converter* c, uint64_t number_of_points, const float bmin[3], const float bmax[3],
+                    uint32_t hierarchies) {
+    if (!c || !bmin || !bmax) return set_err(-EINVAL, "null argument");
+    Metadata& m = c->meta;
+    m.number_of_points = number_of_points;
+    m.hierarchies = hierarchies;
+    for (int a = 0; a < 3; a++) {
+        m.bmin[a] = number_of_points ? bmin[a] : 0.0f;
+        m.bmax[a] = number_of_points ? bmax[a] : 0.0f;
+    }
+    c->summary_set = true;
+    return 0;
+}
+
+int pcc_clear_input(pcc_converter* c) {
+    if (!c) return set_err(-EINVAL, "null argument");
+    GUARD_BEGIN
+    c->eng->clear_input();
+    c->built = false;
+    c->keyed = false;
+    c->summary_set = false;
     return 0;
     GUARD_END
 }

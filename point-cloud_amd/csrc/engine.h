@@ -69,6 +69,15 @@ public:
     // Synthetic input generated straight into HBM (bench / tests).
     void add_file_synth(uint64_t seed, int kind, uint64_t n, uint32_t batch, float lo, float ext);
 
+    // Sharded build.  declare_files() fixes the GLOBAL file/batch
+    // structure (points per file, in CLI order) without adding points; then
+    // add_keyed_device() appends this shard's points with their global input
+    // indices (keys, ascending).  Event batches come from the global table.
+    void declare_files(const uint64_t* file_points, uint64_t nfiles, uint32_t batch);
+    void add_keyed_device(const Point* dpts, const uint32_t* dkeys, uint64_t n);
+    // Drops all input (points, keys, files) but keeps device allocations.
+    void clear_input();
+
     // Run the whole build on the device.  Returns 0 or a negative error code
     // (message in last_error()).  Input must already be resident.
     int build();
@@ -109,6 +118,9 @@ private:
     std::vector<uint32_t> file_eb0_;     // first batch index per file
     std::vector<uint32_t> file_batch_;   // batch size per file
     Point* d_in_ = nullptr;
+    uint32_t* d_keys_ = nullptr;         // keyed (sharded) input: global key per point
+    uint64_t keys_cap_ = 0;
+    bool keyed_ = false;
     Dev* dev_ = nullptr;
     std::vector<Level*> levels_;
     float bmin_[3] = {0, 0, 0}, bmax_[3] = {0, 0, 0};
@@ -121,5 +133,18 @@ private:
     std::string err_;
     bool built_ = false;
 };
+
+// ---- sharded build helpers; synchronous, on an internal stream
+// of `device`.  Cell id = ((ix-lo.x)*dims.y + (iy-lo.y))*dims.z + (iz-lo.z).
+struct ShardGrid {
+    int32_t lo[3];
+    uint32_t dims[3];
+    float cs;          // level-0 cell size
+};
+int shard_synth(Point* dst, uint64_t idx0, uint64_t n, uint64_t seed, int kind, float lo, float ext, int device);
+int shard_bbox(const Point* d, uint64_t n, float bmin[3], float bmax[3], int device);
+int shard_histogram(const Point* d, uint64_t n, const ShardGrid& g, uint32_t* dhist, int device);
+int shard_route(const Point* d, uint64_t n, uint32_t key0, const ShardGrid& g, const uint32_t* downer, uint32_t nranks,
+                Point* dsend, uint32_t* dkeys, uint64_t* counts, int device);
 
 }  // namespace pcc

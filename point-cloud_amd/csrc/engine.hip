@@ -30,6 +30,8 @@
 //   * keys (input indices) are unique at every level; event batches are
 //     monotone in key inside every cell.
 #include "engine.h"
+#include <cerrno>
+#include <memory>
 
 #include <algorithm>
 #include <chrono>
@@ -292,6 +294,16 @@ __global__ void k_synth(Point* out, uint64_t first, uint64_t n, uint64_t seed, i
     }
 }
 
+// stream points idx0 .. idx0+n of a synthetic file into out[0 .. n)
+__global__ void k_synth_at(Point* out, uint64_t idx0, uint64_t n, uint64_t seed, int kind, float lo, float ext) {
+    for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < n; j += (uint64_t)gridDim.x * blockDim.x) {
+        float x, y, z;
+        uint32_t c;
+        synth_point(seed, kind, idx0 + j, lo, ext, x, y, z, c);
+        reinterpret_cast<float4*>(out)[j] = make_float4(x, y, z, __uint_as_float(c));
+    }
+}
+
 // bounding-volume/src/lib.rs:23-52 + converter.rs:96-104: the final AABB is the
 // componentwise min/max over all points (f32::min/max are exact).
 constexpr int kBBoxBS = 256, kBBoxBlocks = 2048;
@@ -423,7 +435,8 @@ __global__ __launch_bounds__(kL0BS) void k_l0_up(Arena A, uint64_t n, L0Params P
 // recomputed from the position.  SRC_AOS: read the 16-B input records (index =
 // position); FINAL: also write the event batch of every point.
 template <int BITS, bool SRC_AOS, bool FINAL>
-__global__ __launch_bounds__(kL0BS) void k_l0_down(const Point* __restrict__ in, Arena S, Arena O, uint64_t n,
+__global__ __launch_bounds__(kL0BS) void k_l0_down(const Point* __restrict__ in, const uint32_t* __restrict__ keys,
+                                                   Arena S, Arena O, uint64_t n,
                                                    L0Params P, int shift, const uint32_t* __restrict__ offs,
                                                    uint32_t ntiles, const uint32_t* files, uint32_t nfiles) {
     constexpr int R = 1 << BITS;
@@ -450,7 +463,8 @@ __global__ __launch_bounds__(kL0BS) void k_l0_down(const Point* __restrict__ in,
         if (i < n) {
             if constexpr (SRC_AOS) {
                 const float4 v = reinterpret_cast<const float4*>(in)[i];
-                x[r] = v.x; y[r] = v.y; z[r] = v.z; c[r] = __float_as_uint(v.w); k[r] = (uint32_t)i;
+                x[r] = v.x; y[r] = v.y; z[r] = v.z; c[r] = __float_as_uint(v.w);
+                k[r] = keys ? keys[i] : (uint32_t)i;   // sharded input carries global keys
             } else {
                 x[r] = S.x[i]; y[r] = S.y[i]; z[r] = S.z[i]; c[r] = S.c[i]; k[r] = S.k[i];
             }
@@ -1286,6 +1300,9 @@ void Engine::free_all() {
     }
     (void)hipFree(d_in_);
     d_in_ = nullptr;
+    (void)hipFree(d_keys_);
+    d_keys_ = nullptr;
+    keys_cap_ = 0;
 }
 
 int Engine::fail(int code, const std::string& msg) {
@@ -1340,6 +1357,48 @@ void Engine::add_file_synth(uint64_t seed, int kind, uint64_t n, uint32_t batch,
     file_batch_.push_back(std::max<uint32_t>(batch, 1));
     n_ += n;
     nbatches_ += batches_of(n, batch);
+}
+
+void Engine::declare_files(const uint64_t* file_points, uint64_t nfiles, uint32_t batch) {
+    uint64_t g = 0;
+    for (uint64_t f = 0; f < nfiles; f++) {
+        file_start_.push_back(g);
+        file_eb0_.push_back(nbatches_);
+        file_batch_.push_back(std::max<uint32_t>(batch, 1));
+        g += file_points[f];
+        nbatches_ += batches_of(file_points[f], batch);
+    }
+    keyed_ = true;
+}
+
+void Engine::add_keyed_device(const Point* dpts, const uint32_t* dkeys, uint64_t n) {
+    reserve(n_ + n);
+    if (keys_cap_ < n_ + n) {
+        uint32_t* k = nullptr;
+        HIP_CHECK(hipMalloc(&k, std::max<uint64_t>(cap_, 1) * 4));
+        if (n_) HIP_CHECK(hipMemcpyAsync(k, d_keys_, n_ * 4, hipMemcpyDeviceToDevice, stream_));
+        HIP_CHECK(hipStreamSynchronize(stream_));
+        (void)hipFree(d_keys_);
+        d_keys_ = k;
+        keys_cap_ = cap_;
+    }
+    if (n) {
+        HIP_CHECK(hipMemcpyAsync(d_in_ + n_, dpts, n * sizeof(Point), hipMemcpyDeviceToDevice, stream_));
+        HIP_CHECK(hipMemcpyAsync(d_keys_ + n_, dkeys, n * 4, hipMemcpyDeviceToDevice, stream_));
+    }
+    n_ += n;
+    keyed_ = true;
+}
+
+void Engine::clear_input() {
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    n_ = 0;
+    nbatches_ = 0;
+    file_start_.clear();
+    file_eb0_.clear();
+    file_batch_.clear();
+    keyed_ = false;
+    built_ = false;
 }
 
 int Engine::build() {
@@ -1424,7 +1483,7 @@ int Engine::build() {
 }
 
 template <int BITS>
-static void l0_pass(int p, int passes, const Point* in, Arena src, Arena dst, uint64_t n, const L0Params& P, int shift,
+static void l0_pass(int p, int passes, const Point* in, const uint32_t* keys, Arena src, Arena dst, uint64_t n, const L0Params& P, int shift,
                     uint32_t* counts, uint32_t ntiles, uint32_t* hist, uint32_t D, Counters* ctr, const uint32_t* files,
                     uint32_t nfiles, ScanTemp& scan, hipStream_t st) {
     const uint64_t nc = (uint64_t)ntiles << BITS;
@@ -1432,10 +1491,10 @@ static void l0_pass(int p, int passes, const Point* in, Arena src, Arena dst, ui
     else k_l0_up<BITS><<<ntiles, kL0BS, 0, st>>>(src, n, P, shift, counts, ntiles);
     scan_excl_u32(counts, counts, (uint32_t)nc, nullptr, scan, st);
     const bool fin = p == passes - 1;
-    if (p == 0 && fin) k_l0_down<BITS, true, true><<<ntiles, kL0BS, 0, st>>>(in, src, dst, n, P, shift, counts, ntiles, files, nfiles);
-    else if (p == 0) k_l0_down<BITS, true, false><<<ntiles, kL0BS, 0, st>>>(in, src, dst, n, P, shift, counts, ntiles, files, nfiles);
-    else if (fin) k_l0_down<BITS, false, true><<<ntiles, kL0BS, 0, st>>>(in, src, dst, n, P, shift, counts, ntiles, files, nfiles);
-    else k_l0_down<BITS, false, false><<<ntiles, kL0BS, 0, st>>>(in, src, dst, n, P, shift, counts, ntiles, files, nfiles);
+    if (p == 0 && fin) k_l0_down<BITS, true, true><<<ntiles, kL0BS, 0, st>>>(in, keys, src, dst, n, P, shift, counts, ntiles, files, nfiles);
+    else if (p == 0) k_l0_down<BITS, true, false><<<ntiles, kL0BS, 0, st>>>(in, keys, src, dst, n, P, shift, counts, ntiles, files, nfiles);
+    else if (fin) k_l0_down<BITS, false, true><<<ntiles, kL0BS, 0, st>>>(in, keys, src, dst, n, P, shift, counts, ntiles, files, nfiles);
+    else k_l0_down<BITS, false, false><<<ntiles, kL0BS, 0, st>>>(in, keys, src, dst, n, P, shift, counts, ntiles, files, nfiles);
     HIP_CHECK(hipGetLastError());
 }
 
@@ -1478,14 +1537,14 @@ int Engine::level0_bin() {
     Arena src = A1, dst = (passes % 2) ? A0 : A1;
     for (int p = 0, shift = 0; p < passes; p++, shift += per) {
         switch (per) {
-            case 1: l0_pass<1>(p, passes, d_in_, src, dst, n_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, (uint32_t)file_start_.size(), dev_->scan, stream_); break;
-            case 2: l0_pass<2>(p, passes, d_in_, src, dst, n_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, (uint32_t)file_start_.size(), dev_->scan, stream_); break;
-            case 3: l0_pass<3>(p, passes, d_in_, src, dst, n_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, (uint32_t)file_start_.size(), dev_->scan, stream_); break;
-            case 4: l0_pass<4>(p, passes, d_in_, src, dst, n_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, (uint32_t)file_start_.size(), dev_->scan, stream_); break;
-            case 5: l0_pass<5>(p, passes, d_in_, src, dst, n_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, (uint32_t)file_start_.size(), dev_->scan, stream_); break;
-            case 6: l0_pass<6>(p, passes, d_in_, src, dst, n_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, (uint32_t)file_start_.size(), dev_->scan, stream_); break;
-            case 7: l0_pass<7>(p, passes, d_in_, src, dst, n_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, (uint32_t)file_start_.size(), dev_->scan, stream_); break;
-            default: l0_pass<8>(p, passes, d_in_, src, dst, n_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, (uint32_t)file_start_.size(), dev_->scan, stream_); break;
+            case 1: l0_pass<1>(p, passes, d_in_, keyed_ ? d_keys_ : nullptr, src, dst, n_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, (uint32_t)file_start_.size(), dev_->scan, stream_); break;
+            case 2: l0_pass<2>(p, passes, d_in_, keyed_ ? d_keys_ : nullptr, src, dst, n_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, (uint32_t)file_start_.size(), dev_->scan, stream_); break;
+            case 3: l0_pass<3>(p, passes, d_in_, keyed_ ? d_keys_ : nullptr, src, dst, n_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, (uint32_t)file_start_.size(), dev_->scan, stream_); break;
+            case 4: l0_pass<4>(p, passes, d_in_, keyed_ ? d_keys_ : nullptr, src, dst, n_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, (uint32_t)file_start_.size(), dev_->scan, stream_); break;
+            case 5: l0_pass<5>(p, passes, d_in_, keyed_ ? d_keys_ : nullptr, src, dst, n_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, (uint32_t)file_start_.size(), dev_->scan, stream_); break;
+            case 6: l0_pass<6>(p, passes, d_in_, keyed_ ? d_keys_ : nullptr, src, dst, n_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, (uint32_t)file_start_.size(), dev_->scan, stream_); break;
+            case 7: l0_pass<7>(p, passes, d_in_, keyed_ ? d_keys_ : nullptr, src, dst, n_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, (uint32_t)file_start_.size(), dev_->scan, stream_); break;
+            default: l0_pass<8>(p, passes, d_in_, keyed_ ? d_keys_ : nullptr, src, dst, n_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, (uint32_t)file_start_.size(), dev_->scan, stream_); break;
         }
         src = dst;
         dst = (dst.x == A0.x) ? A1 : A0;
@@ -1789,6 +1848,178 @@ int Engine::download(std::vector<LevelHost>& out, std::vector<Point>& grid, std:
         out.push_back(std::move(H));
     }
     return 0;
+}
+
+}  // namespace pcc
+
+namespace pcc {
+// ------------------------------------------------------------------ sharding
+// Level-0 ownership for the multi-GPU build: every level-h cell has a unique
+// level-0 ancestor, so level-0 cells are the unit of ownership.  The grid is
+// spanned by the GLOBAL bounding box (all-reduced by the caller); a point's
+// linear cell id is ((ix - lo.x) * dims.y + (iy - lo.y)) * dims.z + (iz - lo.z).
+namespace {
+struct ShardScratch {
+    int device = -1;
+    hipStream_t st = nullptr;
+    uint32_t* buf[4] = {nullptr, nullptr, nullptr, nullptr};
+    uint64_t cap = 0;
+    float* part = nullptr;
+    uint32_t* flag = nullptr;
+    uint32_t* cnt = nullptr;
+    SortTemp sort;
+    ~ShardScratch() {
+        for (auto* b : buf) (void)hipFree(b);
+        (void)hipFree(part); (void)hipFree(flag); (void)hipFree(cnt);
+        (void)hipFree(sort.counts); (void)hipFree(sort.scan.bsums);
+        if (st) (void)hipStreamDestroy(st);
+    }
+};
+thread_local std::unique_ptr<ShardScratch> t_shard;
+
+ShardScratch& shard_scratch(int device) {
+    HIP_CHECK(hipSetDevice(device));
+    if (!t_shard || t_shard->device != device) {
+        t_shard = std::make_unique<ShardScratch>();
+        t_shard->device = device;
+        HIP_CHECK(hipStreamCreateWithFlags(&t_shard->st, hipStreamNonBlocking));
+        HIP_CHECK(hipMalloc(&t_shard->part, kBBoxBlocks * 6 * sizeof(float)));
+        HIP_CHECK(hipMalloc(&t_shard->flag, 4));
+        HIP_CHECK(hipMalloc(&t_shard->cnt, 64 * 4));
+    }
+    return *t_shard;
+}
+
+__device__ __forceinline__ uint32_t shard_cell(const ShardGrid& g, float x, float y, float z) {
+    const int32_t ix = cell_index1(x, g.cs) - g.lo[0], iy = cell_index1(y, g.cs) - g.lo[1], iz = cell_index1(z, g.cs) - g.lo[2];
+    const bool in = ix >= 0 && iy >= 0 && iz >= 0 && (uint32_t)ix < g.dims[0] && (uint32_t)iy < g.dims[1] && (uint32_t)iz < g.dims[2];
+    return in ? ((uint32_t)ix * g.dims[1] + (uint32_t)iy) * g.dims[2] + (uint32_t)iz : 0xFFFFFFFFu;
+}
+
+constexpr int kShBS = 256;
+// per-block LDS histogram (ncells <= kShLds), else global atomics
+constexpr uint32_t kShLds = 8192;
+__global__ __launch_bounds__(kShBS) void k_shard_hist(const Point* __restrict__ in, uint64_t n, ShardGrid g,
+                                                      uint32_t ncells, uint32_t* hist, uint32_t* bad) {
+    __shared__ uint32_t h[kShLds];
+    const bool lds = ncells <= kShLds;
+    if (lds)
+        for (uint32_t i = threadIdx.x; i < ncells; i += kShBS) h[i] = 0;
+    __syncthreads();
+    const float4* p4 = reinterpret_cast<const float4*>(in);
+    uint32_t nbad = 0;
+    for (uint64_t i = blockIdx.x * (uint64_t)kShBS + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kShBS) {
+        const float4 v = p4[i];
+        const uint32_t c = shard_cell(g, v.x, v.y, v.z);
+        if (c == 0xFFFFFFFFu) { nbad++; continue; }
+        if (lds) atomicAdd(&h[c], 1u); else atomicAdd(&hist[c], 1u);
+    }
+    if (nbad) atomicAdd(bad, nbad);
+    __syncthreads();
+    if (lds)
+        for (uint32_t i = threadIdx.x; i < ncells; i += kShBS)
+            if (h[i]) atomicAdd(&hist[i], h[i]);
+}
+
+// owner rank per point (sort key) and its local index (payload)
+__global__ __launch_bounds__(kShBS) void k_shard_owner(const Point* __restrict__ in, uint32_t n, ShardGrid g,
+                                                       const uint32_t* __restrict__ owner, uint32_t nranks,
+                                                       uint32_t* ow, uint32_t* idx, uint32_t* cnt, uint32_t* bad) {
+    __shared__ uint32_t c[64];
+    if (threadIdx.x < 64) c[threadIdx.x] = 0;
+    __syncthreads();
+    const float4* p4 = reinterpret_cast<const float4*>(in);
+    for (uint32_t i = blockIdx.x * kShBS + threadIdx.x; i < n; i += gridDim.x * kShBS) {
+        const float4 v = p4[i];
+        const uint32_t cl = shard_cell(g, v.x, v.y, v.z);
+        uint32_t r = cl == 0xFFFFFFFFu ? 0xFFFFFFFFu : owner[cl];
+        if (r >= nranks) { atomicOr(bad, 1u); r = 0; }
+        ow[i] = r;
+        idx[i] = i;
+        atomicAdd(&c[r], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < nranks && c[threadIdx.x]) atomicAdd(&cnt[threadIdx.x], c[threadIdx.x]);
+}
+
+__global__ __launch_bounds__(kShBS) void k_shard_gather(const Point* __restrict__ in, uint32_t n, const uint32_t* __restrict__ idx,
+                                                        uint32_t key0, Point* out, uint32_t* keys) {
+    for (uint32_t j = blockIdx.x * kShBS + threadIdx.x; j < n; j += gridDim.x * kShBS) {
+        const uint32_t i = idx[j];
+        reinterpret_cast<float4*>(out)[j] = reinterpret_cast<const float4*>(in)[i];
+        keys[j] = key0 + i;
+    }
+}
+}  // namespace
+
+int shard_synth(Point* dst, uint64_t idx0, uint64_t n, uint64_t seed, int kind, float lo, float ext, int device) {
+    ShardScratch& S = shard_scratch(device);
+    if (n) k_synth_at<<<grid_for(n, 256, 1 << 20), 256, 0, S.st>>>(dst, idx0, n, seed, kind, lo, ext);
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipStreamSynchronize(S.st));
+    return 0;
+}
+
+int shard_bbox(const Point* d, uint64_t n, float bmin[3], float bmax[3], int device) {
+    ShardScratch& S = shard_scratch(device);
+    for (int a = 0; a < 3; a++) { bmin[a] = INFINITY; bmax[a] = -INFINITY; }
+    if (!n) return 0;
+    HIP_CHECK(hipMemsetAsync(S.flag, 0, 4, S.st));
+    const unsigned nbb = grid_for(n, kBBoxBS, kBBoxBlocks);
+    k_bbox<<<nbb, kBBoxBS, 0, S.st>>>(d, n, S.part, S.flag);
+    k_bbox_final<<<1, 64, 0, S.st>>>(S.part, nbb);
+    HIP_CHECK(hipGetLastError());
+    float bb[6];
+    uint32_t bad = 0;
+    HIP_CHECK(hipMemcpyAsync(bb, S.part, sizeof bb, hipMemcpyDeviceToHost, S.st));
+    HIP_CHECK(hipMemcpyAsync(&bad, S.flag, 4, hipMemcpyDeviceToHost, S.st));
+    HIP_CHECK(hipStreamSynchronize(S.st));
+    if (bad) return -EINVAL;
+    for (int a = 0; a < 3; a++) { bmin[a] = bb[a]; bmax[a] = bb[3 + a]; }
+    return 0;
+}
+
+int shard_histogram(const Point* d, uint64_t n, const ShardGrid& g, uint32_t* dhist, int device) {
+    ShardScratch& S = shard_scratch(device);
+    const uint64_t nc = (uint64_t)g.dims[0] * g.dims[1] * g.dims[2];
+    HIP_CHECK(hipMemsetAsync(dhist, 0, nc * 4, S.st));
+    HIP_CHECK(hipMemsetAsync(S.flag, 0, 4, S.st));
+    if (n) k_shard_hist<<<grid_for(n, kShBS, 1024), kShBS, 0, S.st>>>(d, n, g, (uint32_t)nc, dhist, S.flag);
+    HIP_CHECK(hipGetLastError());
+    uint32_t bad = 0;
+    HIP_CHECK(hipMemcpyAsync(&bad, S.flag, 4, hipMemcpyDeviceToHost, S.st));
+    HIP_CHECK(hipStreamSynchronize(S.st));
+    return bad ? -ERANGE : 0;
+}
+
+int shard_route(const Point* d, uint64_t n, uint32_t key0, const ShardGrid& g, const uint32_t* downer, uint32_t nranks,
+                Point* dsend, uint32_t* dkeys, uint64_t* counts, int device) {
+    ShardScratch& S = shard_scratch(device);
+    if (nranks == 0 || nranks > 64) return -EINVAL;
+    if (n >= (1ull << 32)) return -EOVERFLOW;
+    if (S.cap < n) {
+        for (auto*& b : S.buf) { (void)hipFree(b); b = nullptr; HIP_CHECK(hipMalloc(&b, std::max<uint64_t>(n, 1) * 4)); }
+        S.cap = n;
+    }
+    HIP_CHECK(hipMemsetAsync(S.cnt, 0, 64 * 4, S.st));
+    HIP_CHECK(hipMemsetAsync(S.flag, 0, 4, S.st));
+    uint32_t hc[64] = {};
+    if (n) {
+        const uint32_t n32 = (uint32_t)n;
+        k_shard_owner<<<grid_for(n, kShBS, 4096), kShBS, 0, S.st>>>(d, n32, g, downer, nranks, S.buf[0], S.buf[1], S.cnt, S.flag);
+        int bits = 0;
+        while ((1u << bits) < nranks) bits++;
+        int which = 0;
+        if (bits) which = radix_sort_pairs(S.buf[0], S.buf[1], S.buf[2], S.buf[3], n32, bits, S.sort, S.st);
+        k_shard_gather<<<grid_for(n, kShBS, 8192), kShBS, 0, S.st>>>(d, n32, which ? S.buf[3] : S.buf[1], key0, dsend, dkeys);
+        HIP_CHECK(hipGetLastError());
+        HIP_CHECK(hipMemcpyAsync(hc, S.cnt, 64 * 4, hipMemcpyDeviceToHost, S.st));
+    }
+    uint32_t bad = 0;
+    HIP_CHECK(hipMemcpyAsync(&bad, S.flag, 4, hipMemcpyDeviceToHost, S.st));
+    HIP_CHECK(hipStreamSynchronize(S.st));
+    for (uint32_t r = 0; r < nranks; r++) counts[r] = hc[r];
+    return bad ? -ERANGE : 0;
 }
 
 }  // namespace pcc

@@ -188,7 +188,7 @@ static void put32(std::string& b, uint32_t v) { b.append(reinterpret_cast<const 
 static void putf(std::string& b, float v) { b.append(reinterpret_cast<const char*>(&v), 4); }
 
 int write_output(const std::string& dir, const Metadata& meta, const std::vector<LevelHost>& levels,
-                 const std::vector<Point>& grid, const std::vector<Point>& kept, std::string& err) {
+                 const std::vector<Point>& grid, const std::vector<Point>& kept, std::string& err, bool with_metadata) {
     if (mkdir(dir.c_str(), 0755) != 0 && errno != EEXIST) { err = "cannot create " + dir; return -errno; }
     for (uint32_t h = 0; h < meta.hierarchies; h++) {   // converter.rs:141-158
         std::string hd = dir + "/h_" + std::to_string(h);
@@ -247,6 +247,10 @@ int write_output(const std::string& dir, const Metadata& meta, const std::vector
             if (fclose(f) != 0 || !ok) { err = "write failed: " + path; return -EIO; }
         }
     }
+    return with_metadata ? write_metadata(dir, meta, err) : 0;
+}
+
+int write_metadata(const std::string& dir, const Metadata& meta, std::string& err) {
     const std::string mp = dir + "/metadata.json";
     FILE* f = fopen(mp.c_str(), "wb");
     if (!f) { err = "cannot write " + mp; return -errno; }

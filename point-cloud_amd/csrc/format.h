@@ -26,8 +26,12 @@ bool parse_metadata_json(const std::string& text, Metadata& m, std::string& err)
 
 // Writes h_{h}/c_{x}_{y}_{z}.bin for every cell of every level, then metadata.json
 // (converter.rs:218-238 order: cells first, metadata last).
+// with_metadata=false writes the cells only (sharded build: rank 0 writes the
+// global metadata.json once all ranks' cells are on disk).
 int write_output(const std::string& dir, const Metadata& meta, const std::vector<LevelHost>& levels,
-                 const std::vector<Point>& grid, const std::vector<Point>& kept, std::string& err);
+                 const std::vector<Point>& grid, const std::vector<Point>& kept, std::string& err,
+                 bool with_metadata = true);
+int write_metadata(const std::string& dir, const Metadata& meta, std::string& err);
 
 // PLY reader.  Returns points of the `vertex` element.  `ascii` is set when the
 // file is ASCII-encoded: the reference's ASCII branch parses but never stores

@@ -29,7 +29,9 @@ POINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("z", "<f4"), ("rgba", "u1",
 EXPORTS = ["pcc_abi_version", "pcc_last_error", "pcc_options_default", "pcc_open", "pcc_add_points",
            "pcc_add_points_device", "pcc_add_empty_batches", "pcc_add_synthetic", "pcc_build", "pcc_write",
            "pcc_finish", "pcc_close", "pcc_get_stats", "pcc_set_profiling", "pcc_get_profile", "pcc_device_input",
-           "pcc_convert_files"]
+           "pcc_convert_files", "pcc_shard_grid_from_bbox", "pcc_synth_device", "pcc_shard_bbox",
+           "pcc_shard_histogram", "pcc_shard_route", "pcc_declare_files", "pcc_add_keyed_points_device",
+           "pcc_set_summary", "pcc_write_cells", "pcc_write_metadata", "pcc_clear_input"]
 
 
 class Options(C.Structure):
@@ -54,6 +56,15 @@ class Profile(C.Structure):
     _fields_ = [("level0_ms", C.c_double), ("dense_ms", C.c_double), ("small_ms", C.c_double),
                 ("bucket_ms", C.c_double), ("next_ms", C.c_double), ("dense_arrivals", C.c_uint64),
                 ("small_arrivals", C.c_uint64), ("dense_launches", C.c_uint32), ("small_launches", C.c_uint32)]
+
+
+class ShardGrid(C.Structure):
+    """pcc_shard_grid: level-0 cell grid spanned by the global bounding box."""
+    _fields_ = [("lo", C.c_int32 * 3), ("dims", C.c_uint32 * 3), ("cell_size", C.c_float)]
+
+    @property
+    def ncells(self) -> int:
+        return int(self.dims[0]) * int(self.dims[1]) * int(self.dims[2])
 
 
 class PccError(RuntimeError):
@@ -92,6 +103,19 @@ def lib():
         L.pcc_device_input.argtypes = [vp]
         L.pcc_device_input.restype = vp
         L.pcc_convert_files.argtypes = [C.c_char_p, C.POINTER(C.c_char_p), C.c_size_t, C.POINTER(Options)]
+        f3 = C.POINTER(C.c_float)
+        L.pcc_shard_grid_from_bbox.argtypes = [f3, f3, C.c_float, C.POINTER(ShardGrid)]
+        L.pcc_synth_device.argtypes = [vp, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int, C.c_float, C.c_float, C.c_int]
+        L.pcc_shard_bbox.argtypes = [vp, C.c_uint64, f3, f3, C.c_int]
+        L.pcc_shard_histogram.argtypes = [vp, C.c_uint64, C.POINTER(ShardGrid), vp, C.c_int]
+        L.pcc_shard_route.argtypes = [vp, C.c_uint64, C.c_uint32, C.POINTER(ShardGrid), vp, C.c_uint32, vp, vp,
+                                      C.POINTER(C.c_uint64), C.c_int]
+        L.pcc_declare_files.argtypes = [vp, C.POINTER(C.c_uint64), C.c_uint64]
+        L.pcc_add_keyed_points_device.argtypes = [vp, vp, vp, C.c_uint64]
+        L.pcc_set_summary.argtypes = [vp, C.c_uint64, f3, f3, C.c_uint32]
+        L.pcc_write_cells.argtypes = [vp]
+        L.pcc_write_metadata.argtypes = [vp]
+        L.pcc_clear_input.argtypes = [vp]
         _lib = L
     return _lib
 
@@ -156,6 +180,27 @@ class Converter:
     def device_input(self) -> int:
         return lib().pcc_device_input(self._h)
 
+    # ---- sharded build (driven by pcconv.dist)
+    def declare_files(self, file_points):
+        arr = (C.c_uint64 * len(file_points))(*[int(v) for v in file_points])
+        _check(lib().pcc_declare_files(self._h, arr, len(file_points)))
+
+    def add_keyed_points_device(self, pts_ptr: int, keys_ptr: int, n: int):
+        _check(lib().pcc_add_keyed_points_device(self._h, C.c_void_p(pts_ptr), C.c_void_p(keys_ptr), n))
+
+    def set_summary(self, number_of_points: int, bmin, bmax, hierarchies: int):
+        _check(lib().pcc_set_summary(self._h, number_of_points, (C.c_float * 3)(*bmin), (C.c_float * 3)(*bmax),
+                                     hierarchies))
+
+    def write_cells(self):
+        _check(lib().pcc_write_cells(self._h))
+
+    def write_metadata(self):
+        _check(lib().pcc_write_metadata(self._h))
+
+    def clear_input(self):
+        _check(lib().pcc_clear_input(self._h))
+
     def finish(self):
         """converter.rs:241-246 Drop: build if needed, write cells then metadata.json."""
         h, self._h = self._h, None
@@ -181,6 +226,35 @@ class Converter:
             self.close()
         except Exception:
             pass
+
+
+def shard_grid_from_bbox(gmin, gmax, max_cell_size: float = 1000.0) -> ShardGrid:
+    g = ShardGrid()
+    _check(lib().pcc_shard_grid_from_bbox((C.c_float * 3)(*gmin), (C.c_float * 3)(*gmax), max_cell_size, C.byref(g)))
+    return g
+
+
+def synth_device(dst_ptr: int, first: int, n: int, seed: int, kind: int = 0, lo: float = -1000.0,
+                 extent: float = 2000.0, device: int = 0):
+    _check(lib().pcc_synth_device(C.c_void_p(dst_ptr), first, n, seed, kind, lo, extent, device))
+
+
+def shard_bbox(pts_ptr: int, n: int, device: int = 0):
+    bmin, bmax = (C.c_float * 3)(), (C.c_float * 3)()
+    _check(lib().pcc_shard_bbox(C.c_void_p(pts_ptr), n, bmin, bmax, device))
+    return list(bmin), list(bmax)
+
+
+def shard_histogram(pts_ptr: int, n: int, grid: ShardGrid, hist_ptr: int, device: int = 0):
+    _check(lib().pcc_shard_histogram(C.c_void_p(pts_ptr), n, C.byref(grid), C.c_void_p(hist_ptr), device))
+
+
+def shard_route(pts_ptr: int, n: int, key0: int, grid: ShardGrid, owner_ptr: int, nranks: int, send_ptr: int,
+                keys_ptr: int, device: int = 0):
+    counts = (C.c_uint64 * nranks)()
+    _check(lib().pcc_shard_route(C.c_void_p(pts_ptr), n, key0, C.byref(grid), C.c_void_p(owner_ptr), nranks,
+                                 C.c_void_p(send_ptr), C.c_void_p(keys_ptr), counts, device))
+    return [int(c) for c in counts]
 
 
 def convert_from_paths(paths, output: str, batch_size: int = 10_000, device: int = 0):

@@ -1,0 +1,294 @@
+"""Sharded multi-GPU build: one process per GPU, one conversion.
+
+The reference converter is single-threaded (point-converter/src/converter.rs:72-139).
+Its level-0 subtrees are independent, because every level-h cell has a unique
+level-0 ancestor (converter.rs:32-47 groups a point of cell c at h+1 into a child
+of c).  So the unit of ownership is the level-0 cell, and one step is:
+
+  1. every rank holds a contiguous key range of the global input (keys = global
+     input index, lib.rs:31-52 order) resident in HBM;
+  2. local bbox -> all-reduce(max of [-min, max]) -> global bbox (the metadata
+     bounding box, converter.rs:96-104) and the level-0 grid it spans;
+  3. per-cell histogram -> all-reduce(sum) -> identical owner table on every
+     rank (`assign_owners`, deterministic);
+  4. stable partition by owner (HIP) -> all-to-all of counts, then all-to-all-v
+     of the 16-B points and the u32 keys (RCCL over xGMI).  Segments arrive in
+     source-rank order, so each rank's input stays in global key order;
+  5. independent level-synchronous builds with the GLOBAL batch structure
+     (pcc_declare_files + pcc_add_keyed_points_device);
+  6. all-reduce(max) of `hierarchies`; every rank writes its own (disjoint) cell
+     files, rank 0 writes metadata.json after a barrier.
+
+The collectives go through a small communicator interface: `TorchComm`
+(torch.distributed; backend "nccl" is RCCL on ROCm, "gloo" for the CPU tests) or
+`ThreadComm` (ranks as threads of one process, used to run the exchange on a
+single GPU in tests).  Local work goes through an ops object: `HipShardOps` is
+the product (libpcconv.so, no fallback); tests inject CPU restatements.
+"""
+from __future__ import annotations
+
+import os
+import tempfile
+import threading
+import time
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+import pcconv
+
+
+# ----------------------------------------------------------------- communicators
+class TorchComm:
+    """torch.distributed process group (nccl == RCCL on ROCm, or gloo)."""
+
+    def __init__(self, device: torch.device):
+        import torch.distributed as dist
+        self.dist = dist
+        self.rank = dist.get_rank()
+        self.world = dist.get_world_size()
+        self.device = device
+
+    def allreduce_(self, t: torch.Tensor, op: str) -> torch.Tensor:
+        ops = {"sum": self.dist.ReduceOp.SUM, "max": self.dist.ReduceOp.MAX}
+        self.dist.all_reduce(t, op=ops[op])
+        return t
+
+    def alltoall_counts(self, counts: list[int]) -> list[int]:
+        s = torch.tensor(counts, dtype=torch.int64, device=self.device)
+        r = torch.empty_like(s)
+        self.dist.all_to_all_single(r, s)
+        return [int(v) for v in r.tolist()]
+
+    def alltoallv(self, send: torch.Tensor, send_counts: list[int], recv_counts: list[int]) -> torch.Tensor:
+        out = torch.empty((sum(recv_counts),) + tuple(send.shape[1:]), dtype=send.dtype, device=send.device)
+        self.dist.all_to_all_single(out, send, recv_counts, send_counts)
+        return out
+
+    def barrier(self):
+        self.dist.barrier()
+
+
+class ThreadGroup:
+    """Shared state of `world` in-process ranks (one thread each)."""
+
+    def __init__(self, world: int):
+        self.world = world
+        self.bar = threading.Barrier(world)
+        self.slot: list = [None] * world
+
+
+class ThreadComm:
+    """Collectives between threads of one process (same semantics as TorchComm)."""
+
+    def __init__(self, group: ThreadGroup, rank: int, device: torch.device):
+        self.g = group
+        self.rank = rank
+        self.world = group.world
+        self.device = device
+
+    def _exchange(self, obj):
+        self.g.slot[self.rank] = obj
+        self.g.bar.wait()
+        allv = list(self.g.slot)
+        self.g.bar.wait()   # nobody overwrites a slot before everyone has read it
+        return allv
+
+    def allreduce_(self, t: torch.Tensor, op: str) -> torch.Tensor:
+        allv = self._exchange(t.clone())
+        acc = allv[0].clone()
+        for v in allv[1:]:
+            acc = acc + v.to(acc.device) if op == "sum" else torch.maximum(acc, v.to(acc.device))
+        t.copy_(acc)
+        return t
+
+    def alltoall_counts(self, counts: list[int]) -> list[int]:
+        allv = self._exchange(list(counts))
+        return [int(allv[src][self.rank]) for src in range(self.world)]
+
+    def alltoallv(self, send: torch.Tensor, send_counts: list[int], recv_counts: list[int]) -> torch.Tensor:
+        allv = self._exchange((send, list(send_counts)))
+        parts = []
+        for src in range(self.world):
+            t, c = allv[src]
+            o = sum(c[: self.rank])
+            parts.append(t[o:o + c[self.rank]].to(send.device))
+        out = torch.cat(parts) if parts else send[:0]
+        self.g.bar.wait()   # senders may free/reuse their buffers only after every copy
+        return out
+
+    def barrier(self):
+        self.g.bar.wait()
+
+
+# ----------------------------------------------------------------- ownership
+def assign_owners(hist: np.ndarray, world: int, greedy_max: int = 4096) -> np.ndarray:
+    """Owner rank of every level-0 cell from the GLOBAL histogram (identical on
+    every rank).  Up to `greedy_max` non-empty cells: LPT greedy (largest cell
+    first, ties by cell id, to the least-loaded rank, ties by rank).  Beyond
+    that: contiguous cell-id ranges split at equal point counts."""
+    hist = np.asarray(hist, dtype=np.int64)
+    owner = np.zeros(len(hist), dtype=np.uint32)
+    nz = np.flatnonzero(hist)
+    if world <= 1 or len(nz) == 0:
+        return owner
+    if len(nz) <= greedy_max:
+        order = nz[np.lexsort((nz, -hist[nz]))]
+        load = np.zeros(world, dtype=np.int64)
+        for c in order:
+            r = int(np.argmin(load))
+            owner[c] = r
+            load[r] += hist[c]
+        return owner
+    before = np.cumsum(hist) - hist
+    owner[:] = np.minimum(world - 1, (before * world) // max(int(hist.sum()), 1)).astype(np.uint32)
+    return owner
+
+
+# ----------------------------------------------------------------- local ops (product)
+class HipShardOps:
+    """Local per-rank work on the GPU through libpcconv.so (no CPU fallback)."""
+
+    def __init__(self, device_index: int, out_dir: str | None = None, batch_size: int = 10_000,
+                 config: dict | None = None):
+        self.dev = device_index
+        self.cfg = dict(config or {})
+        self.max_cell_size = float(self.cfg.get("max_cell_size", 1000.0))
+        self._tmp = None
+        if out_dir is None:
+            self._tmp = tempfile.TemporaryDirectory(prefix="pcc_shard_")
+            out_dir = self._tmp.name
+        self.conv = pcconv.Converter(out_dir, batch_size=batch_size, device=device_index, config=self.cfg)
+
+    def _ready(self):
+        # inputs may come from torch kernels or RCCL on torch's streams; the
+        # library runs on its own stream, so order them through the host
+        torch.cuda.synchronize(self.dev)
+
+    def bbox(self, pts: torch.Tensor):
+        self._ready()
+        return pcconv.shard_bbox(pts.data_ptr(), pts.shape[0], self.dev)
+
+    def grid(self, gmin, gmax) -> pcconv.ShardGrid:
+        return pcconv.shard_grid_from_bbox(gmin, gmax, self.max_cell_size)
+
+    def histogram(self, pts: torch.Tensor, grid) -> torch.Tensor:
+        h = torch.empty(grid.ncells, dtype=torch.int32, device=pts.device)
+        self._ready()
+        pcconv.shard_histogram(pts.data_ptr(), pts.shape[0], grid, h.data_ptr(), self.dev)
+        return h
+
+    def route(self, pts: torch.Tensor, key0: int, grid, owner: torch.Tensor, world: int):
+        n = pts.shape[0]
+        send = torch.empty_like(pts)
+        keys = torch.empty(n, dtype=torch.int32, device=pts.device)
+        self._ready()
+        counts = pcconv.shard_route(pts.data_ptr(), n, key0, grid, owner.data_ptr(), world, send.data_ptr(),
+                                    keys.data_ptr(), self.dev)
+        return send, keys, counts
+
+    def build(self, file_points, pts: torch.Tensor, keys: torch.Tensor) -> dict:
+        c = self.conv
+        self._ready()
+        c.clear_input()
+        c.declare_files(file_points)
+        c.add_keyed_points_device(pts.data_ptr(), keys.data_ptr(), pts.shape[0])
+        return c.build()
+
+    def write(self, summary: dict, cells: bool, metadata: bool):
+        c = self.conv
+        c.set_summary(summary["number_of_points"], summary["bbox_min"], summary["bbox_max"], summary["hierarchies"])
+        if cells:
+            c.write_cells()
+        if metadata:
+            c.write_metadata()
+
+    def close(self):
+        self.conv.close()
+        if self._tmp is not None:
+            self._tmp.cleanup()
+
+
+# ----------------------------------------------------------------- one sharded step
+@dataclass
+class ShardResult:
+    summary: dict
+    local: dict
+    recv_points: int
+    owned_cells: int
+    ms: dict = field(default_factory=dict)
+
+
+def shard_build(comm, ops, pts: torch.Tensor, key0: int, file_points, write: bool = False,
+                sync=None) -> ShardResult:
+    """One sharded conversion step.  `pts` is this rank's (n, 4) int32 view of
+    16-B points with global keys key0 .. key0+n-1 (contiguous ranges in rank
+    order).  `file_points` is the GLOBAL file structure.  `sync` (optional)
+    synchronises the device for stage timing."""
+    ms = {}
+    t0 = time.perf_counter()
+
+    def mark(name):
+        nonlocal t0
+        if sync is not None:
+            sync()
+        t1 = time.perf_counter()
+        ms[name] = ms.get(name, 0.0) + (t1 - t0) * 1e3
+        t0 = t1
+
+    n_total = int(sum(int(v) for v in file_points))
+    # 2. global bounding box (converter.rs:96-104: componentwise min/max)
+    if pts.shape[0]:
+        bmin, bmax = ops.bbox(pts)
+    else:
+        bmin, bmax = [float("inf")] * 3, [float("-inf")] * 3
+    bb = torch.tensor([-bmin[0], -bmin[1], -bmin[2], bmax[0], bmax[1], bmax[2]], dtype=torch.float32,
+                      device=comm.device)
+    comm.allreduce_(bb, "max")
+    bbh = bb.cpu().tolist()
+    gmin, gmax = [-bbh[0], -bbh[1], -bbh[2]], bbh[3:]
+    mark("bbox")
+    if n_total == 0:
+        recv = pts[:0]
+        keys = torch.empty(0, dtype=torch.int32, device=pts.device)
+        owned = 0
+    else:
+        # 3. level-0 ownership
+        grid = ops.grid(gmin, gmax)
+        hist = ops.histogram(pts, grid)
+        hist = comm.allreduce_(hist.to(comm.device), "sum")
+        hist_h = hist.cpu().numpy().astype(np.int64)
+        owner_h = assign_owners(hist_h, comm.world)
+        owned = int(np.count_nonzero((owner_h == comm.rank) & (hist_h > 0)))
+        owner = torch.from_numpy(owner_h.astype(np.int32)).to(pts.device)
+        mark("plan")
+        # 4. route + exchange (all-to-all-v of points and keys)
+        send, skeys, counts = ops.route(pts, key0, grid, owner, comm.world)
+        mark("route")
+        rcounts = comm.alltoall_counts(counts)
+        recv = comm.alltoallv(send.to(comm.device), counts, rcounts).to(pts.device)
+        keys = comm.alltoallv(skeys.to(comm.device), counts, rcounts).to(pts.device)
+        mark("exchange")
+    # 5. independent build of the owned level-0 subtrees
+    local = ops.build(file_points, recv, keys)
+    mark("build")
+    # 6. global metadata values
+    hz = torch.tensor([int(local["hierarchies"])], dtype=torch.int64, device=comm.device)
+    comm.allreduce_(hz, "max")
+    summary = {"number_of_points": n_total, "hierarchies": int(hz.item()),
+               "bbox_min": gmin if n_total else [0.0, 0.0, 0.0], "bbox_max": gmax if n_total else [0.0, 0.0, 0.0]}
+    mark("summary")
+    if write:
+        ops.write(summary, cells=True, metadata=False)
+        comm.barrier()
+        if comm.rank == 0:
+            ops.write(summary, cells=False, metadata=True)
+        comm.barrier()
+        mark("write")
+    return ShardResult(summary=summary, local=local, recv_points=int(recv.shape[0]), owned_cells=owned, ms=ms)
+
+
+def key_range(n_total: int, rank: int, world: int) -> tuple[int, int]:
+    """Contiguous key range [a, b) of rank `rank` (input split evenly in order)."""
+    return (n_total * rank) // world, (n_total * (rank + 1)) // world

@@ -1,0 +1,169 @@
+"""Sharded (multi-GPU) orchestration on CPU ranks — SURVEY.md §8e.
+
+pcconv/dist.py runs unchanged over gloo (world size 2, separate processes) and
+over in-process thread ranks, with the CPU test double tests/shard_np.py for the
+local work.  The union of the ranks' cell files plus rank 0's metadata must equal
+the single-process sequential oracle's output on the same input.
+"""
+import json
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "..", "point-cloud_amd"))
+
+import canon  # noqa: E402
+from gpu_util import run_oracle  # noqa: E402
+from oracle_ctypes import synth  # noqa: E402
+from pcconv.dist import ThreadComm, ThreadGroup, TorchComm, assign_owners, key_range, shard_build  # noqa: E402
+from shard_np import NumpyShardOps, as_tensor  # noqa: E402
+
+
+def make_input(case):
+    """(list of per-file point arrays) for a named case."""
+    if case == "uniform":
+        return [synth(11, 0, 120_000)]
+    if case == "files":     # ragged files incl. an empty one: batch structure crosses rank key ranges
+        return [synth(12, 0, 33_333), synth(13, 0, 0), synth(14, 1, 47_001, lo=-1500.0, ext=3000.0)]
+    if case == "clustered":
+        return [synth(15, 1, 90_000)]
+    raise KeyError(case)
+
+
+def rank_slice(files, rank, world):
+    allp = np.concatenate(files) if files else np.zeros(0)
+    a, b = key_range(len(allp), rank, world)
+    return allp[a:b], a
+
+
+def check_against_oracle(tmp_path, files, out_dir, summary, cfg=None, batch=10_000):
+    ref = str(tmp_path / "oracle")
+    err, _ = run_oracle(ref, files, cfg, batch)
+    assert err == 0
+    ca, ma = canon.read_dir_fast(ref)
+    cb, mb = canon.read_dir_fast(out_dir)
+    d = canon.diff_fast(ca, cb)
+    assert not d, d
+    assert summary["number_of_points"] == ma["number_of_points"] == mb["number_of_points"]
+    assert summary["hierarchies"] == ma["hierarchies"] == mb["hierarchies"]
+    assert ma["bmin"] == mb["bmin"] and ma["bmax"] == mb["bmax"]
+
+
+# ------------------------------------------------------------- owner table
+def test_assign_owners_greedy_balanced_and_deterministic():
+    h = np.array([0, 50, 10, 10, 0, 40, 30, 20], dtype=np.int64)
+    o = assign_owners(h, 2)
+    assert (assign_owners(h, 2) == o).all()
+    load = [int(h[o == r].sum()) for r in range(2)]
+    assert sorted(load) == [80, 80]
+    assert (o[h == 0] == 0).all()
+    assert (assign_owners(h, 1) == 0).all()
+
+
+def test_assign_owners_eight_octants_one_per_rank():
+    h = np.full(8, 125_000_000, dtype=np.int64)
+    assert sorted(assign_owners(h, 8).tolist()) == list(range(8))
+    o4 = assign_owners(h, 4)
+    assert [int((o4 == r).sum()) for r in range(4)] == [2, 2, 2, 2]
+
+
+def test_assign_owners_many_cells_prefix_split():
+    rng = np.random.default_rng(0)
+    h = rng.integers(0, 1000, size=20_000)
+    o = assign_owners(h, 3, greedy_max=100)
+    assert (np.diff(o[h > 0].astype(np.int64)) >= 0).all()   # contiguous ranges
+    load = np.array([h[o == r].sum() for r in range(3)])
+    assert load.max() - load.min() <= 2 * h.max()
+
+
+# ------------------------------------------------------------- thread ranks
+@pytest.mark.parametrize("case,world", [("uniform", 2), ("files", 3), ("clustered", 4)])
+def test_thread_ranks_match_oracle(tmp_path, case, world):
+    import threading
+    files = make_input(case)
+    fp = [len(f) for f in files]
+    out = str(tmp_path / "out")
+    grp = ThreadGroup(world)
+    res, errs = [None] * world, []
+
+    def worker(r):
+        try:
+            pts, key0 = rank_slice(files, r, world)
+            ops = NumpyShardOps(out)
+            res[r] = shard_build(ThreadComm(grp, r, torch.device("cpu")), ops, as_tensor(pts), key0, fp, write=True)
+            ops.close()
+        except BaseException as e:  # noqa: BLE001
+            errs.append(e)
+            grp.bar.abort()
+
+    th = [threading.Thread(target=worker, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs
+    assert sum(r.recv_points for r in res) == sum(fp)
+    assert all(r.summary == res[0].summary for r in res)
+    check_against_oracle(tmp_path, files, out, res[0].summary)
+
+
+def test_thread_ranks_empty_input(tmp_path):
+    import threading
+    grp = ThreadGroup(2)
+    res = [None, None]
+
+    def worker(r):
+        ops = NumpyShardOps(str(tmp_path / "out"))
+        pts = as_tensor(np.zeros(0, dtype=synth(1, 0, 1).dtype))
+        res[r] = shard_build(ThreadComm(grp, r, torch.device("cpu")), ops, pts, 0, [0], write=False)
+
+    th = [threading.Thread(target=worker, args=(r,)) for r in range(2)]
+    [t.start() for t in th]
+    [t.join() for t in th]
+    assert res[0].summary == {"number_of_points": 0, "hierarchies": 1, "bbox_min": [0.0] * 3, "bbox_max": [0.0] * 3}
+
+
+# ------------------------------------------------------------- gloo, 2 processes
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _gloo_worker(rank, world, port, case, out, res_dir):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        files = make_input(case)
+        pts, key0 = rank_slice(files, rank, world)
+        ops = NumpyShardOps(out)
+        r = shard_build(TorchComm(torch.device("cpu")), ops, as_tensor(pts), key0, [len(f) for f in files],
+                        write=True)
+        ops.close()
+        with open(os.path.join(res_dir, f"rank{rank}.json"), "w") as f:
+            json.dump({"summary": r.summary, "recv": r.recv_points, "owned": r.owned_cells}, f)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("case", ["uniform", "files"])
+def test_gloo_world2_matches_oracle(tmp_path, case):
+    import torch.multiprocessing as mp
+    out, rd = str(tmp_path / "out"), str(tmp_path / "res")
+    os.makedirs(rd)
+    mp.spawn(_gloo_worker, args=(2, _free_port(), case, out, rd), nprocs=2, join=True)
+    r = [json.load(open(os.path.join(rd, f"rank{i}.json"))) for i in range(2)]
+    files = make_input(case)
+    assert r[0]["summary"] == r[1]["summary"]
+    assert r[0]["recv"] + r[1]["recv"] == sum(len(f) for f in files)
+    if case == "uniform":
+        assert r[0]["owned"] == r[1]["owned"] == 4     # 8 level-0 octants, 4 per rank
+    check_against_oracle(tmp_path, files, out, r[0]["summary"])

@@ -1,0 +1,133 @@
+"""Sharded build on the GPU through the C-ABI.
+
+One MI355X per test box, so ranks are threads of one process sharing cuda:0
+(pcconv.dist.ThreadComm): the exchange moves real device tensors and every
+rank runs the product path (HipShardOps -> libpcconv.so).  The merged output
+must equal the single-process sequential oracle.
+"""
+import os
+import sys
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "..", "point-cloud_amd"))
+
+import pcconv  # noqa: E402
+from pcconv.dist import HipShardOps, ThreadComm, ThreadGroup, key_range, shard_build  # noqa: E402
+from shard_np import NumpyShardOps, as_points, as_tensor  # noqa: E402
+from test_dist_cpu import check_against_oracle, make_input, rank_slice  # noqa: E402
+from oracle_ctypes import synth  # noqa: E402
+from gpu_util import compare_dirs, run_gpu  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+
+
+def test_keyed_input_equals_plain_input(tmp_path):
+    """All points keyed 0..N-1 with the declared file structure == pcc_add_points."""
+    files = [synth(21, 0, 150_000), synth(22, 1, 61_234)]
+    allp = np.concatenate(files)
+    plain = str(tmp_path / "plain")
+    run_gpu(plain, files)
+    keyed = str(tmp_path / "keyed")
+    c = pcconv.Converter(keyed)
+    c.declare_files([len(f) for f in files])
+    pts = as_tensor(allp).to(DEV)
+    keys = torch.arange(len(allp), dtype=torch.int32, device=DEV)
+    torch.cuda.synchronize()
+    c.add_keyed_points_device(pts.data_ptr(), keys.data_ptr(), len(allp))
+    c.finish()
+    d, ma, mb = compare_dirs(plain, keyed)
+    assert not d, d
+    assert ma == mb
+
+
+def test_shard_histogram_and_route_match_numpy():
+    pts_np = synth(23, 1, 200_001, lo=-2500.0, ext=5000.0)
+    pts = as_tensor(pts_np).to(DEV)
+    ref = NumpyShardOps("/nonexistent")
+    gmin, gmax = ref.bbox(as_tensor(pts_np))
+    assert pcconv.shard_bbox(pts.data_ptr(), len(pts_np)) == (gmin, gmax)
+    g = pcconv.shard_grid_from_bbox(gmin, gmax)
+    h = torch.empty(g.ncells, dtype=torch.int32, device=DEV)
+    torch.cuda.synchronize()
+    pcconv.shard_histogram(pts.data_ptr(), len(pts_np), g, h.data_ptr())
+    href = ref.histogram(as_tensor(pts_np), g)
+    assert torch.equal(h.cpu(), href)
+    for world in (2, 3, 5):
+        owner = torch.from_numpy((np.arange(g.ncells) * 7 % world).astype(np.int32))
+        send = torch.empty_like(pts)
+        keys = torch.empty(len(pts_np), dtype=torch.int32, device=DEV)
+        od = owner.to(DEV)
+        torch.cuda.synchronize()
+        counts = pcconv.shard_route(pts.data_ptr(), len(pts_np), 1000, g, od.data_ptr(), world, send.data_ptr(),
+                                    keys.data_ptr())
+        s2, k2, c2 = ref.route(as_tensor(pts_np), 1000, g, owner, world)
+        assert counts == c2
+        assert torch.equal(send.cpu(), s2)
+        assert torch.equal(keys.cpu(), k2)
+
+
+def test_synth_device_matches_oracle_stream():
+    p = torch.empty((77_777, 4), dtype=torch.int32, device=DEV)
+    pcconv.synth_device(p.data_ptr(), 123_456, 77_777, 9, 1)
+    assert (as_points(p.cpu()).view(np.uint8) == synth(9, 1, 77_777, first=123_456).view(np.uint8)).all()
+
+
+def _run_threads(files, world, out, cfg=None, batch=10_000):
+    fp = [len(f) for f in files]
+    grp = ThreadGroup(world)
+    res, errs = [None] * world, []
+
+    def worker(r):
+        try:
+            torch.cuda.set_device(DEV)
+            pts, key0 = rank_slice(files, r, world)
+            ops = HipShardOps(0, out_dir=out, batch_size=batch, config=cfg)
+            t = as_tensor(pts).to(DEV)
+            res[r] = shard_build(ThreadComm(grp, r, DEV), ops, t, key0, fp, write=True)
+            ops.close()
+        except BaseException as e:  # noqa: BLE001
+            errs.append(e)
+            grp.bar.abort()
+
+    th = [threading.Thread(target=worker, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs
+    return res
+
+
+@pytest.mark.parametrize("case,world", [("uniform", 2), ("files", 3), ("clustered", 4), ("uniform", 8)])
+def test_sharded_threads_match_oracle(tmp_path, case, world):
+    files = make_input(case)
+    out = str(tmp_path / "out")
+    res = _run_threads(files, world, out)
+    assert sum(r.recv_points for r in res) == sum(len(f) for f in files)
+    check_against_oracle(tmp_path, files, out, res[0].summary)
+
+
+def test_sharded_threads_2m_multilevel(tmp_path):
+    """2M uniform points, 32-slot sub-grid: several levels per shard, 4 octants per rank."""
+    cfg = dict(sub_grid_dimension=32)
+    files = [synth(31, 0, 2_000_000)]
+    out = str(tmp_path / "out")
+    res = _run_threads(files, 2, out, cfg=cfg)
+    assert [r.owned_cells for r in res] == [4, 4]
+    assert res[0].summary["hierarchies"] >= 2
+    check_against_oracle(tmp_path, files, out, res[0].summary, cfg=cfg)
+
+
+def test_sharded_small_limit_deep(tmp_path):
+    """Tiny overflow limit + clustered data: deep hierarchies per shard."""
+    cfg = dict(cell_point_overflow_limit=64, sub_grid_dimension=8)
+    files = [synth(32, 1, 60_000)]
+    out = str(tmp_path / "out")
+    res = _run_threads(files, 3, out, cfg=cfg, batch=777)
+    check_against_oracle(tmp_path, files, out, res[0].summary, cfg=cfg, batch=777)
