@@ -1,0 +1,78 @@
+"""Golden fixtures (tests/golden/*.json, made by tests/golden/make_golden.py).
+
+Vectors are accepted by make_golden.py only when pyref.convert_sequential,
+pyref.convert_keyed and the C oracle agree; the reference itself ships no
+fixtures for this path, so they are PARITY-UNPINNED against the Rust binary
+(SURVEY.md §8c).  CPU: the C oracle must reproduce every fixture.  GPU: the HIP
+build through the C-ABI must reproduce every fixture.
+"""
+import glob
+import json
+import os
+import sys
+import tempfile
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "..", "point-cloud_amd"))
+
+import canon  # noqa: E402
+from golden.make_golden import canon_json  # noqa: E402
+from oracle_ctypes import POINT_DTYPE, Oracle, synth  # noqa: E402
+
+FIXTURES = sorted(glob.glob(os.path.join(HERE, "golden", "*.json")))
+assert FIXTURES, "tests/golden fixtures missing"
+
+
+def load(path):
+    with open(path) as f:
+        fx = json.load(f)
+    if "files_hex" in fx:
+        files = [np.frombuffer(bytes.fromhex(h), dtype=POINT_DTYPE) for h in fx["files_hex"]]
+    else:
+        s = fx["synth"]
+        files = [synth(s["seed"], s["kind"], s["n"], lo=s["lo"], ext=s["extent"])]
+    return fx, files
+
+
+def check(fx, out_dir):
+    cells, meta = canon.read_dir(out_dir)
+    if "expected" in fx:
+        got = json.loads(json.dumps(canon_json(cells, meta)))
+        exp = fx["expected"]
+        assert got["metadata"] == exp["metadata"]
+        assert len(got["cells"]) == len(exp["cells"])
+        for a, b in zip(got["cells"], exp["cells"]):
+            assert a == b, a["id"]
+    else:
+        assert len(cells) == fx["cells"]
+        assert canon.digest(cells) == fx["digest"]
+        assert json.loads(json.dumps(meta)) == fx["metadata"]
+
+
+@pytest.mark.parametrize("path", FIXTURES, ids=[os.path.basename(p)[:-5] for p in FIXTURES])
+def test_oracle_reproduces_golden(path):
+    fx, files = load(path)
+    o = Oracle(fx["config"])
+    for f in files:
+        o.add_file(f, fx["batch"])
+    assert o.error == 0
+    with tempfile.TemporaryDirectory() as d:
+        o.write(d)
+        o.close()
+        check(fx, d)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("path", FIXTURES, ids=[os.path.basename(p)[:-5] for p in FIXTURES])
+def test_gpu_reproduces_golden(path, tmp_path):
+    import pcconv
+    fx, files = load(path)
+    out = str(tmp_path / "gpu")
+    conv = pcconv.Converter(out, batch_size=fx["batch"], config=fx["config"])
+    for f in files:
+        conv.add_points(f)
+    conv.finish()
+    check(fx, out)
