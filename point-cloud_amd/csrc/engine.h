@@ -106,6 +106,7 @@ private:
     void ev_collect();
     int level0_bin();
     int run_level(uint32_t h);
+    void run_dcap(Level* L);
     void free_all();
 
     Config cfg_;

@@ -68,6 +68,7 @@ enum ErrBits : uint32_t {
     ERR_L0_RANGE = 1u << 5,
     ERR_CAPACITY = 1u << 6,
     ERR_CLAIM = 1u << 7,
+    ERR_SLAB_SIZE = 1u << 8,
 };
 
 struct Counters {
@@ -81,9 +82,11 @@ struct Counters {
     unsigned long long dense_arrivals, small_arrivals;
 };
 
+// One level's arrivals: the 16-B record (x, y, z, rgba bits) as one float4 so
+// every load/store of a point is a single dwordx4; key and event batch apart.
 struct Arena {
-    float *x, *y, *z;
-    uint32_t *c, *k, *e;
+    float4* p;
+    uint32_t *k, *e;
 };
 
 struct Engine::Dev {
@@ -92,6 +95,8 @@ struct Engine::Dev {
     float* bbox_part = nullptr;     // per-block min/max partials
     uint32_t* bbox_flag = nullptr;
     uint32_t* files = nullptr;      // per file: start_lo, start_hi, eb0, batch
+    uint32_t* fate = nullptr;       // per arena position: emission position of a displaced record
+    uint16_t* status = nullptr;     // per arena position: slot-table entry + 1 of a record
     ScanTemp scan;
     uint64_t cap = 0;
     // chunked bump allocator for per-build tables and output regions (reset at
@@ -133,6 +138,7 @@ struct Engine::Level {
     uint32_t* dcap = nullptr;        // 24 * nslabs: arrivals of this slab per child slab (capacity)
     uint32_t* dest_off = nullptr;    // 24 * nslabs: exclusive scan of dcap = emission regions (next arena)
     uint32_t* dest_n = nullptr;      // 24 * nslabs: emissions actually written
+    uint32_t max_slab = 0;           // largest slab (arrivals)
     uint32_t* gcap = nullptr;        // 24 * 24 * nslabs: capacities of the child slabs' own child slabs
     uint32_t* grid_off = nullptr;    // exclusive scan of slab_n = winner regions (capacity n)
     uint32_t* slab_grid_n = nullptr;
@@ -423,7 +429,8 @@ __global__ __launch_bounds__(kL0BS) void k_l0_up(Arena A, uint64_t n, L0Params P
     for (int r = 0; r < kL0IPT; r++) {
         const uint64_t i = base + (uint64_t)r * kL0BS + threadIdx.x;
         if (i < n) {
-            const int64_t d = l0_dense(P, A.x[i], A.y[i], A.z[i]);
+            const float4 v = A.p[i];
+            const int64_t d = l0_dense(P, v.x, v.y, v.z);
             atomicAdd(&dh[((uint64_t)(d < 0 ? 0 : d) >> shift) & (R - 1)], 1u);
         }
     }
@@ -466,7 +473,8 @@ __global__ __launch_bounds__(kL0BS) void k_l0_down(const Point* __restrict__ in,
                 x[r] = v.x; y[r] = v.y; z[r] = v.z; c[r] = __float_as_uint(v.w);
                 k[r] = keys ? keys[i] : (uint32_t)i;   // sharded input carries global keys
             } else {
-                x[r] = S.x[i]; y[r] = S.y[i]; z[r] = S.z[i]; c[r] = S.c[i]; k[r] = S.k[i];
+                const float4 v = S.p[i];
+                x[r] = v.x; y[r] = v.y; z[r] = v.z; c[r] = __float_as_uint(v.w); k[r] = S.k[i];
             }
             const int64_t d = l0_dense(P, x[r], y[r], z[r]);
             dg[r] = (uint16_t)(((uint64_t)(d < 0 ? 0 : d) >> shift) & (R - 1));
@@ -517,7 +525,8 @@ __global__ __launch_bounds__(kL0BS) void k_l0_down(const Point* __restrict__ in,
     for (uint32_t j = threadIdx.x; j < tn; j += kL0BS) {
         const uint32_t d = sd[j];
         const uint32_t dst = goff[d] + (j - dbase[d]);
-        O.x[dst] = sx[j]; O.y[dst] = sy[j]; O.z[dst] = sz[j]; O.c[dst] = sc[j]; O.k[dst] = sk[j];
+        O.p[dst] = make_float4(sx[j], sy[j], sz[j], __uint_as_float(sc[j]));
+        O.k[dst] = sk[j];
         if constexpr (FINAL) O.e[dst] = event_batch(files, nfiles, sk[j]);
     }
 }
@@ -562,42 +571,6 @@ __global__ void k_l0_tables(const uint32_t* hist, const uint32_t* cnt_scan, cons
     }
 }
 
-// capacities of the level-0 slabs: arrivals per child slab
-constexpr uint32_t kDcapChunk = 32768;
-__global__ __launch_bounds__(256) void k_l0_dcap(Arena A, L0Params P, const int32_t* cell_idx,
-                                                 const uint32_t* slab_cell, const int32_t* slab_layer,
-                                                 const uint32_t* slab_off, const uint32_t* slab_n, uint32_t* dcap,
-                                                 Counters* ctr) {
-    __shared__ uint32_t cnt[kDests];
-    const uint32_t s = blockIdx.x, j0 = blockIdx.y * kDcapChunk;
-    const uint32_t cr_ = slab_cell[s], off = slab_off[s], n = slab_n[s];
-    if (j0 >= n) return;
-    const uint32_t j1 = min(n, j0 + kDcapChunk);
-    if (threadIdx.x < kDests) cnt[threadIdx.x] = 0;
-    __syncthreads();
-    const int32_t t = slab_layer[s];
-    const int32_t cx = cell_idx[3 * cr_], cy = cell_idx[3 * cr_ + 1], cz = cell_idx[3 * cr_ + 2];
-    uint32_t err = 0;
-    uint32_t loc[kDests] = {};
-    for (uint32_t j = j0 + threadIdx.x; j < j1; j += 256) {
-        int32_t ix, iy, iz, u;
-        const int d = route(P.csc, P.crc, cx, cy, cz, t, A.x[off + j], A.y[off + j], A.z[off + j], ix, iy, iz, u, err);
-        if (d >= 0) {
-#pragma unroll
-            for (int q = 0; q < kDests; q++) loc[q] += (q == d);
-        }
-    }
-#pragma unroll
-    for (int q = 0; q < kDests; q++) {
-        uint32_t v = loc[q];
-        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-        if ((threadIdx.x & 63) == 0 && v) atomicAdd(&cnt[q], v);
-    }
-    if (err) set_err(ctr, err);
-    __syncthreads();
-    if (threadIdx.x < kDests && cnt[threadIdx.x]) atomicAdd(&dcap[s * kDests + threadIdx.x], cnt[threadIdx.x]);
-}
-
 // ------------------------------------------------------------------ slab kernels
 struct SlabParams {
     Arena in, nx;
@@ -614,13 +587,14 @@ struct SlabParams {
     const uint32_t* dest_off;
     uint32_t* slab_grid_n;
     uint32_t* dest_n;
-    uint32_t* gcap;
+    uint32_t* fate;       // per arrival: emission position of a displaced record (pass 1 -> pass 2)
+    uint16_t* status;     // per arrival: table entry + 1 if it became a slot record, else 0
+    uint32_t* gcap;       // 24 x 24 per slab: arrivals of each child slab per grandchild slab
     Counters* ctr;
     float cs;
     LevelGeo G;
     int32_t tx, ty;
     int32_t check_gchild;
-    int32_t ablate;   // timing-only diagnostics (PCC_ABLATE): 1 no emission, 2 no claim rounds, 4 no occupant loads
     unsigned long long* stamps;   // diagnostic build only
 };
 
@@ -695,6 +669,26 @@ __device__ __forceinline__ int claim_insert(uint32_t* H, uint32_t local, uint32_
     return -1;
 }
 
+// Slot-table entry: (d2 bits << 33) | (dest << 28) | j.  d2 >= +0 so its sign
+// bit is free; dest (0..23) is the occupant's child slab, so displacing it needs
+// no access to its payload; j < 2^28 indexes the slab's arrivals.
+constexpr uint32_t kJBits = 28;
+constexpr uint32_t kJMask = (1u << kJBits) - 1;
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ u32x4 bld4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+}
+__device__ __forceinline__ void bst4(__amdgpu_buffer_rsrc_t r, uint32_t off, u32x4 v) {
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 0);
+}
+__device__ __forceinline__ void bst16(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t v) {
+    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)v, r, off, 0, 0);
+}
+__device__ __forceinline__ uint32_t bld16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_amdgcn_raw_buffer_load_b16(r, off, 0, 0);
+}
+
 template <bool DENSE>
 __global__ __launch_bounds__(SlabLds<DENSE>::BS) void k_slab(SlabParams P) {
     using L = SlabLds<DENSE>;
@@ -709,20 +703,24 @@ __global__ __launch_bounds__(SlabLds<DENSE>::BS) void k_slab(SlabParams P) {
     const int32_t cx = P.cell_idx[3 * cr_], cy = P.cell_idx[3 * cr_ + 1], cz = P.cell_idx[3 * cr_ + 2];
     const uint32_t sb = P.cell_sb[cr_];
     const LevelGeo& G = P.G;
+    if (n > kJMask) {   // the entry packs j in 28 bits
+        if (tid == 0) set_err(P.ctr, ERR_SLAB_SIZE);
+        return;
+    }
     // reference slot: the one holding the cell centre (metadata.rs:104-106)
     const I3 c0 = hex_from_world_fast(cell_pos1(cx, P.cs), cell_pos1(cy, P.cs), cell_pos1(cz, P.cs), G);
     const int32_t rx = c0.x - P.tx / 2, ry = c0.y - P.ty / 2;
     uint32_t err = 0;
     if (tid == 0) atomicAdd(DENSE ? &P.ctr->dense_arrivals : &P.ctr->small_arrivals, (unsigned long long)n);
-    // buffer descriptors: this slab's arrivals, and the contiguous region of its
-    // 24 child slabs in the next arena (out-of-range offsets drop a store)
+    // buffer descriptors: this slab's arrivals + per-arrival status/fate, and the
+    // contiguous region of its 24 child slabs in the next arena (out-of-range
+    // offsets drop a store)
     const uint64_t nb = (uint64_t)n * 4;
-    const __amdgpu_buffer_rsrc_t rX = srd(P.in.x + off, nb), rY = srd(P.in.y + off, nb), rZ = srd(P.in.z + off, nb);
-    const __amdgpu_buffer_rsrc_t rC = srd(P.in.c + off, nb), rK = srd(P.in.k + off, nb), rE = srd(P.in.e + off, nb);
+    const __amdgpu_buffer_rsrc_t rP = srd(P.in.p + off, nb * 4), rK = srd(P.in.k + off, nb), rE = srd(P.in.e + off, nb);
+    const __amdgpu_buffer_rsrc_t rF = srd(P.fate + off, nb), rS = srd(P.status + off, (uint64_t)n * 2);
     const uint32_t dbase = P.dest_off[s * kDests];
     const uint64_t db = (uint64_t)(P.dest_off[s * kDests + kDests - 1] + P.dcap[s * kDests + kDests - 1] - dbase) * 4;
-    const __amdgpu_buffer_rsrc_t oX = srd(P.nx.x + dbase, db), oY = srd(P.nx.y + dbase, db), oZ = srd(P.nx.z + dbase, db);
-    const __amdgpu_buffer_rsrc_t oC = srd(P.nx.c + dbase, db), oK = srd(P.nx.k + dbase, db), oE = srd(P.nx.e + dbase, db);
+    const __amdgpu_buffer_rsrc_t oP = srd(P.nx.p + dbase, db * 4), oK = srd(P.nx.k + dbase, db), oE = srd(P.nx.e + dbase, db);
 
     for (int i = tid; i < TAB; i += BS) {
         S.tab[i] = kEmpty64;
@@ -740,22 +738,26 @@ __global__ __launch_bounds__(SlabLds<DENSE>::BS) void k_slab(SlabParams P) {
     __syncthreads();
     STAMP(0);
 
-    // Software pipeline, one chunk of BS arrivals (key order) per step:
-    //   phase A : slot/d2 of chunk i, claim inserts; routing + wave ranks of chunk i-1
-    //   barrier : then per round: apply claim winners | barrier | (round 1: chunk i-1
-    //             stores) check remaining | re-claim | barrier ...
-    // Chunk i-1's occupant loads were issued one step earlier.  A/B stages
-    // alternate so the loop carries no register copies of loaded values.
+    // ---- pass 1: replay the slab in key order (cell.rs:70-94), one chunk of BS
+    // arrivals per step, software-pipelined:
+    //   phase A : slot/d2/own route of chunk i, claim inserts; wave ranks of the
+    //             emissions of chunk i-1 (stage prv)
+    //   barrier : per round: apply claim winners | barrier | (round 1: stores of
+    //             chunk i-1) check remaining | re-claim | barrier ...
+    // An emission is either the arrival itself (kind 0: full record written) or
+    // the occupant it displaced (kind 1: key/eb of the displacer written now, the
+    // occupant's payload in pass 2 through fate[]).
     struct Stage {
-        int32_t em;
-        uint32_t j, k, e, c, oc;
-        float x, y, z, ox, oy, oz;
+        int32_t em;             // -1 none, 0 self, 1 displaced occupant
+        int32_t g;              // self emission: grandchild slab (0..23) inside its child slab, -1 none
+        uint32_t jo, d, k, e, c;
+        float x, y, z;
     };
-    Stage A = {-1, 0, 0, 0, 0, 0, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    Stage A = {-1, -1, 0, 0, 0, 0, 0, 0.f, 0.f, 0.f};
     Stage B = A;
-    uint32_t jo = min(tid, nm1) * 4;
-    float nxx = __uint_as_float(bld(rX, jo)), nxy = __uint_as_float(bld(rY, jo)), nxz = __uint_as_float(bld(rZ, jo));
-    uint32_t nxc = bld(rC, jo), nxk = bld(rK, jo), nxe = bld(rE, jo);
+    uint32_t jo = min(tid, nm1);
+    u32x4 nxp = bld4(rP, jo * 16);
+    uint32_t nxk = bld(rK, jo * 4), nxe = bld(rE, jo * 4);
     const uint64_t lt = lanemask_lt();
     const uint32_t nchunks = (n + BS - 1) / BS;
     auto step = [&](uint32_t ci, Stage& cur, Stage& prv) {
@@ -763,22 +765,33 @@ __global__ __launch_bounds__(SlabLds<DENSE>::BS) void k_slab(SlabParams P) {
         uint32_t* claim = S.claim[par];
         const uint32_t j = ci * BS + tid;
         const bool valid = j < n;
-        const float x = nxx, y = nxy, z = nxz;
-        const uint32_t c = nxc, k = nxk, eb = max(nxe, sb);
-        jo = min(j + BS, nm1) * 4;   // prefetch chunk i+1 (clamped)
-        nxx = __uint_as_float(bld(rX, jo)); nxy = __uint_as_float(bld(rY, jo)); nxz = __uint_as_float(bld(rZ, jo));
-        nxc = bld(rC, jo); nxk = bld(rK, jo); nxe = bld(rE, jo);
-        // ---- phase A (1): slot + distance of chunk i (hex.rs:67-85, 55-65)
+        const float x = __uint_as_float(nxp.x), y = __uint_as_float(nxp.y), z = __uint_as_float(nxp.z);
+        const uint32_t c = nxp.w, k = nxk, eb = max(nxe, sb);
+        jo = min(j + BS, nm1);   // prefetch chunk i+1 (clamped)
+        nxp = bld4(rP, jo * 16);
+        nxk = bld(rK, jo * 4); nxe = bld(rE, jo * 4);
+        // ---- phase A (1): slot + distance (hex.rs:67-85, 55-65) + own child slab
         const I3 sl = hex_from_world_fast(x, y, z, G);
         const int32_t lx = sl.x - rx, ly = sl.y - ry;
         const bool layer_ok = sl.z == t;
         const bool range_ok = lx >= 0 && ly >= 0 && lx < P.tx && ly < P.ty;
         err |= (valid && !layer_ok) ? (uint32_t)ERR_LAYER : ((valid && !range_ok) ? (uint32_t)ERR_SLOT_RANGE : 0u);
-        bool pending = valid && layer_ok && range_ok && !(P.ablate & 2);
+        bool pending = valid && layer_ok && range_ok;
         const uint32_t local = pending ? (uint32_t)(ly * P.tx + lx) : 0u;
         float X, Y, Z;
         hex_to_world(sl, G.cr, X, Y, Z);
         const float d2 = dist2(X, Y, Z, x, y, z);
+        uint32_t dn;
+        int32_t gn;
+        {
+            int32_t ix, iy, iz, u, jx, jy, jz, v;
+            uint32_t rerr = 0, gerr = 0;
+            const int d = route_fast(G.csc, G.inv_csc, G.crc, G.inv_crc, cx, cy, cz, t, x, y, z, ix, iy, iz, u, rerr);
+            gn = route_fast(G.csg, G.inv_csg, G.crg, G.inv_crg, ix, iy, iz, u, x, y, z, jx, jy, jz, v, gerr);
+            if (valid) err |= rerr | ((P.check_gchild && d >= 0) ? gerr : 0u);
+            dn = d < 0 ? 0u : (uint32_t)d;
+            if (d < 0) gn = -1;
+        }
         int e = 0, hc = -1;
         if (pending) {
             e = slot_entry<DENSE>(S, local);
@@ -790,27 +803,9 @@ __global__ __launch_bounds__(SlabLds<DENSE>::BS) void k_slab(SlabParams P) {
             if ((tid & 63) == 0 && np) atomicAdd(&S.npend[par], np);
         }
         STAMP(1);
-        // ---- phase A (2): routing + wave ranks of chunk i-1 (stage prv)
-        const bool disp = prv.em >= 0 && (uint32_t)prv.em != prv.j;
-        const float ex = disp ? prv.ox : prv.x, ey = disp ? prv.oy : prv.y, ez = disp ? prv.oz : prv.z;
-        const uint32_t ec = disp ? prv.oc : prv.c;
-        int d, d2i;
-        {
-            int32_t ix, iy, iz, u;
-            uint32_t rerr = 0;
-            d = route_fast(G.csc, G.inv_csc, G.crc, G.inv_crc, cx, cy, cz, t, ex, ey, ez, ix, iy, iz, u, rerr);
-            int32_t jx, jy, jz, v;
-            uint32_t gerr = 0;
-            d2i = route_fast(G.csg, G.inv_csg, G.crg, G.inv_crg, ix, iy, iz, u, ex, ey, ez, jx, jy, jz, v, gerr);
-            if (prv.em >= 0) {
-                err |= rerr;
-                if (P.check_gchild && d >= 0) err |= gerr;
-            } else {
-                d = -1;
-            }
-            if (d < 0) d2i = -1;
-        }
-        const bool vd = d >= 0;
+        // ---- phase A (2): wave ranks of chunk i-1's emissions per child slab
+        const bool vd = prv.em >= 0;
+        const int d = vd ? (int)prv.d : 0;
         uint64_t same = __ballot(vd);
 #pragma unroll
         for (int b = 0; b < 5; b++) {
@@ -819,15 +814,16 @@ __global__ __launch_bounds__(SlabLds<DENSE>::BS) void k_slab(SlabParams P) {
         }
         const uint32_t rw = __popcll(same & lt);
         if (vd && rw == 0) S.wcnt[wv][d] = (uint32_t)__popcll(same);
-        {   // grandchild capacities: one LDS add per distinct (d, d2i) in the wave
-            const bool vg = vd && d2i >= 0;
+        {   // grandchild capacities of self emissions: one LDS add per distinct (d, g) in the wave
+            const bool vg = vd && prv.em == 0 && prv.g >= 0;
+            const int32_t gg = vg ? prv.g : 0;
             uint64_t sg = same & __ballot(vg);
 #pragma unroll
             for (int b = 0; b < 5; b++) {
-                const uint64_t bb = __ballot(vg && ((d2i >> b) & 1));
-                sg &= ((d2i >> b) & 1) ? bb : ~bb;
+                const uint64_t bb = __ballot(vg && ((gg >> b) & 1));
+                sg &= ((gg >> b) & 1) ? bb : ~bb;
             }
-            if (vg && __popcll(sg & lt) == 0) atomicAdd(&S.gcnt[d * kDests + d2i], (uint32_t)__popcll(sg));
+            if (vg && __popcll(sg & lt) == 0) atomicAdd(&S.gcnt[d * kDests + gg], (uint32_t)__popcll(sg));
         }
         STAMP(2);
         lds_barrier();
@@ -839,22 +835,30 @@ __global__ __launch_bounds__(SlabLds<DENSE>::BS) void k_slab(SlabParams P) {
             for (int q = 0; q < NW; q++) { const uint32_t cc = S.wcnt[q][tid]; S.wpre[q][tid] = acc; acc += cc; S.wcnt[q][tid] = 0; }
             S.dcur[tid] = acc;
         }
-        // cell.rs:70-94 replayed in key order: per round, the earliest pending
-        // arrival of every slot (min thread index = min key) is applied.
+        // per round, the earliest pending arrival of every slot (min thread index
+        // = min key) is applied
         int32_t em = -1;
+        uint32_t emj = 0, emd = 0;
+        bool rec = false;
         bool first = true;
         for (;;) {
             bool won = false;
             if (pending && (claim[hc] & kClaimDone) == tid) {
                 const unsigned long long occ = S.tab[e];
-                const unsigned long long mine = ((unsigned long long)f2u(d2) << 32) | j;
+                const unsigned long long mine =
+                    ((unsigned long long)f2u(d2) << 33) | ((unsigned long long)dn << kJBits) | j;
                 if (occ == kEmpty64) {
                     S.tab[e] = mine;
-                } else if (d2 < __uint_as_float((uint32_t)(occ >> 32))) {  // strict: ties keep the old point
+                    rec = true;
+                } else if (d2 < __uint_as_float((uint32_t)(occ >> 33))) {  // strict: ties keep the old point
                     S.tab[e] = mine;
-                    em = (int32_t)(uint32_t)occ;   // displaced occupant, emitted at this arrival's key
+                    rec = true;
+                    em = 1;                                // displaced occupant, emitted at this arrival's key
+                    emj = (uint32_t)occ & kJMask;
+                    emd = (uint32_t)(occ >> kJBits) & 31u;
                 } else {
-                    em = (int32_t)j;               // the arrival itself overflows
+                    em = 0;                                // the arrival itself overflows
+                    emd = dn;
                 }
                 pending = false;
                 won = true;
@@ -870,13 +874,17 @@ __global__ __launch_bounds__(SlabLds<DENSE>::BS) void k_slab(SlabParams P) {
             STAMP(5);
             if (first) {   // chunk i-1: stores into its child slabs (positions from phase B)
                 first = false;
-                const int dd = vd ? d : 0;
-                const uint32_t r = S.wpre[wv][dd] + rw;
-                const bool ok = vd && r < S.dcap[dd];
+                const uint32_t r = S.wpre[wv][d] + rw;
+                const bool ok = vd && r < S.dcap[d];
                 err |= (vd && !ok) ? (uint32_t)ERR_CAPACITY : 0u;
-                const uint32_t po = ok ? (S.doff[dd] + r) * 4 : 0xFFFFFFFFu;
-                bst(oX, po, __float_as_uint(ex)); bst(oY, po, __float_as_uint(ey)); bst(oZ, po, __float_as_uint(ez));
-                bst(oC, po, ec); bst(oK, po, prv.k); bst(oE, po, prv.e);
+                const uint32_t pos = S.doff[d] + r;
+                const uint32_t po = ok ? pos * 4 : 0xFFFFFFFFu;
+                const uint32_t ps = (ok && prv.em == 0) ? pos * 16 : 0xFFFFFFFFu;
+                u32x4 rec;
+                rec.x = __float_as_uint(prv.x); rec.y = __float_as_uint(prv.y); rec.z = __float_as_uint(prv.z); rec.w = prv.c;
+                bst4(oP, ps, rec);
+                bst(oK, po, prv.k); bst(oE, po, prv.e);
+                bst(rF, (ok && prv.em == 1) ? prv.jo * 4 : 0xFFFFFFFFu, pos);
                 STAMP(6);
             }
             if (S.npend[par] == 0) break;
@@ -886,13 +894,9 @@ __global__ __launch_bounds__(SlabLds<DENSE>::BS) void k_slab(SlabParams P) {
             STAMP(5);
         }
         if (hc >= 0) claim[hc] = kEmpty32;   // this buffer is next used two chunks later
-        if (P.ablate & 1) em = -1;
-        if (P.ablate & 4) em = em >= 0 ? (int32_t)j : em;
-        // chunk i -> stage `cur`; its occupant loads are consumed one step later
-        cur.em = em; cur.j = j; cur.k = k; cur.e = eb; cur.c = c; cur.x = x; cur.y = y; cur.z = z;
-        const uint32_t so = ((em >= 0 && (uint32_t)em != j) ? (uint32_t)em : min(j, nm1)) * 4;
-        cur.ox = __uint_as_float(bld(rX, so)); cur.oy = __uint_as_float(bld(rY, so));
-        cur.oz = __uint_as_float(bld(rZ, so)); cur.oc = bld(rC, so);
+        // status: table entry + 1 of every arrival that became a slot record
+        bst16(rS, valid ? j * 2 : 0xFFFFFFFFu, rec ? (uint32_t)e + 1u : 0u);
+        cur.em = em; cur.g = gn; cur.jo = emj; cur.d = emd; cur.k = k; cur.e = eb; cur.c = c; cur.x = x; cur.y = y; cur.z = z;
         STAMP(7);
         STAMP_COUNT(10, 1);
     };
@@ -901,37 +905,65 @@ __global__ __launch_bounds__(SlabLds<DENSE>::BS) void k_slab(SlabParams P) {
         step(ci, A, B);
         step(ci + 1, B, A);
     }
-    __syncthreads();
-    // winners -> this slab's grid region (capacity n; order inside a cell is free:
-    // cell.rs:158-160 HashMap order).  All gathers of a thread are issued before
-    // any store so their latencies overlap.
-    constexpr int WPT = (TAB + BS - 1) / BS;
+    STAMP(7);
+    __syncthreads();   // also orders this workgroup's status/fate stores before pass 2 reads them
+    STAMP(11);
+
+    // ---- pass 2: stream the slab's arrivals once.  A record whose table entry
+    // still holds it is this slab's grid point (cell.rs:158-160: order inside a
+    // cell is free); any other record was displaced, and its payload goes to the
+    // emission position stored in fate[].
+    constexpr int U = 4;
     const __amdgpu_buffer_rsrc_t rG = srd(P.grid + P.grid_off[s], (uint64_t)n * 16);
-    uint32_t wj[WPT], wpos[WPT];
+    for (uint32_t j0 = 0; j0 < n; j0 += U * BS) {
+        uint32_t st[U];
 #pragma unroll
-    for (int r = 0; r < WPT; r++) {
-        const int i = r * BS + (int)tid;
-        const unsigned long long en = i < TAB ? S.tab[i] : kEmpty64;
-        const bool occ = en != kEmpty64;
-        wj[r] = occ ? (uint32_t)en : 0u;
-        const uint64_t m = __ballot(occ);
-        uint32_t wb = 0;
-        if ((tid & 63) == 0 && m) wb = atomicAdd(&S.nwin, (uint32_t)__popcll(m));
-        wb = __shfl(wb, 0, 64);
-        wpos[r] = occ ? (wb + (uint32_t)__popcll(m & lt)) * 16 : 0xFFFFFFFFu;
-    }
-    uint32_t wx[WPT], wy[WPT], wz[WPT], wc[WPT];
+        for (int u = 0; u < U; u++) {
+            const uint32_t j = j0 + u * BS + tid;
+            st[u] = bld16(rS, j < n ? j * 2 : 0xFFFFFFFFu);
+        }
+        uint32_t wpos[U], fpos[U], src[U];
 #pragma unroll
-    for (int r = 0; r < WPT; r++) {
-        const uint32_t jo2 = min(wj[r], nm1) * 4;
-        wx[r] = bld(rX, jo2); wy[r] = bld(rY, jo2); wz[r] = bld(rZ, jo2); wc[r] = bld(rC, jo2);
-    }
+        for (int u = 0; u < U; u++) {
+            const uint32_t j = j0 + u * BS + tid;
+            bool win = false, dsp = false;
+            if (st[u]) {
+                const unsigned long long occ = S.tab[st[u] - 1];
+                win = ((uint32_t)occ & kJMask) == j;
+                dsp = !win;
+            }
+            const uint64_t m = __ballot(win);
+            uint32_t wb = 0;
+            if ((tid & 63) == 0 && m) wb = atomicAdd(&S.nwin, (uint32_t)__popcll(m));
+            wb = __shfl(wb, 0, 64);
+            wpos[u] = win ? (wb + (uint32_t)__popcll(m & lt)) * 16 : 0xFFFFFFFFu;
+            fpos[u] = dsp ? 0u : 0xFFFFFFFFu;
+            src[u] = (win || dsp) ? j : 0xFFFFFFFFu;
+        }
+        uint32_t fp[U];
+        u32x4 pv[U];
 #pragma unroll
-    for (int r = 0; r < WPT; r++) {
-        __builtin_amdgcn_raw_buffer_store_b32(wx[r], rG, wpos[r], 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b32(wy[r], rG, wpos[r] == 0xFFFFFFFFu ? wpos[r] : wpos[r] + 4, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b32(wz[r], rG, wpos[r] == 0xFFFFFFFFu ? wpos[r] : wpos[r] + 8, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b32(wc[r], rG, wpos[r] == 0xFFFFFFFFu ? wpos[r] : wpos[r] + 12, 0, 0);
+        for (int u = 0; u < U; u++) {
+            fp[u] = bld(rF, fpos[u] == 0u ? src[u] * 4 : 0xFFFFFFFFu);
+            pv[u] = bld4(rP, src[u] == 0xFFFFFFFFu ? 0xFFFFFFFFu : src[u] * 16);
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            bst4(rG, wpos[u], pv[u]);
+            bst4(oP, fpos[u] == 0u ? fp[u] * 16 : 0xFFFFFFFFu, pv[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {   // grandchild capacities of displaced emissions
+            if (fpos[u] == 0u) {
+                const float x = __uint_as_float(pv[u].x), y = __uint_as_float(pv[u].y), z = __uint_as_float(pv[u].z);
+                int32_t ix, iy, iz, uu, jx, jy, jz, v;
+                uint32_t rerr = 0, gerr = 0;
+                const int d = route_fast(G.csc, G.inv_csc, G.crc, G.inv_crc, cx, cy, cz, t, x, y, z, ix, iy, iz, uu, rerr);
+                const int g = route_fast(G.csg, G.inv_csg, G.crg, G.inv_crg, ix, iy, iz, uu, x, y, z, jx, jy, jz, v, gerr);
+                err |= rerr | ((P.check_gchild && d >= 0) ? gerr : 0u);
+                if (d >= 0 && g >= 0) atomicAdd(&S.gcnt[d * kDests + g], 1u);
+            }
+        }
     }
     STAMP(8);
     STAMP_FLUSH(P.stamps);
@@ -948,6 +980,53 @@ __global__ __launch_bounds__(SlabLds<DENSE>::BS) void k_slab(SlabParams P) {
         const int dd = i / kDests;
         if (S.dcur[dd]) P.gcap[(uint64_t)s * kDests * kDests + i] = S.gcnt[i];
     }
+}
+
+// Capacities of the level-0 slabs: arrivals per child slab (24 per slab), one
+// streaming pass over the level's arena.  Grid (nslabs, Y): block (s, y) takes
+// arrivals y*256 + tid, stride Y*256.
+struct DcapParams {
+    Arena A;
+    const int32_t* cell_idx;
+    const uint32_t* slab_cell;
+    const int32_t* slab_layer;
+    const uint32_t* slab_off;
+    const uint32_t* slab_n;
+    uint32_t* dcap;
+    Counters* ctr;
+    float csc, inv_csc, crc, inv_crc;   // child level cell size / hex radius
+    uint32_t check;                     // routing errors only matter if the child level can exist
+};
+__global__ __launch_bounds__(256) void k_dcap(DcapParams P) {
+    __shared__ uint32_t cnt[kDests];
+    const uint32_t s = blockIdx.x;
+    const uint32_t off = P.slab_off[s], n = P.slab_n[s];
+    const uint32_t j0 = blockIdx.y * 256;
+    if (j0 >= n) return;
+    if (threadIdx.x < kDests) cnt[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t cr_ = P.slab_cell[s];
+    const int32_t t = P.slab_layer[s];
+    const int32_t cx = P.cell_idx[3 * cr_], cy = P.cell_idx[3 * cr_ + 1], cz = P.cell_idx[3 * cr_ + 2];
+    uint32_t err = 0;
+    uint32_t loc[kDests] = {};
+    const uint32_t stride = gridDim.y * 256;
+    for (uint32_t j = j0 + threadIdx.x; j < n; j += stride) {
+        int32_t ix, iy, iz, u;
+        const float4 v = P.A.p[off + j];
+        const int d = route_fast(P.csc, P.inv_csc, P.crc, P.inv_crc, cx, cy, cz, t, v.x, v.y, v.z, ix, iy, iz, u, err);
+#pragma unroll
+        for (int q = 0; q < kDests; q++) loc[q] += (q == d);
+    }
+#pragma unroll
+    for (int q = 0; q < kDests; q++) {
+        uint32_t v = loc[q];
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+        if ((threadIdx.x & 63) == 0 && v) atomicAdd(&cnt[q], v);
+    }
+    if (err && P.check) set_err(P.ctr, err);
+    __syncthreads();
+    if (threadIdx.x < kDests && cnt[threadIdx.x]) atomicAdd(&P.dcap[s * kDests + threadIdx.x], cnt[threadIdx.x]);
 }
 
 // ------------------------------------------------------------------ bucket resolution
@@ -1062,7 +1141,7 @@ __global__ __launch_bounds__(kBktBS) void k_bucket(BucketParams B) {
             }
         for (uint32_t i = threadIdx.x; i < tot; i += kBktBS) {
             const uint32_t o = spos[i];
-            const float4 v = make_float4(B.nx.x[o], B.nx.y[o], B.nx.z[o], __uint_as_float(B.nx.c[o]));
+            const float4 v = B.nx.p[o];
             reinterpret_cast<float4*>(B.kept)[s_off + i] = v;
         }
         if (threadIdx.x == 0) { B.bkt_state[b] = 1; B.bkt_off[b] = s_off; B.bkt_n[b] = tot; B.bkt_nd[b] = 0; B.bkt_sb[b] = 0; }
@@ -1125,7 +1204,7 @@ struct NextParams {
 
 __global__ __launch_bounds__(256) void k_next_emit(NextParams Q) {
     __shared__ uint32_t lds[256 / 64 + 1];
-    __shared__ uint32_t carry, s_big, s_small, s_bigbase, s_smallbase;
+    __shared__ uint32_t carry, s_big, s_small, s_bigbase, s_smallbase, s_max;
     __shared__ unsigned long long s_arr;
     const uint32_t b = blockIdx.x;
     if (Q.bkt_state[b] != 2) return;
@@ -1142,6 +1221,7 @@ __global__ __launch_bounds__(256) void k_next_emit(NextParams Q) {
         s_big = 0;
         s_small = 0;
         s_arr = 0;
+        s_max = 0;
     }
     __syncthreads();
     const uint32_t s0 = Q.cell_slab0[cell], s1 = Q.cell_slab0[cell + 1];
@@ -1153,10 +1233,12 @@ __global__ __launch_bounds__(256) void k_next_emit(NextParams Q) {
         if (n) {
             atomicAdd(n >= kSmallMax ? &s_big : &s_small, 1u);
             atomicAdd(&s_arr, (unsigned long long)n);
+            atomicMax(&s_max, n);
         }
     }
     __syncthreads();
     if (threadIdx.x == 0) {
+        if (s_max) atomicMax(&Q.ctr->max_slab, s_max);
         s_bigbase = s_big ? atomicAdd(&Q.ctr->nbig, s_big) : 0;
         s_smallbase = s_small ? atomicAdd(&Q.ctr->nsmall, s_small) : 0;
         if (s_arr) atomicAdd(&Q.ctr->arrivals_next, s_arr);
@@ -1287,9 +1369,10 @@ void Engine::free_all() {
     levels_.clear();
     if (dev_) {
         for (int a = 0; a < 2; a++) {
-            (void)hipFree(dev_->ar[a].x); (void)hipFree(dev_->ar[a].y); (void)hipFree(dev_->ar[a].z);
-            (void)hipFree(dev_->ar[a].c); (void)hipFree(dev_->ar[a].k); (void)hipFree(dev_->ar[a].e);
+            (void)hipFree(dev_->ar[a].p); (void)hipFree(dev_->ar[a].k); (void)hipFree(dev_->ar[a].e);
         }
+        (void)hipFree(dev_->fate);
+        (void)hipFree(dev_->status);
         (void)hipFree(dev_->ctr);
         (void)hipFree(dev_->bbox_part);
         (void)hipFree(dev_->bbox_flag);
@@ -1423,10 +1506,12 @@ int Engine::build() {
     if (dev_->cap < n_) {
         for (int a = 0; a < 2; a++) {
             Arena& A = dev_->ar[a];
-            (void)hipFree(A.x); (void)hipFree(A.y); (void)hipFree(A.z); (void)hipFree(A.c); (void)hipFree(A.k); (void)hipFree(A.e);
-            HIP_CHECK(hipMalloc(&A.x, n_ * 4)); HIP_CHECK(hipMalloc(&A.y, n_ * 4)); HIP_CHECK(hipMalloc(&A.z, n_ * 4));
-            HIP_CHECK(hipMalloc(&A.c, n_ * 4)); HIP_CHECK(hipMalloc(&A.k, n_ * 4)); HIP_CHECK(hipMalloc(&A.e, n_ * 4));
+            (void)hipFree(A.p); (void)hipFree(A.k); (void)hipFree(A.e);
+            HIP_CHECK(hipMalloc(&A.p, n_ * 16)); HIP_CHECK(hipMalloc(&A.k, n_ * 4)); HIP_CHECK(hipMalloc(&A.e, n_ * 4));
         }
+        (void)hipFree(dev_->fate); (void)hipFree(dev_->status);
+        HIP_CHECK(hipMalloc(&dev_->fate, n_ * 4));
+        HIP_CHECK(hipMalloc(&dev_->status, n_ * 2));
         dev_->cap = n_;
     }
     // file table for event batches
@@ -1547,7 +1632,7 @@ int Engine::level0_bin() {
             default: l0_pass<8>(p, passes, d_in_, keyed_ ? d_keys_ : nullptr, src, dst, n_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, (uint32_t)file_start_.size(), dev_->scan, stream_); break;
         }
         src = dst;
-        dst = (dst.x == A0.x) ? A1 : A0;
+        dst = (dst.p == A0.p) ? A1 : A0;
     }
     // slab / cell tables from the dense histogram
     k_l0_flags<<<grid_for(std::max<uint64_t>(D, G), 256, 1u << 30), 256, 0, stream_>>>(hist, (uint32_t)D, P.nl, sflag, cflag, (uint32_t)G);
@@ -1587,10 +1672,8 @@ int Engine::level0_bin() {
     {
         HIP_CHECK(hipMemcpyAsync(&hc, dev_->ctr, sizeof hc, hipMemcpyDeviceToHost, stream_));
         HIP_CHECK(hipStreamSynchronize(stream_));
-        const uint32_t maxn = hc.max_slab;   // largest level-0 slab bounds the chunk grid
-        HIP_CHECK(hipMemsetAsync(L->dcap, 0, (uint64_t)L->nslabs * kDests * 4, stream_));
-        dim3 gd(L->nslabs, (maxn + kDcapChunk - 1) / kDcapChunk);
-        k_l0_dcap<<<gd, 256, 0, stream_>>>(A0, P, L->cell_idx, L->slab_cell, L->slab_layer, L->slab_off, L->slab_n, L->dcap, dev_->ctr);
+        L->max_slab = hc.max_slab;
+        run_dcap(L);
     }
     HIP_CHECK(hipGetLastError());
     ev_end(ST_L0);
@@ -1603,6 +1686,30 @@ int Engine::level0_bin() {
     stats_.slabs += L->nslabs;
     stats_.arrivals += n_;
     return 0;
+}
+
+// capacities (arrivals per child slab) of level L's slabs
+void Engine::run_dcap(Level* L) {
+    const float csc = cell_size(cfg_.max_cell_size, L->h + 1);
+    DcapParams D;
+    D.A = dev_->ar[L->arena];
+    D.cell_idx = L->cell_idx;
+    D.slab_cell = L->slab_cell;
+    D.slab_layer = L->slab_layer;
+    D.slab_off = L->slab_off;
+    D.slab_n = L->slab_n;
+    D.dcap = L->dcap;
+    D.ctr = dev_->ctr;
+    D.csc = csc;
+    D.inv_csc = 1.0f / csc;
+    D.crc = hex_radius(sub_cell_size(csc, cfg_.sub_grid_dimension));
+    D.inv_crc = 1.0f / D.crc;
+    D.check = (L->h + 1 < kMaxDepth) ? 1u : 0u;
+    HIP_CHECK(hipMemsetAsync(L->dcap, 0, (uint64_t)L->nslabs * kDests * 4, stream_));
+    // blocks of one slab: enough to cover its arrivals in <= 64 strides, at most 128
+    const uint32_t y = std::min<uint32_t>(128, std::max<uint32_t>(1, (L->max_slab + 256 * 64 - 1) / (256 * 64)));
+    if (L->nslabs) k_dcap<<<dim3(L->nslabs, y), 256, 0, stream_>>>(D);
+    HIP_CHECK(hipGetLastError());
 }
 
 int Engine::run_level(uint32_t h) {
@@ -1638,6 +1745,7 @@ int Engine::run_level(uint32_t h) {
         HIP_CHECK(hipStreamSynchronize(stream_));
         hc.kept_cur = 0;
         hc.nbig = hc.nsmall = 0;
+        hc.max_slab = 0;
         hc.arrivals_next = 0;
         HIP_CHECK(hipMemcpyAsync(dev_->ctr, &hc, sizeof hc, hipMemcpyHostToDevice, stream_));
     }
@@ -1656,7 +1764,10 @@ int Engine::run_level(uint32_t h) {
     SP.dest_off = L->dest_off;
     SP.slab_grid_n = L->slab_grid_n;
     SP.dest_n = L->dest_n;
+    SP.fate = dev_->fate;       // indexed by arena position (slab_off + j), reused by every level
+    SP.status = dev_->status;
     SP.gcap = L->gcap;
+    SP.check_gchild = (h + 2 < kMaxDepth) ? 1 : 0;
     SP.ctr = dev_->ctr;
     SP.cs = cs;
     {
@@ -1676,8 +1787,6 @@ int Engine::run_level(uint32_t h) {
     }
     SP.tx = g.tx;
     SP.ty = g.ty;
-    SP.check_gchild = (h + 2 < kMaxDepth) ? 1 : 0;
-    SP.ablate = getenv("PCC_ABLATE") ? atoi(getenv("PCC_ABLATE")) : 0;
     SP.stamps = nullptr;
 #ifdef PCC_STAMPS
     unsigned long long* stamps = static_cast<unsigned long long*>(dev_->get(2 * 12 * 8));
@@ -1733,12 +1842,13 @@ int Engine::run_level(uint32_t h) {
     {
         unsigned long long hs[24];
         HIP_CHECK(hipMemcpy(hs, stamps, sizeof hs, hipMemcpyDeviceToHost));
-        const char* nm[12] = {"prologue", "slotA", "routeA", "B0wait", "rounds", "rndwait", "stores", "occload",
-                              "winners", "#rounds", "#steps", "-"};
+        const char* nm[12] = {"prologue", "slotA", "routeA", "B0wait", "rounds", "rndwait", "stores", "tail",
+                              "pass2", "#rounds", "#steps", "p2sync"};
         for (int v = 0; v < 2; v++) {
             if (!hs[12 * v + 10]) continue;
             fprintf(stderr, "[stamps] level %u %s waves*steps=%llu  cycles/step:", h, v ? "small" : "dense", hs[12 * v + 10]);
-            for (int q = 0; q < 9; q++) fprintf(stderr, " %s=%.0f", nm[q], (double)hs[12 * v + q] / hs[12 * v + 10]);
+            for (int q = 0; q < 12; q++)
+                if (q != 9 && q != 10) fprintf(stderr, " %s=%.0f", nm[q], (double)hs[12 * v + q] / hs[12 * v + 10]);
             fprintf(stderr, " rounds/step=%.2f\n", (double)hs[12 * v + 9] / hs[12 * v + 10]);
         }
     }
@@ -1754,7 +1864,8 @@ int Engine::run_level(uint32_t h) {
     if (hc.err) {
         char buf[200];
         snprintf(buf, sizeof buf,
-                 "device error flags 0x%x at level %u (1 slot range, 2 layer, 4 octant, 8 sel, 16 kept cap, 64 capacity, 128 claim)",
+                 "device error flags 0x%x at level %u (1 slot range, 2 layer, 4 octant, 8 sel, 16 kept cap, 64 capacity, "
+                 "128 claim, 256 slab > 2^28 arrivals)",
                  hc.err, h);
         return fail(-5, buf);
     }
@@ -1787,6 +1898,7 @@ int Engine::run_level(uint32_t h) {
         Q.dest_off = L->dest_off;
         Q.dest_n = L->dest_n;
         Q.gcap = L->gcap;
+        Q.ndcap = N->dcap;
         Q.ncell_idx = N->cell_idx;
         Q.ncell_sb = N->cell_sb;
         Q.ncell_slab0 = N->cell_slab0;
@@ -1794,7 +1906,6 @@ int Engine::run_level(uint32_t h) {
         Q.nslab_layer = N->slab_layer;
         Q.nslab_off = N->slab_off;
         Q.nslab_n = N->slab_n;
-        Q.ndcap = N->dcap;
         Q.nbig_list = N->big_list;
         Q.nsmall_list = N->small_list;
         Q.ctr = dev_->ctr;
@@ -1808,6 +1919,7 @@ int Engine::run_level(uint32_t h) {
         N->nbig = hc.nbig;
         N->nsmall = hc.nsmall;
         N->arrivals = hc.arrivals_next;
+        N->max_slab = hc.max_slab;
         stats_.arrivals += hc.arrivals_next;
         stats_.cells += N->ncells;
         stats_.slabs += N->nslabs;
