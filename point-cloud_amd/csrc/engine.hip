@@ -159,10 +159,10 @@ struct Engine::Level {
 // Diagnostic build only (-DPCC_STAMPS): per-wave s_memtime phase sums of the
 // slab kernel, added into P.stamps[phase]; never compiled into the product.
 #ifdef PCC_STAMPS
-#define STAMP_DECL unsigned long long st_t0 = __builtin_amdgcn_s_memtime(), st_acc[12] = {};
+#define STAMP_DECL unsigned long long st_t0 = __builtin_amdgcn_s_memtime(), st_acc[16] = {};
 #define STAMP(ph) do { const unsigned long long st_n = __builtin_amdgcn_s_memtime(); st_acc[ph] += st_n - st_t0; st_t0 = st_n; } while (0)
 #define STAMP_COUNT(ph, v) do { st_acc[ph] += (v); } while (0)
-#define STAMP_FLUSH(ptr) do { if ((threadIdx.x & 63) == 0) for (int q_ = 0; q_ < 12; q_++) atomicAdd((ptr) + q_, st_acc[q_]); } while (0)
+#define STAMP_FLUSH(ptr) do { if ((threadIdx.x & 63) == 0) for (int q_ = 0; q_ < 16; q_++) atomicAdd((ptr) + q_, st_acc[q_]); } while (0)
 #else
 #define STAMP_DECL
 #define STAMP(ph) do {} while (0)
@@ -207,32 +207,6 @@ __device__ __forceinline__ int route(float csc, float crc, int32_t cx, int32_t c
     return (bad_oct || bad_sel) ? -1 : (bx | (by << 1) | (bz << 2)) * 3 + sel;
 }
 
-// floorf(fl(a / b)) and truncf(fl(a / b)) without a full division in the common
-// case: the product with the correctly rounded reciprocal differs from the
-// correctly rounded quotient by at most ~4 ulp, so unless it lies within a
-// (16x wider) margin of an integer, both have the same floor/trunc.  Lanes near
-// an integer fall back to the exact IEEE division (wave-uniform branch guard).
-__device__ __forceinline__ float floor_div(float a, float b, float inv_b) {
-    const float q = a * inv_b;
-    const float m = (fabsf(q) * 0x1p-20f) + 0x1p-126f;
-    const bool amb = floorf(q - m) != floorf(q + m);
-    float r = floorf(q);
-    if (__ballot(amb)) {
-        if (amb) r = floorf(a / b);
-    }
-    return r;
-}
-__device__ __forceinline__ float trunc_div(float a, float b, float inv_b) {
-    const float q = a * inv_b;
-    const float m = (fabsf(q) * 0x1p-20f) + 0x1p-126f;
-    const bool amb = truncf(q - m) != truncf(q + m);
-    float r = truncf(q);
-    if (__ballot(amb)) {
-        if (amb) r = truncf(a / b);
-    }
-    return r;
-}
-
 // Per-level constants for the slot / routing arithmetic (all computed on the
 // host with the reference's own f32 formulas; see pcc_math.h).
 struct LevelGeo {
@@ -241,34 +215,86 @@ struct LevelGeo {
     float csg, inv_csg, crg, inv_crg;    // grandchild level
 };
 
-// hex.rs:67-85 + 45-51 with the floor/trunc-only divisions done by floor_div.
-__device__ __forceinline__ I3 hex_from_world_fast(float px, float py, float pz, const LevelGeo& G) {
+// floorf(fl(a / b)) and truncf(fl(a / b)) without a full division in the common
+// case: the product with the correctly rounded reciprocal differs from the
+// correctly rounded quotient by at most ~4 ulp, so unless it lies within a
+// (16x wider) margin of an integer, both have the same floor/trunc.  Lanes near
+// an integer are recomputed with the exact IEEE division.
+// Same quotients with the ambiguity test only accumulated: callers OR the flags
+// of all their divisions and resolve flagged lanes with exact IEEE divisions
+// behind ONE wave-uniform branch (one ballot per point instead of one per
+// division).
+__device__ __forceinline__ float floor_q(float a, float inv_b, bool& amb) {
+    const float q = a * inv_b;
+    const float m = (fabsf(q) * 0x1p-20f) + 0x1p-126f;
+    amb |= floorf(q - m) != floorf(q + m);
+    return floorf(q);
+}
+__device__ __forceinline__ float trunc_q(float a, float inv_b, bool& amb) {
+    const float q = a * inv_b;
+    const float m = (fabsf(q) * 0x1p-20f) + 0x1p-126f;
+    amb |= truncf(q - m) != truncf(q + m);
+    return truncf(q);
+}
+__device__ __forceinline__ I3 hex_q(float px, float py, float pz, const LevelGeo& G, bool& amb) {
     const float x = px / G.crx;
     const float y = py / G.cry;
     const float t = (kSqrt3 * y) + 1.0f;
     const float t1 = floorf(t + x);
     const float t2 = t - x;
     const float t3 = (2.0f * x) + 1.0f;
-    const int32_t q = sat_i32(floor_div(t1 + t3, 3.0f, 0x1.555556p-2f));
-    const int32_t r = (int32_t)(0u - (uint32_t)sat_i32(floor_div(t1 + t2, 3.0f, 0x1.555556p-2f)));
-    const int32_t h = sat_i32(trunc_div(pz, G.cr, G.inv_cr));
+    const int32_t q = sat_i32(floor_q(t1 + t3, 0x1.555556p-2f, amb));
+    const int32_t r = (int32_t)(0u - (uint32_t)sat_i32(floor_q(t1 + t2, 0x1.555556p-2f, amb)));
+    const int32_t h = sat_i32(trunc_q(pz, G.inv_cr, amb));
     I3 o = {q + (r - (r & 1)) / 2, r, h};
     return o;
 }
-
-__device__ __forceinline__ int route_fast(float cs, float inv_cs, float cr, float inv_cr, int32_t cx, int32_t cy,
-                                          int32_t cz, int32_t t, float x, float y, float z, int32_t& ix,
-                                          int32_t& iy, int32_t& iz, int32_t& u, uint32_t& err) {
-    ix = sat_i32(floor_div(x, cs, inv_cs));
-    iy = sat_i32(floor_div(y, cs, inv_cs));
-    iz = sat_i32(floor_div(z, cs, inv_cs));
-    u = sat_i32(trunc_div(z, cr, inv_cr));
-    const int32_t bx = ix - 2 * cx, by = iy - 2 * cy, bz = iz - 2 * cz;
-    const int32_t sel = u - 2 * t + 1;
+// child cell index and hex layer of a point at the next level (metadata.rs:100-102, hex.rs:83)
+struct RouteIdx { int32_t ix, iy, iz, u; };
+__device__ __forceinline__ RouteIdx route_idx_q(float cs, float inv_cs, float inv_cr, float x, float y, float z,
+                                               bool& amb) {
+    RouteIdx R;
+    R.ix = sat_i32(floor_q(x, inv_cs, amb));
+    R.iy = sat_i32(floor_q(y, inv_cs, amb));
+    R.iz = sat_i32(floor_q(z, inv_cs, amb));
+    R.u = sat_i32(trunc_q(z, inv_cr, amb));
+    return R;
+}
+__device__ __forceinline__ RouteIdx route_idx_exact(float cs, float cr, float x, float y, float z) {
+    RouteIdx R;
+    R.ix = cell_index1(x, cs);
+    R.iy = cell_index1(y, cs);
+    R.iz = cell_index1(z, cs);
+    R.u = sat_i32(z / cr);
+    return R;
+}
+// child slab (octant * 3 + layer select) of a point with child index R inside
+// parent cell (cx, cy, cz) / layer t; -1 (and err) if inconsistent
+__device__ __forceinline__ int route_dest(const RouteIdx& R, int32_t cx, int32_t cy, int32_t cz, int32_t t,
+                                          uint32_t& err) {
+    const int32_t bx = R.ix - 2 * cx, by = R.iy - 2 * cy, bz = R.iz - 2 * cz;
+    const int32_t sel = R.u - 2 * t + 1;
     const bool bad_oct = ((bx | by | bz) & ~1) != 0;
     const bool bad_sel = sel < 0 || sel > 2;
     err |= bad_oct ? (uint32_t)ERR_OCTANT : (bad_sel ? (uint32_t)ERR_SEL : 0u);
     return (bad_oct || bad_sel) ? -1 : (bx | (by << 1) | (bz << 2)) * 3 + sel;
+}
+// slot, child route and grandchild route of one point, one ballot for all divisions
+struct SlotRoute { I3 sl; RouteIdx rc, rg; };
+__device__ __forceinline__ SlotRoute slot_route(float x, float y, float z, const LevelGeo& G) {
+    bool amb = false;
+    SlotRoute S;
+    S.sl = hex_q(x, y, z, G, amb);
+    S.rc = route_idx_q(G.csc, G.inv_csc, G.inv_crc, x, y, z, amb);
+    S.rg = route_idx_q(G.csg, G.inv_csg, G.inv_crg, x, y, z, amb);
+    if (__ballot(amb)) {
+        if (amb) {
+            S.sl = hex_from_world(x, y, z, G.cr);
+            S.rc = route_idx_exact(G.csc, G.crc, x, y, z);
+            S.rg = route_idx_exact(G.csg, G.crg, x, y, z);
+        }
+    }
+    return S;
 }
 
 // Buffer descriptor of a wave-uniform range.  Base and size are forced into
@@ -353,11 +379,33 @@ __global__ void k_bbox_final(float* part, uint32_t nb) {
 // ------------------------------------------------------------------ level-0 binning
 struct L0Params {
     float cs, cr, csc, crc;   // level 0 and level 1 cell size / hex radius
+    float inv_cs, inv_cr;     // reciprocals for the fast floor/trunc quotients
     int32_t lo[3];
     int32_t g[3];
     int32_t nl;
     int32_t dim2;   // 2 * sub_grid_dimension
+    // sparse mode (bounding box spans > 2^20 level-0 cells): occupied cells in a
+    // hash set keyed by the packed grid offset, compact cell id instead of the
+    // dense linear index
+    int32_t hashed;
+    uint32_t hmask;
+    const unsigned long long* hkeys;
+    const uint32_t* hcid;
+    const unsigned long long* ckeys;   // packed grid offset per compact cell id
 };
+
+constexpr unsigned long long kHashEmpty = ~0ull;
+__device__ __forceinline__ unsigned long long l0_pack(int32_t gx, int32_t gy, int32_t gz) {
+    return (unsigned long long)gx | ((unsigned long long)gy << 21) | ((unsigned long long)gz << 42);
+}
+__device__ __forceinline__ uint32_t l0_hash(unsigned long long k) {
+    k ^= k >> 31;
+    k *= 0x7fb5d329728ea185ull;
+    k ^= k >> 27;
+    k *= 0x81dadef4bc2dd44dull;
+    k ^= k >> 33;
+    return (uint32_t)k;
+}
 
 // dense slab id of a point: ((cell - lo) linearised) * nl + (layer - (dim2*iz - 2));
 // ordered by (cell, layer) exactly like the compact slab ids.
@@ -367,7 +415,54 @@ __device__ __forceinline__ int64_t l0_dense(const L0Params& P, float x, float y,
     int32_t t = sat_i32(z / P.cr);   // hex.rs:83 z slot (truncation)
     int64_t ll = (int64_t)t - ((int64_t)P.dim2 * iz - 2);
     if (gx < 0 || gy < 0 || gz < 0 || gx >= P.g[0] || gy >= P.g[1] || gz >= P.g[2] || ll < 0 || ll >= P.nl) return -1;
+    if (P.hashed) {
+        const unsigned long long key = l0_pack(gx, gy, gz);
+        uint32_t h = l0_hash(key) & P.hmask;
+        for (uint32_t probe = 0; probe <= P.hmask; probe++) {
+            const unsigned long long k = P.hkeys[h];
+            if (k == key) return (int64_t)P.hcid[h] * P.nl + ll;
+            if (k == kHashEmpty) return -1;
+            h = (h + 1) & P.hmask;
+        }
+        return -1;
+    }
     return (((int64_t)gz * P.g[1] + gy) * P.g[0] + gx) * P.nl + ll;
+}
+
+// sparse mode: insert every point's level-0 cell into the hash set (a plain read
+// first, so repeated cells cost no atomic); counts distinct cells
+__global__ __launch_bounds__(256) void k_l0_hash_insert(const Point* __restrict__ in, uint64_t n, L0Params P,
+                                                        unsigned long long* hkeys, uint32_t* count, uint32_t* bad) {
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+        const float4 v = reinterpret_cast<const float4*>(in)[i];
+        const int32_t gx = cell_index1(v.x, P.cs) - P.lo[0], gy = cell_index1(v.y, P.cs) - P.lo[1];
+        const int32_t gz = cell_index1(v.z, P.cs) - P.lo[2];
+        if (gx < 0 || gy < 0 || gz < 0 || gx >= P.g[0] || gy >= P.g[1] || gz >= P.g[2]) { atomicOr(bad, 1u); continue; }
+        const unsigned long long key = l0_pack(gx, gy, gz);
+        uint32_t h = l0_hash(key) & P.hmask;
+        uint32_t probe = 0;
+        for (; probe <= P.hmask; probe++) {
+            unsigned long long k = hkeys[h];
+            if (k == kHashEmpty) {
+                k = atomicCAS(&hkeys[h], kHashEmpty, key);
+                if (k == kHashEmpty) { atomicAdd(count, 1u); break; }
+            }
+            if (k == key) break;
+            h = (h + 1) & P.hmask;
+        }
+        if (probe > P.hmask) atomicOr(bad, 2u);   // table full: the host grows it and retries
+    }
+}
+
+// compact ids of the occupied hash entries
+__global__ void k_l0_hash_flags(const unsigned long long* hkeys, uint32_t cap, uint32_t* flag) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < cap) flag[i] = hkeys[i] != kHashEmpty ? 1u : 0u;
+}
+__global__ void k_l0_hash_ids(const unsigned long long* hkeys, uint32_t cap, uint32_t* hcid,
+                              unsigned long long* ckeys) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < cap && hkeys[i] != kHashEmpty) ckeys[hcid[i]] = hkeys[i];
 }
 
 constexpr int kL0BS = 256, kL0IPT = 8, kL0Tile = kL0BS * kL0IPT, kL0W = kL0BS / 64;
@@ -549,9 +644,17 @@ __global__ void k_l0_tables(const uint32_t* hist, const uint32_t* cnt_scan, cons
     const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
     if (d < G && cflag[d]) {
         const uint32_t r = cflag_scan[d];
-        const int32_t gx = (int32_t)(d % (uint32_t)P.g[0]);
-        const int32_t gy = (int32_t)((d / (uint32_t)P.g[0]) % (uint32_t)P.g[1]);
-        const int32_t gz = (int32_t)(d / ((uint32_t)P.g[0] * (uint32_t)P.g[1]));
+        int32_t gx, gy, gz;
+        if (P.hashed) {
+            const unsigned long long key = P.ckeys[d];
+            gx = (int32_t)(key & 0x1FFFFF);
+            gy = (int32_t)((key >> 21) & 0x1FFFFF);
+            gz = (int32_t)(key >> 42);
+        } else {
+            gx = (int32_t)(d % (uint32_t)P.g[0]);
+            gy = (int32_t)((d / (uint32_t)P.g[0]) % (uint32_t)P.g[1]);
+            gz = (int32_t)(d / ((uint32_t)P.g[0] * (uint32_t)P.g[1]));
+        }
         cell_idx[3 * r] = P.lo[0] + gx;
         cell_idx[3 * r + 1] = P.lo[1] + gy;
         cell_idx[3 * r + 2] = P.lo[2] + gz;
@@ -562,7 +665,7 @@ __global__ void k_l0_tables(const uint32_t* hist, const uint32_t* cnt_scan, cons
         const uint32_t sid = sflag_scan[d];
         const uint32_t g = d / (uint32_t)P.nl;
         const int32_t ll = (int32_t)(d % (uint32_t)P.nl);
-        const int32_t gz = (int32_t)(g / ((uint32_t)P.g[0] * (uint32_t)P.g[1]));
+        const int32_t gz = P.hashed ? (int32_t)(P.ckeys[g] >> 42) : (int32_t)(g / ((uint32_t)P.g[0] * (uint32_t)P.g[1]));
         const int32_t iz = P.lo[2] + gz;
         slab_cell[sid] = cflag_scan[g];
         slab_layer[sid] = ll + (P.dim2 * iz - 2);
@@ -708,7 +811,7 @@ __global__ __launch_bounds__(SlabLds<DENSE>::BS) void k_slab(SlabParams P) {
         return;
     }
     // reference slot: the one holding the cell centre (metadata.rs:104-106)
-    const I3 c0 = hex_from_world_fast(cell_pos1(cx, P.cs), cell_pos1(cy, P.cs), cell_pos1(cz, P.cs), G);
+    const I3 c0 = hex_from_world(cell_pos1(cx, P.cs), cell_pos1(cy, P.cs), cell_pos1(cz, P.cs), G.cr);
     const int32_t rx = c0.x - P.tx / 2, ry = c0.y - P.ty / 2;
     uint32_t err = 0;
     if (tid == 0) atomicAdd(DENSE ? &P.ctr->dense_arrivals : &P.ctr->small_arrivals, (unsigned long long)n);
@@ -771,7 +874,12 @@ __global__ __launch_bounds__(SlabLds<DENSE>::BS) void k_slab(SlabParams P) {
         nxp = bld4(rP, jo * 16);
         nxk = bld(rK, jo * 4); nxe = bld(rE, jo * 4);
         // ---- phase A (1): slot + distance (hex.rs:67-85, 55-65) + own child slab
-        const I3 sl = hex_from_world_fast(x, y, z, G);
+#ifdef PCC_STAMPS
+        if (__float_as_uint(x) == 0x7FC00001u) err |= 1u << 30;   // consume the prefetched loads here
+        STAMP(12);
+#endif
+        const SlotRoute sr = slot_route(x, y, z, G);
+        const I3 sl = sr.sl;
         const int32_t lx = sl.x - rx, ly = sl.y - ry;
         const bool layer_ok = sl.z == t;
         const bool range_ok = lx >= 0 && ly >= 0 && lx < P.tx && ly < P.ty;
@@ -784,14 +892,17 @@ __global__ __launch_bounds__(SlabLds<DENSE>::BS) void k_slab(SlabParams P) {
         uint32_t dn;
         int32_t gn;
         {
-            int32_t ix, iy, iz, u, jx, jy, jz, v;
             uint32_t rerr = 0, gerr = 0;
-            const int d = route_fast(G.csc, G.inv_csc, G.crc, G.inv_crc, cx, cy, cz, t, x, y, z, ix, iy, iz, u, rerr);
-            gn = route_fast(G.csg, G.inv_csg, G.crg, G.inv_crg, ix, iy, iz, u, x, y, z, jx, jy, jz, v, gerr);
+            const int d = route_dest(sr.rc, cx, cy, cz, t, rerr);
+            gn = route_dest(sr.rg, sr.rc.ix, sr.rc.iy, sr.rc.iz, sr.rc.u, gerr);
             if (valid) err |= rerr | ((P.check_gchild && d >= 0) ? gerr : 0u);
             dn = d < 0 ? 0u : (uint32_t)d;
             if (d < 0) gn = -1;
         }
+#ifdef PCC_STAMPS
+        if (d2 == 12345.0f) err |= 1u << 29;   // finish the math before the stamp
+        STAMP(13);
+#endif
         int e = 0, hc = -1;
         if (pending) {
             e = slot_entry<DENSE>(S, local);
@@ -956,10 +1067,10 @@ __global__ __launch_bounds__(SlabLds<DENSE>::BS) void k_slab(SlabParams P) {
         for (int u = 0; u < U; u++) {   // grandchild capacities of displaced emissions
             if (fpos[u] == 0u) {
                 const float x = __uint_as_float(pv[u].x), y = __uint_as_float(pv[u].y), z = __uint_as_float(pv[u].z);
-                int32_t ix, iy, iz, uu, jx, jy, jz, v;
+                const SlotRoute sr = slot_route(x, y, z, G);
                 uint32_t rerr = 0, gerr = 0;
-                const int d = route_fast(G.csc, G.inv_csc, G.crc, G.inv_crc, cx, cy, cz, t, x, y, z, ix, iy, iz, uu, rerr);
-                const int g = route_fast(G.csg, G.inv_csg, G.crg, G.inv_crg, ix, iy, iz, uu, x, y, z, jx, jy, jz, v, gerr);
+                const int d = route_dest(sr.rc, cx, cy, cz, t, rerr);
+                const int g = route_dest(sr.rg, sr.rc.ix, sr.rc.iy, sr.rc.iz, sr.rc.u, gerr);
                 err |= rerr | ((P.check_gchild && d >= 0) ? gerr : 0u);
                 if (d >= 0 && g >= 0) atomicAdd(&S.gcnt[d * kDests + g], 1u);
             }
@@ -1012,9 +1123,13 @@ __global__ __launch_bounds__(256) void k_dcap(DcapParams P) {
     uint32_t loc[kDests] = {};
     const uint32_t stride = gridDim.y * 256;
     for (uint32_t j = j0 + threadIdx.x; j < n; j += stride) {
-        int32_t ix, iy, iz, u;
         const float4 v = P.A.p[off + j];
-        const int d = route_fast(P.csc, P.inv_csc, P.crc, P.inv_crc, cx, cy, cz, t, v.x, v.y, v.z, ix, iy, iz, u, err);
+        bool amb = false;
+        RouteIdx R = route_idx_q(P.csc, P.inv_csc, P.inv_crc, v.x, v.y, v.z, amb);
+        if (__ballot(amb)) {
+            if (amb) R = route_idx_exact(P.csc, P.crc, v.x, v.y, v.z);
+        }
+        const int d = route_dest(R, cx, cy, cz, t, err);
 #pragma unroll
         for (int q = 0; q < kDests; q++) loc[q] += (q == d);
     }
@@ -1591,19 +1706,59 @@ int Engine::level0_bin() {
     P.cr = hex_radius(sub_cell_size(cs, dim));
     P.csc = csc;
     P.crc = hex_radius(sub_cell_size(csc, dim));
+    P.inv_cs = 1.0f / P.cs;
+    P.inv_cr = 1.0f / P.cr;
     const SlabGeom g = slab_geom(dim);
     P.nl = g.nl;
     P.dim2 = 2 * (int32_t)dim;
     uint64_t G = 1;
+    bool wide = false;
+    P.hashed = 0;
+    P.hmask = 0;
+    P.hkeys = nullptr;
+    P.hcid = nullptr;
+    P.ckeys = nullptr;
     for (int a = 0; a < 3; a++) {
         P.lo[a] = cell_index1(bmin_[a], cs);
-        const int32_t hi = cell_index1(bmax_[a], cs);
-        P.g[a] = hi - P.lo[a] + 1;
-        G *= (uint64_t)P.g[a];
+        const int64_t ext = (int64_t)cell_index1(bmax_[a], cs) - P.lo[a] + 1;
+        wide |= ext > (1 << 21);
+        P.g[a] = (int32_t)std::min<int64_t>(ext, INT32_MAX);
+        G *= (uint64_t)ext;
+    }
+    if (wide)
+        return fail(-27, "level-0 cell grid too large (bounding box spans > 2^21 cells of max_cell_size on an axis)");
+    if (G > (1u << 20)) {
+        // sparse bounding box: hash set of the occupied level-0 cells, compact ids
+        P.hashed = 1;
+        uint32_t* cnt = static_cast<uint32_t*>(dev_->get(8));
+        for (uint64_t cap = 1u << 20;; cap <<= 1) {
+            if (cap > (1ull << 31)) return fail(-27, "too many occupied level-0 cells");
+            P.hmask = (uint32_t)(cap - 1);
+            unsigned long long* hk = static_cast<unsigned long long*>(dev_->get(cap * 8));
+            HIP_CHECK(hipMemsetAsync(hk, 0xFF, cap * 8, stream_));
+            HIP_CHECK(hipMemsetAsync(cnt, 0, 8, stream_));
+            k_l0_hash_insert<<<grid_for(n_, 256, 8192), 256, 0, stream_>>>(d_in_, n_, P, hk, cnt, cnt + 1);
+            HIP_CHECK(hipGetLastError());
+            uint32_t hc2[2];
+            HIP_CHECK(hipMemcpyAsync(hc2, cnt, 8, hipMemcpyDeviceToHost, stream_));
+            HIP_CHECK(hipStreamSynchronize(stream_));
+            if (hc2[1] & 1u) return fail(-34, "level-0 binning: point outside the bounding grid (internal error)");
+            if ((hc2[1] & 2u) || hc2[0] > cap * 6 / 10) continue;   // too full: grow and rebuild
+            uint32_t* hcid = static_cast<uint32_t*>(dev_->get(cap * 4));
+            k_l0_hash_flags<<<grid_for(cap, 256, 1u << 30), 256, 0, stream_>>>(hk, (uint32_t)cap, hcid);
+            scan_excl_u32(hcid, hcid, (uint32_t)cap, cnt, dev_->scan, stream_);
+            unsigned long long* ck = static_cast<unsigned long long*>(dev_->get((uint64_t)hc2[0] * 8));
+            k_l0_hash_ids<<<grid_for(cap, 256, 1u << 30), 256, 0, stream_>>>(hk, (uint32_t)cap, hcid, ck);
+            HIP_CHECK(hipGetLastError());
+            P.hkeys = hk;
+            P.hcid = hcid;
+            P.ckeys = ck;
+            G = hc2[0];
+            break;
+        }
     }
     const uint64_t D = G * (uint64_t)P.nl;
-    if (G > (1u << 20))
-        return fail(-27, "level-0 cell grid too large (bounding box spans > 2^20 cells of max_cell_size)");
+    if (D >= (1ull << 32)) return fail(-27, "too many level-0 slabs (occupied cells x hex layers >= 2^32)");
     uint32_t* hist = static_cast<uint32_t*>(dev_->get(D * 4));
     uint32_t* cnt_scan = static_cast<uint32_t*>(dev_->get(D * 4));
     uint32_t* sflag = static_cast<uint32_t*>(dev_->get(D * 4));
@@ -1789,8 +1944,8 @@ int Engine::run_level(uint32_t h) {
     SP.ty = g.ty;
     SP.stamps = nullptr;
 #ifdef PCC_STAMPS
-    unsigned long long* stamps = static_cast<unsigned long long*>(dev_->get(2 * 12 * 8));
-    HIP_CHECK(hipMemsetAsync(stamps, 0, 2 * 12 * 8, stream_));
+    unsigned long long* stamps = static_cast<unsigned long long*>(dev_->get(2 * 16 * 8));
+    HIP_CHECK(hipMemsetAsync(stamps, 0, 2 * 16 * 8, stream_));
 #endif
     if (L->nbig) {
         SP.list = L->big_list;
@@ -1804,7 +1959,7 @@ int Engine::run_level(uint32_t h) {
     if (L->nsmall) {
         SP.list = L->small_list;
 #ifdef PCC_STAMPS
-        SP.stamps = stamps + 12;
+        SP.stamps = stamps + 16;
 #endif
         ev_begin(ST_SMALL);
         k_slab<false><<<L->nsmall, kSmallBS, 0, stream_>>>(SP);
@@ -1840,16 +1995,16 @@ int Engine::run_level(uint32_t h) {
     ev_end(ST_NEXT);
 #ifdef PCC_STAMPS
     {
-        unsigned long long hs[24];
+        unsigned long long hs[32];
         HIP_CHECK(hipMemcpy(hs, stamps, sizeof hs, hipMemcpyDeviceToHost));
-        const char* nm[12] = {"prologue", "slotA", "routeA", "B0wait", "rounds", "rndwait", "stores", "tail",
-                              "pass2", "#rounds", "#steps", "p2sync"};
+        const char* nm[16] = {"prologue", "claimA", "routeA", "B0wait", "rounds", "rndwait", "stores", "tail",
+                              "pass2", "#rounds", "#steps", "p2sync", "ldwait", "math", "-", "-"};
         for (int v = 0; v < 2; v++) {
-            if (!hs[12 * v + 10]) continue;
-            fprintf(stderr, "[stamps] level %u %s waves*steps=%llu  cycles/step:", h, v ? "small" : "dense", hs[12 * v + 10]);
-            for (int q = 0; q < 12; q++)
-                if (q != 9 && q != 10) fprintf(stderr, " %s=%.0f", nm[q], (double)hs[12 * v + q] / hs[12 * v + 10]);
-            fprintf(stderr, " rounds/step=%.2f\n", (double)hs[12 * v + 9] / hs[12 * v + 10]);
+            if (!hs[16 * v + 10]) continue;
+            fprintf(stderr, "[stamps] level %u %s waves*steps=%llu  cycles/step:", h, v ? "small" : "dense", hs[16 * v + 10]);
+            for (int q = 0; q < 14; q++)
+                if (q != 9 && q != 10) fprintf(stderr, " %s=%.0f", nm[q], (double)hs[16 * v + q] / hs[16 * v + 10]);
+            fprintf(stderr, " rounds/step=%.2f\n", (double)hs[16 * v + 9] / hs[16 * v + 10]);
         }
     }
 #endif

@@ -76,6 +76,43 @@ def test_duplicates_exact_limit_chains():
     _check(files, batch=10_000, fast=True)
 
 
+def _outliers(n, lo, hi, seed):
+    rng = np.random.default_rng(seed)
+    o = np.zeros(n, dtype=POINT_DTYPE)
+    for a in "xyz":
+        o[a] = rng.uniform(lo, hi, n).astype(np.float32)
+    o["rgba"] = rng.integers(0, 256, (n, 4), dtype=np.uint8)
+    return o
+
+
+def test_sparse_bbox_far_outliers():
+    """Bounding box spanning > 2^20 level-0 cells (far outliers): the GPU build
+    switches to the hashed level-0 cell set (sparse mode)."""
+    pts = synth(51, 1, 300_000)
+    out = _outliers(64, -4.0e7, 4.0e7, 51)
+    allp = np.concatenate([pts[:150_000], out, pts[150_000:]])
+    _check([allp], fast=True)
+
+
+def test_sparse_bbox_small_cells_many_occupied():
+    """Tiny max_cell_size: ~10^6 occupied level-0 cells over a 2^30-cell box."""
+    pts = synth(52, 0, 400_000, lo=-500.0, ext=1000.0)
+    _check([pts], cfg=dict(cell_point_overflow_limit=4, sub_grid_dimension=2, max_cell_size=1.0), fast=True)
+
+
+def test_bbox_beyond_hashed_range_is_an_error():
+    """More than 2^21 level-0 cells along an axis: explicit error, no wrong output."""
+    import pcconv
+    p = _outliers(1000, -5.0e9, 5.0e9, 53)
+    with tempfile.TemporaryDirectory() as tg:
+        c = pcconv.Converter(tg)
+        c.add_points(p)
+        with pytest.raises(pcconv.PccError) as ei:
+            c.build()
+        assert ei.value.code == -27
+        c.close()
+
+
 def test_depth_limit_is_an_error():
     """More than L identical points never terminate in the reference (metadata.rs:92
     overflows 2u32.pow(h) at h = 32); the GPU build reports it instead of hanging."""
