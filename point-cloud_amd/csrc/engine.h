@@ -133,6 +133,8 @@ private:
     std::vector<hipEvent_t> ev_pool_;
     std::string err_;
     bool built_ = false;
+    uint32_t small_grid_ = 1024;         // resident workgroups of the persistent small-slab kernel
+    uint32_t wave_grid_ = 2048;          // resident one-wave workgroups of k_slab_wave
 };
 
 // ---- sharded build helpers; synchronous, on an internal stream

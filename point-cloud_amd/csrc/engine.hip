@@ -693,6 +693,10 @@ struct SlabParams {
     uint32_t* fate;       // per arrival: emission position of a displaced record (pass 1 -> pass 2)
     uint16_t* status;     // per arrival: table entry + 1 if it became a slot record, else 0
     uint32_t* gcap;       // 24 x 24 per slab: arrivals of each child slab per grandchild slab
+    const struct SmallDesc* sdesc;   // small-slab descriptors (k_slab_small)
+    uint32_t nlist;
+    const struct SmallDesc* wdesc;   // one-wave slab descriptors (k_slab_wave)
+    uint32_t nwave;
     Counters* ctr;
     float cs;
     LevelGeo G;
@@ -814,7 +818,6 @@ __global__ __launch_bounds__(SlabLds<DENSE>::BS) void k_slab(SlabParams P) {
     const I3 c0 = hex_from_world(cell_pos1(cx, P.cs), cell_pos1(cy, P.cs), cell_pos1(cz, P.cs), G.cr);
     const int32_t rx = c0.x - P.tx / 2, ry = c0.y - P.ty / 2;
     uint32_t err = 0;
-    if (tid == 0) atomicAdd(DENSE ? &P.ctr->dense_arrivals : &P.ctr->small_arrivals, (unsigned long long)n);
     // buffer descriptors: this slab's arrivals + per-arrival status/fate, and the
     // contiguous region of its 24 child slabs in the next arena (out-of-range
     // offsets drop a store)
@@ -1082,7 +1085,6 @@ __global__ __launch_bounds__(SlabLds<DENSE>::BS) void k_slab(SlabParams P) {
     __syncthreads();
     if (tid == 0) {
         P.slab_grid_n[s] = S.nwin;
-        atomicAdd(&P.ctr->grid_total, (unsigned long long)S.nwin);
         if (S.err) set_err(P.ctr, S.err);
     }
     if (tid < kDests) P.dest_n[s * kDests + tid] = S.dcur[tid] < S.dcap[tid] ? S.dcur[tid] : S.dcap[tid];
@@ -1090,6 +1092,543 @@ __global__ __launch_bounds__(SlabLds<DENSE>::BS) void k_slab(SlabParams P) {
     for (int i = tid; i < kDests * kDests; i += BS) {
         const int dd = i / kDests;
         if (S.dcur[dd]) P.gcap[(uint64_t)s * kDests * kDests + i] = S.gcnt[i];
+    }
+}
+
+// Small slabs (< kSmallMax arrivals): at most kSmallCh chunks of kSmallBS, so a
+// thread keeps its own arrivals (payload, table entry, child and grandchild
+// slab) in registers from pass 1 to pass 2, all loads are issued up front, and a
+// displaced record finds its emission position in LDS: pass 2 makes no global
+// loads.  The slot hash table is sized to the slab (power of two >= 2n).
+constexpr int kSmallCh = (int)((kSmallMax + kSmallBS - 1) / kSmallBS);
+struct SmallLds {
+    unsigned long long tab[kSmallTab];
+    uint32_t tkey[kSmallTab];
+    uint32_t claim[2][kSmallClaim];
+    uint32_t fate[kSmallMax];
+    uint32_t gcnt[kDests * kDests];
+    uint32_t doff[kDests], dcap[kDests], dcur[kDests];
+    uint32_t wcnt[kSmallBS / 64][kDests], wpre[kSmallBS / 64][kDests];
+    uint32_t npend[2], nwin, err;
+};
+
+__device__ __forceinline__ int small_entry(SmallLds& S, uint32_t local, uint32_t mask) {
+    uint32_t h = hash_slot(local) & mask;
+    for (uint32_t probe = 0; probe <= mask; probe++) {
+        const uint32_t k = S.tkey[h];
+        if (k == local) return (int)h;
+        if (k == kEmpty32) {
+            const uint32_t old = atomicCAS(&S.tkey[h], kEmpty32, local);
+            if (old == kEmpty32 || old == local) return (int)h;
+        }
+        h = (h + 1) & mask;
+    }
+    return -1;
+}
+
+// flattened descriptor of a small slab: one scalar load instead of the chain
+// list -> slab tables -> cell tables
+struct SmallDesc {
+    uint32_t s, off, n, dbase;
+    int32_t t, cx, cy, cz;
+    uint32_t sb, dlen, pad0, pad1;
+};
+constexpr uint32_t kWaveMax = 512;   // small slabs below this size: one wave each (k_slab_wave)
+__global__ void k_small_desc(const uint32_t* list, uint32_t nlist, const uint32_t* slab_cell, const int32_t* slab_layer,
+                             const uint32_t* slab_off, const uint32_t* slab_n, const int32_t* cell_idx,
+                             const uint32_t* cell_sb, const uint32_t* dest_off, const uint32_t* dcap, SmallDesc* wave_out,
+                             SmallDesc* block_out, uint32_t* counts) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nlist) return;
+    const uint32_t s = list[i], cr_ = slab_cell[s];
+    SmallDesc D;
+    D.s = s;
+    D.off = slab_off[s];
+    D.n = slab_n[s];
+    D.dbase = dest_off[s * kDests];
+    D.dlen = dest_off[s * kDests + kDests - 1] + dcap[s * kDests + kDests - 1] - D.dbase;
+    D.t = slab_layer[s];
+    D.cx = cell_idx[3 * cr_];
+    D.cy = cell_idx[3 * cr_ + 1];
+    D.cz = cell_idx[3 * cr_ + 2];
+    D.sb = cell_sb[cr_];
+    D.pad0 = D.pad1 = 0;
+    // one atomic per wave and class
+    const bool w = D.n < kWaveMax;
+    const uint64_t mw = __ballot(w), mb = __ballot(!w);
+    const uint64_t lt = lanemask_lt();
+    const uint32_t lead = __lane_id() == (uint32_t)(__ffsll((long long)__ballot(1)) - 1);
+    uint32_t bw = 0, bb = 0;
+    if (lead) {
+        if (mw) bw = atomicAdd(&counts[0], (uint32_t)__popcll(mw));
+        if (mb) bb = atomicAdd(&counts[1], (uint32_t)__popcll(mb));
+    }
+    const int src = __ffsll((long long)__ballot(1)) - 1;
+    bw = __shfl(bw, src, 64);
+    bb = __shfl(bb, src, 64);
+    if (w) wave_out[bw + __popcll(mw & lt)] = D;
+    else block_out[bb + __popcll(mb & lt)] = D;
+}
+
+// Per-thread register copy of one small slab's inputs (loaded one slab ahead).
+struct SmallPre {
+    u32x4 pp[kSmallCh];
+    uint32_t pk[kSmallCh], pe[kSmallCh];
+    uint32_t doff, dcap;
+};
+
+__device__ __forceinline__ void small_prefetch(const SlabParams& P, uint32_t li, SmallDesc& D, SmallPre& R,
+                                               uint32_t tid) {
+    if (li >= P.nlist) return;   // block-uniform
+    D = P.sdesc[li];
+    const uint64_t nb = (uint64_t)D.n * 4;
+    const __amdgpu_buffer_rsrc_t rP = srd(P.in.p + D.off, nb * 4), rK = srd(P.in.k + D.off, nb), rE = srd(P.in.e + D.off, nb);
+#pragma unroll
+    for (int c = 0; c < kSmallCh; c++) {
+        const uint32_t j = c * kSmallBS + tid;
+        const bool v = j < D.n;
+        R.pp[c] = bld4(rP, v ? j * 16 : 0xFFFFFFFFu);
+        R.pk[c] = bld(rK, v ? j * 4 : 0xFFFFFFFFu);
+        R.pe[c] = bld(rE, v ? j * 4 : 0xFFFFFFFFu);
+    }
+    const __amdgpu_buffer_rsrc_t rD = srd(P.dest_off + (uint64_t)D.s * kDests, kDests * 4);
+    const __amdgpu_buffer_rsrc_t rC = srd(P.dcap + (uint64_t)D.s * kDests, kDests * 4);
+    R.doff = bld(rD, tid < kDests ? tid * 4 : 0xFFFFFFFFu);
+    R.dcap = bld(rC, tid < kDests ? tid * 4 : 0xFFFFFFFFu);
+}
+
+__device__ __forceinline__ void small_process(const SlabParams& P, SmallLds& S, const SmallDesc& D, SmallPre& R,
+                                              uint32_t tid) {
+    constexpr int BS = kSmallBS, NW = BS / 64, CH = kSmallCh;
+    STAMP_DECL
+    const uint32_t wv = tid / 64;
+    const uint32_t s = D.s;
+    const int32_t t = D.t;
+    const uint32_t n = D.n;
+    const uint32_t dbase = D.dbase;
+    const uint64_t db = (uint64_t)D.dlen * 4;
+    const int32_t cx = D.cx, cy = D.cy, cz = D.cz;
+    const uint32_t sb = D.sb;
+    const LevelGeo& G = P.G;
+    const uint32_t nch = (n + BS - 1) / BS;
+    uint32_t cap = 64;
+    while (cap < 2 * n && cap < (uint32_t)kSmallTab) cap <<= 1;
+    const uint32_t mask = cap - 1;
+    const uint64_t nb = (uint64_t)n * 4;
+    const __amdgpu_buffer_rsrc_t oP = srd(P.nx.p + dbase, db * 4), oK = srd(P.nx.k + dbase, db), oE = srd(P.nx.e + dbase, db);
+    u32x4* pp = R.pp;
+    uint32_t* pk = R.pk;
+    uint32_t* pe = R.pe;
+    for (uint32_t i = tid; i < cap; i += BS) { S.tab[i] = kEmpty64; S.tkey[i] = kEmpty32; }
+    for (int i = tid; i < 2 * kSmallClaim; i += BS) (&S.claim[0][0])[i] = kEmpty32;
+    for (int i = tid; i < kDests * kDests; i += BS) S.gcnt[i] = 0;
+    if (tid < kDests) {
+        S.dcur[tid] = 0;
+        S.doff[tid] = R.doff - dbase;
+        S.dcap[tid] = R.dcap;
+    }
+    if (tid < NW * kDests) (&S.wcnt[0][0])[tid] = 0;
+    if (tid == 0) { S.npend[0] = 0; S.npend[1] = 0; S.nwin = 0; S.err = 0; }
+    // reference slot: the one holding the cell centre (metadata.rs:104-106)
+    const I3 c0 = hex_from_world(cell_pos1(cx, P.cs), cell_pos1(cy, P.cs), cell_pos1(cz, P.cs), G.cr);
+    const int32_t rx = c0.x - P.tx / 2, ry = c0.y - P.ty / 2;
+    uint32_t err = 0;
+    const uint64_t lt = lanemask_lt();
+    __syncthreads();
+    STAMP(0);
+
+    int32_t rec_e[CH];    // table entry of an arrival that became a slot record, else -1
+    int32_t own_d[CH], own_g[CH];
+    // emission of the previous chunk: kind (-1 none, 0 self, 1 displaced), occupant, child slab, grandchild
+    int32_t em = -1, emg = -1;
+    uint32_t emj = 0, emd = 0;
+#pragma unroll
+    for (int ci = 0; ci <= CH; ci++) {
+        if ((uint32_t)ci > nch) break;   // block-uniform
+        const uint32_t par = ci & 1;
+        uint32_t* claim = S.claim[par];
+        const bool have = ci < CH && (uint32_t)ci < nch;
+        const uint32_t j = ci * BS + tid;
+        const bool valid = have && j < n;
+        bool pending = false;
+        uint32_t local = 0;
+        int e = 0, hc = -1;
+        float d2 = 0.f;
+        uint32_t dn = 0;
+        if (ci < CH) {
+            const float x = __uint_as_float(pp[ci].x), y = __uint_as_float(pp[ci].y), z = __uint_as_float(pp[ci].z);
+            const SlotRoute sr = slot_route(x, y, z, G);
+            const int32_t lx = sr.sl.x - rx, ly = sr.sl.y - ry;
+            const bool layer_ok = sr.sl.z == t;
+            const bool range_ok = lx >= 0 && ly >= 0 && lx < P.tx && ly < P.ty;
+            err |= (valid && !layer_ok) ? (uint32_t)ERR_LAYER : ((valid && !range_ok) ? (uint32_t)ERR_SLOT_RANGE : 0u);
+            pending = valid && layer_ok && range_ok;
+            local = pending ? (uint32_t)(ly * P.tx + lx) : 0u;
+            float X, Y, Z;
+            hex_to_world(sr.sl, G.cr, X, Y, Z);
+            d2 = dist2(X, Y, Z, x, y, z);
+            uint32_t rerr = 0, gerr = 0;
+            const int d = route_dest(sr.rc, cx, cy, cz, t, rerr);
+            int g = route_dest(sr.rg, sr.rc.ix, sr.rc.iy, sr.rc.iz, sr.rc.u, gerr);
+            if (valid) err |= rerr | ((P.check_gchild && d >= 0) ? gerr : 0u);
+            dn = d < 0 ? 0u : (uint32_t)d;
+            if (d < 0) g = -1;
+            own_d[ci] = (int32_t)dn;
+            own_g[ci] = g;
+            rec_e[ci] = -1;
+            if (pending) {
+                e = small_entry(S, local, mask);
+                if (e >= 0) hc = claim_insert<kSmallClaim>(claim, local, tid);
+                if (e < 0 || hc < 0) { err |= ERR_CLAIM; pending = false; }
+            }
+        }
+        {
+            const uint32_t np = (uint32_t)__popcll(__ballot(pending));
+            if ((tid & 63) == 0 && np) atomicAdd(&S.npend[par], np);
+        }
+        STAMP(1);
+        STAMP_COUNT(10, 1);
+        // wave ranks of chunk ci-1's emissions per child slab
+        const bool vd = em >= 0;
+        const int d = vd ? (int)emd : 0;
+        uint64_t same = __ballot(vd);
+#pragma unroll
+        for (int b = 0; b < 5; b++) {
+            const uint64_t bb = __ballot(vd && ((d >> b) & 1));
+            same &= ((d >> b) & 1) ? bb : ~bb;
+        }
+        const uint32_t rw = __popcll(same & lt);
+        if (vd && rw == 0) S.wcnt[wv][d] = (uint32_t)__popcll(same);
+        {   // grandchild capacities of self emissions
+            const bool vg = vd && em == 0 && emg >= 0;
+            const int32_t gg = vg ? emg : 0;
+            uint64_t sg = same & __ballot(vg);
+#pragma unroll
+            for (int b = 0; b < 5; b++) {
+                const uint64_t bb = __ballot(vg && ((gg >> b) & 1));
+                sg &= ((gg >> b) & 1) ? bb : ~bb;
+            }
+            if (vg && __popcll(sg & lt) == 0) atomicAdd(&S.gcnt[d * kDests + gg], (uint32_t)__popcll(sg));
+        }
+        STAMP(2);
+        lds_barrier();
+        STAMP(3);
+        if (tid < kDests) {
+            uint32_t acc = S.dcur[tid];
+#pragma unroll
+            for (int q = 0; q < NW; q++) { const uint32_t cc = S.wcnt[q][tid]; S.wpre[q][tid] = acc; acc += cc; S.wcnt[q][tid] = 0; }
+            S.dcur[tid] = acc;
+        }
+        int32_t nem = -1;
+        uint32_t nemj = 0, nemd = 0;
+        bool first = true;
+        for (;;) {
+            bool won = false;
+            if (pending && (claim[hc] & kClaimDone) == tid) {
+                const unsigned long long occ = S.tab[e];
+                const unsigned long long mine =
+                    ((unsigned long long)f2u(d2) << 33) | ((unsigned long long)dn << kJBits) | j;
+                if (occ == kEmpty64) {
+                    S.tab[e] = mine;
+                    rec_e[ci] = e;
+                } else if (d2 < __uint_as_float((uint32_t)(occ >> 33))) {   // strict: ties keep the old point
+                    S.tab[e] = mine;
+                    rec_e[ci] = e;
+                    nem = 1;
+                    nemj = (uint32_t)occ & kJMask;
+                    nemd = (uint32_t)(occ >> kJBits) & 31u;
+                } else {
+                    nem = 0;
+                    nemd = dn;
+                }
+                pending = false;
+                won = true;
+                claim[hc] = (local << 11) | kClaimDone;
+            }
+            {
+                const uint64_t wm = __ballot(won);
+                if ((tid & 63) == 0 && wm) atomicSub(&S.npend[par], (uint32_t)__popcll(wm));
+            }
+            STAMP(4);
+            STAMP_COUNT(9, 1);
+            lds_barrier();
+            STAMP(5);
+            if (first) {   // chunk ci-1: stores into its child slabs
+                first = false;
+                const uint32_t r = S.wpre[wv][d] + rw;
+                const bool ok = vd && r < S.dcap[d];
+                err |= (vd && !ok) ? (uint32_t)ERR_CAPACITY : 0u;
+                const uint32_t pos = S.doff[d] + r;
+                const uint32_t po = ok ? pos * 4 : 0xFFFFFFFFu;
+                if (ci > 0) {
+                    const int pc = ci - 1 < CH ? ci - 1 : 0;
+                    bst4(oP, (ok && em == 0) ? pos * 16 : 0xFFFFFFFFu, pp[pc]);
+                    bst(oK, po, pk[pc]);
+                    bst(oE, po, max(pe[pc], sb));
+                }
+                if (ok && em == 1) S.fate[emj] = pos;
+                STAMP(6);
+            }
+            if (S.npend[par] == 0) break;
+            if (pending) atomicMin(&claim[hc], (local << 11) | tid);
+            STAMP(4);
+            lds_barrier();
+            STAMP(5);
+        }
+        if (hc >= 0) claim[hc] = kEmpty32;
+        em = nem; emj = nemj; emd = nemd;
+        emg = ci < CH ? own_g[ci] : -1;
+    }
+    STAMP(7);
+    __syncthreads();   // fate[] and the final table are complete
+    STAMP(11);
+
+    // pass 2 from registers: grid points and displaced payloads
+    const __amdgpu_buffer_rsrc_t rG = srd(P.grid + P.grid_off[s], (uint64_t)n * 16);
+#pragma unroll
+    for (int ci = 0; ci < CH; ci++) {
+        if ((uint32_t)ci >= nch) break;
+        const uint32_t j = ci * BS + tid;
+        bool win = false, dsp = false;
+        if (rec_e[ci] >= 0) {
+            const unsigned long long occ = S.tab[rec_e[ci]];
+            win = ((uint32_t)occ & kJMask) == j;
+            dsp = !win;
+        }
+        const uint64_t m = __ballot(win);
+        uint32_t wb = 0;
+        if ((tid & 63) == 0 && m) wb = atomicAdd(&S.nwin, (uint32_t)__popcll(m));
+        wb = __shfl(wb, 0, 64);
+        bst4(rG, win ? (wb + (uint32_t)__popcll(m & lt)) * 16 : 0xFFFFFFFFu, pp[ci]);
+        if (dsp) {
+            bst4(oP, S.fate[j] * 16, pp[ci]);
+            if (own_g[ci] >= 0) atomicAdd(&S.gcnt[own_d[ci] * kDests + own_g[ci]], 1u);
+        }
+    }
+    STAMP(8);
+    if (err) atomicOr(&S.err, err);
+    __syncthreads();
+    if (tid == 0) {
+        P.slab_grid_n[s] = S.nwin;
+        if (S.err) set_err(P.ctr, S.err);
+    }
+    if (tid < kDests) P.dest_n[s * kDests + tid] = S.dcur[tid] < S.dcap[tid] ? S.dcur[tid] : S.dcap[tid];
+    for (int i = tid; i < kDests * kDests; i += BS) {
+        const int dd = i / kDests;
+        if (S.dcur[dd]) P.gcap[(uint64_t)s * kDests * kDests + i] = S.gcnt[i];
+    }
+    STAMP_FLUSH(P.stamps);
+}
+
+// Persistent: each workgroup walks the small-slab list with a grid stride.
+__global__ __launch_bounds__(kSmallBS) void k_slab_small(SlabParams P) {
+    __shared__ SmallLds S;
+    const uint32_t tid = threadIdx.x;
+    SmallDesc D;
+    SmallPre R;
+    for (uint32_t li = blockIdx.x; li < P.nlist; li += gridDim.x) {
+        small_prefetch(P, li, D, R, tid);
+        small_process(P, S, D, R, tid);
+        __syncthreads();   // the next slab re-initialises the LDS tables
+    }
+}
+
+// ------------------------------------------------------------------ one wave per slab
+// Slabs of < kWaveMax arrivals (most of the deepest levels): one 64-lane wave
+// per slab, persistent over the wave list, ~13 KB of LDS each so a CU holds ~11
+// slabs at once, and no s_barrier between waves.  Same-slot arrivals of a
+// 64-arrival chunk are applied in lane (= key) order by claim rounds on the slot
+// key word (claim lane in the top byte); LDS operations of one wave execute in
+// program order.  Grandchild capacities go to gcap with global atomics (gcap is
+// zeroed for the level first).
+constexpr int kWaveTab = 1024;
+constexpr int kWaveCh = (int)(kWaveMax / 64);
+constexpr uint32_t kNoClaim = 0x7Fu << 24;
+struct WaveLds {
+    unsigned long long tab[kWaveTab];
+    uint32_t tkey[kWaveTab];     // (claim lane << 24) | slot, kEmpty32 = empty
+    uint16_t fate[kWaveMax];
+    uint32_t doff[kDests], dcap[kDests], dcur[kDests];
+};
+
+__device__ __forceinline__ int wave_entry(WaveLds& W, uint32_t local, uint32_t mask) {
+    uint32_t h = hash_slot(local) & mask;
+    for (uint32_t probe = 0; probe <= mask; probe++) {
+        const uint32_t k = W.tkey[h];
+        if ((k & 0xFFFFFFu) == local) return (int)h;
+        if (k == kEmpty32) {
+            const uint32_t old = atomicCAS(&W.tkey[h], kEmpty32, kNoClaim | local);
+            if (old == kEmpty32 || (old & 0xFFFFFFu) == local) return (int)h;
+        }
+        h = (h + 1) & mask;
+    }
+    return -1;
+}
+
+// wave-aggregated global add of 1 per active lane, grouped by key (< 1024)
+__device__ __forceinline__ void wave_add_by_key(uint32_t* base, bool active, uint32_t key, uint64_t lt) {
+    uint64_t same = __ballot(active);
+#pragma unroll
+    for (int b = 0; b < 10; b++) {
+        const uint64_t bb = __ballot(active && ((key >> b) & 1));
+        same &= ((key >> b) & 1) ? bb : ~bb;
+    }
+    if (active && __popcll(same & lt) == 0) atomicAdd(base + key, (uint32_t)__popcll(same));
+}
+
+__global__ __launch_bounds__(64) void k_slab_wave(SlabParams P) {
+    constexpr int CH = kWaveCh;
+    __shared__ WaveLds W;
+    const uint32_t lane = threadIdx.x;
+    const uint64_t lt = lanemask_lt();
+    const LevelGeo& G = P.G;
+    for (uint32_t li = blockIdx.x; li < P.nwave; li += gridDim.x) {
+        const SmallDesc D = P.wdesc[li];
+        const uint32_t s = D.s, n = D.n, off = D.off, dbase = D.dbase, sb = D.sb;
+        const int32_t t = D.t, cx = D.cx, cy = D.cy, cz = D.cz;
+        const uint32_t nch = (n + 63) / 64;
+        uint32_t cap = 64;
+        while (cap < 2 * n && cap < (uint32_t)kWaveTab) cap <<= 1;
+        const uint32_t mask = cap - 1;
+        const uint64_t nb = (uint64_t)n * 4, db = (uint64_t)D.dlen * 4;
+        const __amdgpu_buffer_rsrc_t rP = srd(P.in.p + off, nb * 4), rK = srd(P.in.k + off, nb), rE = srd(P.in.e + off, nb);
+        const __amdgpu_buffer_rsrc_t oP = srd(P.nx.p + dbase, db * 4), oK = srd(P.nx.k + dbase, db), oE = srd(P.nx.e + dbase, db);
+        u32x4 pp[CH];
+        uint32_t pk[CH], pe[CH];
+#pragma unroll
+        for (int c = 0; c < CH; c++) {
+            const uint32_t j = c * 64 + lane;
+            const bool v = j < n;
+            pp[c] = bld4(rP, v ? j * 16 : 0xFFFFFFFFu);
+            pk[c] = bld(rK, v ? j * 4 : 0xFFFFFFFFu);
+            pe[c] = max(bld(rE, v ? j * 4 : 0xFFFFFFFFu), sb);
+        }
+        for (uint32_t i = lane; i < cap; i += 64) { W.tab[i] = kEmpty64; W.tkey[i] = kEmpty32; }
+        if (lane < kDests) {
+            W.dcur[lane] = 0;
+            W.doff[lane] = P.dest_off[s * kDests + lane] - dbase;
+            W.dcap[lane] = P.dcap[s * kDests + lane];
+        }
+        const I3 c0 = hex_from_world(cell_pos1(cx, P.cs), cell_pos1(cy, P.cs), cell_pos1(cz, P.cs), G.cr);
+        const int32_t rx = c0.x - P.tx / 2, ry = c0.y - P.ty / 2;
+        uint32_t* gcap_s = P.gcap + (uint64_t)s * kDests * kDests;
+        uint32_t err = 0;
+        __syncthreads();   // one wave: orders the LDS initialisation
+
+        int32_t rec_e[CH], own_d[CH], own_g[CH];
+#pragma unroll
+        for (int c = 0; c < CH; c++) {
+            rec_e[c] = -1;
+            own_d[c] = 0;
+            own_g[c] = -1;
+            if ((uint32_t)c >= nch) continue;   // wave-uniform
+            const uint32_t j = c * 64 + lane;
+            const bool valid = j < n;
+            const float x = __uint_as_float(pp[c].x), y = __uint_as_float(pp[c].y), z = __uint_as_float(pp[c].z);
+            const SlotRoute sr = slot_route(x, y, z, G);
+            const int32_t lx = sr.sl.x - rx, ly = sr.sl.y - ry;
+            const bool layer_ok = sr.sl.z == t;
+            const bool range_ok = lx >= 0 && ly >= 0 && lx < P.tx && ly < P.ty;
+            err |= (valid && !layer_ok) ? (uint32_t)ERR_LAYER : ((valid && !range_ok) ? (uint32_t)ERR_SLOT_RANGE : 0u);
+            bool pending = valid && layer_ok && range_ok;
+            const uint32_t local = pending ? (uint32_t)(ly * P.tx + lx) : 0u;
+            float X, Y, Z;
+            hex_to_world(sr.sl, G.cr, X, Y, Z);
+            const float d2 = dist2(X, Y, Z, x, y, z);
+            uint32_t rerr = 0, gerr = 0;
+            const int d = route_dest(sr.rc, cx, cy, cz, t, rerr);
+            int g = route_dest(sr.rg, sr.rc.ix, sr.rc.iy, sr.rc.iz, sr.rc.u, gerr);
+            if (valid) err |= rerr | ((P.check_gchild && d >= 0) ? gerr : 0u);
+            const uint32_t dn = d < 0 ? 0u : (uint32_t)d;
+            if (d < 0) g = -1;
+            own_d[c] = (int32_t)dn;
+            own_g[c] = g;
+            int e = 0;
+            if (pending) {
+                e = wave_entry(W, local, mask);
+                if (e < 0) { err |= ERR_CLAIM; pending = false; }
+            }
+            // claim rounds inside the wave: the lowest pending lane of each slot is applied
+            int32_t em = -1;
+            uint32_t emj = 0, emd = 0;
+            while (__ballot(pending)) {
+                if (pending) atomicMin(&W.tkey[e], (lane << 24) | local);
+                __syncthreads();
+                const bool win = pending && (W.tkey[e] >> 24) == lane;
+                if (win) {
+                    const unsigned long long occ = W.tab[e];
+                    const unsigned long long mine =
+                        ((unsigned long long)f2u(d2) << 33) | ((unsigned long long)dn << kJBits) | j;
+                    if (occ == kEmpty64) {
+                        W.tab[e] = mine;
+                        rec_e[c] = e;
+                    } else if (d2 < __uint_as_float((uint32_t)(occ >> 33))) {   // strict: ties keep the old point
+                        W.tab[e] = mine;
+                        rec_e[c] = e;
+                        em = 1;
+                        emj = (uint32_t)occ & kJMask;
+                        emd = (uint32_t)(occ >> kJBits) & 31u;
+                    } else {
+                        em = 0;
+                        emd = dn;
+                    }
+                    pending = false;
+                    W.tkey[e] = kNoClaim | local;
+                }
+                __syncthreads();
+            }
+            // emissions of this chunk, in lane order per child slab
+            const bool vd = em >= 0;
+            const int dd = vd ? (int)emd : 0;
+            uint64_t same = __ballot(vd);
+#pragma unroll
+            for (int b = 0; b < 5; b++) {
+                const uint64_t bb = __ballot(vd && ((dd >> b) & 1));
+                same &= ((dd >> b) & 1) ? bb : ~bb;
+            }
+            const uint32_t rw = __popcll(same & lt);
+            uint32_t r0 = 0;
+            if (vd && rw == 0) r0 = atomicAdd(&W.dcur[dd], (uint32_t)__popcll(same));
+            const int leader = vd ? (int)(__ffsll((long long)same) - 1) : (int)lane;
+            r0 = __shfl(r0, leader, 64);
+            const uint32_t r = r0 + rw;
+            const bool ok = vd && r < W.dcap[dd];
+            err |= (vd && !ok) ? (uint32_t)ERR_CAPACITY : 0u;
+            const uint32_t pos = W.doff[dd] + r;
+            const uint32_t po = ok ? pos * 4 : 0xFFFFFFFFu;
+            bst4(oP, (ok && em == 0) ? pos * 16 : 0xFFFFFFFFu, pp[c]);
+            bst(oK, po, pk[c]);
+            bst(oE, po, pe[c]);
+            if (ok && em == 1) W.fate[emj] = (uint16_t)pos;
+            wave_add_by_key(gcap_s, ok && em == 0 && g >= 0, (uint32_t)(dd * kDests + (g < 0 ? 0 : g)), lt);
+        }
+        __syncthreads();
+        // pass 2 from registers: grid points and displaced payloads
+        const __amdgpu_buffer_rsrc_t rG = srd(P.grid + P.grid_off[s], (uint64_t)n * 16);
+        uint32_t nwin = 0;
+#pragma unroll
+        for (int c = 0; c < CH; c++) {
+            if ((uint32_t)c >= nch) break;
+            const uint32_t j = c * 64 + lane;
+            bool win = false, dsp = false;
+            if (rec_e[c] >= 0) {
+                const unsigned long long occ = W.tab[rec_e[c]];
+                win = ((uint32_t)occ & kJMask) == j;
+                dsp = !win;
+            }
+            const uint64_t m = __ballot(win);
+            bst4(rG, win ? (nwin + (uint32_t)__popcll(m & lt)) * 16 : 0xFFFFFFFFu, pp[c]);
+            nwin += (uint32_t)__popcll(m);
+            bst4(oP, dsp ? (uint32_t)W.fate[j] * 16 : 0xFFFFFFFFu, pp[c]);
+            wave_add_by_key(gcap_s, dsp && own_g[c] >= 0, (uint32_t)(own_d[c] * kDests + (own_g[c] < 0 ? 0 : own_g[c])), lt);
+        }
+        if (lane == 0) {
+            P.slab_grid_n[s] = nwin;
+        }
+        const uint32_t wer = __reduce_or_sync(~0ull, err);
+        if (lane == 0 && wer) set_err(P.ctr, wer);
+        if (lane < kDests) P.dest_n[s * kDests + lane] = W.dcur[lane] < W.dcap[lane] ? W.dcur[lane] : W.dcap[lane];
+        __syncthreads();   // the next slab re-initialises the LDS tables
     }
 }
 
@@ -1219,7 +1758,6 @@ __global__ __launch_bounds__(kBktBS) void k_bucket(BucketParams B) {
         if (threadIdx.x == 0) {
             s_cnt = 0;
             s_off = atomicAdd(&B.ctr->kept_cur, tot);
-            atomicAdd(&B.ctr->kept_total, (unsigned long long)tot);
             if ((uint64_t)s_off + tot > B.kept_cap) set_err(B.ctr, ERR_KEPT_CAP);
         }
         __syncthreads();
@@ -1320,7 +1858,7 @@ struct NextParams {
 __global__ __launch_bounds__(256) void k_next_emit(NextParams Q) {
     __shared__ uint32_t lds[256 / 64 + 1];
     __shared__ uint32_t carry, s_big, s_small, s_bigbase, s_smallbase, s_max;
-    __shared__ unsigned long long s_arr;
+    __shared__ unsigned long long s_arr, s_arr_big;
     const uint32_t b = blockIdx.x;
     if (Q.bkt_state[b] != 2) return;
     const uint32_t cell = b >> 3, oct = b & 7;
@@ -1336,6 +1874,7 @@ __global__ __launch_bounds__(256) void k_next_emit(NextParams Q) {
         s_big = 0;
         s_small = 0;
         s_arr = 0;
+        s_arr_big = 0;
         s_max = 0;
     }
     __syncthreads();
@@ -1348,6 +1887,7 @@ __global__ __launch_bounds__(256) void k_next_emit(NextParams Q) {
         if (n) {
             atomicAdd(n >= kSmallMax ? &s_big : &s_small, 1u);
             atomicAdd(&s_arr, (unsigned long long)n);
+            if (n >= kSmallMax) atomicAdd(&s_arr_big, (unsigned long long)n);
             atomicMax(&s_max, n);
         }
     }
@@ -1357,6 +1897,8 @@ __global__ __launch_bounds__(256) void k_next_emit(NextParams Q) {
         s_bigbase = s_big ? atomicAdd(&Q.ctr->nbig, s_big) : 0;
         s_smallbase = s_small ? atomicAdd(&Q.ctr->nsmall, s_small) : 0;
         if (s_arr) atomicAdd(&Q.ctr->arrivals_next, s_arr);
+        if (s_arr_big) atomicAdd(&Q.ctr->dense_arrivals, s_arr_big);
+        if (s_arr > s_arr_big) atomicAdd(&Q.ctr->small_arrivals, s_arr - s_arr_big);
         s_big = 0;
         s_small = 0;
     }
@@ -1392,18 +1934,27 @@ __global__ __launch_bounds__(256) void k_next_emit(NextParams Q) {
 __global__ __launch_bounds__(256) void k_l0_lists(const uint32_t* slab_n, uint32_t nslabs, uint32_t* big,
                                                   uint32_t* small, Counters* ctr) {
     __shared__ uint32_t nb, ns, bb, bs;
-    if (threadIdx.x == 0) { nb = 0; ns = 0; }
+    __shared__ unsigned long long ab, as;
+    if (threadIdx.x == 0) { nb = 0; ns = 0; ab = 0; as = 0; }
     __syncthreads();
     const uint32_t s = blockIdx.x * 256 + threadIdx.x;
     uint32_t rb = 0, rs = 0;
     const bool v = s < nslabs;
     const bool isbig = v && slab_n[s] >= kSmallMax;
-    if (v) { if (isbig) rb = atomicAdd(&nb, 1u); else rs = atomicAdd(&ns, 1u); }
+    if (v) {
+        if (isbig) { rb = atomicAdd(&nb, 1u); atomicAdd(&ab, (unsigned long long)slab_n[s]); }
+        else { rs = atomicAdd(&ns, 1u); atomicAdd(&as, (unsigned long long)slab_n[s]); }
+    }
     uint32_t mx = v ? slab_n[s] : 0;
     for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o, 64));
     if ((threadIdx.x & 63) == 0 && mx) atomicMax(&ctr->max_slab, mx);
     __syncthreads();
-    if (threadIdx.x == 0) { bb = nb ? atomicAdd(&ctr->nbig, nb) : 0; bs = ns ? atomicAdd(&ctr->nsmall, ns) : 0; }
+    if (threadIdx.x == 0) {
+        bb = nb ? atomicAdd(&ctr->nbig, nb) : 0;
+        bs = ns ? atomicAdd(&ctr->nsmall, ns) : 0;
+        if (ab) atomicAdd(&ctr->dense_arrivals, ab);
+        if (as) atomicAdd(&ctr->small_arrivals, as);
+    }
     __syncthreads();
     if (v) { if (isbig) big[bb + rb] = s; else small[bs + rs] = s; }
 }
@@ -1426,6 +1977,13 @@ Engine::Engine(const Config& cfg, int device, hipStream_t stream) : cfg_(cfg), d
     HIP_CHECK(hipMalloc(&dev_->ctr, sizeof(Counters)));
     HIP_CHECK(hipMalloc(&dev_->bbox_part, kBBoxBlocks * 6 * sizeof(float)));
     HIP_CHECK(hipMalloc(&dev_->bbox_flag, sizeof(uint32_t)));
+    // resident workgroups of the persistent small-slab kernel
+    int cus = 0, per = 0;
+    HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device_));
+    HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_slab_small, kSmallBS, 0));
+    small_grid_ = (uint32_t)std::max(1, cus * std::max(per, 1));
+    HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_slab_wave, 64, 0));
+    wave_grid_ = (uint32_t)std::max(1, cus * std::max(per, 1));
 }
 
 Engine::~Engine() {
@@ -1947,6 +2505,16 @@ int Engine::run_level(uint32_t h) {
     unsigned long long* stamps = static_cast<unsigned long long*>(dev_->get(2 * 16 * 8));
     HIP_CHECK(hipMemsetAsync(stamps, 0, 2 * 16 * 8, stream_));
 #endif
+    const bool verbose = getenv("PCC_VERBOSE") != nullptr;
+    const auto tv0 = std::chrono::steady_clock::now();
+    if (verbose) {
+        HIP_CHECK(hipStreamSynchronize(stream_));
+        fprintf(stderr, "[pcc] level %u: cells %u slabs %u (dense %u, small %u) arrivals %llu max_slab %u\n", h, L->ncells,
+                L->nslabs, L->nbig, L->nsmall, (unsigned long long)L->arrivals, L->max_slab);
+    }
+    // one-wave slabs accumulate grandchild capacities with atomics: zero gcap
+    // before any slab kernel of this level writes its rows
+    if (L->nsmall) HIP_CHECK(hipMemsetAsync(L->gcap, 0, (uint64_t)L->nslabs * kDests * kDests * 4, stream_));
     if (L->nbig) {
         SP.list = L->big_list;
 #ifdef PCC_STAMPS
@@ -1955,6 +2523,11 @@ int Engine::run_level(uint32_t h) {
         ev_begin(ST_DENSE);
         k_slab<true><<<L->nbig, kDenseBS, 0, stream_>>>(SP);
         ev_end(ST_DENSE);
+        if (verbose) {
+            HIP_CHECK(hipStreamSynchronize(stream_));
+            fprintf(stderr, "[pcc]   dense slabs %.3f ms\n",
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tv0).count());
+        }
     }
     if (L->nsmall) {
         SP.list = L->small_list;
@@ -1962,7 +2535,26 @@ int Engine::run_level(uint32_t h) {
         SP.stamps = stamps + 16;
 #endif
         ev_begin(ST_SMALL);
-        k_slab<false><<<L->nsmall, kSmallBS, 0, stream_>>>(SP);
+        SmallDesc* wd = static_cast<SmallDesc*>(dev_->get((uint64_t)L->nsmall * sizeof(SmallDesc)));
+        SmallDesc* bd = static_cast<SmallDesc*>(dev_->get((uint64_t)L->nsmall * sizeof(SmallDesc)));
+        uint32_t* cnt = static_cast<uint32_t*>(dev_->get(8));
+        HIP_CHECK(hipMemsetAsync(cnt, 0, 8, stream_));
+        k_small_desc<<<grid_for(L->nsmall, 256, 1u << 30), 256, 0, stream_>>>(
+            L->small_list, L->nsmall, L->slab_cell, L->slab_layer, L->slab_off, L->slab_n, L->cell_idx, L->cell_sb,
+            L->dest_off, L->dcap, wd, bd, cnt);
+        uint32_t hcnt[2];
+        HIP_CHECK(hipMemcpyAsync(hcnt, cnt, 8, hipMemcpyDeviceToHost, stream_));
+        HIP_CHECK(hipStreamSynchronize(stream_));
+        if (hcnt[0]) {   // wave slabs accumulate grandchild capacities with atomics (gcap zeroed above)
+            SP.wdesc = wd;
+            SP.nwave = hcnt[0];
+            k_slab_wave<<<std::min<uint32_t>(hcnt[0], wave_grid_), 64, 0, stream_>>>(SP);
+        }
+        if (hcnt[1]) {
+            SP.sdesc = bd;
+            SP.nlist = hcnt[1];
+            k_slab_small<<<std::min<uint32_t>(hcnt[1], small_grid_), kSmallBS, 0, stream_>>>(SP);
+        }
         ev_end(ST_SMALL);
     }
     HIP_CHECK(hipGetLastError());
@@ -1985,6 +2577,10 @@ int Engine::run_level(uint32_t h) {
     k_bucket<<<nb, kBktBS, 0, stream_>>>(BP);
     ev_end(ST_BUCKET);
     HIP_CHECK(hipGetLastError());
+    // this level's grid points (one scan instead of per-slab global atomics)
+    uint32_t* gsc = static_cast<uint32_t*>(dev_->get((uint64_t)L->nslabs * 4 + 16));
+    uint32_t* gtot = static_cast<uint32_t*>(dev_->get(16));
+    scan_excl_u32(L->slab_grid_n, gsc, L->nslabs, gtot, dev_->scan, stream_);
     ev_begin(ST_NEXT);
     uint32_t* flag = static_cast<uint32_t*>(dev_->get(nb * 4ull));
     uint32_t* ndv = static_cast<uint32_t*>(dev_->get(nb * 4ull));
@@ -1996,9 +2592,10 @@ int Engine::run_level(uint32_t h) {
 #ifdef PCC_STAMPS
     {
         unsigned long long hs[32];
-        HIP_CHECK(hipMemcpy(hs, stamps, sizeof hs, hipMemcpyDeviceToHost));
+        HIP_CHECK(hipMemcpyAsync(hs, stamps, sizeof hs, hipMemcpyDeviceToHost, stream_));
+        HIP_CHECK(hipStreamSynchronize(stream_));
         const char* nm[16] = {"prologue", "claimA", "routeA", "B0wait", "rounds", "rndwait", "stores", "tail",
-                              "pass2", "#rounds", "#steps", "p2sync", "ldwait", "math", "-", "-"};
+                              "pass2", "#rounds", "#steps", "p2sync", "ldwait/epi", "math", "-", "-"};
         for (int v = 0; v < 2; v++) {
             if (!hs[16 * v + 10]) continue;
             fprintf(stderr, "[stamps] level %u %s waves*steps=%llu  cycles/step:", h, v ? "small" : "dense", hs[16 * v + 10]);
@@ -2008,14 +2605,15 @@ int Engine::run_level(uint32_t h) {
         }
     }
 #endif
-    uint32_t ht[2];
+    uint32_t ht[2], hg = 0;
     Counters hc;
+    HIP_CHECK(hipMemcpyAsync(&hg, gtot, 4, hipMemcpyDeviceToHost, stream_));
     HIP_CHECK(hipMemcpyAsync(ht, tots, 8, hipMemcpyDeviceToHost, stream_));
     HIP_CHECK(hipMemcpyAsync(&hc, dev_->ctr, sizeof hc, hipMemcpyDeviceToHost, stream_));
     HIP_CHECK(hipStreamSynchronize(stream_));
     L->kept_used = hc.kept_cur;
-    stats_.grid_points = hc.grid_total;
-    stats_.kept_points = hc.kept_total;
+    stats_.grid_points += hg;
+    stats_.kept_points += hc.kept_cur;
     if (hc.err) {
         char buf[200];
         snprintf(buf, sizeof buf,
