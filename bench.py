@@ -58,6 +58,23 @@ def cpu_baseline(args):
 METRIC = "points/sec converted (octree+LOD build), 1B synthetic pts, 1/2/4/8 MI355X"
 
 
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r1_pmc_traffic_1b.json")
+
+
+def pmc_traffic(workload):
+    """HBM bytes per launch of k_slab<true> from the committed rocprofv3 PMC summary
+    (scripts/pmc.sh + scripts/pmc_summary.py: 2 x FETCH_SIZE + WRITE_SIZE, per
+    MI355X_MICROARCH.md), only when it was measured on this exact workload."""
+    try:
+        with open(PMC_SUMMARY) as f:
+            pm = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    if pm.get("workload") != workload:
+        return None, None
+    return pm["dense_kernel"]["hbm_bytes_per_launch"], os.path.relpath(PMC_SUMMARY, ROOT)
+
+
 def record(args, n_gpus, ms, st_levels, st_cells, st_slabs, arrivals, k, dense_ms, parallelism):
     """The one JSON line (rank 0).  roofline: dense slab kernel k_slab<true>,
     algorithmic bytes = 32 B per arrival it processed over its
@@ -65,6 +82,9 @@ def record(args, n_gpus, ms, st_levels, st_cells, st_slabs, arrivals, k, dense_m
     dense_arr = k["dense_arrivals"]
     achieved = 32.0 * dense_arr / (dense_ms / 1e3) / 1e9 if dense_ms > 0 else 0.0
     whole = 32.0 * arrivals / (ms / 1e3) / 1e9
+    workload = ("config4: %d uniform points in [-1000,1000)^3, seed %d" if args.kind == 0 else
+                "config3-shape: %d clustered points, seed %d") % (args.points, args.seed)
+    traffic, tsrc = pmc_traffic(workload)
     return {
         "metric": METRIC,
         "value": args.points / (ms / 1e3),
@@ -78,12 +98,13 @@ def record(args, n_gpus, ms, st_levels, st_cells, st_slabs, arrivals, k, dense_m
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (counter-hash generator in HBM, SURVEY.md §8d)",
-        "config": {"workload": ("config4: %d uniform points in [-1000,1000)^3, seed %d" if args.kind == 0 else
-                                "config3-shape: %d clustered points, seed %d") % (args.points, args.seed),
+        "config": {"workload": workload,
                    "batch": 10000, "levels": st_levels, "cells": st_cells, "slabs": st_slabs,
                    "arrivals_W": arrivals, "parallelism": parallelism},
         "roofline": {"bound": "hbm", "kernel": "k_slab<dense>", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "traffic_unit": "HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE)", "traffic_source": tsrc,
+                     "alg_bytes_per_launch": 32.0 * k["dense_arrivals"] / max(k["dense_launches"], 1),
                      "alg_bytes_per_arrival": 32, "kernel_ms_per_step": dense_ms,
                      "whole_build_alg_GBs": whole, "whole_build_frac": whole / HBM_PEAK_GBS},
         "stage_ms": k,

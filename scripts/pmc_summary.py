@@ -1,0 +1,54 @@
+#!/usr/bin/env python3
+"""Summarise the rocprofv3 PMC passes of scripts/pmc.sh into profiles/<name>.json.
+
+HBM bytes per kernel follow MI355X_MICROARCH.md "HBM [CDNA4]": WRITE_SIZE (KB) is
+exact; FETCH_SIZE (KB) reports half of the bytes of wide coalesced reads on
+gfx950, so it is doubled.  Per-launch values are averages over the launches of
+one build (bench.py --steps 1 --warmup 0)."""
+import csv
+import json
+import sys
+from collections import OrderedDict
+
+
+def load(path, counter):
+    rows = []
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] == counter:
+            rows.append((r["Kernel_Name"], float(r["Counter_Value"]) * 1024.0,
+                         int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
+    return rows
+
+
+def main(out_dir, name, bench_json):
+    fetch = load(f"{out_dir}/pmc_fetch/fetch_counter_collection.csv", "FETCH_SIZE")
+    write = load(f"{out_dir}/pmc_write/write_counter_collection.csv", "WRITE_SIZE")
+    k = OrderedDict()
+    for nm, v, t in fetch:
+        e = k.setdefault(nm, {"launches": 0, "fetch_bytes_raw": 0.0, "write_bytes": 0.0, "ns": 0})
+        e["launches"] += 1
+        e["fetch_bytes_raw"] += v
+        e["ns"] += t
+    for nm, v, t in write:
+        k.setdefault(nm, {"launches": 0, "fetch_bytes_raw": 0.0, "write_bytes": 0.0, "ns": 0})["write_bytes"] += v
+    for e in k.values():
+        e["hbm_bytes"] = 2.0 * e["fetch_bytes_raw"] + e["write_bytes"]
+        e["hbm_bytes_per_launch"] = e["hbm_bytes"] / max(e["launches"], 1)
+    bench = json.load(open(bench_json))
+    dense = next(v for n, v in k.items() if n.startswith("void pcc::k_slab<true>"))
+    arr = bench["stage_ms"]["dense_arrivals"]
+    summary = {
+        "workload": bench["config"]["workload"],
+        "command": "rocprofv3 --pmc FETCH_SIZE|WRITE_SIZE --kernel-trace -- python3 bench.py --steps 1 --warmup 0 --cpu-sample 0",
+        "correction": "hbm_bytes = 2 x FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md HBM [CDNA4])",
+        "dense_kernel": {"launches": dense["launches"], "hbm_bytes_per_launch": dense["hbm_bytes_per_launch"],
+                         "alg_bytes_per_launch": 32.0 * arr / dense["launches"],
+                         "traffic_over_alg": dense["hbm_bytes"] / (32.0 * arr)},
+        "kernels": k,
+    }
+    json.dump(summary, open(f"profiles/{name}.json", "w"), indent=1)
+    print(json.dumps(summary["dense_kernel"]))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2], sys.argv[3])
