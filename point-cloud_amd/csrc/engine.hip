@@ -465,7 +465,7 @@ __global__ void k_l0_hash_ids(const unsigned long long* hkeys, uint32_t cap, uin
     if (i < cap && hkeys[i] != kHashEmpty) ckeys[hcid[i]] = hkeys[i];
 }
 
-constexpr int kL0BS = 256, kL0IPT = 8, kL0Tile = kL0BS * kL0IPT, kL0W = kL0BS / 64;
+constexpr int kL0BS = 256, kL0IPT = 4, kL0Tile = kL0BS * kL0IPT, kL0W = kL0BS / 64;
 constexpr int kHistLds = 8192;
 
 // pass-0 upsweep from the AoS input: per-tile digit histogram + full dense-slab histogram
@@ -542,36 +542,36 @@ __global__ __launch_bounds__(kL0BS) void k_l0_down(const Point* __restrict__ in,
                                                    L0Params P, int shift, const uint32_t* __restrict__ offs,
                                                    uint32_t ntiles, const uint32_t* files, uint32_t nfiles) {
     constexpr int R = 1 << BITS;
-    __shared__ float sx[kL0Tile], sy[kL0Tile], sz[kL0Tile];
-    __shared__ uint32_t sc[kL0Tile], sk[kL0Tile];
+    __shared__ float4 sp[kL0Tile];
+    __shared__ uint32_t sk[kL0Tile];
     __shared__ uint16_t sd[kL0Tile];
-    __shared__ uint32_t wcnt[kL0W][R], wpre[kL0W][R];
-    __shared__ uint32_t run[R], dbase[R], goff[R];
+    // per (row r, wave) digit counts of the whole tile, then ONE prefix pass in
+    // key order (r-major, wave, lane): two barriers per tile
+    __shared__ uint16_t wcnt[kL0IPT][kL0W][R], wpre[kL0IPT][kL0W][R];
+    __shared__ uint32_t tot[R], dbase[R], goff[R];
     __shared__ uint32_t lds[kL0W + 1];
     const uint32_t w = threadIdx.x / 64;
-    for (int i = threadIdx.x; i < R; i += kL0BS) {
-        run[i] = 0;
-        goff[i] = offs[(uint64_t)i * ntiles + blockIdx.x];
-        for (int q = 0; q < kL0W; q++) wcnt[q][i] = 0;
-    }
+    for (int i = threadIdx.x; i < R; i += kL0BS) goff[i] = offs[(uint64_t)i * ntiles + blockIdx.x];
+    for (int i = threadIdx.x; i < kL0IPT * kL0W * R; i += kL0BS) (&wcnt[0][0][0])[i] = 0;
     const uint64_t base = (uint64_t)blockIdx.x * kL0Tile;
-    float x[kL0IPT], y[kL0IPT], z[kL0IPT];
-    uint32_t c[kL0IPT], k[kL0IPT], rank[kL0IPT];
+    float4 v[kL0IPT];
+    uint32_t k[kL0IPT], rw[kL0IPT];
     uint16_t dg[kL0IPT];
 #pragma unroll
     for (int r = 0; r < kL0IPT; r++) {
         const uint64_t i = base + (uint64_t)r * kL0BS + threadIdx.x;
         dg[r] = 0;
+        k[r] = 0;
+        v[r] = make_float4(0.f, 0.f, 0.f, 0.f);
         if (i < n) {
             if constexpr (SRC_AOS) {
-                const float4 v = reinterpret_cast<const float4*>(in)[i];
-                x[r] = v.x; y[r] = v.y; z[r] = v.z; c[r] = __float_as_uint(v.w);
+                v[r] = reinterpret_cast<const float4*>(in)[i];
                 k[r] = keys ? keys[i] : (uint32_t)i;   // sharded input carries global keys
             } else {
-                const float4 v = S.p[i];
-                x[r] = v.x; y[r] = v.y; z[r] = v.z; c[r] = __float_as_uint(v.w); k[r] = S.k[i];
+                v[r] = S.p[i];
+                k[r] = S.k[i];
             }
-            const int64_t d = l0_dense(P, x[r], y[r], z[r]);
+            const int64_t d = l0_dense(P, v[r].x, v[r].y, v[r].z);
             dg[r] = (uint16_t)(((uint64_t)(d < 0 ? 0 : d) >> shift) & (R - 1));
         }
     }
@@ -588,22 +588,23 @@ __global__ __launch_bounds__(kL0BS) void k_l0_down(const Point* __restrict__ in,
             const uint64_t bb = __ballot(valid && ((d >> b) & 1));
             same &= ((d >> b) & 1) ? bb : ~bb;
         }
-        const uint32_t rw = __popcll(same & lt);
-        if (valid && rw == 0) wcnt[w][d] = (uint32_t)__popcll(same);
-        __syncthreads();
-        for (int t = threadIdx.x; t < R; t += kL0BS) {
-            uint32_t acc = run[t];
-#pragma unroll
-            for (int q = 0; q < kL0W; q++) { const uint32_t cc = wcnt[q][t]; wpre[q][t] = acc; acc += cc; wcnt[q][t] = 0; }
-            run[t] = acc;
-        }
-        __syncthreads();
-        rank[r] = valid ? wpre[w][d] + rw : 0;
+        rw[r] = __popcll(same & lt);
+        if (valid && rw[r] == 0) wcnt[r][w][d] = (uint16_t)__popcll(same);
     }
+    __syncthreads();
+    for (int t = threadIdx.x; t < R; t += kL0BS) {
+        uint32_t acc = 0;
+#pragma unroll
+        for (int r = 0; r < kL0IPT; r++)
+#pragma unroll
+            for (int q = 0; q < kL0W; q++) { const uint32_t cc = wcnt[r][q][t]; wpre[r][q][t] = (uint16_t)acc; acc += cc; }
+        tot[t] = acc;
+    }
+    __syncthreads();
     {
-        uint32_t tot;
-        const uint32_t cc = threadIdx.x < (uint32_t)R ? run[threadIdx.x] : 0;
-        const uint32_t e = block_excl_scan<kL0BS>(cc, lds, &tot);
+        uint32_t tt;
+        const uint32_t cc = threadIdx.x < (uint32_t)R ? tot[threadIdx.x] : 0;
+        const uint32_t e = block_excl_scan<kL0BS>(cc, lds, &tt);
         if (threadIdx.x < (uint32_t)R) dbase[threadIdx.x] = e;
     }
     __syncthreads();
@@ -611,8 +612,8 @@ __global__ __launch_bounds__(kL0BS) void k_l0_down(const Point* __restrict__ in,
     for (int r = 0; r < kL0IPT; r++) {
         const uint64_t i = base + (uint64_t)r * kL0BS + threadIdx.x;
         if (i < n) {
-            const uint32_t p = dbase[dg[r]] + rank[r];
-            sx[p] = x[r]; sy[p] = y[r]; sz[p] = z[r]; sc[p] = c[r]; sk[p] = k[r]; sd[p] = dg[r];
+            const uint32_t p = dbase[dg[r]] + wpre[r][w][dg[r]] + rw[r];
+            sp[p] = v[r]; sk[p] = k[r]; sd[p] = dg[r];
         }
     }
     __syncthreads();
@@ -620,7 +621,7 @@ __global__ __launch_bounds__(kL0BS) void k_l0_down(const Point* __restrict__ in,
     for (uint32_t j = threadIdx.x; j < tn; j += kL0BS) {
         const uint32_t d = sd[j];
         const uint32_t dst = goff[d] + (j - dbase[d]);
-        O.p[dst] = make_float4(sx[j], sy[j], sz[j], __uint_as_float(sc[j]));
+        O.p[dst] = sp[j];
         O.k[dst] = sk[j];
         if constexpr (FINAL) O.e[dst] = event_batch(files, nfiles, sk[j]);
     }
