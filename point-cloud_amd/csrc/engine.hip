@@ -279,14 +279,27 @@ __device__ __forceinline__ int route_dest(const RouteIdx& R, int32_t cx, int32_t
     err |= bad_oct ? (uint32_t)ERR_OCTANT : (bad_sel ? (uint32_t)ERR_SEL : 0u);
     return (bad_oct || bad_sel) ? -1 : (bx | (by << 1) | (bz << 2)) * 3 + sel;
 }
-// slot, child route and grandchild route of one point, one ballot for all divisions
+// slot, child route and grandchild route of one point, one ballot for all
+// divisions.  The grandchild level halves cell size and hex radius exactly
+// (metadata.rs:92,96: powers of two), so x / cs_g = 2 * RN(x / cs_c) exactly and
+// one quotient per axis gives both: grandchild index ig = floor(2q), child index
+// floor(q) = ig >> 1; layers u_g = trunc(2q), u_c = u_g / 2 (C division
+// truncates).  Quotients with |2q| >= 2^30 take the exact path.
 struct SlotRoute { I3 sl; RouteIdx rc, rg; };
 __device__ __forceinline__ SlotRoute slot_route(float x, float y, float z, const LevelGeo& G) {
     bool amb = false;
     SlotRoute S;
     S.sl = hex_q(x, y, z, G, amb);
-    S.rc = route_idx_q(G.csc, G.inv_csc, G.inv_crc, x, y, z, amb);
-    S.rg = route_idx_q(G.csg, G.inv_csg, G.inv_crg, x, y, z, amb);
+    const float qx = x * G.inv_csg, qy = y * G.inv_csg, qz = z * G.inv_csg, qu = z * G.inv_crg;
+    amb |= fmaxf(fmaxf(fabsf(qx), fabsf(qy)), fmaxf(fabsf(qz), fabsf(qu))) >= 0x1p30f;
+    S.rg.ix = sat_i32(floor_q(x, G.inv_csg, amb));
+    S.rg.iy = sat_i32(floor_q(y, G.inv_csg, amb));
+    S.rg.iz = sat_i32(floor_q(z, G.inv_csg, amb));
+    S.rg.u = sat_i32(trunc_q(z, G.inv_crg, amb));
+    S.rc.ix = S.rg.ix >> 1;
+    S.rc.iy = S.rg.iy >> 1;
+    S.rc.iz = S.rg.iz >> 1;
+    S.rc.u = S.rg.u / 2;
     if (__ballot(amb)) {
         if (amb) {
             S.sl = hex_from_world(x, y, z, G.cr);
@@ -862,21 +875,31 @@ __global__ __launch_bounds__(SlabLds<DENSE>::BS) void k_slab(SlabParams P) {
     };
     Stage A = {-1, -1, 0, 0, 0, 0, 0, 0.f, 0.f, 0.f};
     Stage B = A;
-    uint32_t jo = min(tid, nm1);
-    u32x4 nxp = bld4(rP, jo * 16);
-    uint32_t nxk = bld(rK, jo * 4), nxe = bld(rE, jo * 4);
+    // arrivals are prefetched two chunks ahead (buffer ci & 1)
+    struct Pre { u32x4 p; uint32_t k, e; };
+    Pre pre[2];
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+        const uint32_t jo = min((uint32_t)(q * BS) + tid, nm1);
+        pre[q].p = bld4(rP, jo * 16);
+        pre[q].k = bld(rK, jo * 4);
+        pre[q].e = bld(rE, jo * 4);
+    }
     const uint64_t lt = lanemask_lt();
     const uint32_t nchunks = (n + BS - 1) / BS;
-    auto step = [&](uint32_t ci, Stage& cur, Stage& prv) {
+    auto step = [&](uint32_t ci, Stage& cur, Stage& prv, Pre& nx) {
         const uint32_t par = ci & 1;
         uint32_t* claim = S.claim[par];
         const uint32_t j = ci * BS + tid;
         const bool valid = j < n;
-        const float x = __uint_as_float(nxp.x), y = __uint_as_float(nxp.y), z = __uint_as_float(nxp.z);
-        const uint32_t c = nxp.w, k = nxk, eb = max(nxe, sb);
-        jo = min(j + BS, nm1);   // prefetch chunk i+1 (clamped)
-        nxp = bld4(rP, jo * 16);
-        nxk = bld(rK, jo * 4); nxe = bld(rE, jo * 4);
+        const float x = __uint_as_float(nx.p.x), y = __uint_as_float(nx.p.y), z = __uint_as_float(nx.p.z);
+        const uint32_t c = nx.p.w, k = nx.k, eb = max(nx.e, sb);
+        {   // prefetch chunk i+2 (clamped) into the buffer just consumed
+            const uint32_t jo = min(j + 2 * BS, nm1);
+            nx.p = bld4(rP, jo * 16);
+            nx.k = bld(rK, jo * 4);
+            nx.e = bld(rE, jo * 4);
+        }
         // ---- phase A (1): slot + distance (hex.rs:67-85, 55-65) + own child slab
 #ifdef PCC_STAMPS
         if (__float_as_uint(x) == 0x7FC00001u) err |= 1u << 30;   // consume the prefetched loads here
@@ -1017,8 +1040,8 @@ __global__ __launch_bounds__(SlabLds<DENSE>::BS) void k_slab(SlabParams P) {
     };
     // nchunks + 1 steps (the last one only emits), rounded up to an even count
     for (uint32_t ci = 0; ci <= nchunks; ci += 2) {
-        step(ci, A, B);
-        step(ci + 1, B, A);
+        step(ci, A, B, pre[0]);
+        step(ci + 1, B, A, pre[1]);
     }
     STAMP(7);
     __syncthreads();   // also orders this workgroup's status/fate stores before pass 2 reads them

@@ -20,13 +20,21 @@ constexpr float kSqrt3 = 1.73205080757f;  // hex.rs:3
 
 struct I3 { int32_t x, y, z; };
 
-// Rust `f32 as i32`: saturating, NaN -> 0.  Branch-free (selects only) so it
-// does not split wavefront control flow on the GPU.
+// Rust `f32 as i32`: saturating, NaN -> 0.  On gfx950 this is exactly what
+// v_cvt_i32_f32 does in hardware (verified for NaN, +-inf, +-2^31 boundaries
+// and rounding toward zero: scripts/cvt_test.hip), so the device path is one
+// instruction; the host path is branch-free selects.
 PCC_HD int32_t sat_i32(float v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    int32_t r;
+    asm("v_cvt_i32_f32 %0, %1" : "=v"(r) : "v"(v));
+    return r;
+#else
     const float c = fminf(fmaxf(v, -2147483648.0f), 2147483520.0f);  // 2147483520 = largest f32 < 2^31
     int32_t r = (int32_t)c;
     r = (v >= 2147483648.0f) ? INT32_MAX : r;
     return (v != v) ? 0 : r;
+#endif
 }
 
 // metadata.rs:91-93  max_cell_size / 2u32.pow(h) as f32
