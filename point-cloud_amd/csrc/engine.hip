@@ -930,11 +930,25 @@ __global__ __launch_bounds__(SlabLds<DENSE>::BS) void k_slab(SlabParams P) {
         if (d2 == 12345.0f) err |= 1u << 29;   // finish the math before the stamp
         STAMP(13);
 #endif
+        // An arrival that does not beat the slot's occupant as it stands before
+        // this chunk overflows at once (occupants only improve within a chunk,
+        // cell.rs:80 strict <): only candidate records enter the claim rounds,
+        // so a chunk needs as many rounds as its most contended slot has
+        // candidates, not arrivals (clustered clouds: tens of arrivals per slot).
         int e = 0, hc = -1;
+        bool self_em = false;
         if (pending) {
             e = slot_entry<DENSE>(S, local);
-            if (e >= 0) hc = claim_insert<CLAIM>(claim, local, tid);
-            if (e < 0 || hc < 0) { err |= ERR_CLAIM; pending = false; }
+            if (e >= 0) {
+                const unsigned long long occ = S.tab[e];
+                if (occ != kEmpty64 && !(d2 < __uint_as_float((uint32_t)(occ >> 33)))) {
+                    self_em = true;
+                    pending = false;
+                } else {
+                    hc = claim_insert<CLAIM>(claim, local, tid);
+                }
+            }
+            if (e < 0 || (pending && hc < 0)) { err |= ERR_CLAIM; pending = false; }
         }
         {
             const uint32_t np = (uint32_t)__popcll(__ballot(pending));
@@ -975,8 +989,8 @@ __global__ __launch_bounds__(SlabLds<DENSE>::BS) void k_slab(SlabParams P) {
         }
         // per round, the earliest pending arrival of every slot (min thread index
         // = min key) is applied
-        int32_t em = -1;
-        uint32_t emj = 0, emd = 0;
+        int32_t em = self_em ? 0 : -1;
+        uint32_t emj = 0, emd = self_em ? dn : 0u;
         bool rec = false;
         bool first = true;
         for (;;) {
@@ -1238,7 +1252,6 @@ __device__ __forceinline__ void small_process(const SlabParams& P, SmallLds& S, 
     uint32_t cap = 64;
     while (cap < 2 * n && cap < (uint32_t)kSmallTab) cap <<= 1;
     const uint32_t mask = cap - 1;
-    const uint64_t nb = (uint64_t)n * 4;
     const __amdgpu_buffer_rsrc_t oP = srd(P.nx.p + dbase, db * 4), oK = srd(P.nx.k + dbase, db), oE = srd(P.nx.e + dbase, db);
     u32x4* pp = R.pp;
     uint32_t* pk = R.pk;
@@ -1274,7 +1287,7 @@ __device__ __forceinline__ void small_process(const SlabParams& P, SmallLds& S, 
         const bool have = ci < CH && (uint32_t)ci < nch;
         const uint32_t j = ci * BS + tid;
         const bool valid = have && j < n;
-        bool pending = false;
+        bool pending = false, self_em = false;
         uint32_t local = 0;
         int e = 0, hc = -1;
         float d2 = 0.f;
@@ -1300,10 +1313,18 @@ __device__ __forceinline__ void small_process(const SlabParams& P, SmallLds& S, 
             own_d[ci] = (int32_t)dn;
             own_g[ci] = g;
             rec_e[ci] = -1;
-            if (pending) {
+            if (pending) {   // occupant pre-filter (see k_slab)
                 e = small_entry(S, local, mask);
-                if (e >= 0) hc = claim_insert<kSmallClaim>(claim, local, tid);
-                if (e < 0 || hc < 0) { err |= ERR_CLAIM; pending = false; }
+                if (e >= 0) {
+                    const unsigned long long occ = S.tab[e];
+                    if (occ != kEmpty64 && !(d2 < __uint_as_float((uint32_t)(occ >> 33)))) {
+                        self_em = true;
+                        pending = false;
+                    } else {
+                        hc = claim_insert<kSmallClaim>(claim, local, tid);
+                    }
+                }
+                if (e < 0 || (pending && hc < 0)) { err |= ERR_CLAIM; pending = false; }
             }
         }
         {
@@ -1343,8 +1364,8 @@ __device__ __forceinline__ void small_process(const SlabParams& P, SmallLds& S, 
             for (int q = 0; q < NW; q++) { const uint32_t cc = S.wcnt[q][tid]; S.wpre[q][tid] = acc; acc += cc; S.wcnt[q][tid] = 0; }
             S.dcur[tid] = acc;
         }
-        int32_t nem = -1;
-        uint32_t nemj = 0, nemd = 0;
+        int32_t nem = self_em ? 0 : -1;
+        uint32_t nemj = 0, nemd = self_em ? dn : 0u;
         bool first = true;
         for (;;) {
             bool won = false;
@@ -1568,13 +1589,23 @@ __global__ __launch_bounds__(64) void k_slab_wave(SlabParams P) {
             own_d[c] = (int32_t)dn;
             own_g[c] = g;
             int e = 0;
-            if (pending) {
-                e = wave_entry(W, local, mask);
-                if (e < 0) { err |= ERR_CLAIM; pending = false; }
-            }
-            // claim rounds inside the wave: the lowest pending lane of each slot is applied
             int32_t em = -1;
             uint32_t emj = 0, emd = 0;
+            if (pending) {
+                e = wave_entry(W, local, mask);
+                if (e < 0) {
+                    err |= ERR_CLAIM;
+                    pending = false;
+                } else {   // occupant pre-filter (see k_slab)
+                    const unsigned long long occ = W.tab[e];
+                    if (occ != kEmpty64 && !(d2 < __uint_as_float((uint32_t)(occ >> 33)))) {
+                        pending = false;
+                        em = 0;
+                        emd = dn;
+                    }
+                }
+            }
+            // claim rounds inside the wave: the lowest pending lane of each slot is applied
             while (__ballot(pending)) {
                 if (pending) atomicMin(&W.tkey[e], (lane << 24) | local);
                 __syncthreads();
