@@ -83,10 +83,14 @@ struct Counters {
 };
 
 // One level's arrivals: the 16-B record (x, y, z, rgba bits) as one float4 so
-// every load/store of a point is a single dwordx4; key and event batch apart.
+// every load/store of a point is a single dwordx4, and the key (input index)
+// apart.  The event batch is not stored: inside a level-h cell it is
+// max(eb0(key), cell_sb) (lib.rs:31-52 batches, SURVEY.md Appendix C.3
+// eb' = max(eb, sb) along the cell's ancestor chain, whose spill batches only
+// grow), recomputed where it is needed (k_bucket).
 struct Arena {
     float4* p;
-    uint32_t *k, *e;
+    uint32_t* k;
 };
 
 struct Engine::Dev {
@@ -95,8 +99,6 @@ struct Engine::Dev {
     float* bbox_part = nullptr;     // per-block min/max partials
     uint32_t* bbox_flag = nullptr;
     uint32_t* files = nullptr;      // per file: start_lo, start_hi, eb0, batch
-    uint32_t* fate = nullptr;       // per arena position: emission position of a displaced record
-    uint16_t* status = nullptr;     // per arena position: slot-table entry + 1 of a record
     ScanTemp scan;
     uint64_t cap = 0;
     // chunked bump allocator for per-build tables and output regions (reset at
@@ -127,7 +129,7 @@ struct Engine::Level {
     int arena = 0;
     Engine::Dev* dev = nullptr;
     int32_t* cell_idx = nullptr;     // 3 * ncells
-    uint32_t* cell_sb = nullptr;     // spill batch of the parent bucket (eb' = max(eb, sb))
+    uint32_t* cell_sb = nullptr;     // spill batch of the parent bucket (running max along the ancestors)
     uint32_t* cell_slab0 = nullptr;  // ncells + 1
     uint32_t* slab_cell = nullptr;
     int32_t* slab_layer = nullptr;
@@ -636,7 +638,6 @@ __global__ __launch_bounds__(kL0BS) void k_l0_down(const Point* __restrict__ in,
         const uint32_t dst = goff[d] + (j - dbase[d]);
         O.p[dst] = sp[j];
         O.k[dst] = sk[j];
-        if constexpr (FINAL) O.e[dst] = event_batch(files, nfiles, sk[j]);
     }
 }
 
@@ -704,8 +705,6 @@ struct SlabParams {
     const uint32_t* dest_off;
     uint32_t* slab_grid_n;
     uint32_t* dest_n;
-    uint32_t* fate;       // per arrival: emission position of a displaced record (pass 1 -> pass 2)
-    uint16_t* status;     // per arrival: table entry + 1 if it became a slot record, else 0
     uint32_t* gcap;       // 24 x 24 per slab: arrivals of each child slab per grandchild slab
     const struct SmallDesc* sdesc;   // small-slab descriptors (k_slab_small)
     uint32_t nlist;
@@ -719,26 +718,13 @@ struct SlabParams {
     unsigned long long* stamps;   // diagnostic build only
 };
 
-template <bool DENSE>
-struct SlabLds;
-
-template <>
-struct SlabLds<true> {
+// Dense slabs (>= kSmallMax arrivals): one 1024-thread workgroup per slab, the
+// slab's whole hex layer as a direct-mapped slot table in LDS.
+struct DenseLds {
     static constexpr int BS = kDenseBS, TAB = kDenseTab, CLAIM = kDenseClaim, NW = BS / 64;
-    unsigned long long tab[TAB];
-    uint32_t claim[2][CLAIM];   // double-buffered by chunk parity: no clearing barrier
-    uint32_t tkey[1];
-    uint32_t gcnt[kDests * kDests];
-    uint32_t doff[kDests], dcap[kDests], dcur[kDests];
-    uint32_t wcnt[NW][kDests], wpre[NW][kDests];
-    uint32_t npend[2], nwin, err;
-};
-template <>
-struct SlabLds<false> {
-    static constexpr int BS = kSmallBS, TAB = kSmallTab, CLAIM = kSmallClaim, NW = BS / 64;
-    unsigned long long tab[TAB];
-    uint32_t claim[2][CLAIM];
-    uint32_t tkey[TAB];
+    unsigned long long tab[TAB];   // occupant: (d2 bits << 33) | (child slab << 28) | j
+    uint8_t tgd[TAB];              // occupant's grandchild slab inside its child slab (0xFF: none)
+    uint32_t claim[2][CLAIM];      // double-buffered by chunk parity: no clearing barrier
     uint32_t gcnt[kDests * kDests];
     uint32_t doff[kDests], dcap[kDests], dcur[kDests];
     uint32_t wcnt[NW][kDests], wpre[NW][kDests];
@@ -746,26 +732,6 @@ struct SlabLds<false> {
 };
 
 __device__ __forceinline__ uint32_t hash_slot(uint32_t k) { return (k * 2654435761u) >> 15; }
-
-// slot -> table entry (DENSE: direct; otherwise LDS open addressing on the local slot id)
-template <bool DENSE>
-__device__ __forceinline__ int slot_entry(SlabLds<DENSE>& S, uint32_t local) {
-    if constexpr (DENSE) {
-        return (int)local;
-    } else {
-        uint32_t h = hash_slot(local) & (SlabLds<false>::TAB - 1);
-        for (int probe = 0; probe < SlabLds<false>::TAB; probe++) {
-            const uint32_t k = S.tkey[h];
-            if (k == local) return (int)h;
-            if (k == kEmpty32) {
-                const uint32_t old = atomicCAS(&S.tkey[h], kEmpty32, local);
-                if (old == kEmpty32 || old == local) return (int)h;
-            }
-            h = (h + 1) & (SlabLds<false>::TAB - 1);
-        }
-        return -1;
-    }
-}
 
 // Per-chunk claim table keyed by slot: entry = (slot << 11) | min pending thread
 // (0x7FF once that thread has been applied).  Slots < 2^14, threads < 2^10.
@@ -792,7 +758,7 @@ __device__ __forceinline__ int claim_insert(uint32_t* H, uint32_t local, uint32_
 
 // Slot-table entry: (d2 bits << 33) | (dest << 28) | j.  d2 >= +0 so its sign
 // bit is free; dest (0..23) is the occupant's child slab, so displacing it needs
-// no access to its payload; j < 2^28 indexes the slab's arrivals.
+// no access to its payload for routing; j < 2^28 indexes the slab's arrivals.
 constexpr uint32_t kJBits = 28;
 constexpr uint32_t kJMask = (1u << kJBits) - 1;
 
@@ -803,16 +769,22 @@ __device__ __forceinline__ u32x4 bld4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
 __device__ __forceinline__ void bst4(__amdgpu_buffer_rsrc_t r, uint32_t off, u32x4 v) {
     __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 0);
 }
-__device__ __forceinline__ void bst16(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t v) {
-    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)v, r, off, 0, 0);
-}
-__device__ __forceinline__ uint32_t bld16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-    return __builtin_amdgcn_raw_buffer_load_b16(r, off, 0, 0);
-}
 
-template <bool DENSE>
-__global__ __launch_bounds__(SlabLds<DENSE>::BS) void k_slab(SlabParams P) {
-    using L = SlabLds<DENSE>;
+// One pass over the slab in key order (cell.rs:70-94), one chunk of BS
+// arrivals per step, software-pipelined:
+//   phase A : slot/d2/own routes of chunk i; arrivals that cannot beat their
+//             slot's occupant overflow at once, the others (candidate records)
+//             enter the claim table; wave ranks of chunk i-1's emissions
+//   barrier : per round: apply claim winners | barrier | (round 1: stores of
+//             chunk i-1) | re-claim | barrier ...
+// An emission is the arrival itself (kind 0) or the occupant it displaced
+// (kind 1), always at the arrival's key.  A displaced occupant's payload is
+// gathered from the slab's arrivals when it is displaced and stored one step
+// later with the rest of the chunk's emissions.  After the last chunk the
+// table's occupants are the slab's grid points (cell.rs:158-160: order inside
+// a cell file is free); their payloads are gathered once.
+__global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
+    using L = DenseLds;
     constexpr int BS = L::BS, TAB = L::TAB, CLAIM = L::CLAIM, NW = L::NW;
     __shared__ L S;
     STAMP_DECL
@@ -822,7 +794,6 @@ __global__ __launch_bounds__(SlabLds<DENSE>::BS) void k_slab(SlabParams P) {
     const int32_t t = P.slab_layer[s];
     const uint32_t off = P.slab_off[s], n = P.slab_n[s], nm1 = n - 1;
     const int32_t cx = P.cell_idx[3 * cr_], cy = P.cell_idx[3 * cr_ + 1], cz = P.cell_idx[3 * cr_ + 2];
-    const uint32_t sb = P.cell_sb[cr_];
     const LevelGeo& G = P.G;
     if (n > kJMask) {   // the entry packs j in 28 bits
         if (tid == 0) set_err(P.ctr, ERR_SLAB_SIZE);
@@ -832,20 +803,15 @@ __global__ __launch_bounds__(SlabLds<DENSE>::BS) void k_slab(SlabParams P) {
     const I3 c0 = hex_from_world(cell_pos1(cx, P.cs), cell_pos1(cy, P.cs), cell_pos1(cz, P.cs), G.cr);
     const int32_t rx = c0.x - P.tx / 2, ry = c0.y - P.ty / 2;
     uint32_t err = 0;
-    // buffer descriptors: this slab's arrivals + per-arrival status/fate, and the
-    // contiguous region of its 24 child slabs in the next arena (out-of-range
-    // offsets drop a store)
+    // buffer descriptors: this slab's arrivals and the contiguous region of its
+    // 24 child slabs in the next arena (out-of-range offsets drop a store)
     const uint64_t nb = (uint64_t)n * 4;
-    const __amdgpu_buffer_rsrc_t rP = srd(P.in.p + off, nb * 4), rK = srd(P.in.k + off, nb), rE = srd(P.in.e + off, nb);
-    const __amdgpu_buffer_rsrc_t rF = srd(P.fate + off, nb), rS = srd(P.status + off, (uint64_t)n * 2);
+    const __amdgpu_buffer_rsrc_t rP = srd(P.in.p + off, nb * 4), rK = srd(P.in.k + off, nb);
     const uint32_t dbase = P.dest_off[s * kDests];
     const uint64_t db = (uint64_t)(P.dest_off[s * kDests + kDests - 1] + P.dcap[s * kDests + kDests - 1] - dbase) * 4;
-    const __amdgpu_buffer_rsrc_t oP = srd(P.nx.p + dbase, db * 4), oK = srd(P.nx.k + dbase, db), oE = srd(P.nx.e + dbase, db);
+    const __amdgpu_buffer_rsrc_t oP = srd(P.nx.p + dbase, db * 4), oK = srd(P.nx.k + dbase, db);
 
-    for (int i = tid; i < TAB; i += BS) {
-        S.tab[i] = kEmpty64;
-        if constexpr (!DENSE) S.tkey[i] = kEmpty32;
-    }
+    for (int i = tid; i < TAB; i += BS) S.tab[i] = kEmpty64;
     for (int i = tid; i < 2 * CLAIM; i += BS) (&S.claim[0][0])[i] = kEmpty32;
     for (int i = tid; i < kDests * kDests; i += BS) S.gcnt[i] = 0;
     if (tid < kDests) {
@@ -858,32 +824,25 @@ __global__ __launch_bounds__(SlabLds<DENSE>::BS) void k_slab(SlabParams P) {
     __syncthreads();
     STAMP(0);
 
-    // ---- pass 1: replay the slab in key order (cell.rs:70-94), one chunk of BS
-    // arrivals per step, software-pipelined:
-    //   phase A : slot/d2/own route of chunk i, claim inserts; wave ranks of the
-    //             emissions of chunk i-1 (stage prv)
-    //   barrier : per round: apply claim winners | barrier | (round 1: stores of
-    //             chunk i-1) check remaining | re-claim | barrier ...
-    // An emission is either the arrival itself (kind 0: full record written) or
-    // the occupant it displaced (kind 1: key/eb of the displacer written now, the
-    // occupant's payload in pass 2 through fate[]).
     struct Stage {
-        int32_t em;             // -1 none, 0 self, 1 displaced occupant
-        int32_t g;              // self emission: grandchild slab (0..23) inside its child slab, -1 none
-        uint32_t jo, d, k, e, c;
-        float x, y, z;
+        int32_t em;     // -1 none, 0 self, 1 displaced occupant
+        int32_t g;      // grandchild slab (0..23) of the emitted point inside its child slab, -1 none
+        uint32_t d, k;  // child slab of the emitted point, key (always the arrival's own)
+        u32x4 own, gp;  // own payload; gathered payload of a displaced occupant
     };
-    Stage A = {-1, -1, 0, 0, 0, 0, 0, 0.f, 0.f, 0.f};
+    Stage A;
+    A.em = -1; A.g = -1; A.d = 0; A.k = 0;
+    A.own = u32x4{0u, 0u, 0u, 0u};
+    A.gp = A.own;
     Stage B = A;
     // arrivals are prefetched two chunks ahead (buffer ci & 1)
-    struct Pre { u32x4 p; uint32_t k, e; };
+    struct Pre { u32x4 p; uint32_t k; };
     Pre pre[2];
 #pragma unroll
     for (int q = 0; q < 2; q++) {
         const uint32_t jo = min((uint32_t)(q * BS) + tid, nm1);
         pre[q].p = bld4(rP, jo * 16);
         pre[q].k = bld(rK, jo * 4);
-        pre[q].e = bld(rE, jo * 4);
     }
     const uint64_t lt = lanemask_lt();
     const uint32_t nchunks = (n + BS - 1) / BS;
@@ -892,17 +851,17 @@ __global__ __launch_bounds__(SlabLds<DENSE>::BS) void k_slab(SlabParams P) {
         uint32_t* claim = S.claim[par];
         const uint32_t j = ci * BS + tid;
         const bool valid = j < n;
-        const float x = __uint_as_float(nx.p.x), y = __uint_as_float(nx.p.y), z = __uint_as_float(nx.p.z);
-        const uint32_t c = nx.p.w, k = nx.k, eb = max(nx.e, sb);
+        const u32x4 own = nx.p;
+        const uint32_t k = nx.k;
         {   // prefetch chunk i+2 (clamped) into the buffer just consumed
             const uint32_t jo = min(j + 2 * BS, nm1);
             nx.p = bld4(rP, jo * 16);
             nx.k = bld(rK, jo * 4);
-            nx.e = bld(rE, jo * 4);
         }
-        // ---- phase A (1): slot + distance (hex.rs:67-85, 55-65) + own child slab
+        const float x = __uint_as_float(own.x), y = __uint_as_float(own.y), z = __uint_as_float(own.z);
+        // ---- phase A (1): slot + distance (hex.rs:67-85, 55-65) + own child / grandchild slab
 #ifdef PCC_STAMPS
-        if (__float_as_uint(x) == 0x7FC00001u) err |= 1u << 30;   // consume the prefetched loads here
+        if (own.x == 0x7FC00001u) err |= 1u << 30;   // consume the prefetched loads here
         STAMP(12);
 #endif
         const SlotRoute sr = slot_route(x, y, z, G);
@@ -930,32 +889,30 @@ __global__ __launch_bounds__(SlabLds<DENSE>::BS) void k_slab(SlabParams P) {
         if (d2 == 12345.0f) err |= 1u << 29;   // finish the math before the stamp
         STAMP(13);
 #endif
-        // An arrival that does not beat the slot's occupant as it stands before
+        // An arrival that does not beat its slot's occupant as it stands before
         // this chunk overflows at once (occupants only improve within a chunk,
         // cell.rs:80 strict <): only candidate records enter the claim rounds,
         // so a chunk needs as many rounds as its most contended slot has
-        // candidates, not arrivals (clustered clouds: tens of arrivals per slot).
-        int e = 0, hc = -1;
+        // candidates, not arrivals.
+        int hc = -1;
         bool self_em = false;
         if (pending) {
-            e = slot_entry<DENSE>(S, local);
-            if (e >= 0) {
-                const unsigned long long occ = S.tab[e];
-                if (occ != kEmpty64 && !(d2 < __uint_as_float((uint32_t)(occ >> 33)))) {
-                    self_em = true;
-                    pending = false;
-                } else {
-                    hc = claim_insert<CLAIM>(claim, local, tid);
-                }
+            const unsigned long long occ = S.tab[local];
+            if (occ != kEmpty64 && !(d2 < __uint_as_float((uint32_t)(occ >> 33)))) {
+                self_em = true;
+                pending = false;
+            } else {
+                hc = claim_insert<CLAIM>(claim, local, tid);
+                if (hc < 0) { err |= ERR_CLAIM; pending = false; }
             }
-            if (e < 0 || (pending && hc < 0)) { err |= ERR_CLAIM; pending = false; }
         }
         {
             const uint32_t np = (uint32_t)__popcll(__ballot(pending));
             if ((tid & 63) == 0 && np) atomicAdd(&S.npend[par], np);
         }
         STAMP(1);
-        // ---- phase A (2): wave ranks of chunk i-1's emissions per child slab
+        // ---- phase A (2): wave ranks of chunk i-1's emissions per child slab and
+        // their grandchild capacities (one LDS add per distinct (d, g) in the wave)
         const bool vd = prv.em >= 0;
         const int d = vd ? (int)prv.d : 0;
         uint64_t same = __ballot(vd);
@@ -966,8 +923,8 @@ __global__ __launch_bounds__(SlabLds<DENSE>::BS) void k_slab(SlabParams P) {
         }
         const uint32_t rw = __popcll(same & lt);
         if (vd && rw == 0) S.wcnt[wv][d] = (uint32_t)__popcll(same);
-        {   // grandchild capacities of self emissions: one LDS add per distinct (d, g) in the wave
-            const bool vg = vd && prv.em == 0 && prv.g >= 0;
+        {
+            const bool vg = vd && prv.g >= 0;
             const int32_t gg = vg ? prv.g : 0;
             uint64_t sg = same & __ballot(vg);
 #pragma unroll
@@ -987,30 +944,33 @@ __global__ __launch_bounds__(SlabLds<DENSE>::BS) void k_slab(SlabParams P) {
             for (int q = 0; q < NW; q++) { const uint32_t cc = S.wcnt[q][tid]; S.wpre[q][tid] = acc; acc += cc; S.wcnt[q][tid] = 0; }
             S.dcur[tid] = acc;
         }
-        // per round, the earliest pending arrival of every slot (min thread index
-        // = min key) is applied
-        int32_t em = self_em ? 0 : -1;
-        uint32_t emj = 0, emd = self_em ? dn : 0u;
-        bool rec = false;
+        // per round, the earliest pending candidate of every slot (min thread
+        // index = min key) is applied
+        int32_t em = self_em ? 0 : -1, emg = self_em ? gn : -1;
+        uint32_t emd = self_em ? dn : 0u;
+        u32x4 gp = u32x4{0u, 0u, 0u, 0u};
         bool first = true;
         for (;;) {
             bool won = false;
             if (pending && (claim[hc] & kClaimDone) == tid) {
-                const unsigned long long occ = S.tab[e];
+                const unsigned long long occ = S.tab[local];
                 const unsigned long long mine =
                     ((unsigned long long)f2u(d2) << 33) | ((unsigned long long)dn << kJBits) | j;
                 if (occ == kEmpty64) {
-                    S.tab[e] = mine;
-                    rec = true;
+                    S.tab[local] = mine;
+                    S.tgd[local] = (uint8_t)(gn < 0 ? 0xFF : gn);
                 } else if (d2 < __uint_as_float((uint32_t)(occ >> 33))) {  // strict: ties keep the old point
-                    S.tab[e] = mine;
-                    rec = true;
+                    const uint32_t og = S.tgd[local];
+                    S.tab[local] = mine;
+                    S.tgd[local] = (uint8_t)(gn < 0 ? 0xFF : gn);
                     em = 1;                                // displaced occupant, emitted at this arrival's key
-                    emj = (uint32_t)occ & kJMask;
                     emd = (uint32_t)(occ >> kJBits) & 31u;
+                    emg = og == 0xFFu ? -1 : (int32_t)og;
+                    gp = bld4(rP, ((uint32_t)occ & kJMask) * 16);
                 } else {
                     em = 0;                                // the arrival itself overflows
                     emd = dn;
+                    emg = gn;
                 }
                 pending = false;
                 won = true;
@@ -1030,13 +990,8 @@ __global__ __launch_bounds__(SlabLds<DENSE>::BS) void k_slab(SlabParams P) {
                 const bool ok = vd && r < S.dcap[d];
                 err |= (vd && !ok) ? (uint32_t)ERR_CAPACITY : 0u;
                 const uint32_t pos = S.doff[d] + r;
-                const uint32_t po = ok ? pos * 4 : 0xFFFFFFFFu;
-                const uint32_t ps = (ok && prv.em == 0) ? pos * 16 : 0xFFFFFFFFu;
-                u32x4 rec;
-                rec.x = __float_as_uint(prv.x); rec.y = __float_as_uint(prv.y); rec.z = __float_as_uint(prv.z); rec.w = prv.c;
-                bst4(oP, ps, rec);
-                bst(oK, po, prv.k); bst(oE, po, prv.e);
-                bst(rF, (ok && prv.em == 1) ? prv.jo * 4 : 0xFFFFFFFFu, pos);
+                bst4(oP, ok ? pos * 16 : 0xFFFFFFFFu, prv.em == 1 ? prv.gp : prv.own);
+                bst(oK, ok ? pos * 4 : 0xFFFFFFFFu, prv.k);
                 STAMP(6);
             }
             if (S.npend[par] == 0) break;
@@ -1046,9 +1001,7 @@ __global__ __launch_bounds__(SlabLds<DENSE>::BS) void k_slab(SlabParams P) {
             STAMP(5);
         }
         if (hc >= 0) claim[hc] = kEmpty32;   // this buffer is next used two chunks later
-        // status: table entry + 1 of every arrival that became a slot record
-        bst16(rS, valid ? j * 2 : 0xFFFFFFFFu, rec ? (uint32_t)e + 1u : 0u);
-        cur.em = em; cur.g = gn; cur.jo = emj; cur.d = emd; cur.k = k; cur.e = eb; cur.c = c; cur.x = x; cur.y = y; cur.z = z;
+        cur.em = em; cur.g = emg; cur.d = emd; cur.k = k; cur.own = own; cur.gp = gp;
         STAMP(7);
         STAMP_COUNT(10, 1);
     };
@@ -1058,64 +1011,32 @@ __global__ __launch_bounds__(SlabLds<DENSE>::BS) void k_slab(SlabParams P) {
         step(ci + 1, B, A, pre[1]);
     }
     STAMP(7);
-    __syncthreads();   // also orders this workgroup's status/fate stores before pass 2 reads them
+    __syncthreads();
     STAMP(11);
 
-    // ---- pass 2: stream the slab's arrivals once.  A record whose table entry
-    // still holds it is this slab's grid point (cell.rs:158-160: order inside a
-    // cell is free); any other record was displaced, and its payload goes to the
-    // emission position stored in fate[].
-    constexpr int U = 4;
+    // ---- grid points: the table's occupants, payloads gathered with U loads in
+    // flight per thread, compacted into the slab's grid region
+    constexpr int U = 8;
     const __amdgpu_buffer_rsrc_t rG = srd(P.grid + P.grid_off[s], (uint64_t)n * 16);
-    for (uint32_t j0 = 0; j0 < n; j0 += U * BS) {
-        uint32_t st[U];
+    for (int i0 = 0; i0 < TAB; i0 += U * BS) {
+        uint32_t wpos[U], src[U];
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            const uint32_t j = j0 + u * BS + tid;
-            st[u] = bld16(rS, j < n ? j * 2 : 0xFFFFFFFFu);
-        }
-        uint32_t wpos[U], fpos[U], src[U];
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            const uint32_t j = j0 + u * BS + tid;
-            bool win = false, dsp = false;
-            if (st[u]) {
-                const unsigned long long occ = S.tab[st[u] - 1];
-                win = ((uint32_t)occ & kJMask) == j;
-                dsp = !win;
-            }
+            const int i = i0 + u * BS + (int)tid;
+            const unsigned long long occ = i < TAB ? S.tab[i] : kEmpty64;
+            const bool win = occ != kEmpty64;
             const uint64_t m = __ballot(win);
             uint32_t wb = 0;
             if ((tid & 63) == 0 && m) wb = atomicAdd(&S.nwin, (uint32_t)__popcll(m));
             wb = __shfl(wb, 0, 64);
             wpos[u] = win ? (wb + (uint32_t)__popcll(m & lt)) * 16 : 0xFFFFFFFFu;
-            fpos[u] = dsp ? 0u : 0xFFFFFFFFu;
-            src[u] = (win || dsp) ? j : 0xFFFFFFFFu;
+            src[u] = win ? ((uint32_t)occ & kJMask) * 16 : 0xFFFFFFFFu;
         }
-        uint32_t fp[U];
         u32x4 pv[U];
 #pragma unroll
-        for (int u = 0; u < U; u++) {
-            fp[u] = bld(rF, fpos[u] == 0u ? src[u] * 4 : 0xFFFFFFFFu);
-            pv[u] = bld4(rP, src[u] == 0xFFFFFFFFu ? 0xFFFFFFFFu : src[u] * 16);
-        }
+        for (int u = 0; u < U; u++) pv[u] = bld4(rP, src[u]);
 #pragma unroll
-        for (int u = 0; u < U; u++) {
-            bst4(rG, wpos[u], pv[u]);
-            bst4(oP, fpos[u] == 0u ? fp[u] * 16 : 0xFFFFFFFFu, pv[u]);
-        }
-#pragma unroll
-        for (int u = 0; u < U; u++) {   // grandchild capacities of displaced emissions
-            if (fpos[u] == 0u) {
-                const float x = __uint_as_float(pv[u].x), y = __uint_as_float(pv[u].y), z = __uint_as_float(pv[u].z);
-                const SlotRoute sr = slot_route(x, y, z, G);
-                uint32_t rerr = 0, gerr = 0;
-                const int d = route_dest(sr.rc, cx, cy, cz, t, rerr);
-                const int g = route_dest(sr.rg, sr.rc.ix, sr.rc.iy, sr.rc.iz, sr.rc.u, gerr);
-                err |= rerr | ((P.check_gchild && d >= 0) ? gerr : 0u);
-                if (d >= 0 && g >= 0) atomicAdd(&S.gcnt[d * kDests + g], 1u);
-            }
-        }
+        for (int u = 0; u < U; u++) bst4(rG, wpos[u], pv[u]);
     }
     STAMP(8);
     STAMP_FLUSH(P.stamps);
@@ -1211,7 +1132,7 @@ __global__ void k_small_desc(const uint32_t* list, uint32_t nlist, const uint32_
 // Per-thread register copy of one small slab's inputs (loaded one slab ahead).
 struct SmallPre {
     u32x4 pp[kSmallCh];
-    uint32_t pk[kSmallCh], pe[kSmallCh];
+    uint32_t pk[kSmallCh];
     uint32_t doff, dcap;
 };
 
@@ -1220,14 +1141,13 @@ __device__ __forceinline__ void small_prefetch(const SlabParams& P, uint32_t li,
     if (li >= P.nlist) return;   // block-uniform
     D = P.sdesc[li];
     const uint64_t nb = (uint64_t)D.n * 4;
-    const __amdgpu_buffer_rsrc_t rP = srd(P.in.p + D.off, nb * 4), rK = srd(P.in.k + D.off, nb), rE = srd(P.in.e + D.off, nb);
+    const __amdgpu_buffer_rsrc_t rP = srd(P.in.p + D.off, nb * 4), rK = srd(P.in.k + D.off, nb);
 #pragma unroll
     for (int c = 0; c < kSmallCh; c++) {
         const uint32_t j = c * kSmallBS + tid;
         const bool v = j < D.n;
         R.pp[c] = bld4(rP, v ? j * 16 : 0xFFFFFFFFu);
         R.pk[c] = bld(rK, v ? j * 4 : 0xFFFFFFFFu);
-        R.pe[c] = bld(rE, v ? j * 4 : 0xFFFFFFFFu);
     }
     const __amdgpu_buffer_rsrc_t rD = srd(P.dest_off + (uint64_t)D.s * kDests, kDests * 4);
     const __amdgpu_buffer_rsrc_t rC = srd(P.dcap + (uint64_t)D.s * kDests, kDests * 4);
@@ -1246,16 +1166,14 @@ __device__ __forceinline__ void small_process(const SlabParams& P, SmallLds& S, 
     const uint32_t dbase = D.dbase;
     const uint64_t db = (uint64_t)D.dlen * 4;
     const int32_t cx = D.cx, cy = D.cy, cz = D.cz;
-    const uint32_t sb = D.sb;
     const LevelGeo& G = P.G;
     const uint32_t nch = (n + BS - 1) / BS;
     uint32_t cap = 64;
     while (cap < 2 * n && cap < (uint32_t)kSmallTab) cap <<= 1;
     const uint32_t mask = cap - 1;
-    const __amdgpu_buffer_rsrc_t oP = srd(P.nx.p + dbase, db * 4), oK = srd(P.nx.k + dbase, db), oE = srd(P.nx.e + dbase, db);
+    const __amdgpu_buffer_rsrc_t oP = srd(P.nx.p + dbase, db * 4), oK = srd(P.nx.k + dbase, db);
     u32x4* pp = R.pp;
     uint32_t* pk = R.pk;
-    uint32_t* pe = R.pe;
     for (uint32_t i = tid; i < cap; i += BS) { S.tab[i] = kEmpty64; S.tkey[i] = kEmpty32; }
     for (int i = tid; i < 2 * kSmallClaim; i += BS) (&S.claim[0][0])[i] = kEmpty32;
     for (int i = tid; i < kDests * kDests; i += BS) S.gcnt[i] = 0;
@@ -1409,7 +1327,6 @@ __device__ __forceinline__ void small_process(const SlabParams& P, SmallLds& S, 
                     const int pc = ci - 1 < CH ? ci - 1 : 0;
                     bst4(oP, (ok && em == 0) ? pos * 16 : 0xFFFFFFFFu, pp[pc]);
                     bst(oK, po, pk[pc]);
-                    bst(oE, po, max(pe[pc], sb));
                 }
                 if (ok && em == 1) S.fate[emj] = pos;
                 STAMP(6);
@@ -1529,24 +1446,23 @@ __global__ __launch_bounds__(64) void k_slab_wave(SlabParams P) {
     const LevelGeo& G = P.G;
     for (uint32_t li = blockIdx.x; li < P.nwave; li += gridDim.x) {
         const SmallDesc D = P.wdesc[li];
-        const uint32_t s = D.s, n = D.n, off = D.off, dbase = D.dbase, sb = D.sb;
+        const uint32_t s = D.s, n = D.n, off = D.off, dbase = D.dbase;
         const int32_t t = D.t, cx = D.cx, cy = D.cy, cz = D.cz;
         const uint32_t nch = (n + 63) / 64;
         uint32_t cap = 64;
         while (cap < 2 * n && cap < (uint32_t)kWaveTab) cap <<= 1;
         const uint32_t mask = cap - 1;
         const uint64_t nb = (uint64_t)n * 4, db = (uint64_t)D.dlen * 4;
-        const __amdgpu_buffer_rsrc_t rP = srd(P.in.p + off, nb * 4), rK = srd(P.in.k + off, nb), rE = srd(P.in.e + off, nb);
-        const __amdgpu_buffer_rsrc_t oP = srd(P.nx.p + dbase, db * 4), oK = srd(P.nx.k + dbase, db), oE = srd(P.nx.e + dbase, db);
+        const __amdgpu_buffer_rsrc_t rP = srd(P.in.p + off, nb * 4), rK = srd(P.in.k + off, nb);
+        const __amdgpu_buffer_rsrc_t oP = srd(P.nx.p + dbase, db * 4), oK = srd(P.nx.k + dbase, db);
         u32x4 pp[CH];
-        uint32_t pk[CH], pe[CH];
+        uint32_t pk[CH];
 #pragma unroll
         for (int c = 0; c < CH; c++) {
             const uint32_t j = c * 64 + lane;
             const bool v = j < n;
             pp[c] = bld4(rP, v ? j * 16 : 0xFFFFFFFFu);
             pk[c] = bld(rK, v ? j * 4 : 0xFFFFFFFFu);
-            pe[c] = max(bld(rE, v ? j * 4 : 0xFFFFFFFFu), sb);
         }
         for (uint32_t i = lane; i < cap; i += 64) { W.tab[i] = kEmpty64; W.tkey[i] = kEmpty32; }
         if (lane < kDests) {
@@ -1653,7 +1569,6 @@ __global__ __launch_bounds__(64) void k_slab_wave(SlabParams P) {
             const uint32_t po = ok ? pos * 4 : 0xFFFFFFFFu;
             bst4(oP, (ok && em == 0) ? pos * 16 : 0xFFFFFFFFu, pp[c]);
             bst(oK, po, pk[c]);
-            bst(oE, po, pe[c]);
             if (ok && em == 1) W.fate[emj] = (uint16_t)pos;
             wave_add_by_key(gcap_s, ok && em == 0 && g >= 0, (uint32_t)(dd * kDests + (g < 0 ? 0 : g)), lt);
         }
@@ -1741,6 +1656,9 @@ __global__ __launch_bounds__(256) void k_dcap(DcapParams P) {
 // ------------------------------------------------------------------ bucket resolution
 struct BucketParams {
     Arena nx;          // arrivals of level h+1 (== emissions of level h)
+    const uint32_t* files;    // event batches from keys (lib.rs:31-52)
+    uint32_t nfiles;
+    const uint32_t* cell_sb;  // running spill batch of the level-h cells
     Point* kept;
     uint64_t kept_cap;
     const uint32_t* cell_slab0;
@@ -1757,12 +1675,17 @@ struct BucketParams {
 
 constexpr int kBktBS = 256;
 
+// event batch of an emission of a level-h cell: max(eb0(key), cell's running sb)
+__device__ __forceinline__ uint32_t emission_eb(const BucketParams& B, uint32_t key, uint32_t csb) {
+    return max(event_batch(B.files, B.nfiles, key), csb);
+}
 // number of elements with eb <= e among the first min(n, cap) of a key-ordered dest list
-__device__ __forceinline__ uint32_t count_le(const uint32_t* E, uint32_t off, uint32_t n, uint32_t cap, uint32_t e) {
+__device__ __forceinline__ uint32_t count_le(const BucketParams& B, uint32_t off, uint32_t n, uint32_t cap, uint32_t e,
+                                             uint32_t csb) {
     uint32_t lo = 0, hi = n < cap ? n : cap;
     while (lo < hi) {
         uint32_t mid = (lo + hi) >> 1;
-        if (E[off + mid] <= e) lo = mid + 1; else hi = mid;
+        if (emission_eb(B, B.nx.k[off + mid], csb) <= e) lo = mid + 1; else hi = mid;
     }
     return lo;
 }
@@ -1779,6 +1702,7 @@ __global__ __launch_bounds__(kBktBS) void k_bucket(BucketParams B) {
     const uint32_t s0 = B.cell_slab0[cell], s1 = B.cell_slab0[cell + 1];
     const uint32_t nd = (s1 - s0) * 3;
     const uint32_t L = B.L;
+    const uint32_t csb = B.cell_sb[cell];
     uint32_t tot = 0, nne = 0, emin = 0xFFFFFFFFu, emax = 0;
     for (uint32_t i = threadIdx.x; i < nd; i += kBktBS) {
         const uint32_t di = (s0 + i / 3) * kDests + oct * 3 + i % 3;
@@ -1787,8 +1711,8 @@ __global__ __launch_bounds__(kBktBS) void k_bucket(BucketParams B) {
             const uint32_t o = B.dest_off[di];
             tot += n;
             nne++;
-            emin = min(emin, B.nx.e[o]);
-            emax = max(emax, B.nx.e[o + n - 1]);
+            emin = min(emin, emission_eb(B, B.nx.k[o], csb));
+            emax = max(emax, emission_eb(B, B.nx.k[o + n - 1], csb));
         }
     }
     if (threadIdx.x == 0) { s_min = 0xFFFFFFFFu; s_max = 0; }
@@ -1862,7 +1786,7 @@ __global__ __launch_bounds__(kBktBS) void k_bucket(BucketParams B) {
         for (uint32_t i = threadIdx.x; i < nd; i += kBktBS) {
             const uint32_t di = (s0 + i / 3) * kDests + oct * 3 + i % 3;
             const uint32_t n = B.dest_n[di];
-            if (n) c += count_le(B.nx.e, B.dest_off[di], n, L + 1, e);
+            if (n) c += count_le(B, B.dest_off[di], n, L + 1, e, csb);
         }
         return block_sum<kBktBS>(c, lds);
     };
@@ -2097,10 +2021,8 @@ void Engine::free_all() {
     levels_.clear();
     if (dev_) {
         for (int a = 0; a < 2; a++) {
-            (void)hipFree(dev_->ar[a].p); (void)hipFree(dev_->ar[a].k); (void)hipFree(dev_->ar[a].e);
+            (void)hipFree(dev_->ar[a].p); (void)hipFree(dev_->ar[a].k);
         }
-        (void)hipFree(dev_->fate);
-        (void)hipFree(dev_->status);
         (void)hipFree(dev_->ctr);
         (void)hipFree(dev_->bbox_part);
         (void)hipFree(dev_->bbox_flag);
@@ -2234,12 +2156,9 @@ int Engine::build() {
     if (dev_->cap < n_) {
         for (int a = 0; a < 2; a++) {
             Arena& A = dev_->ar[a];
-            (void)hipFree(A.p); (void)hipFree(A.k); (void)hipFree(A.e);
-            HIP_CHECK(hipMalloc(&A.p, n_ * 16)); HIP_CHECK(hipMalloc(&A.k, n_ * 4)); HIP_CHECK(hipMalloc(&A.e, n_ * 4));
+            (void)hipFree(A.p); (void)hipFree(A.k);
+            HIP_CHECK(hipMalloc(&A.p, n_ * 16)); HIP_CHECK(hipMalloc(&A.k, n_ * 4));
         }
-        (void)hipFree(dev_->fate); (void)hipFree(dev_->status);
-        HIP_CHECK(hipMalloc(&dev_->fate, n_ * 4));
-        HIP_CHECK(hipMalloc(&dev_->status, n_ * 2));
         dev_->cap = n_;
     }
     // file table for event batches
@@ -2532,8 +2451,6 @@ int Engine::run_level(uint32_t h) {
     SP.dest_off = L->dest_off;
     SP.slab_grid_n = L->slab_grid_n;
     SP.dest_n = L->dest_n;
-    SP.fate = dev_->fate;       // indexed by arena position (slab_off + j), reused by every level
-    SP.status = dev_->status;
     SP.gcap = L->gcap;
     SP.check_gchild = (h + 2 < kMaxDepth) ? 1 : 0;
     SP.ctr = dev_->ctr;
@@ -2576,7 +2493,7 @@ int Engine::run_level(uint32_t h) {
         SP.stamps = stamps;
 #endif
         ev_begin(ST_DENSE);
-        k_slab<true><<<L->nbig, kDenseBS, 0, stream_>>>(SP);
+        k_slab<<<L->nbig, kDenseBS, 0, stream_>>>(SP);
         ev_end(ST_DENSE);
         if (verbose) {
             HIP_CHECK(hipStreamSynchronize(stream_));
@@ -2615,6 +2532,9 @@ int Engine::run_level(uint32_t h) {
     HIP_CHECK(hipGetLastError());
     BucketParams BP;
     BP.nx = nx;
+    BP.files = dev_->files;
+    BP.nfiles = (uint32_t)file_start_.size();
+    BP.cell_sb = L->cell_sb;
     BP.kept = L->kept;
     BP.kept_cap = L->kept_cap;
     BP.cell_slab0 = L->cell_slab0;
