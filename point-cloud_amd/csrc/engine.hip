@@ -827,37 +827,43 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
     struct Stage {
         int32_t em;     // -1 none, 0 self, 1 displaced occupant
         int32_t g;      // grandchild slab (0..23) of the emitted point inside its child slab, -1 none
-        uint32_t d, k;  // child slab of the emitted point, key (always the arrival's own)
-        u32x4 own, gp;  // own payload; gathered payload of a displaced occupant
+        uint32_t d;     // child slab of the emitted point
+        u32x4 gp;       // gathered payload of a displaced occupant
     };
     Stage A;
-    A.em = -1; A.g = -1; A.d = 0; A.k = 0;
-    A.own = u32x4{0u, 0u, 0u, 0u};
-    A.gp = A.own;
+    A.em = -1; A.g = -1; A.d = 0;
+    A.gp = u32x4{0u, 0u, 0u, 0u};
     Stage B = A;
-    // arrivals are prefetched two chunks ahead (buffer ci & 1)
+    // Arrivals are prefetched two chunks ahead into a ring of four register
+    // buffers: chunk i lives in buf[i % 4] from its load (step i-2) to its
+    // emission store (step i+1), so no loaded register is ever copied (a copy
+    // would wait for the load, and vmcnt also counts the stores issued since).
     struct Pre { u32x4 p; uint32_t k; };
-    Pre pre[2];
+    Pre pre[4];
 #pragma unroll
-    for (int q = 0; q < 2; q++) {
+    for (int q = 0; q < 4; q++) {
         const uint32_t jo = min((uint32_t)(q * BS) + tid, nm1);
-        pre[q].p = bld4(rP, jo * 16);
-        pre[q].k = bld(rK, jo * 4);
+        if (q < 2) {
+            pre[q].p = bld4(rP, jo * 16);
+            pre[q].k = bld(rK, jo * 4);
+        } else {
+            pre[q].p = u32x4{0u, 0u, 0u, 0u};
+            pre[q].k = 0;
+        }
     }
     const uint64_t lt = lanemask_lt();
     const uint32_t nchunks = (n + BS - 1) / BS;
-    auto step = [&](uint32_t ci, Stage& cur, Stage& prv, Pre& nx) {
+    auto step = [&](uint32_t ci, Stage& cur, Stage& prv, const Pre& mine, const Pre& prvb, Pre& pf) {
         const uint32_t par = ci & 1;
         uint32_t* claim = S.claim[par];
         const uint32_t j = ci * BS + tid;
         const bool valid = j < n;
-        const u32x4 own = nx.p;
-        const uint32_t k = nx.k;
-        {   // prefetch chunk i+2 (clamped) into the buffer just consumed
+        {   // prefetch chunk i+2 (clamped)
             const uint32_t jo = min(j + 2 * BS, nm1);
-            nx.p = bld4(rP, jo * 16);
-            nx.k = bld(rK, jo * 4);
+            pf.p = bld4(rP, jo * 16);
+            pf.k = bld(rK, jo * 4);
         }
+        const u32x4 own = mine.p;
         const float x = __uint_as_float(own.x), y = __uint_as_float(own.y), z = __uint_as_float(own.z);
         // ---- phase A (1): slot + distance (hex.rs:67-85, 55-65) + own child / grandchild slab
 #ifdef PCC_STAMPS
@@ -948,7 +954,7 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
         // index = min key) is applied
         int32_t em = self_em ? 0 : -1, emg = self_em ? gn : -1;
         uint32_t emd = self_em ? dn : 0u;
-        u32x4 gp = u32x4{0u, 0u, 0u, 0u};
+        uint32_t gsrc = 0xFFFFFFFFu;   // byte offset of a displaced occupant's payload
         bool first = true;
         for (;;) {
             bool won = false;
@@ -966,7 +972,7 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
                     em = 1;                                // displaced occupant, emitted at this arrival's key
                     emd = (uint32_t)(occ >> kJBits) & 31u;
                     emg = og == 0xFFu ? -1 : (int32_t)og;
-                    gp = bld4(rP, ((uint32_t)occ & kJMask) * 16);
+                    gsrc = ((uint32_t)occ & kJMask) * 16;
                 } else {
                     em = 0;                                // the arrival itself overflows
                     emd = dn;
@@ -990,8 +996,8 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
                 const bool ok = vd && r < S.dcap[d];
                 err |= (vd && !ok) ? (uint32_t)ERR_CAPACITY : 0u;
                 const uint32_t pos = S.doff[d] + r;
-                bst4(oP, ok ? pos * 16 : 0xFFFFFFFFu, prv.em == 1 ? prv.gp : prv.own);
-                bst(oK, ok ? pos * 4 : 0xFFFFFFFFu, prv.k);
+                bst4(oP, ok ? pos * 16 : 0xFFFFFFFFu, prv.em == 1 ? prv.gp : prvb.p);
+                bst(oK, ok ? pos * 4 : 0xFFFFFFFFu, prvb.k);
                 STAMP(6);
             }
             if (S.npend[par] == 0) break;
@@ -1001,14 +1007,22 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
             STAMP(5);
         }
         if (hc >= 0) claim[hc] = kEmpty32;   // this buffer is next used two chunks later
-        cur.em = em; cur.g = emg; cur.d = emd; cur.k = k; cur.own = own; cur.gp = gp;
+        // gather outside the divergent apply branches (a load into registers that
+        // another branch writes would force a full vmcnt drain); consumed one step later
+        cur.gp = bld4(rP, gsrc);
+        cur.em = em; cur.g = emg; cur.d = emd;
         STAMP(7);
         STAMP_COUNT(10, 1);
     };
-    // nchunks + 1 steps (the last one only emits), rounded up to an even count
-    for (uint32_t ci = 0; ci <= nchunks; ci += 2) {
-        step(ci, A, B, pre[0]);
-        step(ci + 1, B, A, pre[1]);
+    // nchunks + 1 steps (the last one only emits)
+    for (uint32_t ci = 0; ci <= nchunks; ci += 4) {
+        step(ci, A, B, pre[0], pre[3], pre[2]);
+        if (ci + 1 > nchunks) break;
+        step(ci + 1, B, A, pre[1], pre[0], pre[3]);
+        if (ci + 2 > nchunks) break;
+        step(ci + 2, A, B, pre[2], pre[1], pre[0]);
+        if (ci + 3 > nchunks) break;
+        step(ci + 3, B, A, pre[3], pre[2], pre[1]);
     }
     STAMP(7);
     __syncthreads();
