@@ -74,8 +74,12 @@ typedef struct pcc_converter pcc_converter;
 int pcc_options_default(pcc_options* opt);
 
 /* lib.rs:86-101 load_metadata + converter.rs:79-94 Converter::new.
- * Creates out_dir.  An existing metadata.json supplies the config; merging into
- * an existing non-empty cloud is not supported yet (-ENOTSUP). */
+ * Creates out_dir.  An existing metadata.json supplies the config; when it
+ * describes a non-empty cloud, every h_{h}/c_*.bin cell is loaded as the
+ * starting state (converter.rs:187-207 load_or_create_cell) and the points added
+ * afterwards are merged into it (incremental merge: the result equals converting
+ * the old and the new files in one run).  Merging is single-GPU (-95 with
+ * pcc_declare_files). */
 int pcc_open(const char* out_dir, const pcc_options* opt, pcc_converter** out);
 
 /* converter.rs:106-112 add_points_batch over ceil(n/batch) consecutive slices

@@ -54,6 +54,8 @@ def lib():
         L.orc_hierarchies.argtypes = [C.c_void_p]
         L.orc_hierarchies.restype = C.c_uint32
         L.orc_synth.argtypes = [C.c_uint64, C.c_int, C.c_uint64, C.c_uint64, C.c_float, C.c_float, C.c_void_p]
+        L.orc_load.argtypes = [C.c_void_p, C.c_char_p]
+        L.orc_load.restype = C.c_int
         _lib = L
     return _lib
 
@@ -83,6 +85,13 @@ class Oracle:
     def add_batch(self, pts: np.ndarray):
         pts = np.ascontiguousarray(pts, dtype=POINT_DTYPE)
         lib().orc_add_batch(self._h, pts.ctypes.data, len(pts))
+
+    def load(self, out_dir: str):
+        """Existing converted cloud as the starting state (lib.rs:86-101 +
+        converter.rs:187-207): its metadata.json config replaces this oracle's."""
+        r = lib().orc_load(self._h, out_dir.encode())
+        if r:
+            raise OSError(-r, "oracle load failed", out_dir)
 
     def write(self, out_dir: str):
         r = lib().orc_write(self._h, out_dir.encode())

@@ -96,6 +96,11 @@ def _pos(pt):
     return tuple(np.uint32(pt[a]).view(np.float32) for a in range(3))
 
 
+def _unpt(pt):
+    """inverse of _pt: (x, y, z float32, rgba tuple)."""
+    return _pos(pt) + (pt[3],)
+
+
 # --------------------------------------------------------------------------- sequential
 class _Cell:
     def __init__(self, h, idx, cfg):
@@ -108,10 +113,24 @@ class _Cell:
         self.buckets = {}   # child idx -> list | None
 
 
-def convert_sequential(files, cfg, batch=10_000):
-    """files: list of point lists (each point = (x, y, z, rgba)).  lib.rs:11-60."""
+def convert_sequential(files, cfg, batch=10_000, prior=None):
+    """files: list of point lists (each point = (x, y, z, rgba)).  lib.rs:11-60.
+
+    prior: optional (canonical cells, canonical metadata) of an existing cloud
+    (tests/canon.py form) = the state lib.rs:86-101 + converter.rs:187-207
+    load from disk before the new files are added (incremental merge)."""
     cells = {}
     meta = dict(number_of_points=0, hierarchies=0, bmin=None, bmax=None)
+    if prior is not None:
+        pcells, pmeta = prior
+        meta = dict(number_of_points=pmeta["number_of_points"], hierarchies=pmeta["hierarchies"],
+                    bmin=[F(v) for v in pmeta["bmin"]], bmax=[F(v) for v in pmeta["bmax"]])
+        for key, pc in pcells.items():
+            c = _Cell(key[0], tuple(key[1:]), cfg)
+            c.total, c.number, c.overflow = pc["header"][:3]
+            c.grid = {s: _unpt(p) for s, p in pc["grid"]}
+            c.buckets = {ci: (None if b is None else [_unpt(p) for p in b]) for ci, b in pc["buckets"]}
+            cells[(key[0], tuple(key[1:]))] = c
     L = cfg["cell_point_overflow_limit"]
 
     def add_in_hierarchy(h, groups):  # converter.rs:114-139

@@ -1,7 +1,9 @@
 // capi.cpp — extern "C" boundary (include/pcconv.h) over pcc::Engine.
 #include <sys/stat.h>
 
+#include <algorithm>
 #include <cerrno>
+#include <cmath>
 #include <chrono>
 #include <cstdarg>
 #include <cstdio>
@@ -62,6 +64,8 @@ struct pcc_converter {
     bool keyed = false;         // pcc_declare_files: sharded input
     bool summary_set = false;   // pcc_set_summary: global metadata values
     double build_ms = 0;
+    bool merge = false;         // out_dir held a non-empty cloud: incremental merge
+    Metadata prior;             // its metadata.json
 };
 
 #define GUARD_BEGIN try {
@@ -107,9 +111,11 @@ int pcc_open(const char* out_dir, const pcc_options* opt, pcc_converter** out) {
         std::string err;
         Metadata m;
         if (!parse_metadata_json(ss.str(), m, err)) return set_err(-EINVAL, err);
-        if (m.number_of_points > 0)
-            return set_err(-ENOTSUP, "incremental merge into an existing point cloud is not supported by the GPU build yet");
         c->meta.config = m.config;
+        if (m.number_of_points > 0) {
+            c->merge = true;
+            c->prior = m;
+        }
     }
     // converter.rs:79-94 create_dir_all
     if (!mkdirs(c->out_dir)) return set_err(-EIO, "cannot create output directory " + c->out_dir);
@@ -118,6 +124,16 @@ int pcc_open(const char* out_dir, const pcc_options* opt, pcc_converter** out) {
         return set_err(-ENODEV, "no HIP device available: the MI355X build needs a GPU (there is no CPU fallback)");
     if (c->opt.device < 0 || c->opt.device >= ndev) return set_err(-ENODEV, "invalid HIP device ordinal");
     c->eng = std::make_unique<Engine>(c->meta.config, c->opt.device);
+    if (c->merge) {   // converter.rs:187-207: existing cells are the starting state
+        std::vector<CellFile> cells;
+        std::string err;
+        int rc = read_cloud(c->out_dir, c->prior.hierarchies, cells, err);
+        if (rc) return set_err(rc, err);
+        PriorState ps;
+        rc = prior_from_cells(cells, c->meta.config, ps, err);
+        if (rc) return set_err(rc, err);
+        c->eng->set_prior(ps);
+    }
     *out = c.release();
     return 0;
     GUARD_END
@@ -176,6 +192,15 @@ int pcc_build(pcc_converter* c) {
     m.hierarchies = c->eng->hierarchies();
     if (m.number_of_points > 0)
         for (int a = 0; a < 3; a++) { m.bmin[a] = c->eng->bbox_min()[a]; m.bmax[a] = c->eng->bbox_max()[a]; }
+    if (c->merge) {   // lib.rs:86-101: counters continue from the loaded metadata; Aabb::extend_aabb
+        const Metadata& p = c->prior;
+        if (m.number_of_points == 0)
+            for (int a = 0; a < 3; a++) { m.bmin[a] = p.bmin[a]; m.bmax[a] = p.bmax[a]; }
+        else
+            for (int a = 0; a < 3; a++) { m.bmin[a] = std::fmin(m.bmin[a], p.bmin[a]); m.bmax[a] = std::fmax(m.bmax[a], p.bmax[a]); }
+        m.number_of_points += p.number_of_points;
+        m.hierarchies = std::max(m.hierarchies, p.hierarchies);
+    }
     return 0;
     GUARD_END
 }
@@ -338,6 +363,10 @@ int pcc_get_stats(const pcc_converter* c, pcc_stats* s) {
     const BuildStats& b = c->eng->stats();
     s->number_of_points = c->eng->num_points();
     s->hierarchies = c->eng->hierarchies();
+    if (c->merge && c->built) {   // merged cloud: metadata values (existing + new)
+        s->number_of_points = c->meta.number_of_points;
+        s->hierarchies = c->meta.hierarchies;
+    }
     s->levels = b.levels;
     s->cells = b.cells;
     s->slabs = b.slabs;

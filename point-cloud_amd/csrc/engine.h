@@ -37,6 +37,23 @@ struct LevelHost {
     uint64_t kept_base = 0;             // offset of this level's kept lists in the downloaded kept array
 };
 
+// Existing cloud loaded for an incremental merge (lib.rs:86-101 +
+// converter.rs:187-207).  Seeds are ALL its points in
+// key order: per level h, first the grid points of every level-h cell, then the
+// points of every kept (Some) list in stored order.  A seed enters the build at
+// level 0 like any input point; at levels above its own it is a forced
+// emission (it passes through None buckets down to its cell), at its own level
+// a grid seed takes its slot (it precedes every new point, so it wins every
+// tie) and a kept seed is a forced emission into its bucket, ahead of the new
+// emissions.  forced_lo[h] = first key of level h's kept seeds: at level h every
+// key in [forced_lo[h], S) is forced.
+struct PriorCell { int32_t x, y, z; uint32_t st; };   // st: 2 bits per octant: 0 absent, 1 Some, 2 None
+struct PriorState {
+    std::vector<Point> seeds;
+    std::vector<uint64_t> forced_lo;                 // per prior level
+    std::vector<std::vector<PriorCell>> cells;       // per prior level, sorted by (x, y, z)
+};
+
 struct StageProfile {
     double level0_ms = 0, dense_ms = 0, small_ms = 0, bucket_ms = 0, next_ms = 0;
     uint64_t dense_arrivals = 0, small_arrivals = 0;
@@ -77,6 +94,9 @@ public:
     void add_keyed_device(const Point* dpts, const uint32_t* dkeys, uint64_t n);
     // Drops all input (points, keys, files) but keeps device allocations.
     void clear_input();
+    // Incremental merge: the existing cloud's state (kept until the engine dies).
+    void set_prior(const PriorState& p);
+    bool has_prior() const { return prior_; }
 
     // Run the whole build on the device.  Returns 0 or a negative error code
     // (message in last_error()).  Input must already be resident.
@@ -120,6 +140,19 @@ private:
     std::vector<uint32_t> file_batch_;   // batch size per file
     Point* d_in_ = nullptr;
     uint32_t* d_keys_ = nullptr;         // keyed (sharded) input: global key per point
+    // build source: d_in_ (n_ points) or, when merging, [seeds | d_in_]
+    const Point* src_ = nullptr;
+    uint64_t nsrc_ = 0;
+    uint32_t nfiles_dev_ = 0;            // entries of the device file table
+    bool prior_ = false;
+    Point* d_seeds_ = nullptr;
+    uint64_t nseeds_ = 0;
+    Point* d_comb_ = nullptr;
+    uint64_t comb_cap_ = 0;
+    bool comb_ok_ = false;
+    std::vector<uint64_t> forced_lo_;
+    std::vector<uint32_t*> d_prior_cells_;   // PriorCell arrays per level
+    std::vector<uint32_t> n_prior_cells_;
     uint64_t keys_cap_ = 0;
     bool keyed_ = false;
     Dev* dev_ = nullptr;

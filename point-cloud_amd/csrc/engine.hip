@@ -715,6 +715,7 @@ struct SlabParams {
     LevelGeo G;
     int32_t tx, ty;
     int32_t check_gchild;
+    uint32_t kf_lo, kf_n;         // merge mode: keys in [kf_lo, kf_lo + kf_n) are forced emissions (engine.h PriorState)
     unsigned long long* stamps;   // diagnostic build only
 };
 
@@ -858,6 +859,7 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
         uint32_t* claim = S.claim[par];
         const uint32_t j = ci * BS + tid;
         const bool valid = j < n;
+        const bool forced = valid && mine.k - P.kf_lo < P.kf_n;
         {   // prefetch chunk i+2 (clamped)
             const uint32_t jo = min(j + 2 * BS, nm1);
             pf.p = bld4(rP, jo * 16);
@@ -901,7 +903,8 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
         // so a chunk needs as many rounds as its most contended slot has
         // candidates, not arrivals.
         int hc = -1;
-        bool self_em = false;
+        bool self_em = forced && pending;
+        pending = pending && !forced;
         if (pending) {
             const unsigned long long occ = S.tab[local];
             if (occ != kEmpty64 && !(d2 < __uint_as_float((uint32_t)(occ >> 33)))) {
@@ -1233,6 +1236,10 @@ __device__ __forceinline__ void small_process(const SlabParams& P, SmallLds& S, 
             err |= (valid && !layer_ok) ? (uint32_t)ERR_LAYER : ((valid && !range_ok) ? (uint32_t)ERR_SLOT_RANGE : 0u);
             pending = valid && layer_ok && range_ok;
             local = pending ? (uint32_t)(ly * P.tx + lx) : 0u;
+            if (pending && pk[ci] - P.kf_lo < P.kf_n) {   // merge mode: forced emission
+                pending = false;
+                self_em = true;
+            }
             float X, Y, Z;
             hex_to_world(sr.sl, G.cr, X, Y, Z);
             d2 = dist2(X, Y, Z, x, y, z);
@@ -1521,6 +1528,11 @@ __global__ __launch_bounds__(64) void k_slab_wave(SlabParams P) {
             int e = 0;
             int32_t em = -1;
             uint32_t emj = 0, emd = 0;
+            if (pending && pk[c] - P.kf_lo < P.kf_n) {   // merge mode: forced emission
+                pending = false;
+                em = 0;
+                emd = dn;
+            }
             if (pending) {
                 e = wave_entry(W, local, mask);
                 if (e < 0) {
@@ -1673,6 +1685,9 @@ struct BucketParams {
     const uint32_t* files;    // event batches from keys (lib.rs:31-52)
     uint32_t nfiles;
     const uint32_t* cell_sb;  // running spill batch of the level-h cells
+    const int32_t* cell_idx;  // merge mode: the existing cloud's bucket states of this level's cells
+    const PriorCell* prior;   // sorted by (x, y, z)
+    uint32_t nprior;
     Point* kept;
     uint64_t kept_cap;
     const uint32_t* cell_slab0;
@@ -1737,6 +1752,24 @@ __global__ __launch_bounds__(kBktBS) void k_bucket(BucketParams B) {
     nne = block_sum<kBktBS>(nne, lds);
     emin = s_min;
     emax = s_max;
+    if (B.nprior) {   // merge mode: a bucket that is None on disk forwards everything at once (cell.rs:128-130)
+        const int32_t x = B.cell_idx[3 * cell], y = B.cell_idx[3 * cell + 1], z = B.cell_idx[3 * cell + 2];
+        uint32_t lo = 0, hi = B.nprior;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            const PriorCell& q = B.prior[mid];
+            const bool less = q.x != x ? q.x < x : (q.y != y ? q.y < y : q.z < z);
+            if (less) lo = mid + 1; else hi = mid;
+        }
+        const bool found = lo < B.nprior && B.prior[lo].x == x && B.prior[lo].y == y && B.prior[lo].z == z;
+        if (found && ((B.prior[lo].st >> (2 * oct)) & 3u) == 2u) {
+            // state 3: None with nothing forwarded in this build (no child cell to build)
+            if (threadIdx.x == 0) {
+                B.bkt_state[b] = tot ? 2u : 3u; B.bkt_n[b] = tot; B.bkt_nd[b] = tot ? nne : 0u; B.bkt_sb[b] = 0; B.bkt_off[b] = 0;
+            }
+            return;
+        }
+    }
     if (tot == 0) {
         if (threadIdx.x == 0) { B.bkt_state[b] = 0; B.bkt_n[b] = 0; B.bkt_nd[b] = 0; B.bkt_off[b] = 0; B.bkt_sb[b] = 0; }
         return;
@@ -2050,6 +2083,12 @@ void Engine::free_all() {
     (void)hipFree(d_keys_);
     d_keys_ = nullptr;
     keys_cap_ = 0;
+    (void)hipFree(d_seeds_);
+    d_seeds_ = nullptr;
+    (void)hipFree(d_comb_);
+    d_comb_ = nullptr;
+    for (uint32_t* q : d_prior_cells_) (void)hipFree(q);
+    d_prior_cells_.clear();
 }
 
 int Engine::fail(int code, const std::string& msg) {
@@ -2075,6 +2114,7 @@ static uint32_t batches_of(uint64_t n, uint32_t batch) {
 }
 
 void Engine::add_file_host(const Point* pts, uint64_t n, uint32_t batch) {
+    comb_ok_ = false;
     reserve(n_ + n);
     if (n) HIP_CHECK(hipMemcpyAsync(d_in_ + n_, pts, n * sizeof(Point), hipMemcpyHostToDevice, stream_));
     file_start_.push_back(n_);
@@ -2086,6 +2126,7 @@ void Engine::add_file_host(const Point* pts, uint64_t n, uint32_t batch) {
 }
 
 void Engine::add_file_device(const Point* dpts, uint64_t n, uint32_t batch) {
+    comb_ok_ = false;
     reserve(n_ + n);
     if (n) HIP_CHECK(hipMemcpyAsync(d_in_ + n_, dpts, n * sizeof(Point), hipMemcpyDeviceToDevice, stream_));
     file_start_.push_back(n_);
@@ -2096,6 +2137,7 @@ void Engine::add_file_device(const Point* dpts, uint64_t n, uint32_t batch) {
 }
 
 void Engine::add_file_synth(uint64_t seed, int kind, uint64_t n, uint32_t batch, float lo, float ext) {
+    comb_ok_ = false;
     reserve(n_ + n);
     if (n) k_synth<<<grid_for(n, 256, 1 << 20), 256, 0, stream_>>>(d_in_, n_, n, seed, kind, lo, ext);
     HIP_CHECK(hipGetLastError());
@@ -2137,8 +2179,34 @@ void Engine::add_keyed_device(const Point* dpts, const uint32_t* dkeys, uint64_t
     keyed_ = true;
 }
 
+void Engine::set_prior(const PriorState& p) {
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    for (uint32_t* q : d_prior_cells_) (void)hipFree(q);
+    d_prior_cells_.clear();
+    n_prior_cells_.clear();
+    (void)hipFree(d_seeds_);
+    d_seeds_ = nullptr;
+    nseeds_ = p.seeds.size();
+    if (nseeds_) {
+        HIP_CHECK(hipMalloc(&d_seeds_, nseeds_ * sizeof(Point)));
+        HIP_CHECK(hipMemcpy(d_seeds_, p.seeds.data(), nseeds_ * sizeof(Point), hipMemcpyHostToDevice));
+    }
+    forced_lo_ = p.forced_lo;
+    for (const auto& lv : p.cells) {
+        uint32_t* d = nullptr;
+        const size_t bytes = std::max<size_t>(lv.size(), 1) * sizeof(PriorCell);
+        HIP_CHECK(hipMalloc(&d, bytes));
+        if (!lv.empty()) HIP_CHECK(hipMemcpy(d, lv.data(), lv.size() * sizeof(PriorCell), hipMemcpyHostToDevice));
+        d_prior_cells_.push_back(d);
+        n_prior_cells_.push_back((uint32_t)lv.size());
+    }
+    prior_ = true;
+    comb_ok_ = false;
+}
+
 void Engine::clear_input() {
     HIP_CHECK(hipStreamSynchronize(stream_));
+    comb_ok_ = false;
     n_ = 0;
     nbatches_ = 0;
     file_start_.clear();
@@ -2165,35 +2233,69 @@ int Engine::build() {
     hierarchies_ = nbatches_ > 0 ? 1u : 0u;   // converter.rs:141-158 runs for every batch, even empty
     stats_ = BuildStats();
     if (n_ == 0) return 0;
+    if (prior_ && keyed_) return fail(-95, "incremental merge of a sharded (keyed) build is not supported");
+
+    // Input of the build.  Merge mode: the existing
+    // cloud's points come first as "seeds" with keys 0 .. S-1, so every one of
+    // them precedes every new point in key order, then the new points with keys
+    // S + i.  All seeds belong to a pseudo batch 0 before the new batches.
+    if (prior_) {
+        if (!comb_ok_) {
+            if (comb_cap_ < nseeds_ + n_) {
+                (void)hipFree(d_comb_);
+                HIP_CHECK(hipMalloc(&d_comb_, (nseeds_ + n_) * sizeof(Point)));
+                comb_cap_ = nseeds_ + n_;
+            }
+            if (nseeds_) HIP_CHECK(hipMemcpyAsync(d_comb_, d_seeds_, nseeds_ * sizeof(Point), hipMemcpyDeviceToDevice, stream_));
+            HIP_CHECK(hipMemcpyAsync(d_comb_ + nseeds_, d_in_, n_ * sizeof(Point), hipMemcpyDeviceToDevice, stream_));
+            comb_ok_ = true;
+        }
+        src_ = d_comb_;
+        nsrc_ = nseeds_ + n_;
+    } else {
+        src_ = d_in_;
+        nsrc_ = n_;
+    }
+    if (nsrc_ >= 0xFFFFFFFFull) return fail(-75, "more than 2^32-1 points (existing + new) per build are not supported");
 
     // arenas: SoA, N entries each (ping-pong between levels)
-    if (dev_->cap < n_) {
+    if (dev_->cap < nsrc_) {
         for (int a = 0; a < 2; a++) {
             Arena& A = dev_->ar[a];
             (void)hipFree(A.p); (void)hipFree(A.k);
-            HIP_CHECK(hipMalloc(&A.p, n_ * 16)); HIP_CHECK(hipMalloc(&A.k, n_ * 4));
+            HIP_CHECK(hipMalloc(&A.p, nsrc_ * 16)); HIP_CHECK(hipMalloc(&A.k, nsrc_ * 4));
         }
-        dev_->cap = n_;
+        dev_->cap = nsrc_;
     }
     // file table for event batches
     {
         std::vector<uint32_t> ft;
+        const uint64_t s0 = prior_ ? nseeds_ : 0;
+        const uint32_t e0 = prior_ ? 1u : 0u;
+        if (prior_) {   // pseudo file of the seeds: one batch, index 0
+            ft.push_back(0);
+            ft.push_back(0);
+            ft.push_back(0);
+            ft.push_back((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(nseeds_, 0xFFFFFFFFull)));
+        }
         for (size_t f = 0; f < file_start_.size(); f++) {
-            ft.push_back((uint32_t)file_start_[f]);
-            ft.push_back((uint32_t)(file_start_[f] >> 32));
-            ft.push_back(file_eb0_[f]);
+            const uint64_t st = file_start_[f] + s0;
+            ft.push_back((uint32_t)st);
+            ft.push_back((uint32_t)(st >> 32));
+            ft.push_back(file_eb0_[f] + e0);
             ft.push_back(file_batch_[f]);
         }
-        dev_->files = static_cast<uint32_t*>(dev_->get(ft.size() * 4));
-        HIP_CHECK(hipMemcpyAsync(dev_->files, ft.data(), ft.size() * 4, hipMemcpyHostToDevice, stream_));
+        nfiles_dev_ = (uint32_t)(ft.size() / 4);
+        dev_->files = static_cast<uint32_t*>(dev_->get(std::max<size_t>(ft.size(), 4) * 4));
+        if (!ft.empty()) HIP_CHECK(hipMemcpyAsync(dev_->files, ft.data(), ft.size() * 4, hipMemcpyHostToDevice, stream_));
     }
     HIP_CHECK(hipMemsetAsync(dev_->ctr, 0, sizeof(Counters), stream_));
 
     // bbox (K0)
     ev_begin(ST_L0);
     HIP_CHECK(hipMemsetAsync(dev_->bbox_flag, 0, 4, stream_));
-    const unsigned nbb = grid_for(n_, kBBoxBS, kBBoxBlocks);
-    k_bbox<<<nbb, kBBoxBS, 0, stream_>>>(d_in_, n_, dev_->bbox_part, dev_->bbox_flag);
+    const unsigned nbb = grid_for(nsrc_, kBBoxBS, kBBoxBlocks);
+    k_bbox<<<nbb, kBBoxBS, 0, stream_>>>(src_, nsrc_, dev_->bbox_part, dev_->bbox_flag);
     k_bbox_final<<<1, 64, 0, stream_>>>(dev_->bbox_part, nbb);
     HIP_CHECK(hipGetLastError());
     float bb[6];
@@ -2283,7 +2385,7 @@ int Engine::level0_bin() {
             unsigned long long* hk = static_cast<unsigned long long*>(dev_->get(cap * 8));
             HIP_CHECK(hipMemsetAsync(hk, 0xFF, cap * 8, stream_));
             HIP_CHECK(hipMemsetAsync(cnt, 0, 8, stream_));
-            k_l0_hash_insert<<<grid_for(n_, 256, 8192), 256, 0, stream_>>>(d_in_, n_, P, hk, cnt, cnt + 1);
+            k_l0_hash_insert<<<grid_for(nsrc_, 256, 8192), 256, 0, stream_>>>(src_, nsrc_, P, hk, cnt, cnt + 1);
             HIP_CHECK(hipGetLastError());
             uint32_t hc2[2];
             HIP_CHECK(hipMemcpyAsync(hc2, cnt, 8, hipMemcpyDeviceToHost, stream_));
@@ -2317,20 +2419,20 @@ int Engine::level0_bin() {
     while ((1ull << bits) < D) bits++;
     const int passes = std::max(1, (bits + 7) / 8);
     const int per = std::max(1, (bits + passes - 1) / passes);
-    const uint32_t ntiles = (uint32_t)((n_ + kL0Tile - 1) / kL0Tile);
+    const uint32_t ntiles = (uint32_t)((nsrc_ + kL0Tile - 1) / kL0Tile);
     uint32_t* counts = static_cast<uint32_t*>(dev_->get(((uint64_t)ntiles << per) * 4 + 64));
     Arena A0 = dev_->ar[0], A1 = dev_->ar[1];
     Arena src = A1, dst = (passes % 2) ? A0 : A1;
     for (int p = 0, shift = 0; p < passes; p++, shift += per) {
         switch (per) {
-            case 1: l0_pass<1>(p, passes, d_in_, keyed_ ? d_keys_ : nullptr, src, dst, n_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, (uint32_t)file_start_.size(), dev_->scan, stream_); break;
-            case 2: l0_pass<2>(p, passes, d_in_, keyed_ ? d_keys_ : nullptr, src, dst, n_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, (uint32_t)file_start_.size(), dev_->scan, stream_); break;
-            case 3: l0_pass<3>(p, passes, d_in_, keyed_ ? d_keys_ : nullptr, src, dst, n_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, (uint32_t)file_start_.size(), dev_->scan, stream_); break;
-            case 4: l0_pass<4>(p, passes, d_in_, keyed_ ? d_keys_ : nullptr, src, dst, n_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, (uint32_t)file_start_.size(), dev_->scan, stream_); break;
-            case 5: l0_pass<5>(p, passes, d_in_, keyed_ ? d_keys_ : nullptr, src, dst, n_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, (uint32_t)file_start_.size(), dev_->scan, stream_); break;
-            case 6: l0_pass<6>(p, passes, d_in_, keyed_ ? d_keys_ : nullptr, src, dst, n_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, (uint32_t)file_start_.size(), dev_->scan, stream_); break;
-            case 7: l0_pass<7>(p, passes, d_in_, keyed_ ? d_keys_ : nullptr, src, dst, n_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, (uint32_t)file_start_.size(), dev_->scan, stream_); break;
-            default: l0_pass<8>(p, passes, d_in_, keyed_ ? d_keys_ : nullptr, src, dst, n_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, (uint32_t)file_start_.size(), dev_->scan, stream_); break;
+            case 1: l0_pass<1>(p, passes, src_, keyed_ ? d_keys_ : nullptr, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, nfiles_dev_, dev_->scan, stream_); break;
+            case 2: l0_pass<2>(p, passes, src_, keyed_ ? d_keys_ : nullptr, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, nfiles_dev_, dev_->scan, stream_); break;
+            case 3: l0_pass<3>(p, passes, src_, keyed_ ? d_keys_ : nullptr, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, nfiles_dev_, dev_->scan, stream_); break;
+            case 4: l0_pass<4>(p, passes, src_, keyed_ ? d_keys_ : nullptr, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, nfiles_dev_, dev_->scan, stream_); break;
+            case 5: l0_pass<5>(p, passes, src_, keyed_ ? d_keys_ : nullptr, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, nfiles_dev_, dev_->scan, stream_); break;
+            case 6: l0_pass<6>(p, passes, src_, keyed_ ? d_keys_ : nullptr, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, nfiles_dev_, dev_->scan, stream_); break;
+            case 7: l0_pass<7>(p, passes, src_, keyed_ ? d_keys_ : nullptr, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, nfiles_dev_, dev_->scan, stream_); break;
+            default: l0_pass<8>(p, passes, src_, keyed_ ? d_keys_ : nullptr, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, nfiles_dev_, dev_->scan, stream_); break;
         }
         src = dst;
         dst = (dst.p == A0.p) ? A1 : A0;
@@ -2346,7 +2448,7 @@ int Engine::level0_bin() {
     HIP_CHECK(hipMemcpyAsync(&hc, dev_->ctr, sizeof hc, hipMemcpyDeviceToHost, stream_));
     HIP_CHECK(hipStreamSynchronize(stream_));
     if (hc.err) return fail(-34, "level-0 binning: point outside the bounding grid (internal error)");
-    if (tots[0] != n_) return fail(-5, "level-0 histogram mismatch");
+    if (tots[0] != nsrc_) return fail(-5, "level-0 histogram mismatch");
     Level* L = new Level();
     L->dev = dev_;
     levels_.push_back(L);
@@ -2354,7 +2456,7 @@ int Engine::level0_bin() {
     L->ncells = tots[2];
     L->nslabs = tots[1];
     L->arena = 0;
-    L->arrivals = n_;
+    L->arrivals = nsrc_;
     L->alloc(L->cell_idx, 3ull * L->ncells);
     L->alloc(L->cell_sb, L->ncells);
     L->alloc(L->cell_slab0, L->ncells + 1ull);
@@ -2385,7 +2487,7 @@ int Engine::level0_bin() {
     L->nsmall = hc.nsmall;
     stats_.cells += L->ncells;
     stats_.slabs += L->nslabs;
-    stats_.arrivals += n_;
+    stats_.arrivals += nsrc_;
     return 0;
 }
 
@@ -2467,6 +2569,12 @@ int Engine::run_level(uint32_t h) {
     SP.dest_n = L->dest_n;
     SP.gcap = L->gcap;
     SP.check_gchild = (h + 2 < kMaxDepth) ? 1 : 0;
+    SP.kf_lo = 0;
+    SP.kf_n = 0;
+    if (prior_ && h < forced_lo_.size()) {
+        SP.kf_lo = (uint32_t)forced_lo_[h];
+        SP.kf_n = (uint32_t)(nseeds_ - forced_lo_[h]);
+    }
     SP.ctr = dev_->ctr;
     SP.cs = cs;
     {
@@ -2547,8 +2655,11 @@ int Engine::run_level(uint32_t h) {
     BucketParams BP;
     BP.nx = nx;
     BP.files = dev_->files;
-    BP.nfiles = (uint32_t)file_start_.size();
+    BP.nfiles = nfiles_dev_;
     BP.cell_sb = L->cell_sb;
+    BP.cell_idx = L->cell_idx;
+    BP.prior = (prior_ && h < d_prior_cells_.size()) ? reinterpret_cast<const PriorCell*>(d_prior_cells_[h]) : nullptr;
+    BP.nprior = (prior_ && h < n_prior_cells_.size()) ? n_prior_cells_[h] : 0u;
     BP.kept = L->kept;
     BP.kept_cap = L->kept_cap;
     BP.cell_slab0 = L->cell_slab0;

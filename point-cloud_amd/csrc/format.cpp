@@ -1,6 +1,7 @@
 // format.cpp — cell / metadata writers and the PLY reader (see format.h).
 #include "format.h"
 
+#include <dirent.h>
 #include <sys/stat.h>
 
 #include <algorithm>
@@ -257,6 +258,115 @@ int write_metadata(const std::string& dir, const Metadata& meta, std::string& er
     const std::string js = metadata_json(meta);
     const bool ok = fwrite(js.data(), 1, js.size(), f) == js.size();
     if (fclose(f) != 0 || !ok) { err = "write failed: " + mp; return -EIO; }
+    return 0;
+}
+
+// ------------------------------------------------------------------ existing cloud
+bool read_cell_file(const std::string& path, CellFile& out, std::string& err) {
+    FILE* f = fopen(path.c_str(), "rb");
+    if (!f) { err = "cannot open " + path; return false; }
+    std::string b;
+    char tmp[1 << 16];
+    size_t r;
+    while ((r = fread(tmp, 1, sizeof tmp, f)) > 0) b.append(tmp, r);
+    fclose(f);
+    auto bad = [&](const char* what) { err = path + ": " + what; return false; };
+    if (b.size() < 49) return bad("truncated header");
+    const char* p = b.data();
+    auto u32 = [&](size_t o) { uint32_t v; memcpy(&v, p + o, 4); return v; };
+    auto i32 = [&](size_t o) { int32_t v; memcpy(&v, p + o, 4); return v; };
+    out.h = u32(0);
+    out.idx[0] = i32(4); out.idx[1] = i32(8); out.idx[2] = i32(12);
+    out.total = u32(16); out.number = u32(20); out.overflow = u32(24);
+    size_t off = 48;
+    if (off + 16ull * out.number + 1 > b.size()) return bad("truncated grid");
+    out.grid.resize(out.number);
+    memcpy(out.grid.data(), p + off, 16ull * out.number);
+    off += 16ull * out.number;
+    const uint32_t nb = (uint8_t)p[off++];
+    if (nb > 8) return bad("more than 8 overflow entries");
+    out.entries.clear();
+    for (uint32_t j = 0; j < nb; j++) {
+        if (off + 16 > b.size()) return bad("truncated overflow entry");
+        CellFile::Entry e;
+        e.child[0] = i32(off); e.child[1] = i32(off + 4); e.child[2] = i32(off + 8);
+        const uint32_t n = u32(off + 12);
+        off += 16;
+        e.some = n != 0;
+        if (off + 16ull * n > b.size()) return bad("truncated overflow list");
+        e.pts.resize(n);
+        memcpy(e.pts.data(), p + off, 16ull * n);
+        off += 16ull * n;
+        out.entries.push_back(std::move(e));
+    }
+    if (off != b.size()) return bad("trailing bytes");
+    return true;
+}
+
+int read_cloud(const std::string& dir, uint32_t hierarchies, std::vector<CellFile>& cells, std::string& err) {
+    cells.clear();
+    for (uint32_t h = 0; h < hierarchies; h++) {
+        const std::string hd = dir + "/h_" + std::to_string(h);
+        DIR* d = opendir(hd.c_str());
+        if (!d) continue;   // converter.rs:187-207: a missing file is a new cell
+        std::vector<std::string> names;
+        while (dirent* e = readdir(d)) names.push_back(e->d_name);
+        closedir(d);
+        std::sort(names.begin(), names.end());
+        for (const std::string& nm : names) {
+            int x, y, z;
+            char tail[8] = {0};
+            if (sscanf(nm.c_str(), "c_%d_%d_%d.%3s", &x, &y, &z, tail) != 4 || strcmp(tail, "bin") != 0) continue;
+            CellFile c;
+            if (!read_cell_file(hd + "/" + nm, c, err)) return -EINVAL;
+            if (c.h != h || c.idx[0] != x || c.idx[1] != y || c.idx[2] != z) {
+                err = hd + "/" + nm + ": header does not match the file name";
+                return -EINVAL;
+            }
+            cells.push_back(std::move(c));
+        }
+    }
+    return 0;
+}
+
+int prior_from_cells(const std::vector<CellFile>& cells, const Config& cfg, PriorState& out, std::string& err) {
+    uint32_t levels = 0;
+    for (const CellFile& c : cells) levels = std::max(levels, c.h + 1);
+    out.seeds.clear();
+    out.forced_lo.assign(levels, 0);
+    out.cells.assign(levels, {});
+    std::vector<std::vector<const CellFile*>> by(levels);
+    for (const CellFile& c : cells) by[c.h].push_back(&c);
+    for (uint32_t h = 0; h < levels; h++) {
+        // grid seeds.  Cell::read_from re-keys the grid by slot (cell.rs:189-195);
+        // files written by the reference or by this build hold one point per slot,
+        // so the file order is kept as is (a file with a repeated slot is not a
+        // state the reference can produce and is not detected here).
+        for (const CellFile* c : by[h]) out.seeds.insert(out.seeds.end(), c->grid.begin(), c->grid.end());
+        out.forced_lo[h] = out.seeds.size();
+        // kept seeds: every Some list in stored order; bucket states per cell
+        for (const CellFile* c : by[h]) {
+            PriorCell pc{c->idx[0], c->idx[1], c->idx[2], 0u};
+            for (const CellFile::Entry& e : c->entries) {
+                const int32_t bx = e.child[0] - 2 * c->idx[0], by_ = e.child[1] - 2 * c->idx[1], bz = e.child[2] - 2 * c->idx[2];
+                if (((bx | by_ | bz) & ~1) != 0) {
+                    err = "overflow entry that is not a child of its cell";
+                    return -EINVAL;
+                }
+                const int oct = bx | (by_ << 1) | (bz << 2);
+                pc.st |= (e.some ? 1u : 2u) << (2 * oct);
+                if (e.some) out.seeds.insert(out.seeds.end(), e.pts.begin(), e.pts.end());
+            }
+            out.cells[h].push_back(pc);
+        }
+        std::sort(out.cells[h].begin(), out.cells[h].end(), [](const PriorCell& a, const PriorCell& b) {
+            return a.x != b.x ? a.x < b.x : (a.y != b.y ? a.y < b.y : a.z < b.z);
+        });
+    }
+    if (out.seeds.size() >= 0xFFFFFFFFull) {
+        err = "existing cloud has more than 2^32-1 points";
+        return -EOVERFLOW;
+    }
     return 0;
 }
 

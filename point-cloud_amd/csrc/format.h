@@ -33,6 +33,28 @@ int write_output(const std::string& dir, const Metadata& meta, const std::vector
                  bool with_metadata = true);
 int write_metadata(const std::string& dir, const Metadata& meta, std::string& err);
 
+// One cell file as Cell::read_from sees it (cell.rs:183-229, Header::read_from
+// cell.rs:300-335): grid points in file order, overflow entries in file order
+// (n == 0 <=> None, cell.rs:210-212).
+struct CellFile {
+    uint32_t h = 0;
+    int32_t idx[3] = {0, 0, 0};
+    uint32_t total = 0, number = 0, overflow = 0;
+    std::vector<Point> grid;
+    struct Entry {
+        int32_t child[3];
+        bool some;
+        std::vector<Point> pts;
+    };
+    std::vector<Entry> entries;
+};
+bool read_cell_file(const std::string& path, CellFile& out, std::string& err);
+// Every h_{h}/c_{x}_{y}_{z}.bin with h < hierarchies (the layout own.rs:16-62 and
+// converter.rs:187-207 read; the order of the returned cells is unspecified).
+int read_cloud(const std::string& dir, uint32_t hierarchies, std::vector<CellFile>& cells, std::string& err);
+// The existing cloud as the engine's merge state (engine.h PriorState).
+int prior_from_cells(const std::vector<CellFile>& cells, const Config& cfg, PriorState& out, std::string& err);
+
 // PLY reader.  Returns points of the `vertex` element.  `ascii` is set when the
 // file is ASCII-encoded: the reference's ASCII branch parses but never stores
 // the points (ply.rs:43-51), so callers must feed empty batches instead.

@@ -1,0 +1,73 @@
+"""GPU parity of the incremental merge (config 5 shape; lib.rs:86-101 +
+converter.rs:187-207): the HIP build opened on a
+directory that already holds a converted cloud, fed new files, must write
+exactly the cloud the sequential oracle produces when it converts the old and
+the new files in one run (the equivalence tests/test_merge_oracle.py pins on
+the CPU).  The existing cloud is written by the oracle, or by the HIP build
+itself, so both writers' files are read back."""
+import os
+import shutil
+import tempfile
+
+import pytest
+
+from gpu_util import compare_dirs, run_gpu, run_oracle  # noqa: E402
+from oracle_ctypes import synth  # noqa: E402
+from test_merge_oracle import _split  # noqa: E402
+from test_oracle_xcheck import _case, _to_np  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def _merge_check(first, second, cfg=None, batch=10_000, prior_by="oracle", fast=False):
+    with tempfile.TemporaryDirectory() as tg, tempfile.TemporaryDirectory() as to:
+        if prior_by == "oracle":
+            err, _ = run_oracle(tg, first, cfg=cfg, batch=batch)
+            assert err == 0
+        else:
+            run_gpu(tg, first, cfg=cfg, batch=batch)
+        st = run_gpu(tg, second, cfg=None, batch=batch)   # config comes from the existing metadata.json
+        err, _ = run_oracle(to, first + second, cfg=cfg, batch=batch)
+        assert err == 0
+        d, mg, mo = compare_dirs(tg, to, fast=fast)
+        assert d == [], d
+        assert mg == mo
+        assert st["grid_points"] + st["kept_points"] == st["number_of_points"]
+        return st
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_merge_adversarial_small(seed):
+    files, cfg, batch = _case(seed)
+    first, second = _split(files, seed)
+    _merge_check([_to_np(f) for f in first], [_to_np(f) for f in second], cfg=cfg, batch=batch)
+
+
+def test_merge_uniform_prior_from_gpu():
+    pts = synth(21, 0, 400_000)
+    _merge_check([pts[:300_000]], [pts[300_000:]], prior_by="gpu", fast=True)
+
+
+def test_merge_clustered_deep():
+    a = synth(22, 1, 600_000)
+    b = synth(23, 1, 250_000)
+    st = _merge_check([a], [b[:100_000], b[100_000:]], fast=True)
+    assert st["levels"] >= 3
+
+
+def test_merge_small_limit_spills_kept_lists():
+    """Tiny limit: existing Some lists spill in the merge, existing None buckets forward."""
+    pts = synth(24, 0, 60_000, lo=-40.0, ext=80.0)
+    cfg = dict(cell_point_overflow_limit=4, sub_grid_dimension=6, max_cell_size=64.0)
+    _merge_check([pts[:20_000], pts[20_000:30_000]], [pts[30_000:]], cfg=cfg, batch=777)
+
+
+def test_merge_no_new_points_keeps_cloud():
+    pts = synth(25, 0, 50_000)
+    with tempfile.TemporaryDirectory() as tg, tempfile.TemporaryDirectory() as to:
+        run_oracle(to, [pts])
+        shutil.rmtree(tg)
+        shutil.copytree(to, tg)
+        run_gpu(tg, [pts[:0]])
+        d, mg, mo = compare_dirs(tg, to, fast=False)
+        assert d == [] and mg == mo
