@@ -37,6 +37,9 @@ def parse():
     ap.add_argument("--seed", type=int, default=4)
     ap.add_argument("--cpu-sample", type=int, default=20_000_000, help="oracle prefix sample (points); 0 = skip")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--merge-prior", type=int, default=0,
+                    help="config 5: merge --points new points (seed --seed) into a cloud built from this many "
+                         "config-4 points (seed 4); 0 = fresh build")
     return ap.parse_args()
 
 
@@ -46,10 +49,17 @@ def cpu_baseline(args):
     n = min(args.cpu_sample, args.points)
     pts = synth(args.seed, args.kind, n)
     o = Oracle()
+    if args.merge_prior:   # untimed existing cloud: a prefix of the config-4 stream, 5x the timed sample
+        o.add_file(synth(4, 0, min(args.merge_prior, 5 * n)))
     t0 = time.perf_counter()
     o.add_file(pts)
     dt = time.perf_counter() - t0
     o.close()
+    if args.merge_prior:
+        return {"value": n / dt, "unit": "points/s", "cores": 1, "kind": "port",
+                "sample": f"merge of the first {n} points of the seed-{args.seed} stream into an in-memory cloud of "
+                          f"the first {min(args.merge_prior, 5 * n)} config-4 points, sequential C restatement "
+                          f"(oracle/pcc_oracle.c, 10 000-point batches), {dt:.1f} s"}
     return {"value": n / dt, "unit": "points/s", "cores": 1, "kind": "port",
             "sample": f"first {n} points of the same seed-{args.seed} stream through the sequential C restatement "
                       f"(oracle/pcc_oracle.c, in-memory cells, 10 000-point batches), {dt:.1f} s"}
@@ -84,6 +94,9 @@ def record(args, n_gpus, ms, st_levels, st_cells, st_slabs, arrivals, k, dense_m
     whole = 32.0 * arrivals / (ms / 1e3) / 1e9
     workload = ("config4: %d uniform points in [-1000,1000)^3, seed %d" if args.kind == 0 else
                 "config3-shape: %d clustered points, seed %d") % (args.points, args.seed)
+    if args.merge_prior:
+        workload = ("config5: +%d %s points (seed %d) merged into the %d-point config-4 cloud (seed 4)" %
+                    (args.points, "uniform" if args.kind == 0 else "clustered", args.seed, args.merge_prior))
     traffic, tsrc = pmc_traffic(workload)
     return {
         "metric": METRIC,
@@ -176,6 +189,12 @@ def main():
     import tempfile
     tmp = tempfile.mkdtemp(prefix="pcc_bench_")
     conv = pcconv.Converter(tmp, batch_size=10_000, device=0)
+    if args.merge_prior:   # config 5: the existing cloud is built (untimed) and adopted in memory
+        prior = pcconv.Converter(tempfile.mkdtemp(prefix="pcc_prior_"), batch_size=10_000, device=0)
+        prior.add_synthetic(4, 0, args.merge_prior)
+        prior.build()
+        conv.adopt_prior(prior)
+        prior.close()
     conv.add_synthetic(args.seed, args.kind, args.points)
     conv.set_profiling(True)
     for _ in range(args.warmup):

@@ -109,6 +109,12 @@ int pcc_write(pcc_converter* c);
 /* converter.rs:241-246 Drop: build (if needed), write everything, free. */
 int pcc_finish(pcc_converter* c);
 
+/* Incremental merge without files: the built cloud of `src` (built now if
+ * needed) becomes the starting state of the freshly opened `dst`, exactly as if
+ * src had been written to dst's directory and dst opened on it (bench.py
+ * config 5).  Same config required. */
+int pcc_adopt_prior(pcc_converter* dst, pcc_converter* src);
+
 /* Free without writing anything. */
 int pcc_close(pcc_converter* c);
 

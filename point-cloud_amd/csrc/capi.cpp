@@ -345,6 +345,62 @@ int pcc_clear_input(pcc_converter* c) {
     GUARD_END
 }
 
+// The built cloud of `src` as the merge state of `dst` (in memory, no files):
+// the same state pcc_open would load from src's output directory.
+int pcc_adopt_prior(pcc_converter* dst, pcc_converter* src) {
+    if (!dst || !src) return set_err(-EINVAL, "null argument");
+    if (dst->built || dst->eng->num_points() || dst->merge) return set_err(-EINVAL, "destination must be freshly opened");
+    const Config& a = dst->meta.config;
+    const Config& b = src->meta.config;
+    if (a.cell_point_overflow_limit != b.cell_point_overflow_limit || a.sub_grid_dimension != b.sub_grid_dimension ||
+        a.max_cell_size != b.max_cell_size)
+        return set_err(-EINVAL, "configs differ");
+    if (!src->built) {
+        const int rc = pcc_build(src);
+        if (rc) return rc;
+    }
+    GUARD_BEGIN
+    std::vector<LevelHost> levels;
+    std::vector<Point> grid, kept;
+    int rc = src->eng->download(levels, grid, kept);
+    if (rc) return set_err(rc, src->eng->last_error());
+    std::vector<CellFile> cells;
+    for (const LevelHost& L : levels) {   // cell.rs:155-181 contents without the file round trip
+        const uint32_t ncells = (uint32_t)(L.cell_idx.size() / 3);
+        for (uint32_t c = 0; c < ncells; c++) {
+            CellFile f;
+            f.h = L.h;
+            for (int q = 0; q < 3; q++) f.idx[q] = L.cell_idx[3 * c + q];
+            for (uint32_t s = L.cell_slab0[c]; s < L.cell_slab0[c + 1]; s++)
+                f.grid.insert(f.grid.end(), grid.begin() + L.grid_base + L.slab_grid_off[s],
+                              grid.begin() + L.grid_base + L.slab_grid_off[s] + L.slab_grid_n[s]);
+            for (int o = 0; o < 8; o++) {
+                const uint32_t st = L.bkt_state[8 * c + o];
+                if (!st) continue;
+                CellFile::Entry e;
+                e.child[0] = 2 * f.idx[0] + (o & 1);
+                e.child[1] = 2 * f.idx[1] + ((o >> 1) & 1);
+                e.child[2] = 2 * f.idx[2] + ((o >> 2) & 1);
+                e.some = st == 1;
+                if (e.some)
+                    e.pts.assign(kept.begin() + L.kept_base + L.bkt_off[8 * c + o],
+                                 kept.begin() + L.kept_base + L.bkt_off[8 * c + o] + L.bkt_n[8 * c + o]);
+                f.entries.push_back(std::move(e));
+            }
+            cells.push_back(std::move(f));
+        }
+    }
+    PriorState ps;
+    std::string err;
+    rc = prior_from_cells(cells, dst->meta.config, ps, err);
+    if (rc) return set_err(rc, err);
+    dst->eng->set_prior(ps);
+    dst->merge = true;
+    dst->prior = src->meta;
+    return 0;
+    GUARD_END
+}
+
 int pcc_finish(pcc_converter* c) {
     if (!c) return set_err(-EINVAL, "null argument");
     const int rc = pcc_write(c);

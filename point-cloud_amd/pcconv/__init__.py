@@ -12,6 +12,8 @@ Reference-to-mirror map:
   Converter.add_points(points)        converter.rs:106-112 (one call == one input file,
                                       ceil(n / batch_size) batches, lib.rs:31-52)
   Converter.finish()                  converter.rs:241-246 Drop (cells, then metadata.json)
+  Converter(existing_dir)             incremental merge: lib.rs:86-101 + converter.rs:187-207
+                                      (the directory's cells are the starting state)
 """
 from __future__ import annotations
 
@@ -31,7 +33,7 @@ EXPORTS = ["pcc_abi_version", "pcc_last_error", "pcc_options_default", "pcc_open
            "pcc_finish", "pcc_close", "pcc_get_stats", "pcc_set_profiling", "pcc_get_profile", "pcc_device_input",
            "pcc_convert_files", "pcc_shard_grid_from_bbox", "pcc_synth_device", "pcc_shard_bbox",
            "pcc_shard_histogram", "pcc_shard_route", "pcc_declare_files", "pcc_add_keyed_points_device",
-           "pcc_set_summary", "pcc_write_cells", "pcc_write_metadata", "pcc_clear_input"]
+           "pcc_set_summary", "pcc_write_cells", "pcc_write_metadata", "pcc_clear_input", "pcc_adopt_prior"]
 
 
 class Options(C.Structure):
@@ -116,6 +118,7 @@ def lib():
         L.pcc_write_cells.argtypes = [vp]
         L.pcc_write_metadata.argtypes = [vp]
         L.pcc_clear_input.argtypes = [vp]
+        L.pcc_adopt_prior.argtypes = [vp, vp]
         _lib = L
     return _lib
 
@@ -200,6 +203,12 @@ class Converter:
 
     def clear_input(self):
         _check(lib().pcc_clear_input(self._h))
+
+    def adopt_prior(self, other: "Converter"):
+        """Incremental merge without files: `other`'s built cloud becomes this
+        (freshly opened) converter's existing cloud, as if it had been written to
+        this converter's directory before opening it (lib.rs:86-101)."""
+        _check(lib().pcc_adopt_prior(self._h, other._h))
 
     def finish(self):
         """converter.rs:241-246 Drop: build if needed, write cells then metadata.json."""

@@ -71,3 +71,26 @@ def test_merge_no_new_points_keeps_cloud():
         run_gpu(tg, [pts[:0]])
         d, mg, mo = compare_dirs(tg, to, fast=False)
         assert d == [] and mg == mo
+
+
+def test_adopt_prior_equals_directory_merge():
+    """pcc_adopt_prior (bench.py config 5, no files) == opening the directory."""
+    import pcconv
+    a = synth(26, 0, 200_000)
+    b = synth(27, 0, 80_000)
+    with tempfile.TemporaryDirectory() as t0, tempfile.TemporaryDirectory() as t1, \
+            tempfile.TemporaryDirectory() as to:
+        src = pcconv.Converter(t0)
+        src.add_points(a)
+        src.build()
+        dst = pcconv.Converter(t1)
+        dst.adopt_prior(src)
+        src.close()
+        dst.add_points(b)
+        st = dst.build()
+        dst.write()
+        dst.close()
+        run_oracle(to, [a, b])
+        d, mg, mo = compare_dirs(t1, to, fast=True)
+        assert d == [] and mg == mo
+        assert st["number_of_points"] == 280_000
