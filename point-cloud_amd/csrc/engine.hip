@@ -160,6 +160,14 @@ struct Engine::Level {
 // ------------------------------------------------------------------ diagnostics
 // Diagnostic build only (-DPCC_STAMPS): per-wave s_memtime phase sums of the
 // slab kernel, added into P.stamps[phase]; never compiled into the product.
+// Diagnostic builds only (-DPCC_ABL=mask, `make abl`): timing ablations of the
+// dense slab kernel that break its results (1: no grid gather, 2: no emission
+// stores, 4: no displaced-payload gathers, 8: no grandchild counts, 16: no
+// emission ranks, 32: no claims (every arrival overflows)).  Only the first
+// level's timing is meaningful under 2..32.  Never compiled into the product.
+#ifndef PCC_ABL
+#define PCC_ABL 0
+#endif
 #ifdef PCC_STAMPS
 #define STAMP_DECL unsigned long long st_t0 = __builtin_amdgcn_s_memtime(), st_acc[16] = {};
 #define STAMP(ph) do { const unsigned long long st_n = __builtin_amdgcn_s_memtime(); st_acc[ph] += st_n - st_t0; st_t0 = st_n; } while (0)
@@ -724,12 +732,15 @@ struct SlabParams {
 struct DenseLds {
     static constexpr int BS = kDenseBS, TAB = kDenseTab, CLAIM = kDenseClaim, NW = BS / 64;
     unsigned long long tab[TAB];   // occupant: (d2 bits << 33) | (child slab << 28) | j
-    uint8_t tgd[TAB];              // occupant's grandchild slab inside its child slab (0xFF: none)
-    uint32_t claim[2][CLAIM];      // double-buffered by chunk parity: no clearing barrier
+    uint32_t claim[2][CLAIM];      // per chunk parity: (slot << 11) | head of the slot's candidate list
+    uint32_t cd2[BS];              // candidates of the current chunk, by thread: d2 bits,
+    uint16_t cnext[BS];            //   next candidate of the same slot (kNil: end),
+    uint16_t cdg[BS];              //   own child slab
     uint32_t gcnt[kDests * kDests];
-    uint32_t doff[kDests], dcap[kDests], dcur[kDests];
-    uint32_t wcnt[NW][kDests], wpre[NW][kDests];
-    uint32_t npend[2], nwin, err;
+    uint32_t doff[kDests], dcap[kDests];
+    uint32_t dcur[2][kDests];      // emissions per child slab before chunk c: dcur[c & 1]
+    uint32_t wcnt[NW][kDests];
+    uint32_t nwin, err;
 };
 
 __device__ __forceinline__ uint32_t hash_slot(uint32_t k) { return (k * 2654435761u) >> 15; }
@@ -757,6 +768,30 @@ __device__ __forceinline__ int claim_insert(uint32_t* H, uint32_t local, uint32_
     return -1;
 }
 
+// Same table as a list head per slot: the entry's low 11 bits are the last
+// inserted thread; returns the entry and the previous head (kNil: none).
+constexpr uint32_t kNil = 0x7FFu;
+template <int CLAIM>
+__device__ __forceinline__ int claim_push(uint32_t* H, uint32_t local, uint32_t tid, uint32_t& prev) {
+    const uint32_t mine = (local << 11) | tid;
+    uint32_t h = hash_slot(local) & (CLAIM - 1);
+    for (int probe = 0; probe < CLAIM; probe++) {
+        uint32_t e = H[h];
+        if (e == kEmpty32) {
+            const uint32_t old = atomicCAS(&H[h], kEmpty32, mine);
+            if (old == kEmpty32) { prev = kNil; return (int)h; }
+            e = old;
+        }
+        if ((e >> 11) == local) {
+            prev = atomicExch(&H[h], mine) & kNil;
+            return (int)h;
+        }
+        h = (h + 1) & (CLAIM - 1);
+    }
+    prev = kNil;
+    return -1;
+}
+
 // Slot-table entry: (d2 bits << 33) | (dest << 28) | j.  d2 >= +0 so its sign
 // bit is free; dest (0..23) is the occupant's child slab, so displacing it needs
 // no access to its payload for routing; j < 2^28 indexes the slab's arrivals.
@@ -771,25 +806,32 @@ __device__ __forceinline__ void bst4(__amdgpu_buffer_rsrc_t r, uint32_t off, u32
     __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 0);
 }
 
-// One pass over the slab in key order (cell.rs:70-94), one chunk of BS
-// arrivals per step, software-pipelined:
-//   phase A : slot/d2/own routes of chunk i; arrivals that cannot beat their
-//             slot's occupant overflow at once, the others (candidate records)
-//             enter the claim table; wave ranks of chunk i-1's emissions
-//   barrier : per round: apply claim winners | barrier | (round 1: stores of
-//             chunk i-1) | re-claim | barrier ...
-// An emission is the arrival itself (kind 0) or the occupant it displaced
-// (kind 1), always at the arrival's key.  A displaced occupant's payload is
-// gathered from the slab's arrivals when it is displaced and stored one step
-// later with the rest of the chunk's emissions.  After the last chunk the
-// table's occupants are the slab's grid points (cell.rs:158-160: order inside
-// a cell file is free); their payloads are gathered once.
+// One pass over the slab in key order (cell.rs:70-94), one chunk of BS arrivals
+// per step and exactly two barriers per step:
+//   phase A : slot / d2 / routes of chunk i.  An arrival that does not beat its
+//             slot's occupant overflows at once (occupants only improve); the
+//             others (candidates) push themselves onto their slot's list.  Wave
+//             ranks of chunk i-1's emissions per child slab.
+//   barrier
+//   phase B : chunk i-1's emissions are stored (positions from per-wave prefixes
+//             of the wave counts).  Every candidate walks its slot's list: it is
+//             a record iff no earlier candidate has d2 <= its own; a record is
+//             the new occupant iff no later candidate has a smaller d2, and it
+//             emits, at its own key, the record before it (the earlier
+//             candidate with the least (d2, key)) or, if it is the first record,
+//             the slot's previous occupant.  Everything else overflows at its key.
+//   barrier
+// The payload of a displaced record is gathered from the slab's arrivals and
+// stored one step later with the rest of the chunk's emissions.  After the last
+// chunk the table's occupants are the slab's grid points (cell.rs:158-160:
+// order inside a cell file is free).  Grandchild capacities count every
+// arrival's (child, grandchild) slab and subtract the grid points' at the end.
 __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
     using L = DenseLds;
     constexpr int BS = L::BS, TAB = L::TAB, CLAIM = L::CLAIM, NW = L::NW;
     __shared__ L S;
     STAMP_DECL
-    const uint32_t tid = threadIdx.x, wv = tid / 64;
+    const uint32_t tid = threadIdx.x, wv = tid / 64, lane = tid & 63;
     const uint32_t s = P.list[blockIdx.x];
     const uint32_t cr_ = P.slab_cell[s];
     const int32_t t = P.slab_layer[s];
@@ -816,23 +858,23 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
     for (int i = tid; i < 2 * CLAIM; i += BS) (&S.claim[0][0])[i] = kEmpty32;
     for (int i = tid; i < kDests * kDests; i += BS) S.gcnt[i] = 0;
     if (tid < kDests) {
-        S.dcur[tid] = 0;
+        S.dcur[0][tid] = 0;
+        S.dcur[1][tid] = 0;
         S.doff[tid] = P.dest_off[s * kDests + tid] - dbase;
         S.dcap[tid] = P.dcap[s * kDests + tid];
     }
-    if (tid < NW * kDests) (&S.wcnt[0][0])[tid] = 0;
-    if (tid == 0) { S.npend[0] = 0; S.npend[1] = 0; S.nwin = 0; S.err = 0; }
+    if (tid == 0) { S.nwin = 0; S.err = 0; }
     __syncthreads();
     STAMP(0);
 
     struct Stage {
-        int32_t em;     // -1 none, 0 self, 1 displaced occupant
-        int32_t g;      // grandchild slab (0..23) of the emitted point inside its child slab, -1 none
+        int32_t em;     // -1 none, 0 self, 1 displaced record / occupant
         uint32_t d;     // child slab of the emitted point
-        u32x4 gp;       // gathered payload of a displaced occupant
+        int32_t hc;     // claim entry of a candidate (cleared one step later)
+        u32x4 gp;       // gathered payload of a displaced point
     };
     Stage A;
-    A.em = -1; A.g = -1; A.d = 0;
+    A.em = -1; A.d = 0; A.hc = -1;
     A.gp = u32x4{0u, 0u, 0u, 0u};
     Stage B = A;
     // Arrivals are prefetched two chunks ahead into a ring of four register
@@ -852,7 +894,6 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
             pre[q].k = 0;
         }
     }
-    const uint64_t lt = lanemask_lt();
     const uint32_t nchunks = (n + BS - 1) / BS;
     auto step = [&](uint32_t ci, Stage& cur, Stage& prv, const Pre& mine, const Pre& prvb, Pre& pf) {
         const uint32_t par = ci & 1;
@@ -865,6 +906,8 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
             pf.p = bld4(rP, jo * 16);
             pf.k = bld(rK, jo * 4);
         }
+        // the claim entries of chunk i-1 (other parity) are dead since the last barrier
+        if (prv.hc >= 0) S.claim[par ^ 1][prv.hc] = kEmpty32;
         const u32x4 own = mine.p;
         const float x = __uint_as_float(own.x), y = __uint_as_float(own.y), z = __uint_as_float(own.z);
         // ---- phase A (1): slot + distance (hex.rs:67-85, 55-65) + own child / grandchild slab
@@ -878,8 +921,8 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
         const bool layer_ok = sl.z == t;
         const bool range_ok = lx >= 0 && ly >= 0 && lx < P.tx && ly < P.ty;
         err |= (valid && !layer_ok) ? (uint32_t)ERR_LAYER : ((valid && !range_ok) ? (uint32_t)ERR_SLOT_RANGE : 0u);
-        bool pending = valid && layer_ok && range_ok;
-        const uint32_t local = pending ? (uint32_t)(ly * P.tx + lx) : 0u;
+        const bool slotted = valid && layer_ok && range_ok;
+        const uint32_t local = slotted ? (uint32_t)(ly * P.tx + lx) : 0u;
         float X, Y, Z;
         hex_to_world(sl, G.cr, X, Y, Z);
         const float d2 = dist2(X, Y, Z, x, y, z);
@@ -897,124 +940,104 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
         if (d2 == 12345.0f) err |= 1u << 29;   // finish the math before the stamp
         STAMP(13);
 #endif
-        // An arrival that does not beat its slot's occupant as it stands before
-        // this chunk overflows at once (occupants only improve within a chunk,
-        // cell.rs:80 strict <): only candidate records enter the claim rounds,
-        // so a chunk needs as many rounds as its most contended slot has
-        // candidates, not arrivals.
+        // grandchild capacities count every arrival (grid points are subtracted at the end)
+        if (slotted && gn >= 0 && !(PCC_ABL & 8)) atomicAdd(&S.gcnt[dn * kDests + (uint32_t)gn], 1u);
+        // Occupant filter (cell.rs:80 strict <: ties keep the old point); the
+        // candidates push themselves onto their slot's list.
+        unsigned long long occ = kEmpty64;
+        bool cand = false;
         int hc = -1;
-        bool self_em = forced && pending;
-        pending = pending && !forced;
-        if (pending) {
-            const unsigned long long occ = S.tab[local];
-            if (occ != kEmpty64 && !(d2 < __uint_as_float((uint32_t)(occ >> 33)))) {
-                self_em = true;
-                pending = false;
-            } else {
-                hc = claim_insert<CLAIM>(claim, local, tid);
-                if (hc < 0) { err |= ERR_CLAIM; pending = false; }
-            }
+        if (slotted && !forced) {
+            occ = S.tab[local];
+            cand = occ == kEmpty64 || d2 < __uint_as_float((uint32_t)(occ >> 33));
+            if (PCC_ABL & 32) cand = false;
         }
-        {
-            const uint32_t np = (uint32_t)__popcll(__ballot(pending));
-            if ((tid & 63) == 0 && np) atomicAdd(&S.npend[par], np);
+        if (cand) {
+            uint32_t prev;
+            hc = claim_push<CLAIM>(claim, local, tid, prev);
+            if (hc < 0) { err |= ERR_CLAIM; cand = false; }
+            S.cd2[tid] = f2u(d2);
+            S.cnext[tid] = (uint16_t)prev;
+            S.cdg[tid] = (uint16_t)dn;
         }
         STAMP(1);
-        // ---- phase A (2): wave ranks of chunk i-1's emissions per child slab and
-        // their grandchild capacities (one LDS add per distinct (d, g) in the wave)
+        // ---- phase A (2): wave ranks of chunk i-1's emissions per child slab
         const bool vd = prv.em >= 0;
         const int d = vd ? (int)prv.d : 0;
-        uint64_t same = __ballot(vd);
-#pragma unroll
-        for (int b = 0; b < 5; b++) {
-            const uint64_t bb = __ballot(vd && ((d >> b) & 1));
-            same &= ((d >> b) & 1) ? bb : ~bb;
-        }
-        const uint32_t rw = __popcll(same & lt);
+        const uint64_t same = (PCC_ABL & 16) ? __ballot(vd) : wave_peers<5>((uint32_t)d, vd);
+        const uint32_t rw = (PCC_ABL & 16) ? 0u : mask_rank(same);
+        if (lane < kDests) S.wcnt[wv][lane] = 0;
         if (vd && rw == 0) S.wcnt[wv][d] = (uint32_t)__popcll(same);
-        {
-            const bool vg = vd && prv.g >= 0;
-            const int32_t gg = vg ? prv.g : 0;
-            uint64_t sg = same & __ballot(vg);
-#pragma unroll
-            for (int b = 0; b < 5; b++) {
-                const uint64_t bb = __ballot(vg && ((gg >> b) & 1));
-                sg &= ((gg >> b) & 1) ? bb : ~bb;
-            }
-            if (vg && __popcll(sg & lt) == 0) atomicAdd(&S.gcnt[d * kDests + gg], (uint32_t)__popcll(sg));
-        }
         STAMP(2);
         lds_barrier();
         STAMP(3);
-        // ---- phase B: ranks of chunk i-1 -> positions (wave 0), claim rounds of chunk i
-        if (tid < kDests) {
-            uint32_t acc = S.dcur[tid];
-#pragma unroll
-            for (int q = 0; q < NW; q++) { const uint32_t cc = S.wcnt[q][tid]; S.wpre[q][tid] = acc; acc += cc; S.wcnt[q][tid] = 0; }
-            S.dcur[tid] = acc;
-        }
-        // per round, the earliest pending candidate of every slot (min thread
-        // index = min key) is applied
-        int32_t em = self_em ? 0 : -1, emg = self_em ? gn : -1;
-        uint32_t emd = self_em ? dn : 0u;
-        uint32_t gsrc = 0xFFFFFFFFu;   // byte offset of a displaced occupant's payload
-        bool first = true;
-        for (;;) {
-            bool won = false;
-            if (pending && (claim[hc] & kClaimDone) == tid) {
-                const unsigned long long occ = S.tab[local];
-                const unsigned long long mine =
-                    ((unsigned long long)f2u(d2) << 33) | ((unsigned long long)dn << kJBits) | j;
-                if (occ == kEmpty64) {
-                    S.tab[local] = mine;
-                    S.tgd[local] = (uint8_t)(gn < 0 ? 0xFF : gn);
-                } else if (d2 < __uint_as_float((uint32_t)(occ >> 33))) {  // strict: ties keep the old point
-                    const uint32_t og = S.tgd[local];
-                    S.tab[local] = mine;
-                    S.tgd[local] = (uint8_t)(gn < 0 ? 0xFF : gn);
-                    em = 1;                                // displaced occupant, emitted at this arrival's key
-                    emd = (uint32_t)(occ >> kJBits) & 31u;
-                    emg = og == 0xFFu ? -1 : (int32_t)og;
-                    gsrc = ((uint32_t)occ & kJMask) * 16;
-                } else {
-                    em = 0;                                // the arrival itself overflows
-                    emd = dn;
-                    emg = gn;
+        // ---- phase B (1): chunk i-1's emissions.  Position = emissions to the
+        // same child slab before the chunk + in earlier waves + earlier lanes.
+        {
+            const uint32_t rp = par ^ 1;   // chunk i-1's parity
+            uint32_t pre_l = 0, tot_l = 0;
+            if (lane < kDests) {
+                pre_l = S.dcur[rp][lane];
+                tot_l = pre_l;
+                for (uint32_t q = 0; q < (uint32_t)NW; q++) {
+                    const uint32_t c = S.wcnt[q][lane];
+                    pre_l += q < wv ? c : 0u;
+                    tot_l += c;
                 }
-                pending = false;
-                won = true;
-                claim[hc] = (local << 11) | kClaimDone;
+                if (wv == 0) S.dcur[par][lane] = tot_l;
             }
-            {   // one LDS atomic per wave (same-address LDS atomics serialise per lane)
-                const uint64_t wm = __ballot(won);
-                if ((tid & 63) == 0 && wm) atomicSub(&S.npend[par], (uint32_t)__popcll(wm));
-            }
-            STAMP(4);
-            STAMP_COUNT(9, 1);
-            lds_barrier();
-            STAMP(5);
-            if (first) {   // chunk i-1: stores into its child slabs (positions from phase B)
-                first = false;
-                const uint32_t r = S.wpre[wv][d] + rw;
-                const bool ok = vd && r < S.dcap[d];
-                err |= (vd && !ok) ? (uint32_t)ERR_CAPACITY : 0u;
-                const uint32_t pos = S.doff[d] + r;
+            const uint32_t r = (uint32_t)__shfl((int)pre_l, d, 64) + rw;
+            const bool ok = vd && r < S.dcap[d];
+            err |= (vd && !ok) ? (uint32_t)ERR_CAPACITY : 0u;
+            const uint32_t pos = S.doff[d] + r;
+            if (!(PCC_ABL & 2)) {
                 bst4(oP, ok ? pos * 16 : 0xFFFFFFFFu, prv.em == 1 ? prv.gp : prvb.p);
                 bst(oK, ok ? pos * 4 : 0xFFFFFFFFu, prvb.k);
-                STAMP(6);
             }
-            if (S.npend[par] == 0) break;
-            if (pending) atomicMin(&claim[hc], (local << 11) | tid);
-            STAMP(4);
-            lds_barrier();
-            STAMP(5);
+            STAMP(6);
         }
-        if (hc >= 0) claim[hc] = kEmpty32;   // this buffer is next used two chunks later
-        // gather outside the divergent apply branches (a load into registers that
-        // another branch writes would force a full vmcnt drain); consumed one step later
-        cur.gp = bld4(rP, gsrc);
-        cur.em = em; cur.g = emg; cur.d = emd;
-        STAMP(7);
+        // ---- phase B (2): records of chunk i (walk of the slot's candidate list)
+        int32_t em = (slotted && !cand && (forced || occ != kEmpty64 || (PCC_ABL & 32))) ? 0 : -1;
+        uint32_t emd = dn;
+        uint32_t gsrc = 0xFFFFFFFFu;   // byte offset of a displaced point's payload
+        if (cand) {
+            const uint32_t me = f2u(d2);   // d2 >= +0: the bit patterns order like the values
+            // earliest least earlier candidate (the record before this one, if
+            // this one is a record) and whether a later candidate beats this one
+            uint32_t bd = 0xFFFFFFFFu, bt = kNil;
+            bool beaten = false;
+            for (uint32_t xk = claim[hc] & kNil; xk != kNil; xk = S.cnext[xk]) {
+                const uint32_t dx = S.cd2[xk];
+                if (xk < tid) {
+                    if (dx < bd || (dx == bd && xk < bt)) { bd = dx; bt = xk; }
+                } else if (xk > tid) {
+                    beaten |= dx < me;
+                }
+            }
+            if (bt != kNil && !(me < bd)) {
+                em = 0;                                // not a record: overflows at its key
+            } else {
+                if (bt != kNil) {                      // displaces the record before it
+                    em = 1;
+                    emd = S.cdg[bt];
+                    gsrc = (ci * BS + bt) * 16;
+                } else if (occ != kEmpty64) {          // first record: displaces the occupant
+                    em = 1;
+                    emd = (uint32_t)(occ >> kJBits) & 31u;
+                    gsrc = ((uint32_t)occ & kJMask) * 16;
+                }
+                if (!beaten)                           // last record: the new occupant
+                    S.tab[local] = ((unsigned long long)me << 33) | ((unsigned long long)dn << kJBits) | j;
+            }
+        }
+        STAMP(4);
+        STAMP_COUNT(9, 1);
+        // gather outside the divergent branches (a load into registers that
+        // another branch writes would force a full vmcnt drain); stored next step
+        cur.gp = bld4(rP, (PCC_ABL & 4) ? 0xFFFFFFFFu : gsrc);
+        cur.em = em; cur.d = emd; cur.hc = hc;
+        lds_barrier();
+        STAMP(5);
         STAMP_COUNT(10, 1);
     };
     // nchunks + 1 steps (the last one only emits)
@@ -1032,11 +1055,13 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
     STAMP(11);
 
     // ---- grid points: the table's occupants, payloads gathered with U loads in
-    // flight per thread, compacted into the slab's grid region
+    // flight per thread, compacted into the slab's grid region; their own
+    // grandchild slabs leave the capacities
     constexpr int U = 8;
+    const uint64_t lt = lanemask_lt();
     const __amdgpu_buffer_rsrc_t rG = srd(P.grid + P.grid_off[s], (uint64_t)n * 16);
-    for (int i0 = 0; i0 < TAB; i0 += U * BS) {
-        uint32_t wpos[U], src[U];
+    for (int i0 = 0; i0 < ((PCC_ABL & 1) ? 0 : TAB); i0 += U * BS) {
+        uint32_t wpos[U], src[U], od[U];
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const int i = i0 + u * BS + (int)tid;
@@ -1048,26 +1073,39 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
             wb = __shfl(wb, 0, 64);
             wpos[u] = win ? (wb + (uint32_t)__popcll(m & lt)) * 16 : 0xFFFFFFFFu;
             src[u] = win ? ((uint32_t)occ & kJMask) * 16 : 0xFFFFFFFFu;
+            od[u] = win ? ((uint32_t)(occ >> kJBits) & 31u) : 0xFFFFFFFFu;
         }
         u32x4 pv[U];
 #pragma unroll
         for (int u = 0; u < U; u++) pv[u] = bld4(rP, src[u]);
 #pragma unroll
         for (int u = 0; u < U; u++) bst4(rG, wpos[u], pv[u]);
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            if (od[u] != 0xFFFFFFFFu && !(PCC_ABL & 8)) {
+                const SlotRoute sr = slot_route(__uint_as_float(pv[u].x), __uint_as_float(pv[u].y),
+                                                __uint_as_float(pv[u].z), G);
+                uint32_t rerr = 0, gerr = 0;
+                const int dd = route_dest(sr.rc, cx, cy, cz, t, rerr);
+                const int gg = route_dest(sr.rg, sr.rc.ix, sr.rc.iy, sr.rc.iz, sr.rc.u, gerr);
+                if (dd >= 0 && gg >= 0) atomicSub(&S.gcnt[od[u] * kDests + (uint32_t)gg], 1u);
+            }
+        }
     }
     STAMP(8);
     STAMP_FLUSH(P.stamps);
     if (err) atomicOr(&S.err, err);
     __syncthreads();
+    const uint32_t fp = nchunks & 1;   // dcur after the last (emit-only) step
     if (tid == 0) {
         P.slab_grid_n[s] = S.nwin;
         if (S.err) set_err(P.ctr, S.err);
     }
-    if (tid < kDests) P.dest_n[s * kDests + tid] = S.dcur[tid] < S.dcap[tid] ? S.dcur[tid] : S.dcap[tid];
+    if (tid < kDests) P.dest_n[s * kDests + tid] = S.dcur[fp][tid] < S.dcap[tid] ? S.dcur[fp][tid] : S.dcap[tid];
     // capacities of the child slabs' own child slabs (only rows that will exist)
     for (int i = tid; i < kDests * kDests; i += BS) {
         const int dd = i / kDests;
-        if (S.dcur[dd]) P.gcap[(uint64_t)s * kDests * kDests + i] = S.gcnt[i];
+        if (S.dcur[fp][dd]) P.gcap[(uint64_t)s * kDests * kDests + i] = S.gcnt[i];
     }
 }
 

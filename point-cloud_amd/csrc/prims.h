@@ -16,6 +16,28 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
     return l == 0 ? 0ull : (~0ull >> (64 - l));
 }
 
+// Peers of this lane: the lanes with `act` whose value v (NB low bits) equals
+// this lane's.  One v_cmp per bit (its lane mask is the ballot) and the per-lane
+// select as a 32-bit xor on both halves; every lane of the wave must be active.
+template <int NB>
+__device__ __forceinline__ uint64_t wave_peers(uint32_t v, bool act) {
+    const uint64_t a = __builtin_amdgcn_ballot_w64(act);
+    uint32_t lo = (uint32_t)a, hi = (uint32_t)(a >> 32);
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+        const uint32_t bit = (v >> b) & 1u;
+        const uint64_t bb = __builtin_amdgcn_ballot_w64(bit != 0);
+        const uint32_t inv = bit - 1u;   // 0 if the bit is set, ~0 otherwise
+        lo &= (uint32_t)bb ^ inv;
+        hi &= (uint32_t)(bb >> 32) ^ inv;
+    }
+    return ((uint64_t)hi << 32) | lo;
+}
+// number of set bits of m below this lane
+__device__ __forceinline__ uint32_t mask_rank(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
 // Workgroup barrier that orders LDS only: waits lgkmcnt(0) but leaves global
 // loads in flight (a plain __syncthreads() drains vmcnt and kills prefetch).
 __device__ __forceinline__ void lds_barrier() {
