@@ -735,7 +735,7 @@ struct DenseLds {
     uint32_t claim[2][CLAIM];      // per chunk parity: (slot << 11) | head of the slot's candidate list
     uint32_t cd2[BS];              // candidates of the current chunk, by thread: d2 bits,
     uint16_t cnext[BS];            //   next candidate of the same slot (kNil: end),
-    uint16_t cdg[BS];              //   own child slab
+    uint16_t cdg[BS];              //   own child slab | (grandchild slab + 1) << 5
     uint32_t gcnt[kDests * kDests];
     uint32_t doff[kDests], dcap[kDests];
     uint32_t dcur[2][kDests];      // emissions per child slab before chunk c: dcur[c & 1]
@@ -792,11 +792,14 @@ __device__ __forceinline__ int claim_push(uint32_t* H, uint32_t local, uint32_t 
     return -1;
 }
 
-// Slot-table entry: (d2 bits << 33) | (dest << 28) | j.  d2 >= +0 so its sign
-// bit is free; dest (0..23) is the occupant's child slab, so displacing it needs
-// no access to its payload for routing; j < 2^28 indexes the slab's arrivals.
+// Slot-table entry: (d2 bits << 33) | (dest << 28) | ((g + 1) << 23) | j.  d2 >= +0
+// so its sign bit is free; dest (0..23) and g (grandchild slab inside dest, -1
+// none) route a displaced occupant without its payload; j < 2^23 indexes the
+// slab's arrivals.  Slabs of 2^23 arrivals or more ("wide") use j < 2^28 in
+// place of g and recompute a displaced occupant's g from its gathered payload.
 constexpr uint32_t kJBits = 28;
 constexpr uint32_t kJMask = (1u << kJBits) - 1;
+constexpr uint32_t kJMaskNarrow = (1u << 23) - 1;
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ u32x4 bld4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
@@ -825,7 +828,7 @@ __device__ __forceinline__ void bst4(__amdgpu_buffer_rsrc_t r, uint32_t off, u32
 // stored one step later with the rest of the chunk's emissions.  After the last
 // chunk the table's occupants are the slab's grid points (cell.rs:158-160:
 // order inside a cell file is free).  Grandchild capacities count every
-// arrival's (child, grandchild) slab and subtract the grid points' at the end.
+// emission's (child, grandchild) slab when its rank is taken.
 __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
     using L = DenseLds;
     constexpr int BS = L::BS, TAB = L::TAB, CLAIM = L::CLAIM, NW = L::NW;
@@ -842,6 +845,8 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
         if (tid == 0) set_err(P.ctr, ERR_SLAB_SIZE);
         return;
     }
+    const bool wide = n > kJMaskNarrow;
+    const uint32_t jmask = wide ? kJMask : kJMaskNarrow;
     // reference slot: the one holding the cell centre (metadata.rs:104-106)
     const I3 c0 = hex_from_world(cell_pos1(cx, P.cs), cell_pos1(cy, P.cs), cell_pos1(cz, P.cs), G.cr);
     const int32_t rx = c0.x - P.tx / 2, ry = c0.y - P.ty / 2;
@@ -870,11 +875,12 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
     struct Stage {
         int32_t em;     // -1 none, 0 self, 1 displaced record / occupant
         uint32_t d;     // child slab of the emitted point
+        int32_t g;      // its grandchild slab (-1 none, -2 unknown: wide slab, from gp)
         int32_t hc;     // claim entry of a candidate (cleared one step later)
         u32x4 gp;       // gathered payload of a displaced point
     };
     Stage A;
-    A.em = -1; A.d = 0; A.hc = -1;
+    A.em = -1; A.d = 0; A.g = -1; A.hc = -1;
     A.gp = u32x4{0u, 0u, 0u, 0u};
     Stage B = A;
     // Arrivals are prefetched two chunks ahead into a ring of four register
@@ -940,8 +946,6 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
         if (d2 == 12345.0f) err |= 1u << 29;   // finish the math before the stamp
         STAMP(13);
 #endif
-        // grandchild capacities count every arrival (grid points are subtracted at the end)
-        if (slotted && gn >= 0 && !(PCC_ABL & 8)) atomicAdd(&S.gcnt[dn * kDests + (uint32_t)gn], 1u);
         // Occupant filter (cell.rs:80 strict <: ties keep the old point); the
         // candidates push themselves onto their slot's list.
         unsigned long long occ = kEmpty64;
@@ -958,7 +962,7 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
             if (hc < 0) { err |= ERR_CLAIM; cand = false; }
             S.cd2[tid] = f2u(d2);
             S.cnext[tid] = (uint16_t)prev;
-            S.cdg[tid] = (uint16_t)dn;
+            S.cdg[tid] = (uint16_t)(dn | ((uint32_t)(gn + 1) << 5));
         }
         STAMP(1);
         // ---- phase A (2): wave ranks of chunk i-1's emissions per child slab
@@ -968,6 +972,18 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
         const uint32_t rw = (PCC_ABL & 16) ? 0u : mask_rank(same);
         if (lane < kDests) S.wcnt[wv][lane] = 0;
         if (vd && rw == 0) S.wcnt[wv][d] = (uint32_t)__popcll(same);
+        // grandchild capacities: one LDS add per emission
+        {
+            int32_t gg = prv.g;
+            if (wide && vd && gg == -2) {   // displaced occupant of a wide slab: route its payload
+                const SlotRoute sr = slot_route(__uint_as_float(prv.gp.x), __uint_as_float(prv.gp.y),
+                                                __uint_as_float(prv.gp.z), G);
+                uint32_t rerr = 0, gerr = 0;
+                const int dd = route_dest(sr.rc, cx, cy, cz, t, rerr);
+                gg = dd >= 0 ? route_dest(sr.rg, sr.rc.ix, sr.rc.iy, sr.rc.iz, sr.rc.u, gerr) : -1;
+            }
+            if (!(PCC_ABL & 8) && vd && gg >= 0) atomicAdd(&S.gcnt[d * kDests + gg], 1u);
+        }
         STAMP(2);
         lds_barrier();
         STAMP(3);
@@ -999,6 +1015,7 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
         // ---- phase B (2): records of chunk i (walk of the slot's candidate list)
         int32_t em = (slotted && !cand && (forced || occ != kEmpty64 || (PCC_ABL & 32))) ? 0 : -1;
         uint32_t emd = dn;
+        int32_t emg = gn;
         uint32_t gsrc = 0xFFFFFFFFu;   // byte offset of a displaced point's payload
         if (cand) {
             const uint32_t me = f2u(d2);   // d2 >= +0: the bit patterns order like the values
@@ -1018,16 +1035,20 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
                 em = 0;                                // not a record: overflows at its key
             } else {
                 if (bt != kNil) {                      // displaces the record before it
+                    const uint32_t dg = S.cdg[bt];
                     em = 1;
-                    emd = S.cdg[bt];
+                    emd = dg & 31u;
+                    emg = (int32_t)(dg >> 5) - 1;
                     gsrc = (ci * BS + bt) * 16;
                 } else if (occ != kEmpty64) {          // first record: displaces the occupant
                     em = 1;
                     emd = (uint32_t)(occ >> kJBits) & 31u;
-                    gsrc = ((uint32_t)occ & kJMask) * 16;
+                    emg = wide ? -2 : (int32_t)(((uint32_t)occ >> 23) & 31u) - 1;
+                    gsrc = ((uint32_t)occ & jmask) * 16;
                 }
                 if (!beaten)                           // last record: the new occupant
-                    S.tab[local] = ((unsigned long long)me << 33) | ((unsigned long long)dn << kJBits) | j;
+                    S.tab[local] = ((unsigned long long)me << 33) | ((unsigned long long)dn << kJBits) |
+                                   (wide ? 0u : ((uint32_t)(gn + 1) << 23)) | j;
             }
         }
         STAMP(4);
@@ -1035,7 +1056,7 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
         // gather outside the divergent branches (a load into registers that
         // another branch writes would force a full vmcnt drain); stored next step
         cur.gp = bld4(rP, (PCC_ABL & 4) ? 0xFFFFFFFFu : gsrc);
-        cur.em = em; cur.d = emd; cur.hc = hc;
+        cur.em = em; cur.d = emd; cur.g = emg; cur.hc = hc;
         lds_barrier();
         STAMP(5);
         STAMP_COUNT(10, 1);
@@ -1055,13 +1076,12 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
     STAMP(11);
 
     // ---- grid points: the table's occupants, payloads gathered with U loads in
-    // flight per thread, compacted into the slab's grid region; their own
-    // grandchild slabs leave the capacities
+    // flight per thread, compacted into the slab's grid region
     constexpr int U = 8;
     const uint64_t lt = lanemask_lt();
     const __amdgpu_buffer_rsrc_t rG = srd(P.grid + P.grid_off[s], (uint64_t)n * 16);
     for (int i0 = 0; i0 < ((PCC_ABL & 1) ? 0 : TAB); i0 += U * BS) {
-        uint32_t wpos[U], src[U], od[U];
+        uint32_t wpos[U], src[U];
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const int i = i0 + u * BS + (int)tid;
@@ -1072,25 +1092,13 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
             if ((tid & 63) == 0 && m) wb = atomicAdd(&S.nwin, (uint32_t)__popcll(m));
             wb = __shfl(wb, 0, 64);
             wpos[u] = win ? (wb + (uint32_t)__popcll(m & lt)) * 16 : 0xFFFFFFFFu;
-            src[u] = win ? ((uint32_t)occ & kJMask) * 16 : 0xFFFFFFFFu;
-            od[u] = win ? ((uint32_t)(occ >> kJBits) & 31u) : 0xFFFFFFFFu;
+            src[u] = win ? ((uint32_t)occ & jmask) * 16 : 0xFFFFFFFFu;
         }
         u32x4 pv[U];
 #pragma unroll
         for (int u = 0; u < U; u++) pv[u] = bld4(rP, src[u]);
 #pragma unroll
         for (int u = 0; u < U; u++) bst4(rG, wpos[u], pv[u]);
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            if (od[u] != 0xFFFFFFFFu && !(PCC_ABL & 8)) {
-                const SlotRoute sr = slot_route(__uint_as_float(pv[u].x), __uint_as_float(pv[u].y),
-                                                __uint_as_float(pv[u].z), G);
-                uint32_t rerr = 0, gerr = 0;
-                const int dd = route_dest(sr.rc, cx, cy, cz, t, rerr);
-                const int gg = route_dest(sr.rg, sr.rc.ix, sr.rc.iy, sr.rc.iz, sr.rc.u, gerr);
-                if (dd >= 0 && gg >= 0) atomicSub(&S.gcnt[od[u] * kDests + (uint32_t)gg], 1u);
-            }
-        }
     }
     STAMP(8);
     STAMP_FLUSH(P.stamps);

@@ -169,3 +169,17 @@ def test_ply_cli_roundtrip():
         o.close()
         d, mg, mo = compare_dirs(out, ref)
         assert d == [] and mg == mo
+
+
+def test_wide_slab_over_2_23_arrivals():
+    """One level-0 slab of 9M arrivals (> 2^23): the wide slot-table entry layout
+    (28-bit arrival index, displaced occupants routed from their payload)."""
+    rng = np.random.default_rng(31)
+    n = 9_000_000
+    pts = np.zeros(n, dtype=POINT_DTYPE)
+    pts["x"] = rng.uniform(0.0, 1000.0, n).astype(np.float32)
+    pts["y"] = rng.uniform(0.0, 1000.0, n).astype(np.float32)
+    pts["z"] = rng.uniform(0.0, 5.0, n).astype(np.float32)   # hex layer 0 of level 0 (r = 5.2083)
+    pts["rgba"] = rng.integers(0, 256, (n, 4), dtype=np.uint8)
+    st = _check([pts], fast=True)
+    assert st["levels"] >= 2
