@@ -9,7 +9,7 @@ input to finished cell images in HBM (grid winners, overflow lists, headers'
 values, metadata values).  File writing is not part of a step.
 
 Prints ONE JSON line (rank 0).  Extra objects:
-  roofline     — dominant kernel (dense slab kernel, k_slab<true>): algorithmic
+  roofline     — dominant kernel (dense slab kernel, k_slab): algorithmic
                  bytes (32 B per arrival it processes) / its
                  summed HIP-event duration on the engine stream;
   cpu_baseline — the C oracle (sequential restatement, 1 thread) on a prefix
@@ -72,7 +72,7 @@ PMC_SUMMARY = os.path.join(ROOT, "profiles", "r1_pmc_traffic_1b.json")
 
 
 def pmc_traffic(workload):
-    """HBM bytes per launch of k_slab<true> from the committed rocprofv3 PMC summary
+    """HBM bytes per launch of k_slab (dense slabs) from the committed rocprofv3 PMC summary
     (scripts/pmc.sh + scripts/pmc_summary.py: 2 x FETCH_SIZE + WRITE_SIZE, per
     MI355X_MICROARCH.md), only when it was measured on this exact workload."""
     try:
@@ -86,7 +86,7 @@ def pmc_traffic(workload):
 
 
 def record(args, n_gpus, ms, st_levels, st_cells, st_slabs, arrivals, k, dense_ms, parallelism):
-    """The one JSON line (rank 0).  roofline: dense slab kernel k_slab<true>,
+    """The one JSON line (rank 0).  roofline: dense slab kernel k_slab,
     algorithmic bytes = 32 B per arrival it processed over its
     HIP-event time on the engine stream (rank 0's engine when N > 1)."""
     dense_arr = k["dense_arrivals"]
@@ -114,7 +114,7 @@ def record(args, n_gpus, ms, st_levels, st_cells, st_slabs, arrivals, k, dense_m
         "config": {"workload": workload,
                    "batch": 10000, "levels": st_levels, "cells": st_cells, "slabs": st_slabs,
                    "arrivals_W": arrivals, "parallelism": parallelism},
-        "roofline": {"bound": "hbm", "kernel": "k_slab<dense>", "achieved": achieved, "peak": HBM_PEAK_GBS,
+        "roofline": {"bound": "hbm", "kernel": "k_slab (dense slabs)", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_unit": "HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE)", "traffic_source": tsrc,
                      "alg_bytes_per_launch": 32.0 * k["dense_arrivals"] / max(k["dense_launches"], 1),

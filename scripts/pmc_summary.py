@@ -35,7 +35,7 @@ def main(out_dir, name, bench_json):
         e["hbm_bytes"] = 2.0 * e["fetch_bytes_raw"] + e["write_bytes"]
         e["hbm_bytes_per_launch"] = e["hbm_bytes"] / max(e["launches"], 1)
     bench = json.load(open(bench_json))
-    dense = next(v for n, v in k.items() if n.startswith("void pcc::k_slab<true>"))
+    dense = next(v for n, v in k.items() if n.startswith("pcc::k_slab("))
     arr = bench["stage_ms"]["dense_arrivals"]
     summary = {
         "workload": bench["config"]["workload"],
