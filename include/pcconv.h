@@ -127,9 +127,11 @@ int pcc_get_profile(const pcc_converter* c, pcc_profile* out);
 /* Device pointer of the converter's resident input (n points), for timing. */
 const pcc_point* pcc_device_input(const pcc_converter* c);
 
-/* lib.rs:11-60 convert_from_paths: every file in order (".ply" supported;
- * ".las"/".laz"/".json" inputs are reported as unsupported), one converter,
- * then finish.  Logs like the reference CLI. */
+/* lib.rs:11-60 convert_from_paths: every file in order, one converter, then
+ * finish.  Logs like the reference CLI.  Inputs by extension (lib.rs:62-84):
+ * ".ply" (binary LE/BE; ASCII as empty batches, ply.rs:43-51), ".las"
+ * (uncompressed LAS 1.0-1.4; LAZ point data is reported and skipped), ".json"
+ * (another converted cloud's metadata.json, own.rs, in a fixed enumeration). */
 int pcc_convert_files(const char* out_dir, const char* const* paths, size_t npaths, const pcc_options* opt);
 
 /* ---- Sharded multi-GPU build -------------------------------

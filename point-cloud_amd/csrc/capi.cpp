@@ -491,9 +491,31 @@ int pcc_convert_files(const char* out_dir, const char* const* paths, size_t npat
                 rc = pcc_add_points(c, reinterpret_cast<const pcc_point*>(r.points.data()), r.points.size());
             }
             if (rc) { pcc_close(c); return rc; }
-        } else if (ext == "las" || ext == "laz" || ext == "json") {
-            log_line("ERROR", "'%s' input is not supported by this build yet (LAS/LAZ and point-cloud merge are "
-                     "listed as next steps in DESIGN.md)", ext.c_str());
+        } else if (ext == "las" || ext == "laz") {   // converter/las.rs:14-46
+            LasResult r;
+            std::string err;
+            if (!read_las(p, r, err)) {
+                pcc_close(c);
+                return set_err(-EIO, err);   // the reference unwraps Reader::from_path (las.rs:16)
+            }
+            if (r.laz) {
+                log_line("ERROR", "LAZ-compressed point data is not supported by this build (%s)", p.c_str());
+                continue;
+            }
+            log_line("INFO", "Converting %llu points", (unsigned long long)r.count);
+            rc = pcc_add_points(c, reinterpret_cast<const pcc_point*>(r.points.data()), r.points.size());
+            if (rc) { pcc_close(c); return rc; }
+        } else if (ext == "json") {   // converter/own.rs: another converted cloud as input
+            std::vector<Point> pts;
+            uint64_t total = 0;
+            std::string err;
+            if (read_cloud_points(p, pts, total, err)) {
+                log_line("ERROR", "%s", err.c_str());   // lib.rs:75-77 unwraps; reported instead
+                continue;
+            }
+            log_line("INFO", "Converting %llu points", (unsigned long long)total);
+            rc = pcc_add_points(c, reinterpret_cast<const pcc_point*>(pts.data()), pts.size());
+            if (rc) { pcc_close(c); return rc; }
         } else {
             log_line("WARN", "Unsupported file format '%s'", ext.c_str());   // lib.rs:78-81
         }

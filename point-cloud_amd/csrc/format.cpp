@@ -370,6 +370,88 @@ int prior_from_cells(const std::vector<CellFile>& cells, const Config& cfg, Prio
     return 0;
 }
 
+// ------------------------------------------------------------------ LAS
+bool read_las(const std::string& path, LasResult& out, std::string& err) {
+    FILE* f = fopen(path.c_str(), "rb");
+    if (!f) { err = "cannot open " + path; return false; }
+    uint8_t h[375] = {0};
+    const size_t got = fread(h, 1, sizeof h, f);
+    auto bad = [&](const std::string& what) { err = path + ": " + what; fclose(f); return false; };
+    if (got < 227 || memcmp(h, "LASF", 4) != 0) return bad("not a LAS file");
+    auto u16 = [&](size_t o) { uint16_t v; memcpy(&v, h + o, 2); return v; };
+    auto u32 = [&](size_t o) { uint32_t v; memcpy(&v, h + o, 4); return v; };
+    auto u64 = [&](size_t o) { uint64_t v; memcpy(&v, h + o, 8); return v; };
+    auto f64 = [&](size_t o) { double v; memcpy(&v, h + o, 8); return v; };
+    const uint8_t minor = h[25];
+    const uint16_t hsize = u16(94);
+    const uint32_t data_off = u32(96);
+    const uint8_t fmt_raw = h[104];
+    const uint16_t rec = u16(105);
+    uint64_t n = u32(107);
+    if (minor >= 4 && hsize >= 375 && got >= 255) n = u64(247);   // LAS 1.4 64-bit count
+    out.count = n;
+    out.points.clear();
+    if (fmt_raw & 0x80) { out.laz = true; fclose(f); return true; }   // LAZ-compressed point data
+    const uint8_t fmt = fmt_raw & 0x3F;
+    if (fmt > 10) return bad("unsupported point data format " + std::to_string(fmt));
+    static const int kColorOff[11] = {-1, -1, 20, 28, -1, 28, -1, 30, 30, -1, 30};
+    static const int kMinLen[11] = {20, 28, 26, 34, 57, 63, 30, 36, 38, 59, 67};
+    if (rec < kMinLen[fmt]) return bad("point record shorter than its format");
+    const double sx = f64(131), sy = f64(139), sz = f64(147);
+    const double ox = f64(155), oy = f64(163), oz = f64(171);
+    const int co = kColorOff[fmt];
+    if (fseek(f, (long)data_off, SEEK_SET) != 0) return bad("bad offset to point data");
+    out.points.resize(n);
+    std::vector<uint8_t> buf;
+    const uint64_t chunk = 1 << 16;
+    buf.resize(chunk * rec);
+    for (uint64_t base = 0; base < n; base += chunk) {
+        const uint64_t m = std::min<uint64_t>(chunk, n - base);
+        if (fread(buf.data(), rec, m, f) != m) return bad("truncated point data");
+        for (uint64_t i = 0; i < m; i++) {
+            const uint8_t* r = buf.data() + i * rec;
+            int32_t X, Y, Z;
+            memcpy(&X, r, 4); memcpy(&Y, r + 4, 4); memcpy(&Z, r + 8, 4);
+            Point& p = out.points[base + i];
+            // las Transform::direct: scale * n + offset in f64 (no FMA), then `as f32`
+            p.x = (float)((sx * (double)X) + ox);
+            p.y = (float)((sy * (double)Y) + oy);
+            p.z = (float)((sz * (double)Z) + oz);
+            uint16_t c[3] = {0, 0, 0};
+            if (co >= 0) memcpy(c, r + co, 6);
+            p.rgba[0] = (uint8_t)c[0];   // las.rs:40 `color.red as u8`
+            p.rgba[1] = (uint8_t)c[1];
+            p.rgba[2] = (uint8_t)c[2];
+            p.rgba[3] = 255;
+        }
+    }
+    fclose(f);
+    return true;
+}
+
+int read_cloud_points(const std::string& metadata_path, std::vector<Point>& pts, uint64_t& number_of_points,
+                      std::string& err) {
+    std::ifstream f(metadata_path);
+    if (!f) { err = "cannot open " + metadata_path; return -ENOENT; }
+    std::stringstream ss;
+    ss << f.rdbuf();
+    Metadata m;
+    if (!parse_metadata_json(ss.str(), m, err)) return -EINVAL;   // own.rs:57-60
+    const size_t slash = metadata_path.find_last_of('/');
+    const std::string dir = slash == std::string::npos ? "." : metadata_path.substr(0, slash);
+    std::vector<CellFile> cells;
+    const int rc = read_cloud(dir, m.hierarchies, cells, err);
+    if (rc) return rc;
+    pts.clear();
+    for (const CellFile& c : cells) {   // Cell::all_points cell.rs:66-68
+        pts.insert(pts.end(), c.grid.begin(), c.grid.end());
+        for (const CellFile::Entry& e : c.entries)
+            if (e.some) pts.insert(pts.end(), e.pts.begin(), e.pts.end());
+    }
+    number_of_points = m.number_of_points;
+    return 0;
+}
+
 // ------------------------------------------------------------------ PLY
 namespace {
 enum PType { P_I8, P_U8, P_I16, P_U16, P_I32, P_U32, P_F32, P_F64, P_BAD };

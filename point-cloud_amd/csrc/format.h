@@ -65,4 +65,24 @@ struct PlyResult {
 };
 bool read_ply(const std::string& path, PlyResult& out, std::string& err);
 
+// LAS reader (converter/las.rs:23-46 over las 0.8.4 [dep]): uncompressed LAS
+// 1.0-1.4, point formats 0-10.  x = (scale * X + offset) in f64 (las
+// Transform::direct), then `as f32`; colour = u16 `as u8` (low byte), alpha 255;
+// formats without colour give (0, 0, 0, 255) (Color::default).  Compressed
+// point data (LAZ) is reported as unsupported (`laz` = true, no points).
+struct LasResult {
+    std::vector<Point> points;
+    uint64_t count = 0;   // header number_of_points
+    bool laz = false;
+};
+bool read_las(const std::string& path, LasResult& out, std::string& err);
+
+// Points of a converted cloud used as an input file (converter/own.rs:16-78):
+// h_0 .. h_{H-1}, every cell's grid points then its Some lists.  The reference
+// enumerates directories and FxHashMaps in unspecified order; this reader fixes
+// the order (file names sorted, grid and overflow entries in file order), so
+// parity for this input is defined relative to that enumeration.
+int read_cloud_points(const std::string& metadata_path, std::vector<Point>& pts, uint64_t& number_of_points,
+                      std::string& err);
+
 }  // namespace pcc
