@@ -1468,8 +1468,8 @@ __global__ __launch_bounds__(kSmallBS) void k_slab_small(SlabParams P) {
 // slabs at once, and no s_barrier between waves.  Same-slot arrivals of a
 // 64-arrival chunk are applied in lane (= key) order by claim rounds on the slot
 // key word (claim lane in the top byte); LDS operations of one wave execute in
-// program order.  Grandchild capacities go to gcap with global atomics (gcap is
-// zeroed for the level first).
+// program order.  Grandchild capacities are counted in LDS (two 16-bit counters
+// per word: a slab has < 512 arrivals) and stored once per slab.
 constexpr int kWaveTab = 1024;
 constexpr int kWaveCh = (int)(kWaveMax / 64);
 constexpr uint32_t kNoClaim = 0x7Fu << 24;
@@ -1478,7 +1478,11 @@ struct WaveLds {
     uint32_t tkey[kWaveTab];     // (claim lane << 24) | slot, kEmpty32 = empty
     uint16_t fate[kWaveMax];
     uint32_t doff[kDests], dcap[kDests], dcur[kDests];
+    uint32_t gcnt[kDests * kDests / 2];   // (child, grandchild) counts, 16 bits each
 };
+__device__ __forceinline__ void wave_gcount(WaveLds& W, bool active, uint32_t key) {
+    if (active) atomicAdd(&W.gcnt[key >> 1], (key & 1u) ? 0x10000u : 1u);
+}
 
 __device__ __forceinline__ int wave_entry(WaveLds& W, uint32_t local, uint32_t mask) {
     uint32_t h = hash_slot(local) & mask;
@@ -1492,17 +1496,6 @@ __device__ __forceinline__ int wave_entry(WaveLds& W, uint32_t local, uint32_t m
         h = (h + 1) & mask;
     }
     return -1;
-}
-
-// wave-aggregated global add of 1 per active lane, grouped by key (< 1024)
-__device__ __forceinline__ void wave_add_by_key(uint32_t* base, bool active, uint32_t key, uint64_t lt) {
-    uint64_t same = __ballot(active);
-#pragma unroll
-    for (int b = 0; b < 10; b++) {
-        const uint64_t bb = __ballot(active && ((key >> b) & 1));
-        same &= ((key >> b) & 1) ? bb : ~bb;
-    }
-    if (active && __popcll(same & lt) == 0) atomicAdd(base + key, (uint32_t)__popcll(same));
 }
 
 __global__ __launch_bounds__(64) void k_slab_wave(SlabParams P) {
@@ -1532,6 +1525,7 @@ __global__ __launch_bounds__(64) void k_slab_wave(SlabParams P) {
             pk[c] = bld(rK, v ? j * 4 : 0xFFFFFFFFu);
         }
         for (uint32_t i = lane; i < cap; i += 64) { W.tab[i] = kEmpty64; W.tkey[i] = kEmpty32; }
+        for (uint32_t i = lane; i < kDests * kDests / 2; i += 64) W.gcnt[i] = 0;
         if (lane < kDests) {
             W.dcur[lane] = 0;
             W.doff[lane] = P.dest_off[s * kDests + lane] - dbase;
@@ -1623,13 +1617,8 @@ __global__ __launch_bounds__(64) void k_slab_wave(SlabParams P) {
             // emissions of this chunk, in lane order per child slab
             const bool vd = em >= 0;
             const int dd = vd ? (int)emd : 0;
-            uint64_t same = __ballot(vd);
-#pragma unroll
-            for (int b = 0; b < 5; b++) {
-                const uint64_t bb = __ballot(vd && ((dd >> b) & 1));
-                same &= ((dd >> b) & 1) ? bb : ~bb;
-            }
-            const uint32_t rw = __popcll(same & lt);
+            const uint64_t same = wave_peers<5>((uint32_t)dd, vd);
+            const uint32_t rw = mask_rank(same);
             uint32_t r0 = 0;
             if (vd && rw == 0) r0 = atomicAdd(&W.dcur[dd], (uint32_t)__popcll(same));
             const int leader = vd ? (int)(__ffsll((long long)same) - 1) : (int)lane;
@@ -1642,7 +1631,7 @@ __global__ __launch_bounds__(64) void k_slab_wave(SlabParams P) {
             bst4(oP, (ok && em == 0) ? pos * 16 : 0xFFFFFFFFu, pp[c]);
             bst(oK, po, pk[c]);
             if (ok && em == 1) W.fate[emj] = (uint16_t)pos;
-            wave_add_by_key(gcap_s, ok && em == 0 && g >= 0, (uint32_t)(dd * kDests + (g < 0 ? 0 : g)), lt);
+            wave_gcount(W, ok && em == 0 && g >= 0, (uint32_t)(dd * kDests + (g < 0 ? 0 : g)));
         }
         __syncthreads();
         // pass 2 from registers: grid points and displaced payloads
@@ -1662,7 +1651,7 @@ __global__ __launch_bounds__(64) void k_slab_wave(SlabParams P) {
             bst4(rG, win ? (nwin + (uint32_t)__popcll(m & lt)) * 16 : 0xFFFFFFFFu, pp[c]);
             nwin += (uint32_t)__popcll(m);
             bst4(oP, dsp ? (uint32_t)W.fate[j] * 16 : 0xFFFFFFFFu, pp[c]);
-            wave_add_by_key(gcap_s, dsp && own_g[c] >= 0, (uint32_t)(own_d[c] * kDests + (own_g[c] < 0 ? 0 : own_g[c])), lt);
+            wave_gcount(W, dsp && own_g[c] >= 0, (uint32_t)(own_d[c] * kDests + (own_g[c] < 0 ? 0 : own_g[c])));
         }
         if (lane == 0) {
             P.slab_grid_n[s] = nwin;
@@ -1670,6 +1659,10 @@ __global__ __launch_bounds__(64) void k_slab_wave(SlabParams P) {
         const uint32_t wer = __reduce_or_sync(~0ull, err);
         if (lane == 0 && wer) set_err(P.ctr, wer);
         if (lane < kDests) P.dest_n[s * kDests + lane] = W.dcur[lane] < W.dcap[lane] ? W.dcur[lane] : W.dcap[lane];
+        // grandchild capacities of the child slabs that received emissions
+        for (uint32_t i = lane; i < kDests * kDests; i += 64) {
+            if (W.dcur[i / kDests]) gcap_s[i] = (W.gcnt[i >> 1] >> ((i & 1u) * 16)) & 0xFFFFu;
+        }
         __syncthreads();   // the next slab re-initialises the LDS tables
     }
 }
@@ -2652,9 +2645,6 @@ int Engine::run_level(uint32_t h) {
         fprintf(stderr, "[pcc] level %u: cells %u slabs %u (dense %u, small %u) arrivals %llu max_slab %u\n", h, L->ncells,
                 L->nslabs, L->nbig, L->nsmall, (unsigned long long)L->arrivals, L->max_slab);
     }
-    // one-wave slabs accumulate grandchild capacities with atomics: zero gcap
-    // before any slab kernel of this level writes its rows
-    if (L->nsmall) HIP_CHECK(hipMemsetAsync(L->gcap, 0, (uint64_t)L->nslabs * kDests * kDests * 4, stream_));
     if (L->nbig) {
         SP.list = L->big_list;
 #ifdef PCC_STAMPS
@@ -2685,7 +2675,7 @@ int Engine::run_level(uint32_t h) {
         uint32_t hcnt[2];
         HIP_CHECK(hipMemcpyAsync(hcnt, cnt, 8, hipMemcpyDeviceToHost, stream_));
         HIP_CHECK(hipStreamSynchronize(stream_));
-        if (hcnt[0]) {   // wave slabs accumulate grandchild capacities with atomics (gcap zeroed above)
+        if (hcnt[0]) {
             SP.wdesc = wd;
             SP.nwave = hcnt[0];
             k_slab_wave<<<std::min<uint32_t>(hcnt[0], wave_grid_), 64, 0, stream_>>>(SP);
