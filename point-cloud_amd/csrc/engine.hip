@@ -430,26 +430,35 @@ __device__ __forceinline__ uint32_t l0_hash(unsigned long long k) {
     return (uint32_t)k;
 }
 
-// dense slab id of a point: ((cell - lo) linearised) * nl + (layer - (dim2*iz - 2));
-// ordered by (cell, layer) exactly like the compact slab ids.
+// Dense slab id of a point: ((cell - lo) linearised) * kL0Layers + (layer -
+// (dim2*iz - 2)); ordered by (cell, layer) exactly like the compact slab ids.
+// The layer part (< nl <= 194) is a function of z alone, so the radix pass on
+// the low 6 bits needs no bounding box and runs fused with its reduction.
+constexpr int kL0LayerBits = 8;
+constexpr uint32_t kL0Layers = 1u << kL0LayerBits;
+__device__ __forceinline__ int64_t l0_layer(const L0Params& P, float z, int32_t& iz) {
+    iz = cell_index1(z, P.cs);
+    const int32_t t = sat_i32(z / P.cr);   // hex.rs:83 z slot (truncation)
+    return (int64_t)t - ((int64_t)P.dim2 * iz - 2);
+}
 __device__ __forceinline__ int64_t l0_dense(const L0Params& P, float x, float y, float z) {
-    int32_t ix = cell_index1(x, P.cs), iy = cell_index1(y, P.cs), iz = cell_index1(z, P.cs);
+    int32_t iz;
+    const int64_t ll = l0_layer(P, z, iz);
+    int32_t ix = cell_index1(x, P.cs), iy = cell_index1(y, P.cs);
     int32_t gx = ix - P.lo[0], gy = iy - P.lo[1], gz = iz - P.lo[2];
-    int32_t t = sat_i32(z / P.cr);   // hex.rs:83 z slot (truncation)
-    int64_t ll = (int64_t)t - ((int64_t)P.dim2 * iz - 2);
     if (gx < 0 || gy < 0 || gz < 0 || gx >= P.g[0] || gy >= P.g[1] || gz >= P.g[2] || ll < 0 || ll >= P.nl) return -1;
     if (P.hashed) {
         const unsigned long long key = l0_pack(gx, gy, gz);
         uint32_t h = l0_hash(key) & P.hmask;
         for (uint32_t probe = 0; probe <= P.hmask; probe++) {
             const unsigned long long k = P.hkeys[h];
-            if (k == key) return (int64_t)P.hcid[h] * P.nl + ll;
+            if (k == key) return (int64_t)P.hcid[h] * kL0Layers + ll;
             if (k == kHashEmpty) return -1;
             h = (h + 1) & P.hmask;
         }
         return -1;
     }
-    return (((int64_t)gz * P.g[1] + gy) * P.g[0] + gx) * P.nl + ll;
+    return (((int64_t)gz * P.g[1] + gy) * P.g[0] + gx) * kL0Layers + ll;
 }
 
 // sparse mode: insert every point's level-0 cell into the hash set (a plain read
@@ -491,19 +500,19 @@ __global__ void k_l0_hash_ids(const unsigned long long* hkeys, uint32_t cap, uin
 constexpr int kL0BS = 256, kL0IPT = 4, kL0Tile = kL0BS * kL0IPT, kL0W = kL0BS / 64;
 constexpr int kHistLds = 8192;
 
-// pass-0 upsweep from the AoS input: per-tile digit histogram + full dense-slab histogram
-// (grid-stride over tiles so the dense histogram is flushed once per workgroup)
-template <int BITS>
-__global__ __launch_bounds__(kL0BS) void k_l0_up0(const Point* __restrict__ in, uint64_t n, L0Params P, int shift,
-                                                  uint32_t* __restrict__ counts, uint32_t ntiles, uint32_t* hist,
-                                                  uint32_t D, Counters* ctr) {
-    constexpr int R = 1 << BITS;
+// Pass-0 upsweep from the AoS input, fused with the bounding box
+// (converter.rs:96-104, bounding-volume/src/lib.rs:38-52): per-tile histogram of
+// the low 6 bits of the layer (no bbox needed) and per-block min/max partials
+// (finished by k_bbox_final).  Grid-stride over the tiles.
+__global__ __launch_bounds__(kL0BS) void k_l0_up0_bbox(const Point* __restrict__ in, uint64_t n, L0Params P,
+                                                       uint32_t* __restrict__ counts, uint32_t ntiles, float* part,
+                                                       uint32_t* flag) {
+    constexpr int R = 1 << 6;
     __shared__ uint32_t dh[R];
-    __shared__ uint32_t h[kHistLds];
-    const bool lds = D <= (uint32_t)kHistLds;
-    if (lds) for (uint32_t i = threadIdx.x; i < D; i += kL0BS) h[i] = 0;
+    __shared__ float sb[kL0BS / 64][6];
     const float4* p4 = reinterpret_cast<const float4*>(in);
-    uint32_t err = 0;
+    float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+    bool bad = false;
     for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         for (int i = threadIdx.x; i < R; i += kL0BS) dh[i] = 0;
         __syncthreads();
@@ -513,6 +522,60 @@ __global__ __launch_bounds__(kL0BS) void k_l0_up0(const Point* __restrict__ in, 
         for (int r = 0; r < kL0IPT; r++) {
             const uint64_t i = base + (uint64_t)r * kL0BS + threadIdx.x;
             if (i < n) v[r] = p4[i];
+        }
+#pragma unroll
+        for (int r = 0; r < kL0IPT; r++) {
+            const uint64_t i = base + (uint64_t)r * kL0BS + threadIdx.x;
+            if (i < n) {
+                bad |= !(isfinite(v[r].x) && isfinite(v[r].y) && isfinite(v[r].z));
+                mn[0] = fminf(mn[0], v[r].x); mn[1] = fminf(mn[1], v[r].y); mn[2] = fminf(mn[2], v[r].z);
+                mx[0] = fmaxf(mx[0], v[r].x); mx[1] = fmaxf(mx[1], v[r].y); mx[2] = fmaxf(mx[2], v[r].z);
+                int32_t iz;
+                const int64_t ll = l0_layer(P, v[r].z, iz);
+                atomicAdd(&dh[(uint32_t)ll & (R - 1)], 1u);
+            }
+        }
+        __syncthreads();
+        for (int d = threadIdx.x; d < R; d += kL0BS) counts[(uint64_t)d * ntiles + tile] = dh[d];
+    }
+    for (int d = 32; d > 0; d >>= 1)
+        for (int a = 0; a < 3; a++) {
+            mn[a] = fminf(mn[a], __shfl_xor(mn[a], d, 64));
+            mx[a] = fmaxf(mx[a], __shfl_xor(mx[a], d, 64));
+        }
+    const int w = threadIdx.x / 64;
+    if (bad) atomicOr(flag, 1u);
+    if ((threadIdx.x & 63) == 0)
+        for (int a = 0; a < 3; a++) { sb[w][a] = mn[a]; sb[w][3 + a] = mx[a]; }
+    __syncthreads();
+    if (threadIdx.x < 6) {
+        float r = sb[0][threadIdx.x];
+        for (int q = 1; q < kL0BS / 64; q++) r = threadIdx.x < 3 ? fminf(r, sb[q][threadIdx.x]) : fmaxf(r, sb[q][threadIdx.x]);
+        part[blockIdx.x * 6 + threadIdx.x] = r;
+    }
+}
+
+// Pass-1 upsweep from the arena: per-tile digit histogram + the full dense-slab
+// histogram (LDS-privatised when it fits), grid-stride over the tiles.
+template <int BITS>
+__global__ __launch_bounds__(kL0BS) void k_l0_up_hist(Arena A, uint64_t n, L0Params P, int shift,
+                                                      uint32_t* __restrict__ counts, uint32_t ntiles, uint32_t* hist,
+                                                      uint32_t D, Counters* ctr) {
+    constexpr int R = 1 << BITS;
+    __shared__ uint32_t dh[R];
+    __shared__ uint32_t h[kHistLds];
+    const bool lds = D <= (uint32_t)kHistLds;
+    if (lds) for (uint32_t i = threadIdx.x; i < D; i += kL0BS) h[i] = 0;
+    uint32_t err = 0;
+    for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        for (int i = threadIdx.x; i < R; i += kL0BS) dh[i] = 0;
+        __syncthreads();
+        const uint64_t base = (uint64_t)tile * kL0Tile;
+        float4 v[kL0IPT];
+#pragma unroll
+        for (int r = 0; r < kL0IPT; r++) {
+            const uint64_t i = base + (uint64_t)r * kL0BS + threadIdx.x;
+            if (i < n) v[r] = A.p[i];
         }
 #pragma unroll
         for (int r = 0; r < kL0IPT; r++) {
@@ -655,7 +718,7 @@ __global__ void k_l0_flags(const uint32_t* hist, uint32_t D, int32_t nl, uint32_
     if (d < D) sflag[d] = hist[d] ? 1u : 0u;
     if (d < G) {
         uint32_t any = 0;
-        for (int32_t l = 0; l < nl; l++) any |= hist[(uint64_t)d * nl + l];
+        for (int32_t l = 0; l < nl; l++) any |= hist[(uint64_t)d * kL0Layers + l];
         cflag[d] = any ? 1u : 0u;
     }
 }
@@ -682,12 +745,12 @@ __global__ void k_l0_tables(const uint32_t* hist, const uint32_t* cnt_scan, cons
         cell_idx[3 * r + 1] = P.lo[1] + gy;
         cell_idx[3 * r + 2] = P.lo[2] + gz;
         cell_sb[r] = 0;
-        cell_slab0[r] = sflag_scan[(uint64_t)d * P.nl];
+        cell_slab0[r] = sflag_scan[(uint64_t)d * kL0Layers];
     }
     if (d < D && hist[d]) {
         const uint32_t sid = sflag_scan[d];
-        const uint32_t g = d / (uint32_t)P.nl;
-        const int32_t ll = (int32_t)(d % (uint32_t)P.nl);
+        const uint32_t g = d / kL0Layers;
+        const int32_t ll = (int32_t)(d % kL0Layers);
         const int32_t gz = P.hashed ? (int32_t)(P.ckeys[g] >> 42) : (int32_t)(g / ((uint32_t)P.g[0] * (uint32_t)P.g[1]));
         const int32_t iz = P.lo[2] + gz;
         slab_cell[sid] = cflag_scan[g];
@@ -2330,22 +2393,8 @@ int Engine::build() {
     }
     HIP_CHECK(hipMemsetAsync(dev_->ctr, 0, sizeof(Counters), stream_));
 
-    // bbox (K0)
     ev_begin(ST_L0);
-    HIP_CHECK(hipMemsetAsync(dev_->bbox_flag, 0, 4, stream_));
-    const unsigned nbb = grid_for(nsrc_, kBBoxBS, kBBoxBlocks);
-    k_bbox<<<nbb, kBBoxBS, 0, stream_>>>(src_, nsrc_, dev_->bbox_part, dev_->bbox_flag);
-    k_bbox_final<<<1, 64, 0, stream_>>>(dev_->bbox_part, nbb);
-    HIP_CHECK(hipGetLastError());
-    float bb[6];
-    uint32_t bad = 0;
-    HIP_CHECK(hipMemcpyAsync(bb, dev_->bbox_part, sizeof bb, hipMemcpyDeviceToHost, stream_));
-    HIP_CHECK(hipMemcpyAsync(&bad, dev_->bbox_flag, 4, hipMemcpyDeviceToHost, stream_));
-    HIP_CHECK(hipStreamSynchronize(stream_));
-    if (bad) return fail(-22, "input contains NaN or infinite coordinates (unsupported)");
-    for (int a = 0; a < 3; a++) { bmin_[a] = bb[a]; bmax_[a] = bb[3 + a]; }
-
-    int rc = level0_bin();
+    int rc = level0_bin();   // also computes the bounding box (converter.rs:96-104)
     if (rc) return rc;
     stats_.ms_level0_bin = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     for (uint32_t h = 0;; h++) {
@@ -2370,18 +2419,15 @@ int Engine::build() {
 }
 
 template <int BITS>
-static void l0_pass(int p, int passes, const Point* in, const uint32_t* keys, Arena src, Arena dst, uint64_t n, const L0Params& P, int shift,
+static void l0_pass(int p, int passes, Arena src, Arena dst, uint64_t n, const L0Params& P, int shift,
                     uint32_t* counts, uint32_t ntiles, uint32_t* hist, uint32_t D, Counters* ctr, const uint32_t* files,
                     uint32_t nfiles, ScanTemp& scan, hipStream_t st) {
     const uint64_t nc = (uint64_t)ntiles << BITS;
-    if (p == 0) k_l0_up0<BITS><<<std::min<uint32_t>(ntiles, 2048), kL0BS, 0, st>>>(in, n, P, shift, counts, ntiles, hist, D, ctr);
+    if (p == 0) k_l0_up_hist<BITS><<<std::min<uint32_t>(ntiles, 2048), kL0BS, 0, st>>>(src, n, P, shift, counts, ntiles, hist, D, ctr);
     else k_l0_up<BITS><<<ntiles, kL0BS, 0, st>>>(src, n, P, shift, counts, ntiles);
     scan_excl_u32(counts, counts, (uint32_t)nc, nullptr, scan, st);
-    const bool fin = p == passes - 1;
-    if (p == 0 && fin) k_l0_down<BITS, true, true><<<ntiles, kL0BS, 0, st>>>(in, keys, src, dst, n, P, shift, counts, ntiles, files, nfiles);
-    else if (p == 0) k_l0_down<BITS, true, false><<<ntiles, kL0BS, 0, st>>>(in, keys, src, dst, n, P, shift, counts, ntiles, files, nfiles);
-    else if (fin) k_l0_down<BITS, false, true><<<ntiles, kL0BS, 0, st>>>(in, keys, src, dst, n, P, shift, counts, ntiles, files, nfiles);
-    else k_l0_down<BITS, false, false><<<ntiles, kL0BS, 0, st>>>(in, keys, src, dst, n, P, shift, counts, ntiles, files, nfiles);
+    if (p == passes - 1) k_l0_down<BITS, false, true><<<ntiles, kL0BS, 0, st>>>(nullptr, nullptr, src, dst, n, P, shift, counts, ntiles, files, nfiles);
+    else k_l0_down<BITS, false, false><<<ntiles, kL0BS, 0, st>>>(nullptr, nullptr, src, dst, n, P, shift, counts, ntiles, files, nfiles);
     HIP_CHECK(hipGetLastError());
 }
 
@@ -2398,6 +2444,7 @@ int Engine::level0_bin() {
     const SlabGeom g = slab_geom(dim);
     P.nl = g.nl;
     P.dim2 = 2 * (int32_t)dim;
+    if (P.nl > (int32_t)kL0Layers) return fail(-22, "sub_grid_dimension too large for the level-0 layer field");
     uint64_t G = 1;
     bool wide = false;
     P.hashed = 0;
@@ -2405,6 +2452,24 @@ int Engine::level0_bin() {
     P.hkeys = nullptr;
     P.hcid = nullptr;
     P.ckeys = nullptr;
+    // pass 0 of the LSD sort (low 6 bits of the layer: no grid needed) fused
+    // with the bounding box
+    const uint32_t ntiles = (uint32_t)((nsrc_ + kL0Tile - 1) / kL0Tile);
+    uint32_t* counts0 = static_cast<uint32_t*>(dev_->get(((uint64_t)ntiles << 6) * 4 + 64));
+    {
+        HIP_CHECK(hipMemsetAsync(dev_->bbox_flag, 0, 4, stream_));
+        const uint32_t nbb = std::min<uint32_t>(ntiles, kBBoxBlocks);
+        k_l0_up0_bbox<<<nbb, kL0BS, 0, stream_>>>(src_, nsrc_, P, counts0, ntiles, dev_->bbox_part, dev_->bbox_flag);
+        k_bbox_final<<<1, 64, 0, stream_>>>(dev_->bbox_part, nbb);
+        HIP_CHECK(hipGetLastError());
+        float bb[6];
+        uint32_t bad = 0;
+        HIP_CHECK(hipMemcpyAsync(bb, dev_->bbox_part, sizeof bb, hipMemcpyDeviceToHost, stream_));
+        HIP_CHECK(hipMemcpyAsync(&bad, dev_->bbox_flag, 4, hipMemcpyDeviceToHost, stream_));
+        HIP_CHECK(hipStreamSynchronize(stream_));
+        if (bad) return fail(-22, "input contains NaN or infinite coordinates (unsupported)");
+        for (int a = 0; a < 3; a++) { bmin_[a] = bb[a]; bmax_[a] = bb[3 + a]; }
+    }
     for (int a = 0; a < 3; a++) {
         P.lo[a] = cell_index1(bmin_[a], cs);
         const int64_t ext = (int64_t)cell_index1(bmax_[a], cs) - P.lo[a] + 1;
@@ -2444,7 +2509,7 @@ int Engine::level0_bin() {
             break;
         }
     }
-    const uint64_t D = G * (uint64_t)P.nl;
+    const uint64_t D = G * (uint64_t)kL0Layers;
     if (D >= (1ull << 32)) return fail(-27, "too many level-0 slabs (occupied cells x hex layers >= 2^32)");
     uint32_t* hist = static_cast<uint32_t*>(dev_->get(D * 4));
     uint32_t* cnt_scan = static_cast<uint32_t*>(dev_->get(D * 4));
@@ -2453,25 +2518,35 @@ int Engine::level0_bin() {
     uint32_t* cscan = static_cast<uint32_t*>(dev_->get(G * 4));
     uint32_t* d_tot = static_cast<uint32_t*>(dev_->get(16));
     HIP_CHECK(hipMemsetAsync(hist, 0, D * 4, stream_));
-    // LSD passes over the dense slab id (key recomputed from positions every pass)
-    int bits = 0;
-    while ((1ull << bits) < D) bits++;
-    const int passes = std::max(1, (bits + 7) / 8);
-    const int per = std::max(1, (bits + passes - 1) / passes);
-    const uint32_t ntiles = (uint32_t)((nsrc_ + kL0Tile - 1) / kL0Tile);
+    // LSD passes over the dense slab id (key recomputed from positions every
+    // pass): pass 0 on the low 6 layer bits (upsweep done above), then the rest
+    // of the layer and the cell bits in passes of at most 8 bits; the first of
+    // those also builds the dense histogram.
+    int cbits = 0;
+    while ((1ull << cbits) < G) cbits++;
+    const int rem = kL0LayerBits - 6 + cbits;
+    const int passes = std::max(1, (rem + 7) / 8);
+    const int per = std::max(1, (rem + passes - 1) / passes);
     uint32_t* counts = static_cast<uint32_t*>(dev_->get(((uint64_t)ntiles << per) * 4 + 64));
     Arena A0 = dev_->ar[0], A1 = dev_->ar[1];
-    Arena src = A1, dst = (passes % 2) ? A0 : A1;
-    for (int p = 0, shift = 0; p < passes; p++, shift += per) {
+    // the final pass must land in arena 0
+    Arena dst = (passes % 2) ? A1 : A0;
+    scan_excl_u32(counts0, counts0, (uint32_t)((uint64_t)ntiles << 6), nullptr, dev_->scan, stream_);
+    k_l0_down<6, true, false><<<ntiles, kL0BS, 0, stream_>>>(src_, keyed_ ? d_keys_ : nullptr, A1, dst, nsrc_, P, 0,
+                                                              counts0, ntiles, dev_->files, nfiles_dev_);
+    HIP_CHECK(hipGetLastError());
+    Arena src = dst;
+    dst = (dst.p == A0.p) ? A1 : A0;
+    for (int p = 0, shift = 6; p < passes; p++, shift += per) {
         switch (per) {
-            case 1: l0_pass<1>(p, passes, src_, keyed_ ? d_keys_ : nullptr, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, nfiles_dev_, dev_->scan, stream_); break;
-            case 2: l0_pass<2>(p, passes, src_, keyed_ ? d_keys_ : nullptr, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, nfiles_dev_, dev_->scan, stream_); break;
-            case 3: l0_pass<3>(p, passes, src_, keyed_ ? d_keys_ : nullptr, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, nfiles_dev_, dev_->scan, stream_); break;
-            case 4: l0_pass<4>(p, passes, src_, keyed_ ? d_keys_ : nullptr, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, nfiles_dev_, dev_->scan, stream_); break;
-            case 5: l0_pass<5>(p, passes, src_, keyed_ ? d_keys_ : nullptr, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, nfiles_dev_, dev_->scan, stream_); break;
-            case 6: l0_pass<6>(p, passes, src_, keyed_ ? d_keys_ : nullptr, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, nfiles_dev_, dev_->scan, stream_); break;
-            case 7: l0_pass<7>(p, passes, src_, keyed_ ? d_keys_ : nullptr, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, nfiles_dev_, dev_->scan, stream_); break;
-            default: l0_pass<8>(p, passes, src_, keyed_ ? d_keys_ : nullptr, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, nfiles_dev_, dev_->scan, stream_); break;
+            case 1: l0_pass<1>(p, passes, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, nfiles_dev_, dev_->scan, stream_); break;
+            case 2: l0_pass<2>(p, passes, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, nfiles_dev_, dev_->scan, stream_); break;
+            case 3: l0_pass<3>(p, passes, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, nfiles_dev_, dev_->scan, stream_); break;
+            case 4: l0_pass<4>(p, passes, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, nfiles_dev_, dev_->scan, stream_); break;
+            case 5: l0_pass<5>(p, passes, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, nfiles_dev_, dev_->scan, stream_); break;
+            case 6: l0_pass<6>(p, passes, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, nfiles_dev_, dev_->scan, stream_); break;
+            case 7: l0_pass<7>(p, passes, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, nfiles_dev_, dev_->scan, stream_); break;
+            default: l0_pass<8>(p, passes, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, nfiles_dev_, dev_->scan, stream_); break;
         }
         src = dst;
         dst = (dst.p == A0.p) ? A1 : A0;
