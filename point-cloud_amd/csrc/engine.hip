@@ -51,6 +51,7 @@ constexpr uint32_t kEmpty32 = 0xFFFFFFFFu;
 constexpr int kDenseBS = 1024;
 constexpr int kDenseTab = 116 * 132;  // one z-layer of a dim-96 cell (slab_geom)
 constexpr int kDenseClaim = 2048;
+constexpr uint32_t kDenseStreamMax = 24576;   // k_slab: stream (not gather) the grid points up to this many arrivals
 constexpr int kSmallBS = 256;
 constexpr uint32_t kSmallMax = 1024;  // slabs with fewer arrivals use the hashed kernel
 constexpr int kSmallTab = 2048;
@@ -172,7 +173,7 @@ struct Engine::Level {
 #define STAMP_DECL unsigned long long st_t0 = __builtin_amdgcn_s_memtime(), st_acc[16] = {};
 #define STAMP(ph) do { const unsigned long long st_n = __builtin_amdgcn_s_memtime(); st_acc[ph] += st_n - st_t0; st_t0 = st_n; } while (0)
 #define STAMP_COUNT(ph, v) do { st_acc[ph] += (v); } while (0)
-#define STAMP_FLUSH(ptr) do { if ((threadIdx.x & 63) == 0) for (int q_ = 0; q_ < 16; q_++) atomicAdd((ptr) + q_, st_acc[q_]); } while (0)
+#define STAMP_FLUSH(ptr) do { if ((threadIdx.x & 63) == 0 && (blockIdx.x & 63) == 0) for (int q_ = 0; q_ < 16; q_++) atomicAdd((ptr) + q_, st_acc[q_]); } while (0)
 #else
 #define STAMP_DECL
 #define STAMP(ph) do {} while (0)
@@ -391,11 +392,26 @@ __global__ __launch_bounds__(kBBoxBS) void k_bbox(const Point* __restrict__ in, 
     }
 }
 
-__global__ void k_bbox_final(float* part, uint32_t nb) {
+// Reduces the per-block partials (min xyz, max xyz) into part[0..6); one block
+// of 256 threads, strided over the partials.
+__global__ __launch_bounds__(256) void k_bbox_final(float* part, uint32_t nb) {
+    __shared__ float sb[4][6];
+    float r[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    for (uint32_t b = threadIdx.x; b < nb; b += 256)
+        for (int a = 0; a < 6; a++) r[a] = a < 3 ? fminf(r[a], part[b * 6 + a]) : fmaxf(r[a], part[b * 6 + a]);
+    for (int d = 32; d > 0; d >>= 1)
+        for (int a = 0; a < 6; a++) {
+            const float o = __shfl_xor(r[a], d, 64);
+            r[a] = a < 3 ? fminf(r[a], o) : fmaxf(r[a], o);
+        }
+    if ((threadIdx.x & 63) == 0)
+        for (int a = 0; a < 6; a++) sb[threadIdx.x / 64][a] = r[a];
+    __syncthreads();
     if (threadIdx.x < 6) {
-        float r = part[threadIdx.x];
-        for (uint32_t b = 1; b < nb; b++) r = threadIdx.x < 3 ? fminf(r, part[b * 6 + threadIdx.x]) : fmaxf(r, part[b * 6 + threadIdx.x]);
-        part[threadIdx.x] = r;
+        const int a = threadIdx.x;
+        float v = sb[0][a];
+        for (int q = 1; q < 4; q++) v = a < 3 ? fminf(v, sb[q][a]) : fmaxf(v, sb[q][a]);
+        part[a] = v;
     }
 }
 
@@ -922,18 +938,6 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
     const uint64_t db = (uint64_t)(P.dest_off[s * kDests + kDests - 1] + P.dcap[s * kDests + kDests - 1] - dbase) * 4;
     const __amdgpu_buffer_rsrc_t oP = srd(P.nx.p + dbase, db * 4), oK = srd(P.nx.k + dbase, db);
 
-    for (int i = tid; i < TAB; i += BS) S.tab[i] = kEmpty64;
-    for (int i = tid; i < 2 * CLAIM; i += BS) (&S.claim[0][0])[i] = kEmpty32;
-    for (int i = tid; i < kDests * kDests; i += BS) S.gcnt[i] = 0;
-    if (tid < kDests) {
-        S.dcur[0][tid] = 0;
-        S.dcur[1][tid] = 0;
-        S.doff[tid] = P.dest_off[s * kDests + tid] - dbase;
-        S.dcap[tid] = P.dcap[s * kDests + tid];
-    }
-    if (tid == 0) { S.nwin = 0; S.err = 0; }
-    __syncthreads();
-    STAMP(0);
 
     struct Stage {
         int32_t em;     // -1 none, 0 self, 1 displaced record / occupant
@@ -963,6 +967,19 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
             pre[q].k = 0;
         }
     }
+    // the LDS initialisation overlaps the first two chunks' loads
+    for (int i = tid; i < TAB; i += BS) S.tab[i] = kEmpty64;
+    for (int i = tid; i < 2 * CLAIM; i += BS) (&S.claim[0][0])[i] = kEmpty32;
+    for (int i = tid; i < kDests * kDests; i += BS) S.gcnt[i] = 0;
+    if (tid < kDests) {
+        S.dcur[0][tid] = 0;
+        S.dcur[1][tid] = 0;
+        S.doff[tid] = P.dest_off[s * kDests + tid] - dbase;
+        S.dcap[tid] = P.dcap[s * kDests + tid];
+    }
+    if (tid == 0) { S.nwin = 0; S.err = 0; }
+    __syncthreads();
+    STAMP(0);
     const uint32_t nchunks = (n + BS - 1) / BS;
     auto step = [&](uint32_t ci, Stage& cur, Stage& prv, const Pre& mine, const Pre& prvb, Pre& pf) {
         const uint32_t par = ci & 1;
@@ -1138,24 +1155,73 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
     __syncthreads();
     STAMP(11);
 
-    // ---- grid points: the table's occupants, payloads gathered with U loads in
-    // flight per thread, compacted into the slab's grid region
-    constexpr int U = 8;
+    // ---- grid points: the table's occupants, compacted into the slab's grid
+    // region (cell.rs:158-160: order inside a cell file is free).
+    constexpr int U = (TAB + BS - 1) / BS;
     const uint64_t lt = lanemask_lt();
     const __amdgpu_buffer_rsrc_t rG = srd(P.grid + P.grid_off[s], (uint64_t)n * 16);
-    for (int i0 = 0; i0 < ((PCC_ABL & 1) ? 0 : TAB); i0 += U * BS) {
-        uint32_t wpos[U], src[U];
+    if (PCC_ABL & 1) {
+    } else if (n <= kDenseStreamMax) {
+        // Small slab: clear the winners' bits in a bitmap over the arrivals (the
+        // claim tables, all ones after the last step), then stream the arrivals
+        // once in order, coalesced, instead of gathering the winners.
+        uint32_t* bm = &S.claim[0][0];
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            const int i = i0 + u * BS + (int)tid;
+            const int i = u * BS + (int)tid;
+            const unsigned long long occ = i < TAB ? S.tab[i] : kEmpty64;
+            if (occ != kEmpty64) {
+                const uint32_t jw = (uint32_t)occ & jmask;
+                atomicAnd(&bm[jw >> 5], ~(1u << (jw & 31u)));
+            }
+        }
+        __syncthreads();
+        constexpr int V = 4;
+        for (uint32_t j0 = 0; j0 < n; j0 += V * BS) {
+            u32x4 pv[V];
+#pragma unroll
+            for (int u = 0; u < V; u++) pv[u] = bld4(rP, (j0 + u * BS + tid) * 16);   // past n: zero (buffer range)
+            uint64_t m[V];
+            uint32_t tot = 0;
+#pragma unroll
+            for (int u = 0; u < V; u++) {
+                const uint32_t jj = j0 + u * BS + tid;
+                m[u] = __ballot(jj < n && !((bm[jj >> 5] >> (jj & 31u)) & 1u));
+                tot += (uint32_t)__popcll(m[u]);
+            }
+            uint32_t wb = 0;
+            if (lane == 0 && tot) wb = atomicAdd(&S.nwin, tot);
+            wb = __shfl(wb, 0, 64);
+#pragma unroll
+            for (int u = 0; u < V; u++) {
+                const bool win = (m[u] >> lane) & 1ull;
+                bst4(rG, win ? (wb + (uint32_t)__popcll(m[u] & lt)) * 16 : 0xFFFFFFFFu, pv[u]);
+                wb += (uint32_t)__popcll(m[u]);
+            }
+        }
+    } else {
+        // Large slab: gather the winners' payloads, U loads in flight per thread,
+        // one LDS atomic per wave for the positions.
+        uint32_t wpos[U], src[U];
+        uint64_t m[U];
+        uint32_t tot = 0;
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int i = u * BS + (int)tid;
             const unsigned long long occ = i < TAB ? S.tab[i] : kEmpty64;
             const bool win = occ != kEmpty64;
-            const uint64_t m = __ballot(win);
-            uint32_t wb = 0;
-            if ((tid & 63) == 0 && m) wb = atomicAdd(&S.nwin, (uint32_t)__popcll(m));
-            wb = __shfl(wb, 0, 64);
-            wpos[u] = win ? (wb + (uint32_t)__popcll(m & lt)) * 16 : 0xFFFFFFFFu;
+            m[u] = __ballot(win);
+            tot += (uint32_t)__popcll(m[u]);
             src[u] = win ? ((uint32_t)occ & jmask) * 16 : 0xFFFFFFFFu;
+        }
+        uint32_t wb = 0;
+        if (lane == 0 && tot) wb = atomicAdd(&S.nwin, tot);
+        wb = __shfl(wb, 0, 64);
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const bool win = (m[u] >> lane) & 1ull;
+            wpos[u] = win ? (wb + (uint32_t)__popcll(m[u] & lt)) * 16 : 0xFFFFFFFFu;
+            wb += (uint32_t)__popcll(m[u]);
         }
         u32x4 pv[U];
 #pragma unroll
@@ -2460,7 +2526,7 @@ int Engine::level0_bin() {
         HIP_CHECK(hipMemsetAsync(dev_->bbox_flag, 0, 4, stream_));
         const uint32_t nbb = std::min<uint32_t>(ntiles, kBBoxBlocks);
         k_l0_up0_bbox<<<nbb, kL0BS, 0, stream_>>>(src_, nsrc_, P, counts0, ntiles, dev_->bbox_part, dev_->bbox_flag);
-        k_bbox_final<<<1, 64, 0, stream_>>>(dev_->bbox_part, nbb);
+        k_bbox_final<<<1, 256, 0, stream_>>>(dev_->bbox_part, nbb);
         HIP_CHECK(hipGetLastError());
         float bb[6];
         uint32_t bad = 0;
@@ -3043,7 +3109,7 @@ int shard_bbox(const Point* d, uint64_t n, float bmin[3], float bmax[3], int dev
     HIP_CHECK(hipMemsetAsync(S.flag, 0, 4, S.st));
     const unsigned nbb = grid_for(n, kBBoxBS, kBBoxBlocks);
     k_bbox<<<nbb, kBBoxBS, 0, S.st>>>(d, n, S.part, S.flag);
-    k_bbox_final<<<1, 64, 0, S.st>>>(S.part, nbb);
+    k_bbox_final<<<1, 256, 0, S.st>>>(S.part, nbb);
     HIP_CHECK(hipGetLastError());
     float bb[6];
     uint32_t bad = 0;

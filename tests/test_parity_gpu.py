@@ -53,6 +53,14 @@ def test_batch_size_one_and_tiny_limit():
     _check([pts], cfg=dict(cell_point_overflow_limit=3, sub_grid_dimension=4, max_cell_size=8.0), batch=1)
 
 
+def test_gui_batch_size_50k():
+    """The GUI path's default batch size (src/plugins/converter.rs:198-201,604: 50 000 per
+    batch) over ragged files: batch boundaries move the event batches."""
+    pts = synth(14, 1, 1_300_000)
+    files = [pts[:420_001], pts[420_001:420_001], pts[420_001:]]
+    _check(files, batch=50_000, fast=True)
+
+
 def test_clustered_1m():
     pts = synth(3, 1, 1_000_000)
     st = _check([pts], fast=True)
