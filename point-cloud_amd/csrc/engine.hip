@@ -513,7 +513,11 @@ __global__ void k_l0_hash_ids(const unsigned long long* hkeys, uint32_t cap, uin
     if (i < cap && hkeys[i] != kHashEmpty) ckeys[hcid[i]] = hkeys[i];
 }
 
-constexpr int kL0BS = 256, kL0IPT = 4, kL0Tile = kL0BS * kL0IPT, kL0W = kL0BS / 64;
+#ifndef PCC_L0BS
+#define PCC_L0BS 256
+#define PCC_L0IPT 4
+#endif
+constexpr int kL0BS = PCC_L0BS, kL0IPT = PCC_L0IPT, kL0Tile = kL0BS * kL0IPT, kL0W = kL0BS / 64;
 constexpr int kHistLds = 8192;
 
 // Pass-0 upsweep from the AoS input, fused with the bounding box
@@ -1304,21 +1308,22 @@ __global__ void k_small_desc(const uint32_t* list, uint32_t nlist, const uint32_
     D.cz = cell_idx[3 * cr_ + 2];
     D.sb = cell_sb[cr_];
     D.pad0 = D.pad1 = 0;
-    // one atomic per wave and class
-    const bool w = D.n < kWaveMax;
-    const uint64_t mw = __ballot(w), mb = __ballot(!w);
+    // size class: 0..2 one wave (< 128, < 256, < 512 arrivals), 3 block; the
+    // wave classes share wave_out, class c from offset c * nlist
+    const uint32_t cls = D.n < kWaveMax / 4 ? 0u : (D.n < kWaveMax / 2 ? 1u : (D.n < kWaveMax ? 2u : 3u));
     const uint64_t lt = lanemask_lt();
-    const uint32_t lead = __lane_id() == (uint32_t)(__ffsll((long long)__ballot(1)) - 1);
-    uint32_t bw = 0, bb = 0;
-    if (lead) {
-        if (mw) bw = atomicAdd(&counts[0], (uint32_t)__popcll(mw));
-        if (mb) bb = atomicAdd(&counts[1], (uint32_t)__popcll(mb));
-    }
     const int src = __ffsll((long long)__ballot(1)) - 1;
-    bw = __shfl(bw, src, 64);
-    bb = __shfl(bb, src, 64);
-    if (w) wave_out[bw + __popcll(mw & lt)] = D;
-    else block_out[bb + __popcll(mb & lt)] = D;
+    uint32_t base = 0, rank = 0;
+#pragma unroll
+    for (uint32_t c = 0; c < 4; c++) {
+        const uint64_t m = __ballot(cls == c);
+        uint32_t b = 0;
+        if (__lane_id() == (uint32_t)src && m) b = atomicAdd(&counts[c], (uint32_t)__popcll(m));
+        b = __shfl(b, src, 64);
+        if (cls == c) { base = b; rank = (uint32_t)__popcll(m & lt); }
+    }
+    if (cls < 3) wave_out[(uint64_t)cls * nlist + base + rank] = D;
+    else block_out[base + rank] = D;
 }
 
 // Per-thread register copy of one small slab's inputs (loaded one slab ahead).
@@ -1599,21 +1604,26 @@ __global__ __launch_bounds__(kSmallBS) void k_slab_small(SlabParams P) {
 // key word (claim lane in the top byte); LDS operations of one wave execute in
 // program order.  Grandchild capacities are counted in LDS (two 16-bit counters
 // per word: a slab has < 512 arrivals) and stored once per slab.
-constexpr int kWaveTab = 1024;
-constexpr int kWaveCh = (int)(kWaveMax / 64);
+// Instantiated per size class (CH chunks of 64: slabs of < 64 * CH arrivals,
+// table 128 * CH entries), so the classes of small slabs hold less LDS and
+// fewer registers and more of them fit on a CU.
 constexpr uint32_t kNoClaim = 0x7Fu << 24;
+template <int CH>
 struct WaveLds {
-    unsigned long long tab[kWaveTab];
-    uint32_t tkey[kWaveTab];     // (claim lane << 24) | slot, kEmpty32 = empty
-    uint16_t fate[kWaveMax];
+    static constexpr int TAB = 128 * CH;
+    unsigned long long tab[TAB];
+    uint32_t tkey[TAB];          // (claim lane << 24) | slot, kEmpty32 = empty
+    uint16_t fate[64 * CH];
     uint32_t doff[kDests], dcap[kDests], dcur[kDests];
     uint32_t gcnt[kDests * kDests / 2];   // (child, grandchild) counts, 16 bits each
 };
-__device__ __forceinline__ void wave_gcount(WaveLds& W, bool active, uint32_t key) {
+template <class WL>
+__device__ __forceinline__ void wave_gcount(WL& W, bool active, uint32_t key) {
     if (active) atomicAdd(&W.gcnt[key >> 1], (key & 1u) ? 0x10000u : 1u);
 }
 
-__device__ __forceinline__ int wave_entry(WaveLds& W, uint32_t local, uint32_t mask) {
+template <class WL>
+__device__ __forceinline__ int wave_entry(WL& W, uint32_t local, uint32_t mask) {
     uint32_t h = hash_slot(local) & mask;
     for (uint32_t probe = 0; probe <= mask; probe++) {
         const uint32_t k = W.tkey[h];
@@ -1627,9 +1637,10 @@ __device__ __forceinline__ int wave_entry(WaveLds& W, uint32_t local, uint32_t m
     return -1;
 }
 
+template <int CH>
 __global__ __launch_bounds__(64) void k_slab_wave(SlabParams P) {
-    constexpr int CH = kWaveCh;
-    __shared__ WaveLds W;
+    using WL = WaveLds<CH>;
+    __shared__ WL W;
     const uint32_t lane = threadIdx.x;
     const uint64_t lt = lanemask_lt();
     const LevelGeo& G = P.G;
@@ -1639,7 +1650,7 @@ __global__ __launch_bounds__(64) void k_slab_wave(SlabParams P) {
         const int32_t t = D.t, cx = D.cx, cy = D.cy, cz = D.cz;
         const uint32_t nch = (n + 63) / 64;
         uint32_t cap = 64;
-        while (cap < 2 * n && cap < (uint32_t)kWaveTab) cap <<= 1;
+        while (cap < 2 * n && cap < (uint32_t)WL::TAB) cap <<= 1;
         const uint32_t mask = cap - 1;
         const uint64_t nb = (uint64_t)n * 4, db = (uint64_t)D.dlen * 4;
         const __amdgpu_buffer_rsrc_t rP = srd(P.in.p + off, nb * 4), rK = srd(P.in.k + off, nb);
@@ -2176,8 +2187,12 @@ Engine::Engine(const Config& cfg, int device, hipStream_t stream) : cfg_(cfg), d
     HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device_));
     HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_slab_small, kSmallBS, 0));
     small_grid_ = (uint32_t)std::max(1, cus * std::max(per, 1));
-    HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_slab_wave, 64, 0));
-    wave_grid_ = (uint32_t)std::max(1, cus * std::max(per, 1));
+    HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_slab_wave<kWaveMax / 256>, 64, 0));
+    wave_grid_[0] = (uint32_t)std::max(1, cus * std::max(per, 1));
+    HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_slab_wave<kWaveMax / 128>, 64, 0));
+    wave_grid_[1] = (uint32_t)std::max(1, cus * std::max(per, 1));
+    HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_slab_wave<kWaveMax / 64>, 64, 0));
+    wave_grid_[2] = (uint32_t)std::max(1, cus * std::max(per, 1));
 }
 
 Engine::~Engine() {
@@ -2806,25 +2821,29 @@ int Engine::run_level(uint32_t h) {
         SP.stamps = stamps + 16;
 #endif
         ev_begin(ST_SMALL);
-        SmallDesc* wd = static_cast<SmallDesc*>(dev_->get((uint64_t)L->nsmall * sizeof(SmallDesc)));
+        SmallDesc* wd = static_cast<SmallDesc*>(dev_->get((uint64_t)L->nsmall * 3 * sizeof(SmallDesc)));
         SmallDesc* bd = static_cast<SmallDesc*>(dev_->get((uint64_t)L->nsmall * sizeof(SmallDesc)));
-        uint32_t* cnt = static_cast<uint32_t*>(dev_->get(8));
-        HIP_CHECK(hipMemsetAsync(cnt, 0, 8, stream_));
+        uint32_t* cnt = static_cast<uint32_t*>(dev_->get(16));
+        HIP_CHECK(hipMemsetAsync(cnt, 0, 16, stream_));
         k_small_desc<<<grid_for(L->nsmall, 256, 1u << 30), 256, 0, stream_>>>(
             L->small_list, L->nsmall, L->slab_cell, L->slab_layer, L->slab_off, L->slab_n, L->cell_idx, L->cell_sb,
             L->dest_off, L->dcap, wd, bd, cnt);
-        uint32_t hcnt[2];
-        HIP_CHECK(hipMemcpyAsync(hcnt, cnt, 8, hipMemcpyDeviceToHost, stream_));
+        uint32_t hcnt[4];
+        HIP_CHECK(hipMemcpyAsync(hcnt, cnt, 16, hipMemcpyDeviceToHost, stream_));
         HIP_CHECK(hipStreamSynchronize(stream_));
-        if (hcnt[0]) {
-            SP.wdesc = wd;
-            SP.nwave = hcnt[0];
-            k_slab_wave<<<std::min<uint32_t>(hcnt[0], wave_grid_), 64, 0, stream_>>>(SP);
+        for (int c = 0; c < 3; c++) {
+            if (!hcnt[c]) continue;
+            SP.wdesc = wd + (uint64_t)c * L->nsmall;
+            SP.nwave = hcnt[c];
+            const uint32_t gr = std::min<uint32_t>(hcnt[c], wave_grid_[c]);
+            if (c == 0) k_slab_wave<kWaveMax / 256><<<gr, 64, 0, stream_>>>(SP);
+            else if (c == 1) k_slab_wave<kWaveMax / 128><<<gr, 64, 0, stream_>>>(SP);
+            else k_slab_wave<kWaveMax / 64><<<gr, 64, 0, stream_>>>(SP);
         }
-        if (hcnt[1]) {
+        if (hcnt[3]) {
             SP.sdesc = bd;
-            SP.nlist = hcnt[1];
-            k_slab_small<<<std::min<uint32_t>(hcnt[1], small_grid_), kSmallBS, 0, stream_>>>(SP);
+            SP.nlist = hcnt[3];
+            k_slab_small<<<std::min<uint32_t>(hcnt[3], small_grid_), kSmallBS, 0, stream_>>>(SP);
         }
         ev_end(ST_SMALL);
     }
