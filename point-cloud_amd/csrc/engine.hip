@@ -859,12 +859,9 @@ __device__ __forceinline__ int claim_push(uint32_t* H, uint32_t local, uint32_t 
     const uint32_t mine = (local << 11) | tid;
     uint32_t h = hash_slot(local) & (CLAIM - 1);
     for (int probe = 0; probe < CLAIM; probe++) {
-        uint32_t e = H[h];
-        if (e == kEmpty32) {
-            const uint32_t old = atomicCAS(&H[h], kEmpty32, mine);
-            if (old == kEmpty32) { prev = kNil; return (int)h; }
-            e = old;
-        }
+        // CAS first: an empty entry (the common case) costs one LDS round trip
+        const uint32_t e = atomicCAS(&H[h], kEmpty32, mine);
+        if (e == kEmpty32) { prev = kNil; return (int)h; }
         if ((e >> 11) == local) {
             prev = atomicExch(&H[h], mine) & kNil;
             return (int)h;
@@ -890,6 +887,87 @@ __device__ __forceinline__ u32x4 bld4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
 }
 __device__ __forceinline__ void bst4(__amdgpu_buffer_rsrc_t r, uint32_t off, u32x4 v) {
     __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 0);
+}
+
+// Grid points of a dense slab: the slot table's occupants, compacted into the
+// slab's grid region (cell.rs:158-160: order inside a cell file is free).
+template <class L>
+__device__ __forceinline__ void dense_grid_points(const SlabParams& P, L& S, uint32_t* bm, __amdgpu_buffer_rsrc_t rP,
+                                                  uint32_t s, uint32_t n, uint32_t jmask, uint32_t tid, uint32_t lane) {
+    constexpr int BS = L::BS, TAB = L::TAB;
+    // ---- grid points: the table's occupants, compacted into the slab's grid
+    // region (cell.rs:158-160: order inside a cell file is free).
+    constexpr int U = (TAB + BS - 1) / BS;
+    const uint64_t lt = lanemask_lt();
+    const __amdgpu_buffer_rsrc_t rG = srd(P.grid + P.grid_off[s], (uint64_t)n * 16);
+    if (PCC_ABL & 1) {
+    } else if (n <= kDenseStreamMax) {
+        // Small slab: clear the winners' bits in a bitmap over the arrivals (bm:
+        // the claim tables, all ones after the last step), then stream the arrivals
+        // once in order, coalesced, instead of gathering the winners.
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int i = u * BS + (int)tid;
+            const unsigned long long occ = i < TAB ? S.tab[i] : kEmpty64;
+            if (occ != kEmpty64) {
+                const uint32_t jw = (uint32_t)occ & jmask;
+                atomicAnd(&bm[jw >> 5], ~(1u << (jw & 31u)));
+            }
+        }
+        __syncthreads();
+        constexpr int V = 4;
+        for (uint32_t j0 = 0; j0 < n; j0 += V * BS) {
+            u32x4 pv[V];
+#pragma unroll
+            for (int u = 0; u < V; u++) pv[u] = bld4(rP, (j0 + u * BS + tid) * 16);   // past n: zero (buffer range)
+            uint64_t m[V];
+            uint32_t tot = 0;
+#pragma unroll
+            for (int u = 0; u < V; u++) {
+                const uint32_t jj = j0 + u * BS + tid;
+                m[u] = __ballot(jj < n && !((bm[jj >> 5] >> (jj & 31u)) & 1u));
+                tot += (uint32_t)__popcll(m[u]);
+            }
+            uint32_t wb = 0;
+            if (lane == 0 && tot) wb = atomicAdd(&S.nwin, tot);
+            wb = __shfl(wb, 0, 64);
+#pragma unroll
+            for (int u = 0; u < V; u++) {
+                const bool win = (m[u] >> lane) & 1ull;
+                bst4(rG, win ? (wb + (uint32_t)__popcll(m[u] & lt)) * 16 : 0xFFFFFFFFu, pv[u]);
+                wb += (uint32_t)__popcll(m[u]);
+            }
+        }
+    } else {
+        // Large slab: gather the winners' payloads, U loads in flight per thread,
+        // one LDS atomic per wave for the positions.
+        uint32_t wpos[U], src[U];
+        uint64_t m[U];
+        uint32_t tot = 0;
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int i = u * BS + (int)tid;
+            const unsigned long long occ = i < TAB ? S.tab[i] : kEmpty64;
+            const bool win = occ != kEmpty64;
+            m[u] = __ballot(win);
+            tot += (uint32_t)__popcll(m[u]);
+            src[u] = win ? ((uint32_t)occ & jmask) * 16 : 0xFFFFFFFFu;
+        }
+        uint32_t wb = 0;
+        if (lane == 0 && tot) wb = atomicAdd(&S.nwin, tot);
+        wb = __shfl(wb, 0, 64);
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const bool win = (m[u] >> lane) & 1ull;
+            wpos[u] = win ? (wb + (uint32_t)__popcll(m[u] & lt)) * 16 : 0xFFFFFFFFu;
+            wb += (uint32_t)__popcll(m[u]);
+        }
+        u32x4 pv[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) pv[u] = bld4(rP, src[u]);
+#pragma unroll
+        for (int u = 0; u < U; u++) bst4(rG, wpos[u], pv[u]);
+    }
 }
 
 // One pass over the slab in key order (cell.rs:70-94), one chunk of BS arrivals
@@ -1035,17 +1113,17 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
         unsigned long long occ = kEmpty64;
         bool cand = false;
         int hc = -1;
+        uint32_t myprev = kNil;
         if (slotted && !forced) {
             occ = S.tab[local];
             cand = occ == kEmpty64 || d2 < __uint_as_float((uint32_t)(occ >> 33));
             if (PCC_ABL & 32) cand = false;
         }
         if (cand) {
-            uint32_t prev;
-            hc = claim_push<CLAIM>(claim, local, tid, prev);
+            hc = claim_push<CLAIM>(claim, local, tid, myprev);
             if (hc < 0) { err |= ERR_CLAIM; cand = false; }
             S.cd2[tid] = f2u(d2);
-            S.cnext[tid] = (uint16_t)prev;
+            S.cnext[tid] = (uint16_t)myprev;
             S.cdg[tid] = (uint16_t)(dn | ((uint32_t)(gn + 1) << 5));
         }
         STAMP(1);
@@ -1108,6 +1186,10 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
             uint32_t bd = 0xFFFFFFFFu, bt = kNil;
             bool beaten = false;
             for (uint32_t xk = claim[hc] & kNil; xk != kNil; xk = S.cnext[xk]) {
+                if (xk == tid) {   // own entry: known without LDS reads
+                    xk = myprev;
+                    if (xk == kNil) break;
+                }
                 const uint32_t dx = S.cd2[xk];
                 if (xk < tid) {
                     if (dx < bd || (dx == bd && xk < bt)) { bd = dx; bt = xk; }
@@ -1159,80 +1241,7 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
     __syncthreads();
     STAMP(11);
 
-    // ---- grid points: the table's occupants, compacted into the slab's grid
-    // region (cell.rs:158-160: order inside a cell file is free).
-    constexpr int U = (TAB + BS - 1) / BS;
-    const uint64_t lt = lanemask_lt();
-    const __amdgpu_buffer_rsrc_t rG = srd(P.grid + P.grid_off[s], (uint64_t)n * 16);
-    if (PCC_ABL & 1) {
-    } else if (n <= kDenseStreamMax) {
-        // Small slab: clear the winners' bits in a bitmap over the arrivals (the
-        // claim tables, all ones after the last step), then stream the arrivals
-        // once in order, coalesced, instead of gathering the winners.
-        uint32_t* bm = &S.claim[0][0];
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            const int i = u * BS + (int)tid;
-            const unsigned long long occ = i < TAB ? S.tab[i] : kEmpty64;
-            if (occ != kEmpty64) {
-                const uint32_t jw = (uint32_t)occ & jmask;
-                atomicAnd(&bm[jw >> 5], ~(1u << (jw & 31u)));
-            }
-        }
-        __syncthreads();
-        constexpr int V = 4;
-        for (uint32_t j0 = 0; j0 < n; j0 += V * BS) {
-            u32x4 pv[V];
-#pragma unroll
-            for (int u = 0; u < V; u++) pv[u] = bld4(rP, (j0 + u * BS + tid) * 16);   // past n: zero (buffer range)
-            uint64_t m[V];
-            uint32_t tot = 0;
-#pragma unroll
-            for (int u = 0; u < V; u++) {
-                const uint32_t jj = j0 + u * BS + tid;
-                m[u] = __ballot(jj < n && !((bm[jj >> 5] >> (jj & 31u)) & 1u));
-                tot += (uint32_t)__popcll(m[u]);
-            }
-            uint32_t wb = 0;
-            if (lane == 0 && tot) wb = atomicAdd(&S.nwin, tot);
-            wb = __shfl(wb, 0, 64);
-#pragma unroll
-            for (int u = 0; u < V; u++) {
-                const bool win = (m[u] >> lane) & 1ull;
-                bst4(rG, win ? (wb + (uint32_t)__popcll(m[u] & lt)) * 16 : 0xFFFFFFFFu, pv[u]);
-                wb += (uint32_t)__popcll(m[u]);
-            }
-        }
-    } else {
-        // Large slab: gather the winners' payloads, U loads in flight per thread,
-        // one LDS atomic per wave for the positions.
-        uint32_t wpos[U], src[U];
-        uint64_t m[U];
-        uint32_t tot = 0;
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            const int i = u * BS + (int)tid;
-            const unsigned long long occ = i < TAB ? S.tab[i] : kEmpty64;
-            const bool win = occ != kEmpty64;
-            m[u] = __ballot(win);
-            tot += (uint32_t)__popcll(m[u]);
-            src[u] = win ? ((uint32_t)occ & jmask) * 16 : 0xFFFFFFFFu;
-        }
-        uint32_t wb = 0;
-        if (lane == 0 && tot) wb = atomicAdd(&S.nwin, tot);
-        wb = __shfl(wb, 0, 64);
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            const bool win = (m[u] >> lane) & 1ull;
-            wpos[u] = win ? (wb + (uint32_t)__popcll(m[u] & lt)) * 16 : 0xFFFFFFFFu;
-            wb += (uint32_t)__popcll(m[u]);
-        }
-        u32x4 pv[U];
-#pragma unroll
-        for (int u = 0; u < U; u++) pv[u] = bld4(rP, src[u]);
-#pragma unroll
-        for (int u = 0; u < U; u++) bst4(rG, wpos[u], pv[u]);
-    }
+    dense_grid_points<L>(P, S, &S.claim[0][0], rP, s, n, jmask, tid, lane);
     STAMP(8);
     STAMP_FLUSH(P.stamps);
     if (err) atomicOr(&S.err, err);
