@@ -514,8 +514,8 @@ __global__ void k_l0_hash_ids(const unsigned long long* hkeys, uint32_t cap, uin
 }
 
 #ifndef PCC_L0BS
-#define PCC_L0BS 256
-#define PCC_L0IPT 4
+#define PCC_L0BS 1024
+#define PCC_L0IPT 3
 #endif
 constexpr int kL0BS = PCC_L0BS, kL0IPT = PCC_L0IPT, kL0Tile = kL0BS * kL0IPT, kL0W = kL0BS / 64;
 constexpr int kHistLds = 8192;
@@ -781,6 +781,14 @@ __global__ void k_l0_tables(const uint32_t* hist, const uint32_t* cnt_scan, cons
 }
 
 // ------------------------------------------------------------------ slab kernels
+// Per-slab launch descriptor (one 48-B record: the slab kernels' prologue is
+// one load instead of a chain of dependent table loads).
+struct SmallDesc {
+    uint32_t s, off, n, dbase;
+    int32_t t, cx, cy, cz;
+    uint32_t sb, dlen, pad0, pad1;
+};
+
 struct SlabParams {
     Arena in, nx;
     Point* grid;
@@ -800,6 +808,7 @@ struct SlabParams {
     const struct SmallDesc* sdesc;   // small-slab descriptors (k_slab_small)
     uint32_t nlist;
     const struct SmallDesc* wdesc;   // one-wave slab descriptors (k_slab_wave)
+    const struct SmallDesc* ddesc;   // dense slab descriptors (k_slab), by block
     uint32_t nwave;
     Counters* ctr;
     float cs;
@@ -996,11 +1005,11 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
     __shared__ L S;
     STAMP_DECL
     const uint32_t tid = threadIdx.x, wv = tid / 64, lane = tid & 63;
-    const uint32_t s = P.list[blockIdx.x];
-    const uint32_t cr_ = P.slab_cell[s];
-    const int32_t t = P.slab_layer[s];
-    const uint32_t off = P.slab_off[s], n = P.slab_n[s], nm1 = n - 1;
-    const int32_t cx = P.cell_idx[3 * cr_], cy = P.cell_idx[3 * cr_ + 1], cz = P.cell_idx[3 * cr_ + 2];
+    const SmallDesc D = P.ddesc[blockIdx.x];
+    const uint32_t s = D.s;
+    const int32_t t = D.t;
+    const uint32_t off = D.off, n = D.n, nm1 = n - 1;
+    const int32_t cx = D.cx, cy = D.cy, cz = D.cz;
     const LevelGeo& G = P.G;
     if (n > kJMask) {   // the entry packs j in 28 bits
         if (tid == 0) set_err(P.ctr, ERR_SLAB_SIZE);
@@ -1016,8 +1025,8 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
     // 24 child slabs in the next arena (out-of-range offsets drop a store)
     const uint64_t nb = (uint64_t)n * 4;
     const __amdgpu_buffer_rsrc_t rP = srd(P.in.p + off, nb * 4), rK = srd(P.in.k + off, nb);
-    const uint32_t dbase = P.dest_off[s * kDests];
-    const uint64_t db = (uint64_t)(P.dest_off[s * kDests + kDests - 1] + P.dcap[s * kDests + kDests - 1] - dbase) * 4;
+    const uint32_t dbase = D.dbase;
+    const uint64_t db = (uint64_t)D.dlen * 4;
     const __amdgpu_buffer_rsrc_t oP = srd(P.nx.p + dbase, db * 4), oK = srd(P.nx.k + dbase, db);
 
 
@@ -1292,19 +1301,11 @@ __device__ __forceinline__ int small_entry(SmallLds& S, uint32_t local, uint32_t
 
 // flattened descriptor of a small slab: one scalar load instead of the chain
 // list -> slab tables -> cell tables
-struct SmallDesc {
-    uint32_t s, off, n, dbase;
-    int32_t t, cx, cy, cz;
-    uint32_t sb, dlen, pad0, pad1;
-};
 constexpr uint32_t kWaveMax = 512;   // small slabs below this size: one wave each (k_slab_wave)
-__global__ void k_small_desc(const uint32_t* list, uint32_t nlist, const uint32_t* slab_cell, const int32_t* slab_layer,
-                             const uint32_t* slab_off, const uint32_t* slab_n, const int32_t* cell_idx,
-                             const uint32_t* cell_sb, const uint32_t* dest_off, const uint32_t* dcap, SmallDesc* wave_out,
-                             SmallDesc* block_out, uint32_t* counts) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nlist) return;
-    const uint32_t s = list[i], cr_ = slab_cell[s];
+__device__ __forceinline__ SmallDesc slab_desc(uint32_t s, const uint32_t* slab_cell, const int32_t* slab_layer,
+                                               const uint32_t* slab_off, const uint32_t* slab_n, const int32_t* cell_idx,
+                                               const uint32_t* cell_sb, const uint32_t* dest_off, const uint32_t* dcap) {
+    const uint32_t cr_ = slab_cell[s];
     SmallDesc D;
     D.s = s;
     D.off = slab_off[s];
@@ -1317,22 +1318,49 @@ __global__ void k_small_desc(const uint32_t* list, uint32_t nlist, const uint32_
     D.cz = cell_idx[3 * cr_ + 2];
     D.sb = cell_sb[cr_];
     D.pad0 = D.pad1 = 0;
+    return D;
+}
+
+__global__ void k_dense_desc(const uint32_t* list, uint32_t nlist, const uint32_t* slab_cell, const int32_t* slab_layer,
+                             const uint32_t* slab_off, const uint32_t* slab_n, const int32_t* cell_idx,
+                             const uint32_t* cell_sb, const uint32_t* dest_off, const uint32_t* dcap, SmallDesc* out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < nlist) out[i] = slab_desc(list[i], slab_cell, slab_layer, slab_off, slab_n, cell_idx, cell_sb, dest_off, dcap);
+}
+
+__global__ void k_small_desc(const uint32_t* list, uint32_t nlist, const uint32_t* slab_cell, const int32_t* slab_layer,
+                             const uint32_t* slab_off, const uint32_t* slab_n, const int32_t* cell_idx,
+                             const uint32_t* cell_sb, const uint32_t* dest_off, const uint32_t* dcap, SmallDesc* wave_out,
+                             SmallDesc* block_out, uint32_t* counts) {
+    __shared__ uint32_t wc[4][4], bpre[4][4];
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool in = i < nlist;
+    const SmallDesc D = slab_desc(in ? list[i] : list[0], slab_cell, slab_layer, slab_off, slab_n, cell_idx, cell_sb,
+                                  dest_off, dcap);
     // size class: 0..2 one wave (< 128, < 256, < 512 arrivals), 3 block; the
-    // wave classes share wave_out, class c from offset c * nlist
-    const uint32_t cls = D.n < kWaveMax / 4 ? 0u : (D.n < kWaveMax / 2 ? 1u : (D.n < kWaveMax ? 2u : 3u));
+    // wave classes share wave_out, class c from offset c * nlist.  One global
+    // atomic per block and class.
+    const uint32_t cls = !in ? 4u : (D.n < kWaveMax / 4 ? 0u : (D.n < kWaveMax / 2 ? 1u : (D.n < kWaveMax ? 2u : 3u)));
     const uint64_t lt = lanemask_lt();
-    const int src = __ffsll((long long)__ballot(1)) - 1;
-    uint32_t base = 0, rank = 0;
+    const uint32_t w = threadIdx.x / 64;
+    uint32_t rank = 0;
 #pragma unroll
     for (uint32_t c = 0; c < 4; c++) {
         const uint64_t m = __ballot(cls == c);
-        uint32_t b = 0;
-        if (__lane_id() == (uint32_t)src && m) b = atomicAdd(&counts[c], (uint32_t)__popcll(m));
-        b = __shfl(b, src, 64);
-        if (cls == c) { base = b; rank = (uint32_t)__popcll(m & lt); }
+        if (cls == c) rank = (uint32_t)__popcll(m & lt);
+        if (__lane_id() == 0) wc[w][c] = (uint32_t)__popcll(m);
     }
-    if (cls < 3) wave_out[(uint64_t)cls * nlist + base + rank] = D;
-    else block_out[base + rank] = D;
+    __syncthreads();
+    if (threadIdx.x < 4) {
+        const uint32_t c = threadIdx.x;
+        uint32_t acc = 0;
+        for (int q = 0; q < 4; q++) { bpre[q][c] = acc; acc += wc[q][c]; }
+        const uint32_t b = acc ? atomicAdd(&counts[c], acc) : 0u;
+        for (int q = 0; q < 4; q++) bpre[q][c] += b;
+    }
+    __syncthreads();
+    if (cls < 3) wave_out[(uint64_t)cls * nlist + bpre[w][cls] + rank] = D;
+    else if (cls == 3) block_out[bpre[w][3] + rank] = D;
 }
 
 // Per-thread register copy of one small slab's inputs (loaded one slab ahead).
@@ -2812,6 +2840,12 @@ int Engine::run_level(uint32_t h) {
     }
     if (L->nbig) {
         SP.list = L->big_list;
+        SmallDesc* dd = static_cast<SmallDesc*>(dev_->get((uint64_t)L->nbig * sizeof(SmallDesc)));
+        k_dense_desc<<<grid_for(L->nbig, 256, 1u << 30), 256, 0, stream_>>>(L->big_list, L->nbig, L->slab_cell,
+                                                                           L->slab_layer, L->slab_off, L->slab_n,
+                                                                           L->cell_idx, L->cell_sb, L->dest_off,
+                                                                           L->dcap, dd);
+        SP.ddesc = dd;
 #ifdef PCC_STAMPS
         SP.stamps = stamps;
 #endif
