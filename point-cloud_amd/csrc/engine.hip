@@ -1924,15 +1924,20 @@ constexpr int kBktBS = 256;
 __device__ __forceinline__ uint32_t emission_eb(const BucketParams& B, uint32_t key, uint32_t csb) {
     return max(event_batch(B.files, B.nfiles, key), csb);
 }
-// number of elements with eb <= e among the first min(n, cap) of a key-ordered dest list
-__device__ __forceinline__ uint32_t count_le(const BucketParams& B, uint32_t off, uint32_t n, uint32_t cap, uint32_t e,
-                                             uint32_t csb) {
-    uint32_t lo = 0, hi = n < cap ? n : cap;
+// Smallest key with event_batch(key) > e: the first key of batch e + 1, in the
+// last file whose first batch is <= e + 1 (clamped to the next file's start:
+// a short last batch, or batches of an empty reader).
+__device__ __forceinline__ uint32_t first_key_after(const uint32_t* files, uint32_t nfiles, uint32_t e) {
+    const uint32_t b = e + 1;
+    uint32_t lo = 0, hi = nfiles - 1;
     while (lo < hi) {
-        uint32_t mid = (lo + hi) >> 1;
-        if (emission_eb(B, B.nx.k[off + mid], csb) <= e) lo = mid + 1; else hi = mid;
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (files[4 * mid + 2] <= b) lo = mid; else hi = mid - 1;
     }
-    return lo;
+    const uint64_t start = (uint64_t)files[4 * lo] | ((uint64_t)files[4 * lo + 1] << 32);
+    uint64_t k = files[4 * lo + 2] <= b ? start + (uint64_t)(b - files[4 * lo + 2]) * files[4 * lo + 3] : start;
+    if (lo + 1 < nfiles) k = min(k, (uint64_t)files[4 * lo + 4] | ((uint64_t)files[4 * lo + 5] << 32));
+    return (uint32_t)min(k, (uint64_t)0xFFFFFFFFu);
 }
 
 // cell.rs:108-153 add_points_in_overflow, resolved for all batches at once
@@ -2043,22 +2048,74 @@ __global__ __launch_bounds__(kBktBS) void k_bucket(BucketParams B) {
         return;
     }
     // None: spilled.  Spill batch sb = smallest e with c(e) >= L + [c(e0) == L],
-    // c(e) = #bucket emissions with eb <= e (== Appendix C.3's rank rule).
-    auto count = [&](uint32_t e) -> uint32_t {
-        uint32_t c = 0;
-        for (uint32_t i = threadIdx.x; i < nd; i += kBktBS) {
+    // c(e) = #bucket emissions with eb <= e (== Appendix C.3's rank rule).  eb is
+    // monotone in the key inside a list, so a list's share of c(e) is the lower
+    // bound of K(e) = the first key with eb0 > e (0 below the cell's sb).  Binary
+    // search over e; each list keeps the window of its count that the search so
+    // far allows (counts are monotone in e), so a step costs a few loads per list.
+    constexpr int WL = 4;   // lists per thread with a window (nd <= WL * kBktBS)
+    __shared__ uint32_t s_k;
+    const bool windowed = nd <= (uint32_t)(WL * kBktBS);
+    uint32_t wlo[WL], whi[WL], woff[WL], wr[WL];
+#pragma unroll
+    for (int w = 0; w < WL; w++) {
+        wlo[w] = whi[w] = woff[w] = wr[w] = 0;
+        const uint32_t i = threadIdx.x + (uint32_t)w * kBktBS;
+        if (windowed && i < nd) {
             const uint32_t di = (s0 + i / 3) * kDests + oct * 3 + i % 3;
             const uint32_t n = B.dest_n[di];
-            if (n) c += count_le(B, B.dest_off[di], n, L + 1, e, csb);
+            if (n) { woff[w] = B.dest_off[di]; whi[w] = n < L + 1 ? n : L + 1; }
+        }
+    }
+    auto eval = [&](uint32_t e) -> uint32_t {   // c(e) (first L + 1 of each list); wr = per-list shares
+        __syncthreads();
+        if (threadIdx.x == 0) s_k = e < csb ? 0u : first_key_after(B.files, B.nfiles, e);
+        __syncthreads();
+        const uint32_t K = s_k;
+        uint32_t c = 0;
+        if (windowed) {
+#pragma unroll
+            for (int w = 0; w < WL; w++) {
+                uint32_t lo2 = wlo[w], hi2 = whi[w];
+                while (lo2 < hi2) {
+                    const uint32_t mid = (lo2 + hi2) >> 1;
+                    if (B.nx.k[woff[w] + mid] < K) lo2 = mid + 1; else hi2 = mid;
+                }
+                wr[w] = lo2;
+                c += lo2;
+            }
+        } else {
+            for (uint32_t i = threadIdx.x; i < nd; i += kBktBS) {
+                const uint32_t di = (s0 + i / 3) * kDests + oct * 3 + i % 3;
+                const uint32_t n = B.dest_n[di];
+                if (!n) continue;
+                const uint32_t o = B.dest_off[di];
+                uint32_t lo2 = 0, hi2 = n < L + 1 ? n : L + 1;
+                while (lo2 < hi2) {
+                    const uint32_t mid = (lo2 + hi2) >> 1;
+                    if (B.nx.k[o + mid] < K) lo2 = mid + 1; else hi2 = mid;
+                }
+                c += lo2;
+            }
         }
         return block_sum<kBktBS>(c, lds);
     };
-    const uint32_t c0 = count(emin);
+    const uint32_t c0 = eval(emin);
+#pragma unroll
+    for (int w = 0; w < WL; w++) wlo[w] = wr[w];   // every later e is >= emin
     const uint32_t target = L + (c0 == L ? 1u : 0u);
-    uint32_t lo = emin, hi = emax;
+    uint32_t lo = emin, hi = emax;   // c(emax) = tot >= target
     while (lo < hi) {
         const uint32_t mid = lo + (hi - lo) / 2;
-        if (count(mid) >= target) hi = mid; else lo = mid + 1;
+        if (eval(mid) >= target) {
+            hi = mid;
+#pragma unroll
+            for (int w = 0; w < WL; w++) whi[w] = wr[w];
+        } else {
+            lo = mid + 1;
+#pragma unroll
+            for (int w = 0; w < WL; w++) wlo[w] = wr[w];
+        }
     }
     if (threadIdx.x == 0) { B.bkt_state[b] = 2; B.bkt_n[b] = tot; B.bkt_nd[b] = nne; B.bkt_sb[b] = lo; B.bkt_off[b] = 0; }
 }
