@@ -78,9 +78,18 @@ int pcc_options_default(pcc_options* opt);
  * describes a non-empty cloud, every h_{h}/c_*.bin cell is loaded as the
  * starting state (converter.rs:187-207 load_or_create_cell) and the points added
  * afterwards are merged into it (incremental merge: the result equals converting
- * the old and the new files in one run).  Merging is single-GPU (-95 with
- * pcc_declare_files). */
+ * the old and the new files in one run).  With pcc_declare_files (sharded
+ * input) the merge runs on this rank's keys: its seeds, then its new points. */
 int pcc_open(const char* out_dir, const pcc_options* opt, pcc_converter** out);
+
+/* pcc_open for one rank of a sharded merge (the load of
+ * converter.rs:187-207 restricted to the rank's own cells): only the cells of
+ * the n level-0 subtrees in l0_cells (x, y, z triples) are loaded, and only
+ * those are rewritten by pcc_write_cells.  Level-0 subtrees are independent
+ * (a level-h cell's ancestor is its index >> h), so the union over ranks of
+ * the rewritten subtrees equals a single-GPU merge. */
+int pcc_open_subtrees(const char* out_dir, const pcc_options* opt, const int32_t* l0_cells, uint64_t n,
+                      pcc_converter** out);
 
 /* converter.rs:106-112 add_points_batch over ceil(n/batch) consecutive slices
  * (lib.rs:31-52).  Host memory; copied to the device; caller keeps ownership. */

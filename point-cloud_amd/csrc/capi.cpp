@@ -92,7 +92,8 @@ int pcc_options_default(pcc_options* o) {
     return 0;
 }
 
-int pcc_open(const char* out_dir, const pcc_options* opt, pcc_converter** out) {
+static int open_impl(const char* out_dir, const pcc_options* opt, const std::vector<int32_t>* subtrees,
+                     pcc_converter** out) {
     if (!out_dir || !out) return set_err(-EINVAL, "null argument");
     GUARD_BEGIN
     auto c = std::make_unique<pcc_converter>();
@@ -127,7 +128,7 @@ int pcc_open(const char* out_dir, const pcc_options* opt, pcc_converter** out) {
     if (c->merge) {   // converter.rs:187-207: existing cells are the starting state
         std::vector<CellFile> cells;
         std::string err;
-        int rc = read_cloud(c->out_dir, c->prior.hierarchies, cells, err);
+        int rc = read_cloud(c->out_dir, c->prior.hierarchies, cells, err, subtrees);
         if (rc) return set_err(rc, err);
         PriorState ps;
         rc = prior_from_cells(cells, c->meta.config, ps, err);
@@ -137,6 +138,20 @@ int pcc_open(const char* out_dir, const pcc_options* opt, pcc_converter** out) {
     *out = c.release();
     return 0;
     GUARD_END
+}
+
+int pcc_open(const char* out_dir, const pcc_options* opt, pcc_converter** out) {
+    return open_impl(out_dir, opt, nullptr, out);
+}
+
+// Sharded merge: the existing cloud's state is read
+// for the given level-0 subtrees only; cells of other subtrees are neither read
+// nor rewritten by this converter.
+int pcc_open_subtrees(const char* out_dir, const pcc_options* opt, const int32_t* l0_cells, uint64_t n,
+                      pcc_converter** out) {
+    if (!l0_cells && n) return set_err(-EINVAL, "null argument");
+    const std::vector<int32_t> st(l0_cells, l0_cells + 3 * n);
+    return open_impl(out_dir, opt, &st, out);
 }
 
 int pcc_add_points(pcc_converter* c, const pcc_point* pts, uint64_t n) {

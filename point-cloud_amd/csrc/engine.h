@@ -149,6 +149,9 @@ private:
     uint64_t nseeds_ = 0;
     Point* d_comb_ = nullptr;
     uint64_t comb_cap_ = 0;
+    uint32_t* d_ckeys_ = nullptr;        // merge of keyed input: seed keys 0..S-1, then S + key
+    uint64_t ckeys_cap_ = 0;
+    const uint32_t* src_keys_ = nullptr; // keys of src_ (nullptr: key = index)
     bool comb_ok_ = false;
     std::vector<uint64_t> forced_lo_;
     std::vector<uint32_t*> d_prior_cells_;   // PriorCell arrays per level

@@ -2260,6 +2260,12 @@ __global__ __launch_bounds__(256) void k_l0_lists(const uint32_t* slab_n, uint32
 
 __global__ void k_set_u32(uint32_t* p, uint32_t v) { *p = v; }
 
+// keys of a merged keyed input: seeds 0..S-1, then S + the new points' global keys
+__global__ void k_comb_keys(uint32_t* out, const uint32_t* keys, uint64_t S, uint64_t n) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < S + n; i += (uint64_t)gridDim.x * blockDim.x)
+        out[i] = i < S ? (uint32_t)i : (uint32_t)(S + keys[i - S]);
+}
+
 // ------------------------------------------------------------------ host side
 static unsigned grid_for(uint64_t n, unsigned bs, unsigned cap = 65536) {
     uint64_t g = (n + bs - 1) / bs;
@@ -2364,6 +2370,9 @@ void Engine::free_all() {
     d_seeds_ = nullptr;
     (void)hipFree(d_comb_);
     d_comb_ = nullptr;
+    (void)hipFree(d_ckeys_);
+    d_ckeys_ = nullptr;
+    ckeys_cap_ = 0;
     for (uint32_t* q : d_prior_cells_) (void)hipFree(q);
     d_prior_cells_.clear();
 }
@@ -2454,6 +2463,7 @@ void Engine::add_keyed_device(const Point* dpts, const uint32_t* dkeys, uint64_t
     }
     n_ += n;
     keyed_ = true;
+    comb_ok_ = false;
 }
 
 void Engine::set_prior(const PriorState& p) {
@@ -2510,7 +2520,6 @@ int Engine::build() {
     hierarchies_ = nbatches_ > 0 ? 1u : 0u;   // converter.rs:141-158 runs for every batch, even empty
     stats_ = BuildStats();
     if (n_ == 0) return 0;
-    if (prior_ && keyed_) return fail(-95, "incremental merge of a sharded (keyed) build is not supported");
 
     // Input of the build.  Merge mode: the existing
     // cloud's points come first as "seeds" with keys 0 .. S-1, so every one of
@@ -2525,12 +2534,23 @@ int Engine::build() {
             }
             if (nseeds_) HIP_CHECK(hipMemcpyAsync(d_comb_, d_seeds_, nseeds_ * sizeof(Point), hipMemcpyDeviceToDevice, stream_));
             HIP_CHECK(hipMemcpyAsync(d_comb_ + nseeds_, d_in_, n_ * sizeof(Point), hipMemcpyDeviceToDevice, stream_));
+            if (keyed_) {   // sharded merge: this rank's seeds, then its new points with S + global key
+                if (ckeys_cap_ < nseeds_ + n_) {
+                    (void)hipFree(d_ckeys_);
+                    HIP_CHECK(hipMalloc(&d_ckeys_, (nseeds_ + n_) * 4));
+                    ckeys_cap_ = nseeds_ + n_;
+                }
+                k_comb_keys<<<grid_for(nseeds_ + n_, 256), 256, 0, stream_>>>(d_ckeys_, d_keys_, nseeds_, n_);
+                HIP_CHECK(hipGetLastError());
+            }
             comb_ok_ = true;
         }
         src_ = d_comb_;
+        src_keys_ = keyed_ ? d_ckeys_ : nullptr;
         nsrc_ = nseeds_ + n_;
     } else {
         src_ = d_in_;
+        src_keys_ = keyed_ ? d_keys_ : nullptr;
         nsrc_ = n_;
     }
     if (nsrc_ >= 0xFFFFFFFFull) return fail(-75, "more than 2^32-1 points (existing + new) per build are not supported");
@@ -2707,7 +2727,7 @@ int Engine::level0_bin() {
     // the final pass must land in arena 0
     Arena dst = (passes % 2) ? A1 : A0;
     scan_excl_u32(counts0, counts0, (uint32_t)((uint64_t)ntiles << 6), nullptr, dev_->scan, stream_);
-    k_l0_down<6, true, false><<<ntiles, kL0BS, 0, stream_>>>(src_, keyed_ ? d_keys_ : nullptr, A1, dst, nsrc_, P, 0,
+    k_l0_down<6, true, false><<<ntiles, kL0BS, 0, stream_>>>(src_, src_keys_, A1, dst, nsrc_, P, 0,
                                                               counts0, ntiles, dev_->files, nfiles_dev_);
     HIP_CHECK(hipGetLastError());
     Arena src = dst;

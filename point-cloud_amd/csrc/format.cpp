@@ -1,4 +1,5 @@
 // format.cpp — cell / metadata writers and the PLY reader (see format.h).
+#include <array>
 #include "format.h"
 
 #include <dirent.h>
@@ -303,8 +304,17 @@ bool read_cell_file(const std::string& path, CellFile& out, std::string& err) {
     return true;
 }
 
-int read_cloud(const std::string& dir, uint32_t hierarchies, std::vector<CellFile>& cells, std::string& err) {
+int read_cloud(const std::string& dir, uint32_t hierarchies, std::vector<CellFile>& cells, std::string& err,
+               const std::vector<int32_t>* subtrees) {
     cells.clear();
+    // level-0 subtrees to keep (sorted triples); a level-h cell's level-0
+    // ancestor is its index >> h (arithmetic: child = 2 * parent + bit)
+    std::vector<std::array<int32_t, 3>> keep;
+    if (subtrees) {
+        for (size_t i = 0; i + 2 < subtrees->size(); i += 3)
+            keep.push_back({(*subtrees)[i], (*subtrees)[i + 1], (*subtrees)[i + 2]});
+        std::sort(keep.begin(), keep.end());
+    }
     for (uint32_t h = 0; h < hierarchies; h++) {
         const std::string hd = dir + "/h_" + std::to_string(h);
         DIR* d = opendir(hd.c_str());
@@ -317,6 +327,8 @@ int read_cloud(const std::string& dir, uint32_t hierarchies, std::vector<CellFil
             int x, y, z;
             char tail[8] = {0};
             if (sscanf(nm.c_str(), "c_%d_%d_%d.%3s", &x, &y, &z, tail) != 4 || strcmp(tail, "bin") != 0) continue;
+            if (subtrees && !std::binary_search(keep.begin(), keep.end(), std::array<int32_t, 3>{x >> h, y >> h, z >> h}))
+                continue;
             CellFile c;
             if (!read_cell_file(hd + "/" + nm, c, err)) return -EINVAL;
             if (c.h != h || c.idx[0] != x || c.idx[1] != y || c.idx[2] != z) {

@@ -51,7 +51,9 @@ struct CellFile {
 bool read_cell_file(const std::string& path, CellFile& out, std::string& err);
 // Every h_{h}/c_{x}_{y}_{z}.bin with h < hierarchies (the layout own.rs:16-62 and
 // converter.rs:187-207 read; the order of the returned cells is unspecified).
-int read_cloud(const std::string& dir, uint32_t hierarchies, std::vector<CellFile>& cells, std::string& err);
+// subtrees (optional): level-0 cell triples; only cells below them are read
+int read_cloud(const std::string& dir, uint32_t hierarchies, std::vector<CellFile>& cells, std::string& err,
+               const std::vector<int32_t>* subtrees = nullptr);
 // The existing cloud as the engine's merge state (engine.h PriorState).
 int prior_from_cells(const std::vector<CellFile>& cells, const Config& cfg, PriorState& out, std::string& err);
 

@@ -33,7 +33,8 @@ EXPORTS = ["pcc_abi_version", "pcc_last_error", "pcc_options_default", "pcc_open
            "pcc_finish", "pcc_close", "pcc_get_stats", "pcc_set_profiling", "pcc_get_profile", "pcc_device_input",
            "pcc_convert_files", "pcc_shard_grid_from_bbox", "pcc_synth_device", "pcc_shard_bbox",
            "pcc_shard_histogram", "pcc_shard_route", "pcc_declare_files", "pcc_add_keyed_points_device",
-           "pcc_set_summary", "pcc_write_cells", "pcc_write_metadata", "pcc_clear_input", "pcc_adopt_prior"]
+           "pcc_set_summary", "pcc_write_cells", "pcc_write_metadata", "pcc_clear_input", "pcc_adopt_prior",
+           "pcc_open_subtrees"]
 
 
 class Options(C.Structure):
@@ -91,6 +92,7 @@ def lib():
         L.pcc_last_error.restype = C.c_char_p
         L.pcc_options_default.argtypes = [C.POINTER(Options)]
         L.pcc_open.argtypes = [C.c_char_p, C.POINTER(Options), C.POINTER(vp)]
+        L.pcc_open_subtrees.argtypes = [C.c_char_p, C.POINTER(Options), vp, C.c_uint64, C.POINTER(vp)]
         L.pcc_add_points.argtypes = [vp, vp, C.c_uint64]
         L.pcc_add_points_device.argtypes = [vp, vp, C.c_uint64]
         L.pcc_add_empty_batches.argtypes = [vp, C.c_uint32]
@@ -139,10 +141,17 @@ def default_options(**kw) -> Options:
 class Converter:
     """converter.rs:72-94 Converter, built on the GPU at finish()/build()."""
 
-    def __init__(self, out_dir: str, batch_size: int = 10_000, device: int = 0, config: dict | None = None):
+    def __init__(self, out_dir: str, batch_size: int = 10_000, device: int = 0, config: dict | None = None,
+                 subtrees=None):
+        """`subtrees` (sharded merge, pcc_open_subtrees): level-0 cell triples
+        whose existing cells this converter loads and rewrites."""
         opt = default_options(batch_size=batch_size, device=device, **(config or {}))
         h = C.c_void_p()
-        _check(lib().pcc_open(os.fsencode(out_dir), C.byref(opt), C.byref(h)))
+        if subtrees is None:
+            _check(lib().pcc_open(os.fsencode(out_dir), C.byref(opt), C.byref(h)))
+        else:
+            st = np.ascontiguousarray(np.asarray(subtrees, dtype=np.int32).reshape(-1, 3))
+            _check(lib().pcc_open_subtrees(os.fsencode(out_dir), C.byref(opt), st.ctypes.data, len(st), C.byref(h)))
         self._h = h
         self.out_dir = out_dir
 

@@ -19,6 +19,14 @@ of c).  So the unit of ownership is the level-0 cell, and one step is:
   6. all-reduce(max) of `hierarchies`; every rank writes its own (disjoint) cell
      files, rank 0 writes metadata.json after a barrier.
 
+Incremental merge (config 5, `merge=True`): the output directory holds an
+existing cloud.  After step 3 every rank opens it restricted to the level-0
+subtrees it owns and that receive new points (pcc_open_subtrees: converter.rs:
+187-207 for its own cells only), merges its routed points into them (its seeds
+first, then its new points in global key order) and rewrites those subtrees;
+the other subtrees stay as they are on disk.  The metadata values continue from
+the existing metadata.json (lib.rs:86-101: counters, Aabb::extend_aabb).
+
 The collectives go through a small communicator interface: `TorchComm`
 (torch.distributed; backend "nccl" is RCCL on ROCm, "gloo" for the CPU tests) or
 `ThreadComm` (ranks as threads of one process, used to run the exchange on a
@@ -151,15 +159,39 @@ class HipShardOps:
     """Local per-rank work on the GPU through libpcconv.so (no CPU fallback)."""
 
     def __init__(self, device_index: int, out_dir: str | None = None, batch_size: int = 10_000,
-                 config: dict | None = None):
+                 config: dict | None = None, merge: bool = False):
         self.dev = device_index
         self.cfg = dict(config or {})
         self.max_cell_size = float(self.cfg.get("max_cell_size", 1000.0))
+        self.batch_size = batch_size
+        self.merge = merge
         self._tmp = None
+        self.subtrees = None
+        if merge:   # the converter opens on the existing cloud once the owned subtrees are known
+            if out_dir is None:
+                raise ValueError("a sharded merge needs the directory of the existing cloud")
+            self.out_dir = out_dir
+            self.conv = None
+            return
         if out_dir is None:
             self._tmp = tempfile.TemporaryDirectory(prefix="pcc_shard_")
             out_dir = self._tmp.name
+        self.out_dir = out_dir
         self.conv = pcconv.Converter(out_dir, batch_size=batch_size, device=device_index, config=self.cfg)
+
+    def prior_meta(self) -> dict:
+        return read_prior_meta(self.out_dir)
+
+    def set_subtrees(self, cells: np.ndarray):
+        """Merge mode: (re)open the existing cloud restricted to these level-0 cells."""
+        cells = np.asarray(cells, dtype=np.int32).reshape(-1, 3)
+        if self.conv is not None and self.subtrees is not None and np.array_equal(cells, self.subtrees):
+            return
+        if self.conv is not None:
+            self.conv.close()
+        self.conv = pcconv.Converter(self.out_dir, batch_size=self.batch_size, device=self.dev, config=self.cfg,
+                                     subtrees=cells)
+        self.subtrees = cells
 
     def _ready(self):
         # inputs may come from torch kernels or RCCL on torch's streams; the
@@ -205,7 +237,8 @@ class HipShardOps:
             c.write_metadata()
 
     def close(self):
-        self.conv.close()
+        if self.conv is not None:
+            self.conv.close()
         if self._tmp is not None:
             self._tmp.cleanup()
 
@@ -220,12 +253,32 @@ class ShardResult:
     ms: dict = field(default_factory=dict)
 
 
+def read_prior_meta(out_dir: str) -> dict:
+    """metadata.json of an existing cloud (lib.rs:86-101 load_metadata)."""
+    import json
+    with open(os.path.join(out_dir, "metadata.json")) as f:
+        m = json.load(f)
+    return {"number_of_points": int(m["number_of_points"]), "hierarchies": int(m["hierarchies"]),
+            "bbox_min": [float(v) for v in m["bounding_box"]["min"]],
+            "bbox_max": [float(v) for v in m["bounding_box"]["max"]]}
+
+
+def cell_triples(ids: np.ndarray, grid) -> np.ndarray:
+    """Level-0 cell indices (x, y, z) of linear shard-grid ids ((x*dy + y)*dz + z)."""
+    ids = np.asarray(ids, dtype=np.int64)
+    d1, d2 = int(grid.dims[1]), int(grid.dims[2])
+    out = np.stack([ids // (d1 * d2) + int(grid.lo[0]), (ids // d2) % d1 + int(grid.lo[1]), ids % d2 + int(grid.lo[2])],
+                   axis=1)
+    return out.astype(np.int32).reshape(-1, 3)
+
+
 def shard_build(comm, ops, pts: torch.Tensor, key0: int, file_points, write: bool = False,
-                sync=None) -> ShardResult:
+                sync=None, merge: bool = False) -> ShardResult:
     """One sharded conversion step.  `pts` is this rank's (n, 4) int32 view of
     16-B points with global keys key0 .. key0+n-1 (contiguous ranges in rank
     order).  `file_points` is the GLOBAL file structure.  `sync` (optional)
-    synchronises the device for stage timing."""
+    synchronises the device for stage timing.  `merge`: incremental merge into
+    the existing cloud of the ops' directory (module docstring)."""
     ms = {}
     t0 = time.perf_counter()
 
@@ -253,6 +306,8 @@ def shard_build(comm, ops, pts: torch.Tensor, key0: int, file_points, write: boo
         recv = pts[:0]
         keys = torch.empty(0, dtype=torch.int32, device=pts.device)
         owned = 0
+        if merge:
+            ops.set_subtrees(np.zeros((0, 3), dtype=np.int32))
     else:
         # 3. level-0 ownership
         grid = ops.grid(gmin, gmax)
@@ -262,6 +317,8 @@ def shard_build(comm, ops, pts: torch.Tensor, key0: int, file_points, write: boo
         owner_h = assign_owners(hist_h, comm.world)
         owned = int(np.count_nonzero((owner_h == comm.rank) & (hist_h > 0)))
         owner = torch.from_numpy(owner_h.astype(np.int32)).to(pts.device)
+        if merge:   # the existing cells of the owned subtrees that receive new points
+            ops.set_subtrees(cell_triples(np.flatnonzero((owner_h == comm.rank) & (hist_h > 0)), grid))
         mark("plan")
         # 4. route + exchange (all-to-all-v of points and keys)
         send, skeys, counts = ops.route(pts, key0, grid, owner, comm.world)
@@ -278,6 +335,16 @@ def shard_build(comm, ops, pts: torch.Tensor, key0: int, file_points, write: boo
     comm.allreduce_(hz, "max")
     summary = {"number_of_points": n_total, "hierarchies": int(hz.item()),
                "bbox_min": gmin if n_total else [0.0, 0.0, 0.0], "bbox_max": gmax if n_total else [0.0, 0.0, 0.0]}
+    if merge:   # lib.rs:86-101: counters continue; converter.rs:96-104 Aabb::extend_aabb
+        pm = ops.prior_meta()
+        if pm["number_of_points"] > 0:
+            if n_total:
+                summary["bbox_min"] = [min(a, b) for a, b in zip(gmin, pm["bbox_min"])]
+                summary["bbox_max"] = [max(a, b) for a, b in zip(gmax, pm["bbox_max"])]
+            else:
+                summary["bbox_min"], summary["bbox_max"] = pm["bbox_min"], pm["bbox_max"]
+        summary["number_of_points"] = n_total + pm["number_of_points"]
+        summary["hierarchies"] = max(summary["hierarchies"], pm["hierarchies"])
     mark("summary")
     if write:
         ops.write(summary, cells=True, metadata=False)

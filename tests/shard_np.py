@@ -36,12 +36,36 @@ def cell_index(v: np.ndarray, cs: float) -> np.ndarray:
 
 
 class NumpyShardOps:
-    def __init__(self, out_dir: str, batch_size: int = 10_000, config: dict | None = None):
+    def __init__(self, out_dir: str, batch_size: int = 10_000, config: dict | None = None, merge: bool = False):
         self.out_dir = out_dir
         self.batch = batch_size
         self.cfg = dict(config or {})
         self.max_cell_size = float(self.cfg.get("max_cell_size", 1000.0))
         self.oracle = None
+        self.merge = merge
+        self.subtree_dir = None
+
+    def prior_meta(self):
+        from pcconv.dist import read_prior_meta
+        return read_prior_meta(self.out_dir)
+
+    def set_subtrees(self, cells):
+        """Merge mode: a copy of the existing cloud holding only the cells below
+        these level-0 cells (what pcc_open_subtrees loads), for the oracle's loader."""
+        keep = {tuple(int(v) for v in c) for c in np.asarray(cells).reshape(-1, 3)}
+        if self.subtree_dir is not None:
+            shutil.rmtree(self.subtree_dir, ignore_errors=True)
+        d = self.subtree_dir = tempfile.mkdtemp(prefix="pcc_np_subtrees_")
+        shutil.copy(os.path.join(self.out_dir, "metadata.json"), d)
+        for name in os.listdir(self.out_dir):
+            if not name.startswith("h_"):
+                continue
+            h = int(name[2:])
+            os.makedirs(os.path.join(d, name), exist_ok=True)
+            for fn in os.listdir(os.path.join(self.out_dir, name)):
+                x, y, z = (int(v) for v in fn[2:-4].split("_"))
+                if (x >> h, y >> h, z >> h) in keep:
+                    shutil.copy(os.path.join(self.out_dir, name, fn), os.path.join(d, name, fn))
 
     def bbox(self, pts):
         p = as_points(pts)
@@ -75,6 +99,8 @@ class NumpyShardOps:
         if self.oracle is not None:
             self.oracle.close()
         o = self.oracle = Oracle(self.cfg)
+        if self.merge:
+            o.load(self.subtree_dir)
         g = 0
         for fp in file_points:
             off = 0
@@ -117,3 +143,6 @@ class NumpyShardOps:
         if self.oracle is not None:
             self.oracle.close()
             self.oracle = None
+        if self.subtree_dir is not None:
+            shutil.rmtree(self.subtree_dir, ignore_errors=True)
+            self.subtree_dir = None

@@ -167,3 +167,95 @@ def test_gloo_world2_matches_oracle(tmp_path, case):
     if case == "uniform":
         assert r[0]["owned"] == r[1]["owned"] == 4     # 8 level-0 octants, 4 per rank
     check_against_oracle(tmp_path, files, out, r[0]["summary"])
+
+
+# ------------------------------------------------------------- sharded incremental merge (config 5)
+def make_merge_input(case):
+    """(existing files, new files) for a named merge case."""
+    if case == "uniform":
+        return [synth(21, 0, 80_000)], [synth(22, 0, 30_000)]
+    if case == "partial":   # new points in one octant plus new level-0 cells beyond the old bbox
+        return [synth(23, 0, 60_000)], [synth(24, 0, 20_000, lo=100.0, ext=800.0),
+                                        synth(25, 0, 7_000, lo=-1900.0, ext=800.0)]
+    if case == "clustered":
+        return [synth(26, 1, 50_000)], [synth(27, 1, 40_000)]
+    raise KeyError(case)
+
+
+def _thread_merge(out, new_files, world):
+    import threading
+    fp = [len(f) for f in new_files]
+    grp = ThreadGroup(world)
+    res, errs = [None] * world, []
+
+    def worker(r):
+        try:
+            pts, key0 = rank_slice(new_files, r, world)
+            ops = NumpyShardOps(out, merge=True)
+            res[r] = shard_build(ThreadComm(grp, r, torch.device("cpu")), ops, as_tensor(pts), key0, fp, write=True,
+                                 merge=True)
+            ops.close()
+        except BaseException as e:  # noqa: BLE001
+            errs.append(e)
+            grp.bar.abort()
+
+    th = [threading.Thread(target=worker, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs
+    return res
+
+
+@pytest.mark.parametrize("case,world", [("uniform", 2), ("partial", 3), ("clustered", 4)])
+def test_thread_ranks_merge_matches_oracle(tmp_path, case, world):
+    """Existing cloud (oracle-written) + new points merged by `world` ranks, each
+    rewriting only its subtrees, == the oracle converting old and new files in
+    one run (the reference's incremental-merge semantics, converter.rs:187-207)."""
+    old, new = make_merge_input(case)
+    out = str(tmp_path / "out")
+    err, _ = run_oracle(out, old)
+    assert err == 0
+    res = _thread_merge(out, new, world)
+    assert all(r.summary == res[0].summary for r in res)
+    assert sum(r.recv_points for r in res) == sum(len(f) for f in new)
+    check_against_oracle(tmp_path, old + new, out, res[0].summary)
+
+
+def test_thread_ranks_merge_no_new_points(tmp_path):
+    old, _ = make_merge_input("uniform")
+    out = str(tmp_path / "out")
+    assert run_oracle(out, old)[0] == 0
+    res = _thread_merge(out, [np.zeros(0, dtype=old[0].dtype)], 2)
+    assert res[0].summary["number_of_points"] == len(old[0])
+    check_against_oracle(tmp_path, old + [np.zeros(0, dtype=old[0].dtype)], out, res[0].summary)
+
+
+def _gloo_merge_worker(rank, world, port, case, out, res_dir):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        _, new = make_merge_input(case)
+        pts, key0 = rank_slice(new, rank, world)
+        ops = NumpyShardOps(out, merge=True)
+        r = shard_build(TorchComm(torch.device("cpu")), ops, as_tensor(pts), key0, [len(f) for f in new],
+                        write=True, merge=True)
+        ops.close()
+        with open(os.path.join(res_dir, f"rank{rank}.json"), "w") as f:
+            json.dump({"summary": r.summary, "recv": r.recv_points}, f)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_merge_matches_oracle(tmp_path):
+    import torch.multiprocessing as mp
+    old, new = make_merge_input("partial")
+    out, rd = str(tmp_path / "out"), str(tmp_path / "res")
+    os.makedirs(rd)
+    assert run_oracle(out, old)[0] == 0
+    mp.spawn(_gloo_merge_worker, args=(2, _free_port(), "partial", out, rd), nprocs=2, join=True)
+    r = [json.load(open(os.path.join(rd, f"rank{i}.json"))) for i in range(2)]
+    assert r[0]["summary"] == r[1]["summary"]
+    check_against_oracle(tmp_path, old + new, out, r[0]["summary"])

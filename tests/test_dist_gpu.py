@@ -19,7 +19,8 @@ sys.path.insert(0, os.path.join(HERE, "..", "point-cloud_amd"))
 import pcconv  # noqa: E402
 from pcconv.dist import HipShardOps, ThreadComm, ThreadGroup, key_range, shard_build  # noqa: E402
 from shard_np import NumpyShardOps, as_points, as_tensor  # noqa: E402
-from test_dist_cpu import check_against_oracle, make_input, rank_slice  # noqa: E402
+from test_dist_cpu import check_against_oracle, make_input, make_merge_input, rank_slice  # noqa: E402
+from gpu_util import run_oracle  # noqa: E402
 from oracle_ctypes import synth  # noqa: E402
 from gpu_util import compare_dirs, run_gpu  # noqa: E402
 
@@ -78,7 +79,7 @@ def test_synth_device_matches_oracle_stream():
     assert (as_points(p.cpu()).view(np.uint8) == synth(9, 1, 77_777, first=123_456).view(np.uint8)).all()
 
 
-def _run_threads(files, world, out, cfg=None, batch=10_000):
+def _run_threads(files, world, out, cfg=None, batch=10_000, merge=False):
     fp = [len(f) for f in files]
     grp = ThreadGroup(world)
     res, errs = [None] * world, []
@@ -87,9 +88,9 @@ def _run_threads(files, world, out, cfg=None, batch=10_000):
         try:
             torch.cuda.set_device(DEV)
             pts, key0 = rank_slice(files, r, world)
-            ops = HipShardOps(0, out_dir=out, batch_size=batch, config=cfg)
+            ops = HipShardOps(0, out_dir=out, batch_size=batch, config=cfg, merge=merge)
             t = as_tensor(pts).to(DEV)
-            res[r] = shard_build(ThreadComm(grp, r, DEV), ops, t, key0, fp, write=True)
+            res[r] = shard_build(ThreadComm(grp, r, DEV), ops, t, key0, fp, write=True, merge=merge)
             ops.close()
         except BaseException as e:  # noqa: BLE001
             errs.append(e)
@@ -131,3 +132,28 @@ def test_sharded_small_limit_deep(tmp_path):
     out = str(tmp_path / "out")
     res = _run_threads(files, 3, out, cfg=cfg, batch=777)
     check_against_oracle(tmp_path, files, out, res[0].summary, cfg=cfg, batch=777)
+
+
+@pytest.mark.parametrize("case,world", [("uniform", 2), ("partial", 3), ("clustered", 4)])
+def test_sharded_merge_threads_match_oracle(tmp_path, case, world):
+    """Config 5 sharded: every rank opens the existing cloud for
+    its own subtrees (pcc_open_subtrees), merges its routed points on the GPU and
+    rewrites them == the oracle converting old and new files in one run."""
+    old, new = make_merge_input(case)
+    out = str(tmp_path / "out")
+    assert run_oracle(out, old)[0] == 0
+    res = _run_threads(new, world, out, merge=True)
+    assert sum(r.recv_points for r in res) == sum(len(f) for f in new)
+    check_against_oracle(tmp_path, old + new, out, res[0].summary)
+
+
+def test_sharded_merge_into_gpu_built_cloud_multilevel(tmp_path):
+    """A GPU-built 1.5M cloud (several levels, spilled buckets) + 500k new points
+    merged by 2 ranks."""
+    cfg = dict(sub_grid_dimension=32, cell_point_overflow_limit=500)
+    old, new = [synth(33, 1, 1_500_000)], [synth(34, 1, 500_000)]
+    out = str(tmp_path / "out")
+    run_gpu(out, old, cfg=cfg)
+    res = _run_threads(new, 2, out, cfg=cfg, merge=True)
+    assert res[0].summary["hierarchies"] >= 3
+    check_against_oracle(tmp_path, old + new, out, res[0].summary, cfg=cfg)
