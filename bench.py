@@ -131,6 +131,11 @@ def main_sharded(args, rank, world):
     from pcconv.dist import HipShardOps, TorchComm, key_range, shard_build
     import pcconv
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # RCCL writes its version banner to fd 1 at communicator creation: route fd 1
+    # to stderr for the run and keep the real stdout for the one JSON line
+    sys.stdout.flush()
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     dist.init_process_group("nccl", device_id=dev)
@@ -173,7 +178,8 @@ def main_sharded(args, rank, world):
                      sum(p[3] for p in per), k, dense_ms, f"level-0 cell sharding over {world} ranks (RCCL all-to-all-v)")
         rec["sharding"] = {"points_per_rank": [p[4] for p in per], "stage_ms_rank0": stage,
                            "hierarchies": res.summary["hierarchies"]}
-        print(json.dumps(rec), flush=True)
+        json_out.write(json.dumps(rec) + "\n")
+        json_out.flush()
     dist.destroy_process_group()
 
 
@@ -181,7 +187,7 @@ def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    if world > 1:
+    if world > 1 or os.environ.get("PCC_BENCH_SHARDED") == "1":   # the env var: sharded path at N=1 (check)
         args.gpus = world
         main_sharded(args, rank, world)
         return

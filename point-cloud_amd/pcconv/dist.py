@@ -69,9 +69,39 @@ class TorchComm:
         self.dist.all_to_all_single(r, s)
         return [int(v) for v in r.tolist()]
 
+    # bytes one all-to-all call moves per rank at most (a single call of 2 GiB or more
+    # of payload returns corrupted data on this stack); larger exchanges run in
+    # rounds, each peer segment split at the same row offsets on both sides
+    chunk_bytes = 1 << 30
+
     def alltoallv(self, send: torch.Tensor, send_counts: list[int], recv_counts: list[int]) -> torch.Tensor:
         out = torch.empty((sum(recv_counts),) + tuple(send.shape[1:]), dtype=send.dtype, device=send.device)
-        self.dist.all_to_all_single(out, send, recv_counts, send_counts)
+        row = send.element_size() * max(1, int(np.prod(send.shape[1:])))
+        mr = max(1, self.chunk_bytes // (row * self.world))   # rows per peer per round
+        local = max([-(-int(c) // mr) for c in list(send_counts) + list(recv_counts)] + [1])
+        r = torch.tensor([local], dtype=torch.int64, device=self.device)
+        self.dist.all_reduce(r, op=self.dist.ReduceOp.MAX)
+        rounds = int(r.item())
+        if rounds == 1:
+            self.dist.all_to_all_single(out, send, recv_counts, send_counts)
+            return out
+        so = np.concatenate([[0], np.cumsum(send_counts)]).astype(np.int64)
+        ro = np.concatenate([[0], np.cumsum(recv_counts)]).astype(np.int64)
+        for k in range(rounds):   # round k: rows [k*mr, (k+1)*mr) of every peer segment
+            ins, outs = [], []
+            for p in range(self.world):
+                a = min(k * mr, int(send_counts[p]))
+                ins.append(send.narrow(0, int(so[p]) + a, min(mr, int(send_counts[p]) - a)))
+                b = min(k * mr, int(recv_counts[p]))
+                outs.append(out.narrow(0, int(ro[p]) + b, min(mr, int(recv_counts[p]) - b)))
+            tmp = torch.empty((sum(int(o.shape[0]) for o in outs),) + tuple(send.shape[1:]), dtype=send.dtype,
+                              device=send.device)
+            self.dist.all_to_all_single(tmp, torch.cat(ins), [int(o.shape[0]) for o in outs],
+                                        [int(i.shape[0]) for i in ins])
+            o = 0
+            for dst in outs:
+                dst.copy_(tmp.narrow(0, o, int(dst.shape[0])))
+                o += int(dst.shape[0])
         return out
 
     def barrier(self):

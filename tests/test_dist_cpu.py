@@ -259,3 +259,33 @@ def test_gloo_world2_merge_matches_oracle(tmp_path):
     r = [json.load(open(os.path.join(rd, f"rank{i}.json"))) for i in range(2)]
     assert r[0]["summary"] == r[1]["summary"]
     check_against_oracle(tmp_path, old + new, out, r[0]["summary"])
+
+
+def _gloo_chunked_worker(rank, world, port, out, res_dir):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        files = make_input("files")
+        pts, key0 = rank_slice(files, rank, world)
+        comm = TorchComm(torch.device("cpu"))
+        comm.chunk_bytes = 1 << 16   # force the all-to-all-v into many rounds
+        ops = NumpyShardOps(out)
+        r = shard_build(comm, ops, as_tensor(pts), key0, [len(f) for f in files], write=True)
+        ops.close()
+        with open(os.path.join(res_dir, f"rank{rank}.json"), "w") as f:
+            json.dump({"summary": r.summary, "recv": r.recv_points}, f)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_chunked_exchange_matches_oracle(tmp_path):
+    """The all-to-all-v split into rounds (TorchComm.chunk_bytes) gives the same exchange."""
+    import torch.multiprocessing as mp
+    out, rd = str(tmp_path / "out"), str(tmp_path / "res")
+    os.makedirs(rd)
+    mp.spawn(_gloo_chunked_worker, args=(2, _free_port(), out, rd), nprocs=2, join=True)
+    r = [json.load(open(os.path.join(rd, f"rank{i}.json"))) for i in range(2)]
+    files = make_input("files")
+    assert r[0]["recv"] + r[1]["recv"] == sum(len(f) for f in files)
+    check_against_oracle(tmp_path, files, out, r[0]["summary"])
