@@ -12,6 +12,7 @@
 #include <fstream>
 #include <memory>
 #include <sstream>
+#include <thread>
 #include <string>
 
 #include "../../include/pcconv.h"
@@ -227,13 +228,52 @@ static int write_impl(pcc_converter* c, bool with_metadata) {
         if (rc) return rc;
     }
     GUARD_BEGIN
-    std::vector<LevelHost> levels;
-    std::vector<Point> grid, kept;
-    int rc = c->eng->download(levels, grid, kept);
-    if (rc) return set_err(rc, c->eng->last_error());
+    // Async output writer: level i's cell files are
+    // written by a pool of host threads while level i+1 is compacted and copied
+    // off the device.
     std::string err;
-    rc = write_output(c->out_dir, c->meta, levels, grid, kept, err, with_metadata);
+    int rc = make_output_dirs(c->out_dir, c->meta.hierarchies, err);
     if (rc) return set_err(rc, err);
+    struct Slot { LevelHost H; HostPoints grid, kept; };
+    Slot slot[2];
+    int wrc = 0;
+    std::string werr;
+    const unsigned nt = writer_threads();
+    std::thread writer;   // declared after everything it touches, joined before they go
+    struct Join {         // a HIP error thrown below must not leave the writer joinable
+        std::thread& t;
+        ~Join() { if (t.joinable()) t.join(); }
+    } join_writer{writer};
+    const bool verbose = getenv("PCC_VERBOSE") != nullptr;
+    using clk = std::chrono::steady_clock;
+    auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    double wms[2] = {0, 0};
+    for (uint32_t i = 0; i < c->eng->num_levels(); i++) {
+        Slot& S = slot[i & 1];   // the writer of level i-1 holds the other slot
+        const auto t0 = clk::now();
+        rc = c->eng->download_level(i, S.H, S.grid, S.kept);
+        if (rc) break;
+        const auto t1 = clk::now();
+        if (writer.joinable()) writer.join();
+        if (wrc) break;
+        if (verbose)
+            fprintf(stderr, "[pcc] write: level %u download %.1f ms (%zu grid + %zu kept points), waited %.1f ms for level %u's files\n",
+                    i, ms(t0, t1), S.grid.size(), S.kept.size(), ms(t1, clk::now()), i ? i - 1 : 0);
+        writer = std::thread([&, sp = &S, slot_i = i & 1] {
+            const auto w0 = clk::now();
+            wrc = write_level_cells(c->out_dir, c->meta.config, sp->H, sp->grid.data(), sp->kept.data(), nt, werr);
+            wms[slot_i] = ms(w0, clk::now());
+        });
+    }
+    const auto tj = clk::now();
+    if (writer.joinable()) writer.join();
+    if (verbose) fprintf(stderr, "[pcc] write: last level's files %.1f ms after the last download\n", ms(tj, clk::now()));
+    if (rc) return set_err(rc, c->eng->last_error());
+    if (wrc) return set_err(wrc, werr);
+    if (with_metadata) {
+        rc = write_metadata(c->out_dir, c->meta, err);
+        if (rc) return set_err(rc, err);
+    }
     return 0;
     GUARD_END
 }

@@ -37,6 +37,22 @@ struct LevelHost {
     uint64_t kept_base = 0;             // offset of this level's kept lists in the downloaded kept array
 };
 
+// Host staging for downloaded points: uninitialised (no zero fill) and advised
+// for transparent huge pages, grown only, so a level's D2H is not paced by
+// first-touch page faults.
+struct HostPoints {
+    Point* p = nullptr;
+    uint64_t n = 0, cap = 0;
+    HostPoints() = default;
+    HostPoints(const HostPoints&) = delete;
+    HostPoints& operator=(const HostPoints&) = delete;
+    ~HostPoints();
+    void resize(uint64_t m);
+    Point* data() { return p; }
+    const Point* data() const { return p; }
+    uint64_t size() const { return n; }
+};
+
 // Existing cloud loaded for an incremental merge (lib.rs:86-101 +
 // converter.rs:187-207).  Seeds are ALL its points in
 // key order: per level h, first the grid points of every level-h cell, then the
@@ -102,6 +118,9 @@ public:
     // (message in last_error()).  Input must already be resident.
     int build();
     int download(std::vector<LevelHost>& levels, std::vector<Point>& grid, std::vector<Point>& kept);
+    // one level (grid winners compacted on the device); H's bases are 0
+    int download_level(uint32_t i, LevelHost& H, HostPoints& grid, HostPoints& kept);
+    uint32_t num_levels() const;
 
     uint64_t num_points() const { return n_; }
     uint32_t num_batches() const { return nbatches_; }

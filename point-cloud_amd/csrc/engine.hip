@@ -30,6 +30,8 @@
 //   * keys (input indices) are unique at every level; event batches are
 //     monotone in key inside every cell.
 #include "engine.h"
+
+#include <sys/mman.h>
 #include <cerrno>
 #include <memory>
 
@@ -122,6 +124,9 @@ struct Engine::Dev {
         return r;
     }
     void reset_pool() { chunk_i = 0; chunk_used = 0; }
+    // scratch taken after a build (downloads) is returned with release(mark())
+    uint64_t mark() const { return ((uint64_t)chunk_i << 40) | chunk_used; }
+    void release(uint64_t m) { chunk_i = (size_t)(m >> 40); chunk_used = m & ((1ull << 40) - 1); }
 };
 
 struct Engine::Level {
@@ -3096,36 +3101,93 @@ int Engine::run_level(uint32_t h) {
     return 0;
 }
 
+// Grid winners of one level compacted on the device (slab s's n_s winners from
+// its capacity-sized region to cgo[s] = sum of the earlier slabs' winners), so
+// the D2H moves the winners only (about a third of the regions at config 4).
+__global__ __launch_bounds__(256) void k_compact_grid(const Point* __restrict__ grid, const uint32_t* __restrict__ off,
+                                                      const uint32_t* __restrict__ n, const uint32_t* __restrict__ cgo,
+                                                      uint32_t nslabs, Point* __restrict__ dst) {
+    for (uint32_t s = blockIdx.x; s < nslabs; s += gridDim.x) {
+        const float4* src = reinterpret_cast<const float4*>(grid) + off[s];
+        float4* d = reinterpret_cast<float4*>(dst) + cgo[s];
+        for (uint32_t i = threadIdx.x; i < n[s]; i += 256) d[i] = src[i];
+    }
+}
+
+uint32_t Engine::num_levels() const { return (uint32_t)levels_.size(); }
+
+HostPoints::~HostPoints() {
+    if (p) munmap(p, cap * sizeof(Point));
+}
+void HostPoints::resize(uint64_t m) {
+    if (m > cap) {
+        if (p) munmap(p, cap * sizeof(Point));
+        const uint64_t c = std::max<uint64_t>(m, 1);
+        void* q = mmap(nullptr, c * sizeof(Point), PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+        if (q == MAP_FAILED) throw std::bad_alloc();
+        madvise(q, c * sizeof(Point), MADV_HUGEPAGE);
+        p = static_cast<Point*>(q);
+        cap = c;
+    }
+    n = m;
+}
+
+int Engine::download_level(uint32_t i, LevelHost& H, HostPoints& grid, HostPoints& kept) {
+    if (i >= levels_.size()) return -EINVAL;
+    Level* L = levels_[i];
+    H = LevelHost();
+    H.h = L->h;
+    auto cp = [&](auto& vec, auto* dptr, uint64_t n) {
+        vec.resize(n);
+        if (n) HIP_CHECK(hipMemcpyAsync(vec.data(), dptr, n * sizeof(vec[0]), hipMemcpyDeviceToHost, stream_));
+    };
+    cp(H.cell_idx, L->cell_idx, 3ull * L->ncells);
+    cp(H.cell_slab0, L->cell_slab0, L->ncells + 1ull);
+    cp(H.slab_grid_n, L->slab_grid_n, L->nslabs);
+    cp(H.bkt_state, L->bkt_state, 8ull * L->ncells);
+    cp(H.bkt_off, L->bkt_off, 8ull * L->ncells);
+    cp(H.bkt_n, L->bkt_n, 8ull * L->ncells);
+    // compacted winners
+    const uint64_t mark = dev_->mark();
+    uint32_t* cgo = static_cast<uint32_t*>(dev_->get(((uint64_t)L->nslabs + 1) * 4));
+    uint32_t* tot = static_cast<uint32_t*>(dev_->get(4));
+    uint32_t nwin = 0;
+    if (L->nslabs) {
+        scan_excl_u32(L->slab_grid_n, cgo, L->nslabs, tot, dev_->scan, stream_);
+        HIP_CHECK(hipMemcpyAsync(&nwin, tot, 4, hipMemcpyDeviceToHost, stream_));
+        HIP_CHECK(hipStreamSynchronize(stream_));
+    }
+    cp(H.slab_grid_off, cgo, L->nslabs);
+    grid.resize(nwin);
+    if (nwin) {
+        Point* d = static_cast<Point*>(dev_->get((uint64_t)nwin * sizeof(Point)));
+        k_compact_grid<<<std::min<uint32_t>(L->nslabs, 65536), 256, 0, stream_>>>(L->grid, L->grid_off, L->slab_grid_n,
+                                                                                cgo, L->nslabs, d);
+        HIP_CHECK(hipGetLastError());
+        HIP_CHECK(hipMemcpyAsync(grid.data(), d, (uint64_t)nwin * sizeof(Point), hipMemcpyDeviceToHost, stream_));
+    }
+    kept.resize(L->kept_used);
+    if (L->kept_used) HIP_CHECK(hipMemcpyAsync(kept.data(), L->kept, (uint64_t)L->kept_used * sizeof(Point), hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    dev_->release(mark);
+    H.grid_base = 0;
+    H.kept_base = 0;
+    return 0;
+}
+
 int Engine::download(std::vector<LevelHost>& out, std::vector<Point>& grid, std::vector<Point>& kept) {
     out.clear();
     grid.clear();
     kept.clear();
-    uint64_t gsz = 0, ksz = 0;
-    for (Level* L : levels_) { gsz += L->arrivals; ksz += L->kept_used; }
-    grid.resize(gsz);
-    kept.resize(ksz);
-    uint64_t go = 0, ko = 0;
-    for (Level* L : levels_) {
+    HostPoints g, k;
+    for (uint32_t i = 0; i < levels_.size(); i++) {
         LevelHost H;
-        H.h = L->h;
-        auto cp = [&](auto& vec, auto* dptr, uint64_t n) {
-            vec.resize(n);
-            if (n) HIP_CHECK(hipMemcpyAsync(vec.data(), dptr, n * sizeof(vec[0]), hipMemcpyDeviceToHost, stream_));
-        };
-        cp(H.cell_idx, L->cell_idx, 3ull * L->ncells);
-        cp(H.cell_slab0, L->cell_slab0, L->ncells + 1ull);
-        cp(H.slab_grid_off, L->grid_off, L->nslabs);
-        cp(H.slab_grid_n, L->slab_grid_n, L->nslabs);
-        cp(H.bkt_state, L->bkt_state, 8ull * L->ncells);
-        cp(H.bkt_off, L->bkt_off, 8ull * L->ncells);
-        cp(H.bkt_n, L->bkt_n, 8ull * L->ncells);
-        if (L->arrivals) HIP_CHECK(hipMemcpyAsync(grid.data() + go, L->grid, L->arrivals * sizeof(Point), hipMemcpyDeviceToHost, stream_));
-        if (L->kept_used) HIP_CHECK(hipMemcpyAsync(kept.data() + ko, L->kept, (uint64_t)L->kept_used * sizeof(Point), hipMemcpyDeviceToHost, stream_));
-        HIP_CHECK(hipStreamSynchronize(stream_));
-        H.grid_base = go;
-        H.kept_base = ko;
-        go += L->arrivals;
-        ko += L->kept_used;
+        const int rc = download_level(i, H, g, k);
+        if (rc) return rc;
+        H.grid_base = grid.size();
+        H.kept_base = kept.size();
+        grid.insert(grid.end(), g.data(), g.data() + g.size());
+        kept.insert(kept.end(), k.data(), k.data() + k.size());
         out.push_back(std::move(H));
     }
     return 0;

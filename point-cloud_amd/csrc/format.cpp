@@ -1,18 +1,21 @@
 // format.cpp — cell / metadata writers and the PLY reader (see format.h).
-#include <array>
 #include "format.h"
 
 #include <dirent.h>
 #include <sys/stat.h>
 
 #include <algorithm>
+#include <array>
+#include <atomic>
 #include <cerrno>
 #include <charconv>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <fstream>
+#include <mutex>
 #include <sstream>
+#include <thread>
 
 #include "pcc_math.h"
 
@@ -189,21 +192,31 @@ bool parse_metadata_json(const std::string& text, Metadata& m, std::string& err)
 static void put32(std::string& b, uint32_t v) { b.append(reinterpret_cast<const char*>(&v), 4); }
 static void putf(std::string& b, float v) { b.append(reinterpret_cast<const char*>(&v), 4); }
 
-int write_output(const std::string& dir, const Metadata& meta, const std::vector<LevelHost>& levels,
-                 const std::vector<Point>& grid, const std::vector<Point>& kept, std::string& err, bool with_metadata) {
+int make_output_dirs(const std::string& dir, uint32_t hierarchies, std::string& err) {
     if (mkdir(dir.c_str(), 0755) != 0 && errno != EEXIST) { err = "cannot create " + dir; return -errno; }
-    for (uint32_t h = 0; h < meta.hierarchies; h++) {   // converter.rs:141-158
+    for (uint32_t h = 0; h < hierarchies; h++) {   // converter.rs:141-158
         std::string hd = dir + "/h_" + std::to_string(h);
         if (mkdir(hd.c_str(), 0755) != 0 && errno != EEXIST) { err = "cannot create " + hd; return -errno; }
     }
-    const Config& cfg = meta.config;
-    std::string buf;
-    for (const LevelHost& L : levels) {
-        const uint32_t h = L.h;
-        const float size = cell_size(cfg.max_cell_size, h);                 // converter.rs:197-199
-        const float sub = sub_cell_size(size, cfg.sub_grid_dimension);
-        const uint32_t ncells = (uint32_t)(L.cell_idx.size() / 3);
-        for (uint32_t c = 0; c < ncells; c++) {
+    return 0;
+}
+
+// Cell files of one level (Cell::write_to cell.rs:155-181, Header::write_to
+// :280-298), cells split over `nthreads` host threads (files are independent).
+int write_level_cells(const std::string& dir, const Config& cfg, const LevelHost& L, const Point* grid,
+                      const Point* kept, unsigned nthreads, std::string& err) {
+    const uint32_t h = L.h;
+    const float size = cell_size(cfg.max_cell_size, h);                 // converter.rs:197-199
+    const float sub = sub_cell_size(size, cfg.sub_grid_dimension);
+    const uint32_t ncells = (uint32_t)(L.cell_idx.size() / 3);
+    std::atomic<uint32_t> next{0};
+    std::atomic<int> rc{0};
+    std::mutex emu;
+    auto work = [&]() {
+        std::string buf;
+        for (;;) {
+            const uint32_t c = next.fetch_add(1);
+            if (c >= ncells || rc.load() != 0) return;
             const int32_t ix = L.cell_idx[3 * c], iy = L.cell_idx[3 * c + 1], iz = L.cell_idx[3 * c + 2];
             uint32_t number = 0, overflow = 0, nb = 0;
             for (uint32_t s = L.cell_slab0[c]; s < L.cell_slab0[c + 1]; s++) number += L.slab_grid_n[s];
@@ -214,7 +227,6 @@ int write_output(const std::string& dir, const Metadata& meta, const std::vector
             }
             buf.clear();
             buf.reserve(48 + 16ull * (number + overflow) + 1 + 16 * nb);
-            // Header::write_to cell.rs:280-298
             put32(buf, h);
             put32(buf, (uint32_t)ix); put32(buf, (uint32_t)iy); put32(buf, (uint32_t)iz);
             put32(buf, number + overflow);
@@ -225,7 +237,7 @@ int write_output(const std::string& dir, const Metadata& meta, const std::vector
             putf(buf, cell_pos1(ix, size)); putf(buf, cell_pos1(iy, size)); putf(buf, cell_pos1(iz, size));
             // grid points (cell.rs:158-160; order free)
             for (uint32_t s = L.cell_slab0[c]; s < L.cell_slab0[c + 1]; s++)
-                buf.append(reinterpret_cast<const char*>(grid.data() + L.grid_base + L.slab_grid_off[s]), 16ull * L.slab_grid_n[s]);
+                buf.append(reinterpret_cast<const char*>(grid + L.grid_base + L.slab_grid_off[s]), 16ull * L.slab_grid_n[s]);
             buf.push_back((char)(uint8_t)nb);   // cell.rs:162
             for (int o = 0; o < 8; o++) {
                 const uint32_t st = L.bkt_state[8 * c + o];
@@ -235,7 +247,7 @@ int write_output(const std::string& dir, const Metadata& meta, const std::vector
                 put32(buf, (uint32_t)(2 * iz + ((o >> 2) & 1)));
                 if (st == 1) {
                     put32(buf, L.bkt_n[8 * c + o]);
-                    buf.append(reinterpret_cast<const char*>(kept.data() + L.kept_base + L.bkt_off[8 * c + o]), 16ull * L.bkt_n[8 * c + o]);
+                    buf.append(reinterpret_cast<const char*>(kept + L.kept_base + L.bkt_off[8 * c + o]), 16ull * L.bkt_n[8 * c + o]);
                 } else {
                     put32(buf, 0);
                 }
@@ -244,10 +256,39 @@ int write_output(const std::string& dir, const Metadata& meta, const std::vector
             snprintf(name, sizeof name, "/h_%u/c_%d_%d_%d.bin", h, ix, iy, iz);
             const std::string path = dir + name;
             FILE* f = fopen(path.c_str(), "wb");
-            if (!f) { err = "cannot write " + path; return -errno; }
-            const bool ok = fwrite(buf.data(), 1, buf.size(), f) == buf.size();
-            if (fclose(f) != 0 || !ok) { err = "write failed: " + path; return -EIO; }
+            bool ok = f != nullptr;
+            if (ok) {
+                ok = fwrite(buf.data(), 1, buf.size(), f) == buf.size();
+                ok = (fclose(f) == 0) && ok;
+            }
+            if (!ok) {
+                std::lock_guard<std::mutex> g(emu);
+                if (rc.load() == 0) { err = "cannot write " + path; rc.store(-EIO); }
+                return;
+            }
         }
+    };
+    const unsigned nt = std::max(1u, std::min<unsigned>(nthreads, ncells));
+    std::vector<std::thread> th;
+    for (unsigned t = 1; t < nt; t++) th.emplace_back(work);
+    work();
+    for (auto& t : th) t.join();
+    return rc.load();
+}
+
+unsigned writer_threads() {
+    const char* e = getenv("PCC_WRITE_THREADS");
+    if (e && atoi(e) > 0) return (unsigned)atoi(e);
+    return std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+}
+
+int write_output(const std::string& dir, const Metadata& meta, const std::vector<LevelHost>& levels,
+                 const std::vector<Point>& grid, const std::vector<Point>& kept, std::string& err, bool with_metadata) {
+    int rc = make_output_dirs(dir, meta.hierarchies, err);
+    if (rc) return rc;
+    for (const LevelHost& L : levels) {
+        rc = write_level_cells(dir, meta.config, L, grid.data(), kept.data(), writer_threads(), err);
+        if (rc) return rc;
     }
     return with_metadata ? write_metadata(dir, meta, err) : 0;
 }

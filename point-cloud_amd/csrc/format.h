@@ -28,6 +28,11 @@ bool parse_metadata_json(const std::string& text, Metadata& m, std::string& err)
 // (converter.rs:218-238 order: cells first, metadata last).
 // with_metadata=false writes the cells only (sharded build: rank 0 writes the
 // global metadata.json once all ranks' cells are on disk).
+int make_output_dirs(const std::string& dir, uint32_t hierarchies, std::string& err);
+// Cell files of one level, split over nthreads host threads.
+int write_level_cells(const std::string& dir, const Config& cfg, const LevelHost& L, const Point* grid,
+                      const Point* kept, unsigned nthreads, std::string& err);
+unsigned writer_threads();   // PCC_WRITE_THREADS, else min(16, hardware threads)
 int write_output(const std::string& dir, const Metadata& meta, const std::vector<LevelHost>& levels,
                  const std::vector<Point>& grid, const std::vector<Point>& kept, std::string& err,
                  bool with_metadata = true);
