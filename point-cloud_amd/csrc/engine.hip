@@ -227,6 +227,7 @@ __device__ __forceinline__ int route(float csc, float crc, int32_t cx, int32_t c
 // host with the reference's own f32 formulas; see pcc_math.h).
 struct LevelGeo {
     float cr, crx, cry, inv_cr;          // hex radius, cr*S3, (-cr)*S3 (hex.rs:69-70), 1/cr
+    float inv_crx, inv_cry;              // RN(1/crx), RN(1/cry)
     float csc, inv_csc, crc, inv_crc;    // child level cell size / hex radius
     float csg, inv_csg, crg, inv_crg;    // grandchild level
 };
@@ -252,9 +253,20 @@ __device__ __forceinline__ float trunc_q(float a, float inv_b, bool& amb) {
     amb |= truncf(q - m) != truncf(q + m);
     return truncf(q);
 }
+// a / b correctly rounded from y = RN(1/b): q0 = RN(a*y) is within an ulp of
+// a/b, the residual a - b*q0 is exact with an FMA, and RN(q0 + r*y) = RN(a/b)
+// (Markstein).  Operands far from 1 (possible over/underflow of the
+// intermediates) flag the lane for the IEEE path.
+__device__ __forceinline__ float div_rc(float a, float b, float y, bool& amb) {
+    const float aa = fabsf(a);
+    amb |= !(aa <= 0x1p90f && (aa >= 0x1p-90f || aa == 0.0f));
+    const float q0 = a * y;
+    const float r = fmaf(-b, q0, a);
+    return fmaf(r, y, q0);
+}
 __device__ __forceinline__ I3 hex_q(float px, float py, float pz, const LevelGeo& G, bool& amb) {
-    const float x = px / G.crx;
-    const float y = py / G.cry;
+    const float x = div_rc(px, G.crx, G.inv_crx, amb);
+    const float y = div_rc(py, G.cry, G.inv_cry, amb);
     const float t = (kSqrt3 * y) + 1.0f;
     const float t1 = floorf(t + x);
     const float t2 = t - x;
@@ -2896,6 +2908,8 @@ int Engine::run_level(uint32_t h) {
         G.cr = hex_radius(sub_cell_size(cs, dim));
         G.crx = G.cr * kSqrt3;
         G.cry = (-G.cr) * kSqrt3;
+        G.inv_crx = 1.0f / G.crx;
+        G.inv_cry = 1.0f / G.cry;
         G.inv_cr = 1.0f / G.cr;
         G.csc = csc;
         G.inv_csc = 1.0f / csc;
