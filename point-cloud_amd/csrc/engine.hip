@@ -230,6 +230,7 @@ struct LevelGeo {
     float inv_crx, inv_cry;              // RN(1/crx), RN(1/cry)
     float csc, inv_csc, crc, inv_crc;    // child level cell size / hex radius
     float csg, inv_csg, crg, inv_crg;    // grandchild level
+    int32_t exact;                       // a divisor outside [2^-60, 2^60]: IEEE divisions only
 };
 
 // floorf(fl(a / b)) and truncf(fl(a / b)) without a full division in the common
@@ -240,40 +241,51 @@ struct LevelGeo {
 // Same quotients with the ambiguity test only accumulated: callers OR the flags
 // of all their divisions and resolve flagged lanes with exact IEEE divisions
 // behind ONE wave-uniform branch (one ballot per point instead of one per
-// division).
+// division).  (k_dcap; the slab kernels use the exact quotients of div_rc.)
+// An integer lies within m = |q| 2^-20 + 2^-126 of q: fract(q + m) <= 2m, tested
+// against 3m to absorb the rounding of q + m (conservative; any |q| >= 2^23 is
+// flagged).
+__device__ __forceinline__ bool near_int(float q) {
+    const float m = fmaf(fabsf(q), 0x1p-20f, 0x1p-126f);
+    const float m3 = fmaf(fabsf(q), 0x3p-20f, 0x3p-126f);
+    return __builtin_amdgcn_fractf(q + m) <= m3;
+}
 __device__ __forceinline__ float floor_q(float a, float inv_b, bool& amb) {
     const float q = a * inv_b;
-    const float m = (fabsf(q) * 0x1p-20f) + 0x1p-126f;
-    amb |= floorf(q - m) != floorf(q + m);
+    amb |= near_int(q);
     return floorf(q);
 }
 __device__ __forceinline__ float trunc_q(float a, float inv_b, bool& amb) {
     const float q = a * inv_b;
-    const float m = (fabsf(q) * 0x1p-20f) + 0x1p-126f;
-    amb |= truncf(q - m) != truncf(q + m);
+    amb |= near_int(q);
     return truncf(q);
 }
 // a / b correctly rounded from y = RN(1/b): q0 = RN(a*y) is within an ulp of
 // a/b, the residual a - b*q0 is exact with an FMA, and RN(q0 + r*y) = RN(a/b)
-// (Markstein).  Operands far from 1 (possible over/underflow of the
-// intermediates) flag the lane for the IEEE path.
-__device__ __forceinline__ float div_rc(float a, float b, float y, bool& amb) {
-    const float aa = fabsf(a);
-    amb |= !(aa <= 0x1p90f && (aa >= 0x1p-90f || aa == 0.0f));
+// (Markstein; tests/div_rc_check.c compares it with IEEE division).  Valid
+// without over/underflow of the intermediates: the callers keep the operands
+// in {0} U [2^-60, 2^60] and the divisors in [2^-60, 2^60] (rc_ok, G.exact), so
+// every quotient is normal or zero.
+__device__ __forceinline__ float div_rc(float a, float b, float y) {
     const float q0 = a * y;
     const float r = fmaf(-b, q0, a);
     return fmaf(r, y, q0);
 }
-__device__ __forceinline__ I3 hex_q(float px, float py, float pz, const LevelGeo& G, bool& amb) {
-    const float x = div_rc(px, G.crx, G.inv_crx, amb);
-    const float y = div_rc(py, G.cry, G.inv_cry, amb);
+__device__ __forceinline__ bool rc_ok(float a) {   // 0, or |a| in [2^-60, 2^60]
+    return fabsf(a) <= 0x1p60f && (uint32_t)(__builtin_amdgcn_frexp_expf(a) + 58) <= 118u;
+}
+// hex.rs:67-85 with the exact quotients; the sums t1 + t3 and t1 + t2 are 0 or
+// at least 2^-24 in magnitude for coordinates in range, so /3 stays normal.
+__device__ __forceinline__ I3 hex_q(float px, float py, float pz, const LevelGeo& G) {
+    const float x = div_rc(px, G.crx, G.inv_crx);
+    const float y = div_rc(py, G.cry, G.inv_cry);
     const float t = (kSqrt3 * y) + 1.0f;
     const float t1 = floorf(t + x);
     const float t2 = t - x;
     const float t3 = (2.0f * x) + 1.0f;
-    const int32_t q = sat_i32(floor_q(t1 + t3, 0x1.555556p-2f, amb));
-    const int32_t r = (int32_t)(0u - (uint32_t)sat_i32(floor_q(t1 + t2, 0x1.555556p-2f, amb)));
-    const int32_t h = sat_i32(trunc_q(pz, G.inv_cr, amb));
+    const int32_t q = sat_i32(floorf(div_rc(t1 + t3, 3.0f, 0x1.555556p-2f)));
+    const int32_t r = (int32_t)(0u - (uint32_t)sat_i32(floorf(div_rc(t1 + t2, 3.0f, 0x1.555556p-2f))));
+    const int32_t h = sat_i32(truncf(div_rc(pz, G.cr, G.inv_cr)));
     I3 o = {q + (r - (r & 1)) / 2, r, h};
     return o;
 }
@@ -315,15 +327,16 @@ __device__ __forceinline__ int route_dest(const RouteIdx& R, int32_t cx, int32_t
 // truncates).  Quotients with |2q| >= 2^30 take the exact path.
 struct SlotRoute { I3 sl; RouteIdx rc, rg; };
 __device__ __forceinline__ SlotRoute slot_route(float x, float y, float z, const LevelGeo& G) {
-    bool amb = false;
+    bool amb = G.exact || !(rc_ok(x) && rc_ok(y) && rc_ok(z));
     SlotRoute S;
-    S.sl = hex_q(x, y, z, G, amb);
-    const float qx = x * G.inv_csg, qy = y * G.inv_csg, qz = z * G.inv_csg, qu = z * G.inv_crg;
+    S.sl = hex_q(x, y, z, G);
+    const float qx = div_rc(x, G.csg, G.inv_csg), qy = div_rc(y, G.csg, G.inv_csg);
+    const float qz = div_rc(z, G.csg, G.inv_csg), qu = div_rc(z, G.crg, G.inv_crg);
     amb |= fmaxf(fmaxf(fabsf(qx), fabsf(qy)), fmaxf(fabsf(qz), fabsf(qu))) >= 0x1p30f;
-    S.rg.ix = sat_i32(floor_q(x, G.inv_csg, amb));
-    S.rg.iy = sat_i32(floor_q(y, G.inv_csg, amb));
-    S.rg.iz = sat_i32(floor_q(z, G.inv_csg, amb));
-    S.rg.u = sat_i32(trunc_q(z, G.inv_crg, amb));
+    S.rg.ix = sat_i32(floorf(qx));
+    S.rg.iy = sat_i32(floorf(qy));
+    S.rg.iz = sat_i32(floorf(qz));
+    S.rg.u = sat_i32(truncf(qu));
     S.rc.ix = S.rg.ix >> 1;
     S.rc.iy = S.rg.iy >> 1;
     S.rc.iz = S.rg.iz >> 1;
@@ -2919,6 +2932,9 @@ int Engine::run_level(uint32_t h) {
         G.inv_csg = 1.0f / csg;
         G.crg = hex_radius(sub_cell_size(csg, dim));
         G.inv_crg = 1.0f / G.crg;
+        G.exact = 0;
+        for (float v : {G.cr, G.crx, G.cry, G.csg, G.crg})   // div_rc's divisor range
+            if (!(std::fabs(v) >= 0x1p-60f && std::fabs(v) <= 0x1p60f)) G.exact = 1;
     }
     SP.tx = g.tx;
     SP.ty = g.ty;
