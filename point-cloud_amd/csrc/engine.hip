@@ -861,7 +861,7 @@ struct DenseLds {
     uint32_t gcnt[kDests * kDests];
     uint32_t doff[kDests], dcap[kDests];
     uint32_t dcur[2][kDests];      // emissions per child slab before chunk c: dcur[c & 1]
-    uint32_t wcnt[NW][kDests];
+    alignas(16) uint32_t wcnt[kDests][NW / 4];   // emissions per child slab and wave, one byte per wave (<= 64)
     uint32_t nwin, err;
 };
 
@@ -1171,8 +1171,8 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
         const int d = vd ? (int)prv.d : 0;
         const uint64_t same = (PCC_ABL & 16) ? __ballot(vd) : wave_peers<5>((uint32_t)d, vd);
         const uint32_t rw = (PCC_ABL & 16) ? 0u : mask_rank(same);
-        if (lane < kDests) S.wcnt[wv][lane] = 0;
-        if (vd && rw == 0) S.wcnt[wv][d] = (uint32_t)__popcll(same);
+        if (lane < kDests) reinterpret_cast<uint8_t*>(S.wcnt[lane])[wv] = 0;
+        if (vd && rw == 0) reinterpret_cast<uint8_t*>(S.wcnt[d])[wv] = (uint8_t)__popcll(same);
         // grandchild capacities: one LDS add per emission
         {
             int32_t gg = prv.g;
@@ -1193,13 +1193,16 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
         {
             const uint32_t rp = par ^ 1;   // chunk i-1's parity
             uint32_t pre_l = 0, tot_l = 0;
-            if (lane < kDests) {
+            if (lane < kDests) {   // byte sums of the wave counts: earlier waves, all waves
                 pre_l = S.dcur[rp][lane];
                 tot_l = pre_l;
-                for (uint32_t q = 0; q < (uint32_t)NW; q++) {
-                    const uint32_t c = S.wcnt[q][lane];
-                    pre_l += q < wv ? c : 0u;
-                    tot_l += c;
+                const u32x4 w = *reinterpret_cast<const u32x4*>(S.wcnt[lane]);
+#pragma unroll
+                for (uint32_t k = 0; k < (uint32_t)NW / 4; k++) {
+                    const uint32_t nb = wv > 4 * k ? min(wv - 4 * k, 4u) : 0u;   // wave-uniform
+                    const uint32_t m = nb >= 4 ? 0xFFFFFFFFu : ((1u << (8 * nb)) - 1u);
+                    pre_l = __builtin_amdgcn_udot4(w[k] & m, 0x01010101u, pre_l, false);
+                    tot_l = __builtin_amdgcn_udot4(w[k], 0x01010101u, tot_l, false);
                 }
                 if (wv == 0) S.dcur[par][lane] = tot_l;
             }
