@@ -319,6 +319,14 @@ __device__ __forceinline__ int route_dest(const RouteIdx& R, int32_t cx, int32_t
     err |= bad_oct ? (uint32_t)ERR_OCTANT : (bad_sel ? (uint32_t)ERR_SEL : 0u);
     return (bad_oct || bad_sel) ? -1 : (bx | (by << 1) | (bz << 2)) * 3 + sel;
 }
+// route_dest without the error code (callers derive the codes on the rare
+// failing lanes only)
+__device__ __forceinline__ int route_dest_nc(const RouteIdx& R, int32_t cx, int32_t cy, int32_t cz, int32_t t) {
+    const int32_t bx = R.ix - 2 * cx, by = R.iy - 2 * cy, bz = R.iz - 2 * cz;
+    const int32_t sel = R.u - 2 * t + 1;
+    const bool bad = (((bx | by | bz) & ~1) != 0) || (uint32_t)sel > 2u;
+    return bad ? -1 : (bx | (by << 1) | (bz << 2)) * 3 + sel;
+}
 // slot, child route and grandchild route of one point, one ballot for all
 // divisions.  The grandchild level halves cell size and hex radius exactly
 // (metadata.rs:92,96: powers of two), so x / cs_g = 2 * RN(x / cs_c) exactly and
@@ -1127,7 +1135,6 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
         const int32_t lx = sl.x - rx, ly = sl.y - ry;
         const bool layer_ok = sl.z == t;
         const bool range_ok = lx >= 0 && ly >= 0 && lx < P.tx && ly < P.ty;
-        err |= (valid && !layer_ok) ? (uint32_t)ERR_LAYER : ((valid && !range_ok) ? (uint32_t)ERR_SLOT_RANGE : 0u);
         const bool slotted = valid && layer_ok && range_ok;
         const uint32_t local = slotted ? (uint32_t)(ly * P.tx + lx) : 0u;
         float X, Y, Z;
@@ -1136,10 +1143,19 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
         uint32_t dn;
         int32_t gn;
         {
-            uint32_t rerr = 0, gerr = 0;
-            const int d = route_dest(sr.rc, cx, cy, cz, t, rerr);
-            gn = route_dest(sr.rg, sr.rc.ix, sr.rc.iy, sr.rc.iz, sr.rc.u, gerr);
-            if (valid) err |= rerr | ((P.check_gchild && d >= 0) ? gerr : 0u);
+            const int d = route_dest_nc(sr.rc, cx, cy, cz, t);
+            gn = route_dest_nc(sr.rg, sr.rc.ix, sr.rc.iy, sr.rc.iz, sr.rc.u);
+            // error codes only on the (never expected) failing lanes
+            const bool bad = valid && (!layer_ok || !range_ok || d < 0 || (P.check_gchild && gn < 0));
+            if (__ballot(bad)) {
+                if (bad) {
+                    uint32_t rerr = 0, gerr = 0;
+                    err |= !layer_ok ? (uint32_t)ERR_LAYER : (!range_ok ? (uint32_t)ERR_SLOT_RANGE : 0u);
+                    const int d3 = route_dest(sr.rc, cx, cy, cz, t, rerr);
+                    (void)route_dest(sr.rg, sr.rc.ix, sr.rc.iy, sr.rc.iz, sr.rc.u, gerr);
+                    err |= rerr | ((P.check_gchild && d3 >= 0) ? gerr : 0u);
+                }
+            }
             dn = d < 0 ? 0u : (uint32_t)d;
             if (d < 0) gn = -1;
         }
@@ -1227,17 +1243,18 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
             // this one is a record) and whether a later candidate beats this one
             uint32_t bd = 0xFFFFFFFFu, bt = kNil;
             bool beaten = false;
-            for (uint32_t xk = claim[hc] & kNil; xk != kNil; xk = S.cnext[xk]) {
-                if (xk == tid) {   // own entry: known without LDS reads
-                    xk = myprev;
-                    if (xk == kNil) break;
-                }
+            // branch-free body; the own entry is skipped (known without LDS reads)
+            uint32_t xk = claim[hc] & kNil;
+            if (xk == tid) xk = myprev;
+            while (xk != kNil) {
                 const uint32_t dx = S.cd2[xk];
-                if (xk < tid) {
-                    if (dx < bd || (dx == bd && xk < bt)) { bd = dx; bt = xk; }
-                } else if (xk > tid) {
-                    beaten |= dx < me;
-                }
+                const uint32_t nx = S.cnext[xk];
+                const bool earlier = xk < tid;
+                const bool better = earlier && (dx < bd || (dx == bd && xk < bt));
+                bd = better ? dx : bd;
+                bt = better ? xk : bt;
+                beaten |= !earlier && dx < me;
+                xk = nx == tid ? myprev : nx;
             }
             if (bt != kNil && !(me < bd)) {
                 em = 0;                                // not a record: overflows at its key
