@@ -327,6 +327,9 @@ __device__ __forceinline__ int route_dest_nc(const RouteIdx& R, int32_t cx, int3
     const bool bad = (((bx | by | bz) & ~1) != 0) || (uint32_t)sel > 2u;
     return bad ? -1 : (bx | (by << 1) | (bz << 2)) * 3 + sel;
 }
+struct SlotRoute;
+__device__ __forceinline__ uint32_t slot_route_errs(const SlotRoute& sr, bool layer_ok, bool range_ok, int32_t cx,
+                                                    int32_t cy, int32_t cz, int32_t t, bool check_g);
 // slot, child route and grandchild route of one point, one ballot for all
 // divisions.  The grandchild level halves cell size and hex radius exactly
 // (metadata.rs:92,96: powers of two), so x / cs_g = 2 * RN(x / cs_c) exactly and
@@ -357,6 +360,17 @@ __device__ __forceinline__ SlotRoute slot_route(float x, float y, float z, const
         }
     }
     return S;
+}
+
+// Error codes of a point whose slot or routes failed (computed on those rare
+// lanes only; the common path uses route_dest_nc).
+__device__ __forceinline__ uint32_t slot_route_errs(const SlotRoute& sr, bool layer_ok, bool range_ok, int32_t cx,
+                                                    int32_t cy, int32_t cz, int32_t t, bool check_g) {
+    uint32_t rerr = 0, gerr = 0;
+    const uint32_t e = !layer_ok ? (uint32_t)ERR_LAYER : (!range_ok ? (uint32_t)ERR_SLOT_RANGE : 0u);
+    const int d = route_dest(sr.rc, cx, cy, cz, t, rerr);
+    (void)route_dest(sr.rg, sr.rc.ix, sr.rc.iy, sr.rc.iz, sr.rc.u, gerr);
+    return e | rerr | ((check_g && d >= 0) ? gerr : 0u);
 }
 
 // Buffer descriptor of a wave-uniform range.  Base and size are forced into
@@ -1148,13 +1162,7 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
             // error codes only on the (never expected) failing lanes
             const bool bad = valid && (!layer_ok || !range_ok || d < 0 || (P.check_gchild && gn < 0));
             if (__ballot(bad)) {
-                if (bad) {
-                    uint32_t rerr = 0, gerr = 0;
-                    err |= !layer_ok ? (uint32_t)ERR_LAYER : (!range_ok ? (uint32_t)ERR_SLOT_RANGE : 0u);
-                    const int d3 = route_dest(sr.rc, cx, cy, cz, t, rerr);
-                    (void)route_dest(sr.rg, sr.rc.ix, sr.rc.iy, sr.rc.iz, sr.rc.u, gerr);
-                    err |= rerr | ((P.check_gchild && d3 >= 0) ? gerr : 0u);
-                }
+                if (bad) err |= slot_route_errs(sr, layer_ok, range_ok, cx, cy, cz, t, P.check_gchild);
             }
             dn = d < 0 ? 0u : (uint32_t)d;
             if (d < 0) gn = -1;
@@ -1500,7 +1508,6 @@ __device__ __forceinline__ void small_process(const SlabParams& P, SmallLds& S, 
             const int32_t lx = sr.sl.x - rx, ly = sr.sl.y - ry;
             const bool layer_ok = sr.sl.z == t;
             const bool range_ok = lx >= 0 && ly >= 0 && lx < P.tx && ly < P.ty;
-            err |= (valid && !layer_ok) ? (uint32_t)ERR_LAYER : ((valid && !range_ok) ? (uint32_t)ERR_SLOT_RANGE : 0u);
             pending = valid && layer_ok && range_ok;
             local = pending ? (uint32_t)(ly * P.tx + lx) : 0u;
             if (pending && pk[ci] - P.kf_lo < P.kf_n) {   // merge mode: forced emission
@@ -1510,10 +1517,12 @@ __device__ __forceinline__ void small_process(const SlabParams& P, SmallLds& S, 
             float X, Y, Z;
             hex_to_world(sr.sl, G.cr, X, Y, Z);
             d2 = dist2(X, Y, Z, x, y, z);
-            uint32_t rerr = 0, gerr = 0;
-            const int d = route_dest(sr.rc, cx, cy, cz, t, rerr);
-            int g = route_dest(sr.rg, sr.rc.ix, sr.rc.iy, sr.rc.iz, sr.rc.u, gerr);
-            if (valid) err |= rerr | ((P.check_gchild && d >= 0) ? gerr : 0u);
+            const int d = route_dest_nc(sr.rc, cx, cy, cz, t);
+            int g = route_dest_nc(sr.rg, sr.rc.ix, sr.rc.iy, sr.rc.iz, sr.rc.u);
+            const bool bad = valid && (!layer_ok || !range_ok || d < 0 || (P.check_gchild && g < 0));
+            if (__ballot(bad)) {
+                if (bad) err |= slot_route_errs(sr, layer_ok, range_ok, cx, cy, cz, t, P.check_gchild);
+            }
             dn = d < 0 ? 0u : (uint32_t)d;
             if (d < 0) g = -1;
             own_d[ci] = (int32_t)dn;
@@ -1778,16 +1787,17 @@ __global__ __launch_bounds__(64) void k_slab_wave(SlabParams P) {
             const int32_t lx = sr.sl.x - rx, ly = sr.sl.y - ry;
             const bool layer_ok = sr.sl.z == t;
             const bool range_ok = lx >= 0 && ly >= 0 && lx < P.tx && ly < P.ty;
-            err |= (valid && !layer_ok) ? (uint32_t)ERR_LAYER : ((valid && !range_ok) ? (uint32_t)ERR_SLOT_RANGE : 0u);
             bool pending = valid && layer_ok && range_ok;
             const uint32_t local = pending ? (uint32_t)(ly * P.tx + lx) : 0u;
             float X, Y, Z;
             hex_to_world(sr.sl, G.cr, X, Y, Z);
             const float d2 = dist2(X, Y, Z, x, y, z);
-            uint32_t rerr = 0, gerr = 0;
-            const int d = route_dest(sr.rc, cx, cy, cz, t, rerr);
-            int g = route_dest(sr.rg, sr.rc.ix, sr.rc.iy, sr.rc.iz, sr.rc.u, gerr);
-            if (valid) err |= rerr | ((P.check_gchild && d >= 0) ? gerr : 0u);
+            const int d = route_dest_nc(sr.rc, cx, cy, cz, t);
+            int g = route_dest_nc(sr.rg, sr.rc.ix, sr.rc.iy, sr.rc.iz, sr.rc.u);
+            const bool bad = valid && (!layer_ok || !range_ok || d < 0 || (P.check_gchild && g < 0));
+            if (__ballot(bad)) {
+                if (bad) err |= slot_route_errs(sr, layer_ok, range_ok, cx, cy, cz, t, P.check_gchild);
+            }
             const uint32_t dn = d < 0 ? 0u : (uint32_t)d;
             if (d < 0) g = -1;
             own_d[c] = (int32_t)dn;
