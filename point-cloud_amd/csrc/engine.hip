@@ -1722,12 +1722,9 @@ template <class WL>
 __device__ __forceinline__ int wave_entry(WL& W, uint32_t local, uint32_t mask) {
     uint32_t h = hash_slot(local) & mask;
     for (uint32_t probe = 0; probe <= mask; probe++) {
-        const uint32_t k = W.tkey[h];
-        if ((k & 0xFFFFFFu) == local) return (int)h;
-        if (k == kEmpty32) {
-            const uint32_t old = atomicCAS(&W.tkey[h], kEmpty32, kNoClaim | local);
-            if (old == kEmpty32 || (old & 0xFFFFFFu) == local) return (int)h;
-        }
+        // CAS first: a new or already present slot costs one LDS round trip
+        const uint32_t old = atomicCAS(&W.tkey[h], kEmpty32, kNoClaim | local);
+        if (old == kEmpty32 || (old & 0xFFFFFFu) == local) return (int)h;
         h = (h + 1) & mask;
     }
     return -1;
