@@ -897,12 +897,8 @@ __device__ __forceinline__ int claim_insert(uint32_t* H, uint32_t local, uint32_
     const uint32_t mine = (local << 11) | tid;
     uint32_t h = hash_slot(local) & (CLAIM - 1);
     for (int probe = 0; probe < CLAIM; probe++) {
-        uint32_t e = H[h];
-        if (e == kEmpty32) {
-            const uint32_t old = atomicCAS(&H[h], kEmpty32, mine);
-            if (old == kEmpty32) return (int)h;
-            e = old;
-        }
+        const uint32_t e = atomicCAS(&H[h], kEmpty32, mine);   // CAS first (see claim_push)
+        if (e == kEmpty32) return (int)h;
         if ((e >> 11) == local) {
             atomicMin(&H[h], mine);
             return (int)h;
