@@ -1,0 +1,40 @@
+"""PCIe-inclusive rate: the config-4 points handed over in host
+memory through pcc_add_points (H2D inside the call) and then built, against
+the same build from device-resident input.  The host array is produced by the
+library's own generator on the device and copied out once, untimed.
+Usage: python scripts/pcie_bench.py [N]"""
+import json
+import os
+import sys
+import tempfile
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "..", "point-cloud_amd"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import pcconv  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000_000
+dev = torch.empty((n, 4), dtype=torch.int32, device="cuda")
+pcconv.synth_device(dev.data_ptr(), 0, n, 4, 0, -1000.0, 2000.0, 0)
+torch.cuda.synchronize()
+host = dev.cpu().numpy().view(pcconv.POINT_DTYPE).reshape(-1)
+del dev
+torch.cuda.empty_cache()
+res = {"points": n, "host_bytes": int(host.nbytes)}
+for rep in range(2):   # the first round pays the allocations
+    c = pcconv.Converter(tempfile.mkdtemp(prefix="pcc_pcie_"))
+    t0 = time.perf_counter()
+    c.add_points(host)
+    t1 = time.perf_counter()
+    c.build()
+    t2 = time.perf_counter()
+    c.build()   # again from the resident copy
+    t3 = time.perf_counter()
+    c.close()
+    res[f"round{rep}"] = {"h2d_ms": round((t1 - t0) * 1e3, 1), "build_ms": round((t2 - t1) * 1e3, 1),
+                          "rebuild_ms": round((t3 - t2) * 1e3, 1),
+                          "h2d_GBps": round(host.nbytes / (t1 - t0) / 1e9, 2),
+                          "pcie_inclusive_points_per_s": round(n / (t2 - t0) / 1e9, 3) * 1e9}
+print(json.dumps(res), flush=True)
