@@ -1119,6 +1119,8 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
     if (tid == 0) { S.nwin = 0; S.err = 0; }
     __syncthreads();
     STAMP(0);
+    // child-slab regions of this slab, one per lane < 24, kept in registers
+    const uint32_t my_doff = lane < kDests ? S.doff[lane] : 0u, my_dcap = lane < kDests ? S.dcap[lane] : 0u;
     const uint32_t nchunks = (n + BS - 1) / BS;
     auto step = [&](uint32_t ci, Stage& cur, Stage& prv, const Pre& mine, const Pre& prvb, Pre& pf) {
         const uint32_t par = ci & 1;
@@ -1212,7 +1214,8 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
         // same child slab before the chunk + in earlier waves + earlier lanes.
         {
             const uint32_t rp = par ^ 1;   // chunk i-1's parity
-            uint32_t pre_l = 0, tot_l = 0;
+            uint32_t pre_l = 0, tot_l = 0, base_l = 0;
+            int32_t room_l = 0;
             if (lane < kDests) {   // byte sums of the wave counts: earlier waves, all waves
                 pre_l = S.dcur[rp][lane];
                 tot_l = pre_l;
@@ -1225,11 +1228,15 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
                     tot_l = __builtin_amdgcn_udot4(w[k], 0x01010101u, tot_l, false);
                 }
                 if (wv == 0) S.dcur[par][lane] = tot_l;
+                base_l = my_doff + pre_l;                 // this wave's first position in child slab `lane`
+                room_l = (int32_t)(my_dcap - pre_l);      // and the capacity left from there
             }
-            const uint32_t r = (uint32_t)__shfl((int)pre_l, d, 64) + rw;
-            const bool ok = vd && r < S.dcap[d];
+            // both shuffles with every lane active (a bpermute from an inactive
+            // lane reads nothing)
+            const uint32_t pos = (uint32_t)__shfl((int)base_l, d, 64) + rw;
+            const int32_t room = __shfl(room_l, d, 64);
+            const bool ok = vd && (int32_t)rw < room;
             err |= (vd && !ok) ? (uint32_t)ERR_CAPACITY : 0u;
-            const uint32_t pos = S.doff[d] + r;
             if (!(PCC_ABL & 2)) {
                 bst4(oP, ok ? pos * 16 : 0xFFFFFFFFu, prv.em == 1 ? prv.gp : prvb.p);
                 bst(oK, ok ? pos * 4 : 0xFFFFFFFFu, prvb.k);
