@@ -188,8 +188,6 @@ private:
     std::vector<hipEvent_t> ev_pool_;
     std::string err_;
     bool built_ = false;
-    uint32_t small_grid_ = 1024;         // resident workgroups of the persistent small-slab kernel
-    uint32_t wave_grid_[3] = {2048, 2048, 2048};   // resident one-wave workgroups of k_slab_wave, per size class
 };
 
 // ---- sharded build helpers; synchronous, on an internal stream

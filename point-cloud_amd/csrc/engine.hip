@@ -1682,7 +1682,8 @@ __device__ __forceinline__ void small_process(const SlabParams& P, SmallLds& S, 
     STAMP_FLUSH(P.stamps);
 }
 
-// Persistent: each workgroup walks the small-slab list with a grid stride.
+// One workgroup per slab (launched with one per list entry; the grid stride
+// keeps any smaller grid correct).
 __global__ __launch_bounds__(kSmallBS) void k_slab_small(SlabParams P) {
     __shared__ SmallLds S;
     const uint32_t tid = threadIdx.x;
@@ -2342,17 +2343,6 @@ Engine::Engine(const Config& cfg, int device, hipStream_t stream) : cfg_(cfg), d
     HIP_CHECK(hipMalloc(&dev_->ctr, sizeof(Counters)));
     HIP_CHECK(hipMalloc(&dev_->bbox_part, kBBoxBlocks * 6 * sizeof(float)));
     HIP_CHECK(hipMalloc(&dev_->bbox_flag, sizeof(uint32_t)));
-    // resident workgroups of the persistent small-slab kernel
-    int cus = 0, per = 0;
-    HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device_));
-    HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_slab_small, kSmallBS, 0));
-    small_grid_ = (uint32_t)std::max(1, cus * std::max(per, 1));
-    HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_slab_wave<kWaveMax / 256>, 64, 0));
-    wave_grid_[0] = (uint32_t)std::max(1, cus * std::max(per, 1));
-    HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_slab_wave<kWaveMax / 128>, 64, 0));
-    wave_grid_[1] = (uint32_t)std::max(1, cus * std::max(per, 1));
-    HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_slab_wave<kWaveMax / 64>, 64, 0));
-    wave_grid_[2] = (uint32_t)std::max(1, cus * std::max(per, 1));
 }
 
 Engine::~Engine() {
@@ -3020,7 +3010,10 @@ int Engine::run_level(uint32_t h) {
             if (!hcnt[c]) continue;
             SP.wdesc = wd + (uint64_t)c * L->nsmall;
             SP.nwave = hcnt[c];
-            const uint32_t gr = std::min<uint32_t>(hcnt[c], wave_grid_[c]);
+            // one workgroup per slab: the dispatcher hands a finished wave's
+            // CU slot to the next slab (a persistent grid of resident waves
+            // walking the list was 1.6x slower at level 3 of config 4)
+            const uint32_t gr = hcnt[c];
             if (c == 0) k_slab_wave<kWaveMax / 256><<<gr, 64, 0, stream_>>>(SP);
             else if (c == 1) k_slab_wave<kWaveMax / 128><<<gr, 64, 0, stream_>>>(SP);
             else k_slab_wave<kWaveMax / 64><<<gr, 64, 0, stream_>>>(SP);
@@ -3028,7 +3021,7 @@ int Engine::run_level(uint32_t h) {
         if (hcnt[3]) {
             SP.sdesc = bd;
             SP.nlist = hcnt[3];
-            k_slab_small<<<std::min<uint32_t>(hcnt[3], small_grid_), kSmallBS, 0, stream_>>>(SP);
+            k_slab_small<<<hcnt[3], kSmallBS, 0, stream_>>>(SP);
         }
         ev_end(ST_SMALL);
     }
