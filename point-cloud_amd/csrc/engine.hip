@@ -1979,7 +1979,7 @@ struct BucketParams {
     uint32_t L;
 };
 
-constexpr int kBktBS = 256;
+constexpr int kBktBS = 512;
 
 // event batch of an emission of a level-h cell: max(eb0(key), cell's running sb)
 __device__ __forceinline__ uint32_t emission_eb(const BucketParams& B, uint32_t key, uint32_t csb) {
@@ -2006,7 +2006,7 @@ __device__ __forceinline__ uint32_t first_key_after(const uint32_t* files, uint3
 // inside each of its child slabs.
 __global__ __launch_bounds__(kBktBS) void k_bucket(BucketParams B) {
     __shared__ uint32_t lds[kBktBS / 64 + 1];
-    __shared__ uint32_t skey[kKeptMax], spos[kKeptMax];
+    __shared__ unsigned long long skp[kKeptMax];   // (key << 32) | arena position
     __shared__ uint32_t s_cnt, s_off;
     __shared__ uint32_t s_min, s_max;
     const uint32_t b = blockIdx.x, cell = b >> 3, oct = b & 7;
@@ -2076,32 +2076,28 @@ __global__ __launch_bounds__(kBktBS) void k_bucket(BucketParams B) {
             if (n) {
                 const uint32_t o = B.dest_off[di];
                 const uint32_t p = atomicAdd(&s_cnt, n);
-                for (uint32_t q = 0; q < n; q++) { skey[p + q] = B.nx.k[o + q]; spos[p + q] = o + q; }
+                for (uint32_t q = 0; q < n; q++) skp[p + q] = ((unsigned long long)B.nx.k[o + q] << 32) | (o + q);
             }
         }
         uint32_t np2 = 1;
         while (np2 < tot) np2 <<= 1;
         __syncthreads();
-        for (uint32_t i = tot + threadIdx.x; i < np2; i += kBktBS) { skey[i] = 0xFFFFFFFFu; spos[i] = 0; }
+        for (uint32_t i = tot + threadIdx.x; i < np2; i += kBktBS) skp[i] = ~0ull;
         __syncthreads();
-        // bitonic sort by key (keys are unique)
+        // bitonic sort by key (keys are unique, so the packed words order by
+        // key); one thread per compare-exchange pair
         for (uint32_t kk = 2; kk <= np2; kk <<= 1)
             for (uint32_t jj = kk >> 1; jj > 0; jj >>= 1) {
-                for (uint32_t i = threadIdx.x; i < np2; i += kBktBS) {
-                    const uint32_t ix = i ^ jj;
-                    if (ix > i) {
-                        const bool up = (i & kk) == 0;
-                        const uint32_t a = skey[i], c = skey[ix];
-                        if ((a > c) == up) {
-                            skey[i] = c; skey[ix] = a;
-                            const uint32_t t2 = spos[i]; spos[i] = spos[ix]; spos[ix] = t2;
-                        }
-                    }
+                for (uint32_t p = threadIdx.x; p < np2 / 2; p += kBktBS) {
+                    const uint32_t i = ((p & ~(jj - 1)) << 1) | (p & (jj - 1)), ix = i | jj;
+                    const bool up = (i & kk) == 0;
+                    const unsigned long long a = skp[i], c = skp[ix];
+                    if ((a > c) == up) { skp[i] = c; skp[ix] = a; }
                 }
                 __syncthreads();
             }
         for (uint32_t i = threadIdx.x; i < tot; i += kBktBS) {
-            const uint32_t o = spos[i];
+            const uint32_t o = (uint32_t)skp[i];
             const float4 v = B.nx.p[o];
             reinterpret_cast<float4*>(B.kept)[s_off + i] = v;
         }
