@@ -1698,7 +1698,7 @@ __global__ __launch_bounds__(kSmallBS) void k_slab_small(SlabParams P) {
 
 // ------------------------------------------------------------------ one wave per slab
 // Slabs of < kWaveMax arrivals (most of the deepest levels): one 64-lane wave
-// per slab, persistent over the wave list, ~13 KB of LDS each so a CU holds ~11
+// per slab, one workgroup per slab, ~13 KB of LDS each so a CU holds ~11
 // slabs at once, and no s_barrier between waves.  Same-slot arrivals of a
 // 64-arrival chunk are applied in lane (= key) order by claim rounds on the slot
 // key word (claim lane in the top byte); LDS operations of one wave execute in
