@@ -53,6 +53,20 @@ def test_batch_size_one_and_tiny_limit():
     _check([pts], cfg=dict(cell_point_overflow_limit=3, sub_grid_dimension=4, max_cell_size=8.0), batch=1)
 
 
+@pytest.mark.parametrize("n", [66_000, 140_000])
+def test_max_overflow_limit_kept_lists(n):
+    """Kept lists at the GPU's LDS sort capacity: cell_point_overflow_limit = 8192 (the
+    largest the GPU build accepts) with a 4-slot-wide sub-grid, so most points
+    overflow and buckets of up to 8192 points are kept and sorted by key in k_bucket
+    (cell.rs:108-153), or spilled around the threshold, over several files.  At 66 000
+    points the oracle keeps lists of up to 8 178 points (three above 4 096) and spills
+    five; at 140 000 every level-0 bucket spills."""
+    pts = synth(21, 0, n, lo=0.0, ext=7.999)
+    k = n // 3
+    _check([pts[:k], pts[k:2 * k], pts[2 * k:]],
+           cfg=dict(cell_point_overflow_limit=8192, sub_grid_dimension=4, max_cell_size=8.0))
+
+
 def test_gui_batch_size_50k():
     """The GUI path's default batch size (src/plugins/converter.rs:198-201,604: 50 000 per
     batch) over ragged files: batch boundaries move the event batches."""
