@@ -102,8 +102,9 @@ int pcc_add_points_device(pcc_converter* c, const pcc_point* dev_pts, uint64_t n
  * branch drops every point, ply.rs:43-51, but still counts batches). */
 int pcc_add_empty_batches(pcc_converter* c, uint32_t k);
 
-/* Deterministic synthetic file generated in HBM (kind 0 uniform in
- * [lo, lo+extent)^3, kind 1 clustered); used by bench.py and tests. */
+/* Deterministic synthetic file generated in HBM (kind 0 uniform
+ * in [lo, lo+extent)^3, kind 1 clustered blobs, kind 2 the config-3 Gaussian
+ * mixture: 32 clusters, sigma 10*2^U[0,3), Box-Muller); used by bench.py and tests. */
 int pcc_add_synthetic(pcc_converter* c, uint64_t seed, int kind, uint64_t n, float lo, float extent);
 
 /* Runs the hierarchy/LOD build on the GPU (converter.rs:114-139 for every
@@ -126,6 +127,33 @@ int pcc_adopt_prior(pcc_converter* dst, pcc_converter* src);
 
 /* Free without writing anything. */
 int pcc_close(pcc_converter* c);
+
+/* One cell of the built cloud as the reference holds it in memory (cell.rs:33-38
+ * Cell, Header cell.rs:238-261): the header values exactly as Cell::write_to
+ * stores them (cell.rs:155-181, 280-298), the grid points (points_grid; their
+ * order is unspecified, like the FxHashMap iteration of cell.rs:158-160) and the
+ * overflow entries (child index at h+1; count 0 == None, i.e. forwarded;
+ * otherwise the Some list in stored order), entries ordered by child octant. */
+typedef struct pcc_cell_view {
+    uint32_t hierarchy;                 /* CellId cell.rs:14-18 */
+    int32_t x, y, z;
+    uint32_t total_number_of_points, number_of_points, number_of_overflow_points;
+    float size, sub_cell_size, pos[3];
+    const pcc_point* grid;              /* number_of_points records */
+    uint32_t entries;                   /* overflow entries, <= 8 (cell.rs:162) */
+    int32_t child[8][3];
+    uint32_t count[8];
+    const pcc_point* list[8];
+} pcc_cell_view;
+
+/* Called once per cell; the view's pointers are valid during the call only.  A
+ * nonzero return stops the walk and becomes pcc_visit_cells' return value. */
+typedef int (*pcc_cell_visitor)(const pcc_cell_view* cell, void* user);
+
+/* Every cell of the built cloud, level by level (builds first if needed): the
+ * in-memory counterpart of pcc_write (the GUI keeps cells in memory,
+ * src/plugins/converter.rs:553-592).  Sharded converters visit their own cells. */
+int pcc_visit_cells(pcc_converter* c, pcc_cell_visitor fn, void* user);
 
 int pcc_get_stats(const pcc_converter* c, pcc_stats* out);
 

@@ -26,8 +26,8 @@ _lib = None
 
 
 def build() -> str:
-    src = os.path.join(HERE, "pcc_oracle.c")
-    if not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < os.path.getmtime(src):
+    srcs = [os.path.join(HERE, f) for f in ("pcc_oracle.c", "digest.c", "digest.h")]
+    if not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < max(os.path.getmtime(f) for f in srcs):
         subprocess.check_call(["make", "-s", "-C", HERE, "build/liboracle.so"])
     return LIB_PATH
 
@@ -56,6 +56,16 @@ def lib():
         L.orc_synth.argtypes = [C.c_uint64, C.c_int, C.c_uint64, C.c_uint64, C.c_float, C.c_float, C.c_void_p]
         L.orc_load.argtypes = [C.c_void_p, C.c_char_p]
         L.orc_load.restype = C.c_int
+        # canonical digests (digest.c)
+        L.dg_new.restype = C.c_void_p
+        L.dg_free.argtypes = [C.c_void_p]
+        L.dg_add_view.argtypes = [C.c_void_p, C.c_void_p]
+        L.dg_count.argtypes = [C.c_void_p]
+        L.dg_count.restype = C.c_uint64
+        L.dg_get.argtypes = [C.c_void_p, C.c_uint64, C.POINTER(C.c_int64), C.POINTER(C.c_uint64)]
+        L.dg_totals.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
+        L.dg_view_size.restype = C.c_uint64
+        L.orc_digest.argtypes = [C.c_void_p, C.c_void_p]
         _lib = L
     return _lib
 
@@ -117,6 +127,45 @@ class Oracle:
     def close(self):
         if self._h:
             lib().orc_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Digest:
+    """Canonical digests per level-0 subtree (digest.c): feed cell views of
+    either side (the HIP build's pcc_cell_view through pcc_visit_cells, or the
+    oracle's own cells), then compare `result()`."""
+
+    def __init__(self):
+        self._h = lib().dg_new()
+
+    def add_view(self, view_ptr: int):
+        lib().dg_add_view(self._h, C.c_void_p(view_ptr))
+
+    def add_oracle(self, o: "Oracle"):
+        lib().orc_digest(o._h, self._h)
+
+    def result(self) -> dict:
+        L = lib()
+        n = L.dg_count(self._h)
+        subs = []
+        ai, au = (C.c_int64 * 4)(), (C.c_uint64 * 4)()
+        for i in range(n):
+            L.dg_get(self._h, i, ai, au)
+            subs.append({"subtree": [ai[0], ai[1], ai[2]], "levels": ai[3], "cells": au[0], "points": au[1],
+                         "W": au[2], "digest": "%016x" % au[3]})
+        t = (C.c_uint64 * 2)()
+        L.dg_totals(self._h, t)
+        return {"subtrees": subs, "grid_points": t[0], "kept_points": t[1]}
+
+    def close(self):
+        if self._h:
+            lib().dg_free(self._h)
             self._h = None
 
     def __del__(self):

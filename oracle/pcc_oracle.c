@@ -641,7 +641,62 @@ static uint64_t synth_hash(uint64_t seed, uint64_t i, uint32_t a) {
 }
 static float synth_unit(uint64_t h) { return (float)(uint32_t)(h >> 40) * (1.0f / 16777216.0f); }
 
-/* kind 0: uniform in [lo, lo+ext)^3 ; kind 1: clustered (32 Irwin-Hall(4) blobs) */
+/* kind 2 helpers (config 3 of SURVEY.md §8d: 32-cluster Gaussian mixture,
+ * sigma = 10 * 2^U[0,3), Box-Muller).  The transcendentals are fixed
+ * polynomials evaluated in plain f32 operations (this file is compiled with
+ * -ffp-contract=off), the root is the correctly rounded one. */
+static float syn_from_bits(uint32_t b) { float f; memcpy(&f, &b, 4); return f; }
+static float syn_ln(float u) { /* u = m 2^e ; ln m = 2 atanh((m-1)/(m+1)) */
+    uint32_t b; memcpy(&b, &u, 4);
+    int e = (int)((b >> 23) & 255u) - 127;
+    float m = syn_from_bits((b & 0x7FFFFFu) | 0x3F800000u);
+    float s = (m - 1.0f) / (m + 1.0f), s2 = s * s;
+    float p = 0.0909090909f;
+    p = (p * s2) + 0.111111111f;
+    p = (p * s2) + 0.142857143f;
+    p = (p * s2) + 0.2f;
+    p = (p * s2) + 0.333333333f;
+    p = (p * s2) + 1.0f;
+    return ((float)e * 0.693147181f) + ((2.0f * s) * p);
+}
+static void syn_cos_sin(float u, float* co, float* si) { /* of 2 pi u: quadrant of 4u, Taylor on [0, pi/2) */
+    float a = 4.0f * u, qf = floorf(a);
+    int q = (int)qf;
+    float x = (a - qf) * 1.57079633f, x2 = x * x;
+    float s = -2.50521084e-8f;
+    s = (s * x2) + 2.75573192e-6f;
+    s = (s * x2) - 1.98412698e-4f;
+    s = (s * x2) + 8.33333333e-3f;
+    s = (s * x2) - 0.166666667f;
+    s = ((s * x2) + 1.0f) * x;
+    float c = 2.08767570e-9f;
+    c = (c * x2) - 2.75573192e-7f;
+    c = (c * x2) + 2.48015873e-5f;
+    c = (c * x2) - 1.38888889e-3f;
+    c = (c * x2) + 4.16666667e-2f;
+    c = (c * x2) - 0.5f;
+    c = (c * x2) + 1.0f;
+    switch (q & 3) {
+        case 0: *co = c; *si = s; break;
+        case 1: *co = -s; *si = c; break;
+        case 2: *co = -c; *si = -s; break;
+        default: *co = s; *si = -c; break;
+    }
+}
+static float syn_pow2_frac(float f) { /* 2^f = e^(f ln 2), f in [0,1) */
+    float x = f * 0.693147181f;
+    float p = 1.98412698e-4f;
+    p = (p * x) + 1.38888889e-3f;
+    p = (p * x) + 8.33333333e-3f;
+    p = (p * x) + 4.16666667e-2f;
+    p = (p * x) + 0.166666667f;
+    p = (p * x) + 0.5f;
+    p = (p * x) + 1.0f;
+    return (p * x) + 1.0f;
+}
+
+/* kind 0: uniform in [lo, lo+ext)^3 ; kind 1: clustered (32 Irwin-Hall(4) blobs) ;
+ * kind 2: config-3 Gaussian mixture (above) */
 void orc_synth(uint64_t seed, int kind, uint64_t first, uint64_t n, float lo, float ext, orc_point* out) {
     for (uint64_t j = 0; j < n; j++) {
         uint64_t i = first + j;
@@ -651,6 +706,28 @@ void orc_synth(uint64_t seed, int kind, uint64_t first, uint64_t n, float lo, fl
             p.x = lo + ext * synth_unit(synth_hash(seed, i, 0));
             p.y = lo + ext * synth_unit(synth_hash(seed, i, 1));
             p.z = lo + ext * synth_unit(synth_hash(seed, i, 2));
+        } else if (kind == 2) {
+            uint32_t k = (uint32_t)(hc >> 59);
+            float e3 = 3.0f * synth_unit(synth_hash(seed ^ 0xC2u, k, 0));
+            float ef = floorf(e3);
+            float scale = ef == 0.0f ? 1.0f : (ef == 1.0f ? 2.0f : 4.0f);
+            float sig = 10.0f * (syn_pow2_frac(e3 - ef) * scale);
+            float nv[4];
+            for (uint32_t pr = 0; pr < 2; pr++) {
+                uint64_t h = synth_hash(seed, i, pr);
+                float u1 = (float)((uint32_t)((h >> 40) & 0xFFFFFFu) + 1u) * (1.0f / 16777216.0f);
+                float r = (float)sqrt((double)(-2.0f * syn_ln(u1)));
+                float co, si;
+                syn_cos_sin(synth_unit(h << 24), &co, &si);
+                nv[2 * pr] = r * co;
+                nv[2 * pr + 1] = r * si;
+            }
+            float v[3];
+            for (int a = 0; a < 3; a++) {
+                float c = (lo + 0.05f * ext) + (0.9f * ext) * synth_unit(synth_hash(seed ^ 0xC1u, k, (uint32_t)a));
+                v[a] = c + sig * nv[a];
+            }
+            p.x = v[0]; p.y = v[1]; p.z = v[2];
         } else {
             uint32_t k = (uint32_t)(hc >> 59); /* cluster 0..31 */
             float c[3], sig;
@@ -668,3 +745,31 @@ void orc_synth(uint64_t seed, int kind, uint64_t first, uint64_t n, float lo, fl
         out[j] = p;
     }
 }
+
+/* ---------------------------------------------------------------- digests (digest.c) */
+#include "digest.h"
+/* Every cell of the converter into a canonical-digest accumulator (per level-0
+ * subtree).  Overflow entries are passed in insertion order; dg_cell sorts them. */
+void orc_digest(const orc_conv* c, dg_acc* acc) {
+    for (size_t i = 0; i < c->ncells; i++) {
+        const cell* k = c->cellv[i];
+        dg_view v;
+        memset(&v, 0, sizeof v);
+        v.hierarchy = k->h; v.x = k->idx.x; v.y = k->idx.y; v.z = k->idx.z;
+        v.total = k->total; v.number = k->number; v.overflow = k->overflow;
+        v.size = k->size; v.sub = k->sub;
+        v.pos[0] = k->pos[0]; v.pos[1] = k->pos[1]; v.pos[2] = k->pos[2];
+        v.grid = (const dg_point*)k->gpts.p;
+        v.entries = (uint32_t)k->nb;
+        for (int j = 0; j < k->nb; j++) {
+            v.child[j][0] = k->b[j].idx.x; v.child[j][1] = k->b[j].idx.y; v.child[j][2] = k->b[j].idx.z;
+            v.count[j] = k->b[j].state == 1 ? (uint32_t)k->b[j].pts.len : 0u;
+            v.list[j] = (const dg_point*)k->b[j].pts.p;
+        }
+        dg_add_view(acc, &v);
+    }
+}
+void orc_bbox(const orc_conv* c, float out[6]) {
+    for (int a = 0; a < 3; a++) { out[a] = c->bmin[a]; out[3 + a] = c->bmax[a]; }
+}
+uint64_t orc_number_of_points(const orc_conv* c) { return c->number_of_points; }

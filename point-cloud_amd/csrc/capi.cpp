@@ -185,7 +185,7 @@ int pcc_add_empty_batches(pcc_converter* c, uint32_t k) {
 int pcc_add_synthetic(pcc_converter* c, uint64_t seed, int kind, uint64_t n, float lo, float extent) {
     if (!c) return set_err(-EINVAL, "null argument");
     if (c->built) return set_err(-EINVAL, "points added after build");
-    if (kind != 0 && kind != 1) return set_err(-EINVAL, "kind must be 0 (uniform) or 1 (clustered)");
+    if (kind < 0 || kind > 2) return set_err(-EINVAL, "kind must be 0 (uniform), 1 (clustered blobs) or 2 (config-3 Gaussian mixture)");
     GUARD_BEGIN
     c->eng->add_file_synth(seed, kind, n, c->opt.batch_size, lo, extent);
     HIP_CHECK(hipStreamSynchronize(c->eng->stream()));
@@ -278,6 +278,30 @@ static int write_impl(pcc_converter* c, bool with_metadata) {
     GUARD_END
 }
 
+int pcc_visit_cells(pcc_converter* c, pcc_cell_visitor fn, void* user) {
+    if (!c || !fn) return set_err(-EINVAL, "null argument");
+    if (!c->built) {
+        int rc = pcc_build(c);
+        if (rc) return rc;
+    }
+    GUARD_BEGIN
+    LevelHost H;
+    HostPoints grid, kept;
+    pcc_cell_view v;
+    for (uint32_t i = 0; i < c->eng->num_levels(); i++) {
+        const int rc = c->eng->download_level(i, H, grid, kept);
+        if (rc) return set_err(rc, c->eng->last_error());
+        const uint32_t ncells = (uint32_t)(H.cell_idx.size() / 3);
+        for (uint32_t k = 0; k < ncells; k++) {
+            level_cell_view(c->meta.config, H, k, grid.data(), kept.data(), v);
+            const int r = fn(&v, user);
+            if (r) return r;
+        }
+    }
+    return 0;
+    GUARD_END
+}
+
 int pcc_write(pcc_converter* c) { return write_impl(c, true); }
 int pcc_write_cells(pcc_converter* c) { return write_impl(c, false); }
 
@@ -318,7 +342,7 @@ static ShardGrid to_grid(const pcc_shard_grid* g) {
 int pcc_synth_device(pcc_point* dst, uint64_t first, uint64_t n, uint64_t seed, int kind, float lo, float extent,
                      int device) {
     if (!dst && n) return set_err(-EINVAL, "null argument");
-    if (kind != 0 && kind != 1) return set_err(-EINVAL, "kind must be 0 (uniform) or 1 (clustered)");
+    if (kind < 0 || kind > 2) return set_err(-EINVAL, "kind must be 0 (uniform), 1 (clustered blobs) or 2 (config-3 Gaussian mixture)");
     GUARD_BEGIN
     return shard_synth(reinterpret_cast<Point*>(dst), first, n, seed, kind, lo, extent, device);
     GUARD_END
@@ -531,21 +555,29 @@ int pcc_convert_files(const char* out_dir, const char* const* paths, size_t npat
         const size_t dot = p.find_last_of('.');
         const size_t slash = p.find_last_of('/');
         std::string ext = (dot == std::string::npos || (slash != std::string::npos && dot < slash)) ? "" : p.substr(dot + 1);
+        // lib.rs:31-52: a get_batch error is logged and ends that file; the batches
+        // read before it stay, the failing batch is lost, the next file follows.
+        // So a file whose data ends early contributes its complete batches only.
+        const uint64_t B = c->opt.batch_size;
         if (ext == "ply") {
             PlyResult r;
             std::string err;
             if (!read_ply(p, r, err)) {
                 pcc_close(c);
-                return set_err(-EIO, err);   // the reference unwraps reader construction (ply.rs:20-21)
+                return set_err(-EIO, err);   // the reference unwraps header parsing (ply.rs:20-24)
             }
             log_line("INFO", "Converting %llu points", (unsigned long long)r.vertex_count);
             if (r.ascii) {
-                const uint64_t b = c->opt.batch_size;
-                rc = pcc_add_empty_batches(c, (uint32_t)std::max<uint64_t>(1, (r.vertex_count + b - 1) / b));
+                const uint64_t nb = r.data_error.empty() ? std::max<uint64_t>(1, (r.vertex_count + B - 1) / B)
+                                                         : r.ascii_lines / B;
+                if (nb) rc = pcc_add_empty_batches(c, (uint32_t)nb);
             } else {
-                rc = pcc_add_points(c, reinterpret_cast<const pcc_point*>(r.points.data()), r.points.size());
+                const uint64_t keep = r.data_error.empty() ? r.points.size() : (r.points.size() / B) * B;
+                if (r.data_error.empty() || keep)
+                    rc = pcc_add_points(c, reinterpret_cast<const pcc_point*>(r.points.data()), keep);
             }
             if (rc) { pcc_close(c); return rc; }
+            if (!r.data_error.empty()) log_line("ERROR", "%s", r.data_error.c_str());
         } else if (ext == "las" || ext == "laz") {   // converter/las.rs:14-46
             LasResult r;
             std::string err;
@@ -558,8 +590,11 @@ int pcc_convert_files(const char* out_dir, const char* const* paths, size_t npat
                 continue;
             }
             log_line("INFO", "Converting %llu points", (unsigned long long)r.count);
-            rc = pcc_add_points(c, reinterpret_cast<const pcc_point*>(r.points.data()), r.points.size());
+            const uint64_t keep = r.data_error.empty() ? r.points.size() : (r.points.size() / B) * B;
+            if (r.data_error.empty() || keep)
+                rc = pcc_add_points(c, reinterpret_cast<const pcc_point*>(r.points.data()), keep);
             if (rc) { pcc_close(c); return rc; }
+            if (!r.data_error.empty()) log_line("ERROR", "%s", r.data_error.c_str());
         } else if (ext == "json") {   // converter/own.rs: another converted cloud as input
             std::vector<Point> pts;
             uint64_t total = 0;

@@ -177,6 +177,7 @@ private:
     std::vector<uint32_t> n_prior_cells_;
     uint64_t keys_cap_ = 0;
     bool keyed_ = false;
+    uint64_t declared_total_ = 0;        // keyed input: global points of the declared files
     Dev* dev_ = nullptr;
     std::vector<Level*> levels_;
     float bmin_[3] = {0, 0, 0}, bmax_[3] = {0, 0, 0};

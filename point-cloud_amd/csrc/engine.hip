@@ -2489,6 +2489,7 @@ void Engine::declare_files(const uint64_t* file_points, uint64_t nfiles, uint32_
         g += file_points[f];
         nbatches_ += batches_of(file_points[f], batch);
     }
+    declared_total_ += g;
     keyed_ = true;
 }
 
@@ -2546,6 +2547,7 @@ void Engine::clear_input() {
     file_eb0_.clear();
     file_batch_.clear();
     keyed_ = false;
+    declared_total_ = 0;
     built_ = false;
 }
 
@@ -2571,6 +2573,8 @@ int Engine::build() {
     // cloud's points come first as "seeds" with keys 0 .. S-1, so every one of
     // them precedes every new point in key order, then the new points with keys
     // S + i.  All seeds belong to a pseudo batch 0 before the new batches.
+    if (prior_ && keyed_ && nseeds_ + declared_total_ >= 0xFFFFFFFFull)   // keys S + global key (k_comb_keys)
+        return fail(-75, "sharded merge: this rank's existing points plus the global new points exceed 2^32-1 keys");
     if (prior_) {
         if (!comb_ok_) {
             if (comb_cap_ < nseeds_ + n_) {

@@ -201,57 +201,85 @@ int make_output_dirs(const std::string& dir, uint32_t hierarchies, std::string& 
     return 0;
 }
 
+// Header values of a new cell (converter.rs:197-199, cell.rs:43-49, 264-274) and
+// its contents after the build.  A cell's slabs are consecutive and the
+// downloaded winners are compacted in slab order, so its grid points are one
+// contiguous run.
+void level_cell_view(const Config& cfg, const LevelHost& L, uint32_t c, const Point* grid, const Point* kept,
+                     pcc_cell_view& v) {
+    const float size = cell_size(cfg.max_cell_size, L.h);
+    v.hierarchy = L.h;
+    v.x = L.cell_idx[3 * c];
+    v.y = L.cell_idx[3 * c + 1];
+    v.z = L.cell_idx[3 * c + 2];
+    uint32_t number = 0, overflow = 0, nb = 0;
+    for (uint32_t s = L.cell_slab0[c]; s < L.cell_slab0[c + 1]; s++) number += L.slab_grid_n[s];
+    const uint32_t s0 = L.cell_slab0[c];
+    v.grid = reinterpret_cast<const pcc_point*>(grid + L.grid_base + (s0 < L.slab_grid_off.size() ? L.slab_grid_off[s0] : 0));
+    for (int o = 0; o < 8; o++) {
+        const uint32_t st = L.bkt_state[8 * c + o];
+        if (!st) continue;
+        v.child[nb][0] = 2 * v.x + (o & 1);
+        v.child[nb][1] = 2 * v.y + ((o >> 1) & 1);
+        v.child[nb][2] = 2 * v.z + ((o >> 2) & 1);
+        if (st == 1) {
+            v.count[nb] = L.bkt_n[8 * c + o];
+            v.list[nb] = reinterpret_cast<const pcc_point*>(kept + L.kept_base + L.bkt_off[8 * c + o]);
+            overflow += v.count[nb];
+        } else {
+            v.count[nb] = 0;
+            v.list[nb] = nullptr;
+        }
+        nb++;
+    }
+    v.entries = nb;
+    v.total_number_of_points = number + overflow;
+    v.number_of_points = number;
+    v.number_of_overflow_points = overflow;
+    v.size = size;
+    v.sub_cell_size = sub_cell_size(size, cfg.sub_grid_dimension);
+    v.pos[0] = cell_pos1(v.x, size);
+    v.pos[1] = cell_pos1(v.y, size);
+    v.pos[2] = cell_pos1(v.z, size);
+}
+
 // Cell files of one level (Cell::write_to cell.rs:155-181, Header::write_to
 // :280-298), cells split over `nthreads` host threads (files are independent).
 int write_level_cells(const std::string& dir, const Config& cfg, const LevelHost& L, const Point* grid,
                       const Point* kept, unsigned nthreads, std::string& err) {
     const uint32_t h = L.h;
-    const float size = cell_size(cfg.max_cell_size, h);                 // converter.rs:197-199
-    const float sub = sub_cell_size(size, cfg.sub_grid_dimension);
     const uint32_t ncells = (uint32_t)(L.cell_idx.size() / 3);
     std::atomic<uint32_t> next{0};
     std::atomic<int> rc{0};
     std::mutex emu;
     auto work = [&]() {
         std::string buf;
+        pcc_cell_view v;
         for (;;) {
             const uint32_t c = next.fetch_add(1);
             if (c >= ncells || rc.load() != 0) return;
-            const int32_t ix = L.cell_idx[3 * c], iy = L.cell_idx[3 * c + 1], iz = L.cell_idx[3 * c + 2];
-            uint32_t number = 0, overflow = 0, nb = 0;
-            for (uint32_t s = L.cell_slab0[c]; s < L.cell_slab0[c + 1]; s++) number += L.slab_grid_n[s];
-            for (int o = 0; o < 8; o++) {
-                const uint32_t st = L.bkt_state[8 * c + o];
-                if (st) nb++;
-                if (st == 1) overflow += L.bkt_n[8 * c + o];
-            }
+            level_cell_view(cfg, L, c, grid, kept, v);
             buf.clear();
-            buf.reserve(48 + 16ull * (number + overflow) + 1 + 16 * nb);
-            put32(buf, h);
-            put32(buf, (uint32_t)ix); put32(buf, (uint32_t)iy); put32(buf, (uint32_t)iz);
-            put32(buf, number + overflow);
-            put32(buf, number);
-            put32(buf, overflow);
-            putf(buf, size);
-            putf(buf, sub);
-            putf(buf, cell_pos1(ix, size)); putf(buf, cell_pos1(iy, size)); putf(buf, cell_pos1(iz, size));
+            buf.reserve(48 + 16ull * v.total_number_of_points + 1 + 16 * v.entries);
+            put32(buf, v.hierarchy);
+            put32(buf, (uint32_t)v.x); put32(buf, (uint32_t)v.y); put32(buf, (uint32_t)v.z);
+            put32(buf, v.total_number_of_points);
+            put32(buf, v.number_of_points);
+            put32(buf, v.number_of_overflow_points);
+            putf(buf, v.size);
+            putf(buf, v.sub_cell_size);
+            putf(buf, v.pos[0]); putf(buf, v.pos[1]); putf(buf, v.pos[2]);
             // grid points (cell.rs:158-160; order free)
-            for (uint32_t s = L.cell_slab0[c]; s < L.cell_slab0[c + 1]; s++)
-                buf.append(reinterpret_cast<const char*>(grid + L.grid_base + L.slab_grid_off[s]), 16ull * L.slab_grid_n[s]);
-            buf.push_back((char)(uint8_t)nb);   // cell.rs:162
-            for (int o = 0; o < 8; o++) {
-                const uint32_t st = L.bkt_state[8 * c + o];
-                if (!st) continue;
-                put32(buf, (uint32_t)(2 * ix + (o & 1)));
-                put32(buf, (uint32_t)(2 * iy + ((o >> 1) & 1)));
-                put32(buf, (uint32_t)(2 * iz + ((o >> 2) & 1)));
-                if (st == 1) {
-                    put32(buf, L.bkt_n[8 * c + o]);
-                    buf.append(reinterpret_cast<const char*>(kept + L.kept_base + L.bkt_off[8 * c + o]), 16ull * L.bkt_n[8 * c + o]);
-                } else {
-                    put32(buf, 0);
-                }
+            buf.append(reinterpret_cast<const char*>(v.grid), 16ull * v.number_of_points);
+            buf.push_back((char)(uint8_t)v.entries);   // cell.rs:162
+            for (uint32_t e = 0; e < v.entries; e++) {
+                put32(buf, (uint32_t)v.child[e][0]);
+                put32(buf, (uint32_t)v.child[e][1]);
+                put32(buf, (uint32_t)v.child[e][2]);
+                put32(buf, v.count[e]);
+                if (v.count[e]) buf.append(reinterpret_cast<const char*>(v.list[e]), 16ull * v.count[e]);
             }
+            const int32_t ix = v.x, iy = v.y, iz = v.z;
             char name[96];
             snprintf(name, sizeof name, "/h_%u/c_%d_%d_%d.bin", h, ix, iy, iz);
             const std::string path = dir + name;
@@ -459,8 +487,13 @@ bool read_las(const std::string& path, LasResult& out, std::string& err) {
     const uint64_t chunk = 1 << 16;
     buf.resize(chunk * rec);
     for (uint64_t base = 0; base < n; base += chunk) {
-        const uint64_t m = std::min<uint64_t>(chunk, n - base);
-        if (fread(buf.data(), rec, m, f) != m) return bad("truncated point data");
+        uint64_t m = std::min<uint64_t>(chunk, n - base);
+        const uint64_t got_m = fread(buf.data(), rec, m, f);
+        if (got_m != m) {   // las Reader::read_n fails on the missing records (las.rs:23-46)
+            out.data_error = path + ": truncated point data";
+            m = got_m;
+            out.points.resize(base + m);
+        }
         for (uint64_t i = 0; i < m; i++) {
             const uint8_t* r = buf.data() + i * rec;
             int32_t X, Y, Z;
@@ -477,6 +510,7 @@ bool read_las(const std::string& path, LasResult& out, std::string& err) {
             p.rgba[2] = (uint8_t)c[2];
             p.rgba[3] = 255;
         }
+        if (!out.data_error.empty()) break;
     }
     fclose(f);
     return true;
@@ -612,6 +646,11 @@ bool read_ply(const std::string& path, PlyResult& out, std::string& err) {
     out.points.clear();
     if (enc == ASCII) {   // ply.rs:43-51: lines are parsed but never pushed into the batch
         out.ascii = true;
+        // a missing line makes read_ascii_element fail (ply.rs:46-47): count the lines present
+        uint64_t lines = 0;
+        while (lines < nvert && std::getline(f, line)) lines++;
+        out.ascii_lines = lines;
+        if (lines < nvert) out.data_error = path + ": truncated ASCII vertex data";
         return true;
     }
     const bool sw = enc == BE;
@@ -644,8 +683,13 @@ bool read_ply(const std::string& path, PlyResult& out, std::string& err) {
         for (uint64_t base = 0; base < nvert; base += chunk) {
             const uint64_t m = std::min(chunk, nvert - base);
             f.read(reinterpret_cast<char*>(buf.data()), (std::streamsize)(m * rec));
-            if ((uint64_t)f.gcount() != m * rec) { err = path + ": truncated vertex data"; return false; }
-            for (uint64_t i = 0; i < m; i++) {
+            const uint64_t got_m = (uint64_t)f.gcount() / rec;
+            const bool short_read = got_m != m;
+            if (short_read) {   // read_*_endian_element fails on the first missing record (ply.rs:54-70)
+                out.data_error = path + ": truncated vertex data";
+                out.points.resize(base + got_m);
+            }
+            for (uint64_t i = 0; i < got_m; i++) {
                 Point& pt = out.points[base + i];
                 pt.x = pt.y = pt.z = 0;
                 pt.rgba[0] = pt.rgba[1] = pt.rgba[2] = 0;
@@ -653,6 +697,7 @@ bool read_ply(const std::string& path, PlyResult& out, std::string& err) {
                 const uint8_t* q = buf.data() + i * rec;
                 for (auto& p : vprops) { apply(pt, p, q); q += psize(p.type); }
             }
+            if (short_read) break;
         }
     } else {
         for (uint64_t i = 0; i < nvert; i++) {
@@ -670,7 +715,11 @@ bool read_ply(const std::string& path, PlyResult& out, std::string& err) {
                     f.read(reinterpret_cast<char*>(tmp), psize(p.type));
                     apply(pt, p, tmp);
                 }
-                if (!f) { err = path + ": truncated vertex data"; return false; }
+                if (!f) {
+                    out.data_error = path + ": truncated vertex data";
+                    out.points.resize(i);
+                    return true;
+                }
             }
         }
     }

@@ -7,6 +7,7 @@
 #include <string>
 #include <vector>
 
+#include "../../include/pcconv.h"
 #include "engine.h"
 
 namespace pcc {
@@ -29,6 +30,10 @@ bool parse_metadata_json(const std::string& text, Metadata& m, std::string& err)
 // with_metadata=false writes the cells only (sharded build: rank 0 writes the
 // global metadata.json once all ranks' cells are on disk).
 int make_output_dirs(const std::string& dir, uint32_t hierarchies, std::string& err);
+// Cell c of a downloaded level as the C ABI's view (header values as
+// Cell::write_to stores them, cell.rs:155-181; pointers into grid / kept).
+void level_cell_view(const Config& cfg, const LevelHost& L, uint32_t c, const Point* grid, const Point* kept,
+                     pcc_cell_view& v);
 // Cell files of one level, split over nthreads host threads.
 int write_level_cells(const std::string& dir, const Config& cfg, const LevelHost& L, const Point* grid,
                       const Point* kept, unsigned nthreads, std::string& err);
@@ -69,6 +74,9 @@ struct PlyResult {
     std::vector<Point> points;
     uint64_t vertex_count = 0;
     bool ascii = false;
+    uint64_t ascii_lines = 0;   // ASCII: vertex lines present (a short file ends the reader early)
+    std::string data_error;     // set when the vertex data ends early or is unreadable:
+                                // `points` then holds the records read before the error
 };
 bool read_ply(const std::string& path, PlyResult& out, std::string& err);
 
@@ -81,6 +89,7 @@ struct LasResult {
     std::vector<Point> points;
     uint64_t count = 0;   // header number_of_points
     bool laz = false;
+    std::string data_error;   // truncated point data: `points` holds the records read before it
 };
 bool read_las(const std::string& path, LasResult& out, std::string& err);
 

@@ -34,7 +34,7 @@ EXPORTS = ["pcc_abi_version", "pcc_last_error", "pcc_options_default", "pcc_open
            "pcc_convert_files", "pcc_shard_grid_from_bbox", "pcc_synth_device", "pcc_shard_bbox",
            "pcc_shard_histogram", "pcc_shard_route", "pcc_declare_files", "pcc_add_keyed_points_device",
            "pcc_set_summary", "pcc_write_cells", "pcc_write_metadata", "pcc_clear_input", "pcc_adopt_prior",
-           "pcc_open_subtrees"]
+           "pcc_open_subtrees", "pcc_visit_cells"]
 
 
 class Options(C.Structure):
@@ -68,6 +68,35 @@ class ShardGrid(C.Structure):
     @property
     def ncells(self) -> int:
         return int(self.dims[0]) * int(self.dims[1]) * int(self.dims[2])
+
+
+class CellView(C.Structure):
+    """pcc_cell_view: one built cell in memory (cell.rs:33-38, Header cell.rs:238-261)."""
+    _fields_ = [("hierarchy", C.c_uint32), ("x", C.c_int32), ("y", C.c_int32), ("z", C.c_int32),
+                ("total_number_of_points", C.c_uint32), ("number_of_points", C.c_uint32),
+                ("number_of_overflow_points", C.c_uint32), ("size", C.c_float), ("sub_cell_size", C.c_float),
+                ("pos", C.c_float * 3), ("grid", C.c_void_p), ("entries", C.c_uint32),
+                ("child", (C.c_int32 * 3) * 8), ("count", C.c_uint32 * 8), ("list", C.c_void_p * 8)]
+
+    def grid_points(self) -> np.ndarray:
+        """Copy of the grid points (numpy POINT_DTYPE)."""
+        n = int(self.number_of_points)
+        if n == 0:
+            return np.empty(0, dtype=POINT_DTYPE)
+        return np.frombuffer((C.c_char * (16 * n)).from_address(self.grid), dtype=POINT_DTYPE).copy()
+
+    def overflow(self) -> list:
+        """[(child index, None | numpy list in stored order)] (cell.rs:108-153 entries)."""
+        out = []
+        for e in range(int(self.entries)):
+            n = int(self.count[e])
+            lst = None if n == 0 else np.frombuffer((C.c_char * (16 * n)).from_address(self.list[e]),
+                                                    dtype=POINT_DTYPE).copy()
+            out.append((tuple(self.child[e]), lst))
+        return out
+
+
+CELL_VISITOR = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p)
 
 
 class PccError(RuntimeError):
@@ -121,6 +150,7 @@ def lib():
         L.pcc_write_metadata.argtypes = [vp]
         L.pcc_clear_input.argtypes = [vp]
         L.pcc_adopt_prior.argtypes = [vp, vp]
+        L.pcc_visit_cells.argtypes = [vp, CELL_VISITOR, vp]
         _lib = L
     return _lib
 
@@ -218,6 +248,23 @@ class Converter:
         (freshly opened) converter's existing cloud, as if it had been written to
         this converter's directory before opening it (lib.rs:86-101)."""
         _check(lib().pcc_adopt_prior(self._h, other._h))
+
+    def visit_cells(self, fn):
+        """Calls fn(view_ptr) for every built cell (pcc_visit_cells; the view is a
+        CellView valid during the call only: `CellView.from_address(view_ptr)`).
+        A nonzero return stops the walk and raises PccError with that code."""
+        err = []
+
+        def cb(view, _user):
+            try:
+                return int(fn(view) or 0)
+            except BaseException as e:   # never unwind through the C frames
+                err.append(e)
+                return -1
+        rc = lib().pcc_visit_cells(self._h, CELL_VISITOR(cb), None)
+        if err:
+            raise err[0]
+        _check(rc)
 
     def finish(self):
         """converter.rs:241-246 Drop: build if needed, write cells then metadata.json."""

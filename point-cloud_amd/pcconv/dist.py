@@ -192,7 +192,6 @@ class HipShardOps:
                  config: dict | None = None, merge: bool = False):
         self.dev = device_index
         self.cfg = dict(config or {})
-        self.max_cell_size = float(self.cfg.get("max_cell_size", 1000.0))
         self.batch_size = batch_size
         self.merge = merge
         self._tmp = None
@@ -200,12 +199,26 @@ class HipShardOps:
         if merge:   # the converter opens on the existing cloud once the owned subtrees are known
             if out_dir is None:
                 raise ValueError("a sharded merge needs the directory of the existing cloud")
+            # lib.rs:86-101: the existing metadata.json's config governs the merge;
+            # the shard grid must be the engine's level-0 grid, so a caller config
+            # that disagrees is an error rather than a silently split cell
+            disk = read_prior_meta(out_dir)["config"]
+            for k, v in self.cfg.items():
+                if k in disk and float(disk[k]) != float(v):
+                    raise ValueError(f"config {k}={v} differs from the existing cloud's {disk[k]}")
+            self.cfg = {k: disk[k] for k in ("cell_point_overflow_limit", "sub_grid_dimension", "max_cell_size")}
+            self.max_cell_size = float(self.cfg["max_cell_size"])
             self.out_dir = out_dir
             self.conv = None
             return
+        self.max_cell_size = float(self.cfg.get("max_cell_size", 1000.0))
         if out_dir is None:
             self._tmp = tempfile.TemporaryDirectory(prefix="pcc_shard_")
             out_dir = self._tmp.name
+        elif os.path.exists(os.path.join(out_dir, "metadata.json")) and read_prior_meta(out_dir)["number_of_points"] > 0:
+            # pcc_open would turn this into a merge on every rank (each loading and
+            # rewriting the whole existing cloud): refuse, merge=True is the way
+            raise ValueError(f"{out_dir} already holds a converted cloud; open it with merge=True")
         self.out_dir = out_dir
         self.conv = pcconv.Converter(out_dir, batch_size=batch_size, device=device_index, config=self.cfg)
 
@@ -290,7 +303,10 @@ def read_prior_meta(out_dir: str) -> dict:
         m = json.load(f)
     return {"number_of_points": int(m["number_of_points"]), "hierarchies": int(m["hierarchies"]),
             "bbox_min": [float(v) for v in m["bounding_box"]["min"]],
-            "bbox_max": [float(v) for v in m["bounding_box"]["max"]]}
+            "bbox_max": [float(v) for v in m["bounding_box"]["max"]],
+            "config": {"cell_point_overflow_limit": int(m["config"]["cell_point_overflow_limit"]),
+                       "sub_grid_dimension": int(m["config"]["sub_grid_dimension"]),
+                       "max_cell_size": float(m["config"]["max_cell_size"])}}
 
 
 def cell_triples(ids: np.ndarray, grid) -> np.ndarray:

@@ -2,7 +2,20 @@
  * q0 = RN(a*y), r = fma(-b, q0, a), q = fma(r, y, q0) must equal the IEEE
  * quotient RN(a/b) for operands in {0} U [2^-59, 2^60) and divisors in
  * [2^-60, 2^60] (the ranges the kernels keep to; others take IEEE division).
- * Usage: div_rc_check N [seed]  -> prints mismatches, exit 1 if any. */
+ * Usage: div_rc_check N [seed]  -> prints mismatches, exit 1 if any.
+ *        div_rc_check exhaustive    -> every numerator for the default config's divisors.
+ *
+ * Exhaustive mode.  The sequence is exactly scale invariant in the normal range
+ * (scaling a or b by 2^k scales y, q0, r and q by powers of two exactly, and the
+ * kernels keep every intermediate normal), so its result for a numerator depends
+ * only on the numerator's 23-bit mantissa and sign (symmetric).  Checking all
+ * 2^23 mantissas against each divisor mantissa therefore covers every f32
+ * numerator in range.  The divisors the slab kernels pass to div_rc are, per
+ * level h (engine.hip run_level, LevelGeo): r_h, r_h * S3, -r_h * S3 (hex.rs:69-70),
+ * the grandchild cell size 1000 / 2^(h+2), the grandchild radius r_{h+2}
+ * (metadata.rs:91-97, cell.rs:276-278) and 3 (hex.rs:76-78).  All levels'
+ * divisors are power-of-two scalings of those of level 0 (cell_size halves
+ * exactly), so five mantissas cover every level of the default config. */
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -27,7 +40,29 @@ static float div_rc(float a, float b, float y) {
     return fmaf(r, y, q0);
 }
 
+static int exhaustive(void) {
+    const float S3 = 1.73205080757f;                               /* hex.rs:3 */
+    const float cr = (1000.0f / 96.0f) / 2.0f;                     /* metadata.rs:96, cell.rs:277 */
+    const float div[5] = {cr, cr * S3, (-cr) * S3, 1000.0f, 3.0f};
+    long bad = 0;
+    for (int d = 0; d < 5; d++) {
+        const float b = div[d], y = 1.0f / b;
+        for (uint32_t m = 0; m < (1u << 23); m++) {
+            const float a = u2f((127u << 23) | m);               /* [1, 2) */
+            const float q = div_rc(a, b, y), e = a / b;
+            if (memcmp(&q, &e, 4) != 0) {
+                if (bad < 5) printf("mismatch a=%a b=%a q=%a ieee=%a\n", a, b, q, e);
+                bad++;
+            }
+        }
+        printf("divisor %a: %u numerator mantissas checked\n", b, 1u << 23);
+    }
+    printf("div_rc_check exhaustive mismatches=%ld\n", bad);
+    return bad ? 1 : 0;
+}
+
 int main(int argc, char** argv) {
+    if (argc > 1 && strcmp(argv[1], "exhaustive") == 0) return exhaustive();
     const long n = argc > 1 ? atol(argv[1]) : 10000000;
     if (argc > 2) st ^= (uint64_t)atoll(argv[2]) * 0x9E3779B97F4A7C15ull;
     long bad = 0;

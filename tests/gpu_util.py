@@ -43,6 +43,18 @@ def run_oracle(out_dir, files, cfg=None, batch=10_000):
     return err, arr
 
 
+def gpu_digest(conv) -> dict:
+    """Canonical per-subtree digests of a built converter's cells, walked in
+    memory through pcc_visit_cells (oracle/digest.c does the hashing)."""
+    from oracle_ctypes import Digest
+    d = Digest()
+    try:
+        conv.visit_cells(lambda view: d.add_view(view) or 0)
+        return d.result()
+    finally:
+        d.close()
+
+
 def compare_dirs(a, b, fast=True):
     if fast:
         ca, ma = canon.read_dir_fast(a)

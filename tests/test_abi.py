@@ -77,3 +77,10 @@ def test_open_fails_loudly_without_gpu(tmp_path):
         pcconv.Converter(str(tmp_path / "o"))
     assert e.value.code == -errno.ENODEV
     assert "no CPU fallback" in str(e.value)
+
+
+def test_cell_view_layout_matches_checker():
+    """pcc_cell_view as the Python mirror declares it == the digest checker's copy."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from oracle_ctypes import lib as olib
+    assert C.sizeof(pcconv.CellView) == olib().dg_view_size() == 256

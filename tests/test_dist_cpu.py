@@ -289,3 +289,23 @@ def test_gloo_world2_chunked_exchange_matches_oracle(tmp_path):
     files = make_input("files")
     assert r[0]["recv"] + r[1]["recv"] == sum(len(f) for f in files)
     check_against_oracle(tmp_path, files, out, r[0]["summary"])
+
+
+def test_hip_shard_ops_config_and_fresh_dir_guards(tmp_path):
+    """HipShardOps refuses (before any device work): a merge whose caller config
+    differs from the existing cloud's metadata.json, and a non-merge run into a
+    directory that already holds a cloud (pcc_open would merge on every rank)."""
+    import json
+    from pcconv.dist import HipShardOps
+    d = tmp_path / "cloud"
+    d.mkdir()
+    meta = {"version": "1.0", "name": "Unknown", "number_of_points": 10, "hierarchies": 1,
+            "bounding_box": {"min": [0.0, 0.0, 0.0], "max": [1.0, 1.0, 1.0]},
+            "config": {"cell_point_overflow_limit": 5000, "sub_grid_dimension": 96, "max_cell_size": 500.0}}
+    (d / "metadata.json").write_text(json.dumps(meta))
+    with pytest.raises(ValueError, match="max_cell_size"):
+        HipShardOps(0, out_dir=str(d), config=dict(max_cell_size=1000.0), merge=True)
+    ops = HipShardOps(0, out_dir=str(d), merge=True)   # no converter opened yet
+    assert ops.cfg["max_cell_size"] == 500.0 and ops.max_cell_size == 500.0
+    with pytest.raises(ValueError, match="merge=True"):
+        HipShardOps(0, out_dir=str(d))

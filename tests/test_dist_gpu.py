@@ -157,3 +157,15 @@ def test_sharded_merge_into_gpu_built_cloud_multilevel(tmp_path):
     res = _run_threads(new, 2, out, cfg=cfg, merge=True)
     assert res[0].summary["hierarchies"] >= 3
     check_against_oracle(tmp_path, old + new, out, res[0].summary, cfg=cfg)
+
+
+def test_sharded_merge_takes_config_from_existing_cloud(tmp_path):
+    """The existing cloud was built with a non-default config; the sharded merge
+    is opened WITHOUT a config and must use the one in its metadata.json
+    (lib.rs:86-101) for the shard grid and the engine alike."""
+    cfg = dict(sub_grid_dimension=24, cell_point_overflow_limit=300, max_cell_size=400.0)
+    old, new = [synth(35, 1, 400_000)], [synth(36, 0, 150_000)]
+    out = str(tmp_path / "out")
+    run_gpu(out, old, cfg=cfg)
+    res = _run_threads(new, 3, out, cfg=None, merge=True)
+    check_against_oracle(tmp_path, old + new, out, res[0].summary, cfg=cfg)

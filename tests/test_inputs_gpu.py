@@ -148,3 +148,120 @@ def test_metadata_json_as_input():
         o.close()
         d, mg, mo = compare_dirs(out, ref, fast=True)
         assert d == [] and mg == mo
+
+
+def _write_ply_props(path, cols, enc="binary_little_endian", count=None, drop_bytes=0):
+    """PLY with arbitrary vertex properties: cols = [(name, ply type, numpy array)].
+    `count` overrides the declared vertex count; `drop_bytes` cuts the file short."""
+    n = len(cols[0][2])
+    np_t = {"double": "f8", "float": "f4", "uchar": "u1", "ushort": "u2", "int": "i4"}
+    hdr = "ply\nformat %s 1.0\nelement vertex %d\n" % (enc, n if count is None else count)
+    hdr += "".join("property %s %s\n" % (t, nm) for nm, t, _ in cols) + "end_header\n"
+    with open(path, "wb") as f:
+        f.write(hdr.encode())
+        if enc == "ascii":
+            for i in range(n):
+                f.write((" ".join(repr(c[2][i].item()) for c in cols) + "\n").encode())
+        else:
+            bo = ">" if enc == "binary_big_endian" else "<"
+            dt = np.dtype([(nm, bo + np_t[t]) for nm, t, _ in cols])
+            rec = np.zeros(n, dtype=dt)
+            for nm, _, a in cols:
+                rec[nm] = a
+            data = rec.tobytes()
+            f.write(data[:len(data) - drop_bytes] if drop_bytes else data)
+
+
+def _ply_expect(cols):
+    """point.rs:61-130 restated: x/y/z Float or Double (`as f32`); red/green/blue/alpha
+    UChar, or Float as `(v / 255.0) as u8` (f32 division, saturating cast)."""
+    n = len(cols[0][2])
+    p = np.zeros(n, dtype=POINT_DTYPE)
+    p["rgba"][:, 3] = 255
+    for nm, t, a in cols:
+        if nm in ("x", "y", "z") and t in ("float", "double"):
+            p[nm] = np.asarray(a).astype(np.float32)
+        ch = {"red": 0, "green": 1, "blue": 2, "alpha": 3}.get(nm)
+        if ch is not None:
+            if t == "uchar":
+                p["rgba"][:, ch] = a
+            elif t == "float":
+                v = np.asarray(a, dtype=np.float32) / np.float32(255.0)
+                p["rgba"][:, ch] = np.nan_to_num(np.clip(v, 0, 255), nan=0.0).astype(np.uint8)
+    return p
+
+
+def _cli(files, out):
+    args = [_exe(), "-o", out]
+    for f in files:
+        args += ["-f", f]
+    r = subprocess.run(args, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    return r.stderr
+
+
+def _oracle_dir(path, files_pts, empty_batches=None):
+    o = Oracle()
+    for i, pts in enumerate(files_pts):
+        if empty_batches and i in empty_batches:
+            for _ in range(empty_batches[i]):
+                o.add_batch(pts[:0])
+        elif pts is not None:
+            o.add_file(pts)
+    o.write(path)
+    o.close()
+
+
+def test_ply_big_endian_double_coords_float_colours():
+    """PLY binary big-endian, double coordinates, float colours, an ignored extra
+    property (point.rs:61-130; ply.rs:54-61)."""
+    rng = np.random.default_rng(8)
+    n = 33_333
+    cols = [("x", "double", rng.uniform(-900, 900, n)), ("y", "double", rng.uniform(-900, 900, n)),
+            ("intensity", "ushort", rng.integers(0, 65535, n)), ("z", "double", rng.uniform(-900, 900, n)),
+            ("red", "float", rng.uniform(0, 70_000, n).astype(np.float32)),
+            ("green", "float", rng.uniform(-10, 300, n).astype(np.float32)),
+            ("blue", "uchar", rng.integers(0, 256, n)), ("alpha", "float", np.full(n, 255.0 * 100, np.float32))]
+    with tempfile.TemporaryDirectory() as td:
+        a = os.path.join(td, "be.ply")
+        _write_ply_props(a, cols, enc="binary_big_endian")
+        out, ref = os.path.join(td, "out"), os.path.join(td, "ref")
+        _cli([a], out)
+        _oracle_dir(ref, [_ply_expect(cols)])
+        d, mg, mo = compare_dirs(out, ref, fast=False)
+        assert d == [] and mg == mo
+
+
+def test_truncated_inputs_keep_complete_batches():
+    """lib.rs:31-52: a get_batch error is logged and ends its file; the batches read
+    before stay, the failing batch is lost, the next files are still converted.
+    PLY (binary LE, truncated mid-batch), ASCII PLY (short of lines: its complete
+    batches still count, ply.rs:43-51) and LAS (truncated point data)."""
+    rng = np.random.default_rng(9)
+    pts = synth(61, 0, 80_000)
+    cols = [("x", "float", pts["x"]), ("y", "float", pts["y"]), ("z", "float", pts["z"]),
+            ("red", "uchar", pts["rgba"][:, 0]), ("green", "uchar", pts["rgba"][:, 1]),
+            ("blue", "uchar", pts["rgba"][:, 2]), ("alpha", "uchar", pts["rgba"][:, 3])]
+    with tempfile.TemporaryDirectory() as td:
+        f1 = os.path.join(td, "a.ply")   # 35 000 declared, 23 456 records present -> 2 batches
+        _write_ply_props(f1, [(nm, t, a[:35_000]) for nm, t, a in cols], drop_bytes=16 * (35_000 - 23_456) + 5)
+        f2 = os.path.join(td, "b.ply")   # ASCII, 25 000 declared, 12 345 lines -> 1 empty batch
+        _write_ply_props(f2, [(nm, t, a[:12_345]) for nm, t, a in cols], enc="ascii", count=25_000)
+        n3 = 27_000                      # LAS, 27 000 declared, 26 001 present -> 2 batches
+        X = rng.integers(-100_000, 100_000, n3)
+        Y = rng.integers(-100_000, 100_000, n3)
+        Z = rng.integers(-100_000, 100_000, n3)
+        rgb = rng.integers(0, 65536, (n3, 3))
+        f3 = os.path.join(td, "c.las")
+        write_las(f3, X, Y, Z, (0.01, 0.01, 0.01), (0.0, 0.0, 0.0), fmt=3, rgb=rgb)
+        with open(f3, "r+b") as f:
+            f.truncate(227 + 34 * 26_001 + 7)
+        f4 = os.path.join(td, "d.ply")   # a complete file after the broken ones
+        _write_ply_props(f4, [(nm, t, a[40_000:]) for nm, t, a in cols])
+        out, ref = os.path.join(td, "out"), os.path.join(td, "ref")
+        log = _cli([f1, f2, f3, f4], out)
+        assert log.count("ERROR") == 3, log
+        las = decode(X, Y, Z, (0.01, 0.01, 0.01), (0.0, 0.0, 0.0), rgb)
+        _oracle_dir(ref, [pts[:20_000], pts[:0], las[:20_000], pts[40_000:]], empty_batches={1: 1})
+        d, mg, mo = compare_dirs(out, ref, fast=False)
+        assert d == [] and mg == mo

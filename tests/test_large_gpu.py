@@ -1,0 +1,136 @@
+"""Full-size parity of BASELINE configs 3, 4 and 5.
+
+The HIP build runs each configuration at its real size through the C ABI
+(synthetic input generated in HBM).  Its cells are walked in memory with
+pcc_visit_cells and digested canonically per level-0 subtree (oracle/digest.c,
+SURVEY.md Appendix B.3: headers bit-exact, grid multiset, overflow lists in
+stored order).  The digests must equal the C oracle's, committed in
+tests/golden/large_digests.json by tests/golden/make_large_digests.py.  Also
+checked, size-independently: W recomputed from the headers equals the
+build's arrival count, grid + kept points equal the input, and a repeated
+build gives the same digests."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from gpu_util import gpu_digest  # noqa: E402
+import pcconv  # noqa: E402
+from oracle_ctypes import synth  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+FIX_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "large_digests.json")
+
+
+def fixture(name):
+    with open(FIX_PATH) as f:
+        return json.load(f)[name]
+
+
+def _check(conv, st, fx, n_input):
+    d = gpu_digest(conv)
+    assert d["subtrees"] == fx["subtrees"]
+    assert sum(s["W"] for s in d["subtrees"]) == st["arrivals"] == fx["arrivals"]
+    assert d["grid_points"] + d["kept_points"] == n_input
+    assert (d["grid_points"], d["kept_points"]) == (fx["grid_points"], fx["kept_points"])
+    assert st["hierarchies"] == fx["hierarchies"]
+    bits = np.array(st["bbox_min"] + st["bbox_max"], dtype=np.float32).view(np.uint32).tolist()
+    assert bits == fx["bbox_bits"]
+    return d
+
+
+def test_config3_gaussian_mixture_100m():
+    fx = fixture("config3")
+    s = fx["synth"]
+    conv = pcconv.Converter("/tmp/pcc_cfg3")
+    try:
+        conv.add_synthetic(s["seed"], s["kind"], s["n"])
+        st = conv.build()
+        d1 = _check(conv, st, fx, s["n"])
+        st2 = conv.build()   # repeated build: identical
+        assert gpu_digest(conv) == d1 and st2["arrivals"] == st["arrivals"]
+    finally:
+        conv.close()
+
+
+def test_config4_uniform_1b():
+    fx = fixture("config4")
+    s = fx["synth"]
+    conv = pcconv.Converter("/tmp/pcc_cfg4")
+    try:
+        conv.add_synthetic(s["seed"], s["kind"], s["n"])
+        st = conv.build()
+        d1 = _check(conv, st, fx, s["n"])
+        conv.build()
+        assert gpu_digest(conv) == d1
+    finally:
+        conv.close()
+
+
+def test_config5_merge_100m_into_1b():
+    """+100M points merged into the 1B cloud (pcc_adopt_prior: the built 1B cloud
+    becomes the existing cloud, exactly as if written to disk and reopened)."""
+    fx = fixture("config5")
+    p, s = fx["prior_synth"], fx["synth"]
+    prior = pcconv.Converter("/tmp/pcc_cfg5_prior")
+    conv = pcconv.Converter("/tmp/pcc_cfg5")
+    try:
+        prior.add_synthetic(p["seed"], p["kind"], p["n"])
+        prior.build()
+        conv.adopt_prior(prior)
+        prior.close()
+        conv.add_synthetic(s["seed"], s["kind"], s["n"])
+        st = conv.build()
+        _check(conv, st, fx, p["n"] + s["n"])
+        assert st["number_of_points"] == p["n"] + s["n"]
+    finally:
+        prior.close()
+        conv.close()
+
+
+def test_config3_generator_device_equals_host():
+    """The kind-2 generator (Box-Muller mixture) gives the same bits on gfx950 and
+    in the oracle's independent restatement (the fixtures above rely on it)."""
+    import torch
+    n = 3_000_000
+    t = torch.empty((n, 4), dtype=torch.int32, device="cuda")
+    pcconv.synth_device(t.data_ptr(), 0, n, 3, 2, -1000.0, 2000.0, 0)
+    torch.cuda.synchronize()
+    dev = t.cpu().numpy().view(np.uint8).reshape(-1)
+    host = synth(3, 2, n).view(np.uint8).reshape(-1)
+    assert np.array_equal(dev, host)
+
+
+def test_visit_digest_equals_oracle_digest_small():
+    """The in-memory walk (pcc_visit_cells) and the oracle's own cells give equal
+    digests on a multi-level case, and the walk agrees with the written files."""
+    from gpu_util import compare_dirs, run_oracle
+    import tempfile
+    from oracle_ctypes import Digest, Oracle
+    pts = synth(33, 2, 1_500_000)
+    files = [pts[:700_001], pts[700_001:]]
+    with tempfile.TemporaryDirectory() as tg, tempfile.TemporaryDirectory() as to:
+        conv = pcconv.Converter(tg)
+        try:
+            for f in files:
+                conv.add_points(f)
+            conv.build()
+            dg = gpu_digest(conv)
+            conv.write()
+        finally:
+            conv.close()
+        o = Oracle()
+        for f in files:
+            o.add_file(f)
+        do = Digest()
+        do.add_oracle(o)
+        ref = do.result()
+        do.close()
+        o.close()
+        assert dg == ref
+        assert len(dg["subtrees"]) >= 8 and max(s["levels"] for s in dg["subtrees"]) >= 3
+        err, _ = run_oracle(to, files)
+        d, mg, mo = compare_dirs(tg, to)
+        assert err == 0 and d == [] and mg == mo
