@@ -37,15 +37,73 @@ def parse():
     ap.add_argument("--seed", type=int, default=4)
     ap.add_argument("--cpu-sample", type=int, default=20_000_000, help="oracle prefix sample (points); 0 = skip")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--cpu-full", action="store_true",
+                    help="cpu_baseline = mode (B) over the WHOLE workload, per level-0 part, summed (minutes of CPU)")
     ap.add_argument("--merge-prior", type=int, default=0,
                     help="config 5: merge --points new points (seed --seed) into a cloud built from this many "
                          "config-4 points (seed 4); 0 = fresh build")
     return ap.parse_args()
 
 
+def host_cpu():
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"nproc": os.cpu_count(), "model": model}
+
+
+def cpu_full_mode_b(args):
+    """SURVEY.md §8d mode (B), in-memory, FULL run: the sequential oracle converts
+    every level-0 subtree of the whole workload (oracle/digest_main.c, one process
+    per level-0 cell, global 10 000-point batches); only the conversion is timed
+    (the generator is not) and the single-thread times are summed, since level-0
+    subtrees are independent.  Minutes of CPU: not part of the default run."""
+    import subprocess
+    from concurrent.futures import ThreadPoolExecutor
+    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "build/orc_digest"])
+    exe = os.path.join(ROOT, "oracle", "build", "orc_digest")
+    streams = [str(args.seed), str(args.kind), str(args.points)]
+
+    def part(p):
+        out = subprocess.run([exe, str(p), "8"] + streams, capture_output=True, text=True, check=True).stdout
+        return [json.loads(x) for x in out.splitlines() if '"summary"' in x][-1]["convert_seconds"]
+    with ThreadPoolExecutor(min(8, os.cpu_count() or 1)) as ex:
+        secs = list(ex.map(part, range(8)))
+    tot = sum(secs)
+    return dict({"value": args.points / tot, "unit": "points/s", "cores": 1, "kind": "port",
+                 "sample": f"mode (B) full run: all {args.points} points, 8 level-0 parts converted separately "
+                           f"(sum of single-thread conversion times {tot:.1f} s; per part {[round(x, 1) for x in secs]})"},
+                **host_cpu())
+
+
 def cpu_baseline(args):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from oracle_ctypes import Oracle, synth
+    if args.kind == 0 and not args.merge_prior:
+        # Uniform workload: the points of the whole run that fall in one level-1
+        # cell, [0, 500)^3, at the run's density (N / 64 points).  A point's path
+        # (slot competition, bucket spills, 4 levels at N = 1e9) depends only on the
+        # points around it, so this keeps the full run's depth per point, unlike a
+        # prefix of the stream, which has fewer levels per point.
+        n = args.points // 64
+        pts = synth(args.seed, 0, n, lo=0.0, ext=500.0)
+        o = Oracle()
+        t0 = time.perf_counter()
+        o.add_file(pts)
+        dt = time.perf_counter() - t0
+        lv = o.hierarchies
+        o.close()
+        return dict({"value": n / dt, "unit": "points/s", "cores": 1, "kind": "port",
+                     "sample": f"{n} uniform points (seed {args.seed}) in the level-1 cell [0,500)^3 at the density of "
+                               f"the full {args.points}-point run ({lv} levels, as the full run), sequential C "
+                               f"restatement (oracle/pcc_oracle.c, in-memory cells = mode (B), 10 000-point "
+                               f"batches), {dt:.1f} s"}, **host_cpu())
     n = min(args.cpu_sample, args.points)
     pts = synth(args.seed, args.kind, n)
     o = Oracle()
@@ -56,13 +114,13 @@ def cpu_baseline(args):
     dt = time.perf_counter() - t0
     o.close()
     if args.merge_prior:
-        return {"value": n / dt, "unit": "points/s", "cores": 1, "kind": "port",
-                "sample": f"merge of the first {n} points of the seed-{args.seed} stream into an in-memory cloud of "
-                          f"the first {min(args.merge_prior, 5 * n)} config-4 points, sequential C restatement "
-                          f"(oracle/pcc_oracle.c, 10 000-point batches), {dt:.1f} s"}
-    return {"value": n / dt, "unit": "points/s", "cores": 1, "kind": "port",
-            "sample": f"first {n} points of the same seed-{args.seed} stream through the sequential C restatement "
-                      f"(oracle/pcc_oracle.c, in-memory cells, 10 000-point batches), {dt:.1f} s"}
+        return dict({"value": n / dt, "unit": "points/s", "cores": 1, "kind": "port",
+                     "sample": f"merge of the first {n} points of the seed-{args.seed} stream into an in-memory cloud "
+                               f"of the first {min(args.merge_prior, 5 * n)} config-4 points, sequential C restatement "
+                               f"(oracle/pcc_oracle.c, 10 000-point batches), {dt:.1f} s"}, **host_cpu())
+    return dict({"value": n / dt, "unit": "points/s", "cores": 1, "kind": "port",
+                 "sample": f"first {n} points of the same seed-{args.seed} stream through the sequential C restatement "
+                           f"(oracle/pcc_oracle.c, in-memory cells, 10 000-point batches), {dt:.1f} s"}, **host_cpu())
 
 
 METRIC = "points/sec converted (octree+LOD build), 1B synthetic pts, 1/2/4/8 MI355X"
@@ -216,7 +274,10 @@ def main():
     dense_ms = sum(p["dense_ms"] for p in prof) / len(prof)
     res = record(args, 1, ms, st["levels"], st["cells"], st["slabs"], st["arrivals"], prof[-1], dense_ms,
                  "single GPU")
-    if args.cpu_sample > 0:
+    if args.cpu_full:
+        res["cpu_baseline"] = cpu_full_mode_b(args)
+        res["speedup_vs_cpu"] = res["value"] / res["cpu_baseline"]["value"]
+    elif args.cpu_sample > 0:
         res["cpu_baseline"] = cpu_baseline(args)
         res["speedup_vs_cpu"] = res["value"] / res["cpu_baseline"]["value"]
     print(json.dumps(res), flush=True)

@@ -19,6 +19,7 @@
  */
 #include <inttypes.h>
 #include <math.h>
+#include <time.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -43,6 +44,13 @@ static int part_of(const pt* p, int parts) {   /* metadata.rs:100-102 at h = 0 (
     return ((ix & 1) | ((iy & 1) << 1) | ((iz & 1) << 2)) % parts;
 }
 
+static double now_s(void) {
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (double)t.tv_sec + 1e-9 * (double)t.tv_nsec;
+}
+static double g_convert_s = 0;   /* time inside orc_add_batch only (the generator is not timed) */
+
 static void report(orc_conv* c, int phase, const float bb[6], uint64_t npts) {
     dg_acc* acc = dg_new();
     orc_digest(c, acc);
@@ -60,8 +68,9 @@ static void report(orc_conv* c, int phase, const float bb[6], uint64_t npts) {
     uint32_t b[6];
     memcpy(b, bb, sizeof b);
     printf("{\"phase\": %d, \"summary\": true, \"input_points\": %" PRIu64 ", \"arrivals\": %" PRIu64
-           ", \"grid_points\": %" PRIu64 ", \"kept_points\": %" PRIu64 ", \"error\": %d, \"bbox_bits\": [%u, %u, %u, %u, %u, %u]}\n",
-           phase, npts, orc_arrivals(c), t[0], t[1], orc_error(c), b[0], b[1], b[2], b[3], b[4], b[5]);
+           ", \"grid_points\": %" PRIu64 ", \"kept_points\": %" PRIu64 ", \"error\": %d, \"bbox_bits\": [%u, %u, %u, %u, %u, %u]"
+           ", \"convert_seconds\": %.3f}\n",
+           phase, npts, orc_arrivals(c), t[0], t[1], orc_error(c), b[0], b[1], b[2], b[3], b[4], b[5], g_convert_s);
     fflush(stdout);
     dg_free(acc);
 }
@@ -93,7 +102,9 @@ int main(int argc, char** argv) {
                 for (int a = 0; a < 3; a++) { bb[a] = fminf(bb[a], v[a]); bb[3 + a] = fmaxf(bb[3 + a], v[a]); }
                 if (part_of(&buf[i], parts) == part) sel[k++] = buf[i];
             }
+            const double t0 = now_s();
             orc_add_batch(c, sel, k);
+            g_convert_s += now_s() - t0;
         }
         total += n;
         report(c, s + 1, bb, total);

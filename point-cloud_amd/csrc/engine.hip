@@ -509,13 +509,17 @@ __device__ __forceinline__ int64_t l0_layer(const L0Params& P, float z, int32_t&
     const int32_t t = sat_i32(z / P.cr);   // hex.rs:83 z slot (truncation)
     return (int64_t)t - ((int64_t)P.dim2 * iz - 2);
 }
+// HASHED: -1 = decided by P.hashed at run time, 0 / 1 = known at compile time
+// (the pipelined downsweep must not carry the hash probe loop: its waits would
+// drain the prefetched tile)
+template <int HASHED = -1>
 __device__ __forceinline__ int64_t l0_dense(const L0Params& P, float x, float y, float z) {
     int32_t iz;
     const int64_t ll = l0_layer(P, z, iz);
     int32_t ix = cell_index1(x, P.cs), iy = cell_index1(y, P.cs);
     int32_t gx = ix - P.lo[0], gy = iy - P.lo[1], gz = iz - P.lo[2];
     if (gx < 0 || gy < 0 || gz < 0 || gx >= P.g[0] || gy >= P.g[1] || gz >= P.g[2] || ll < 0 || ll >= P.nl) return -1;
-    if (P.hashed) {
+    if (HASHED == 1 || (HASHED == -1 && P.hashed)) {
         const unsigned long long key = l0_pack(gx, gy, gz);
         uint32_t h = l0_hash(key) & P.hmask;
         for (uint32_t probe = 0; probe <= P.hmask; probe++) {
@@ -571,6 +575,7 @@ __global__ void k_l0_hash_ids(const unsigned long long* hkeys, uint32_t cap, uin
 #endif
 constexpr int kL0BS = PCC_L0BS, kL0IPT = PCC_L0IPT, kL0Tile = kL0BS * kL0IPT, kL0W = kL0BS / 64;
 constexpr int kHistLds = 8192;
+constexpr uint32_t kL0DownGrid = 512;   // persistent blocks of the fused upsweep (2 per CU)
 
 // Pass-0 upsweep from the AoS input, fused with the bounding box
 // (converter.rs:96-104, bounding-volume/src/lib.rs:38-52): per-tile histogram of
@@ -667,6 +672,111 @@ __global__ __launch_bounds__(kL0BS) void k_l0_up_hist(Arena A, uint64_t n, L0Par
     if (lds)
         for (uint32_t i = threadIdx.x; i < D; i += kL0BS)
             if (h[i]) atomicAdd(&hist[i], h[i]);
+}
+
+// Pass-1 upsweep fused with the level-0 capacities (replaces k_dcap when the
+// level-1 grid is small): per point the LEVEL-1 slab (cell index at h = 1,
+// metadata.rs:100-102, and hex layer hex.rs:83) is counted in an LDS histogram.
+// Its level-0 slab follows exactly (cell_size and the hex radius halve exactly,
+// metadata.rs:92,96, so x / cs0 = RN(x / cs1) / 2: ix0 = ix1 >> 1, t0 = u1 / 2),
+// so the per-tile digit counts come from the same 4 divisions, and every
+// level-0 slab's 24 capacities are level-1 histogram bins (k_l0_dcap_from1).
+constexpr int kHist1Lds = 16384;   // level-1 dense slabs held in LDS (64 KB)
+struct L1Grid { int32_t lo[3], g[3]; };
+__device__ __forceinline__ int64_t l1_dense(const L0Params& P, const L1Grid& Q, float x, float y, float z, int64_t& d0) {
+    // IEEE divisions (exact reciprocal quotients measured slower here: 5.1 vs 4.2 ms)
+    const int32_t ix1 = cell_index1(x, P.csc), iy1 = cell_index1(y, P.csc), iz1 = cell_index1(z, P.csc);
+    const int32_t u1 = sat_i32(z / P.crc);
+    const int32_t gx1 = ix1 - Q.lo[0], gy1 = iy1 - Q.lo[1], gz1 = iz1 - Q.lo[2];
+    const int64_t ll1 = (int64_t)u1 - ((int64_t)P.dim2 * iz1 - 2);
+    // level 0 from level 1: floor halves (arithmetic shift), the layer truncates (u1 / 2)
+    const int32_t gx0 = (ix1 >> 1) - P.lo[0], gy0 = (iy1 >> 1) - P.lo[1], iz0 = iz1 >> 1, gz0 = iz0 - P.lo[2];
+    const int64_t ll0 = (int64_t)(u1 / 2) - ((int64_t)P.dim2 * iz0 - 2);
+    const bool ok1 = gx1 >= 0 && gy1 >= 0 && gz1 >= 0 && gx1 < Q.g[0] && gy1 < Q.g[1] && gz1 < Q.g[2] && ll1 >= 0 &&
+                     ll1 < (int64_t)kL0Layers;
+    const bool ok0 = gx0 >= 0 && gy0 >= 0 && gz0 >= 0 && gx0 < P.g[0] && gy0 < P.g[1] && gz0 < P.g[2] && ll0 >= 0 &&
+                     ll0 < P.nl;
+    d0 = ok0 ? (((int64_t)gz0 * P.g[1] + gy0) * P.g[0] + gx0) * kL0Layers + ll0 : -1;
+    return ok1 ? (((int64_t)gz1 * Q.g[1] + gy1) * Q.g[0] + gx1) * kL0Layers + ll1 : -1;
+}
+
+template <int BITS>
+__global__ __launch_bounds__(kL0BS) void k_l0_up_hist1(Arena A, uint64_t n, L0Params P, L1Grid Q, int shift,
+                                                       uint32_t* __restrict__ counts, uint32_t ntiles,
+                                                       uint32_t* hist1, uint32_t D1, Counters* ctr) {
+    constexpr int R = 1 << BITS;
+    __shared__ uint32_t dh[R];
+    __shared__ uint32_t h[kHist1Lds];
+    for (uint32_t i = threadIdx.x; i < D1; i += kL0BS) h[i] = 0;
+    uint32_t err = 0;
+    for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        for (int i = threadIdx.x; i < R; i += kL0BS) dh[i] = 0;
+        __syncthreads();
+        const uint64_t base = (uint64_t)tile * kL0Tile;
+        float4 v[kL0IPT];
+#pragma unroll
+        for (int r = 0; r < kL0IPT; r++) {
+            const uint64_t i = base + (uint64_t)r * kL0BS + threadIdx.x;
+            if (i < n) v[r] = A.p[i];
+        }
+#pragma unroll
+        for (int r = 0; r < kL0IPT; r++) {
+            const uint64_t i = base + (uint64_t)r * kL0BS + threadIdx.x;
+            if (i < n) {
+                int64_t d0;
+                const int64_t d1 = l1_dense(P, Q, v[r].x, v[r].y, v[r].z, d0);
+                if (d1 < 0 || d0 < 0) { err = ERR_L0_RANGE; continue; }
+                atomicAdd(&dh[((uint64_t)d0 >> shift) & (R - 1)], 1u);
+                atomicAdd(&h[d1], 1u);
+            }
+        }
+        __syncthreads();
+        for (int d = threadIdx.x; d < R; d += kL0BS) counts[(uint64_t)d * ntiles + tile] = dh[d];
+    }
+    if (err) set_err(ctr, err);
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < D1; i += kL0BS)
+        if (h[i]) atomicAdd(&hist1[i], h[i]);
+}
+
+// level-0 dense histogram from the level-1 one (each level-1 slab has exactly one parent slab)
+__global__ void k_l0_hist_from1(const uint32_t* __restrict__ hist1, uint32_t D1, L0Params P, L1Grid Q,
+                                uint32_t* __restrict__ hist) {
+    const uint32_t d1 = blockIdx.x * blockDim.x + threadIdx.x;
+    if (d1 >= D1 || !hist1[d1]) return;
+    const uint32_t c1 = d1 / kL0Layers, ll1 = d1 % kL0Layers;
+    const int32_t gx1 = (int32_t)(c1 % (uint32_t)Q.g[0]), gy1 = (int32_t)((c1 / (uint32_t)Q.g[0]) % (uint32_t)Q.g[1]);
+    const int32_t gz1 = (int32_t)(c1 / ((uint32_t)Q.g[0] * (uint32_t)Q.g[1]));
+    const int32_t iz1 = Q.lo[2] + gz1, iz0 = iz1 >> 1;
+    const int32_t u1 = (int32_t)ll1 + (P.dim2 * iz1 - 2);
+    const int32_t ll0 = u1 / 2 - (P.dim2 * iz0 - 2);
+    const uint64_t d0 = (((uint64_t)(iz0 - P.lo[2]) * P.g[1] + (uint32_t)(((Q.lo[1] + gy1) >> 1) - P.lo[1])) * P.g[0] +
+                         (uint32_t)(((Q.lo[0] + gx1) >> 1) - P.lo[0])) * kL0Layers + (uint32_t)ll0;
+    atomicAdd(&hist[d0], hist1[d1]);
+}
+
+// capacities of the level-0 slabs: arrivals per child slab (octant, layer select)
+// = the level-1 histogram bin of that child slab
+__global__ void k_l0_dcap_from1(const uint32_t* __restrict__ hist1, L0Params P, L1Grid Q, const int32_t* cell_idx,
+                                const uint32_t* slab_cell, const int32_t* slab_layer, uint32_t nslabs, uint32_t* dcap) {
+    const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i >= (uint64_t)nslabs * kDests) return;
+    const uint32_t s = (uint32_t)(i / kDests), dest = (uint32_t)(i % kDests), o = dest / 3, sel = dest % 3;
+    const uint32_t c = slab_cell[s];
+    const int32_t t = slab_layer[s];
+    const int32_t cx = 2 * cell_idx[3 * c] + (int32_t)(o & 1), cy = 2 * cell_idx[3 * c + 1] + (int32_t)((o >> 1) & 1);
+    const int32_t cz = 2 * cell_idx[3 * c + 2] + (int32_t)((o >> 2) & 1);
+    const int32_t u = 2 * t - 1 + (int32_t)sel;
+    const int64_t ll1 = (int64_t)u - ((int64_t)P.dim2 * cz - 2);
+    uint32_t v = 0;
+    // a child layer has ONE parent layer, u / 2 (C division): sel 0 exists only for
+    // t <= 0 and sel 2 only for t >= 0, so (t, 2) and (t + 1, 0) never both count u
+    if (u / 2 == t && ll1 >= 0 && ll1 < (int64_t)kL0Layers) {
+        const uint64_t d1 = (((uint64_t)(cz - Q.lo[2]) * Q.g[1] + (uint32_t)(cy - Q.lo[1])) * Q.g[0] + (uint32_t)(cx - Q.lo[0])) *
+                                kL0Layers + (uint64_t)ll1;
+        v = hist1[d1];
+    }
+    dcap[i] = v;
 }
 
 // later-pass upsweep from a SoA arena
@@ -2663,16 +2773,22 @@ int Engine::build() {
     return 0;
 }
 
+// H1: the level-1 histogram of the fused capacities (nullptr: plain level-0 histogram)
 template <int BITS>
 static void l0_pass(int p, int passes, Arena src, Arena dst, uint64_t n, const L0Params& P, int shift,
-                    uint32_t* counts, uint32_t ntiles, uint32_t* hist, uint32_t D, Counters* ctr, const uint32_t* files,
-                    uint32_t nfiles, ScanTemp& scan, hipStream_t st) {
+                    uint32_t* counts, uint32_t ntiles, uint32_t* hist, uint32_t D, Counters* ctr, const L1Grid& Q,
+                    uint32_t* H1, uint32_t D1, ScanTemp& scan, hipStream_t st) {
     const uint64_t nc = (uint64_t)ntiles << BITS;
-    if (p == 0) k_l0_up_hist<BITS><<<std::min<uint32_t>(ntiles, 2048), kL0BS, 0, st>>>(src, n, P, shift, counts, ntiles, hist, D, ctr);
-    else k_l0_up<BITS><<<ntiles, kL0BS, 0, st>>>(src, n, P, shift, counts, ntiles);
+    if (p == 0 && H1) {
+        k_l0_up_hist1<BITS><<<std::min<uint32_t>(ntiles, kL0DownGrid), kL0BS, 0, st>>>(src, n, P, Q, shift, counts, ntiles, H1, D1, ctr);
+        k_l0_hist_from1<<<grid_for(D1, 256, 1u << 30), 256, 0, st>>>(H1, D1, P, Q, hist);
+    } else if (p == 0) {
+        k_l0_up_hist<BITS><<<std::min<uint32_t>(ntiles, 2048), kL0BS, 0, st>>>(src, n, P, shift, counts, ntiles, hist, D, ctr);
+    } else {
+        k_l0_up<BITS><<<ntiles, kL0BS, 0, st>>>(src, n, P, shift, counts, ntiles);
+    }
     scan_excl_u32(counts, counts, (uint32_t)nc, nullptr, scan, st);
-    if (p == passes - 1) k_l0_down<BITS, false, true><<<ntiles, kL0BS, 0, st>>>(nullptr, nullptr, src, dst, n, P, shift, counts, ntiles, files, nfiles);
-    else k_l0_down<BITS, false, false><<<ntiles, kL0BS, 0, st>>>(nullptr, nullptr, src, dst, n, P, shift, counts, ntiles, files, nfiles);
+    k_l0_down<BITS, false, false><<<ntiles, kL0BS, 0, st>>>(nullptr, nullptr, src, dst, n, P, shift, counts, ntiles, nullptr, 0);
     HIP_CHECK(hipGetLastError());
 }
 
@@ -2763,6 +2879,17 @@ int Engine::level0_bin() {
     uint32_t* cscan = static_cast<uint32_t*>(dev_->get(G * 4));
     uint32_t* d_tot = static_cast<uint32_t*>(dev_->get(16));
     HIP_CHECK(hipMemsetAsync(hist, 0, D * 4, stream_));
+    // capacities fused into the pass-1 upsweep when the level-1 slab grid fits LDS
+    L1Grid Q;
+    for (int a = 0; a < 3; a++) { Q.lo[a] = 2 * P.lo[a]; Q.g[a] = 2 * P.g[a]; }
+    const uint64_t D1w = 8ull * G * kL0Layers;
+    const bool fuse_dcap = !P.hashed && D1w <= (uint64_t)kHist1Lds && getenv("PCC_NO_FUSED_DCAP") == nullptr;
+    const uint32_t D1 = fuse_dcap ? (uint32_t)D1w : 0u;
+    uint32_t* H1 = nullptr;
+    if (fuse_dcap) {
+        H1 = static_cast<uint32_t*>(dev_->get((uint64_t)D1 * 4));
+        HIP_CHECK(hipMemsetAsync(H1, 0, (uint64_t)D1 * 4, stream_));
+    }
     // LSD passes over the dense slab id (key recomputed from positions every
     // pass): pass 0 on the low 6 layer bits (upsweep done above), then the rest
     // of the layer and the cell bits in passes of at most 8 bits; the first of
@@ -2777,21 +2904,21 @@ int Engine::level0_bin() {
     // the final pass must land in arena 0
     Arena dst = (passes % 2) ? A1 : A0;
     scan_excl_u32(counts0, counts0, (uint32_t)((uint64_t)ntiles << 6), nullptr, dev_->scan, stream_);
-    k_l0_down<6, true, false><<<ntiles, kL0BS, 0, stream_>>>(src_, src_keys_, A1, dst, nsrc_, P, 0,
-                                                              counts0, ntiles, dev_->files, nfiles_dev_);
+    k_l0_down<6, true, false><<<ntiles, kL0BS, 0, stream_>>>(src_, src_keys_, A1, dst, nsrc_, P, 0, counts0, ntiles,
+                                                              nullptr, 0);
     HIP_CHECK(hipGetLastError());
     Arena src = dst;
     dst = (dst.p == A0.p) ? A1 : A0;
     for (int p = 0, shift = 6; p < passes; p++, shift += per) {
         switch (per) {
-            case 1: l0_pass<1>(p, passes, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, nfiles_dev_, dev_->scan, stream_); break;
-            case 2: l0_pass<2>(p, passes, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, nfiles_dev_, dev_->scan, stream_); break;
-            case 3: l0_pass<3>(p, passes, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, nfiles_dev_, dev_->scan, stream_); break;
-            case 4: l0_pass<4>(p, passes, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, nfiles_dev_, dev_->scan, stream_); break;
-            case 5: l0_pass<5>(p, passes, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, nfiles_dev_, dev_->scan, stream_); break;
-            case 6: l0_pass<6>(p, passes, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, nfiles_dev_, dev_->scan, stream_); break;
-            case 7: l0_pass<7>(p, passes, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, nfiles_dev_, dev_->scan, stream_); break;
-            default: l0_pass<8>(p, passes, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, dev_->files, nfiles_dev_, dev_->scan, stream_); break;
+            case 1: l0_pass<1>(p, passes, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, Q, H1, D1, dev_->scan, stream_); break;
+            case 2: l0_pass<2>(p, passes, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, Q, H1, D1, dev_->scan, stream_); break;
+            case 3: l0_pass<3>(p, passes, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, Q, H1, D1, dev_->scan, stream_); break;
+            case 4: l0_pass<4>(p, passes, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, Q, H1, D1, dev_->scan, stream_); break;
+            case 5: l0_pass<5>(p, passes, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, Q, H1, D1, dev_->scan, stream_); break;
+            case 6: l0_pass<6>(p, passes, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, Q, H1, D1, dev_->scan, stream_); break;
+            case 7: l0_pass<7>(p, passes, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, Q, H1, D1, dev_->scan, stream_); break;
+            default: l0_pass<8>(p, passes, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, Q, H1, D1, dev_->scan, stream_); break;
         }
         src = dst;
         dst = (dst.p == A0.p) ? A1 : A0;
@@ -2835,7 +2962,13 @@ int Engine::level0_bin() {
         HIP_CHECK(hipMemcpyAsync(&hc, dev_->ctr, sizeof hc, hipMemcpyDeviceToHost, stream_));
         HIP_CHECK(hipStreamSynchronize(stream_));
         L->max_slab = hc.max_slab;
-        run_dcap(L);
+        if (fuse_dcap) {
+            const uint64_t nd = (uint64_t)L->nslabs * kDests;
+            k_l0_dcap_from1<<<grid_for(nd, 256, 1u << 30), 256, 0, stream_>>>(H1, P, Q, L->cell_idx, L->slab_cell,
+                                                                              L->slab_layer, L->nslabs, L->dcap);
+        } else {
+            run_dcap(L);
+        }
     }
     HIP_CHECK(hipGetLastError());
     ev_end(ST_L0);
@@ -2903,8 +3036,12 @@ int Engine::run_level(uint32_t h) {
     // per-level counters
     {
         Counters hc;
+        uint32_t cap_total = 0;   // sum of the child-slab capacities: the next arena must hold them
         HIP_CHECK(hipMemcpyAsync(&hc, dev_->ctr, sizeof hc, hipMemcpyDeviceToHost, stream_));
+        HIP_CHECK(hipMemcpyAsync(&cap_total, scratch, 4, hipMemcpyDeviceToHost, stream_));
         HIP_CHECK(hipStreamSynchronize(stream_));
+        if (cap_total > dev_->cap)
+            return fail(-5, "internal error: child-slab capacities exceed the arena (level " + std::to_string(h) + ")");
         hc.kept_cur = 0;
         hc.nbig = hc.nsmall = 0;
         hc.max_slab = 0;

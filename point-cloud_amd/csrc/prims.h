@@ -72,6 +72,30 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* lds /*
     return r;
 }
 
+// Same with LDS-only barriers (global loads issued before stay in flight).
+template <int BS>
+__device__ __forceinline__ uint32_t block_excl_scan_lds(uint32_t v, uint32_t* lds /* BS/64 + 1 */, uint32_t* total) {
+    const uint32_t lane = lane_id(), w = threadIdx.x / kWave;
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+        uint32_t y = __shfl_up(x, d, kWave);
+        if (lane >= (uint32_t)d) x += y;
+    }
+    if (lane == kWave - 1) lds[w] = x;
+    lds_barrier();
+    if (threadIdx.x == 0) {
+        uint32_t acc = 0;
+        for (int i = 0; i < BS / kWave; i++) { uint32_t t = lds[i]; lds[i] = acc; acc += t; }
+        lds[BS / kWave] = acc;
+    }
+    lds_barrier();
+    uint32_t r = lds[w] + x - v;
+    *total = lds[BS / kWave];
+    lds_barrier();
+    return r;
+}
+
 template <int BS>
 __device__ __forceinline__ uint32_t block_sum(uint32_t v, uint32_t* lds) {
     uint32_t t;

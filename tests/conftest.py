@@ -9,3 +9,15 @@ sys.path.insert(0, os.path.join(HERE, "..", "oracle"))
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (runs through the HIP C-ABI)")
     config.addinivalue_line("markers", "slow: long-running")
+
+
+def pytest_sessionstart(session):
+    """Initialise torch's HIP runtime before libpcconv's (torch bundles its own
+    libamdhip64; initialised second, after libpcconv has used the device, it can
+    report no GPUs).  No-op without a GPU."""
+    try:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.init()
+    except Exception:
+        pass

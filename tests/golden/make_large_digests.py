@@ -45,7 +45,7 @@ def run_part(streams, part):
 
 
 def combine(lines, phase):
-    subs = sorted((ln for ln in lines if ln["phase"] == phase and "subtree" in ln), key=lambda d: d["subtree"])
+    subs = sorted((dict(ln) for ln in lines if ln["phase"] == phase and "subtree" in ln), key=lambda d: d["subtree"])
     sums = [ln for ln in lines if ln["phase"] == phase and ln.get("summary")]
     bb = {tuple(s["bbox_bits"]) for s in sums}
     assert len(bb) == 1, "parts disagree on the bounding box"
@@ -76,6 +76,8 @@ def main():
             continue
         with ThreadPoolExecutor(a.jobs) as ex:
             lines = [ln for part in ex.map(lambda p: run_part(cfg["streams"], p), range(PARTS)) for ln in part]
+        with open(os.path.join("/tmp", f"large_digests_{name}.jsonl"), "w") as f:   # raw lines, for re-combining
+            f.write("".join(json.dumps(ln) + "\n" for ln in lines))
         s0 = cfg["streams"][0]
         res[name] = dict(combine(lines, 1), synth=s0)
         if len(cfg["streams"]) > 1:
