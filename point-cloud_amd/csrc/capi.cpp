@@ -14,6 +14,7 @@
 #include <sstream>
 #include <thread>
 #include <string>
+#include <array>
 
 #include "../../include/pcconv.h"
 #include "engine.h"
@@ -67,7 +68,56 @@ struct pcc_converter {
     double build_ms = 0;
     bool merge = false;         // out_dir held a non-empty cloud: incremental merge
     Metadata prior;             // its metadata.json
+    // merge: the existing cloud's cells.  Only cells touched by new points are
+    // rebuilt; the others stay as they are (converter.rs:160-207 loads a cell
+    // only when a batch reaches it), so they are output from here.
+    std::vector<CellFile> prior_cells;
+    bool prior_on_disk = false;         // they are the files in out_dir (nothing to rewrite)
+    std::vector<uint8_t> prior_touched; // per prior cell, after a build
+    uint64_t untouched_grid = 0, untouched_kept = 0, untouched_cells = 0;
 };
+
+namespace {
+// pcc_cell_view of an existing cloud's cell as read from disk (header values
+// recomputed exactly as Cell::new / Header::new do, cell.rs:43-49, 264-274)
+void file_cell_view(const Config& cfg, const CellFile& f, pcc_cell_view& v) {
+    v.hierarchy = f.h;
+    v.x = f.idx[0]; v.y = f.idx[1]; v.z = f.idx[2];
+    v.total_number_of_points = f.total;
+    v.number_of_points = f.number;
+    v.number_of_overflow_points = f.overflow;
+    v.size = cell_size(cfg.max_cell_size, f.h);
+    v.sub_cell_size = sub_cell_size(v.size, cfg.sub_grid_dimension);
+    v.pos[0] = cell_pos1(f.idx[0], v.size); v.pos[1] = cell_pos1(f.idx[1], v.size); v.pos[2] = cell_pos1(f.idx[2], v.size);
+    v.grid = reinterpret_cast<const pcc_point*>(f.grid.data());
+    v.entries = (uint32_t)f.entries.size();
+    for (uint32_t e = 0; e < v.entries; e++) {
+        for (int a = 0; a < 3; a++) v.child[e][a] = f.entries[e].child[a];
+        v.count[e] = f.entries[e].some ? (uint32_t)f.entries[e].pts.size() : 0u;
+        v.list[e] = f.entries[e].some ? reinterpret_cast<const pcc_point*>(f.entries[e].pts.data()) : nullptr;
+    }
+}
+// the merge's untouched existing cells after a build (touched = rebuilt)
+void mark_touched(pcc_converter* c) {
+    c->prior_touched.assign(c->prior_cells.size(), 0);
+    c->untouched_grid = c->untouched_kept = c->untouched_cells = 0;
+    std::vector<int32_t> hxyz;
+    c->eng->built_cells(hxyz);
+    std::vector<std::array<int32_t, 4>> built;
+    for (size_t i = 0; i + 3 < hxyz.size(); i += 4) built.push_back({hxyz[i], hxyz[i + 1], hxyz[i + 2], hxyz[i + 3]});
+    std::sort(built.begin(), built.end());
+    for (size_t i = 0; i < c->prior_cells.size(); i++) {
+        const CellFile& f = c->prior_cells[i];
+        const std::array<int32_t, 4> k{(int32_t)f.h, f.idx[0], f.idx[1], f.idx[2]};
+        c->prior_touched[i] = std::binary_search(built.begin(), built.end(), k) ? 1 : 0;
+        if (!c->prior_touched[i]) {
+            c->untouched_cells++;
+            c->untouched_grid += f.number;
+            c->untouched_kept += f.overflow;
+        }
+    }
+}
+}  // namespace
 
 #define GUARD_BEGIN try {
 #define GUARD_END                                            \
@@ -127,14 +177,14 @@ static int open_impl(const char* out_dir, const pcc_options* opt, const std::vec
     if (c->opt.device < 0 || c->opt.device >= ndev) return set_err(-ENODEV, "invalid HIP device ordinal");
     c->eng = std::make_unique<Engine>(c->meta.config, c->opt.device);
     if (c->merge) {   // converter.rs:187-207: existing cells are the starting state
-        std::vector<CellFile> cells;
         std::string err;
-        int rc = read_cloud(c->out_dir, c->prior.hierarchies, cells, err, subtrees);
+        int rc = read_cloud(c->out_dir, c->prior.hierarchies, c->prior_cells, err, subtrees);
         if (rc) return set_err(rc, err);
         PriorState ps;
-        rc = prior_from_cells(cells, c->meta.config, ps, err);
+        rc = prior_from_cells(c->prior_cells, c->meta.config, ps, err);
         if (rc) return set_err(rc, err);
         c->eng->set_prior(ps);
+        c->prior_on_disk = true;
     }
     *out = c.release();
     return 0;
@@ -202,6 +252,7 @@ int pcc_build(pcc_converter* c) {
     c->build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     if (rc) return set_err(rc, c->eng->last_error());
     c->built = true;
+    if (c->merge) mark_touched(c);
     if (c->summary_set) return 0;
     Metadata& m = c->meta;   // converter.rs:96-112 + 141-145
     m.number_of_points = c->eng->num_points();
@@ -270,6 +321,10 @@ static int write_impl(pcc_converter* c, bool with_metadata) {
     if (verbose) fprintf(stderr, "[pcc] write: last level's files %.1f ms after the last download\n", ms(tj, clk::now()));
     if (rc) return set_err(rc, c->eng->last_error());
     if (wrc) return set_err(wrc, werr);
+    if (c->merge && !c->prior_on_disk) {   // adopted cloud: its untouched cells are not on disk here
+        rc = write_cell_files(c->out_dir, c->meta.config, c->prior_cells, &c->prior_touched, err);
+        if (rc) return set_err(rc, err);
+    }
     if (with_metadata) {
         rc = write_metadata(c->out_dir, c->meta, err);
         if (rc) return set_err(rc, err);
@@ -297,6 +352,12 @@ int pcc_visit_cells(pcc_converter* c, pcc_cell_visitor fn, void* user) {
             const int r = fn(&v, user);
             if (r) return r;
         }
+    }
+    for (size_t i = 0; i < c->prior_cells.size(); i++) {   // merge: the existing cells no new point reached
+        if (i < c->prior_touched.size() && c->prior_touched[i]) continue;
+        file_cell_view(c->meta.config, c->prior_cells[i], v);
+        const int r = fn(&v, user);
+        if (r) return r;
     }
     return 0;
     GUARD_END
@@ -444,6 +505,8 @@ int pcc_adopt_prior(pcc_converter* dst, pcc_converter* src) {
     int rc = src->eng->download(levels, grid, kept);
     if (rc) return set_err(rc, src->eng->last_error());
     std::vector<CellFile> cells;
+    for (size_t i = 0; i < src->prior_cells.size(); i++)   // src is itself a merge: its untouched cells
+        if (i >= src->prior_touched.size() || !src->prior_touched[i]) cells.push_back(src->prior_cells[i]);
     for (const LevelHost& L : levels) {   // cell.rs:155-181 contents without the file round trip
         const uint32_t ncells = (uint32_t)(L.cell_idx.size() / 3);
         for (uint32_t c = 0; c < ncells; c++) {
@@ -476,6 +539,8 @@ int pcc_adopt_prior(pcc_converter* dst, pcc_converter* src) {
     dst->eng->set_prior(ps);
     dst->merge = true;
     dst->prior = src->meta;
+    dst->prior_cells = std::move(cells);
+    dst->prior_on_disk = false;
     return 0;
     GUARD_END
 }
@@ -506,8 +571,9 @@ int pcc_get_stats(const pcc_converter* c, pcc_stats* s) {
     s->cells = b.cells;
     s->slabs = b.slabs;
     s->arrivals = b.arrivals;
-    s->grid_points = b.grid_points;
-    s->kept_points = b.kept_points;
+    s->grid_points = b.grid_points + c->untouched_grid;   // merge: + the existing cells left as they are
+    s->kept_points = b.kept_points + c->untouched_kept;
+    s->cells += c->untouched_cells;
     s->build_ms = c->build_ms;
     for (int a = 0; a < 3; a++) { s->bbox_min[a] = c->meta.bmin[a]; s->bbox_max[a] = c->meta.bmax[a]; }
     return 0;

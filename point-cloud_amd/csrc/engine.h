@@ -54,20 +54,45 @@ struct HostPoints {
 };
 
 // Existing cloud loaded for an incremental merge (lib.rs:86-101 +
-// converter.rs:187-207).  Seeds are ALL its points in
-// key order: per level h, first the grid points of every level-h cell, then the
-// points of every kept (Some) list in stored order.  A seed enters the build at
-// level 0 like any input point; at levels above its own it is a forced
-// emission (it passes through None buckets down to its cell), at its own level
-// a grid seed takes its slot (it precedes every new point, so it wins every
-// tie) and a kept seed is a forced emission into its bucket, ahead of the new
-// emissions.  forced_lo[h] = first key of level h's kept seeds: at level h every
-// key in [forced_lo[h], S) is forced.
+// converter.rs:187-207).  Its points are "seeds" with
+// keys below every new point's (keys 0 .. S-1, a pseudo batch 0): per level h,
+// first the grid points of every level-h cell, then the points of every kept
+// (Some) list in stored order; forced_lo[h] = first key of level h's kept seeds.
+//
+// Only TOUCHED cells are rebuilt (cells that receive new arrivals; the
+// reference loads a cell only when a batch touches it, converter.rs:160-207):
+//   * level-0 seeds enter the level-0 binning ahead of the new points (seeds0,
+//     key order);
+//   * a level-h >= 1 seed is injected straight into its own slab: the parent
+//     level reserves room in front of each child slab's emission region
+//     (child_seed counts), and when the child cell is created (its bucket is
+//     None and receives new emissions) its seeds are copied there;
+//   * at its own level a grid seed takes its slot first (it precedes every new
+//     point, so it wins every tie), and a kept seed (key >= forced_lo[h]) is a
+//     forced emission into its bucket, ahead of the new emissions;
+//   * untouched cells stay exactly as they were (the caller keeps them).
+// A level-h slab with seeds always has its parent slab at level h-1: its
+// points passed that layer, and the first arrival of a slab always takes a slot.
 struct PriorCell { int32_t x, y, z; uint32_t st; };   // st: 2 bits per octant: 0 absent, 1 Some, 2 None
+constexpr uint32_t kNoPriorSlab = 0xFFFFFFFFu;
+struct PriorSlabRec {                                  // one (cell, hex layer) of the existing cloud
+    uint32_t seed_off, nseed;                          // level >= 1: its seeds in PriorState::inj
+    uint32_t child[24];                                // its child slabs' records at level h+1 (kNoPriorSlab: none)
+    uint32_t dcap[24];                                 // its seeds per child slab (their capacities)
+};
+struct PriorLevel {
+    std::vector<PriorCell> cells;                      // sorted by (x, y, z)
+    std::vector<uint32_t> cell_slab0;                  // ncells + 1: each cell's records, ascending layer
+    std::vector<int32_t> slab_layer;
+    std::vector<PriorSlabRec> slabs;
+};
 struct PriorState {
-    std::vector<Point> seeds;
-    std::vector<uint64_t> forced_lo;                 // per prior level
-    std::vector<std::vector<PriorCell>> cells;       // per prior level, sorted by (x, y, z)
+    uint64_t nseeds = 0;                               // S: every existing point
+    std::vector<Point> seeds0;                         // level-0 seeds, key order (keys 0 .. seeds0.size()-1)
+    std::vector<Point> inj;                            // levels >= 1, grouped by level, cell, slab: grid then kept
+    std::vector<uint32_t> inj_keys;
+    std::vector<uint64_t> forced_lo;                   // per prior level
+    std::vector<PriorLevel> levels;
 };
 
 struct StageProfile {
@@ -121,6 +146,8 @@ public:
     // one level (grid winners compacted on the device); H's bases are 0
     int download_level(uint32_t i, LevelHost& H, HostPoints& grid, HostPoints& kept);
     uint32_t num_levels() const;
+    // (h, x, y, z) of every cell the last build produced (merge: the touched cells)
+    int built_cells(std::vector<int32_t>& hxyz);
 
     uint64_t num_points() const { return n_; }
     uint32_t num_batches() const { return nbatches_; }
@@ -147,6 +174,7 @@ private:
     int run_level(uint32_t h);
     void run_dcap(Level* L);
     void free_all();
+    void free_prior();
 
     Config cfg_;
     int device_;
@@ -164,8 +192,19 @@ private:
     uint64_t nsrc_ = 0;
     uint32_t nfiles_dev_ = 0;            // entries of the device file table
     bool prior_ = false;
-    Point* d_seeds_ = nullptr;
-    uint64_t nseeds_ = 0;
+    Point* d_seeds_ = nullptr;           // level-0 seeds (key order)
+    uint64_t nseeds0_ = 0;
+    uint64_t nseeds_ = 0;                // S (all levels)
+    Point* d_inj_ = nullptr;             // level >= 1 seeds, grouped by slab
+    uint32_t* d_inj_keys_ = nullptr;
+    struct PriorDev {                    // one prior level on the device
+        PriorCell* cells = nullptr;
+        uint32_t* cell_slab0 = nullptr;
+        int32_t* slab_layer = nullptr;
+        PriorSlabRec* slabs = nullptr;
+        uint32_t ncells = 0, nslabs = 0;
+    };
+    std::vector<PriorDev> pdev_;
     Point* d_comb_ = nullptr;
     uint64_t comb_cap_ = 0;
     uint32_t* d_ckeys_ = nullptr;        // merge of keyed input: seed keys 0..S-1, then S + key
@@ -173,8 +212,6 @@ private:
     const uint32_t* src_keys_ = nullptr; // keys of src_ (nullptr: key = index)
     bool comb_ok_ = false;
     std::vector<uint64_t> forced_lo_;
-    std::vector<uint32_t*> d_prior_cells_;   // PriorCell arrays per level
-    std::vector<uint32_t> n_prior_cells_;
     uint64_t keys_cap_ = 0;
     bool keyed_ = false;
     uint64_t declared_total_ = 0;        // keyed input: global points of the declared files

@@ -159,6 +159,8 @@ struct Engine::Level {
     uint32_t* bkt_n = nullptr;
     uint32_t* bkt_sb = nullptr;
     uint32_t* bkt_nd = nullptr;
+    uint32_t* slab_prior = nullptr;  // merge: the existing cloud's record of each slab (kNoPriorSlab: none)
+    uint32_t* room = nullptr;        // merge: 24 per slab, seeds injected in front of each child slab's emissions
     template <class T>
     void alloc(T*& p, uint64_t n) { p = static_cast<T*>(dev->get(n * sizeof(T))); }
 };
@@ -2085,6 +2087,7 @@ struct BucketParams {
     uint32_t* bkt_n;
     uint32_t* bkt_sb;
     uint32_t* bkt_nd;
+    const uint32_t* room;     // merge: seeds injected into each child slab (a child slab exists if it has any)
     Counters* ctr;
     uint32_t L;
 };
@@ -2128,10 +2131,10 @@ __global__ __launch_bounds__(kBktBS) void k_bucket(BucketParams B) {
     for (uint32_t i = threadIdx.x; i < nd; i += kBktBS) {
         const uint32_t di = (s0 + i / 3) * kDests + oct * 3 + i % 3;
         const uint32_t n = B.dest_n[di];
+        nne += (n || (B.room && B.room[di])) ? 1u : 0u;   // slabs of the child cell, if it is built
         if (n) {
             const uint32_t o = B.dest_off[di];
             tot += n;
-            nne++;
             emin = min(emin, emission_eb(B, B.nx.k[o], csb));
             emax = max(emax, emission_eb(B, B.nx.k[o + n - 1], csb));
         }
@@ -2318,6 +2321,13 @@ struct NextParams {
     uint32_t* ndcap;
     uint32_t* nbig_list;
     uint32_t* nsmall_list;
+    // merge (nullptr otherwise): records of this level's slabs, the reserved seed
+    // room per child slab, the existing cloud's slab records at this level and the next
+    const uint32_t* slab_prior;
+    const uint32_t* room;
+    const PriorSlabRec* prec;
+    const PriorSlabRec* prec_next;
+    uint32_t* nslab_prior;
     Counters* ctr;
 };
 
@@ -2349,7 +2359,7 @@ __global__ __launch_bounds__(256) void k_next_emit(NextParams Q) {
     // pass 1: count big / small slabs of this cell (one global atomic per block)
     for (uint32_t i = threadIdx.x; i < nd; i += 256) {
         const uint32_t di = (s0 + i / 3) * kDests + oct * 3 + i % 3;
-        const uint32_t n = Q.dest_n[di];
+        const uint32_t n = Q.dest_n[di] + (Q.room ? Q.room[di] : 0u);   // + injected seeds
         if (n) {
             atomicAdd(n >= kSmallMax ? &s_big : &s_small, 1u);
             atomicAdd(&s_arr, (unsigned long long)n);
@@ -2371,10 +2381,11 @@ __global__ __launch_bounds__(256) void k_next_emit(NextParams Q) {
     __syncthreads();
     for (uint32_t i0 = 0; i0 < nd; i0 += 256) {
         const uint32_t i = i0 + threadIdx.x;
-        uint32_t n = 0, di = 0;
+        uint32_t n = 0, di = 0, rm = 0;
         if (i < nd) {
             di = (s0 + i / 3) * kDests + oct * 3 + i % 3;
-            n = Q.dest_n[di];
+            rm = Q.room ? Q.room[di] : 0u;
+            n = Q.dest_n[di] + rm;
         }
         uint32_t tot;
         const uint32_t ex = block_excl_scan<256>(n ? 1u : 0u, lds, &tot);
@@ -2383,10 +2394,17 @@ __global__ __launch_bounds__(256) void k_next_emit(NextParams Q) {
             const int32_t t = Q.slab_layer[s0 + i / 3];
             Q.nslab_cell[sid] = r;
             Q.nslab_layer[sid] = 2 * t + (int32_t)(i % 3) - 1;
-            Q.nslab_off[sid] = Q.dest_off[di];
+            Q.nslab_off[sid] = Q.dest_off[di] - rm;   // the seeds are copied in front of the emissions
             Q.nslab_n[sid] = n;
             const uint32_t* g = Q.gcap + (uint64_t)di * kDests;
-            for (int q = 0; q < kDests; q++) Q.ndcap[(uint64_t)sid * kDests + q] = g[q];
+            uint32_t pr = kNoPriorSlab;
+            if (Q.nslab_prior) {
+                const uint32_t ps = Q.slab_prior[s0 + i / 3];
+                pr = (rm && ps != kNoPriorSlab) ? Q.prec[ps].child[oct * 3 + i % 3] : kNoPriorSlab;
+                Q.nslab_prior[sid] = pr;
+            }
+            const uint32_t* sd = pr != kNoPriorSlab ? Q.prec_next[pr].dcap : nullptr;
+            for (int q = 0; q < kDests; q++) Q.ndcap[(uint64_t)sid * kDests + q] = g[q] + (sd ? sd[q] : 0u);
             if (n >= kSmallMax) Q.nbig_list[s_bigbase + atomicAdd(&s_big, 1u)] = sid;
             else Q.nsmall_list[s_smallbase + atomicAdd(&s_small, 1u)] = sid;
         }
@@ -2427,10 +2445,71 @@ __global__ __launch_bounds__(256) void k_l0_lists(const uint32_t* slab_n, uint32
 
 __global__ void k_set_u32(uint32_t* p, uint32_t v) { *p = v; }
 
-// keys of a merged keyed input: seeds 0..S-1, then S + the new points' global keys
-__global__ void k_comb_keys(uint32_t* out, const uint32_t* keys, uint64_t S, uint64_t n) {
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < S + n; i += (uint64_t)gridDim.x * blockDim.x)
-        out[i] = i < S ? (uint32_t)i : (uint32_t)(S + keys[i - S]);
+// merge: the existing cloud's record of each level-0 slab (cell by binary search
+// over the sorted prior cells, then the layer inside the cell's records)
+__global__ void k_prior_lookup0(const int32_t* cell_idx, const uint32_t* slab_cell, const int32_t* slab_layer,
+                                uint32_t nslabs, const PriorCell* pc, const uint32_t* pc_slab0, const int32_t* p_layer,
+                                uint32_t npc, uint32_t* slab_prior) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= nslabs) return;
+    const uint32_t c = slab_cell[s];
+    const int32_t x = cell_idx[3 * c], y = cell_idx[3 * c + 1], z = cell_idx[3 * c + 2], t = slab_layer[s];
+    uint32_t lo = 0, hi = npc;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        const PriorCell& q = pc[mid];
+        const bool less = q.x != x ? q.x < x : (q.y != y ? q.y < y : q.z < z);
+        if (less) lo = mid + 1; else hi = mid;
+    }
+    uint32_t r = kNoPriorSlab;
+    if (lo < npc && pc[lo].x == x && pc[lo].y == y && pc[lo].z == z) {
+        uint32_t a = pc_slab0[lo], b = pc_slab0[lo + 1];
+        while (a < b) {
+            const uint32_t mid = (a + b) >> 1;
+            if (p_layer[mid] < t) a = mid + 1; else b = mid;
+        }
+        if (a < pc_slab0[lo + 1] && p_layer[a] == t) r = a;
+    }
+    slab_prior[s] = r;
+}
+
+// merge: seeds reserved in front of each child slab (room) and the scan input
+// (capacity + room) of the emission regions
+__global__ void k_room(const uint32_t* slab_prior, uint32_t nslabs, const PriorSlabRec* prec,
+                       const PriorSlabRec* prec_next, const uint32_t* dcap, uint32_t* room, uint32_t* cap_room) {
+    const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i >= (uint64_t)nslabs * kDests) return;
+    const uint32_t ps = slab_prior[i / kDests];
+    const uint32_t ch = ps != kNoPriorSlab ? prec[ps].child[i % kDests] : kNoPriorSlab;
+    const uint32_t r = ch != kNoPriorSlab ? prec_next[ch].nseed : 0u;
+    room[i] = r;
+    cap_room[i] = dcap[i] + r;
+}
+// dest_off = (exclusive scan of capacity + room) + room: the emissions follow the seeds
+__global__ void k_add_room(uint32_t* dest_off, const uint32_t* room, uint64_t n) {
+    const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i < n) dest_off[i] += room[i];
+}
+// merge: copy each new slab's seeds (points and keys) in front of its emissions
+__global__ __launch_bounds__(256) void k_inject_seeds(const uint32_t* slab_prior, const uint32_t* slab_off, uint32_t nslabs,
+                                                      const PriorSlabRec* prec, const float4* __restrict__ inj,
+                                                      const uint32_t* __restrict__ inj_keys, Arena A) {
+    for (uint32_t s = blockIdx.x; s < nslabs; s += gridDim.x) {
+        const uint32_t pr = slab_prior[s];
+        if (pr == kNoPriorSlab) continue;
+        const uint32_t so = prec[pr].seed_off, n = prec[pr].nseed, o = slab_off[s];
+        for (uint32_t j = threadIdx.x; j < n; j += 256) {
+            A.p[(uint64_t)o + j] = inj[(uint64_t)so + j];
+            A.k[(uint64_t)o + j] = inj_keys[(uint64_t)so + j];
+        }
+    }
+}
+
+// keys of a merge's level-0 input: the level-0 seeds 0 .. n0-1, then S + each new
+// point's key (its index, or its global key for sharded input)
+__global__ void k_comb_keys(uint32_t* out, const uint32_t* keys, uint64_t n0, uint64_t S, uint64_t n) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n0 + n; i += (uint64_t)gridDim.x * blockDim.x)
+        out[i] = i < n0 ? (uint32_t)i : (uint32_t)(S + (keys ? (uint64_t)keys[i - n0] : i - n0));
 }
 
 // ------------------------------------------------------------------ host side
@@ -2522,15 +2601,25 @@ void Engine::free_all() {
     (void)hipFree(d_keys_);
     d_keys_ = nullptr;
     keys_cap_ = 0;
-    (void)hipFree(d_seeds_);
-    d_seeds_ = nullptr;
     (void)hipFree(d_comb_);
     d_comb_ = nullptr;
     (void)hipFree(d_ckeys_);
     d_ckeys_ = nullptr;
     ckeys_cap_ = 0;
-    for (uint32_t* q : d_prior_cells_) (void)hipFree(q);
-    d_prior_cells_.clear();
+    free_prior();
+}
+
+void Engine::free_prior() {
+    (void)hipFree(d_seeds_);
+    d_seeds_ = nullptr;
+    (void)hipFree(d_inj_);
+    d_inj_ = nullptr;
+    (void)hipFree(d_inj_keys_);
+    d_inj_keys_ = nullptr;
+    for (PriorDev& d : pdev_) {
+        (void)hipFree(d.cells); (void)hipFree(d.cell_slab0); (void)hipFree(d.slab_layer); (void)hipFree(d.slabs);
+    }
+    pdev_.clear();
 }
 
 int Engine::fail(int code, const std::string& msg) {
@@ -2623,26 +2712,32 @@ void Engine::add_keyed_device(const Point* dpts, const uint32_t* dkeys, uint64_t
     comb_ok_ = false;
 }
 
+template <class T>
+static T* upload(const std::vector<T>& v) {
+    T* d = nullptr;
+    HIP_CHECK(hipMalloc(&d, std::max<size_t>(v.size(), 1) * sizeof(T)));
+    if (!v.empty()) HIP_CHECK(hipMemcpy(d, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    return d;
+}
+
 void Engine::set_prior(const PriorState& p) {
     HIP_CHECK(hipStreamSynchronize(stream_));
-    for (uint32_t* q : d_prior_cells_) (void)hipFree(q);
-    d_prior_cells_.clear();
-    n_prior_cells_.clear();
-    (void)hipFree(d_seeds_);
-    d_seeds_ = nullptr;
-    nseeds_ = p.seeds.size();
-    if (nseeds_) {
-        HIP_CHECK(hipMalloc(&d_seeds_, nseeds_ * sizeof(Point)));
-        HIP_CHECK(hipMemcpy(d_seeds_, p.seeds.data(), nseeds_ * sizeof(Point), hipMemcpyHostToDevice));
-    }
+    free_prior();
+    nseeds_ = p.nseeds;
+    nseeds0_ = p.seeds0.size();
+    d_seeds_ = upload(p.seeds0);
+    d_inj_ = upload(p.inj);
+    d_inj_keys_ = upload(p.inj_keys);
     forced_lo_ = p.forced_lo;
-    for (const auto& lv : p.cells) {
-        uint32_t* d = nullptr;
-        const size_t bytes = std::max<size_t>(lv.size(), 1) * sizeof(PriorCell);
-        HIP_CHECK(hipMalloc(&d, bytes));
-        if (!lv.empty()) HIP_CHECK(hipMemcpy(d, lv.data(), lv.size() * sizeof(PriorCell), hipMemcpyHostToDevice));
-        d_prior_cells_.push_back(d);
-        n_prior_cells_.push_back((uint32_t)lv.size());
+    for (const PriorLevel& lv : p.levels) {
+        PriorDev d;
+        d.cells = upload(lv.cells);
+        d.cell_slab0 = upload(lv.cell_slab0);
+        d.slab_layer = upload(lv.slab_layer);
+        d.slabs = upload(lv.slabs);
+        d.ncells = (uint32_t)lv.cells.size();
+        d.nslabs = (uint32_t)lv.slabs.size();
+        pdev_.push_back(d);
     }
     prior_ = true;
     comb_ok_ = false;
@@ -2685,44 +2780,46 @@ int Engine::build() {
     // S + i.  All seeds belong to a pseudo batch 0 before the new batches.
     if (prior_ && keyed_ && nseeds_ + declared_total_ >= 0xFFFFFFFFull)   // keys S + global key (k_comb_keys)
         return fail(-75, "sharded merge: this rank's existing points plus the global new points exceed 2^32-1 keys");
-    if (prior_) {
+    if (prior_) {   // level-0 input: the level-0 seeds (keys 0 .. n0-1), then the new points (S + key)
+        const uint64_t n0 = nseeds0_;
         if (!comb_ok_) {
-            if (comb_cap_ < nseeds_ + n_) {
+            if (comb_cap_ < n0 + n_) {
                 (void)hipFree(d_comb_);
-                HIP_CHECK(hipMalloc(&d_comb_, (nseeds_ + n_) * sizeof(Point)));
-                comb_cap_ = nseeds_ + n_;
+                HIP_CHECK(hipMalloc(&d_comb_, std::max<uint64_t>(n0 + n_, 1) * sizeof(Point)));
+                comb_cap_ = n0 + n_;
             }
-            if (nseeds_) HIP_CHECK(hipMemcpyAsync(d_comb_, d_seeds_, nseeds_ * sizeof(Point), hipMemcpyDeviceToDevice, stream_));
-            HIP_CHECK(hipMemcpyAsync(d_comb_ + nseeds_, d_in_, n_ * sizeof(Point), hipMemcpyDeviceToDevice, stream_));
-            if (keyed_) {   // sharded merge: this rank's seeds, then its new points with S + global key
-                if (ckeys_cap_ < nseeds_ + n_) {
-                    (void)hipFree(d_ckeys_);
-                    HIP_CHECK(hipMalloc(&d_ckeys_, (nseeds_ + n_) * 4));
-                    ckeys_cap_ = nseeds_ + n_;
-                }
-                k_comb_keys<<<grid_for(nseeds_ + n_, 256), 256, 0, stream_>>>(d_ckeys_, d_keys_, nseeds_, n_);
-                HIP_CHECK(hipGetLastError());
+            if (n0) HIP_CHECK(hipMemcpyAsync(d_comb_, d_seeds_, n0 * sizeof(Point), hipMemcpyDeviceToDevice, stream_));
+            HIP_CHECK(hipMemcpyAsync(d_comb_ + n0, d_in_, n_ * sizeof(Point), hipMemcpyDeviceToDevice, stream_));
+            if (ckeys_cap_ < n0 + n_) {
+                (void)hipFree(d_ckeys_);
+                HIP_CHECK(hipMalloc(&d_ckeys_, std::max<uint64_t>(n0 + n_, 1) * 4));
+                ckeys_cap_ = n0 + n_;
             }
+            k_comb_keys<<<grid_for(n0 + n_, 256), 256, 0, stream_>>>(d_ckeys_, keyed_ ? d_keys_ : nullptr, n0, nseeds_, n_);
+            HIP_CHECK(hipGetLastError());
             comb_ok_ = true;
         }
         src_ = d_comb_;
-        src_keys_ = keyed_ ? d_ckeys_ : nullptr;
-        nsrc_ = nseeds_ + n_;
+        src_keys_ = d_ckeys_;
+        nsrc_ = n0 + n_;
     } else {
         src_ = d_in_;
         src_keys_ = keyed_ ? d_keys_ : nullptr;
         nsrc_ = n_;
     }
-    if (nsrc_ >= 0xFFFFFFFFull) return fail(-75, "more than 2^32-1 points (existing + new) per build are not supported");
+    if ((prior_ ? nseeds_ : 0) + n_ >= 0xFFFFFFFFull)
+        return fail(-75, "more than 2^32-1 points (existing + new) per build are not supported");
 
-    // arenas: SoA, N entries each (ping-pong between levels)
-    if (dev_->cap < nsrc_) {
+    // arenas: SoA, ping-pong between levels.  A merge's levels also hold the
+    // injected seeds of the touched cells (at most every existing point).
+    const uint64_t acap = prior_ ? nseeds_ + n_ : nsrc_;
+    if (dev_->cap < acap) {
         for (int a = 0; a < 2; a++) {
             Arena& A = dev_->ar[a];
             (void)hipFree(A.p); (void)hipFree(A.k);
-            HIP_CHECK(hipMalloc(&A.p, nsrc_ * 16)); HIP_CHECK(hipMalloc(&A.k, nsrc_ * 4));
+            HIP_CHECK(hipMalloc(&A.p, acap * 16)); HIP_CHECK(hipMalloc(&A.k, acap * 4));
         }
-        dev_->cap = nsrc_;
+        dev_->cap = acap;
     }
     // file table for event batches
     {
@@ -2957,6 +3054,12 @@ int Engine::level0_bin() {
         hist, cnt_scan, sflag, cflag, cscan, (uint32_t)D, (uint32_t)G, P, L->cell_idx, L->cell_sb, L->cell_slab0,
         L->slab_cell, L->slab_layer, L->slab_off, L->slab_n);
     k_set_u32<<<1, 1, 0, stream_>>>(L->cell_slab0 + L->ncells, L->nslabs);
+    if (prior_ && !pdev_.empty() && L->nslabs) {   // merge: each level-0 slab's record in the existing cloud
+        L->alloc(L->slab_prior, L->nslabs);
+        k_prior_lookup0<<<grid_for(L->nslabs, 256, 1u << 30), 256, 0, stream_>>>(
+            L->cell_idx, L->slab_cell, L->slab_layer, L->nslabs, pdev_[0].cells, pdev_[0].cell_slab0, pdev_[0].slab_layer,
+            pdev_[0].ncells, L->slab_prior);
+    }
     k_l0_lists<<<grid_for(L->nslabs, 256, 1u << 30), 256, 0, stream_>>>(L->slab_n, L->nslabs, L->big_list, L->small_list, dev_->ctr);
     {
         HIP_CHECK(hipMemcpyAsync(&hc, dev_->ctr, sizeof hc, hipMemcpyDeviceToHost, stream_));
@@ -3030,8 +3133,20 @@ int Engine::run_level(uint32_t h) {
     L->kept_cap = std::min<uint64_t>(L->arrivals, 8ull * L->ncells * cfg_.cell_point_overflow_limit);
     L->alloc(L->kept, L->kept_cap);
     uint32_t* scratch = static_cast<uint32_t*>(dev_->get(16));
-    // output regions from exclusive scans (no allocation atomics in the slab kernels)
-    scan_excl_u32(L->dcap, L->dest_off, (uint32_t)ND, scratch, dev_->scan, stream_);
+    // output regions from exclusive scans (no allocation atomics in the slab kernels).
+    // Merge: each child slab's region starts with room for its injected seeds.
+    const bool inject = prior_ && L->slab_prior && h + 1 < pdev_.size();
+    if (inject) {
+        L->alloc(L->room, ND);
+        uint32_t* capr = static_cast<uint32_t*>(dev_->get(ND * 4));
+        k_room<<<grid_for(ND, 256, 1u << 30), 256, 0, stream_>>>(L->slab_prior, L->nslabs, pdev_[h].slabs,
+                                                                 pdev_[h + 1].slabs, L->dcap, L->room, capr);
+        scan_excl_u32(capr, L->dest_off, (uint32_t)ND, scratch, dev_->scan, stream_);
+        k_add_room<<<grid_for(ND, 256, 1u << 30), 256, 0, stream_>>>(L->dest_off, L->room, ND);
+        HIP_CHECK(hipGetLastError());
+    } else {
+        scan_excl_u32(L->dcap, L->dest_off, (uint32_t)ND, scratch, dev_->scan, stream_);
+    }
     scan_excl_u32(L->slab_n, L->grid_off, L->nslabs, scratch + 1, dev_->scan, stream_);
     // per-level counters
     {
@@ -3169,8 +3284,8 @@ int Engine::run_level(uint32_t h) {
     BP.nfiles = nfiles_dev_;
     BP.cell_sb = L->cell_sb;
     BP.cell_idx = L->cell_idx;
-    BP.prior = (prior_ && h < d_prior_cells_.size()) ? reinterpret_cast<const PriorCell*>(d_prior_cells_[h]) : nullptr;
-    BP.nprior = (prior_ && h < n_prior_cells_.size()) ? n_prior_cells_[h] : 0u;
+    BP.prior = (prior_ && h < pdev_.size()) ? pdev_[h].cells : nullptr;
+    BP.nprior = (prior_ && h < pdev_.size()) ? pdev_[h].ncells : 0u;
     BP.kept = L->kept;
     BP.kept_cap = L->kept_cap;
     BP.cell_slab0 = L->cell_slab0;
@@ -3181,6 +3296,7 @@ int Engine::run_level(uint32_t h) {
     BP.bkt_n = L->bkt_n;
     BP.bkt_sb = L->bkt_sb;
     BP.bkt_nd = L->bkt_nd;
+    BP.room = inject ? L->room : nullptr;
     BP.ctr = dev_->ctr;
     BP.L = cfg_.cell_point_overflow_limit;
     const uint32_t nb = 8 * L->ncells;
@@ -3272,10 +3388,20 @@ int Engine::run_level(uint32_t h) {
         Q.nslab_n = N->slab_n;
         Q.nbig_list = N->big_list;
         Q.nsmall_list = N->small_list;
+        Q.slab_prior = inject ? L->slab_prior : nullptr;
+        Q.room = inject ? L->room : nullptr;
+        Q.prec = inject ? pdev_[h].slabs : nullptr;
+        Q.prec_next = inject ? pdev_[h + 1].slabs : nullptr;
+        if (inject) N->alloc(N->slab_prior, N->nslabs);
+        Q.nslab_prior = inject ? N->slab_prior : nullptr;
         Q.ctr = dev_->ctr;
         ev_begin(ST_NEXT);
         k_next_emit<<<nb, 256, 0, stream_>>>(Q);
         k_set_u32<<<1, 1, 0, stream_>>>(N->cell_slab0 + N->ncells, N->nslabs);
+        if (inject && N->nslabs)   // the touched cells' seeds of level h+1, in front of their emissions
+            k_inject_seeds<<<std::min<uint32_t>(N->nslabs, 65536), 256, 0, stream_>>>(
+                N->slab_prior, N->slab_off, N->nslabs, pdev_[h + 1].slabs, reinterpret_cast<const float4*>(d_inj_),
+                d_inj_keys_, dev_->ar[N->arena]);
         ev_end(ST_NEXT);
         HIP_CHECK(hipGetLastError());
         HIP_CHECK(hipMemcpyAsync(&hc, dev_->ctr, sizeof hc, hipMemcpyDeviceToHost, stream_));
@@ -3305,6 +3431,20 @@ __global__ __launch_bounds__(256) void k_compact_grid(const Point* __restrict__ 
 }
 
 uint32_t Engine::num_levels() const { return (uint32_t)levels_.size(); }
+
+int Engine::built_cells(std::vector<int32_t>& hxyz) {
+    hxyz.clear();
+    for (Level* L : levels_) {
+        std::vector<int32_t> idx(3ull * L->ncells);
+        if (!idx.empty()) HIP_CHECK(hipMemcpyAsync(idx.data(), L->cell_idx, idx.size() * 4, hipMemcpyDeviceToHost, stream_));
+        HIP_CHECK(hipStreamSynchronize(stream_));
+        for (uint32_t c = 0; c < L->ncells; c++) {
+            hxyz.push_back((int32_t)L->h);
+            hxyz.insert(hxyz.end(), idx.begin() + 3ull * c, idx.begin() + 3ull * c + 3);
+        }
+    }
+    return 0;
+}
 
 HostPoints::~HostPoints() {
     if (p) munmap(p, cap * sizeof(Point));

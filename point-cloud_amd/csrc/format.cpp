@@ -304,6 +304,40 @@ int write_level_cells(const std::string& dir, const Config& cfg, const LevelHost
     return rc.load();
 }
 
+int write_cell_files(const std::string& dir, const Config& cfg, const std::vector<CellFile>& cells,
+                     const std::vector<uint8_t>* skip, std::string& err) {
+    std::string buf;
+    for (size_t i = 0; i < cells.size(); i++) {
+        if (skip && i < skip->size() && (*skip)[i]) continue;
+        const CellFile& f = cells[i];
+        const float size = cell_size(cfg.max_cell_size, f.h);
+        buf.clear();
+        put32(buf, f.h);
+        put32(buf, (uint32_t)f.idx[0]); put32(buf, (uint32_t)f.idx[1]); put32(buf, (uint32_t)f.idx[2]);
+        put32(buf, f.total); put32(buf, f.number); put32(buf, f.overflow);
+        putf(buf, size);
+        putf(buf, sub_cell_size(size, cfg.sub_grid_dimension));
+        putf(buf, cell_pos1(f.idx[0], size)); putf(buf, cell_pos1(f.idx[1], size)); putf(buf, cell_pos1(f.idx[2], size));
+        buf.append(reinterpret_cast<const char*>(f.grid.data()), 16ull * f.grid.size());
+        buf.push_back((char)(uint8_t)f.entries.size());
+        for (const CellFile::Entry& e : f.entries) {
+            put32(buf, (uint32_t)e.child[0]); put32(buf, (uint32_t)e.child[1]); put32(buf, (uint32_t)e.child[2]);
+            put32(buf, e.some ? (uint32_t)e.pts.size() : 0u);
+            if (e.some) buf.append(reinterpret_cast<const char*>(e.pts.data()), 16ull * e.pts.size());
+        }
+        const std::string hd = dir + "/h_" + std::to_string(f.h);
+        if (mkdir(hd.c_str(), 0755) != 0 && errno != EEXIST) { err = "cannot create " + hd; return -EIO; }
+        char name[96];
+        snprintf(name, sizeof name, "/c_%d_%d_%d.bin", f.idx[0], f.idx[1], f.idx[2]);
+        const std::string path = hd + name;
+        FILE* fp = fopen(path.c_str(), "wb");
+        bool ok = fp != nullptr;
+        if (ok) { ok = fwrite(buf.data(), 1, buf.size(), fp) == buf.size(); ok = (fclose(fp) == 0) && ok; }
+        if (!ok) { err = "cannot write " + path; return -EIO; }
+    }
+    return 0;
+}
+
 unsigned writer_threads() {
     const char* e = getenv("PCC_WRITE_THREADS");
     if (e && atoi(e) > 0) return (unsigned)atoi(e);
@@ -410,43 +444,155 @@ int read_cloud(const std::string& dir, uint32_t hierarchies, std::vector<CellFil
     return 0;
 }
 
+// The existing cloud as the engine's merge state (engine.h PriorState).  Keys
+// follow the reference's order of precedence (all existing points before any
+// new one); per level h: every cell's grid points, then every kept list in
+// stored order.  Cells are taken in (x, y, z) order.  The per-slab grouping of
+// levels >= 1 (hex layer trunc(z / r_h), hex.rs:83) and each seed's child slab
+// at h+1 (metadata.rs:100-102, hex.rs:83) use the build's own f32 formulas.
 int prior_from_cells(const std::vector<CellFile>& cells, const Config& cfg, PriorState& out, std::string& err) {
     uint32_t levels = 0;
     for (const CellFile& c : cells) levels = std::max(levels, c.h + 1);
-    out.seeds.clear();
+    out = PriorState();
     out.forced_lo.assign(levels, 0);
-    out.cells.assign(levels, {});
+    out.levels.assign(levels, PriorLevel());
     std::vector<std::vector<const CellFile*>> by(levels);
     for (const CellFile& c : cells) by[c.h].push_back(&c);
+    for (auto& v : by)
+        std::sort(v.begin(), v.end(), [](const CellFile* a, const CellFile* b) {
+            return a->idx[0] != b->idx[0] ? a->idx[0] < b->idx[0] : (a->idx[1] != b->idx[1] ? a->idx[1] < b->idx[1] : a->idx[2] < b->idx[2]);
+        });
+    // keys and per-cell offsets
+    struct CellPlan { uint64_t gkey, kkey, inj_off; std::vector<int32_t> layers; std::vector<PriorSlabRec> recs; };
+    std::vector<std::vector<CellPlan>> plan(levels);
+    uint64_t key = 0, inj = 0;
     for (uint32_t h = 0; h < levels; h++) {
-        // grid seeds.  Cell::read_from re-keys the grid by slot (cell.rs:189-195);
-        // files written by the reference or by this build hold one point per slot,
-        // so the file order is kept as is (a file with a repeated slot is not a
-        // state the reference can produce and is not detected here).
-        for (const CellFile* c : by[h]) out.seeds.insert(out.seeds.end(), c->grid.begin(), c->grid.end());
-        out.forced_lo[h] = out.seeds.size();
-        // kept seeds: every Some list in stored order; bucket states per cell
-        for (const CellFile* c : by[h]) {
+        plan[h].resize(by[h].size());
+        for (size_t i = 0; i < by[h].size(); i++) { plan[h][i].gkey = key; key += by[h][i]->grid.size(); }
+        out.forced_lo[h] = key;
+        for (size_t i = 0; i < by[h].size(); i++) {
+            plan[h][i].kkey = key;
+            for (const CellFile::Entry& e : by[h][i]->entries) {
+                const int32_t bx = e.child[0] - 2 * by[h][i]->idx[0], by_ = e.child[1] - 2 * by[h][i]->idx[1],
+                              bz = e.child[2] - 2 * by[h][i]->idx[2];
+                if (((bx | by_ | bz) & ~1) != 0) { err = "overflow entry that is not a child of its cell"; return -EINVAL; }
+                if (e.some) key += e.pts.size();
+            }
+            if (h > 0) { plan[h][i].inj_off = inj; inj += key - plan[h][i].kkey + by[h][i]->grid.size(); }
+        }
+    }
+    if (key >= 0xFFFFFFFFull) { err = "existing cloud has more than 2^32-1 points"; return -EOVERFLOW; }
+    out.nseeds = key;
+    out.inj.resize(inj);
+    out.inj_keys.resize(inj);
+    // level-0 seeds in key order
+    for (const CellFile* c : by.empty() ? std::vector<const CellFile*>() : by[0])
+        out.seeds0.insert(out.seeds0.end(), c->grid.begin(), c->grid.end());
+    for (const CellFile* c : by.empty() ? std::vector<const CellFile*>() : by[0])
+        for (const CellFile::Entry& e : c->entries)
+            if (e.some) out.seeds0.insert(out.seeds0.end(), e.pts.begin(), e.pts.end());
+    // per cell (threads): slabs by hex layer, seeds grouped by slab, their child slabs
+    std::atomic<int> bad{0};
+    for (uint32_t h = 0; h < levels; h++) {
+        const float cs = cell_size(cfg.max_cell_size, h), cr = hex_radius(sub_cell_size(cs, cfg.sub_grid_dimension));
+        const float csc = cell_size(cfg.max_cell_size, h + 1), crc = hex_radius(sub_cell_size(csc, cfg.sub_grid_dimension));
+        std::atomic<size_t> next{0};
+        auto work = [&]() {
+            std::vector<std::pair<int32_t, uint32_t>> lay;   // (layer, point #) ; # < grid: grid, else kept
+            std::vector<const Point*> src;
+            std::vector<uint32_t> keys;
+            for (;;) {
+                const size_t i = next.fetch_add(1);
+                if (i >= by[h].size()) return;
+                const CellFile* c = by[h][i];
+                CellPlan& P = plan[h][i];
+                src.clear();
+                keys.clear();
+                for (size_t j = 0; j < c->grid.size(); j++) { src.push_back(&c->grid[j]); keys.push_back((uint32_t)(P.gkey + j)); }
+                uint64_t kk = P.kkey;
+                for (const CellFile::Entry& e : c->entries)
+                    if (e.some)
+                        for (const Point& q : e.pts) { src.push_back(&q); keys.push_back((uint32_t)kk++); }
+                lay.resize(src.size());
+                for (uint32_t j = 0; j < src.size(); j++) lay[j] = {sat_i32(src[j]->z / cr), j};   // hex.rs:83
+                std::stable_sort(lay.begin(), lay.end(),
+                                 [](const std::pair<int32_t, uint32_t>& a, const std::pair<int32_t, uint32_t>& b) { return a.first < b.first; });
+                uint64_t w = P.inj_off;
+                for (size_t j = 0; j < lay.size();) {
+                    size_t e = j;
+                    while (e < lay.size() && lay[e].first == lay[j].first) e++;
+                    const int32_t t = lay[j].first;
+                    PriorSlabRec R;
+                    R.seed_off = (uint32_t)w;
+                    R.nseed = (uint32_t)(e - j);
+                    for (int d = 0; d < 24; d++) { R.child[d] = kNoPriorSlab; R.dcap[d] = 0; }
+                    for (size_t k = j; k < e; k++) {   // grid seeds first (lower keys), then kept: already in key order
+                        const Point* q = src[lay[k].second];
+                        const int32_t bx = cell_index1(q->x, csc) - 2 * c->idx[0], by_ = cell_index1(q->y, csc) - 2 * c->idx[1],
+                                      bz = cell_index1(q->z, csc) - 2 * c->idx[2];
+                        const int32_t sel = sat_i32(q->z / crc) - 2 * t + 1;
+                        if (((bx | by_ | bz) & ~1) != 0 || sel < 0 || sel > 2) {
+                            if (h + 1 < 31) bad.store(1);   // routes only matter if the child level can exist
+                        } else {
+                            R.dcap[(bx | (by_ << 1) | (bz << 2)) * 3 + sel]++;
+                        }
+                        if (h > 0) { out.inj[w] = *q; out.inj_keys[w] = keys[lay[k].second]; w++; }
+                    }
+                    P.layers.push_back(t);
+                    P.recs.push_back(R);
+                    j = e;
+                }
+            }
+        };
+        const unsigned nt = std::max(1u, std::min<unsigned>(16, std::thread::hardware_concurrency()));
+        std::vector<std::thread> th;
+        for (unsigned t = 1; t < nt; t++) th.emplace_back(work);
+        work();
+        for (auto& t : th) t.join();
+        PriorLevel& L = out.levels[h];
+        L.cell_slab0.push_back(0);
+        for (size_t i = 0; i < by[h].size(); i++) {
+            const CellFile* c = by[h][i];
             PriorCell pc{c->idx[0], c->idx[1], c->idx[2], 0u};
             for (const CellFile::Entry& e : c->entries) {
-                const int32_t bx = e.child[0] - 2 * c->idx[0], by_ = e.child[1] - 2 * c->idx[1], bz = e.child[2] - 2 * c->idx[2];
-                if (((bx | by_ | bz) & ~1) != 0) {
-                    err = "overflow entry that is not a child of its cell";
-                    return -EINVAL;
-                }
-                const int oct = bx | (by_ << 1) | (bz << 2);
+                const int oct = (e.child[0] - 2 * c->idx[0]) | ((e.child[1] - 2 * c->idx[1]) << 1) | ((e.child[2] - 2 * c->idx[2]) << 2);
                 pc.st |= (e.some ? 1u : 2u) << (2 * oct);
-                if (e.some) out.seeds.insert(out.seeds.end(), e.pts.begin(), e.pts.end());
             }
-            out.cells[h].push_back(pc);
+            L.cells.push_back(pc);
+            L.slab_layer.insert(L.slab_layer.end(), plan[h][i].layers.begin(), plan[h][i].layers.end());
+            L.slabs.insert(L.slabs.end(), plan[h][i].recs.begin(), plan[h][i].recs.end());
+            L.cell_slab0.push_back((uint32_t)L.slabs.size());
+            std::vector<int32_t>().swap(plan[h][i].layers);
+            std::vector<PriorSlabRec>().swap(plan[h][i].recs);
         }
-        std::sort(out.cells[h].begin(), out.cells[h].end(), [](const PriorCell& a, const PriorCell& b) {
-            return a.x != b.x ? a.x < b.x : (a.y != b.y ? a.y < b.y : a.z < b.z);
-        });
     }
-    if (out.seeds.size() >= 0xFFFFFFFFull) {
-        err = "existing cloud has more than 2^32-1 points";
-        return -EOVERFLOW;
+    if (bad.load()) { err = "existing cloud: a point lies outside its cell's child slabs"; return -EINVAL; }
+    // child links: slab (c, t), destination (octant, sel) -> record of (2c + octant bits, 2t - 1 + sel) at h+1
+    for (uint32_t h = 0; h + 1 < levels; h++) {
+        const PriorLevel& N = out.levels[h + 1];
+        PriorLevel& L = out.levels[h];
+        for (size_t i = 0; i < L.cells.size(); i++) {
+            const PriorCell& c = L.cells[i];
+            for (uint32_t s = L.cell_slab0[i]; s < L.cell_slab0[i + 1]; s++) {
+                const int32_t t = L.slab_layer[s];
+                for (int oct = 0; oct < 8; oct++) {
+                    if (((c.st >> (2 * oct)) & 3u) != 2u) continue;   // only a None bucket has a child cell
+                    const PriorCell key{2 * c.x + (oct & 1), 2 * c.y + ((oct >> 1) & 1), 2 * c.z + ((oct >> 2) & 1), 0};
+                    auto it = std::lower_bound(N.cells.begin(), N.cells.end(), key, [](const PriorCell& a, const PriorCell& b) {
+                        return a.x != b.x ? a.x < b.x : (a.y != b.y ? a.y < b.y : a.z < b.z);
+                    });
+                    if (it == N.cells.end() || it->x != key.x || it->y != key.y || it->z != key.z) continue;
+                    const size_t ci = (size_t)(it - N.cells.begin());
+                    for (int sel = 0; sel < 3; sel++) {
+                        const int32_t u = 2 * t - 1 + sel;
+                        if (u / 2 != t) continue;   // a child layer has one parent layer
+                        const auto b0 = N.slab_layer.begin() + N.cell_slab0[ci], b1 = N.slab_layer.begin() + N.cell_slab0[ci + 1];
+                        const auto jt = std::lower_bound(b0, b1, u);
+                        if (jt != b1 && *jt == u) L.slabs[s].child[oct * 3 + sel] = (uint32_t)(jt - N.slab_layer.begin());
+                    }
+                }
+            }
+        }
     }
     return 0;
 }

@@ -38,6 +38,10 @@ void level_cell_view(const Config& cfg, const LevelHost& L, uint32_t c, const Po
 int write_level_cells(const std::string& dir, const Config& cfg, const LevelHost& L, const Point* grid,
                       const Point* kept, unsigned nthreads, std::string& err);
 unsigned writer_threads();   // PCC_WRITE_THREADS, else min(16, hardware threads)
+struct CellFile;
+// cells as read from disk, written back unchanged (skip[i] != 0: not written)
+int write_cell_files(const std::string& dir, const Config& cfg, const std::vector<CellFile>& cells,
+                     const std::vector<uint8_t>* skip, std::string& err);
 int write_output(const std::string& dir, const Metadata& meta, const std::vector<LevelHost>& levels,
                  const std::vector<Point>& grid, const std::vector<Point>& kept, std::string& err,
                  bool with_metadata = true);
