@@ -233,7 +233,7 @@ def main_sharded(args, rank, world):
         k = prof[-1]
         dense_ms = sum(p["dense_ms"] for p in prof) / len(prof)
         rec = record(args, world, ms, max(p[0] for p in per), sum(p[1] for p in per), sum(p[2] for p in per),
-                     sum(p[3] for p in per), k, dense_ms, f"level-0 cell sharding over {world} ranks (RCCL all-to-all-v)")
+                     sum(p[3] for p in per), k, dense_ms, f"level-0 cell sharding over {world} ranks (grouped RCCL point-to-point exchange)")
         rec["sharding"] = {"points_per_rank": [p[4] for p in per], "stage_ms_rank0": stage,
                            "hierarchies": res.summary["hierarchies"]}
         json_out.write(json.dumps(rec) + "\n")

@@ -215,6 +215,14 @@ int pcc_declare_files(pcc_converter* c, const uint64_t* file_points, uint64_t nf
 /* This rank's points (device memory) with their global keys, ascending. */
 int pcc_add_keyed_points_device(pcc_converter* c, const pcc_point* dev_pts, const uint32_t* dev_keys, uint64_t n);
 
+/* Zero-copy form of the above: the build reads all of this rank's points and
+ * keys straight from these device buffers (typically the exchange's receive
+ * buffers), which must stay valid and unchanged until pcc_build returns.  Only
+ * after pcc_declare_files and before any other input; no input may follow.
+ * dev_keys may be NULL: the keys are then 0 .. n-1 (one rank holds the whole
+ * input in key order, so routing is the identity). */
+int pcc_set_keyed_points_device(pcc_converter* c, const pcc_point* dev_pts, const uint32_t* dev_keys, uint64_t n);
+
 /* Global metadata values after the ranks' all-reduce (converter.rs:96-112,141-158). */
 int pcc_set_summary(pcc_converter* c, uint64_t number_of_points, const float bmin[3], const float bmax[3],
                     uint32_t hierarchies);

@@ -460,6 +460,16 @@ int pcc_add_keyed_points_device(pcc_converter* c, const pcc_point* d, const uint
     GUARD_END
 }
 
+int pcc_set_keyed_points_device(pcc_converter* c, const pcc_point* d, const uint32_t* keys, uint64_t n) {
+    if (!c || (!d && n)) return set_err(-EINVAL, "null argument");
+    if (!c->keyed) return set_err(-EINVAL, "pcc_declare_files must come first");
+    if (c->built) return set_err(-EINVAL, "points added after build");
+    GUARD_BEGIN
+    c->eng->set_keyed_external(reinterpret_cast<const Point*>(d), keys, n);
+    return 0;
+    GUARD_END
+}
+
 int pcc_set_summary(pcc_converter* c, uint64_t number_of_points, const float bmin[3], const float bmax[3],
                     uint32_t hierarchies) {
     if (!c || !bmin || !bmax) return set_err(-EINVAL, "null argument");

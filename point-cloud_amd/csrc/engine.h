@@ -133,6 +133,11 @@ public:
     // indices (keys, ascending).  Event batches come from the global table.
     void declare_files(const uint64_t* file_points, uint64_t nfiles, uint32_t batch);
     void add_keyed_device(const Point* dpts, const uint32_t* dkeys, uint64_t n);
+    // Zero-copy variant: the build reads this shard's n points and keys straight
+    // from caller memory (e.g. the buffers an exchange received into), which must
+    // stay valid and unchanged until the next build() returns.  Replaces any
+    // keyed input; no other input may be added afterwards.
+    void set_keyed_external(const Point* dpts, const uint32_t* dkeys, uint64_t n);
     // Drops all input (points, keys, files) but keeps device allocations.
     void clear_input();
     // Incremental merge: the existing cloud's state (kept until the engine dies).
@@ -187,6 +192,8 @@ private:
     std::vector<uint32_t> file_batch_;   // batch size per file
     Point* d_in_ = nullptr;
     uint32_t* d_keys_ = nullptr;         // keyed (sharded) input: global key per point
+    const Point* ext_in_ = nullptr;      // set_keyed_external(): borrowed input instead of d_in_/d_keys_
+    const uint32_t* ext_keys_ = nullptr;
     // build source: d_in_ (n_ points) or, when merging, [seeds | d_in_]
     const Point* src_ = nullptr;
     uint64_t nsrc_ = 0;

@@ -2628,6 +2628,7 @@ int Engine::fail(int code, const std::string& msg) {
 }
 
 void Engine::reserve(uint64_t n) {
+    if (ext_in_) throw std::runtime_error("input added after borrowed keyed input");
     if (n <= cap_) return;
     if (n >= 0xFFFFFFFFull) throw std::runtime_error("more than 2^32-1 points per build are not supported");
     Point* p = nullptr;
@@ -2692,6 +2693,15 @@ void Engine::declare_files(const uint64_t* file_points, uint64_t nfiles, uint32_
     keyed_ = true;
 }
 
+void Engine::set_keyed_external(const Point* dpts, const uint32_t* dkeys, uint64_t n) {
+    if (n_ || !keyed_) throw std::runtime_error("borrowed keyed input needs declared files and no other input");
+    if (n >= 0xFFFFFFFFull) throw std::runtime_error("more than 2^32-1 points per build are not supported");
+    ext_in_ = dpts;
+    ext_keys_ = dkeys;
+    n_ = n;
+    comb_ok_ = false;
+}
+
 void Engine::add_keyed_device(const Point* dpts, const uint32_t* dkeys, uint64_t n) {
     reserve(n_ + n);
     if (keys_cap_ < n_ + n) {
@@ -2752,6 +2762,8 @@ void Engine::clear_input() {
     file_eb0_.clear();
     file_batch_.clear();
     keyed_ = false;
+    ext_in_ = nullptr;
+    ext_keys_ = nullptr;
     declared_total_ = 0;
     built_ = false;
 }
@@ -2789,13 +2801,15 @@ int Engine::build() {
                 comb_cap_ = n0 + n_;
             }
             if (n0) HIP_CHECK(hipMemcpyAsync(d_comb_, d_seeds_, n0 * sizeof(Point), hipMemcpyDeviceToDevice, stream_));
-            HIP_CHECK(hipMemcpyAsync(d_comb_ + n0, d_in_, n_ * sizeof(Point), hipMemcpyDeviceToDevice, stream_));
+            HIP_CHECK(hipMemcpyAsync(d_comb_ + n0, ext_in_ ? ext_in_ : d_in_, n_ * sizeof(Point),
+                                     hipMemcpyDeviceToDevice, stream_));
             if (ckeys_cap_ < n0 + n_) {
                 (void)hipFree(d_ckeys_);
                 HIP_CHECK(hipMalloc(&d_ckeys_, std::max<uint64_t>(n0 + n_, 1) * 4));
                 ckeys_cap_ = n0 + n_;
             }
-            k_comb_keys<<<grid_for(n0 + n_, 256), 256, 0, stream_>>>(d_ckeys_, keyed_ ? d_keys_ : nullptr, n0, nseeds_, n_);
+            k_comb_keys<<<grid_for(n0 + n_, 256), 256, 0, stream_>>>(d_ckeys_, ext_in_ ? ext_keys_ : keyed_ ? d_keys_ : nullptr,
+                                                                    n0, nseeds_, n_);
             HIP_CHECK(hipGetLastError());
             comb_ok_ = true;
         }
@@ -2803,8 +2817,8 @@ int Engine::build() {
         src_keys_ = d_ckeys_;
         nsrc_ = n0 + n_;
     } else {
-        src_ = d_in_;
-        src_keys_ = keyed_ ? d_keys_ : nullptr;
+        src_ = ext_in_ ? ext_in_ : d_in_;
+        src_keys_ = ext_in_ ? ext_keys_ : keyed_ ? d_keys_ : nullptr;
         nsrc_ = n_;
     }
     if ((prior_ ? nseeds_ : 0) + n_ >= 0xFFFFFFFFull)

@@ -33,6 +33,7 @@ EXPORTS = ["pcc_abi_version", "pcc_last_error", "pcc_options_default", "pcc_open
            "pcc_finish", "pcc_close", "pcc_get_stats", "pcc_set_profiling", "pcc_get_profile", "pcc_device_input",
            "pcc_convert_files", "pcc_shard_grid_from_bbox", "pcc_synth_device", "pcc_shard_bbox",
            "pcc_shard_histogram", "pcc_shard_route", "pcc_declare_files", "pcc_add_keyed_points_device",
+           "pcc_set_keyed_points_device",
            "pcc_set_summary", "pcc_write_cells", "pcc_write_metadata", "pcc_clear_input", "pcc_adopt_prior",
            "pcc_open_subtrees", "pcc_visit_cells"]
 
@@ -145,6 +146,7 @@ def lib():
                                       C.POINTER(C.c_uint64), C.c_int]
         L.pcc_declare_files.argtypes = [vp, C.POINTER(C.c_uint64), C.c_uint64]
         L.pcc_add_keyed_points_device.argtypes = [vp, vp, vp, C.c_uint64]
+        L.pcc_set_keyed_points_device.argtypes = [vp, vp, vp, C.c_uint64]
         L.pcc_set_summary.argtypes = [vp, C.c_uint64, f3, f3, C.c_uint32]
         L.pcc_write_cells.argtypes = [vp]
         L.pcc_write_metadata.argtypes = [vp]
@@ -229,6 +231,10 @@ class Converter:
 
     def add_keyed_points_device(self, pts_ptr: int, keys_ptr: int, n: int):
         _check(lib().pcc_add_keyed_points_device(self._h, C.c_void_p(pts_ptr), C.c_void_p(keys_ptr), n))
+
+    def set_keyed_points_device(self, pts_ptr: int, keys_ptr: int, n: int):
+        """Borrow (no copy) this rank's keyed input until build() returns."""
+        _check(lib().pcc_set_keyed_points_device(self._h, C.c_void_p(pts_ptr), C.c_void_p(keys_ptr), n))
 
     def set_summary(self, number_of_points: int, bmin, bmax, hierarchies: int):
         _check(lib().pcc_set_summary(self._h, number_of_points, (C.c_float * 3)(*bmin), (C.c_float * 3)(*bmax),

@@ -11,11 +11,16 @@ of c).  So the unit of ownership is the level-0 cell, and one step is:
      bounding box, converter.rs:96-104) and the level-0 grid it spans;
   3. per-cell histogram -> all-reduce(sum) -> identical owner table on every
      rank (`assign_owners`, deterministic);
-  4. stable partition by owner (HIP) -> all-to-all of counts, then all-to-all-v
-     of the 16-B points and the u32 keys (RCCL over xGMI).  Segments arrive in
-     source-rank order, so each rank's input stays in global key order;
-  5. independent level-synchronous builds with the GLOBAL batch structure
-     (pcc_declare_files + pcc_add_keyed_points_device);
+  4. stable partition by owner (HIP) -> all-to-all of counts, then one grouped
+     batch of point-to-point transfers (RCCL over xGMI) of the 16-B points and
+     the u32 keys straight into this rank's receive buffers, at most 2^30 bytes
+     per transfer (larger ones corrupt on this stack, TorchComm.max_msg_bytes);
+     the own segment is a device copy.  Segments land in source-rank order, so
+     each rank's input stays in global key order.  With one rank the partition
+     is the identity and nothing is routed;
+  5. independent level-synchronous builds with the GLOBAL batch structure,
+     reading the receive buffers in place (pcc_declare_files +
+     pcc_set_keyed_points_device);
   6. all-reduce(max) of `hierarchies`; every rank writes its own (disjoint) cell
      files, rank 0 writes metadata.json after a barrier.
 
@@ -69,39 +74,39 @@ class TorchComm:
         self.dist.all_to_all_single(r, s)
         return [int(v) for v in r.tolist()]
 
-    # bytes one all-to-all call moves per rank at most (a single call of 2 GiB or more
-    # of payload returns corrupted data on this stack); larger exchanges run in
-    # rounds, each peer segment split at the same row offsets on both sides
-    chunk_bytes = 1 << 30
+    # bytes one RCCL point-to-point transfer may carry.  On this stack a single
+    # send/recv of more than 2^30 bytes (all_to_all_single is built from the same
+    # transfers) returns the second half of the message corrupted, for any dtype;
+    # exactly 2^30 is fine (scripts/a2a_threshold.py, profiles/r2_rccl_threshold.log)
+    max_msg_bytes = 1 << 30
 
-    def alltoallv(self, send: torch.Tensor, send_counts: list[int], recv_counts: list[int]) -> torch.Tensor:
-        out = torch.empty((sum(recv_counts),) + tuple(send.shape[1:]), dtype=send.dtype, device=send.device)
+    def alltoallv_into(self, send: torch.Tensor, send_counts: list[int], recv_counts: list[int],
+                       out: torch.Tensor) -> torch.Tensor:
+        """Rows send[so[p]:so[p]+send_counts[p]] go to rank p; rank p's rows land
+        in out[ro[p]:ro[p]+recv_counts[p]] (source-rank order).  One grouped
+        batch of point-to-point transfers straight into those slices, each at
+        most `max_msg_bytes`; the own segment is a local device copy."""
         row = send.element_size() * max(1, int(np.prod(send.shape[1:])))
-        mr = max(1, self.chunk_bytes // (row * self.world))   # rows per peer per round
-        local = max([-(-int(c) // mr) for c in list(send_counts) + list(recv_counts)] + [1])
-        r = torch.tensor([local], dtype=torch.int64, device=self.device)
-        self.dist.all_reduce(r, op=self.dist.ReduceOp.MAX)
-        rounds = int(r.item())
-        if rounds == 1:
-            self.dist.all_to_all_single(out, send, recv_counts, send_counts)
-            return out
+        mr = max(1, self.max_msg_bytes // row)
         so = np.concatenate([[0], np.cumsum(send_counts)]).astype(np.int64)
         ro = np.concatenate([[0], np.cumsum(recv_counts)]).astype(np.int64)
-        for k in range(rounds):   # round k: rows [k*mr, (k+1)*mr) of every peer segment
-            ins, outs = [], []
-            for p in range(self.world):
-                a = min(k * mr, int(send_counts[p]))
-                ins.append(send.narrow(0, int(so[p]) + a, min(mr, int(send_counts[p]) - a)))
-                b = min(k * mr, int(recv_counts[p]))
-                outs.append(out.narrow(0, int(ro[p]) + b, min(mr, int(recv_counts[p]) - b)))
-            tmp = torch.empty((sum(int(o.shape[0]) for o in outs),) + tuple(send.shape[1:]), dtype=send.dtype,
-                              device=send.device)
-            self.dist.all_to_all_single(tmp, torch.cat(ins), [int(o.shape[0]) for o in outs],
-                                        [int(i.shape[0]) for i in ins])
-            o = 0
-            for dst in outs:
-                dst.copy_(tmp.narrow(0, o, int(dst.shape[0])))
-                o += int(dst.shape[0])
+        me = self.rank
+        if int(send_counts[me]) != int(recv_counts[me]):
+            raise ValueError("own segment: send and receive counts differ")
+        if send_counts[me]:
+            out.narrow(0, int(ro[me]), int(recv_counts[me])).copy_(send.narrow(0, int(so[me]), int(send_counts[me])))
+        ops = []
+        for k in range(1, self.world):   # peers in ring order from this rank
+            p_to, p_from = (me + k) % self.world, (me - k) % self.world
+            for a in range(0, int(send_counts[p_to]), mr):
+                ops.append(self.dist.P2POp(self.dist.isend, send.narrow(0, int(so[p_to]) + a,
+                                                                        min(mr, int(send_counts[p_to]) - a)), p_to))
+            for b in range(0, int(recv_counts[p_from]), mr):
+                ops.append(self.dist.P2POp(self.dist.irecv, out.narrow(0, int(ro[p_from]) + b,
+                                                                       min(mr, int(recv_counts[p_from]) - b)), p_from))
+        if ops:
+            for req in self.dist.batch_isend_irecv(ops):
+                req.wait()
         return out
 
     def barrier(self):
@@ -145,14 +150,18 @@ class ThreadComm:
         allv = self._exchange(list(counts))
         return [int(allv[src][self.rank]) for src in range(self.world)]
 
-    def alltoallv(self, send: torch.Tensor, send_counts: list[int], recv_counts: list[int]) -> torch.Tensor:
+    def alltoallv_into(self, send: torch.Tensor, send_counts: list[int], recv_counts: list[int],
+                       out: torch.Tensor) -> torch.Tensor:
         allv = self._exchange((send, list(send_counts)))
-        parts = []
+        o_out = 0
         for src in range(self.world):
             t, c = allv[src]
             o = sum(c[: self.rank])
-            parts.append(t[o:o + c[self.rank]].to(send.device))
-        out = torch.cat(parts) if parts else send[:0]
+            m = int(c[self.rank])
+            if m != int(recv_counts[src]):
+                raise ValueError("receive count differs from the sender's count")
+            out.narrow(0, o_out, m).copy_(t.narrow(0, o, m))
+            o_out += m
         self.g.bar.wait()   # senders may free/reuse their buffers only after every copy
         return out
 
@@ -263,12 +272,14 @@ class HipShardOps:
                                     keys.data_ptr(), self.dev)
         return send, keys, counts
 
-    def build(self, file_points, pts: torch.Tensor, keys: torch.Tensor) -> dict:
+    def build(self, file_points, pts: torch.Tensor, keys: torch.Tensor | None) -> dict:
+        """keys None: this rank holds the whole input in key order (keys 0..n-1).
+        The build reads `pts`/`keys` in place (borrowed until it returns)."""
         c = self.conv
         self._ready()
         c.clear_input()
         c.declare_files(file_points)
-        c.add_keyed_points_device(pts.data_ptr(), keys.data_ptr(), pts.shape[0])
+        c.set_keyed_points_device(pts.data_ptr(), 0 if keys is None else keys.data_ptr(), pts.shape[0])
         return c.build()
 
     def write(self, summary: dict, cells: bool, metadata: bool):
@@ -366,12 +377,27 @@ def shard_build(comm, ops, pts: torch.Tensor, key0: int, file_points, write: boo
         if merge:   # the existing cells of the owned subtrees that receive new points
             ops.set_subtrees(cell_triples(np.flatnonzero((owner_h == comm.rank) & (hist_h > 0)), grid))
         mark("plan")
-        # 4. route + exchange (all-to-all-v of points and keys)
-        send, skeys, counts = ops.route(pts, key0, grid, owner, comm.world)
-        mark("route")
-        rcounts = comm.alltoall_counts(counts)
-        recv = comm.alltoallv(send.to(comm.device), counts, rcounts).to(pts.device)
-        keys = comm.alltoallv(skeys.to(comm.device), counts, rcounts).to(pts.device)
+        # 4. route + exchange (grouped point-to-point transfers of points and keys)
+        if comm.world == 1:   # one rank owns every cell: the partition is the identity
+            recv, keys = pts, None
+            mark("route")
+        else:
+            send, skeys, counts = ops.route(pts, key0, grid, owner, comm.world)
+            mark("route")
+            rcounts = comm.alltoall_counts(counts)
+            nrecv = int(sum(rcounts))
+            if comm.device == pts.device:   # receive straight into the build's input buffers
+                recv = torch.empty((nrecv,) + tuple(pts.shape[1:]), dtype=pts.dtype, device=pts.device)
+                keys = torch.empty(nrecv, dtype=torch.int32, device=pts.device)
+                comm.alltoallv_into(send, counts, rcounts, recv)
+                comm.alltoallv_into(skeys, counts, rcounts, keys)
+            else:   # host communicator (gloo) driving device ops
+                recv = torch.empty((nrecv,) + tuple(pts.shape[1:]), dtype=pts.dtype, device=comm.device)
+                keys = torch.empty(nrecv, dtype=torch.int32, device=comm.device)
+                comm.alltoallv_into(send.to(comm.device), counts, rcounts, recv)
+                comm.alltoallv_into(skeys.to(comm.device), counts, rcounts, keys)
+                recv, keys = recv.to(pts.device), keys.to(pts.device)
+            del send, skeys
         mark("exchange")
     # 5. independent build of the owned level-0 subtrees
     local = ops.build(file_points, recv, keys)

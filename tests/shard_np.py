@@ -94,7 +94,8 @@ class NumpyShardOps:
 
     def build(self, file_points, pts, keys) -> dict:
         p = as_points(pts)
-        k = keys.cpu().numpy().view(np.uint32).astype(np.int64)
+        k = (np.arange(len(p), dtype=np.int64) if keys is None
+             else keys.cpu().numpy().view(np.uint32).astype(np.int64))
         assert (np.diff(k) > 0).all(), "keyed input must arrive in global key order"
         if self.oracle is not None:
             self.oracle.close()

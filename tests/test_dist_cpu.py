@@ -82,7 +82,7 @@ def test_assign_owners_many_cells_prefix_split():
 
 
 # ------------------------------------------------------------- thread ranks
-@pytest.mark.parametrize("case,world", [("uniform", 2), ("files", 3), ("clustered", 4)])
+@pytest.mark.parametrize("case,world", [("uniform", 1), ("uniform", 2), ("files", 3), ("clustered", 4)])
 def test_thread_ranks_match_oracle(tmp_path, case, world):
     import threading
     files = make_input(case)
@@ -269,7 +269,7 @@ def _gloo_chunked_worker(rank, world, port, out, res_dir):
         files = make_input("files")
         pts, key0 = rank_slice(files, rank, world)
         comm = TorchComm(torch.device("cpu"))
-        comm.chunk_bytes = 1 << 16   # force the all-to-all-v into many rounds
+        comm.max_msg_bytes = 1 << 16   # force every peer segment into many transfers
         ops = NumpyShardOps(out)
         r = shard_build(comm, ops, as_tensor(pts), key0, [len(f) for f in files], write=True)
         ops.close()
@@ -280,7 +280,7 @@ def _gloo_chunked_worker(rank, world, port, out, res_dir):
 
 
 def test_gloo_world2_chunked_exchange_matches_oracle(tmp_path):
-    """The all-to-all-v split into rounds (TorchComm.chunk_bytes) gives the same exchange."""
+    """Peer segments split into many transfers (TorchComm.max_msg_bytes) give the same exchange."""
     import torch.multiprocessing as mp
     out, rd = str(tmp_path / "out"), str(tmp_path / "res")
     os.makedirs(rd)
