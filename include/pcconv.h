@@ -223,6 +223,24 @@ int pcc_add_keyed_points_device(pcc_converter* c, const pcc_point* dev_pts, cons
  * input in key order, so routing is the identity). */
 int pcc_set_keyed_points_device(pcc_converter* c, const pcc_point* dev_pts, const uint32_t* dev_keys, uint64_t n);
 
+/* Level ranges: one heavy level-0 cell built by several ranks (SURVEY §8e/§8f-4;
+ * converter.rs:114-139 recursion split at a level boundary, which is exact
+ * because a level-h cell's build depends only on the points forwarded to it).
+ * root_level h0: the input is the exported arrivals of level-h0 cells (keys =
+ * their global event keys), with the parent buckets' spill batches from
+ * pcc_set_root_spill_batches; cells are written as h_{h0}, h_{h0+1}, ...
+ * max_levels m > 0: build levels h0 .. h0+m-1 only and keep the next level's
+ * arrivals on the device for pcc_export_pending.  Not for merges. */
+int pcc_set_level_range(pcc_converter* c, uint32_t root_level, uint32_t max_levels);
+int pcc_set_root_spill_batches(pcc_converter* c, const int32_t* cells_xyz, const uint32_t* spill_batch, uint64_t ncells);
+/* After pcc_build with max_levels: the cells of the first level not built. */
+int pcc_pending_cells(pcc_converter* c, uint64_t* ncells, uint64_t* npoints);
+/* Their arrivals, cell after cell (cell_points[i] each; a cell's slabs in layer
+ * order, each slab in key order) into device buffers of npoints; the cells'
+ * (x, y, z) and spill batches into host arrays of ncells. */
+int pcc_export_pending(pcc_converter* c, int32_t* cells_xyz, uint32_t* spill_batch, uint64_t* cell_points,
+                       pcc_point* dev_pts, uint32_t* dev_keys);
+
 /* Global metadata values after the ranks' all-reduce (converter.rs:96-112,141-158). */
 int pcc_set_summary(pcc_converter* c, uint64_t number_of_points, const float bmin[3], const float bmax[3],
                     uint32_t hierarchies);

@@ -470,6 +470,42 @@ int pcc_set_keyed_points_device(pcc_converter* c, const pcc_point* d, const uint
     GUARD_END
 }
 
+int pcc_set_level_range(pcc_converter* c, uint32_t root_level, uint32_t max_levels) {
+    if (!c) return set_err(-EINVAL, "null argument");
+    if (c->merge) return set_err(-EINVAL, "a merge cannot be split into level ranges");
+    if (root_level >= 31) return set_err(-EINVAL, "root level must be < 31");
+    c->eng->set_root_level(root_level);
+    c->eng->set_max_levels(max_levels);
+    return 0;
+}
+
+int pcc_set_root_spill_batches(pcc_converter* c, const int32_t* cells_xyz, const uint32_t* spill_batch, uint64_t n) {
+    if (!c || ((!cells_xyz || !spill_batch) && n)) return set_err(-EINVAL, "null argument");
+    GUARD_BEGIN
+    c->eng->set_root_spill_batches(cells_xyz, spill_batch, n);
+    return 0;
+    GUARD_END
+}
+
+int pcc_pending_cells(pcc_converter* c, uint64_t* ncells, uint64_t* npoints) {
+    if (!c || !ncells || !npoints) return set_err(-EINVAL, "null argument");
+    if (!c->built) return set_err(-EINVAL, "nothing built");
+    return c->eng->pending_info(*ncells, *npoints);
+}
+
+int pcc_export_pending(pcc_converter* c, int32_t* cells_xyz, uint32_t* spill_batch, uint64_t* cell_points,
+                       pcc_point* dev_pts, uint32_t* dev_keys) {
+    if (!c) return set_err(-EINVAL, "null argument");
+    if (!c->built) return set_err(-EINVAL, "nothing built");
+    uint64_t nc = 0, np = 0;
+    c->eng->pending_info(nc, np);
+    if (nc && (!cells_xyz || !spill_batch || !cell_points)) return set_err(-EINVAL, "null argument");
+    if (np && (!dev_pts || !dev_keys)) return set_err(-EINVAL, "null argument");
+    GUARD_BEGIN
+    return c->eng->export_pending(cells_xyz, spill_batch, cell_points, reinterpret_cast<Point*>(dev_pts), dev_keys);
+    GUARD_END
+}
+
 int pcc_set_summary(pcc_converter* c, uint64_t number_of_points, const float bmin[3], const float bmax[3],
                     uint32_t hierarchies) {
     if (!c || !bmin || !bmax) return set_err(-EINVAL, "null argument");

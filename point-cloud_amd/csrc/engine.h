@@ -138,6 +138,17 @@ public:
     // stay valid and unchanged until the next build() returns.  Replaces any
     // keyed input; no other input may be added afterwards.
     void set_keyed_external(const Point* dpts, const uint32_t* dkeys, uint64_t n);
+    // Level ranges (sharded build of a heavy level-0 cell).
+    // set_max_levels(m): build levels h0 .. h0+m-1 only; the next level's
+    // arrivals stay on the device as the "pending" level, exported per cell
+    // (contiguous, slab order, each slab in key order) with the spill batch of
+    // its parent bucket.  set_root_level(h0) + set_root_spill_batches(): build
+    // a sub-tree whose input is such exported arrivals of level-h0 cells.
+    void set_max_levels(uint32_t m) { max_levels_ = m; }
+    void set_root_level(uint32_t h0) { h0_ = h0; }
+    void set_root_spill_batches(const int32_t* xyz, const uint32_t* sb, uint64_t n);
+    int pending_info(uint64_t& ncells, uint64_t& npoints) const;
+    int export_pending(int32_t* xyz, uint32_t* sb, uint64_t* cell_n, Point* dpts, uint32_t* dkeys);
     // Drops all input (points, keys, files) but keeps device allocations.
     void clear_input();
     // Incremental merge: the existing cloud's state (kept until the engine dies).
@@ -176,7 +187,7 @@ private:
     void ev_end(int stage);
     void ev_collect();
     int level0_bin();
-    int run_level(uint32_t h);
+    int run_level(uint32_t li);
     void run_dcap(Level* L);
     void free_all();
     void free_prior();
@@ -192,6 +203,10 @@ private:
     std::vector<uint32_t> file_batch_;   // batch size per file
     Point* d_in_ = nullptr;
     uint32_t* d_keys_ = nullptr;         // keyed (sharded) input: global key per point
+    uint32_t h0_ = 0, max_levels_ = 0;   // level range (set_root_level / set_max_levels)
+    Level* pending_ = nullptr;           // the first level not built (max_levels_)
+    std::vector<int32_t> root_xyz_;      // root cells (sorted) and their spill batches
+    std::vector<uint32_t> root_sb_;
     const Point* ext_in_ = nullptr;      // set_keyed_external(): borrowed input instead of d_in_/d_keys_
     const uint32_t* ext_keys_ = nullptr;
     // build source: d_in_ (n_ points) or, when merging, [seeds | d_in_]

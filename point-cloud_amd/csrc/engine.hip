@@ -944,6 +944,43 @@ __global__ void k_l0_tables(const uint32_t* hist, const uint32_t* cnt_scan, cons
     }
 }
 
+// Sub-tree build rooted below level 0 (set_root_level): each root cell takes the
+// spill batch of the parent bucket it came from (exported with the arrivals,
+// export_pending), found by binary search in the (x, y, z)-sorted root table.
+__global__ void k_root_sb(const int32_t* __restrict__ cell_idx, uint32_t ncells, const int32_t* __restrict__ rxyz,
+                          const uint32_t* __restrict__ rsb, uint32_t nroot, uint32_t* __restrict__ cell_sb,
+                          Counters* ctr) {
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= ncells) return;
+    const int32_t x = cell_idx[3 * c], y = cell_idx[3 * c + 1], z = cell_idx[3 * c + 2];
+    uint32_t lo = 0, hi = nroot;
+    while (lo < hi) {
+        const uint32_t m = (lo + hi) / 2;
+        const int32_t* q = rxyz + 3ull * m;
+        const bool less = q[0] != x ? q[0] < x : q[1] != y ? q[1] < y : q[2] < z;
+        if (less) lo = m + 1;
+        else hi = m;
+    }
+    const int32_t* q = rxyz + 3ull * lo;
+    if (lo < nroot && q[0] == x && q[1] == y && q[2] == z) cell_sb[c] = rsb[lo];
+    else atomicOr(&ctr->err, (uint32_t)ERR_L0_RANGE);
+}
+
+// Pending level (set_max_levels): its slabs' arrivals, concatenated in slab
+// order (a cell's slabs are consecutive, so every cell is one range).
+__global__ __launch_bounds__(256) void k_export_slabs(Arena A, const uint32_t* __restrict__ slab_off,
+                                                      const uint32_t* __restrict__ slab_n,
+                                                      const uint32_t* __restrict__ out_off, uint32_t nslabs,
+                                                      float4* __restrict__ dp, uint32_t* __restrict__ dk) {
+    for (uint32_t s = blockIdx.x; s < nslabs; s += gridDim.x) {
+        const uint32_t o = slab_off[s], n = slab_n[s], d = out_off[s];
+        for (uint32_t i = threadIdx.x; i < n; i += 256) {
+            dp[d + i] = A.p[o + i];
+            dk[d + i] = A.k[o + i];
+        }
+    }
+}
+
 // ------------------------------------------------------------------ slab kernels
 // Per-slab launch descriptor (one 48-B record: the slab kernels' prologue is
 // one load instead of a chain of dependent table loads).
@@ -2583,6 +2620,8 @@ void Engine::free_all() {
     for (hipEvent_t e : ev_pool_) (void)hipEventDestroy(e);
     ev_pool_.clear();
     for (Level* l : levels_) delete l;
+    delete pending_;
+    pending_ = nullptr;
     levels_.clear();
     if (dev_) {
         for (int a = 0; a < 2; a++) {
@@ -2772,6 +2811,8 @@ int Engine::build() {
     // a repeated build() re-runs everything from the resident input (bench steps)
     for (Level* l : levels_) delete l;
     levels_.clear();
+    delete pending_;
+    pending_ = nullptr;
     dev_->reset_pool();
     built_ = true;
     prof_ = StageProfile();
@@ -2782,6 +2823,7 @@ int Engine::build() {
     const SlabGeom g = slab_geom(cfg_.sub_grid_dimension);
     if (g.tx * g.ty > kDenseTab)
         return fail(-22, "sub_grid_dimension too large for the LDS slot table (max 96)");
+    if (prior_ && (h0_ || max_levels_)) return fail(-22, "a merge cannot be split into level ranges");
     hierarchies_ = nbatches_ > 0 ? 1u : 0u;   // converter.rs:141-158 runs for every batch, even empty
     stats_ = BuildStats();
     if (n_ == 0) return 0;
@@ -2863,15 +2905,23 @@ int Engine::build() {
     int rc = level0_bin();   // also computes the bounding box (converter.rs:96-104)
     if (rc) return rc;
     stats_.ms_level0_bin = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    for (uint32_t h = 0;; h++) {
-        if (h >= kMaxDepth) return fail(-75, "hierarchy depth limit (31) reached: more than cell_point_overflow_limit duplicate points?");
+    for (uint32_t i = 0;; i++) {
+        if (h0_ + i >= kMaxDepth) return fail(-75, "hierarchy depth limit (31) reached: more than cell_point_overflow_limit duplicate points?");
         const auto tl = std::chrono::steady_clock::now();
-        rc = run_level(h);
+        rc = run_level(i);
         if (rc) return rc;
         stats_.ms_level.push_back(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tl).count());
-        if (levels_.size() == h + 1) break;   // no next level
+        if (levels_.size() == i + 1) break;   // no next level
+        if (max_levels_ && levels_.size() > max_levels_) {   // stop: the next level is exported, not built
+            pending_ = levels_.back();
+            levels_.pop_back();
+            stats_.arrivals -= pending_->arrivals;
+            stats_.cells -= pending_->ncells;
+            stats_.slabs -= pending_->nslabs;
+            break;
+        }
     }
-    hierarchies_ = std::max<uint32_t>(hierarchies_, (uint32_t)levels_.size());
+    hierarchies_ = std::max<uint32_t>(hierarchies_, h0_ + (uint32_t)levels_.size());
     stats_.levels = (uint32_t)levels_.size();
     if (profiling_) {
         ev_collect();
@@ -2905,7 +2955,7 @@ static void l0_pass(int p, int passes, Arena src, Arena dst, uint64_t n, const L
 
 int Engine::level0_bin() {
     const uint32_t dim = cfg_.sub_grid_dimension;
-    const float cs = cell_size(cfg_.max_cell_size, 0), csc = cell_size(cfg_.max_cell_size, 1);
+    const float cs = cell_size(cfg_.max_cell_size, h0_), csc = cell_size(cfg_.max_cell_size, h0_ + 1);
     L0Params P;
     P.cs = cs;
     P.cr = hex_radius(sub_cell_size(cs, dim));
@@ -3049,7 +3099,7 @@ int Engine::level0_bin() {
     Level* L = new Level();
     L->dev = dev_;
     levels_.push_back(L);
-    L->h = 0;
+    L->h = h0_;
     L->ncells = tots[2];
     L->nslabs = tots[1];
     L->arena = 0;
@@ -3068,6 +3118,15 @@ int Engine::level0_bin() {
         hist, cnt_scan, sflag, cflag, cscan, (uint32_t)D, (uint32_t)G, P, L->cell_idx, L->cell_sb, L->cell_slab0,
         L->slab_cell, L->slab_layer, L->slab_off, L->slab_n);
     k_set_u32<<<1, 1, 0, stream_>>>(L->cell_slab0 + L->ncells, L->nslabs);
+    if (!root_xyz_.empty() && L->ncells) {   // sub-tree build: the roots' spill batches
+        int32_t* rx = static_cast<int32_t*>(dev_->get(root_xyz_.size() * 4));
+        uint32_t* rs = static_cast<uint32_t*>(dev_->get(root_sb_.size() * 4));
+        HIP_CHECK(hipMemcpyAsync(rx, root_xyz_.data(), root_xyz_.size() * 4, hipMemcpyHostToDevice, stream_));
+        HIP_CHECK(hipMemcpyAsync(rs, root_sb_.data(), root_sb_.size() * 4, hipMemcpyHostToDevice, stream_));
+        k_root_sb<<<grid_for(L->ncells, 256, 1u << 30), 256, 0, stream_>>>(L->cell_idx, L->ncells, rx, rs,
+                                                                            (uint32_t)root_sb_.size(), L->cell_sb, dev_->ctr);
+        HIP_CHECK(hipGetLastError());
+    }
     if (prior_ && !pdev_.empty() && L->nslabs) {   // merge: each level-0 slab's record in the existing cloud
         L->alloc(L->slab_prior, L->nslabs);
         k_prior_lookup0<<<grid_for(L->nslabs, 256, 1u << 30), 256, 0, stream_>>>(
@@ -3124,8 +3183,9 @@ void Engine::run_dcap(Level* L) {
     HIP_CHECK(hipGetLastError());
 }
 
-int Engine::run_level(uint32_t h) {
-    Level* L = levels_[h];
+int Engine::run_level(uint32_t li) {
+    Level* L = levels_[li];
+    const uint32_t h = L->h;   // absolute level (h0_ + li)
     const uint32_t dim = cfg_.sub_grid_dimension;
     const SlabGeom g = slab_geom(dim);
     const float cs = cell_size(cfg_.max_cell_size, h), csc = cell_size(cfg_.max_cell_size, h + 1),
@@ -3457,6 +3517,49 @@ int Engine::built_cells(std::vector<int32_t>& hxyz) {
             hxyz.insert(hxyz.end(), idx.begin() + 3ull * c, idx.begin() + 3ull * c + 3);
         }
     }
+    return 0;
+}
+
+void Engine::set_root_spill_batches(const int32_t* xyz, const uint32_t* sb, uint64_t n) {
+    std::vector<uint64_t> ord(n);
+    for (uint64_t i = 0; i < n; i++) ord[i] = i;
+    std::sort(ord.begin(), ord.end(), [&](uint64_t a, uint64_t b) {
+        return std::lexicographical_compare(xyz + 3 * a, xyz + 3 * a + 3, xyz + 3 * b, xyz + 3 * b + 3);
+    });
+    root_xyz_.clear();
+    root_sb_.clear();
+    for (uint64_t i : ord) {
+        root_xyz_.insert(root_xyz_.end(), xyz + 3 * i, xyz + 3 * i + 3);
+        root_sb_.push_back(sb[i]);
+    }
+}
+
+int Engine::pending_info(uint64_t& ncells, uint64_t& npoints) const {
+    ncells = pending_ ? pending_->ncells : 0;
+    npoints = pending_ ? pending_->arrivals : 0;
+    return 0;
+}
+
+int Engine::export_pending(int32_t* xyz, uint32_t* sb, uint64_t* cell_n, Point* dpts, uint32_t* dkeys) {
+    if (!pending_) return 0;
+    Level* P = pending_;
+    const uint64_t mk = dev_->mark();
+    uint32_t* off = static_cast<uint32_t*>(dev_->get((uint64_t)P->nslabs * 4 + 16));
+    uint32_t* tot = static_cast<uint32_t*>(dev_->get(16));
+    scan_excl_u32(P->slab_n, off, P->nslabs, tot, dev_->scan, stream_);
+    if (P->nslabs)
+        k_export_slabs<<<std::min<uint32_t>(P->nslabs, 65536), 256, 0, stream_>>>(
+            dev_->ar[P->arena], P->slab_off, P->slab_n, off, P->nslabs, reinterpret_cast<float4*>(dpts), dkeys);
+    HIP_CHECK(hipGetLastError());
+    std::vector<uint32_t> slab0(P->ncells + 1ull), hoff(P->nslabs + 1ull);
+    HIP_CHECK(hipMemcpyAsync(xyz, P->cell_idx, 3ull * P->ncells * 4, hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipMemcpyAsync(sb, P->cell_sb, (uint64_t)P->ncells * 4, hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipMemcpyAsync(slab0.data(), P->cell_slab0, slab0.size() * 4, hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipMemcpyAsync(hoff.data(), off, (uint64_t)P->nslabs * 4, hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    hoff[P->nslabs] = (uint32_t)P->arrivals;
+    for (uint32_t c = 0; c < P->ncells; c++) cell_n[c] = hoff[slab0[c + 1]] - hoff[slab0[c]];
+    dev_->release(mk);
     return 0;
 }
 

@@ -33,7 +33,8 @@ EXPORTS = ["pcc_abi_version", "pcc_last_error", "pcc_options_default", "pcc_open
            "pcc_finish", "pcc_close", "pcc_get_stats", "pcc_set_profiling", "pcc_get_profile", "pcc_device_input",
            "pcc_convert_files", "pcc_shard_grid_from_bbox", "pcc_synth_device", "pcc_shard_bbox",
            "pcc_shard_histogram", "pcc_shard_route", "pcc_declare_files", "pcc_add_keyed_points_device",
-           "pcc_set_keyed_points_device",
+           "pcc_set_keyed_points_device", "pcc_set_level_range", "pcc_set_root_spill_batches",
+           "pcc_pending_cells", "pcc_export_pending",
            "pcc_set_summary", "pcc_write_cells", "pcc_write_metadata", "pcc_clear_input", "pcc_adopt_prior",
            "pcc_open_subtrees", "pcc_visit_cells"]
 
@@ -147,6 +148,10 @@ def lib():
         L.pcc_declare_files.argtypes = [vp, C.POINTER(C.c_uint64), C.c_uint64]
         L.pcc_add_keyed_points_device.argtypes = [vp, vp, vp, C.c_uint64]
         L.pcc_set_keyed_points_device.argtypes = [vp, vp, vp, C.c_uint64]
+        L.pcc_set_level_range.argtypes = [vp, C.c_uint32, C.c_uint32]
+        L.pcc_set_root_spill_batches.argtypes = [vp, vp, vp, C.c_uint64]
+        L.pcc_pending_cells.argtypes = [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+        L.pcc_export_pending.argtypes = [vp, vp, vp, vp, vp, vp]
         L.pcc_set_summary.argtypes = [vp, C.c_uint64, f3, f3, C.c_uint32]
         L.pcc_write_cells.argtypes = [vp]
         L.pcc_write_metadata.argtypes = [vp]
@@ -231,6 +236,30 @@ class Converter:
 
     def add_keyed_points_device(self, pts_ptr: int, keys_ptr: int, n: int):
         _check(lib().pcc_add_keyed_points_device(self._h, C.c_void_p(pts_ptr), C.c_void_p(keys_ptr), n))
+
+    def set_level_range(self, root_level: int, max_levels: int):
+        _check(lib().pcc_set_level_range(self._h, root_level, max_levels))
+
+    def set_root_spill_batches(self, cells_xyz, spill_batch):
+        xyz = np.ascontiguousarray(cells_xyz, dtype=np.int32).reshape(-1, 3)
+        sb = np.ascontiguousarray(spill_batch, dtype=np.uint32).reshape(-1)
+        _check(lib().pcc_set_root_spill_batches(self._h, xyz.ctypes.data, sb.ctypes.data, len(sb)))
+
+    def pending_cells(self) -> tuple[int, int]:
+        nc, npt = C.c_uint64(0), C.c_uint64(0)
+        _check(lib().pcc_pending_cells(self._h, C.byref(nc), C.byref(npt)))
+        return nc.value, npt.value
+
+    def export_pending(self, pts_ptr: int, keys_ptr: int):
+        """(cells (n,3) int32, spill batches (n,) uint32, points per cell (n,)
+        uint64); the arrivals go to the device buffers (pending_cells()[1] each)."""
+        nc, _ = self.pending_cells()
+        xyz = np.zeros((nc, 3), dtype=np.int32)
+        sb = np.zeros(nc, dtype=np.uint32)
+        cn = np.zeros(nc, dtype=np.uint64)
+        _check(lib().pcc_export_pending(self._h, xyz.ctypes.data, sb.ctypes.data, cn.ctypes.data, C.c_void_p(pts_ptr),
+                                        C.c_void_p(keys_ptr)))
+        return xyz, sb, cn
 
     def set_keyed_points_device(self, pts_ptr: int, keys_ptr: int, n: int):
         """Borrow (no copy) this rank's keyed input until build() returns."""
