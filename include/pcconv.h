@@ -208,6 +208,24 @@ int pcc_shard_route(const pcc_point* dev_pts, uint64_t n, uint32_t key0, const p
                     const uint32_t* dev_owner, uint32_t nranks, pcc_point* dev_send, uint32_t* dev_keys,
                     uint64_t* counts, int device);
 
+/* Slab sharding of heavy level-0 cells: the unit is the level-0 slab (cell,
+ * hex z-layer) -- unit id = cell id * PCC_SHARD_LAYERS + the layer's offset in
+ * its cell, t - (2 * sub_grid_dimension * iz - 2) with t = trunc(z / r0)
+ * (hex.rs:83; r0 = level-0 sub_cell_size / 2).  A slab's slots are resolved
+ * on one rank (cell.rs:70-94 is per slot).  dev_hist / dev_owner hold
+ * ncells * PCC_SHARD_LAYERS entries. */
+#define PCC_SHARD_LAYERS 256
+int pcc_shard_slab_histogram(const pcc_point* dev_pts, uint64_t n, const pcc_shard_grid* g, uint32_t sub_grid_dimension,
+                             uint32_t* dev_hist, int device);
+int pcc_shard_route_slabs(const pcc_point* dev_pts, uint64_t n, uint32_t key0, const pcc_shard_grid* g,
+                          uint32_t sub_grid_dimension, const uint32_t* dev_owner, uint32_t nranks, pcc_point* dev_send,
+                          uint32_t* dev_keys, uint64_t* counts, int device);
+
+/* Writes one cell file h_{hierarchy}/c_x_y_z.bin under out_dir from a view
+ * (Cell::write_to cell.rs:155-181): a cell assembled by the caller from the
+ * pieces several ranks built. */
+int pcc_write_cell_view(const char* out_dir, const pcc_cell_view* v);
+
 /* Global file structure (points per input file, CLI order; lib.rs:31-52
  * batching) without points.  Switches the converter to keyed input. */
 int pcc_declare_files(pcc_converter* c, const uint64_t* file_points, uint64_t nfiles);
@@ -230,8 +248,11 @@ int pcc_set_keyed_points_device(pcc_converter* c, const pcc_point* dev_pts, cons
  * their global event keys), with the parent buckets' spill batches from
  * pcc_set_root_spill_batches; cells are written as h_{h0}, h_{h0+1}, ...
  * max_levels m > 0: build levels h0 .. h0+m-1 only and keep the next level's
- * arrivals on the device for pcc_export_pending.  Not for merges. */
-int pcc_set_level_range(pcc_converter* c, uint32_t root_level, uint32_t max_levels);
+ * arrivals on the device for pcc_export_pending.  raw_buckets != 0: the last
+ * built level keeps no overflow lists and forwards every emission (its cells
+ * are partial: the caller resolves their buckets, cell.rs:108-153, from all
+ * ranks' emissions and assembles the cell files).  Not for merges. */
+int pcc_set_level_range(pcc_converter* c, uint32_t root_level, uint32_t max_levels, int raw_buckets);
 int pcc_set_root_spill_batches(pcc_converter* c, const int32_t* cells_xyz, const uint32_t* spill_batch, uint64_t ncells);
 /* After pcc_build with max_levels: the cells of the first level not built. */
 int pcc_pending_cells(pcc_converter* c, uint64_t* ncells, uint64_t* npoints);

@@ -55,6 +55,13 @@ def lib():
         L.orc_hierarchies.restype = C.c_uint32
         L.orc_synth.argtypes = [C.c_uint64, C.c_int, C.c_uint64, C.c_uint64, C.c_float, C.c_float, C.c_void_p]
         L.orc_load.argtypes = [C.c_void_p, C.c_char_p]
+        L.orc_set_level_range.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32]
+        L.orc_pending_count.argtypes = [C.c_void_p]
+        L.orc_pending_count.restype = C.c_uint64
+        L.orc_pending_get.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.orc_add_batch_raw0.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]
+        L.orc_cell_get.argtypes = [C.c_void_p, C.c_uint64, C.POINTER(C.c_int32), C.POINTER(C.c_uint32)]
+        L.orc_cell_grid.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p]
         L.orc_load.restype = C.c_int
         # canonical digests (digest.c)
         L.dg_new.restype = C.c_void_p
@@ -95,6 +102,42 @@ class Oracle:
     def add_batch(self, pts: np.ndarray):
         pts = np.ascontiguousarray(pts, dtype=POINT_DTYPE)
         lib().orc_add_batch(self._h, pts.ctypes.data, len(pts))
+
+    def set_level_range(self, root: int, max_levels: int):
+        """Batches enter at level `root`; with max_levels > 0 the points forwarded
+        to level root+max_levels are recorded (pending()) instead of added."""
+        lib().orc_set_level_range(self._h, root, max_levels)
+
+    def pending(self, with_keys: bool = False):
+        """(points, batch number per point, level cell (n,3)[, causing keys]) in
+        forwarding order (keys only from add_batch_raw0)."""
+        n = lib().orc_pending_count(self._h)
+        p = np.zeros(n, dtype=POINT_DTYPE)
+        b = np.zeros(n, dtype=np.uint32)
+        xyz = np.zeros((n, 3), dtype=np.int32)
+        k = np.zeros(n, dtype=np.uint32)
+        if n:
+            lib().orc_pending_get(self._h, p.ctypes.data, b.ctypes.data, xyz.ctypes.data, k.ctypes.data)
+        return (p, b, xyz, k) if with_keys else (p, b, xyz)
+
+    def cells(self):
+        """[(h, (x, y, z), grid points)] of every cell (grid only: for raw level-0 pieces)."""
+        out = []
+        hx, cnt = (C.c_int32 * 4)(), (C.c_uint32 * 3)()
+        for i in range(self.num_cells):
+            lib().orc_cell_get(self._h, i, hx, cnt)
+            g = np.zeros(cnt[1], dtype=POINT_DTYPE)
+            if cnt[1]:
+                lib().orc_cell_grid(self._h, i, g.ctypes.data)
+            out.append((hx[0], (hx[1], hx[2], hx[3]), g))
+        return out
+
+    def add_batch_raw0(self, pts: np.ndarray, keys: np.ndarray):
+        """Level 0 only, no overflow lists: every emission becomes pending with
+        the key of the arrival that caused it."""
+        pts = np.ascontiguousarray(pts, dtype=POINT_DTYPE)
+        keys = np.ascontiguousarray(keys, dtype=np.uint32)
+        lib().orc_add_batch_raw0(self._h, pts.ctypes.data, keys.ctypes.data, len(pts))
 
     def load(self, out_dir: str):
         """Existing converted cloud as the starting state (lib.rs:86-101 +

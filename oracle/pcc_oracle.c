@@ -201,6 +201,13 @@ typedef struct {
     cell** cellv; size_t ncells, capcells;
     int error;         /* 1 = hierarchy depth limit reached */
     uint64_t arrivals; /* sum over levels of points handed to cells (W) */
+    /* level range (test double of the split sharded build): batches enter at
+     * level `root`; with maxl > 0 the points forwarded to level root+maxl are
+     * recorded (point, batch number, cell) instead of being added */
+    uint32_t root, maxl;
+    uint32_t batch_no;
+    struct pend { orc_point p; uint32_t batch; ivec3 idx; uint32_t key; } *pend;
+    size_t npend, cappend;
 } orc_conv;
 
 orc_conv* orc_new(const orc_config* cfg) {
@@ -217,7 +224,33 @@ void orc_free(orc_conv* c) {
         for (int j = 0; j < k->nb; j++) pl_free(&k->b[j].pts);
         free(k);
     }
-    free(c->cellv); hm_free(&c->cells); free(c);
+    free(c->cellv); hm_free(&c->cells); free(c->pend); free(c);
+}
+
+void orc_set_level_range(orc_conv* c, uint32_t root, uint32_t maxl) {
+    c->root = root;
+    c->maxl = maxl;
+    if (c->hierarchies < root) c->hierarchies = root;
+}
+uint64_t orc_pending_count(const orc_conv* c) { return c->npend; }
+static void pend_push(orc_conv* c, orc_point p, ivec3 idx, uint32_t key) {
+    if (c->npend == c->cappend) {
+        c->cappend = c->cappend ? 2 * c->cappend : 1024;
+        c->pend = (struct pend*)realloc(c->pend, c->cappend * sizeof(*c->pend));
+    }
+    c->pend[c->npend].p = p;
+    c->pend[c->npend].batch = c->batch_no;
+    c->pend[c->npend].idx = idx;
+    c->pend[c->npend].key = key;
+    c->npend++;
+}
+void orc_pending_get(const orc_conv* c, orc_point* p, uint32_t* batch, int32_t* xyz, uint32_t* key) {
+    for (size_t i = 0; i < c->npend; i++) {
+        p[i] = c->pend[i].p;
+        batch[i] = c->pend[i].batch;
+        if (key) key[i] = c->pend[i].key;
+        xyz[3 * i] = c->pend[i].idx.x; xyz[3 * i + 1] = c->pend[i].idx.y; xyz[3 * i + 2] = c->pend[i].idx.z;
+    }
 }
 
 /* converter.rs:187-207 (create branch) + cell.rs:43-49 + Header::new cell.rs:264-274 */
@@ -328,6 +361,12 @@ static void cell_add_overflow(orc_conv* c, cell* k, groups* og, groups* next) {
 /* converter.rs:114-139 add_points_in_hierarchy (iterative over levels) */
 static void add_points_in_hierarchy(orc_conv* c, uint32_t h, groups* cur) {
     for (;;) {
+        if (c->maxl && h >= c->root + c->maxl) { /* level range: record, do not add */
+            for (size_t gi = 0; gi < cur->n; gi++)
+                for (size_t i = 0; i < cur->g[gi].pts.len; i++) pend_push(c, cur->g[gi].pts.p[i], cur->g[gi].idx, 0);
+            groups_free(cur);
+            return;
+        }
         if (h >= 31) { c->error = 1; return; } /* reference overflows 2u32.pow(h) at h=32 */
         if (c->hierarchies <= h) c->hierarchies += 1; /* converter.rs:141-145 */
         groups next; groups_init(&next);
@@ -367,8 +406,26 @@ void orc_add_batch(orc_conv* c, const orc_point* p, uint64_t n) {
     }
     c->number_of_points += n;
     groups g; groups_init(&g);
-    group_points(&g, p, (size_t)n, orc_cell_size(&c->cfg, 0));
-    add_points_in_hierarchy(c, 0, &g);
+    group_points(&g, p, (size_t)n, orc_cell_size(&c->cfg, c->root));
+    add_points_in_hierarchy(c, c->root, &g);
+    c->batch_no++;
+}
+
+/* Level 0 of one batch with no overflow lists (test double of the raw level of
+ * pcc_set_level_range(0, 1, raw) on a rank holding some slabs of a shared
+ * cell): cell.rs:70-94 per point, every emission recorded as pending with its
+ * level-1 cell and the key of the arrival that caused it. */
+void orc_add_batch_raw0(orc_conv* c, const orc_point* p, const uint32_t* keys, uint64_t n) {
+    const float cs = orc_cell_size(&c->cfg, 0), ccs = orc_cell_size(&c->cfg, 1);
+    if (c->hierarchies < 1) c->hierarchies = 1;   /* converter.rs:141-145 */
+    c->number_of_points += n;
+    for (uint64_t i = 0; i < n; i++) {
+        cell* k = get_cell(c, 0, orc_cell_index(p[i].x, p[i].y, p[i].z, cs));
+        c->arrivals += 1;
+        orc_point o;
+        if (cell_add_point(k, p[i], &o)) pend_push(c, o, orc_cell_index(o.x, o.y, o.z, ccs), keys[i]);
+    }
+    c->batch_no++;
 }
 
 /* lib.rs:31-52: one input file = consecutive get_batch(batch) calls until empty */
@@ -379,6 +436,16 @@ void orc_add_file(orc_conv* c, const orc_point* p, uint64_t n, uint32_t batch) {
         orc_add_batch(c, p + off, m);
         off += m;
     } while (off < n);
+}
+
+/* cell i (creation order): hxyz = (h, x, y, z), cnt = (total, number, overflow) */
+void orc_cell_get(const orc_conv* c, uint64_t i, int32_t hxyz[4], uint32_t cnt[3]) {
+    const cell* k = c->cellv[i];
+    hxyz[0] = (int32_t)k->h; hxyz[1] = k->idx.x; hxyz[2] = k->idx.y; hxyz[3] = k->idx.z;
+    cnt[0] = k->total; cnt[1] = k->number; cnt[2] = k->overflow;
+}
+void orc_cell_grid(const orc_conv* c, uint64_t i, orc_point* out) {
+    memcpy(out, c->cellv[i]->gpts.p, c->cellv[i]->gpts.len * sizeof(orc_point));
 }
 
 int orc_error(const orc_conv* c) { return c->error; }

@@ -437,6 +437,42 @@ int pcc_shard_route(const pcc_point* d, uint64_t n, uint32_t key0, const pcc_sha
     GUARD_END
 }
 
+int pcc_shard_slab_histogram(const pcc_point* d, uint64_t n, const pcc_shard_grid* g, uint32_t sub_grid_dimension,
+                             uint32_t* dhist, int device) {
+    if ((!d && n) || !g || !dhist) return set_err(-EINVAL, "null argument");
+    if (sub_grid_dimension == 0 || 2 * sub_grid_dimension + 2 > PCC_SHARD_LAYERS)
+        return set_err(-EINVAL, "sub_grid_dimension out of range for slab sharding");
+    GUARD_BEGIN
+    const int rc = shard_histogram(reinterpret_cast<const Point*>(d), n, to_grid(g), dhist, device, sub_grid_dimension);
+    return rc ? set_err(rc, "point outside the shard grid (grid not spanned by the global bbox?)") : 0;
+    GUARD_END
+}
+
+int pcc_shard_route_slabs(const pcc_point* d, uint64_t n, uint32_t key0, const pcc_shard_grid* g,
+                          uint32_t sub_grid_dimension, const uint32_t* downer, uint32_t nranks, pcc_point* dsend,
+                          uint32_t* dkeys, uint64_t* counts, int device) {
+    if ((!d || !dsend || !dkeys) && n) return set_err(-EINVAL, "null argument");
+    if (!g || !downer || !counts) return set_err(-EINVAL, "null argument");
+    if (sub_grid_dimension == 0 || 2 * sub_grid_dimension + 2 > PCC_SHARD_LAYERS)
+        return set_err(-EINVAL, "sub_grid_dimension out of range for slab sharding");
+    if ((uint64_t)key0 + n > (1ull << 32)) return set_err(-EOVERFLOW, "global keys must fit in 32 bits");
+    GUARD_BEGIN
+    const int rc = shard_route(reinterpret_cast<const Point*>(d), n, key0, to_grid(g), downer, nranks,
+                               reinterpret_cast<Point*>(dsend), dkeys, counts, device, sub_grid_dimension);
+    return rc ? set_err(rc, "routing failed (nranks > 64, point outside grid, or owner >= nranks)") : 0;
+    GUARD_END
+}
+
+int pcc_write_cell_view(const char* out_dir, const pcc_cell_view* v) {
+    if (!out_dir || !v) return set_err(-EINVAL, "null argument");
+    if (v->entries > 8) return set_err(-EINVAL, "a cell has at most 8 overflow entries");
+    GUARD_BEGIN
+    std::string err;
+    const int rc = write_view_file(out_dir, *v, err);
+    return rc ? set_err(rc, err) : 0;
+    GUARD_END
+}
+
 int pcc_declare_files(pcc_converter* c, const uint64_t* file_points, uint64_t nfiles) {
     if (!c || (!file_points && nfiles)) return set_err(-EINVAL, "null argument");
     if (c->built) return set_err(-EINVAL, "files declared after build");
@@ -470,12 +506,12 @@ int pcc_set_keyed_points_device(pcc_converter* c, const pcc_point* d, const uint
     GUARD_END
 }
 
-int pcc_set_level_range(pcc_converter* c, uint32_t root_level, uint32_t max_levels) {
+int pcc_set_level_range(pcc_converter* c, uint32_t root_level, uint32_t max_levels, int raw_buckets) {
     if (!c) return set_err(-EINVAL, "null argument");
     if (c->merge) return set_err(-EINVAL, "a merge cannot be split into level ranges");
     if (root_level >= 31) return set_err(-EINVAL, "root level must be < 31");
     c->eng->set_root_level(root_level);
-    c->eng->set_max_levels(max_levels);
+    c->eng->set_max_levels(max_levels, raw_buckets != 0);
     return 0;
 }
 

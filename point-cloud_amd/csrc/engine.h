@@ -144,7 +144,9 @@ public:
     // (contiguous, slab order, each slab in key order) with the spill batch of
     // its parent bucket.  set_root_level(h0) + set_root_spill_batches(): build
     // a sub-tree whose input is such exported arrivals of level-h0 cells.
-    void set_max_levels(uint32_t m) { max_levels_ = m; }
+    // raw: the last built level forwards every emission (no bucket lists; the
+    // caller resolves those buckets, e.g. across the ranks sharing a cell)
+    void set_max_levels(uint32_t m, bool raw = false);
     void set_root_level(uint32_t h0) { h0_ = h0; }
     void set_root_spill_batches(const int32_t* xyz, const uint32_t* sb, uint64_t n);
     int pending_info(uint64_t& ncells, uint64_t& npoints) const;
@@ -204,6 +206,7 @@ private:
     Point* d_in_ = nullptr;
     uint32_t* d_keys_ = nullptr;         // keyed (sharded) input: global key per point
     uint32_t h0_ = 0, max_levels_ = 0;   // level range (set_root_level / set_max_levels)
+    bool raw_last_ = false;
     Level* pending_ = nullptr;           // the first level not built (max_levels_)
     std::vector<int32_t> root_xyz_;      // root cells (sorted) and their spill batches
     std::vector<uint32_t> root_sb_;
@@ -259,8 +262,9 @@ struct ShardGrid {
 };
 int shard_synth(Point* dst, uint64_t idx0, uint64_t n, uint64_t seed, int kind, float lo, float ext, int device);
 int shard_bbox(const Point* d, uint64_t n, float bmin[3], float bmax[3], int device);
-int shard_histogram(const Point* d, uint64_t n, const ShardGrid& g, uint32_t* dhist, int device);
+// dim > 0: slab mode, unit = cell * 256 + level-0 hex z-layer of a dim sub-grid
+int shard_histogram(const Point* d, uint64_t n, const ShardGrid& g, uint32_t* dhist, int device, uint32_t dim = 0);
 int shard_route(const Point* d, uint64_t n, uint32_t key0, const ShardGrid& g, const uint32_t* downer, uint32_t nranks,
-                Point* dsend, uint32_t* dkeys, uint64_t* counts, int device);
+                Point* dsend, uint32_t* dkeys, uint64_t* counts, int device, uint32_t dim = 0);
 
 }  // namespace pcc

@@ -3372,7 +3372,9 @@ int Engine::run_level(uint32_t li) {
     BP.bkt_nd = L->bkt_nd;
     BP.room = inject ? L->room : nullptr;
     BP.ctr = dev_->ctr;
-    BP.L = cfg_.cell_point_overflow_limit;
+    // raw last level (set_max_levels(m, raw)): every bucket forwards all its
+    // emissions (limit 0), the caller resolves the buckets across ranks
+    BP.L = (raw_last_ && max_levels_ && li + 1 == max_levels_) ? 0u : cfg_.cell_point_overflow_limit;
     const uint32_t nb = 8 * L->ncells;
     ev_begin(ST_BUCKET);
     k_bucket<<<nb, kBktBS, 0, stream_>>>(BP);
@@ -3518,6 +3520,11 @@ int Engine::built_cells(std::vector<int32_t>& hxyz) {
         }
     }
     return 0;
+}
+
+void Engine::set_max_levels(uint32_t m, bool raw) {
+    max_levels_ = m;
+    raw_last_ = raw && m;
 }
 
 void Engine::set_root_spill_batches(const int32_t* xyz, const uint32_t* sb, uint64_t n) {
@@ -3686,11 +3693,27 @@ __device__ __forceinline__ uint32_t shard_cell(const ShardGrid& g, float x, floa
     return in ? ((uint32_t)ix * g.dims[1] + (uint32_t)iy) * g.dims[2] + (uint32_t)iz : 0xFFFFFFFFu;
 }
 
+// Slab mode (dim2 > 0): the unit is the level-0 slab, id = cell * kL0Layers +
+// local hex z-layer, the layer exactly as the engine's level-0 binning computes
+// it (l0_layer: t = trunc(z / r0), minus the cell's first layer dim2*iz - 2).
+struct ShardSlabs {
+    float cr;        // level-0 hex radius (0: cell mode)
+    int32_t dim2;    // 2 * sub_grid_dimension
+};
+__device__ __forceinline__ uint32_t shard_unit(const ShardGrid& g, const ShardSlabs& m, float x, float y, float z) {
+    const uint32_t c = shard_cell(g, x, y, z);
+    if (m.dim2 == 0 || c == 0xFFFFFFFFu) return c;
+    const int32_t iz = cell_index1(z, g.cs);
+    const int64_t ll = (int64_t)sat_i32(z / m.cr) - ((int64_t)m.dim2 * iz - 2);
+    if (ll < 0 || ll >= (int64_t)kL0Layers) return 0xFFFFFFFFu;
+    return c * kL0Layers + (uint32_t)ll;
+}
+
 constexpr int kShBS = 256;
 // per-block LDS histogram (ncells <= kShLds), else global atomics
 constexpr uint32_t kShLds = 8192;
 __global__ __launch_bounds__(kShBS) void k_shard_hist(const Point* __restrict__ in, uint64_t n, ShardGrid g,
-                                                      uint32_t ncells, uint32_t* hist, uint32_t* bad) {
+                                                      ShardSlabs m, uint32_t ncells, uint32_t* hist, uint32_t* bad) {
     __shared__ uint32_t h[kShLds];
     const bool lds = ncells <= kShLds;
     if (lds)
@@ -3700,7 +3723,7 @@ __global__ __launch_bounds__(kShBS) void k_shard_hist(const Point* __restrict__ 
     uint32_t nbad = 0;
     for (uint64_t i = blockIdx.x * (uint64_t)kShBS + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kShBS) {
         const float4 v = p4[i];
-        const uint32_t c = shard_cell(g, v.x, v.y, v.z);
+        const uint32_t c = shard_unit(g, m, v.x, v.y, v.z);
         if (c == 0xFFFFFFFFu) { nbad++; continue; }
         if (lds) atomicAdd(&h[c], 1u); else atomicAdd(&hist[c], 1u);
     }
@@ -3713,7 +3736,7 @@ __global__ __launch_bounds__(kShBS) void k_shard_hist(const Point* __restrict__ 
 
 // owner rank per point (sort key) and its local index (payload)
 __global__ __launch_bounds__(kShBS) void k_shard_owner(const Point* __restrict__ in, uint32_t n, ShardGrid g,
-                                                       const uint32_t* __restrict__ owner, uint32_t nranks,
+                                                       ShardSlabs m, const uint32_t* __restrict__ owner, uint32_t nranks,
                                                        uint32_t* ow, uint32_t* idx, uint32_t* cnt, uint32_t* bad) {
     __shared__ uint32_t c[64];
     if (threadIdx.x < 64) c[threadIdx.x] = 0;
@@ -3721,7 +3744,7 @@ __global__ __launch_bounds__(kShBS) void k_shard_owner(const Point* __restrict__
     const float4* p4 = reinterpret_cast<const float4*>(in);
     for (uint32_t i = blockIdx.x * kShBS + threadIdx.x; i < n; i += gridDim.x * kShBS) {
         const float4 v = p4[i];
-        const uint32_t cl = shard_cell(g, v.x, v.y, v.z);
+        const uint32_t cl = shard_unit(g, m, v.x, v.y, v.z);
         uint32_t r = cl == 0xFFFFFFFFu ? 0xFFFFFFFFu : owner[cl];
         if (r >= nranks) { atomicOr(bad, 1u); r = 0; }
         ow[i] = r;
@@ -3769,12 +3792,20 @@ int shard_bbox(const Point* d, uint64_t n, float bmin[3], float bmax[3], int dev
     return 0;
 }
 
-int shard_histogram(const Point* d, uint64_t n, const ShardGrid& g, uint32_t* dhist, int device) {
+static ShardSlabs shard_slabs(const ShardGrid& g, uint32_t dim) {
+    ShardSlabs m;
+    m.cr = dim ? hex_radius(sub_cell_size(g.cs, dim)) : 0.0f;
+    m.dim2 = 2 * (int32_t)dim;
+    return m;
+}
+
+int shard_histogram(const Point* d, uint64_t n, const ShardGrid& g, uint32_t* dhist, int device, uint32_t dim) {
     ShardScratch& S = shard_scratch(device);
-    const uint64_t nc = (uint64_t)g.dims[0] * g.dims[1] * g.dims[2];
+    const uint64_t nc = (uint64_t)g.dims[0] * g.dims[1] * g.dims[2] * (dim ? kL0Layers : 1u);
+    if (nc >= (1ull << 32)) return -EOVERFLOW;
     HIP_CHECK(hipMemsetAsync(dhist, 0, nc * 4, S.st));
     HIP_CHECK(hipMemsetAsync(S.flag, 0, 4, S.st));
-    if (n) k_shard_hist<<<grid_for(n, kShBS, 1024), kShBS, 0, S.st>>>(d, n, g, (uint32_t)nc, dhist, S.flag);
+    if (n) k_shard_hist<<<grid_for(n, kShBS, 1024), kShBS, 0, S.st>>>(d, n, g, shard_slabs(g, dim), (uint32_t)nc, dhist, S.flag);
     HIP_CHECK(hipGetLastError());
     uint32_t bad = 0;
     HIP_CHECK(hipMemcpyAsync(&bad, S.flag, 4, hipMemcpyDeviceToHost, S.st));
@@ -3783,7 +3814,7 @@ int shard_histogram(const Point* d, uint64_t n, const ShardGrid& g, uint32_t* dh
 }
 
 int shard_route(const Point* d, uint64_t n, uint32_t key0, const ShardGrid& g, const uint32_t* downer, uint32_t nranks,
-                Point* dsend, uint32_t* dkeys, uint64_t* counts, int device) {
+                Point* dsend, uint32_t* dkeys, uint64_t* counts, int device, uint32_t dim) {
     ShardScratch& S = shard_scratch(device);
     if (nranks == 0 || nranks > 64) return -EINVAL;
     if (n >= (1ull << 32)) return -EOVERFLOW;
@@ -3796,7 +3827,8 @@ int shard_route(const Point* d, uint64_t n, uint32_t key0, const ShardGrid& g, c
     uint32_t hc[64] = {};
     if (n) {
         const uint32_t n32 = (uint32_t)n;
-        k_shard_owner<<<grid_for(n, kShBS, 4096), kShBS, 0, S.st>>>(d, n32, g, downer, nranks, S.buf[0], S.buf[1], S.cnt, S.flag);
+        k_shard_owner<<<grid_for(n, kShBS, 4096), kShBS, 0, S.st>>>(d, n32, g, shard_slabs(g, dim), downer, nranks,
+                                                                     S.buf[0], S.buf[1], S.cnt, S.flag);
         int bits = 0;
         while ((1u << bits) < nranks) bits++;
         int which = 0;

@@ -243,6 +243,46 @@ void level_cell_view(const Config& cfg, const LevelHost& L, uint32_t c, const Po
     v.pos[2] = cell_pos1(v.z, size);
 }
 
+// Cell::write_to cell.rs:155-181 with Header::write_to :280-298, from a view.
+void serialize_view(const pcc_cell_view& v, std::string& buf) {
+    buf.clear();
+    buf.reserve(48 + 16ull * v.total_number_of_points + 1 + 16 * v.entries);
+    put32(buf, v.hierarchy);
+    put32(buf, (uint32_t)v.x); put32(buf, (uint32_t)v.y); put32(buf, (uint32_t)v.z);
+    put32(buf, v.total_number_of_points);
+    put32(buf, v.number_of_points);
+    put32(buf, v.number_of_overflow_points);
+    putf(buf, v.size);
+    putf(buf, v.sub_cell_size);
+    putf(buf, v.pos[0]); putf(buf, v.pos[1]); putf(buf, v.pos[2]);
+    // grid points (cell.rs:158-160; order free)
+    buf.append(reinterpret_cast<const char*>(v.grid), 16ull * v.number_of_points);
+    buf.push_back((char)(uint8_t)v.entries);   // cell.rs:162
+    for (uint32_t e = 0; e < v.entries; e++) {
+        put32(buf, (uint32_t)v.child[e][0]);
+        put32(buf, (uint32_t)v.child[e][1]);
+        put32(buf, (uint32_t)v.child[e][2]);
+        put32(buf, v.count[e]);
+        if (v.count[e]) buf.append(reinterpret_cast<const char*>(v.list[e]), 16ull * v.count[e]);
+    }
+}
+
+int write_view_file(const std::string& dir, const pcc_cell_view& v, std::string& err) {
+    const std::string hd = dir + "/h_" + std::to_string(v.hierarchy);
+    if (mkdir(dir.c_str(), 0755) != 0 && errno != EEXIST) { err = "cannot create " + dir; return -EIO; }
+    if (mkdir(hd.c_str(), 0755) != 0 && errno != EEXIST) { err = "cannot create " + hd; return -EIO; }
+    std::string buf;
+    serialize_view(v, buf);
+    char name[96];
+    snprintf(name, sizeof name, "/c_%d_%d_%d.bin", v.x, v.y, v.z);
+    const std::string path = hd + name;
+    FILE* fp = fopen(path.c_str(), "wb");
+    bool ok = fp != nullptr;
+    if (ok) { ok = fwrite(buf.data(), 1, buf.size(), fp) == buf.size(); ok = (fclose(fp) == 0) && ok; }
+    if (!ok) { err = "cannot write " + path; return -EIO; }
+    return 0;
+}
+
 // Cell files of one level (Cell::write_to cell.rs:155-181, Header::write_to
 // :280-298), cells split over `nthreads` host threads (files are independent).
 int write_level_cells(const std::string& dir, const Config& cfg, const LevelHost& L, const Point* grid,
@@ -259,26 +299,7 @@ int write_level_cells(const std::string& dir, const Config& cfg, const LevelHost
             const uint32_t c = next.fetch_add(1);
             if (c >= ncells || rc.load() != 0) return;
             level_cell_view(cfg, L, c, grid, kept, v);
-            buf.clear();
-            buf.reserve(48 + 16ull * v.total_number_of_points + 1 + 16 * v.entries);
-            put32(buf, v.hierarchy);
-            put32(buf, (uint32_t)v.x); put32(buf, (uint32_t)v.y); put32(buf, (uint32_t)v.z);
-            put32(buf, v.total_number_of_points);
-            put32(buf, v.number_of_points);
-            put32(buf, v.number_of_overflow_points);
-            putf(buf, v.size);
-            putf(buf, v.sub_cell_size);
-            putf(buf, v.pos[0]); putf(buf, v.pos[1]); putf(buf, v.pos[2]);
-            // grid points (cell.rs:158-160; order free)
-            buf.append(reinterpret_cast<const char*>(v.grid), 16ull * v.number_of_points);
-            buf.push_back((char)(uint8_t)v.entries);   // cell.rs:162
-            for (uint32_t e = 0; e < v.entries; e++) {
-                put32(buf, (uint32_t)v.child[e][0]);
-                put32(buf, (uint32_t)v.child[e][1]);
-                put32(buf, (uint32_t)v.child[e][2]);
-                put32(buf, v.count[e]);
-                if (v.count[e]) buf.append(reinterpret_cast<const char*>(v.list[e]), 16ull * v.count[e]);
-            }
+            serialize_view(v, buf);
             const int32_t ix = v.x, iy = v.y, iz = v.z;
             char name[96];
             snprintf(name, sizeof name, "/h_%u/c_%d_%d_%d.bin", h, ix, iy, iz);

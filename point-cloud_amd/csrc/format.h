@@ -35,6 +35,9 @@ int make_output_dirs(const std::string& dir, uint32_t hierarchies, std::string& 
 void level_cell_view(const Config& cfg, const LevelHost& L, uint32_t c, const Point* grid, const Point* kept,
                      pcc_cell_view& v);
 // Cell files of one level, split over nthreads host threads.
+// One cell file from a view (h_{h}/c_x_y_z.bin under dir; folders created).
+void serialize_view(const pcc_cell_view& v, std::string& buf);
+int write_view_file(const std::string& dir, const pcc_cell_view& v, std::string& err);
 int write_level_cells(const std::string& dir, const Config& cfg, const LevelHost& L, const Point* grid,
                       const Point* kept, unsigned nthreads, std::string& err);
 unsigned writer_threads();   // PCC_WRITE_THREADS, else min(16, hardware threads)

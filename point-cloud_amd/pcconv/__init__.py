@@ -34,7 +34,8 @@ EXPORTS = ["pcc_abi_version", "pcc_last_error", "pcc_options_default", "pcc_open
            "pcc_convert_files", "pcc_shard_grid_from_bbox", "pcc_synth_device", "pcc_shard_bbox",
            "pcc_shard_histogram", "pcc_shard_route", "pcc_declare_files", "pcc_add_keyed_points_device",
            "pcc_set_keyed_points_device", "pcc_set_level_range", "pcc_set_root_spill_batches",
-           "pcc_pending_cells", "pcc_export_pending",
+           "pcc_pending_cells", "pcc_export_pending", "pcc_shard_slab_histogram", "pcc_shard_route_slabs",
+           "pcc_write_cell_view",
            "pcc_set_summary", "pcc_write_cells", "pcc_write_metadata", "pcc_clear_input", "pcc_adopt_prior",
            "pcc_open_subtrees", "pcc_visit_cells"]
 
@@ -148,7 +149,11 @@ def lib():
         L.pcc_declare_files.argtypes = [vp, C.POINTER(C.c_uint64), C.c_uint64]
         L.pcc_add_keyed_points_device.argtypes = [vp, vp, vp, C.c_uint64]
         L.pcc_set_keyed_points_device.argtypes = [vp, vp, vp, C.c_uint64]
-        L.pcc_set_level_range.argtypes = [vp, C.c_uint32, C.c_uint32]
+        L.pcc_set_level_range.argtypes = [vp, C.c_uint32, C.c_uint32, C.c_int]
+        L.pcc_shard_slab_histogram.argtypes = [vp, C.c_uint64, C.POINTER(ShardGrid), C.c_uint32, vp, C.c_int]
+        L.pcc_shard_route_slabs.argtypes = [vp, C.c_uint64, C.c_uint32, C.POINTER(ShardGrid), C.c_uint32, vp,
+                                            C.c_uint32, vp, vp, C.POINTER(C.c_uint64), C.c_int]
+        L.pcc_write_cell_view.argtypes = [C.c_char_p, vp]
         L.pcc_set_root_spill_batches.argtypes = [vp, vp, vp, C.c_uint64]
         L.pcc_pending_cells.argtypes = [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         L.pcc_export_pending.argtypes = [vp, vp, vp, vp, vp, vp]
@@ -237,8 +242,8 @@ class Converter:
     def add_keyed_points_device(self, pts_ptr: int, keys_ptr: int, n: int):
         _check(lib().pcc_add_keyed_points_device(self._h, C.c_void_p(pts_ptr), C.c_void_p(keys_ptr), n))
 
-    def set_level_range(self, root_level: int, max_levels: int):
-        _check(lib().pcc_set_level_range(self._h, root_level, max_levels))
+    def set_level_range(self, root_level: int, max_levels: int, raw: bool = False):
+        _check(lib().pcc_set_level_range(self._h, root_level, max_levels, 1 if raw else 0))
 
     def set_root_spill_batches(self, cells_xyz, spill_batch):
         xyz = np.ascontiguousarray(cells_xyz, dtype=np.int32).reshape(-1, 3)
@@ -347,6 +352,28 @@ def shard_bbox(pts_ptr: int, n: int, device: int = 0):
 
 def shard_histogram(pts_ptr: int, n: int, grid: ShardGrid, hist_ptr: int, device: int = 0):
     _check(lib().pcc_shard_histogram(C.c_void_p(pts_ptr), n, C.byref(grid), C.c_void_p(hist_ptr), device))
+
+
+SHARD_LAYERS = 256   # PCC_SHARD_LAYERS
+
+
+def shard_slab_histogram(pts_ptr: int, n: int, grid: ShardGrid, sub_grid_dimension: int, hist_ptr: int,
+                         device: int = 0):
+    _check(lib().pcc_shard_slab_histogram(C.c_void_p(pts_ptr), n, C.byref(grid), sub_grid_dimension,
+                                          C.c_void_p(hist_ptr), device))
+
+
+def shard_route_slabs(pts_ptr: int, n: int, key0: int, grid: ShardGrid, sub_grid_dimension: int, owner_ptr: int,
+                      nranks: int, send_ptr: int, keys_ptr: int, device: int = 0):
+    counts = (C.c_uint64 * nranks)()
+    _check(lib().pcc_shard_route_slabs(C.c_void_p(pts_ptr), n, key0, C.byref(grid), sub_grid_dimension,
+                                       C.c_void_p(owner_ptr), nranks, C.c_void_p(send_ptr), C.c_void_p(keys_ptr),
+                                       counts, device))
+    return [int(c) for c in counts]
+
+
+def write_cell_view(out_dir: str, view: "CellView"):
+    _check(lib().pcc_write_cell_view(out_dir.encode(), C.addressof(view)))
 
 
 def shard_route(pts_ptr: int, n: int, key0: int, grid: ShardGrid, owner_ptr: int, nranks: int, send_ptr: int,

@@ -46,6 +46,8 @@ import threading
 import time
 from dataclasses import dataclass, field
 
+import ctypes as C
+
 import numpy as np
 import torch
 
@@ -193,6 +195,308 @@ def assign_owners(hist: np.ndarray, world: int, greedy_max: int = 4096) -> np.nd
     return owner
 
 
+# ----------------------------------------------------------------- split plan (skewed clouds)
+# Cost model of the plan (relative units per point): a level-0 arrival costs
+# about twice a deeper one (it pays the level-0 binning: config 4 spends 36 ms on
+# 1B level-0 arrivals and 38 ms on 2B deeper ones), and a point arrives at about
+# DEPTH deeper levels.  Config 3 averages 3.3 (W / N = 4.3), but its heavy cells
+# are the dense ones and go deeper (W / N of the four largest: 4.0-4.9), and an
+# unsplit heavy cell is what sets the critical path, so the plan uses 4.
+L0_COST, DEEP_COST, DEPTH = 2.0, 1.0, 4.0
+
+
+def _lpt(w: np.ndarray, world: int):
+    """Largest-first greedy: item i (weight w[i], ties by index) to the least
+    loaded rank (ties by rank).  Deterministic on every rank."""
+    w = np.asarray(w, dtype=np.float64)
+    own = np.zeros(len(w), dtype=np.uint32)
+    load = np.zeros(world, dtype=np.float64)
+    for i in np.lexsort((np.arange(len(w)), -w)):
+        r = int(np.argmin(load))
+        own[i] = r
+        load[r] += w[i]
+    return own, load
+
+
+@dataclass
+class SplitPlan:
+    """Who builds what in one sharded step.
+
+    Whole level-0 cells: owner0[c] builds the cell's sub-tree (phase 1).  A
+    split cell c (split[c]) is shared: its level-0 slabs (cell, hex z-layer) go
+    to slab_owner[c * SHARD_LAYERS + layer], which resolve their slots and
+    forward every emission (phase 1, raw level 0); each level-1 cell c1 below
+    it goes to owner1[c1], which resolves that overflow bucket (cell.rs:108-153)
+    from all ranks' emissions and builds the sub-tree if it spilled (phase 2);
+    writer[c] assembles the level-0 cell file from the pieces."""
+    owner0: np.ndarray
+    split: np.ndarray
+    slab_owner: np.ndarray | None = None
+    writer: np.ndarray | None = None
+    owner1: np.ndarray | None = None
+    est: dict = field(default_factory=dict)
+
+
+def plan_split(hist0: np.ndarray, hist1: np.ndarray | None, children: np.ndarray | None, world: int,
+               slab_hist: np.ndarray | None = None, allow: bool = True) -> SplitPlan:
+    """Choose the level-0 cells to share (largest first) so that the estimated
+    critical path max(phase 1) + max(phase 2) is smallest; without a gain of
+    more than 2 % nothing is shared and this is `assign_owners`.  children[c]:
+    the level-1 grid ids of cell c's 8 children (-1: outside the grid);
+    slab_hist: points per (cell, layer), SHARD_LAYERS per cell."""
+    from pcconv import SHARD_LAYERS as NL
+    hist0 = np.asarray(hist0, dtype=np.int64)
+    nz = np.flatnonzero(hist0)
+    base = assign_owners(hist0, world)
+    whole_w = hist0 * (L0_COST + DEEP_COST * DEPTH)
+    total = float(whole_w.sum())
+    mean = total / max(world, 1)
+    no = SplitPlan(base, np.zeros(len(hist0), dtype=bool))
+    lb = np.zeros(world)
+    for c in nz:
+        lb[base[c]] += whole_w[c]
+    no.est = {"phase1_max": float(lb.max()) if world else 0.0, "phase2_max": 0.0,
+              "ratio": float(lb.max() / mean) if mean else 1.0, "split_cells": 0}
+    if not allow or world <= 1 or hist1 is None or slab_hist is None or len(nz) == 0 or len(nz) > 4096:
+        return no
+    sh = np.asarray(slab_hist, dtype=np.int64).reshape(len(hist0), NL)
+    order = nz[np.lexsort((nz, -hist0[nz]))]
+    best, best_t = None, None
+    for k in range(0, min(len(order), 2 * world) + 1):
+        sp = order[:k]
+        whole = order[k:]
+        # phase 1: the whole cells and the shared cells' level-0 slabs
+        sl = np.concatenate([c * NL + np.flatnonzero(sh[c]) for c in sp]) if k else np.zeros(0, np.int64)
+        o1, l1 = _lpt(np.concatenate([whole_w[whole], sh.reshape(-1)[sl] * L0_COST]), world)
+        # phase 2: the level-1 sub-trees of the shared cells
+        ch = children[sp].reshape(-1) if k else np.zeros(0, np.int64)
+        ch = ch[ch >= 0]
+        ch = ch[hist1[ch] > 0] if len(ch) else ch
+        o2, l2 = _lpt(hist1[ch] * DEEP_COST * DEPTH, world)
+        t = float(l1.max() + (l2.max() if len(ch) else 0.0))
+        if best_t is None or t < best_t * 0.98:
+            best_t, best = t, (sp, whole, sl, o1, ch, o2, l1, l2)
+    sp, whole, sl, o1, ch, o2, l1, l2 = best
+    if len(sp) == 0:
+        return no
+    owner0 = np.zeros(len(hist0), dtype=np.uint32)
+    split = np.zeros(len(hist0), dtype=bool)
+    split[sp] = True
+    owner0[whole] = o1[:len(whole)]
+    slab_owner = np.zeros(len(hist0) * NL, dtype=np.uint32)
+    slab_owner[sl] = o1[len(whole):]
+    writer = np.zeros(len(hist0), dtype=np.uint32)
+    for c in sp:   # the rank holding most of the cell's points
+        w = np.bincount(slab_owner[c * NL:(c + 1) * NL], weights=sh[c], minlength=world)
+        writer[c] = int(np.argmax(w))
+    owner1 = np.zeros(len(hist1), dtype=np.uint32)
+    owner1[ch] = o2
+    return SplitPlan(owner0, split, slab_owner, writer, owner1,
+                     {"phase1_max": float(l1.max()), "phase2_max": float(l2.max()) if len(ch) else 0.0,
+                      "ratio": best_t / mean, "split_cells": int(len(sp))})
+
+
+def route_table(plan: SplitPlan, world: int) -> np.ndarray:
+    """Destination of every level-0 slab for the route (SHARD_LAYERS per cell):
+    rank r for a whole cell's points, r + world for a shared cell's slab."""
+    from pcconv import SHARD_LAYERS as NL
+    t = np.repeat(plan.owner0.astype(np.int64), NL)
+    sp = np.repeat(plan.split, NL)
+    t[sp] = plan.slab_owner.astype(np.int64)[sp] + world
+    return t
+
+
+# ----------------------------------------------------------------- shared cells: bucket resolution
+def event_batches(keys: np.ndarray, file_points, batch: int) -> np.ndarray:
+    """Event batch of each global key (lib.rs:31-52: files in CLI order, batches
+    of `batch`, a file end is a batch boundary, an empty file one empty batch)."""
+    fp = np.asarray([int(v) for v in file_points], dtype=np.int64)
+    start = np.concatenate([[0], np.cumsum(fp)])[:-1]
+    nb = np.maximum(1, (fp + batch - 1) // batch)
+    eb0 = np.concatenate([[0], np.cumsum(nb)])[:-1]
+    k = np.asarray(keys, dtype=np.int64)
+    f = np.searchsorted(start, k, side="right") - 1   # last file whose start <= key
+    return eb0[f] + (k - start[f]) // batch
+
+
+def resolve_bucket(keys: np.ndarray, file_points, batch: int, limit: int):
+    """cell.rs:108-153 for one overflow bucket of a level-0 cell, from all its
+    emissions (their causing keys, any order; level 0: event batch = eb0(key)).
+    Returns (spilled, spill batch, key order).  Batch by batch: the first batch's
+    list is kept if it has at most L points, later batches are appended while
+    the list stays below L; otherwise the bucket turns None at that batch and
+    everything is forwarded (the kept points at that batch)."""
+    order = np.argsort(np.asarray(keys, dtype=np.int64), kind="stable")
+    if len(order) == 0:
+        return False, 0, order
+    eb = event_batches(np.asarray(keys)[order], file_points, batch)
+    tot = len(eb)
+    spilled = tot > limit or (tot == limit and eb[0] != eb[-1])
+    if not spilled:
+        return False, 0, order
+    first = int(np.count_nonzero(eb == eb[0]))
+    thr = limit + (1 if first == limit else 0)
+    return True, int(eb[max(thr, 1) - 1]), order
+
+
+def children_ids(ids0: np.ndarray, grid0, grid1) -> np.ndarray:
+    """(n, 8) level-1 grid ids of the children of level-0 cells (-1 outside grid1);
+    the level-1 index of a point is 2 x its level-0 index + 0/1 per axis
+    (metadata.rs:91-102: cell sizes are power-of-two scalings)."""
+    t = cell_triples(ids0, grid0).astype(np.int64)
+    lo1 = np.array([int(v) for v in grid1.lo], dtype=np.int64)
+    d1 = np.array([int(v) for v in grid1.dims], dtype=np.int64)
+    out = np.full((len(t), 8), -1, dtype=np.int64)
+    for o in range(8):
+        q = 2 * t + np.array([o & 1, (o >> 1) & 1, (o >> 2) & 1]) - lo1
+        ok = ((q >= 0) & (q < d1)).all(axis=1)
+        out[ok, o] = (q[ok, 0] * d1[1] + q[ok, 1]) * d1[2] + q[ok, 2]
+    return out
+
+
+def level1_ids(xyz: np.ndarray, grid1) -> np.ndarray:
+    lo1 = np.array([int(v) for v in grid1.lo], dtype=np.int64)
+    d1 = np.array([int(v) for v in grid1.dims], dtype=np.int64)
+    q = np.asarray(xyz, dtype=np.int64).reshape(-1, 3) - lo1
+    if not ((q >= 0) & (q < d1)).all():
+        raise ValueError("exported level-1 cell outside the level-1 grid")
+    return (q[:, 0] * d1[1] + q[:, 1]) * d1[2] + q[:, 2]
+
+
+def cell_ids(xyz: np.ndarray, grid) -> np.ndarray:
+    """Linear shard-grid ids of level-0 cells (x, y, z)."""
+    lo = np.array([int(v) for v in grid.lo], dtype=np.int64)
+    d = np.array([int(v) for v in grid.dims], dtype=np.int64)
+    q = np.asarray(xyz, dtype=np.int64).reshape(-1, 3) - lo
+    if not ((q >= 0) & (q < d)).all():
+        raise ValueError("cell outside the shard grid")
+    return (q[:, 0] * d[1] + q[:, 1]) * d[2] + q[:, 2]
+
+
+def _exchange_segments(comm, dest: np.ndarray, meta: np.ndarray, lens: np.ndarray, tensors: list, dev):
+    """Segment i (metadata row meta[i]; lens[i] rows of every tensor, the
+    segments contiguous in order) to rank dest[i].  Returns the received
+    metadata rows and tensors: source rank by source rank, each source's
+    segments in its sending order, rows of a segment in their order."""
+    W = comm.world
+    dest = np.asarray(dest, dtype=np.int64)
+    lens = np.asarray(lens, dtype=np.int64)
+    meta = np.asarray(meta, dtype=np.int64).reshape(len(dest), -1)
+    order = np.argsort(dest, kind="stable")
+    if len(order) and not np.array_equal(order, np.arange(len(order))):
+        starts = np.concatenate([[0], np.cumsum(lens)])[:-1]
+        idx = torch.cat([torch.arange(int(starts[i]), int(starts[i] + lens[i]), dtype=torch.int64) for i in order])
+        tensors = [t.index_select(0, idx.to(t.device)) for t in tensors]
+    nseg = [int(v) for v in np.bincount(dest, minlength=W)] if len(dest) else [0] * W
+    nrow = [int(v) for v in np.bincount(dest, weights=lens, minlength=W).astype(np.int64)] if len(dest) else [0] * W
+    k = meta.shape[1] if meta.ndim == 2 else 1
+    mt = torch.from_numpy(np.ascontiguousarray(meta[order]).reshape(-1, k)).to(comm.device)
+    rmeta = _exchange(comm, mt, nseg, comm.alltoall_counts(nseg), comm.device).cpu().numpy().reshape(-1, k)
+    rr = comm.alltoall_counts(nrow)
+    return rmeta, [_exchange(comm, t, nrow, rr, dev) for t in tensors]
+
+
+def resolve_level1(rmeta: np.ndarray, pts: torch.Tensor, keys: torch.Tensor, file_points, batch: int, limit: int):
+    """Owner side of a shared cell's overflow buckets.  rmeta rows (x, y, z, n):
+    segments of emissions (pts/keys, in order) of level-1 cells; one cell can
+    come in several segments (one per rank holding slabs of its parent).  Each
+    cell is the bucket of its level-0 parent for that octant (converter.rs:67-68):
+    resolve it over all its emissions (resolve_bucket).  Returns the spilled
+    cells' emissions (the sub-tree input, roots with their spill batches), and
+    per bucket a row (x, y, z, state 1 = Some / 2 = None, n) with the kept
+    lists (key order) of the Some buckets."""
+    rmeta = np.asarray(rmeta, dtype=np.int64).reshape(-1, 4)
+    starts = np.concatenate([[0], np.cumsum(rmeta[:, 3])])[:-1]
+    groups = {}
+    for i, row in enumerate(rmeta):
+        if row[3]:
+            groups.setdefault(tuple(int(v) for v in row[:3]), []).append(i)
+    kh = keys.cpu().numpy().view(np.uint32).astype(np.int64) if len(groups) else np.zeros(0, np.int64)
+    sub_idx, roots, sbs, rows, kept_idx = [], [], [], [], []
+    for c1 in sorted(groups):
+        idx = np.concatenate([np.arange(starts[i], starts[i] + rmeta[i, 3]) for i in groups[c1]])
+        spilled, sb, order = resolve_bucket(kh[idx], file_points, batch, limit)
+        if spilled:
+            sub_idx.append(idx)
+            roots.append(c1)
+            sbs.append(sb)
+            rows.append([*c1, 2, len(idx)])
+        else:
+            kept_idx.append(idx[order])
+            rows.append([*c1, 1, len(idx)])
+    dev = pts.device
+
+    def take(lst, t):
+        if not lst:
+            return t[:0]
+        return t.index_select(0, torch.from_numpy(np.concatenate(lst)).to(dev))
+    return {"sub_pts": take(sub_idx, pts), "sub_keys": take(sub_idx, keys),
+            "roots_xyz": np.array(roots, dtype=np.int32).reshape(-1, 3), "roots_sb": np.array(sbs, dtype=np.uint32),
+            "bucket_rows": np.array(rows, dtype=np.int64).reshape(-1, 5), "kept_pts": take(kept_idx, pts)}
+
+
+def assemble_cells(rmw: np.ndarray, grid_pts: torch.Tensor, rmk: np.ndarray, kept_pts: torch.Tensor, cfg: dict):
+    """Writer side: the level-0 cells this rank assembles from their pieces --
+    grid winners of every rank's slabs (rmw rows (x, y, z, n) over grid_pts) and
+    the bucket rows (x1, y1, z1, state, n) of their octants with the Some lists
+    (kept_pts, in row order).  Header as cell.rs:43-49, 264-274: size =
+    cell_size(0), sub = size / dim, pos = index * size + size / 2; number = grid
+    points, overflow = kept points, total = their sum."""
+    rmw = np.asarray(rmw, dtype=np.int64).reshape(-1, 4)
+    rmk = np.asarray(rmk, dtype=np.int64).reshape(-1, 5)
+    g = grid_pts.cpu().numpy().reshape(-1, 4).astype(np.int32, copy=False)
+    kp = kept_pts.cpu().numpy().reshape(-1, 4).astype(np.int32, copy=False)
+    cells = {}
+    o = 0
+    for x, y, z, n in rmw:
+        c = cells.setdefault((int(x), int(y), int(z)), {"grid": [], "buckets": {}})
+        c["grid"].append(g[o:o + n])
+        o += int(n)
+    o = 0
+    for x1, y1, z1, st, n in rmk:
+        cnt = int(n) if st == 1 else 0
+        c = cells.setdefault((int(x1) >> 1, int(y1) >> 1, int(z1) >> 1), {"grid": [], "buckets": {}})
+        c["buckets"][(int(x1), int(y1), int(z1))] = (int(st), kp[o:o + cnt])
+        o += cnt
+    f32 = np.float32
+    size = f32(cfg["max_cell_size"]) / f32(1.0)
+    sub = size / f32(cfg["sub_grid_dimension"])
+    out = []
+    for (x, y, z), c in sorted(cells.items()):
+        entries = []
+        for oc in range(8):   # octant order, as the engine's cells
+            c1 = (2 * x + (oc & 1), 2 * y + ((oc >> 1) & 1), 2 * z + ((oc >> 2) & 1))
+            if c1 in c["buckets"]:
+                entries.append((c1,) + c["buckets"][c1])
+        grid = np.concatenate(c["grid"]) if c["grid"] else np.zeros((0, 4), np.int32)
+        out.append({"h": 0, "xyz": (x, y, z), "grid": np.ascontiguousarray(grid), "entries": entries,
+                    "size": size, "sub": sub,
+                    "pos": [f32(v) * size + size / f32(2.0) for v in (x, y, z)]})
+    return out
+
+
+def cell_view(c: dict):
+    """pcc_cell_view of an assembled cell (the arrays must outlive the view)."""
+    v = pcconv.CellView()
+    v.hierarchy = c["h"]
+    v.x, v.y, v.z = c["xyz"]
+    v.number_of_points = len(c["grid"])
+    over = sum(len(p) for _, st, p in c["entries"] if st == 1)
+    v.number_of_overflow_points = over
+    v.total_number_of_points = v.number_of_points + over
+    v.size, v.sub_cell_size = float(c["size"]), float(c["sub"])
+    for a in range(3):
+        v.pos[a] = float(c["pos"][a])
+    v.grid = c["grid"].ctypes.data if len(c["grid"]) else None
+    v.entries = len(c["entries"])
+    for i, (c1, st, p) in enumerate(c["entries"]):
+        for a in range(3):
+            v.child[i][a] = c1[a]
+        v.count[i] = len(p) if st == 1 else 0
+        v.list[i] = p.ctypes.data if (st == 1 and len(p)) else None
+    return v
+
+
 # ----------------------------------------------------------------- local ops (product)
 class HipShardOps:
     """Local per-rank work on the GPU through libpcconv.so (no CPU fallback)."""
@@ -219,6 +523,7 @@ class HipShardOps:
             self.max_cell_size = float(self.cfg["max_cell_size"])
             self.out_dir = out_dir
             self.conv = None
+            self.conv_lead = self.conv_sub = None
             return
         self.max_cell_size = float(self.cfg.get("max_cell_size", 1000.0))
         if out_dir is None:
@@ -230,6 +535,11 @@ class HipShardOps:
             raise ValueError(f"{out_dir} already holds a converted cloud; open it with merge=True")
         self.out_dir = out_dir
         self.conv = pcconv.Converter(out_dir, batch_size=batch_size, device=device_index, config=self.cfg)
+        # split cells: level 0 as their leader, level-1 sub-trees as their owner
+        self.conv_lead = pcconv.Converter(out_dir, batch_size=batch_size, device=device_index, config=self.cfg)
+        self.conv_lead.set_level_range(0, 1, raw=True)
+        self.conv_sub = pcconv.Converter(out_dir, batch_size=batch_size, device=device_index, config=self.cfg)
+        self.conv_sub.set_level_range(1, 0)
 
     def prior_meta(self) -> dict:
         return read_prior_meta(self.out_dir)
@@ -254,8 +564,48 @@ class HipShardOps:
         self._ready()
         return pcconv.shard_bbox(pts.data_ptr(), pts.shape[0], self.dev)
 
-    def grid(self, gmin, gmax) -> pcconv.ShardGrid:
-        return pcconv.shard_grid_from_bbox(gmin, gmax, self.max_cell_size)
+    def grid(self, gmin, gmax, level: int = 0):
+        """Shard grid of the level's cells (metadata.rs:91-93 cell size); None when
+        a level > 0 grid would be too large."""
+        cs = self.max_cell_size / float(1 << level)
+        if level == 0:
+            return pcconv.shard_grid_from_bbox(gmin, gmax, cs)
+        try:
+            return pcconv.shard_grid_from_bbox(gmin, gmax, cs)
+        except pcconv.PccError:
+            return None
+
+    def begin_step(self):
+        self._built = []
+        self.assembled = []
+
+    def cfg_full(self) -> dict:
+        d = dict(cell_point_overflow_limit=5000, sub_grid_dimension=96, max_cell_size=1000.0)
+        d.update(self.cfg)
+        return d
+
+    @property
+    def limit(self) -> int:
+        return int(self.cfg_full()["cell_point_overflow_limit"])
+
+    def set_assembled(self, cells: list):
+        self.assembled = cells
+
+    def slab_histogram(self, pts: torch.Tensor, grid) -> torch.Tensor:
+        h = torch.empty(grid.ncells * pcconv.SHARD_LAYERS, dtype=torch.int32, device=pts.device)
+        self._ready()
+        pcconv.shard_slab_histogram(pts.data_ptr(), pts.shape[0], grid, int(self.cfg_full()["sub_grid_dimension"]),
+                                    h.data_ptr(), self.dev)
+        return h
+
+    def route_slabs(self, pts: torch.Tensor, key0: int, grid, table: torch.Tensor, nranks: int):
+        n = pts.shape[0]
+        send = torch.empty_like(pts)
+        keys = torch.empty(n, dtype=torch.int32, device=pts.device)
+        self._ready()
+        counts = pcconv.shard_route_slabs(pts.data_ptr(), n, key0, grid, int(self.cfg_full()["sub_grid_dimension"]),
+                                          table.data_ptr(), nranks, send.data_ptr(), keys.data_ptr(), self.dev)
+        return send, keys, counts
 
     def histogram(self, pts: torch.Tensor, grid) -> torch.Tensor:
         h = torch.empty(grid.ncells, dtype=torch.int32, device=pts.device)
@@ -275,24 +625,78 @@ class HipShardOps:
     def build(self, file_points, pts: torch.Tensor, keys: torch.Tensor | None) -> dict:
         """keys None: this rank holds the whole input in key order (keys 0..n-1).
         The build reads `pts`/`keys` in place (borrowed until it returns)."""
-        c = self.conv
+        return self._keyed_build(self.conv, file_points, pts, keys)
+
+    def _keyed_build(self, c, file_points, pts, keys, roots=None) -> dict:
         self._ready()
         c.clear_input()
         c.declare_files(file_points)
+        if roots is not None:
+            c.set_root_spill_batches(*roots)
         c.set_keyed_points_device(pts.data_ptr(), 0 if keys is None else keys.data_ptr(), pts.shape[0])
-        return c.build()
+        st = c.build()
+        if c not in getattr(self, "_built", []):
+            self._built = getattr(self, "_built", []) + [c]
+        return st
+
+    def lead_build_raw(self, file_points, pts: torch.Tensor, keys: torch.Tensor):
+        """Level 0 of the shared cells' slabs this rank holds, raw (every emission
+        forwarded).  Returns (stats, (level-1 cells (n,3), -, points per cell,
+        their emissions (m,4), causing keys), partial level-0 cells [{xyz, grid}])."""
+        c = self.conv_lead
+        st = self._keyed_build(c, file_points, pts, keys)
+        _, m = c.pending_cells()
+        P = torch.empty((m, 4), dtype=torch.int32, device=pts.device)
+        K = torch.empty(m, dtype=torch.int32, device=pts.device)
+        xyz, sb, cn = c.export_pending(P.data_ptr(), K.data_ptr())
+        partial = []
+
+        def grab(vp):
+            v = pcconv.CellView.from_address(vp)
+            n = int(v.number_of_points)
+            g = (np.frombuffer((C.c_char * (16 * n)).from_address(v.grid), dtype=np.int32).reshape(n, 4).copy()
+                 if n else np.zeros((0, 4), np.int32))
+            partial.append({"xyz": (int(v.x), int(v.y), int(v.z)), "grid": g})
+            return 0
+        c.visit_cells(grab)
+        return st, (xyz, sb, cn, P, K), partial
+
+    def sub_build(self, file_points, pts: torch.Tensor, keys: torch.Tensor, cells_xyz, spill_batch) -> dict:
+        """The level-1 sub-trees of split cells this rank owns (their arrivals, cell
+        after cell, from the leaders' pcc_export_pending)."""
+        return self._keyed_build(self.conv_sub, file_points, pts, keys, roots=(cells_xyz, spill_batch))
+
+    def _outputs(self):
+        # the raw level-0 pieces of shared cells are written by their assemblers
+        return [self.conv] + [c for c in getattr(self, "_built", []) if c is not self.conv and c is not self.conv_lead]
+
+    def visit_cells(self, fn):
+        """pcc_visit_cells over every converter built in the last step, then the
+        shared level-0 cells this rank assembled."""
+        for c in self._outputs():
+            c.visit_cells(fn)
+        for cell in getattr(self, "assembled", []):
+            v = cell_view(cell)
+            fn(C.addressof(v))
 
     def write(self, summary: dict, cells: bool, metadata: bool):
-        c = self.conv
-        c.set_summary(summary["number_of_points"], summary["bbox_min"], summary["bbox_max"], summary["hierarchies"])
+        convs = self._outputs()
+        for c in convs:
+            c.set_summary(summary["number_of_points"], summary["bbox_min"], summary["bbox_max"],
+                          summary["hierarchies"])
         if cells:
-            c.write_cells()
+            for c in convs:
+                c.write_cells()
+            for cell in getattr(self, "assembled", []):
+                pcconv.write_cell_view(self.out_dir, cell_view(cell))
         if metadata:
-            c.write_metadata()
+            self.conv.write_metadata()
 
     def close(self):
-        if self.conv is not None:
-            self.conv.close()
+        for c in (self.conv, getattr(self, "conv_lead", None), getattr(self, "conv_sub", None)):
+            if c is not None:
+                c.close()
+        self.conv = self.conv_lead = self.conv_sub = None
         if self._tmp is not None:
             self._tmp.cleanup()
 
@@ -305,6 +709,9 @@ class ShardResult:
     recv_points: int
     owned_cells: int
     ms: dict = field(default_factory=dict)
+    sub_points: int = 0          # level-1 arrivals received for split cells' sub-trees
+    plan: dict = field(default_factory=dict)   # plan_split's estimate
+    assembled_cells: int = 0     # shared level-0 cells this rank assembled and wrote
 
 
 def read_prior_meta(out_dir: str) -> dict:
@@ -329,13 +736,37 @@ def cell_triples(ids: np.ndarray, grid) -> np.ndarray:
     return out.astype(np.int32).reshape(-1, 3)
 
 
+def _exchange(comm, send: torch.Tensor, counts, rcounts, dev) -> torch.Tensor:
+    """All-to-all-v of rows into a new tensor on `dev` (straight into it when the
+    communicator works on that device, else through the communicator's device)."""
+    n = int(sum(int(v) for v in rcounts))
+    if comm.device == dev:
+        out = torch.empty((n,) + tuple(send.shape[1:]), dtype=send.dtype, device=dev)
+        return comm.alltoallv_into(send, counts, rcounts, out)
+    out = torch.empty((n,) + tuple(send.shape[1:]), dtype=send.dtype, device=comm.device)
+    comm.alltoallv_into(send.to(comm.device), counts, rcounts, out)
+    return out.to(dev)
+
+
+def _combine(parts: list[dict]) -> dict:
+    out = dict(parts[-1])
+    for k in ("arrivals", "cells", "slabs"):
+        if all(k in p for p in parts):
+            out[k] = sum(int(p[k]) for p in parts)
+    for k in ("hierarchies", "levels"):
+        if all(k in p for p in parts):
+            out[k] = max(int(p[k]) for p in parts)
+    return out
+
+
 def shard_build(comm, ops, pts: torch.Tensor, key0: int, file_points, write: bool = False,
-                sync=None, merge: bool = False) -> ShardResult:
+                sync=None, merge: bool = False, split: bool = True) -> ShardResult:
     """One sharded conversion step.  `pts` is this rank's (n, 4) int32 view of
     16-B points with global keys key0 .. key0+n-1 (contiguous ranges in rank
     order).  `file_points` is the GLOBAL file structure.  `sync` (optional)
     synchronises the device for stage timing.  `merge`: incremental merge into
-    the existing cloud of the ops' directory (module docstring)."""
+    the existing cloud of the ops' directory (module docstring).  `split`: allow
+    heavy level-0 cells to be shared at level 1 (plan_split; never for a merge)."""
     ms = {}
     t0 = time.perf_counter()
 
@@ -347,6 +778,7 @@ def shard_build(comm, ops, pts: torch.Tensor, key0: int, file_points, write: boo
         ms[name] = ms.get(name, 0.0) + (t1 - t0) * 1e3
         t0 = t1
 
+    W, dev = comm.world, pts.device
     n_total = int(sum(int(v) for v in file_points))
     # 2. global bounding box (converter.rs:96-104: componentwise min/max)
     if pts.shape[0]:
@@ -359,49 +791,112 @@ def shard_build(comm, ops, pts: torch.Tensor, key0: int, file_points, write: boo
     bbh = bb.cpu().tolist()
     gmin, gmax = [-bbh[0], -bbh[1], -bbh[2]], bbh[3:]
     mark("bbox")
+    plan = None
     if n_total == 0:
         recv = pts[:0]
-        keys = torch.empty(0, dtype=torch.int32, device=pts.device)
+        keys = torch.empty(0, dtype=torch.int32, device=dev)
         owned = 0
         if merge:
             ops.set_subtrees(np.zeros((0, 3), dtype=np.int32))
     else:
-        # 3. level-0 ownership
+        # 3. ownership: level-0 cells; heavy ones shared slab by slab
+        from pcconv import SHARD_LAYERS as NL
         grid = ops.grid(gmin, gmax)
-        hist = ops.histogram(pts, grid)
-        hist = comm.allreduce_(hist.to(comm.device), "sum")
-        hist_h = hist.cpu().numpy().astype(np.int64)
-        owner_h = assign_owners(hist_h, comm.world)
-        owned = int(np.count_nonzero((owner_h == comm.rank) & (hist_h > 0)))
-        owner = torch.from_numpy(owner_h.astype(np.int32)).to(pts.device)
+        grid1 = ops.grid(gmin, gmax, level=1) if (split and not merge and W > 1) else None
+        if grid1 is not None and (int(grid1.ncells) > (1 << 22) or int(grid.ncells) * NL > (1 << 24)):
+            grid1 = None
+        if grid1 is not None:
+            sh = ops.slab_histogram(pts, grid)
+            sh_h = comm.allreduce_(sh.to(comm.device), "sum").cpu().numpy().astype(np.int64)
+            hist_h = sh_h.reshape(-1, NL).sum(axis=1)
+            h1 = ops.histogram(pts, grid1)
+            hist1_h = comm.allreduce_(h1.to(comm.device), "sum").cpu().numpy().astype(np.int64)
+            ch = np.full((len(hist_h), 8), -1, dtype=np.int64)
+            nz = np.flatnonzero(hist_h)
+            ch[nz] = children_ids(nz, grid, grid1)
+            plan = plan_split(hist_h, hist1_h, ch, W, slab_hist=sh_h)
+        else:
+            hist = ops.histogram(pts, grid)
+            hist_h = comm.allreduce_(hist.to(comm.device), "sum").cpu().numpy().astype(np.int64)
+            plan = plan_split(hist_h, None, None, W, allow=False)
+        owner_h = plan.owner0
+        owned = int(np.count_nonzero((owner_h == comm.rank) & (hist_h > 0) & ~plan.split))
         if merge:   # the existing cells of the owned subtrees that receive new points
             ops.set_subtrees(cell_triples(np.flatnonzero((owner_h == comm.rank) & (hist_h > 0)), grid))
         mark("plan")
-        # 4. route + exchange (grouped point-to-point transfers of points and keys)
-        if comm.world == 1:   # one rank owns every cell: the partition is the identity
+        # 4. route + exchange (grouped point-to-point transfers of points and keys).
+        # A shared cell's slabs travel as a second stream: destination "rank + W".
+        nsplit = bool(plan.split.any())
+        if W == 1:   # one rank owns every cell: the partition is the identity
             recv, keys = pts, None
             mark("route")
         else:
-            send, skeys, counts = ops.route(pts, key0, grid, owner, comm.world)
+            if nsplit:
+                tab = torch.from_numpy(route_table(plan, W).astype(np.int32)).to(dev)
+                send, skeys, counts = ops.route_slabs(pts, key0, grid, tab, 2 * W)
+            else:
+                owner = torch.from_numpy(owner_h.astype(np.int32)).to(dev)
+                send, skeys, counts = ops.route(pts, key0, grid, owner, W)
             mark("route")
-            rcounts = comm.alltoall_counts(counts)
-            nrecv = int(sum(rcounts))
-            if comm.device == pts.device:   # receive straight into the build's input buffers
-                recv = torch.empty((nrecv,) + tuple(pts.shape[1:]), dtype=pts.dtype, device=pts.device)
-                keys = torch.empty(nrecv, dtype=torch.int32, device=pts.device)
-                comm.alltoallv_into(send, counts, rcounts, recv)
-                comm.alltoallv_into(skeys, counts, rcounts, keys)
-            else:   # host communicator (gloo) driving device ops
-                recv = torch.empty((nrecv,) + tuple(pts.shape[1:]), dtype=pts.dtype, device=comm.device)
-                keys = torch.empty(nrecv, dtype=torch.int32, device=comm.device)
-                comm.alltoallv_into(send.to(comm.device), counts, rcounts, recv)
-                comm.alltoallv_into(skeys.to(comm.device), counts, rcounts, keys)
-                recv, keys = recv.to(pts.device), keys.to(pts.device)
+            cw = [int(v) for v in counts[:W]]
+            rc = comm.alltoall_counts(cw)
+            nw = sum(cw)
+            recv = _exchange(comm, send.narrow(0, 0, nw), cw, rc, dev)
+            keys = _exchange(comm, skeys.narrow(0, 0, nw), cw, rc, dev)
+            if nsplit:
+                cs = [int(v) for v in counts[W:]]
+                rcs = comm.alltoall_counts(cs)
+                lrecv = _exchange(comm, send.narrow(0, nw, sum(cs)), cs, rcs, dev)
+                lkeys = _exchange(comm, skeys.narrow(0, nw, sum(cs)), cs, rcs, dev)
             del send, skeys
         mark("exchange")
-    # 5. independent build of the owned level-0 subtrees
+    ops.begin_step()
+    phases = {"lead": 0, "sub": 0, "whole": 0}
+    sub_points = 0
+    # 5a. phase 1: the whole level-0 sub-trees this rank owns ...
     local = ops.build(file_points, recv, keys)
+    parts = [local]
+    phases["whole"] = int(local.get("arrivals", 0))
     mark("build")
+    assembled = []
+    if plan is not None and plan.split.any() and W > 1:
+        # ... and the slots of the shared cells' slabs it holds (raw level 0:
+        # every emission forwarded with the key of the arrival that caused it)
+        lst, (xyz, _, cn, P, K), partial = ops.lead_build_raw(file_points, lrecv, lkeys)
+        parts.append(lst)
+        phases["lead"] = int(lst["arrivals"])
+        mark("lead")
+        # 5b. emissions to the owners of their level-1 cells; the partial
+        # level-0 cells (grid winners of these slabs) to their writers
+        xyz = np.asarray(xyz, np.int64).reshape(-1, 3)
+        cn = np.asarray(cn, np.int64)
+        d1 = plan.owner1[level1_ids(xyz, grid1)].astype(np.int64) if len(xyz) else np.zeros(0, np.int64)
+        rm1, (rP, rK) = _exchange_segments(comm, d1, np.column_stack([xyz, cn]), cn, [P, K], dev)
+        del P, K
+        pxyz = np.array([q["xyz"] for q in partial], dtype=np.int64).reshape(-1, 3)
+        pn = np.array([len(q["grid"]) for q in partial], dtype=np.int64)
+        gpts = torch.from_numpy(np.concatenate([q["grid"] for q in partial]) if partial
+                                else np.zeros((0, 4), np.int32)).to(dev)
+        dw = plan.writer[cell_ids(pxyz, grid)].astype(np.int64) if len(pxyz) else np.zeros(0, np.int64)
+        rmw, (rG,) = _exchange_segments(comm, dw, np.column_stack([pxyz, pn]), pn, [gpts], dev)
+        mark("exchange2")
+        # 5c. phase 2: resolve each received level-1 cell's bucket (all ranks'
+        # emissions), build the spilled ones' sub-trees
+        res = resolve_level1(rm1, rP, rK, file_points, ops.batch_size, ops.limit)
+        sub_points = int(res["sub_pts"].shape[0])
+        sst = ops.sub_build(file_points, res["sub_pts"], res["sub_keys"], res["roots_xyz"], res["roots_sb"])
+        parts.append(sst)
+        phases["sub"] = int(sst["arrivals"])
+        mark("subtrees")
+        # 5d. bucket states and kept lists to the writers, who assemble the cells
+        bx = res["bucket_rows"]
+        dk = (plan.writer[cell_ids(bx[:, :3] >> 1, grid)].astype(np.int64) if len(bx) else np.zeros(0, np.int64))
+        rmk, (rKP,) = _exchange_segments(comm, dk, bx, bx[:, 4] * (bx[:, 3] == 1), [res["kept_pts"]], dev)
+        assembled = assemble_cells(rmw, rG, rmk, rKP, ops.cfg_full())
+        ops.set_assembled(assembled)
+        mark("assemble")
+    local = _combine(parts)
+    local["phases"] = phases
     # 6. global metadata values
     hz = torch.tensor([int(local["hierarchies"])], dtype=torch.int64, device=comm.device)
     comm.allreduce_(hz, "max")
@@ -425,7 +920,10 @@ def shard_build(comm, ops, pts: torch.Tensor, key0: int, file_points, write: boo
             ops.write(summary, cells=False, metadata=True)
         comm.barrier()
         mark("write")
-    return ShardResult(summary=summary, local=local, recv_points=int(recv.shape[0]), owned_cells=owned, ms=ms)
+    nrecv = int(recv.shape[0]) + (int(lrecv.shape[0]) if plan is not None and plan.split.any() and W > 1 else 0)
+    return ShardResult(summary=summary, local=local, recv_points=nrecv, owned_cells=owned, ms=ms,
+                       sub_points=sub_points, plan=(plan.est if plan is not None else {}),
+                       assembled_cells=len(assembled))
 
 
 def key_range(n_total: int, rank: int, world: int) -> tuple[int, int]:

@@ -42,6 +42,7 @@ class NumpyShardOps:
         self.cfg = dict(config or {})
         self.max_cell_size = float(self.cfg.get("max_cell_size", 1000.0))
         self.oracle = None
+        self.oracles = []   # every oracle built this step (whole, lead, sub)
         self.merge = merge
         self.subtree_dir = None
 
@@ -71,8 +72,57 @@ class NumpyShardOps:
         p = as_points(pts)
         return ([float(p[a].min()) for a in "xyz"], [float(p[a].max()) for a in "xyz"])
 
-    def grid(self, gmin, gmax):
-        return pcconv.shard_grid_from_bbox(gmin, gmax, self.max_cell_size)   # host-only C-ABI helper
+    def grid(self, gmin, gmax, level: int = 0):
+        return pcconv.shard_grid_from_bbox(gmin, gmax, self.max_cell_size / float(1 << level))   # host-only C-ABI helper
+
+    def begin_step(self):
+        for o in self.oracles:
+            if o is not self.oracle:
+                o.close()
+        self.oracles = [self.oracle] if self.oracle is not None else []
+        self.lead = None
+        self.assembled = []
+
+    def cfg_full(self):
+        d = dict(cell_point_overflow_limit=5000, sub_grid_dimension=96, max_cell_size=1000.0)
+        d.update(self.cfg)
+        return d
+
+    @property
+    def limit(self):
+        return int(self.cfg_full()["cell_point_overflow_limit"])
+
+    @property
+    def batch_size(self):
+        return self.batch
+
+    def set_assembled(self, cells):
+        self.assembled = cells
+
+    def _slabs(self, p, grid):
+        """Slab unit of every point: cell * SHARD_LAYERS + level-0 hex layer offset
+        (engine l0_layer: t = trunc(z / r0) saturating, minus dim2 * iz - 2)."""
+        dim = int(self.cfg_full()["sub_grid_dimension"])
+        cs = np.float32(grid.cell_size)
+        cr = (cs / np.float32(dim)) / np.float32(2.0)
+        z = p["z"].astype(np.float32)
+        iz = cell_index(z, cs)
+        t = np.clip(np.trunc((z / cr).astype(np.float64)), -2147483648.0, 2147483647.0).astype(np.int64)
+        ll = t - (2 * dim * iz - 2)
+        assert ((ll >= 0) & (ll < pcconv.SHARD_LAYERS)).all()
+        return self._cells(p, grid) * pcconv.SHARD_LAYERS + ll
+
+    def slab_histogram(self, pts, grid):
+        u = self._slabs(as_points(pts), grid)
+        return torch.from_numpy(np.bincount(u, minlength=grid.ncells * pcconv.SHARD_LAYERS).astype(np.int32))
+
+    def route_slabs(self, pts, key0, grid, table, world):
+        p = as_points(pts)
+        own = table.cpu().numpy().astype(np.int64)[self._slabs(p, grid)]
+        order = np.argsort(own, kind="stable")
+        counts = np.bincount(own, minlength=world)[:world]
+        keys = (key0 + order).astype(np.uint32).view(np.int32)
+        return as_tensor(p[order]), torch.from_numpy(keys.copy()), [int(c) for c in counts]
 
     def _cells(self, p, grid):
         ix = [cell_index(p[a], grid.cell_size) - grid.lo[i] for i, a in enumerate("xyz")]
@@ -92,16 +142,7 @@ class NumpyShardOps:
         keys = (key0 + order).astype(np.uint32).view(np.int32)
         return as_tensor(p[order]), torch.from_numpy(keys.copy()), [int(c) for c in counts]
 
-    def build(self, file_points, pts, keys) -> dict:
-        p = as_points(pts)
-        k = (np.arange(len(p), dtype=np.int64) if keys is None
-             else keys.cpu().numpy().view(np.uint32).astype(np.int64))
-        assert (np.diff(k) > 0).all(), "keyed input must arrive in global key order"
-        if self.oracle is not None:
-            self.oracle.close()
-        o = self.oracle = Oracle(self.cfg)
-        if self.merge:
-            o.load(self.subtree_dir)
+    def _feed_global_batches(self, o, file_points, p, k):
         g = 0
         for fp in file_points:
             off = 0
@@ -113,23 +154,106 @@ class NumpyShardOps:
                 if off >= fp:
                     break
             g += fp
-        assert o.error == 0
+
+    @staticmethod
+    def _stats(o):
         return {"hierarchies": o.hierarchies, "arrivals": o.arrivals, "cells": o.num_cells, "levels": o.hierarchies,
                 "slabs": 0}
+
+    def build(self, file_points, pts, keys) -> dict:
+        p = as_points(pts)
+        k = (np.arange(len(p), dtype=np.int64) if keys is None
+             else keys.cpu().numpy().view(np.uint32).astype(np.int64))
+        assert (np.diff(k) > 0).all(), "keyed input must arrive in global key order"
+        if self.oracle is not None:
+            if self.oracle in self.oracles:
+                self.oracles.remove(self.oracle)
+            self.oracle.close()
+        o = self.oracle = Oracle(self.cfg)
+        self.oracles.append(o)
+        if self.merge:
+            o.load(self.subtree_dir)
+        self._feed_global_batches(o, file_points, p, k)
+        assert o.error == 0
+        return self._stats(o)
+
+    def lead_build_raw(self, file_points, pts, keys):
+        """Level 0 of the held slabs of shared cells, raw: every emission with the
+        key of the arrival that caused it (orc_add_batch_raw0), grouped by its
+        level-1 cell; plus the partial level-0 cells (grid winners)."""
+        p = as_points(pts)
+        k = keys.cpu().numpy().view(np.uint32).astype(np.int64)
+        assert (np.diff(k) > 0).all(), "keyed input must arrive in global key order"
+        o = self.lead = Oracle(self.cfg)
+        g = 0
+        for fp in file_points:
+            off = 0
+            while True:   # lib.rs:31-52 global batches
+                m = min(self.batch, fp - off)
+                lo, hi = np.searchsorted(k, g + off), np.searchsorted(k, g + off + m)
+                o.add_batch_raw0(p[lo:hi], k[lo:hi].astype(np.uint32))
+                off += m
+                if off >= fp:
+                    break
+            g += fp
+        fp_, _, fx, fk = o.pending(with_keys=True)
+        if len(fp_):
+            cells, inv = np.unique(fx, axis=0, return_inverse=True)
+            inv = inv.reshape(-1)
+            order = np.argsort(inv, kind="stable")
+            cn = np.bincount(inv, minlength=len(cells)).astype(np.uint64)
+        else:
+            cells, order, cn = np.zeros((0, 3), np.int32), np.zeros(0, np.int64), np.zeros(0, np.uint64)
+        P = as_tensor(fp_[order])
+        K = torch.from_numpy(fk[order].astype(np.uint32).view(np.int32).copy())
+        partial = [{"xyz": xyz, "grid": np.ascontiguousarray(gp).view(np.int32).reshape(-1, 4)}
+                   for h, xyz, gp in o.cells() if h == 0]
+        st = self._stats(o)
+        o.close()
+        self.lead = None
+        return st, (cells.astype(np.int32), np.zeros(len(cells), np.uint32), cn, P, K), partial
+
+    def sub_build(self, file_points, pts, keys, cells_xyz, spill_batch) -> dict:
+        """The owned level-1 sub-trees: their arrivals replayed batch by batch, an
+        arrival's batch being max(eb0(key), its root's spill batch), key order
+        inside a batch (the lists forwarded to the cell, converter.rs:114-139)."""
+        from pcconv.dist import event_batches
+        p = as_points(pts)
+        k = keys.cpu().numpy().view(np.uint32).astype(np.int64)
+        sb = {tuple(int(v) for v in c): int(b) for c, b in zip(np.asarray(cells_xyz).reshape(-1, 3), spill_batch)}
+        o = Oracle(self.cfg)
+        self.oracles.append(o)
+        o.set_level_range(1, 0)
+        if len(p):
+            cs = np.float32(self.cfg_full()["max_cell_size"]) / np.float32(2.0)
+            c1 = np.stack([cell_index(p[a], cs) for a in "xyz"], axis=1)
+            root_sb = np.array([sb[tuple(int(v) for v in c)] for c in c1], dtype=np.int64)
+            eff = np.maximum(event_batches(k, file_points, self.batch), root_sb)
+            order = np.lexsort((k, eff))
+            p, eff = p[order], eff[order]
+            cuts = np.flatnonzero(np.diff(eff)) + 1
+            for part in np.split(np.arange(len(p)), cuts):
+                o.add_batch(p[part])
+        assert o.error == 0
+        return self._stats(o)
 
     def write(self, summary, cells: bool, metadata: bool):
         os.makedirs(self.out_dir, exist_ok=True)
         if cells:
-            tmp = tempfile.mkdtemp(prefix="pcc_np_shard_")
-            try:
-                self.oracle.write(tmp)
-                for name in os.listdir(tmp):
-                    if name.startswith("h_"):
-                        os.makedirs(os.path.join(self.out_dir, name), exist_ok=True)
-                        for fn in os.listdir(os.path.join(tmp, name)):
-                            shutil.copy(os.path.join(tmp, name, fn), os.path.join(self.out_dir, name, fn))
-            finally:
-                shutil.rmtree(tmp, ignore_errors=True)
+            from pcconv.dist import cell_view
+            for cell in self.assembled:
+                pcconv.write_cell_view(self.out_dir, cell_view(cell))
+            for o in self.oracles:
+                tmp = tempfile.mkdtemp(prefix="pcc_np_shard_")
+                try:
+                    o.write(tmp)
+                    for name in os.listdir(tmp):
+                        if name.startswith("h_"):
+                            os.makedirs(os.path.join(self.out_dir, name), exist_ok=True)
+                            for fn in os.listdir(os.path.join(tmp, name)):
+                                shutil.copy(os.path.join(tmp, name, fn), os.path.join(self.out_dir, name, fn))
+                finally:
+                    shutil.rmtree(tmp, ignore_errors=True)
         if metadata:
             cfg = dict(dict(cell_point_overflow_limit=5000, sub_grid_dimension=96, max_cell_size=1000.0), **self.cfg)
             meta = {"version": "1.0", "name": "Unknown", "number_of_points": summary["number_of_points"],
@@ -141,9 +265,12 @@ class NumpyShardOps:
                 json.dump(meta, f, indent=2)
 
     def close(self):
-        if self.oracle is not None:
+        for o in self.oracles:
+            o.close()
+        if self.oracle is not None and self.oracle not in self.oracles:
             self.oracle.close()
-            self.oracle = None
+        self.oracles = []
+        self.oracle = None
         if self.subtree_dir is not None:
             shutil.rmtree(self.subtree_dir, ignore_errors=True)
             self.subtree_dir = None

@@ -309,3 +309,103 @@ def test_hip_shard_ops_config_and_fresh_dir_guards(tmp_path):
     assert ops.cfg["max_cell_size"] == 500.0 and ops.max_cell_size == 500.0
     with pytest.raises(ValueError, match="merge=True"):
         HipShardOps(0, out_dir=str(d))
+
+
+# ------------------------------------------------------------- skewed clouds: heavy level-0 cells split at level 1
+SKEW_CFG = {"sub_grid_dimension": 16, "cell_point_overflow_limit": 100, "max_cell_size": 1000.0}
+
+
+def make_skewed(case):
+    if case == "gauss":      # Gaussian mixture (config-3 generator): a few heavy level-0 cells
+        return [synth(61, 2, 150_000)]
+    if case == "gauss_files":
+        return [synth(62, 2, 70_001), synth(63, 0, 0), synth(64, 2, 33_333)]
+    raise KeyError(case)
+
+
+@pytest.mark.parametrize("case,world", [("gauss", 3), ("gauss", 8), ("gauss_files", 5)])
+def test_thread_ranks_split_cells_match_oracle(tmp_path, case, world):
+    """Heavy level-0 cells built by a leader (level 0) and the owners of their
+    level-1 sub-trees (plan_split) == the sequential oracle."""
+    import threading
+    files = make_skewed(case)
+    fp = [len(f) for f in files]
+    out = str(tmp_path / "out")
+    grp = ThreadGroup(world)
+    res, errs = [None] * world, []
+
+    def worker(r):
+        try:
+            pts, key0 = rank_slice(files, r, world)
+            ops = NumpyShardOps(out, config=SKEW_CFG)
+            res[r] = shard_build(ThreadComm(grp, r, torch.device("cpu")), ops, as_tensor(pts), key0, fp, write=True)
+            ops.close()
+        except BaseException as e:  # noqa: BLE001
+            errs.append(e)
+            grp.bar.abort()
+
+    th = [threading.Thread(target=worker, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs
+    assert res[0].plan["split_cells"] > 0
+    assert all(r.plan == res[0].plan for r in res)
+    assert sum(r.recv_points for r in res) == sum(fp)
+    assert sum(r.local["phases"]["sub"] for r in res) > 0
+    assert all(r.summary == res[0].summary for r in res)
+    check_against_oracle(tmp_path, files, out, res[0].summary, cfg=SKEW_CFG)
+
+
+def _gloo_split_worker(rank, world, port, out, res_dir):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        files = make_skewed("gauss")
+        pts, key0 = rank_slice(files, rank, world)
+        comm = TorchComm(torch.device("cpu"))
+        comm.max_msg_bytes = 1 << 14   # many transfers per peer segment in both exchanges
+        ops = NumpyShardOps(out, config=SKEW_CFG)
+        r = shard_build(comm, ops, as_tensor(pts), key0, [len(f) for f in files], write=True)
+        ops.close()
+        with open(os.path.join(res_dir, f"rank{rank}.json"), "w") as f:
+            json.dump({"summary": r.summary, "recv": r.recv_points, "plan": r.plan, "phases": r.local["phases"]}, f)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_split_cells_match_oracle(tmp_path):
+    import torch.multiprocessing as mp
+    out, rd = str(tmp_path / "out"), str(tmp_path / "res")
+    os.makedirs(rd)
+    mp.spawn(_gloo_split_worker, args=(2, _free_port(), out, rd), nprocs=2, join=True)
+    r = [json.load(open(os.path.join(rd, f"rank{i}.json"))) for i in range(2)]
+    files = make_skewed("gauss")
+    assert r[0]["summary"] == r[1]["summary"]
+    assert r[0]["plan"]["split_cells"] > 0
+    assert r[0]["recv"] + r[1]["recv"] == sum(len(f) for f in files)
+    check_against_oracle(tmp_path, files, out, r[0]["summary"], cfg=SKEW_CFG)
+
+
+def test_plan_split_uniform_is_assign_owners():
+    """Equal level-0 cells on as many ranks: nothing to gain, nothing split."""
+    from pcconv.dist import plan_split
+    h0 = np.full(8, 1000, dtype=np.int64)
+    h1 = np.full(64, 125, dtype=np.int64)
+    ch = np.arange(64).reshape(8, 8)
+    sh = np.zeros((8, 256), np.int64)
+    sh[:, 10:30] = 50
+    p = plan_split(h0, h1, ch, 8, slab_hist=sh.reshape(-1))
+    assert not p.split.any() and (p.owner0 == assign_owners(h0, 8)).all()
+    # one heavy cell among light ones: shared, its 40 slabs spread over all ranks
+    h0 = np.array([8000, 10, 10, 10], np.int64)
+    sh = np.zeros((4, 256), np.int64)
+    sh[0, 20:60] = 200
+    sh[1:, 5] = 10
+    p3 = plan_split(h0, np.concatenate([np.full(8, 1000), np.zeros(24)]).astype(np.int64), np.arange(32).reshape(4, 8), 4,
+                    slab_hist=sh.reshape(-1))
+    assert p3.split[0] and not p3.split[1:].any()
+    assert sorted(set(p3.slab_owner[20:60].tolist())) == [0, 1, 2, 3]
+    assert p3.est["ratio"] < 0.8 * plan_split(h0, None, None, 4, allow=False).est["ratio"]

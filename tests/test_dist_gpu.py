@@ -169,3 +169,20 @@ def test_sharded_merge_takes_config_from_existing_cloud(tmp_path):
     run_gpu(out, old, cfg=cfg)
     res = _run_threads(new, 3, out, cfg=None, merge=True)
     check_against_oracle(tmp_path, old + new, out, res[0].summary, cfg=cfg)
+
+
+SKEW_CFG = {"sub_grid_dimension": 16, "cell_point_overflow_limit": 100, "max_cell_size": 1000.0}
+
+
+@pytest.mark.parametrize("world", [4, 8])
+def test_sharded_threads_split_cells_match_oracle(tmp_path, world):
+    """Gaussian-mixture cloud: heavy level-0 cells are built by a leader (level 0,
+    pcc_set_level_range(0, 1)) and the owners of their level-1 sub-trees
+    (pcc_export_pending -> exchange -> pcc_set_level_range(1, 0)) == the oracle."""
+    files = [synth(61, 2, 400_000), synth(62, 2, 50_001)]
+    out = str(tmp_path / "out")
+    res = _run_threads(files, world, out, cfg=SKEW_CFG)
+    assert res[0].plan["split_cells"] > 0
+    assert sum(r.local["phases"]["sub"] for r in res) > 0
+    assert sum(r.recv_points for r in res) == sum(len(f) for f in files)
+    check_against_oracle(tmp_path, files, out, res[0].summary, cfg=SKEW_CFG)

@@ -139,3 +139,81 @@ def test_visit_digest_equals_oracle_digest_small():
         err, _ = run_oracle(to, files)
         d, mg, mo = compare_dirs(tg, to)
         assert err == 0 and d == [] and mg == mo
+
+
+def test_config3_sharded_8_ranks_split_cells():
+    """Config 3 by 8 ranks (threads sharing cuda:0, pcconv.dist.ThreadComm): each
+    rank generates its key range in HBM; the heavy level-0 cells are split at
+    level 1 (plan_split).  The union of the ranks' cells must equal the oracle's
+    digests, and the per-rank work must be balanced: measured arrivals give a
+    critical path (max phase 1 + max phase 2) within 1.2x of a perfect split."""
+    import threading
+
+    import torch
+    from oracle_ctypes import Digest
+    from pcconv.dist import HipShardOps, ThreadComm, ThreadGroup, key_range, shard_build
+    fx = fixture("config3")
+    s = fx["synth"]
+    world = 8
+    dev = torch.device("cuda", 0)
+    grp = ThreadGroup(world)
+    res, ops, errs = [None] * world, [None] * world, []
+
+    def worker(r):
+        try:
+            torch.cuda.set_device(dev)
+            a, b = key_range(s["n"], r, world)
+            pts = torch.empty((b - a, 4), dtype=torch.int32, device=dev)
+            pcconv.synth_device(pts.data_ptr(), a, b - a, s["seed"], s["kind"], -1000.0, 2000.0, 0)
+            torch.cuda.synchronize()
+            ops[r] = HipShardOps(0)
+            res[r] = shard_build(ThreadComm(grp, r, dev), ops[r], pts, a, [s["n"]])
+        except BaseException as e:  # noqa: BLE001
+            errs.append(e)
+            grp.bar.abort()
+
+    th = [threading.Thread(target=worker, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    try:
+        assert not errs, errs
+        d = Digest()
+        for o in ops:
+            o.visit_cells(lambda v: d.add_view(v) or 0)
+        got = d.result()
+        d.close()
+    finally:
+        for o in ops:
+            if o is not None:
+                o.close()
+    assert got["subtrees"] == fx["subtrees"]
+    assert (got["grid_points"], got["kept_points"]) == (fx["grid_points"], fx["kept_points"])
+    assert sum(r.local["arrivals"] for r in res) == fx["arrivals"]
+    assert res[0].summary["hierarchies"] == fx["hierarchies"]
+    # Per-rank load.  Phase 1: the whole level-0 sub-trees a rank owns and the
+    # level 0 of the cells it leads; phase 2: its level-1 sub-trees of split
+    # cells.  Raw = arrivals; weighted = the time model of plan_split (a level-0
+    # arrival costs L0_COST deeper ones: binning + level-0 slabs 36 ms for 1B
+    # level-0 arrivals vs 38 ms for 2B deeper ones on config 4, DESIGN.md §5).
+    from pcconv.dist import L0_COST
+    ph = [r.local["phases"] for r in res]
+    l0 = [r.recv_points for r in res]   # level-0 arrivals (whole + led cells)
+    p1 = [p["lead"] + p["whole"] for p in ph]
+    p2 = [p["sub"] for p in ph]
+    w1 = [a + (L0_COST - 1.0) * b for a, b in zip(p1, l0)]
+    mean = fx["arrivals"] / world
+    wmean = (fx["arrivals"] + (L0_COST - 1.0) * s["n"]) / world
+    ratio = (max(p1) + max(p2)) / mean
+    wratio = (max(w1) + max(p2)) / wmean
+    whole_only = max(sub["W"] for sub in fx["subtrees"])   # the largest level-0 sub-tree alone, unsplit
+    report = {"world": world, "plan": res[0].plan, "phase1_arrivals": p1, "phase2_arrivals": p2,
+              "level0_arrivals": l0, "critical_path_over_mean_raw": ratio,
+              "critical_path_over_mean_weighted": wratio, "largest_level0_subtree_over_mean": whole_only / mean,
+              "sub_points": [r.sub_points for r in res], "ms_rank0": res[0].ms}
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open("gpurun_out/config3_split_balance.json", "w") as f:
+        json.dump(report, f, indent=1)
+    assert res[0].plan["split_cells"] > 0
+    assert wratio <= 1.2, report
