@@ -208,13 +208,17 @@ L0_COST, DEEP_COST, DEPTH = 2.0, 1.0, 4.0
 def _lpt(w: np.ndarray, world: int):
     """Largest-first greedy: item i (weight w[i], ties by index) to the least
     loaded rank (ties by rank).  Deterministic on every rank."""
+    import heapq
     w = np.asarray(w, dtype=np.float64)
     own = np.zeros(len(w), dtype=np.uint32)
     load = np.zeros(world, dtype=np.float64)
-    for i in np.lexsort((np.arange(len(w)), -w)):
-        r = int(np.argmin(load))
+    heap = [(0.0, r) for r in range(world)]
+    for i in np.lexsort((np.arange(len(w)), -w)).tolist():
+        ld, r = heapq.heappop(heap)
         own[i] = r
-        load[r] += w[i]
+        ld += float(w[i])
+        load[r] = ld
+        heapq.heappush(heap, (ld, r))
     return own, load
 
 

@@ -4,10 +4,12 @@
 Streams the config-3 generator (synthetic kind 2, seed 3, 100M points in
 [-1000,1000)^3; oracle/pcc_oracle.c orc_synth) in chunks, histograms it per
 level-0 cell and per level-1 cell, and writes tests/golden/config3_hist.json.
-Then reports, for 2/4/8 ranks, the rank loads of
-  * assign_owners (level-0 ownership only): max/mean of points and of W
-    (W per level-0 sub-tree from tests/golden/large_digests.json);
-  * plan_split (heavy cells shared at level 1): its cost-model estimate.
+Then reports, for 2/4/8 ranks, the rank loads of assign_owners (whole level-0
+cells per rank): max/mean of points and of W (W per level-0 sub-tree from
+tests/golden/large_digests.json).  The measured loads with heavy cells shared
+slab by slab (plan_split) come from the full-size GPU run,
+tests/test_large_gpu.py::test_config3_sharded_8_ranks_split_cells
+(profiles/r2_config3_split_balance_8ranks.json).
 
   python scripts/config3_balance.py [--out profiles/r2_config3_balance.json]
 """
@@ -23,7 +25,7 @@ sys.path.insert(0, os.path.join(ROOT, "point-cloud_amd"))
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 from oracle_ctypes import synth  # noqa: E402
-from pcconv.dist import assign_owners, plan_split  # noqa: E402
+from pcconv.dist import assign_owners  # noqa: E402
 
 N, SEED, KIND, CHUNK = 100_000_000, 3, 2, 5_000_000
 
@@ -92,10 +94,8 @@ def balance_report(fx):
         o = assign_owners(hist0, world)
         lp = np.array([hist0[o == r].sum() for r in range(world)])
         lw = np.array([W[o == r].sum() for r in range(world)])
-        p = plan_split(hist0, hist1, ch, world)
         out["ranks"][str(world)] = {"assign_owners_points_max_over_mean": float(lp.max() / lp.mean()),
-                                    "assign_owners_W_max_over_mean": float(lw.max() / lw.mean()),
-                                    "plan_split_estimate": p.est}
+                                    "assign_owners_W_max_over_mean": float(lw.max() / lw.mean())}
     return out
 
 
