@@ -33,7 +33,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--points", type=int, default=1_000_000_000)
-    ap.add_argument("--kind", type=int, default=0, help="0 uniform (config 4), 1 clustered (config 3)")
+    ap.add_argument("--kind", type=int, default=0,
+                    help="0 uniform (config 4), 2 Gaussian mixture (config 3, SURVEY 8d), 1 clustered blobs")
     ap.add_argument("--seed", type=int, default=4)
     ap.add_argument("--cpu-sample", type=int, default=20_000_000, help="oracle prefix sample (points); 0 = skip")
     ap.add_argument("--no-profile", action="store_true")
@@ -104,6 +105,25 @@ def cpu_baseline(args):
                                f"the full {args.points}-point run ({lv} levels, as the full run), sequential C "
                                f"restatement (oracle/pcc_oracle.c, in-memory cells = mode (B), 10 000-point "
                                f"batches), {dt:.1f} s"}, **host_cpu())
+    if args.kind == 0 and args.merge_prior:
+        # Config 5's shape at the full run's density: the existing cloud's and the
+        # new points' share of one level-1 cell, [0, 500)^3 (1/64 of each, the
+        # same depth per point and the same old:new ratio); the existing cloud is
+        # converted untimed, the merge of the new points is timed
+        n0, n = args.merge_prior // 64, args.points // 64
+        o = Oracle()
+        o.add_file(synth(4, 0, n0, lo=0.0, ext=500.0))
+        pts = synth(args.seed, 0, n, lo=0.0, ext=500.0)
+        t0 = time.perf_counter()
+        o.add_file(pts)
+        dt = time.perf_counter() - t0
+        lv = o.hierarchies
+        o.close()
+        return dict({"value": n / dt, "unit": "points/s", "cores": 1, "kind": "port",
+                     "sample": f"merge of {n} uniform points (seed {args.seed}) into an in-memory cloud of {n0} "
+                               f"(seed 4), both in the level-1 cell [0,500)^3 at the full run's density ({lv} levels), "
+                               f"sequential C restatement (oracle/pcc_oracle.c, 10 000-point batches), {dt:.1f} s"},
+                    **host_cpu())
     n = min(args.cpu_sample, args.points)
     pts = synth(args.seed, args.kind, n)
     o = Oracle()
@@ -126,7 +146,14 @@ def cpu_baseline(args):
 METRIC = "points/sec converted (octree+LOD build), 1B synthetic pts, 1/2/4/8 MI355X"
 
 
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r1_pmc_traffic_1b.json")
+def _latest_pmc():
+    """The newest round's committed PMC summary (profiles/rNN_pmc_traffic_1b.json)."""
+    import glob
+    c = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic_1b.json")))
+    return c[-1] if c else os.path.join(ROOT, "profiles", "r1_pmc_traffic_1b.json")
+
+
+PMC_SUMMARY = _latest_pmc()
 
 
 def pmc_traffic(workload):
@@ -150,8 +177,9 @@ def record(args, n_gpus, ms, st_levels, st_cells, st_slabs, arrivals, k, dense_m
     dense_arr = k["dense_arrivals"]
     achieved = 32.0 * dense_arr / (dense_ms / 1e3) / 1e9 if dense_ms > 0 else 0.0
     whole = 32.0 * arrivals / (ms / 1e3) / 1e9
-    workload = ("config4: %d uniform points in [-1000,1000)^3, seed %d" if args.kind == 0 else
-                "config3-shape: %d clustered points, seed %d") % (args.points, args.seed)
+    workload = {0: "config4: %d uniform points in [-1000,1000)^3, seed %d",
+                2: "config3: %d Gaussian-mixture points (32 clusters, SURVEY 8d), seed %d"}.get(
+        args.kind, "clustered blobs: %d points, seed %d") % (args.points, args.seed)
     if args.merge_prior:
         workload = ("config5: +%d %s points (seed %d) merged into the %d-point config-4 cloud (seed 4)" %
                     (args.points, "uniform" if args.kind == 0 else "clustered", args.seed, args.merge_prior))

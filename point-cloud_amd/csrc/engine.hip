@@ -576,7 +576,7 @@ __global__ void k_l0_hash_ids(const unsigned long long* hkeys, uint32_t cap, uin
 #define PCC_L0IPT 3
 #endif
 constexpr int kL0BS = PCC_L0BS, kL0IPT = PCC_L0IPT, kL0Tile = kL0BS * kL0IPT, kL0W = kL0BS / 64;
-constexpr int kHistLds = 8192;
+constexpr int kHistLds = 16384;   // dense level-0 slabs counted in LDS (64 KB): 64 cells x 256 layers
 constexpr uint32_t kL0DownGrid = 512;   // persistent blocks of the fused upsweep (2 per CU)
 
 // Pass-0 upsweep from the AoS input, fused with the bounding box
@@ -636,6 +636,19 @@ __global__ __launch_bounds__(kL0BS) void k_l0_up0_bbox(const Point* __restrict__
 
 // Pass-1 upsweep from the arena: per-tile digit histogram + the full dense-slab
 // histogram (LDS-privatised when it fits), grid-stride over the tiles.
+// Global histogram increment with one atomic per distinct bin of the active
+// lanes when they all hit the same bin (a run of one slab: clustered or
+// partially sorted input), else one per lane.
+__device__ __forceinline__ void wave_aggregated_add(uint32_t* hist, uint32_t d) {
+    const uint32_t d0 = __builtin_amdgcn_readfirstlane(d);
+    const unsigned long long same = __ballot(d == d0), act = __ballot(1);
+    if (same == act) {
+        if (__lane_id() == (uint32_t)__ffsll((long long)act) - 1) atomicAdd(&hist[d0], (uint32_t)__popcll(act));
+    } else {
+        atomicAdd(&hist[d], 1u);
+    }
+}
+
 template <int BITS>
 __global__ __launch_bounds__(kL0BS) void k_l0_up_hist(Arena A, uint64_t n, L0Params P, int shift,
                                                       uint32_t* __restrict__ counts, uint32_t ntiles, uint32_t* hist,
@@ -663,7 +676,8 @@ __global__ __launch_bounds__(kL0BS) void k_l0_up_hist(Arena A, uint64_t n, L0Par
                 const int64_t d = l0_dense(P, v[r].x, v[r].y, v[r].z);
                 if (d < 0) { err = ERR_L0_RANGE; continue; }
                 atomicAdd(&dh[((uint64_t)d >> shift) & (R - 1)], 1u);
-                if (lds) atomicAdd(&h[d], 1u); else atomicAdd(&hist[d], 1u);
+                if (lds) atomicAdd(&h[d], 1u);
+                else wave_aggregated_add(hist, (uint32_t)d);   // clustered input: few hot slabs
             }
         }
         __syncthreads();
@@ -3711,7 +3725,7 @@ __device__ __forceinline__ uint32_t shard_unit(const ShardGrid& g, const ShardSl
 
 constexpr int kShBS = 256;
 // per-block LDS histogram (ncells <= kShLds), else global atomics
-constexpr uint32_t kShLds = 8192;
+constexpr uint32_t kShLds = 16384;
 __global__ __launch_bounds__(kShBS) void k_shard_hist(const Point* __restrict__ in, uint64_t n, ShardGrid g,
                                                       ShardSlabs m, uint32_t ncells, uint32_t* hist, uint32_t* bad) {
     __shared__ uint32_t h[kShLds];
@@ -3725,7 +3739,7 @@ __global__ __launch_bounds__(kShBS) void k_shard_hist(const Point* __restrict__ 
         const float4 v = p4[i];
         const uint32_t c = shard_unit(g, m, v.x, v.y, v.z);
         if (c == 0xFFFFFFFFu) { nbad++; continue; }
-        if (lds) atomicAdd(&h[c], 1u); else atomicAdd(&hist[c], 1u);
+        if (lds) atomicAdd(&h[c], 1u); else wave_aggregated_add(hist, c);
     }
     if (nbad) atomicAdd(bad, nbad);
     __syncthreads();
