@@ -670,12 +670,17 @@ static int load_cell_file(orc_conv* c, const char* path) {
 /* Loads dir/metadata.json (config, counters, bbox) and every h_{h}/c_*.bin for
  * h < hierarchies.  Returns 0, or -ENOENT when there is no metadata.json. */
 #include <dirent.h>
+/* lib.rs:86-101 + converter.rs:187-207: metadata.json when present (else the
+ * defaults: no points, no hierarchies), and every existing cell file, whatever
+ * metadata.json says -- the reference opens a cell's file whenever the cell is
+ * first touched, so cell files without (or beyond) metadata.json are merged
+ * too (a crashed run's stale cells). */
 int orc_load(orc_conv* c, const char* dir) {
     char path[4096];
     snprintf(path, sizeof path, "%s/metadata.json", dir);
     int r = load_metadata(c, path);
-    if (r) return r == -ENOENT ? -ENOENT : r;
-    for (uint32_t h = 0; h < c->hierarchies; h++) {
+    if (r && r != -ENOENT) return r;
+    for (uint32_t h = 0; h < 31; h++) {
         snprintf(path, sizeof path, "%s/h_%u", dir, h);
         DIR* d = opendir(path);
         if (!d) continue;

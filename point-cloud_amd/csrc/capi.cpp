@@ -1,4 +1,5 @@
 // capi.cpp — extern "C" boundary (include/pcconv.h) over pcc::Engine.
+#include <dirent.h>
 #include <sys/stat.h>
 
 #include <algorithm>
@@ -143,6 +144,22 @@ int pcc_options_default(pcc_options* o) {
     return 0;
 }
 
+static bool any_cell_file(const std::string& dir) {
+    for (uint32_t h = 0; h < 31; h++) {
+        DIR* d = opendir((dir + "/h_" + std::to_string(h)).c_str());
+        if (!d) continue;
+        bool found = false;
+        while (dirent* e = readdir(d)) {
+            int x, y, z;
+            char tail[8] = {0};
+            if (sscanf(e->d_name, "c_%d_%d_%d.%3s", &x, &y, &z, tail) == 4 && strcmp(tail, "bin") == 0) { found = true; break; }
+        }
+        closedir(d);
+        if (found) return true;
+    }
+    return false;
+}
+
 static int open_impl(const char* out_dir, const pcc_options* opt, const std::vector<int32_t>* subtrees,
                      pcc_converter** out) {
     if (!out_dir || !out) return set_err(-EINVAL, "null argument");
@@ -164,11 +181,14 @@ static int open_impl(const char* out_dir, const pcc_options* opt, const std::vec
         Metadata m;
         if (!parse_metadata_json(ss.str(), m, err)) return set_err(-EINVAL, err);
         c->meta.config = m.config;
-        if (m.number_of_points > 0) {
-            c->merge = true;
-            c->prior = m;
-        }
+        c->prior = m;
+        c->merge = m.number_of_points > 0;
     }
+    // converter.rs:187-207 opens a cell's existing file whenever the cell is
+    // first touched, whatever metadata.json says: cell files left without
+    // metadata.json (a run that never reached Drop) are merged as well, with
+    // the counters starting from metadata.json or from zero
+    if (!c->merge && any_cell_file(c->out_dir)) c->merge = true;
     // converter.rs:79-94 create_dir_all
     if (!mkdirs(c->out_dir)) return set_err(-EIO, "cannot create output directory " + c->out_dir);
     int ndev = 0;
@@ -178,7 +198,7 @@ static int open_impl(const char* out_dir, const pcc_options* opt, const std::vec
     c->eng = std::make_unique<Engine>(c->meta.config, c->opt.device);
     if (c->merge) {   // converter.rs:187-207: existing cells are the starting state
         std::string err;
-        int rc = read_cloud(c->out_dir, c->prior.hierarchies, c->prior_cells, err, subtrees);
+        int rc = read_cloud(c->out_dir, 31, c->prior_cells, err, subtrees);
         if (rc) return set_err(rc, err);
         PriorState ps;
         rc = prior_from_cells(c->prior_cells, c->meta.config, ps, err);
@@ -259,11 +279,17 @@ int pcc_build(pcc_converter* c) {
     m.hierarchies = c->eng->hierarchies();
     if (m.number_of_points > 0)
         for (int a = 0; a < 3; a++) { m.bmin[a] = c->eng->bbox_min()[a]; m.bmax[a] = c->eng->bbox_max()[a]; }
+    if (c->merge && c->prior.number_of_points == 0 && m.number_of_points > 0) {
+        // stale cells, no counted cloud: the engine's box also spans the seeds,
+        // the reference's (converter.rs:96-104) only the new points
+        const int rc2 = shard_bbox(c->eng->input_points(), m.number_of_points, m.bmin, m.bmax, c->opt.device);
+        if (rc2) return set_err(rc2, "bounding box of the new points failed");
+    }
     if (c->merge) {   // lib.rs:86-101: counters continue from the loaded metadata; Aabb::extend_aabb
         const Metadata& p = c->prior;
         if (m.number_of_points == 0)
             for (int a = 0; a < 3; a++) { m.bmin[a] = p.bmin[a]; m.bmax[a] = p.bmax[a]; }
-        else
+        else if (p.number_of_points > 0)   // converter.rs:96-104: the first batch assigns when the count is 0
             for (int a = 0; a < 3; a++) { m.bmin[a] = std::fmin(m.bmin[a], p.bmin[a]); m.bmax[a] = std::fmax(m.bmax[a], p.bmax[a]); }
         m.number_of_points += p.number_of_points;
         m.hierarchies = std::max(m.hierarchies, p.hierarchies);

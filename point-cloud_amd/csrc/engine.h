@@ -180,6 +180,8 @@ public:
 
     // device pointer of the input (16 B AoS points), for benchmarking
     Point* device_input() { return d_in_; }
+    // the new points of this build (own buffer or the borrowed keyed input)
+    const Point* input_points() const { return ext_in_ ? ext_in_ : d_in_; }
 
 private:
     struct Level;     // device tables of one level

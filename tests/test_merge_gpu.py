@@ -94,3 +94,42 @@ def test_adopt_prior_equals_directory_merge():
         d, mg, mo = compare_dirs(t1, to, fast=True)
         assert d == [] and mg == mo
         assert st["number_of_points"] == 280_000
+
+
+@pytest.mark.parametrize("meta", ["removed", "zero_points"])
+def test_stale_cells_merge_like_the_reference(meta):
+    """Cell files without a valid cloud behind them (metadata.json missing, or a
+    metadata.json that counts no points: a run that never reached Drop,
+    converter.rs:241-246).  The reference opens every touched cell's existing
+    file (converter.rs:187-207) whatever lib.rs:86-101 found, so the stale cells
+    are merged while the counters start again from metadata.json or zero.  The
+    HIP build must write what the oracle (orc_load: metadata optional, every cell
+    file) writes for the same directory."""
+    import json
+    from gpu_util import Oracle
+    cfg = dict(sub_grid_dimension=16, cell_point_overflow_limit=100)
+    old, new = [synth(71, 1, 200_000)], [synth(72, 1, 80_000)]
+    with tempfile.TemporaryDirectory() as tg, tempfile.TemporaryDirectory() as to:
+        run_gpu(tg, old, cfg=cfg)
+        mp = os.path.join(tg, "metadata.json")
+        if meta == "removed":
+            os.remove(mp)
+        else:
+            m = json.load(open(mp))
+            m["number_of_points"], m["hierarchies"] = 0, 0
+            m["bounding_box"] = {"min": [0.0, 0.0, 0.0], "max": [0.0, 0.0, 0.0]}
+            json.dump(m, open(mp, "w"), indent=2)
+        shutil.rmtree(to)
+        shutil.copytree(tg, to)
+        o = Oracle(cfg)
+        o.load(to)
+        for f in new:
+            o.add_file(f, 10_000)
+        assert o.error == 0
+        o.write(to)
+        o.close()
+        run_gpu(tg, new, cfg=cfg)
+        d, mg, mo = compare_dirs(tg, to)
+        assert d == [], d
+        assert mg == mo
+        assert mg["number_of_points"] == len(new[0])
