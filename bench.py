@@ -263,7 +263,8 @@ def main_sharded(args, rank, world):
         rec = record(args, world, ms, max(p[0] for p in per), sum(p[1] for p in per), sum(p[2] for p in per),
                      sum(p[3] for p in per), k, dense_ms, f"level-0 cell sharding over {world} ranks (grouped RCCL point-to-point exchange)")
         rec["sharding"] = {"points_per_rank": [p[4] for p in per], "stage_ms_rank0": stage,
-                           "hierarchies": res.summary["hierarchies"]}
+                           "hierarchies": res.summary["hierarchies"], "plan": res.plan,
+                           "phases_rank0": res.local.get("phases")}
         json_out.write(json.dumps(rec) + "\n")
         json_out.flush()
     dist.destroy_process_group()

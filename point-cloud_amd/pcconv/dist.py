@@ -813,12 +813,14 @@ def shard_build(comm, ops, pts: torch.Tensor, key0: int, file_points, write: boo
             sh = ops.slab_histogram(pts, grid)
             sh_h = comm.allreduce_(sh.to(comm.device), "sum").cpu().numpy().astype(np.int64)
             hist_h = sh_h.reshape(-1, NL).sum(axis=1)
-            h1 = ops.histogram(pts, grid1)
-            hist1_h = comm.allreduce_(h1.to(comm.device), "sum").cpu().numpy().astype(np.int64)
-            ch = np.full((len(hist_h), 8), -1, dtype=np.int64)
-            nz = np.flatnonzero(hist_h)
-            ch[nz] = children_ids(nz, grid, grid1)
-            plan = plan_split(hist_h, hist1_h, ch, W, slab_hist=sh_h)
+            plan = plan_split(hist_h, None, None, W, allow=False)
+            if plan.est["ratio"] > 1.02:   # whole cells unbalanced: consider sharing (level-1 histogram)
+                h1 = ops.histogram(pts, grid1)
+                hist1_h = comm.allreduce_(h1.to(comm.device), "sum").cpu().numpy().astype(np.int64)
+                ch = np.full((len(hist_h), 8), -1, dtype=np.int64)
+                nz = np.flatnonzero(hist_h)
+                ch[nz] = children_ids(nz, grid, grid1)
+                plan = plan_split(hist_h, hist1_h, ch, W, slab_hist=sh_h)
         else:
             hist = ops.histogram(pts, grid)
             hist_h = comm.allreduce_(hist.to(comm.device), "sum").cpu().numpy().astype(np.int64)
