@@ -501,6 +501,34 @@ def cell_view(c: dict):
     return v
 
 
+def shard_grid(gmin, gmax, max_cell_size: float, level: int = 0):
+    """The unit grid of ownership.  Level 0: the level-0 cells spanned by the
+    global bbox; when that grid exceeds the 2^22 cells pcc_shard_grid_from_bbox
+    allows (a sparse, widely spread cloud), cells of 2^k x the size, k smallest
+    that fits: floor(p / (cs 2^k)) = floor(p / cs) >> k exactly (power-of-two
+    scaling), so a coarse cell is a block of whole level-0 cells and every
+    level-0 sub-tree still has one owner (`grid.coarse` = k; cells are not
+    shared then).  Level 1 (cell sharing): None when too large."""
+    cs = max_cell_size / float(1 << level)
+    if level > 0:
+        try:
+            g = pcconv.shard_grid_from_bbox(gmin, gmax, cs)
+        except pcconv.PccError:
+            return None
+        g.coarse = 0
+        return g
+    for k in range(0, 24):
+        try:
+            g = pcconv.shard_grid_from_bbox(gmin, gmax, cs * float(1 << k))
+        except pcconv.PccError as e:
+            if e.code != -27:   # -EFBIG: grid too large, try coarser cells
+                raise
+            continue
+        g.coarse = k
+        return g
+    raise ValueError("bounding box too large for the shard grid")
+
+
 # ----------------------------------------------------------------- local ops (product)
 class HipShardOps:
     """Local per-rank work on the GPU through libpcconv.so (no CPU fallback)."""
@@ -569,15 +597,7 @@ class HipShardOps:
         return pcconv.shard_bbox(pts.data_ptr(), pts.shape[0], self.dev)
 
     def grid(self, gmin, gmax, level: int = 0):
-        """Shard grid of the level's cells (metadata.rs:91-93 cell size); None when
-        a level > 0 grid would be too large."""
-        cs = self.max_cell_size / float(1 << level)
-        if level == 0:
-            return pcconv.shard_grid_from_bbox(gmin, gmax, cs)
-        try:
-            return pcconv.shard_grid_from_bbox(gmin, gmax, cs)
-        except pcconv.PccError:
-            return None
+        return shard_grid(gmin, gmax, self.max_cell_size, level)
 
     def begin_step(self):
         self._built = []
@@ -806,24 +826,27 @@ def shard_build(comm, ops, pts: torch.Tensor, key0: int, file_points, write: boo
         # 3. ownership: level-0 cells; heavy ones shared slab by slab
         from pcconv import SHARD_LAYERS as NL
         grid = ops.grid(gmin, gmax)
-        grid1 = ops.grid(gmin, gmax, level=1) if (split and not merge and W > 1) else None
+        coarse = int(getattr(grid, "coarse", 0))
+        if merge and coarse:
+            raise ValueError("sharded merge: the existing cloud's bounding box spans more than 2^22 level-0 cells")
+        grid1 = ops.grid(gmin, gmax, level=1) if (split and not merge and W > 1 and not coarse) else None
         if grid1 is not None and (int(grid1.ncells) > (1 << 22) or int(grid.ncells) * NL > (1 << 24)):
             grid1 = None
         if grid1 is not None:
             sh = ops.slab_histogram(pts, grid)
-            sh_h = comm.allreduce_(sh.to(comm.device), "sum").cpu().numpy().astype(np.int64)
+            sh_h = comm.allreduce_(sh.to(comm.device).to(torch.int64), "sum").cpu().numpy()
             hist_h = sh_h.reshape(-1, NL).sum(axis=1)
             plan = plan_split(hist_h, None, None, W, allow=False)
             if plan.est["ratio"] > 1.02:   # whole cells unbalanced: consider sharing (level-1 histogram)
                 h1 = ops.histogram(pts, grid1)
-                hist1_h = comm.allreduce_(h1.to(comm.device), "sum").cpu().numpy().astype(np.int64)
+                hist1_h = comm.allreduce_(h1.to(comm.device).to(torch.int64), "sum").cpu().numpy()
                 ch = np.full((len(hist_h), 8), -1, dtype=np.int64)
                 nz = np.flatnonzero(hist_h)
                 ch[nz] = children_ids(nz, grid, grid1)
                 plan = plan_split(hist_h, hist1_h, ch, W, slab_hist=sh_h)
         else:
             hist = ops.histogram(pts, grid)
-            hist_h = comm.allreduce_(hist.to(comm.device), "sum").cpu().numpy().astype(np.int64)
+            hist_h = comm.allreduce_(hist.to(comm.device).to(torch.int64), "sum").cpu().numpy()
             plan = plan_split(hist_h, None, None, W, allow=False)
         owner_h = plan.owner0
         owned = int(np.count_nonzero((owner_h == comm.rank) & (hist_h > 0) & ~plan.split))

@@ -73,7 +73,8 @@ class NumpyShardOps:
         return ([float(p[a].min()) for a in "xyz"], [float(p[a].max()) for a in "xyz"])
 
     def grid(self, gmin, gmax, level: int = 0):
-        return pcconv.shard_grid_from_bbox(gmin, gmax, self.max_cell_size / float(1 << level))   # host-only C-ABI helper
+        from pcconv.dist import shard_grid
+        return shard_grid(gmin, gmax, self.max_cell_size, level)   # host-only C-ABI helper
 
     def begin_step(self):
         for o in self.oracles:

@@ -409,3 +409,39 @@ def test_plan_split_uniform_is_assign_owners():
     assert p3.split[0] and not p3.split[1:].any()
     assert sorted(set(p3.slab_owner[20:60].tolist())) == [0, 1, 2, 3]
     assert p3.est["ratio"] < 0.8 * plan_split(h0, None, None, 4, allow=False).est["ratio"]
+
+
+def test_thread_ranks_sparse_wide_cloud_coarse_grid(tmp_path):
+    """A cloud whose level-0 grid exceeds the shard grid's 2^22 cells (64e9 cells
+    of size 1 here): ownership falls back to blocks of 2^k x 2^k x 2^k level-0
+    cells (shard_grid), every level-0 sub-tree still on one rank == the oracle."""
+    import threading
+    from pcconv.dist import shard_grid
+    cfg = {"sub_grid_dimension": 4, "cell_point_overflow_limit": 8, "max_cell_size": 1.0}
+    files = [synth(81, 0, 30_000, lo=-2000.0, ext=4000.0), synth(82, 1, 20_000, lo=-2000.0, ext=4000.0)]
+    g = shard_grid([-2000.0] * 3, [2000.0] * 3, 1.0)
+    assert g.coarse > 0 and g.ncells <= (1 << 22)
+    fp = [len(f) for f in files]
+    out = str(tmp_path / "out")
+    world = 3
+    grp = ThreadGroup(world)
+    res, errs = [None] * world, []
+
+    def worker(r):
+        try:
+            pts, key0 = rank_slice(files, r, world)
+            ops = NumpyShardOps(out, config=cfg)
+            res[r] = shard_build(ThreadComm(grp, r, torch.device("cpu")), ops, as_tensor(pts), key0, fp, write=True)
+            ops.close()
+        except BaseException as e:  # noqa: BLE001
+            errs.append(e)
+            grp.bar.abort()
+
+    th = [threading.Thread(target=worker, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs
+    assert sum(r.recv_points for r in res) == sum(fp)
+    check_against_oracle(tmp_path, files, out, res[0].summary, cfg=cfg)

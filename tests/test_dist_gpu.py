@@ -186,3 +186,14 @@ def test_sharded_threads_split_cells_match_oracle(tmp_path, world):
     assert sum(r.local["phases"]["sub"] for r in res) > 0
     assert sum(r.recv_points for r in res) == sum(len(f) for f in files)
     check_against_oracle(tmp_path, files, out, res[0].summary, cfg=SKEW_CFG)
+
+
+def test_sharded_threads_sparse_wide_cloud_coarse_grid(tmp_path):
+    """Level-0 grid beyond the shard grid's 2^22 cells: ownership by blocks of
+    level-0 cells (pcconv.dist.shard_grid), hashed level-0 grid per rank."""
+    cfg = {"sub_grid_dimension": 4, "cell_point_overflow_limit": 8, "max_cell_size": 1.0}
+    files = [synth(81, 0, 30_000, lo=-2000.0, ext=4000.0), synth(82, 1, 20_000, lo=-2000.0, ext=4000.0)]
+    out = str(tmp_path / "out")
+    res = _run_threads(files, 3, out, cfg=cfg)
+    assert sum(r.recv_points for r in res) == sum(len(f) for f in files)
+    check_against_oracle(tmp_path, files, out, res[0].summary, cfg=cfg)
