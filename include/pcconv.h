@@ -95,6 +95,18 @@ int pcc_open_subtrees(const char* out_dir, const pcc_options* opt, const int32_t
  * (lib.rs:31-52).  Host memory; copied to the device; caller keeps ownership. */
 int pcc_add_points(pcc_converter* c, const pcc_point* pts, uint64_t n);
 
+/* One file delivered in pieces (the CLI's readers use it; a host reading a
+ * file in chunks would too): pcc_begin_file, then pcc_append_points for each
+ * piece in file order, then pcc_end_file(keep) -- the file is the first `keep`
+ * points appended (a reader error keeps the complete batches, lib.rs:31-52).
+ * The pieces are staged through pinned host buffers and copied to the device
+ * on a copy stream while the caller reads the next piece.  pcc_cancel_file:
+ * the open file contributes nothing (not even a batch). */
+int pcc_begin_file(pcc_converter* c, uint64_t expected_points);
+int pcc_append_points(pcc_converter* c, const pcc_point* pts, uint64_t n);
+int pcc_end_file(pcc_converter* c, uint64_t keep_points);
+int pcc_cancel_file(pcc_converter* c);
+
 /* Same as pcc_add_points for points already resident in device memory. */
 int pcc_add_points_device(pcc_converter* c, const pcc_point* dev_pts, uint64_t n);
 

@@ -65,6 +65,7 @@ struct pcc_converter {
     std::unique_ptr<Engine> eng;
     bool built = false;
     bool keyed = false;         // pcc_declare_files: sharded input
+    bool streaming = false;     // a file opened by pcc_begin_file
     bool summary_set = false;   // pcc_set_summary: global metadata values
     double build_ms = 0;
     bool merge = false;         // out_dir held a non-empty cloud: incremental merge
@@ -226,6 +227,7 @@ int pcc_open_subtrees(const char* out_dir, const pcc_options* opt, const int32_t
 }
 
 int pcc_add_points(pcc_converter* c, const pcc_point* pts, uint64_t n) {
+    if (c && c->streaming) return set_err(-EINVAL, "a file opened by pcc_begin_file is still open");
     if (c && c->keyed) return set_err(-EINVAL, "converter takes keyed (sharded) input after pcc_declare_files");
     if (!c || (!pts && n)) return set_err(-EINVAL, "null argument");
     if (c->built) return set_err(-EINVAL, "points added after build");
@@ -236,6 +238,7 @@ int pcc_add_points(pcc_converter* c, const pcc_point* pts, uint64_t n) {
 }
 
 int pcc_add_points_device(pcc_converter* c, const pcc_point* pts, uint64_t n) {
+    if (c && c->streaming) return set_err(-EINVAL, "a file opened by pcc_begin_file is still open");
     if (c && c->keyed) return set_err(-EINVAL, "converter takes keyed (sharded) input after pcc_declare_files");
     if (!c || (!pts && n)) return set_err(-EINVAL, "null argument");
     if (c->built) return set_err(-EINVAL, "points added after build");
@@ -245,7 +248,49 @@ int pcc_add_points_device(pcc_converter* c, const pcc_point* pts, uint64_t n) {
     GUARD_END
 }
 
+int pcc_begin_file(pcc_converter* c, uint64_t expected_points) {
+    if (!c) return set_err(-EINVAL, "null argument");
+    if (c->built) return set_err(-EINVAL, "points added after build");
+    if (c->keyed) return set_err(-EINVAL, "keyed (sharded) input takes no files");
+    if (c->streaming) return set_err(-EINVAL, "a file is already open");
+    GUARD_BEGIN
+    c->eng->stream_begin(expected_points);
+    c->streaming = true;
+    return 0;
+    GUARD_END
+}
+
+int pcc_append_points(pcc_converter* c, const pcc_point* pts, uint64_t n) {
+    if (!c || (!pts && n)) return set_err(-EINVAL, "null argument");
+    if (!c->streaming) return set_err(-EINVAL, "pcc_begin_file must come first");
+    GUARD_BEGIN
+    c->eng->stream_push(reinterpret_cast<const Point*>(pts), n);
+    return 0;
+    GUARD_END
+}
+
+int pcc_end_file(pcc_converter* c, uint64_t keep_points) {
+    if (!c) return set_err(-EINVAL, "null argument");
+    if (!c->streaming) return set_err(-EINVAL, "no file is open");
+    GUARD_BEGIN
+    c->eng->stream_end(keep_points, c->opt.batch_size);
+    c->streaming = false;
+    return 0;
+    GUARD_END
+}
+
+int pcc_cancel_file(pcc_converter* c) {
+    if (!c) return set_err(-EINVAL, "null argument");
+    if (!c->streaming) return set_err(-EINVAL, "no file is open");
+    GUARD_BEGIN
+    c->eng->stream_cancel();
+    c->streaming = false;
+    return 0;
+    GUARD_END
+}
+
 int pcc_add_empty_batches(pcc_converter* c, uint32_t k) {
+    if (c && c->streaming) return set_err(-EINVAL, "a file opened by pcc_begin_file is still open");
     if (!c) return set_err(-EINVAL, "null argument");
     if (c->built) return set_err(-EINVAL, "points added after build");
     c->eng->add_empty_batches(k);
@@ -264,6 +309,7 @@ int pcc_add_synthetic(pcc_converter* c, uint64_t seed, int kind, uint64_t n, flo
 }
 
 int pcc_build(pcc_converter* c) {
+    if (c && c->streaming) return set_err(-EINVAL, "a file opened by pcc_begin_file is still open");
     if (!c) return set_err(-EINVAL, "null argument");
     GUARD_BEGIN
     const auto t0 = std::chrono::steady_clock::now();
@@ -734,21 +780,36 @@ int pcc_convert_files(const char* out_dir, const char* const* paths, size_t npat
         // So a file whose data ends early contributes its complete batches only.
         const uint64_t B = c->opt.batch_size;
         if (ext == "ply") {
+            // streamed: the reader's pieces go through the pinned ring to the
+            // device while the next piece is read (HIP-stream upload scheduler)
             PlyResult r;
             std::string err;
-            if (!read_ply(p, r, err)) {
+            bool open = false, logged = false;
+            uint64_t pushed = 0;
+            int src = 0;
+            const PointSink sink = [&](const Point* pts, uint64_t m) -> bool {
+                if (!logged) { log_line("INFO", "Converting %llu points", (unsigned long long)r.vertex_count); logged = true; }
+                if (!open) { if ((src = pcc_begin_file(c, r.vertex_count))) return false; open = true; }
+                if ((src = pcc_append_points(c, reinterpret_cast<const pcc_point*>(pts), m))) return false;
+                pushed += m;
+                return true;
+            };
+            const bool ok = read_ply(p, r, err, sink);
+            if (!ok || src) {
+                if (open) pcc_cancel_file(c);
                 pcc_close(c);
-                return set_err(-EIO, err);   // the reference unwraps header parsing (ply.rs:20-24)
+                return src ? src : set_err(-EIO, err);   // the reference unwraps header parsing (ply.rs:20-24)
             }
-            log_line("INFO", "Converting %llu points", (unsigned long long)r.vertex_count);
+            if (!logged) log_line("INFO", "Converting %llu points", (unsigned long long)r.vertex_count);
             if (r.ascii) {
                 const uint64_t nb = r.data_error.empty() ? std::max<uint64_t>(1, (r.vertex_count + B - 1) / B)
                                                          : r.ascii_lines / B;
                 if (nb) rc = pcc_add_empty_batches(c, (uint32_t)nb);
             } else {
-                const uint64_t keep = r.data_error.empty() ? r.points.size() : (r.points.size() / B) * B;
-                if (r.data_error.empty() || keep)
-                    rc = pcc_add_points(c, reinterpret_cast<const pcc_point*>(r.points.data()), keep);
+                // lib.rs:31-52: a truncated file keeps its complete batches; none at all: no batch
+                const uint64_t keep = r.data_error.empty() ? pushed : (pushed / B) * B;
+                if (open) rc = (r.data_error.empty() || keep) ? pcc_end_file(c, keep) : pcc_cancel_file(c);
+                else if (r.data_error.empty()) rc = pcc_add_points(c, nullptr, 0);   // an empty file: one empty batch
             }
             if (rc) { pcc_close(c); return rc; }
             if (!r.data_error.empty()) log_line("ERROR", "%s", r.data_error.c_str());

@@ -122,6 +122,14 @@ public:
     // (lib.rs:31-52: a file end is a batch boundary).  batch >= 1.
     void add_file_host(const Point* pts, uint64_t n, uint32_t batch);
     void add_file_device(const Point* dpts, uint64_t n, uint32_t batch);
+    // Streaming upload of one file (HIP-stream scheduler): host pieces are
+    // staged through a ring of pinned buffers and copied on a copy stream while
+    // the caller reads the next piece.  stream_end(keep): the file is the first
+    // `keep` points pushed (a truncated file keeps its complete batches).
+    void stream_begin(uint64_t expected);
+    void stream_push(const Point* pts, uint64_t n);
+    uint64_t stream_end(uint64_t keep, uint32_t batch);
+    void stream_cancel();   // the open file contributes nothing
     // A file whose reader yields k empty batches (ASCII PLY quirk, ply.rs:43-51).
     void add_empty_batches(uint32_t k) { nbatches_ += k; }
     // Synthetic input generated straight into HBM (bench / tests).
@@ -200,6 +208,13 @@ private:
     int device_;
     hipStream_t stream_;
     bool own_stream_ = false;
+    struct Staging { Point* host = nullptr; hipEvent_t done = nullptr; bool busy = false; };
+    static constexpr uint64_t kStagePts = 4ull << 20;   // 64 MB per pinned buffer
+    static constexpr int kStages = 4;
+    Staging stage_[kStages];
+    int stage_i_ = 0;
+    hipStream_t copy_ = nullptr;
+    uint64_t stream_n_ = 0;                              // points pushed into the open file
     uint64_t n_ = 0, cap_ = 0;
     uint32_t nbatches_ = 0;
     std::vector<uint64_t> file_start_;   // first point index per file

@@ -2587,6 +2587,11 @@ Engine::~Engine() {
     } catch (...) {
     }
     if (own_stream_) (void)hipStreamDestroy(stream_);
+    for (Staging& b : stage_) {
+        if (b.host) (void)hipHostFree(b.host);
+        if (b.done) (void)hipEventDestroy(b.done);
+    }
+    if (copy_) (void)hipStreamDestroy(copy_);
 }
 
 enum Stage { ST_L0 = 0, ST_DENSE, ST_SMALL, ST_BUCKET, ST_NEXT };
@@ -2708,6 +2713,58 @@ void Engine::add_file_host(const Point* pts, uint64_t n, uint32_t batch) {
     n_ += n;
     nbatches_ += batches_of(n, batch);
     HIP_CHECK(hipStreamSynchronize(stream_));
+}
+
+void Engine::stream_begin(uint64_t expected) {
+    if (!copy_) {
+        HIP_CHECK(hipStreamCreateWithFlags(&copy_, hipStreamNonBlocking));
+        for (Staging& b : stage_) {
+            HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&b.host), kStagePts * sizeof(Point), hipHostMallocDefault));
+            HIP_CHECK(hipEventCreateWithFlags(&b.done, hipEventDisableTiming));
+        }
+    }
+    comb_ok_ = false;
+    reserve(n_ + expected);
+    stream_n_ = 0;
+}
+
+void Engine::stream_push(const Point* pts, uint64_t n) {
+    while (n) {
+        Staging& b = stage_[stage_i_];
+        if (b.busy) HIP_CHECK(hipEventSynchronize(b.done));   // its previous copy has landed
+        const uint64_t m = std::min(n, kStagePts);
+        if (n_ + stream_n_ + m > cap_) {   // grow: the copies in flight must land in the old buffer first
+            HIP_CHECK(hipStreamSynchronize(copy_));
+            reserve(std::max<uint64_t>(n_ + stream_n_ + m, cap_ + cap_ / 2));
+        }
+        std::memcpy(b.host, pts, m * sizeof(Point));
+        HIP_CHECK(hipMemcpyAsync(d_in_ + n_ + stream_n_, b.host, m * sizeof(Point), hipMemcpyHostToDevice, copy_));
+        HIP_CHECK(hipEventRecord(b.done, copy_));
+        b.busy = true;
+        stream_n_ += m;
+        pts += m;
+        n -= m;
+        stage_i_ = (stage_i_ + 1) % kStages;
+    }
+}
+
+uint64_t Engine::stream_end(uint64_t keep, uint32_t batch) {
+    if (copy_) HIP_CHECK(hipStreamSynchronize(copy_));
+    for (Staging& b : stage_) b.busy = false;
+    keep = std::min(keep, stream_n_);
+    file_start_.push_back(n_);
+    file_eb0_.push_back(nbatches_);
+    file_batch_.push_back(std::max<uint32_t>(batch, 1));
+    n_ += keep;
+    nbatches_ += batches_of(keep, batch);
+    stream_n_ = 0;
+    return keep;
+}
+
+void Engine::stream_cancel() {
+    if (copy_) HIP_CHECK(hipStreamSynchronize(copy_));
+    for (Staging& b : stage_) b.busy = false;
+    stream_n_ = 0;
 }
 
 void Engine::add_file_device(const Point* dpts, uint64_t n, uint32_t batch) {

@@ -761,7 +761,7 @@ uint8_t sat_u8(float v) {
 }
 }  // namespace
 
-bool read_ply(const std::string& path, PlyResult& out, std::string& err) {
+bool read_ply(const std::string& path, PlyResult& out, std::string& err, const PointSink& sink) {
     std::ifstream f(path, std::ios::binary);
     if (!f) { err = "cannot open " + path; return false; }
     std::string line;
@@ -821,32 +821,54 @@ bool read_ply(const std::string& path, PlyResult& out, std::string& err) {
         return true;
     }
     const bool sw = enc == BE;
-    // fixed-size fast path
+    // fixed-size records: each property compiled once to (target, type, offset)
     bool fixed = true;
     int rec = 0;
     for (auto& p : vprops) { if (p.list) fixed = false; rec += psize(p.type); }
-    out.points.resize(nvert);
-    std::vector<uint8_t> buf;
-    auto apply = [&](Point& pt, const Prop& p, const uint8_t* q) {
-        // point.rs:61-130
-        const std::string& nm = p.name;
-        if (nm == "x" || nm == "y" || nm == "z") {
+    // point.rs:61-130 property names -> target: 0..2 x/y/z, 3..6 red/green/blue/alpha, -1 ignored
+    auto target = [](const std::string& nm) {
+        if (nm == "x") return 0;
+        if (nm == "y") return 1;
+        if (nm == "z") return 2;
+        if (nm == "red" || nm == "r") return 3;
+        if (nm == "green" || nm == "g") return 4;
+        if (nm == "blue" || nm == "b") return 5;
+        if (nm == "alpha" || nm == "a") return 6;
+        return -1;
+    };
+    auto apply = [&](Point& pt, int tg, PType ty, const uint8_t* q) {
+        if (tg < 0) return;
+        if (tg < 3) {
             float v;
-            if (p.type == P_F32) v = rd<float>(q, sw);
-            else if (p.type == P_F64) v = (float)rd<double>(q, sw);
+            if (ty == P_F32) v = rd<float>(q, sw);
+            else if (ty == P_F64) v = (float)rd<double>(q, sw);
             else return;
-            (nm == "x" ? pt.x : nm == "y" ? pt.y : pt.z) = v;
+            (tg == 0 ? pt.x : tg == 1 ? pt.y : pt.z) = v;
         } else {
-            int ch = (nm == "red" || nm == "r") ? 0 : (nm == "green" || nm == "g") ? 1 : (nm == "blue" || nm == "b") ? 2
-                   : (nm == "alpha" || nm == "a") ? 3 : -1;
-            if (ch < 0) return;
-            if (p.type == P_U8) pt.rgba[ch] = q[0];
-            else if (p.type == P_F32) pt.rgba[ch] = sat_u8(rd<float>(q, sw) / 255.0f);
+            if (ty == P_U8) pt.rgba[tg - 3] = q[0];
+            else if (ty == P_F32) pt.rgba[tg - 3] = sat_u8(rd<float>(q, sw) / 255.0f);
         }
     };
+    const uint64_t chunk = 1 << 18;
+    std::vector<Point> piece;
+    auto emit = [&](const Point* pts, uint64_t m, uint64_t base) -> bool {
+        if (sink) return sink(pts, m);
+        std::memcpy(out.points.data() + base, pts, m * sizeof(Point));
+        return true;
+    };
+    if (!sink) out.points.resize(nvert);
     if (fixed) {
-        const uint64_t chunk = 1 << 16;
-        buf.resize(chunk * rec);
+        struct Op { int tg; PType ty; int off; };
+        std::vector<Op> ops;
+        int off = 0;
+        for (auto& p : vprops) { ops.push_back({target(p.name), p.type, off}); off += psize(p.type); }
+        // the on-disk Point itself (float x, y, z; uchar red, green, blue, alpha; LE): a plain copy
+        const bool raw = !sw && rec == 16 && ops.size() == 7 && ops[0].tg == 0 && ops[0].ty == P_F32 &&
+                         ops[1].tg == 1 && ops[1].ty == P_F32 && ops[2].tg == 2 && ops[2].ty == P_F32 &&
+                         ops[3].tg == 3 && ops[3].ty == P_U8 && ops[4].tg == 4 && ops[4].ty == P_U8 &&
+                         ops[5].tg == 5 && ops[5].ty == P_U8 && ops[6].tg == 6 && ops[6].ty == P_U8;
+        std::vector<uint8_t> buf(chunk * rec);
+        piece.resize(chunk);
         for (uint64_t base = 0; base < nvert; base += chunk) {
             const uint64_t m = std::min(chunk, nvert - base);
             f.read(reinterpret_cast<char*>(buf.data()), (std::streamsize)(m * rec));
@@ -854,25 +876,35 @@ bool read_ply(const std::string& path, PlyResult& out, std::string& err) {
             const bool short_read = got_m != m;
             if (short_read) {   // read_*_endian_element fails on the first missing record (ply.rs:54-70)
                 out.data_error = path + ": truncated vertex data";
-                out.points.resize(base + got_m);
+                if (!sink) out.points.resize(base + got_m);
             }
-            for (uint64_t i = 0; i < got_m; i++) {
-                Point& pt = out.points[base + i];
-                pt.x = pt.y = pt.z = 0;
-                pt.rgba[0] = pt.rgba[1] = pt.rgba[2] = 0;
-                pt.rgba[3] = 255;   // point.rs:16-23
-                const uint8_t* q = buf.data() + i * rec;
-                for (auto& p : vprops) { apply(pt, p, q); q += psize(p.type); }
+            if (raw) {
+                if (!emit(reinterpret_cast<const Point*>(buf.data()), got_m, base)) return true;
+            } else {
+                for (uint64_t i = 0; i < got_m; i++) {
+                    Point& pt = piece[i];
+                    pt.x = pt.y = pt.z = 0;
+                    pt.rgba[0] = pt.rgba[1] = pt.rgba[2] = 0;
+                    pt.rgba[3] = 255;   // point.rs:16-23
+                    const uint8_t* q = buf.data() + i * rec;
+                    for (const Op& op : ops) apply(pt, op.tg, op.ty, q + op.off);
+                }
+                if (!emit(piece.data(), got_m, base)) return true;
             }
             if (short_read) break;
         }
-    } else {
+    } else {   // list properties: record by record
+        std::vector<int> tgs;
+        for (auto& p : vprops) tgs.push_back(target(p.name));
+        piece.resize(chunk);
+        uint64_t k = 0, base = 0;
         for (uint64_t i = 0; i < nvert; i++) {
-            Point& pt = out.points[i];
+            Point& pt = piece[k];
             pt.x = pt.y = pt.z = 0;
             pt.rgba[0] = pt.rgba[1] = pt.rgba[2] = 0;
             pt.rgba[3] = 255;
-            for (auto& p : vprops) {
+            for (size_t pi = 0; pi < vprops.size(); pi++) {
+                const Prop& p = vprops[pi];
                 uint8_t tmp[8];
                 if (p.list) {
                     f.read(reinterpret_cast<char*>(tmp), psize(p.count_type));
@@ -880,15 +912,22 @@ bool read_ply(const std::string& path, PlyResult& out, std::string& err) {
                     f.seekg((std::streamoff)(cnt * psize(p.type)), std::ios::cur);
                 } else {
                     f.read(reinterpret_cast<char*>(tmp), psize(p.type));
-                    apply(pt, p, tmp);
+                    apply(pt, tgs[pi], p.type, tmp);
                 }
                 if (!f) {
                     out.data_error = path + ": truncated vertex data";
-                    out.points.resize(i);
+                    if (!sink) out.points.resize(base + k);
+                    if (k) emit(piece.data(), k, base);
                     return true;
                 }
             }
+            if (++k == chunk) {
+                if (!emit(piece.data(), k, base)) return true;
+                base += k;
+                k = 0;
+            }
         }
+        if (k) emit(piece.data(), k, base);
     }
     return true;
 }

@@ -4,6 +4,7 @@
 //   PLY input      point-converter/src/converter/ply.rs:19-73 + point.rs:56-130
 #pragma once
 #include <stdint.h>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -85,7 +86,10 @@ struct PlyResult {
     std::string data_error;     // set when the vertex data ends early or is unreadable:
                                 // `points` then holds the records read before the error
 };
-bool read_ply(const std::string& path, PlyResult& out, std::string& err);
+// sink: when set, the points are handed over in pieces (file order) instead of
+// being collected in out.points; returning false stops the reader.
+using PointSink = std::function<bool(const Point*, uint64_t)>;
+bool read_ply(const std::string& path, PlyResult& out, std::string& err, const PointSink& sink = nullptr);
 
 // LAS reader (converter/las.rs:23-46 over las 0.8.4 [dep]): uncompressed LAS
 // 1.0-1.4, point formats 0-10.  x = (scale * X + offset) in f64 (las

@@ -35,7 +35,7 @@ EXPORTS = ["pcc_abi_version", "pcc_last_error", "pcc_options_default", "pcc_open
            "pcc_shard_histogram", "pcc_shard_route", "pcc_declare_files", "pcc_add_keyed_points_device",
            "pcc_set_keyed_points_device", "pcc_set_level_range", "pcc_set_root_spill_batches",
            "pcc_pending_cells", "pcc_export_pending", "pcc_shard_slab_histogram", "pcc_shard_route_slabs",
-           "pcc_write_cell_view",
+           "pcc_write_cell_view", "pcc_begin_file", "pcc_append_points", "pcc_end_file", "pcc_cancel_file",
            "pcc_set_summary", "pcc_write_cells", "pcc_write_metadata", "pcc_clear_input", "pcc_adopt_prior",
            "pcc_open_subtrees", "pcc_visit_cells"]
 
@@ -154,6 +154,10 @@ def lib():
         L.pcc_shard_route_slabs.argtypes = [vp, C.c_uint64, C.c_uint32, C.POINTER(ShardGrid), C.c_uint32, vp,
                                             C.c_uint32, vp, vp, C.POINTER(C.c_uint64), C.c_int]
         L.pcc_write_cell_view.argtypes = [C.c_char_p, vp]
+        L.pcc_begin_file.argtypes = [vp, C.c_uint64]
+        L.pcc_append_points.argtypes = [vp, vp, C.c_uint64]
+        L.pcc_end_file.argtypes = [vp, C.c_uint64]
+        L.pcc_cancel_file.argtypes = [vp]
         L.pcc_set_root_spill_batches.argtypes = [vp, vp, vp, C.c_uint64]
         L.pcc_pending_cells.argtypes = [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         L.pcc_export_pending.argtypes = [vp, vp, vp, vp, vp, vp]
@@ -201,6 +205,18 @@ class Converter:
         """One input file (host array of POINT_DTYPE)."""
         pts = np.ascontiguousarray(pts, dtype=POINT_DTYPE)
         _check(lib().pcc_add_points(self._h, pts.ctypes.data, len(pts)))
+
+    def add_file_pieces(self, pieces, keep: int | None = None):
+        """One file delivered in pieces (pcc_begin_file / pcc_append_points /
+        pcc_end_file): the concatenation of `pieces` (numpy POINT arrays), or its
+        first `keep` points."""
+        import numpy as _np
+        pieces = [_np.ascontiguousarray(p) for p in pieces]
+        total = sum(len(p) for p in pieces)
+        _check(lib().pcc_begin_file(self._h, total))
+        for p in pieces:
+            _check(lib().pcc_append_points(self._h, C.c_void_p(p.ctypes.data), len(p)))
+        _check(lib().pcc_end_file(self._h, total if keep is None else keep))
 
     def add_points_device(self, dev_ptr: int, n: int):
         _check(lib().pcc_add_points_device(self._h, C.c_void_p(dev_ptr), n))

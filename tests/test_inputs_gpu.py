@@ -17,7 +17,7 @@ import tempfile
 import numpy as np
 import pytest
 
-from gpu_util import compare_dirs  # noqa: E402
+from gpu_util import compare_dirs, gpu_digest  # noqa: E402
 from oracle_ctypes import POINT_DTYPE, Oracle, synth  # noqa: E402
 
 pytestmark = pytest.mark.gpu
@@ -265,3 +265,29 @@ def test_truncated_inputs_keep_complete_batches():
         _oracle_dir(ref, [pts[:20_000], pts[:0], las[:20_000], pts[40_000:]], empty_batches={1: 1})
         d, mg, mo = compare_dirs(out, ref, fast=False)
         assert d == [] and mg == mo
+
+
+def test_file_in_pieces_equals_one_call(tmp_path):
+    """pcc_begin_file / pcc_append_points / pcc_end_file (the pinned-ring
+    upload the CLI uses) == one pcc_add_points call per file; pieces larger
+    than one 4M-point staging buffer, a 1-point piece, keep < total (a reader
+    error keeps the complete batches) and a cancelled file (no batch)."""
+    import pcconv
+    a, b = synth(91, 0, 9_000_001), synth(92, 1, 123_457)
+    ref = pcconv.Converter(str(tmp_path / "ref"))
+    ref.add_points(a)
+    ref.add_points(b[:120_000])
+    ref.build()
+    dref = gpu_digest(ref)
+    ref.close()
+    c = pcconv.Converter(str(tmp_path / "pieces"))
+    c.add_file_pieces([a[:5_000_000], a[5_000_000:5_000_001], a[5_000_001:]])
+    lib = pcconv.lib()
+    import ctypes as C
+    assert lib.pcc_begin_file(c._h, 10) == 0
+    assert lib.pcc_append_points(c._h, C.c_void_p(b.ctypes.data), 5) == 0
+    assert lib.pcc_cancel_file(c._h) == 0
+    c.add_file_pieces([b[:60_000], b[60_000:]], keep=120_000)
+    c.build()
+    assert gpu_digest(c) == dref
+    c.close()
