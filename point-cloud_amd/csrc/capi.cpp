@@ -813,21 +813,33 @@ int pcc_convert_files(const char* out_dir, const char* const* paths, size_t npat
             }
             if (rc) { pcc_close(c); return rc; }
             if (!r.data_error.empty()) log_line("ERROR", "%s", r.data_error.c_str());
-        } else if (ext == "las" || ext == "laz") {   // converter/las.rs:14-46
+        } else if (ext == "las" || ext == "laz") {   // converter/las.rs:14-46, streamed like PLY
             LasResult r;
             std::string err;
-            if (!read_las(p, r, err)) {
+            bool open = false, logged = false;
+            uint64_t pushed = 0;
+            int src = 0;
+            const PointSink sink = [&](const Point* pts, uint64_t m) -> bool {
+                if (!logged) { log_line("INFO", "Converting %llu points", (unsigned long long)r.count); logged = true; }
+                if (!open) { if ((src = pcc_begin_file(c, r.count))) return false; open = true; }
+                if ((src = pcc_append_points(c, reinterpret_cast<const pcc_point*>(pts), m))) return false;
+                pushed += m;
+                return true;
+            };
+            const bool ok = read_las(p, r, err, sink);
+            if (!ok || src) {
+                if (open) pcc_cancel_file(c);
                 pcc_close(c);
-                return set_err(-EIO, err);   // the reference unwraps Reader::from_path (las.rs:16)
+                return src ? src : set_err(-EIO, err);   // the reference unwraps Reader::from_path (las.rs:16)
             }
             if (r.laz) {
                 log_line("ERROR", "LAZ-compressed point data is not supported by this build (%s)", p.c_str());
                 continue;
             }
-            log_line("INFO", "Converting %llu points", (unsigned long long)r.count);
-            const uint64_t keep = r.data_error.empty() ? r.points.size() : (r.points.size() / B) * B;
-            if (r.data_error.empty() || keep)
-                rc = pcc_add_points(c, reinterpret_cast<const pcc_point*>(r.points.data()), keep);
+            if (!logged) log_line("INFO", "Converting %llu points", (unsigned long long)r.count);
+            const uint64_t keep = r.data_error.empty() ? pushed : (pushed / B) * B;
+            if (open) rc = (r.data_error.empty() || keep) ? pcc_end_file(c, keep) : pcc_cancel_file(c);
+            else if (r.data_error.empty()) rc = pcc_add_points(c, nullptr, 0);   // no points: one empty batch
             if (rc) { pcc_close(c); return rc; }
             if (!r.data_error.empty()) log_line("ERROR", "%s", r.data_error.c_str());
         } else if (ext == "json") {   // converter/own.rs: another converted cloud as input

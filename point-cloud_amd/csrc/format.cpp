@@ -619,7 +619,7 @@ int prior_from_cells(const std::vector<CellFile>& cells, const Config& cfg, Prio
 }
 
 // ------------------------------------------------------------------ LAS
-bool read_las(const std::string& path, LasResult& out, std::string& err) {
+bool read_las(const std::string& path, LasResult& out, std::string& err, const PointSink& sink) {
     FILE* f = fopen(path.c_str(), "rb");
     if (!f) { err = "cannot open " + path; return false; }
     uint8_t h[375] = {0};
@@ -649,23 +649,25 @@ bool read_las(const std::string& path, LasResult& out, std::string& err) {
     const double ox = f64(155), oy = f64(163), oz = f64(171);
     const int co = kColorOff[fmt];
     if (fseek(f, (long)data_off, SEEK_SET) != 0) return bad("bad offset to point data");
-    out.points.resize(n);
+    if (!sink) out.points.resize(n);
     std::vector<uint8_t> buf;
-    const uint64_t chunk = 1 << 16;
+    const uint64_t chunk = 1 << 18;
     buf.resize(chunk * rec);
+    std::vector<Point> piece(sink ? chunk : 0);
     for (uint64_t base = 0; base < n; base += chunk) {
         uint64_t m = std::min<uint64_t>(chunk, n - base);
         const uint64_t got_m = fread(buf.data(), rec, m, f);
         if (got_m != m) {   // las Reader::read_n fails on the missing records (las.rs:23-46)
             out.data_error = path + ": truncated point data";
             m = got_m;
-            out.points.resize(base + m);
+            if (!sink) out.points.resize(base + m);
         }
+        Point* dst = sink ? piece.data() : out.points.data() + base;
         for (uint64_t i = 0; i < m; i++) {
             const uint8_t* r = buf.data() + i * rec;
             int32_t X, Y, Z;
             memcpy(&X, r, 4); memcpy(&Y, r + 4, 4); memcpy(&Z, r + 8, 4);
-            Point& p = out.points[base + i];
+            Point& p = dst[i];
             // las Transform::direct: scale * n + offset in f64 (no FMA), then `as f32`
             p.x = (float)((sx * (double)X) + ox);
             p.y = (float)((sy * (double)Y) + oy);
@@ -677,6 +679,7 @@ bool read_las(const std::string& path, LasResult& out, std::string& err) {
             p.rgba[2] = (uint8_t)c[2];
             p.rgba[3] = 255;
         }
+        if (sink && m && !sink(piece.data(), m)) break;
         if (!out.data_error.empty()) break;
     }
     fclose(f);

@@ -102,7 +102,7 @@ struct LasResult {
     bool laz = false;
     std::string data_error;   // truncated point data: `points` holds the records read before it
 };
-bool read_las(const std::string& path, LasResult& out, std::string& err);
+bool read_las(const std::string& path, LasResult& out, std::string& err, const PointSink& sink = nullptr);
 
 // Points of a converted cloud used as an input file (converter/own.rs:16-78):
 // h_0 .. h_{H-1}, every cell's grid points then its Some lists.  The reference
