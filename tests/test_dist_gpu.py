@@ -197,3 +197,51 @@ def test_sharded_threads_sparse_wide_cloud_coarse_grid(tmp_path):
     res = _run_threads(files, 3, out, cfg=cfg)
     assert sum(r.recv_points for r in res) == sum(len(f) for f in files)
     check_against_oracle(tmp_path, files, out, res[0].summary, cfg=cfg)
+
+
+def _gloo_hip_worker(rank, world, port, case, out, res_dir):
+    """One process per rank on the same GPU: gloo for the collectives (host
+    tensors), the product's HIP ops for the local work (the N > 1 bench path
+    with RCCL swapped for gloo, since RCCL refuses two ranks on one device)."""
+    import json
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.init()
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from pcconv.dist import TorchComm
+        if case == "gauss":
+            files, cfg = [synth(61, 2, 300_000)], SKEW_CFG
+        else:
+            files, cfg = make_input(case), None
+        pts, key0 = rank_slice(files, rank, world)
+        ops = HipShardOps(0, out_dir=out, config=cfg)
+        comm = TorchComm(torch.device("cpu"))
+        comm.max_msg_bytes = 1 << 20
+        r = shard_build(comm, ops, as_tensor(pts).to(DEV), key0, [len(f) for f in files], write=True)
+        ops.close()
+        with open(os.path.join(res_dir, f"rank{rank}.json"), "w") as f:
+            json.dump({"summary": r.summary, "recv": r.recv_points, "plan": r.plan}, f)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("case,world", [("files", 2), ("gauss", 3)])
+def test_gloo_processes_with_hip_ops_match_oracle(tmp_path, case, world):
+    import json
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    out, rd = str(tmp_path / "out"), str(tmp_path / "res")
+    os.makedirs(rd)
+    mp.spawn(_gloo_hip_worker, args=(world, port, case, out, rd), nprocs=world, join=True)
+    r = [json.load(open(os.path.join(rd, f"rank{i}.json"))) for i in range(world)]
+    files, cfg = ([synth(61, 2, 300_000)], SKEW_CFG) if case == "gauss" else (make_input(case), None)
+    assert all(x["summary"] == r[0]["summary"] for x in r)
+    assert sum(x["recv"] for x in r) == sum(len(f) for f in files)
+    if case == "gauss":
+        assert r[0]["plan"]["split_cells"] > 0
+    check_against_oracle(tmp_path, files, out, r[0]["summary"], cfg=cfg)
