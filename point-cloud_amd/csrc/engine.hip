@@ -1031,6 +1031,8 @@ struct SlabParams {
     int32_t tx, ty;
     int32_t check_gchild;
     uint32_t kf_lo, kf_n;         // merge mode: keys in [kf_lo, kf_lo + kf_n) are forced emissions (engine.h PriorState)
+    const float4* inj;            // merge mode: seeds of levels >= 1 (a small slab reads its own in place)
+    const uint32_t* inj_keys;
     unsigned long long* stamps;   // diagnostic build only
 };
 
@@ -1109,10 +1111,38 @@ __device__ __forceinline__ void bst4(__amdgpu_buffer_rsrc_t r, uint32_t off, u32
     __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 0);
 }
 
+// A dense slab's arrivals.  Merge mode (SEEDS): arrivals 0 .. ns-1 are the
+// slab's seeds, read in place from the seed array (the room reserved for them
+// in front of the emissions is never written); every load is issued to both
+// sources with the other one out of range (a buffer load out of range returns
+// 0), so no lane branches.  Offsets are byte offsets (16 j / 4 j) or ~0u.
+template <bool SEEDS>
+struct ArrSrc {
+    __amdgpu_buffer_rsrc_t rP, rK, rS, rT;
+    uint32_t ns16;   // 16 * ns
+    __device__ __forceinline__ u32x4 p(uint32_t o) const {
+        if constexpr (!SEEDS) {
+            return bld4(rP, o);
+        } else {
+            const bool sd = o < ns16;
+            const u32x4 a = bld4(rS, sd ? o : 0xFFFFFFFFu), b = bld4(rP, sd ? 0xFFFFFFFFu : o);
+            return u32x4{a.x | b.x, a.y | b.y, a.z | b.z, a.w | b.w};
+        }
+    }
+    __device__ __forceinline__ uint32_t k(uint32_t o) const {
+        if constexpr (!SEEDS) {
+            return bld(rK, o);
+        } else {
+            const bool sd = o < ns16 / 4;
+            return bld(rT, sd ? o : 0xFFFFFFFFu) | bld(rK, sd ? 0xFFFFFFFFu : o);
+        }
+    }
+};
+
 // Grid points of a dense slab: the slot table's occupants, compacted into the
 // slab's grid region (cell.rs:158-160: order inside a cell file is free).
-template <class L>
-__device__ __forceinline__ void dense_grid_points(const SlabParams& P, L& S, uint32_t* bm, __amdgpu_buffer_rsrc_t rP,
+template <class L, class SRC>
+__device__ __forceinline__ void dense_grid_points(const SlabParams& P, L& S, uint32_t* bm, const SRC& rP,
                                                   uint32_t s, uint32_t n, uint32_t jmask, uint32_t tid, uint32_t lane) {
     constexpr int BS = L::BS, TAB = L::TAB;
     // ---- grid points: the table's occupants, compacted into the slab's grid
@@ -1139,7 +1169,7 @@ __device__ __forceinline__ void dense_grid_points(const SlabParams& P, L& S, uin
         for (uint32_t j0 = 0; j0 < n; j0 += V * BS) {
             u32x4 pv[V];
 #pragma unroll
-            for (int u = 0; u < V; u++) pv[u] = bld4(rP, (j0 + u * BS + tid) * 16);   // past n: zero (buffer range)
+            for (int u = 0; u < V; u++) pv[u] = rP.p((j0 + u * BS + tid) * 16);   // past n: zero (buffer range)
             uint64_t m[V];
             uint32_t tot = 0;
 #pragma unroll
@@ -1184,7 +1214,7 @@ __device__ __forceinline__ void dense_grid_points(const SlabParams& P, L& S, uin
         }
         u32x4 pv[U];
 #pragma unroll
-        for (int u = 0; u < U; u++) pv[u] = bld4(rP, src[u]);
+        for (int u = 0; u < U; u++) pv[u] = rP.p(src[u]);
 #pragma unroll
         for (int u = 0; u < U; u++) bst4(rG, wpos[u], pv[u]);
     }
@@ -1210,6 +1240,7 @@ __device__ __forceinline__ void dense_grid_points(const SlabParams& P, L& S, uin
 // chunk the table's occupants are the slab's grid points (cell.rs:158-160:
 // order inside a cell file is free).  Grandchild capacities count every
 // emission's (child, grandchild) slab when its rank is taken.
+template <bool SEEDS>
 __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
     using L = DenseLds;
     constexpr int BS = L::BS, TAB = L::TAB, CLAIM = L::CLAIM, NW = L::NW;
@@ -1235,7 +1266,19 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
     // buffer descriptors: this slab's arrivals and the contiguous region of its
     // 24 child slabs in the next arena (out-of-range offsets drop a store)
     const uint64_t nb = (uint64_t)n * 4;
-    const __amdgpu_buffer_rsrc_t rP = srd(P.in.p + off, nb * 4), rK = srd(P.in.k + off, nb);
+    ArrSrc<SEEDS> A_;
+    A_.rP = srd(P.in.p + off, nb * 4);
+    A_.rK = srd(P.in.k + off, nb);
+    if constexpr (SEEDS) {
+        A_.rS = srd(P.inj + D.pad0, (uint64_t)D.pad1 * 16);
+        A_.rT = srd(P.inj_keys + D.pad0, (uint64_t)D.pad1 * 4);
+        A_.ns16 = D.pad1 * 16;
+    } else {
+        A_.rS = A_.rP;
+        A_.rT = A_.rK;
+        A_.ns16 = 0;
+    }
+    const ArrSrc<SEEDS>& rP = A_;
     const uint32_t dbase = D.dbase;
     const uint64_t db = (uint64_t)D.dlen * 4;
     const __amdgpu_buffer_rsrc_t oP = srd(P.nx.p + dbase, db * 4), oK = srd(P.nx.k + dbase, db);
@@ -1262,8 +1305,8 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
     for (int q = 0; q < 4; q++) {
         const uint32_t jo = min((uint32_t)(q * BS) + tid, nm1);
         if (q < 2) {
-            pre[q].p = bld4(rP, jo * 16);
-            pre[q].k = bld(rK, jo * 4);
+            pre[q].p = rP.p(jo * 16);
+            pre[q].k = rP.k(jo * 4);
         } else {
             pre[q].p = u32x4{0u, 0u, 0u, 0u};
             pre[q].k = 0;
@@ -1293,8 +1336,8 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
         const bool forced = valid && mine.k - P.kf_lo < P.kf_n;
         {   // prefetch chunk i+2 (clamped)
             const uint32_t jo = min(j + 2 * BS, nm1);
-            pf.p = bld4(rP, jo * 16);
-            pf.k = bld(rK, jo * 4);
+            pf.p = rP.p(jo * 16);
+            pf.k = rP.k(jo * 4);
         }
         // the claim entries of chunk i-1 (other parity) are dead since the last barrier
         if (prv.hc >= 0) S.claim[par ^ 1][prv.hc] = kEmpty32;
@@ -1454,7 +1497,7 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
         STAMP_COUNT(9, 1);
         // gather outside the divergent branches (a load into registers that
         // another branch writes would force a full vmcnt drain); stored next step
-        cur.gp = bld4(rP, (PCC_ABL & 4) ? 0xFFFFFFFFu : gsrc);
+        cur.gp = rP.p((PCC_ABL & 4) ? 0xFFFFFFFFu : gsrc);
         cur.em = em; cur.d = emd; cur.g = emg; cur.hc = hc;
         lds_barrier();
         STAMP(5);
@@ -1547,20 +1590,32 @@ __device__ __forceinline__ SmallDesc slab_desc(uint32_t s, const uint32_t* slab_
 
 __global__ void k_dense_desc(const uint32_t* list, uint32_t nlist, const uint32_t* slab_cell, const int32_t* slab_layer,
                              const uint32_t* slab_off, const uint32_t* slab_n, const int32_t* cell_idx,
-                             const uint32_t* cell_sb, const uint32_t* dest_off, const uint32_t* dcap, SmallDesc* out) {
+                             const uint32_t* cell_sb, const uint32_t* dest_off, const uint32_t* dcap, SmallDesc* out,
+                             const uint32_t* slab_prior, const PriorSlabRec* prec) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < nlist) out[i] = slab_desc(list[i], slab_cell, slab_layer, slab_off, slab_n, cell_idx, cell_sb, dest_off, dcap);
+    if (i >= nlist) return;
+    SmallDesc D = slab_desc(list[i], slab_cell, slab_layer, slab_off, slab_n, cell_idx, cell_sb, dest_off, dcap);
+    if (slab_prior) {   // merge, level >= 1: seeds read in place (pad0 = offset in the seed array, pad1 = count)
+        const uint32_t pr = slab_prior[D.s];
+        if (pr != kNoPriorSlab) { D.pad0 = prec[pr].seed_off; D.pad1 = prec[pr].nseed; }
+    }
+    out[i] = D;
 }
 
 __global__ void k_small_desc(const uint32_t* list, uint32_t nlist, const uint32_t* slab_cell, const int32_t* slab_layer,
                              const uint32_t* slab_off, const uint32_t* slab_n, const int32_t* cell_idx,
                              const uint32_t* cell_sb, const uint32_t* dest_off, const uint32_t* dcap, SmallDesc* wave_out,
-                             SmallDesc* block_out, uint32_t* counts) {
+                             SmallDesc* block_out, uint32_t* counts, const uint32_t* slab_prior,
+                             const PriorSlabRec* prec) {
     __shared__ uint32_t wc[4][4], bpre[4][4];
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     const bool in = i < nlist;
-    const SmallDesc D = slab_desc(in ? list[i] : list[0], slab_cell, slab_layer, slab_off, slab_n, cell_idx, cell_sb,
-                                  dest_off, dcap);
+    SmallDesc D = slab_desc(in ? list[i] : list[0], slab_cell, slab_layer, slab_off, slab_n, cell_idx, cell_sb,
+                            dest_off, dcap);
+    if (slab_prior) {   // merge, level >= 1: the slab's seeds stay in the seed array (pad0 = offset, pad1 = count)
+        const uint32_t pr = slab_prior[D.s];
+        if (pr != kNoPriorSlab) { D.pad0 = prec[pr].seed_off; D.pad1 = prec[pr].nseed; }
+    }
     // size class: 0..2 one wave (< 128, < 256, < 512 arrivals), 3 block; the
     // wave classes share wave_out, class c from offset c * nlist.  One global
     // atomic per block and class.
@@ -1600,12 +1655,26 @@ __device__ __forceinline__ void small_prefetch(const SlabParams& P, uint32_t li,
     D = P.sdesc[li];
     const uint64_t nb = (uint64_t)D.n * 4;
     const __amdgpu_buffer_rsrc_t rP = srd(P.in.p + D.off, nb * 4), rK = srd(P.in.k + D.off, nb);
+    if (D.pad1) {   // merge: arrivals 0 .. pad1-1 are seeds, read from the seed array (no copy into the room)
+        const uint32_t ns = D.pad1;
+        const __amdgpu_buffer_rsrc_t rS = srd(P.inj + D.pad0, (uint64_t)ns * 16),
+                                     rT = srd(P.inj_keys + D.pad0, (uint64_t)ns * 4);
 #pragma unroll
-    for (int c = 0; c < kSmallCh; c++) {
-        const uint32_t j = c * kSmallBS + tid;
-        const bool v = j < D.n;
-        R.pp[c] = bld4(rP, v ? j * 16 : 0xFFFFFFFFu);
-        R.pk[c] = bld(rK, v ? j * 4 : 0xFFFFFFFFu);
+        for (int c = 0; c < kSmallCh; c++) {
+            const uint32_t j = c * kSmallBS + tid;
+            const bool v = j < D.n, sd = j < ns;
+            const u32x4 a = bld4(rS, sd ? j * 16 : 0xFFFFFFFFu), b = bld4(rP, (v && !sd) ? j * 16 : 0xFFFFFFFFu);
+            R.pp[c] = u32x4{a.x | b.x, a.y | b.y, a.z | b.z, a.w | b.w};   // out-of-range loads return 0
+            R.pk[c] = bld(rT, sd ? j * 4 : 0xFFFFFFFFu) | bld(rK, (v && !sd) ? j * 4 : 0xFFFFFFFFu);
+        }
+    } else {
+#pragma unroll
+        for (int c = 0; c < kSmallCh; c++) {
+            const uint32_t j = c * kSmallBS + tid;
+            const bool v = j < D.n;
+            R.pp[c] = bld4(rP, v ? j * 16 : 0xFFFFFFFFu);
+            R.pk[c] = bld(rK, v ? j * 4 : 0xFFFFFFFFu);
+        }
     }
     const __amdgpu_buffer_rsrc_t rD = srd(P.dest_off + (uint64_t)D.s * kDests, kDests * 4);
     const __amdgpu_buffer_rsrc_t rC = srd(P.dcap + (uint64_t)D.s * kDests, kDests * 4);
@@ -1917,12 +1986,26 @@ __global__ __launch_bounds__(64) void k_slab_wave(SlabParams P) {
         const __amdgpu_buffer_rsrc_t oP = srd(P.nx.p + dbase, db * 4), oK = srd(P.nx.k + dbase, db);
         u32x4 pp[CH];
         uint32_t pk[CH];
+        if (D.pad1) {   // merge: the seeds (arrivals 0 .. pad1-1) in place in the seed array
+            const uint32_t ns = D.pad1;
+            const __amdgpu_buffer_rsrc_t rS = srd(P.inj + D.pad0, (uint64_t)ns * 16),
+                                         rT = srd(P.inj_keys + D.pad0, (uint64_t)ns * 4);
 #pragma unroll
-        for (int c = 0; c < CH; c++) {
-            const uint32_t j = c * 64 + lane;
-            const bool v = j < n;
-            pp[c] = bld4(rP, v ? j * 16 : 0xFFFFFFFFu);
-            pk[c] = bld(rK, v ? j * 4 : 0xFFFFFFFFu);
+            for (int c = 0; c < CH; c++) {
+                const uint32_t j = c * 64 + lane;
+                const bool v = j < n, sd = j < ns;
+                const u32x4 a = bld4(rS, sd ? j * 16 : 0xFFFFFFFFu), b = bld4(rP, (v && !sd) ? j * 16 : 0xFFFFFFFFu);
+                pp[c] = u32x4{a.x | b.x, a.y | b.y, a.z | b.z, a.w | b.w};
+                pk[c] = bld(rT, sd ? j * 4 : 0xFFFFFFFFu) | bld(rK, (v && !sd) ? j * 4 : 0xFFFFFFFFu);
+            }
+        } else {
+#pragma unroll
+            for (int c = 0; c < CH; c++) {
+                const uint32_t j = c * 64 + lane;
+                const bool v = j < n;
+                pp[c] = bld4(rP, v ? j * 16 : 0xFFFFFFFFu);
+                pk[c] = bld(rK, v ? j * 4 : 0xFFFFFFFFu);
+            }
         }
         for (uint32_t i = lane; i < cap; i += 64) { W.tab[i] = kEmpty64; W.tkey[i] = kEmpty32; }
         for (uint32_t i = lane; i < kDests * kDests / 2; i += 64) W.gcnt[i] = 0;
@@ -2544,10 +2627,11 @@ __global__ void k_add_room(uint32_t* dest_off, const uint32_t* room, uint64_t n)
 // merge: copy each new slab's seeds (points and keys) in front of its emissions
 __global__ __launch_bounds__(256) void k_inject_seeds(const uint32_t* slab_prior, const uint32_t* slab_off, uint32_t nslabs,
                                                       const PriorSlabRec* prec, const float4* __restrict__ inj,
-                                                      const uint32_t* __restrict__ inj_keys, Arena A) {
+                                                      const uint32_t* __restrict__ inj_keys, Arena A,
+                                                      const uint32_t* __restrict__ slab_n) {
     for (uint32_t s = blockIdx.x; s < nslabs; s += gridDim.x) {
         const uint32_t pr = slab_prior[s];
-        if (pr == kNoPriorSlab) continue;
+        if (pr == kNoPriorSlab || slab_n[s] < kSmallMax) continue;   // small slabs read their seeds in place
         const uint32_t so = prec[pr].seed_off, n = prec[pr].nseed, o = slab_off[s];
         for (uint32_t j = threadIdx.x; j < n; j += 256) {
             A.p[(uint64_t)o + j] = inj[(uint64_t)so + j];
@@ -3332,6 +3416,8 @@ int Engine::run_level(uint32_t li) {
         SP.kf_n = (uint32_t)(nseeds_ - forced_lo_[h]);
     }
     SP.ctr = dev_->ctr;
+    SP.inj = reinterpret_cast<const float4*>(d_inj_);
+    SP.inj_keys = d_inj_keys_;
     SP.cs = cs;
     {
         LevelGeo& G = SP.G;
@@ -3360,6 +3446,9 @@ int Engine::run_level(uint32_t li) {
     unsigned long long* stamps = static_cast<unsigned long long*>(dev_->get(2 * 16 * 8));
     HIP_CHECK(hipMemsetAsync(stamps, 0, 2 * 16 * 8, stream_));
 #endif
+    // merge, levels >= 1: the slab kernels read this level's seeds in place from
+    // the seed array (the room in front of the emissions stays unwritten)
+    const bool seeds_in_place = prior_ && h >= 1 && L->slab_prior && h < pdev_.size();
     const bool verbose = getenv("PCC_VERBOSE") != nullptr;
     const auto tv0 = std::chrono::steady_clock::now();
     if (verbose) {
@@ -3373,13 +3462,16 @@ int Engine::run_level(uint32_t li) {
         k_dense_desc<<<grid_for(L->nbig, 256, 1u << 30), 256, 0, stream_>>>(L->big_list, L->nbig, L->slab_cell,
                                                                            L->slab_layer, L->slab_off, L->slab_n,
                                                                            L->cell_idx, L->cell_sb, L->dest_off,
-                                                                           L->dcap, dd);
+                                                                           L->dcap, dd,
+                                                                           seeds_in_place ? L->slab_prior : nullptr,
+                                                                           seeds_in_place ? pdev_[h].slabs : nullptr);
         SP.ddesc = dd;
 #ifdef PCC_STAMPS
         SP.stamps = stamps;
 #endif
         ev_begin(ST_DENSE);
-        k_slab<<<L->nbig, kDenseBS, 0, stream_>>>(SP);
+        if (seeds_in_place) k_slab<true><<<L->nbig, kDenseBS, 0, stream_>>>(SP);
+        else k_slab<false><<<L->nbig, kDenseBS, 0, stream_>>>(SP);
         ev_end(ST_DENSE);
         if (verbose) {
             HIP_CHECK(hipStreamSynchronize(stream_));
@@ -3399,7 +3491,8 @@ int Engine::run_level(uint32_t li) {
         HIP_CHECK(hipMemsetAsync(cnt, 0, 16, stream_));
         k_small_desc<<<grid_for(L->nsmall, 256, 1u << 30), 256, 0, stream_>>>(
             L->small_list, L->nsmall, L->slab_cell, L->slab_layer, L->slab_off, L->slab_n, L->cell_idx, L->cell_sb,
-            L->dest_off, L->dcap, wd, bd, cnt);
+            L->dest_off, L->dcap, wd, bd, cnt, seeds_in_place ? L->slab_prior : nullptr,
+            seeds_in_place ? pdev_[h].slabs : nullptr);
         uint32_t hcnt[4];
         HIP_CHECK(hipMemcpyAsync(hcnt, cnt, 16, hipMemcpyDeviceToHost, stream_));
         HIP_CHECK(hipStreamSynchronize(stream_));
@@ -3545,10 +3638,10 @@ int Engine::run_level(uint32_t li) {
         ev_begin(ST_NEXT);
         k_next_emit<<<nb, 256, 0, stream_>>>(Q);
         k_set_u32<<<1, 1, 0, stream_>>>(N->cell_slab0 + N->ncells, N->nslabs);
-        if (inject && N->nslabs)   // the touched cells' seeds of level h+1, in front of their emissions
+        if (inject && N->nslabs && getenv("PCC_COPY_SEEDS"))   // diagnostic: copy the seeds into their room
             k_inject_seeds<<<std::min<uint32_t>(N->nslabs, 65536), 256, 0, stream_>>>(
                 N->slab_prior, N->slab_off, N->nslabs, pdev_[h + 1].slabs, reinterpret_cast<const float4*>(d_inj_),
-                d_inj_keys_, dev_->ar[N->arena]);
+                d_inj_keys_, dev_->ar[N->arena], N->slab_n);
         ev_end(ST_NEXT);
         HIP_CHECK(hipGetLastError());
         HIP_CHECK(hipMemcpyAsync(&hc, dev_->ctr, sizeof hc, hipMemcpyDeviceToHost, stream_));
