@@ -910,6 +910,352 @@ __global__ __launch_bounds__(kL0BS) void k_l0_down(const Point* __restrict__ in,
     }
 }
 
+// ---- level-0 binning with one upsweep (at most 8 level-0 cells: the dense-id
+// bits above the 6 low layer bits fit one 5-bit pass).  Pass 1 (k_l0_down6g)
+// runs kL0Groups persistent blocks, block g over a contiguous group of tiles,
+// and counts every point's (low 6 bits d6, high bits d5) pair in LDS.  Its
+// output is ordered by (d6, tile), so the points of group g with low bits d6
+// are one contiguous segment, and those counts give pass 2 the exact output
+// offset of every (segment, d5) run: no second upsweep.  Pass 2 (k_l0_down5g)
+// walks units of consecutive segments of one d6 bucket with running offsets and
+// counts the level-0 capacities (arrivals per child slab) on the way, which
+// replaces the level-1 histogram pass.
+constexpr uint32_t kL0Groups = 2048;
+struct L0Unit { uint32_t d6, g0, g1, pad; };
+
+// Per-tile wave counts, digit-major: cnt[d][r * kL0W + q] = lanes of wave q in
+// row r with digit d (<= 64), pre[d][..] = their exclusive prefix in key order.
+constexpr int kL0RW = kL0IPT * kL0W;   // 48 (row, wave) pairs per tile
+static_assert(kL0RW % 16 == 0, "16-byte rows");
+// Wave 0 of a tile: lane t < R reads digit t's 48 counts as 16-byte words,
+// writes their prefixes and clears them for the next tile, then the tile's digit
+// bases by a wave scan; returns the digit's total.
+template <int R>
+__device__ __forceinline__ uint32_t l0_tile_prefix(uint8_t (*cnt)[kL0RW], uint16_t (*pre)[kL0RW], uint32_t lane,
+                                                   uint32_t& excl) {
+    uint32_t acc = 0;
+    if (lane < (uint32_t)R) {
+        uint2* c2 = reinterpret_cast<uint2*>(cnt[lane]);
+        uint4* p4 = reinterpret_cast<uint4*>(pre[lane]);
+#pragma unroll 1
+        for (int c = 0; c < kL0RW / 8; c++) {   // 8 counts per step: one 8-byte read, one 16-byte write
+            const uint2 wv = c2[c];
+            c2[c] = make_uint2(0u, 0u);
+            uint32_t o[4];
+#pragma unroll
+            for (int k = 0; k < 2; k++) {
+                const uint32_t wd = k ? wv.y : wv.x;
+                const uint32_t b0 = wd & 0xFFu, b1 = (wd >> 8) & 0xFFu, b2 = (wd >> 16) & 0xFFu, b3 = wd >> 24;
+                o[2 * k] = acc | ((acc + b0) << 16);
+                acc += b0 + b1;
+                o[2 * k + 1] = acc | ((acc + b2) << 16);
+                acc += b2 + b3;
+            }
+            p4[c] = make_uint4(o[0], o[1], o[2], o[3]);
+        }
+    }
+    uint32_t x = acc;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= (uint32_t)d) x += y;
+    }
+    excl = x - acc;
+    return acc;
+}
+
+// Stores shaped like one tile's output stores (kL0IPT x (16 B + 4 B)) into a
+// scratch area: issued once before a tile loop so the loop is entered with the
+// pending memory ops of its back-edge (the compiler's waits at the loop header
+// then never cover the previous tile's stores).
+__device__ __forceinline__ void l0_dummy_stores(const Arena& dummy, const float4* v) {
+    const uint32_t slot = (blockIdx.x % 256) * kL0BS + threadIdx.x;
+#pragma unroll
+    for (int r = 0; r < kL0IPT; r++) {
+        dummy.p[slot * kL0IPT + r] = v[r];
+        dummy.k[slot * kL0IPT + r] = 0u;
+    }
+}
+
+// Pass 1.  Per tile: stable LDS partition on the low 6 layer bits, the (d6, d5)
+// pair counted per group; the next tile's loads are issued before this tile's
+// stores and only LDS barriers are used, so no wait ever covers a store.
+// KEYS: global keys from `keys` (sharded input), staged in LDS beside the
+// points (then R5 <= 16 keeps the LDS under half a CU); else key = index.
+template <int R5, bool KEYS>
+__global__ __launch_bounds__(kL0BS, 8) void k_l0_down6g(const Point* __restrict__ in, const uint32_t* __restrict__ keys,
+                                                        Arena O, uint64_t n, L0Params P,
+                                                        const uint32_t* __restrict__ offs, uint32_t ntiles, uint32_t tpg,
+                                                        uint32_t ngroups, uint32_t* __restrict__ gcnt, Arena dummy,
+                                                        Counters* ctr) {
+    constexpr int R = 64;
+    using KT = typename std::conditional<KEYS, uint32_t, uint16_t>::type;
+    __shared__ float4 sp[kL0Tile];
+    __shared__ KT sk[kL0Tile];
+    __shared__ uint8_t sd[kL0Tile];
+    __shared__ alignas(16) uint8_t wcnt[R][kL0RW];
+    __shared__ alignas(16) uint16_t wpre[R][kL0RW];
+    __shared__ uint32_t dbase[R], gofs[R];
+    __shared__ uint32_t h[R * R5];
+    const uint32_t tid = threadIdx.x, w = tid / 64, lane = tid & 63, g = blockIdx.x;
+    const float4* p4 = reinterpret_cast<const float4*>(in);
+    for (int i = tid; i < R * R5; i += kL0BS) h[i] = 0;
+    for (int i = tid; i < kL0RW * R / 4; i += kL0BS) reinterpret_cast<uint32_t*>(&wcnt[0][0])[i] = 0;
+    const uint64_t lt = lanemask_lt();
+    uint32_t err = 0;
+    const uint32_t t0 = g * tpg, t1 = min(t0 + tpg, ntiles);
+    float4 v[kL0IPT];
+    uint32_t kk[kL0IPT];
+    // wave 0, lane d: output position of digit d for the current tile (the
+    // group's tiles are consecutive: the upsweep's scanned count of the first
+    // tile, then + each tile's total)
+    uint32_t goffr = w == 0 ? offs[(uint64_t)lane * ntiles + t0] : 0u;
+    gofs[lane] = goffr;   // (an LDS write: the load is complete before the loop)
+    // every load and store below is issued unconditionally (indices clamped to
+    // the tile), so the number of memory ops per tile is static and the waits
+    // for the prefetched tile never cover this tile's stores
+    auto load_tile = [&](uint32_t tile) {
+        const uint64_t base = (uint64_t)tile * kL0Tile;
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int r = 0; r < kL0IPT; r++) {
+            const uint64_t i = min(base + (uint64_t)r * kL0BS + tid, n - 1);
+            v[r] = p4[i];
+            if constexpr (KEYS) kk[r] = keys[i];
+        }
+        asm volatile("" ::: "memory");   // keep the loads ahead of the tile's stores
+    };
+    load_tile(t0);
+    l0_dummy_stores(dummy, v);   // enter the loop with the back-edge's pending ops
+    for (uint32_t tile = t0; tile < t1; tile++) {
+        const uint64_t base = (uint64_t)tile * kL0Tile;
+        lds_barrier();   // the last tile's stores have read the staging arrays
+        uint32_t dgp = 0, rwp = 0;
+#pragma unroll
+        for (int r = 0; r < kL0IPT; r++) {
+            const uint64_t i = base + (uint64_t)r * kL0BS + tid;
+            const bool valid = i < n;
+            uint32_t d6 = 0;
+            if (valid) {
+                int64_t d = l0_dense<0>(P, v[r].x, v[r].y, v[r].z);
+                if (d < 0) { err = ERR_L0_RANGE; d = 0; }
+                d6 = (uint32_t)d & (R - 1);
+                atomicAdd(&h[d6 * R5 + (((uint32_t)d >> 6) & (R5 - 1))], 1u);
+            }
+            const uint64_t same = wave_peers<6>(d6, valid);
+            const uint32_t rw = (uint32_t)__popcll(same & lt);
+            if (valid && rw == 0) wcnt[d6][r * kL0W + w] = (uint8_t)__popcll(same);
+            dgp |= d6 << (8 * r);
+            rwp |= rw << (8 * r);
+        }
+        lds_barrier();
+        if (w == 0) {
+            uint32_t ex;
+            const uint32_t tot = l0_tile_prefix<R>(wcnt, wpre, lane, ex);
+            dbase[lane] = ex;
+            gofs[lane] = goffr - ex;
+            goffr += tot;
+        }
+        lds_barrier();
+#pragma unroll
+        for (int r = 0; r < kL0IPT; r++) {
+            const uint64_t i = base + (uint64_t)r * kL0BS + tid;
+            if (i < n) {
+                const uint32_t d6 = (dgp >> (8 * r)) & 0xFFu;
+                const uint32_t q = dbase[d6] + wpre[d6][r * kL0W + w] + ((rwp >> (8 * r)) & 0xFFu);
+                sp[q] = v[r];
+                if constexpr (KEYS) sk[q] = kk[r];
+                else sk[q] = (uint16_t)(r * kL0BS + tid);
+                sd[q] = (uint8_t)d6;
+            }
+        }
+        load_tile(min(tile + 1, t1 - 1));   // the last tile loads itself again: no branch
+        lds_barrier();
+        const uint32_t tn = (uint32_t)((n - base) < (uint64_t)kL0Tile ? (n - base) : (uint64_t)kL0Tile);
+#pragma unroll
+        for (int r = 0; r < kL0IPT; r++) {   // past tn: a duplicate of the last store
+            const uint32_t j = min((uint32_t)r * kL0BS + tid, tn - 1);
+            const uint32_t dst = gofs[sd[j]] + j;
+            O.p[dst] = sp[j];
+            if constexpr (KEYS) O.k[dst] = sk[j];
+            else O.k[dst] = (uint32_t)(base + sk[j]);
+        }
+    }
+    lds_barrier();
+    for (int i = tid; i < R * R5; i += kL0BS)
+        gcnt[((uint64_t)(i / R5) * ngroups + g) * R5 + (i % R5)] = h[i];
+    if (err) set_err(ctr, err);
+}
+
+// start of segment (d6, g) of the pass-1 output, g = 0..ngroups (the end)
+__global__ void k_l0_gstarts(const uint32_t* __restrict__ offs, uint32_t ntiles, uint32_t tpg, uint32_t ngroups,
+                             uint64_t n, uint32_t* __restrict__ starts) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= 64 * (ngroups + 1)) return;
+    const uint32_t d6 = i / (ngroups + 1), g = i % (ngroups + 1);
+    const uint64_t idx = (uint64_t)d6 * ntiles + min(g * tpg, ntiles);
+    starts[i] = idx < 64ull * ntiles ? offs[idx] : (uint32_t)n;
+}
+
+// per (d6, d5): exclusive prefix of the group counts (in place) and the dense
+// histogram bin (d5 << 6 | d6).  One block per d6, thread = (chunk, d5).
+template <int R5>
+__global__ __launch_bounds__(1024) void k_l0_gprefix(uint32_t* __restrict__ gcnt, uint32_t ngroups, uint32_t D,
+                                                     uint32_t* __restrict__ hist, Counters* ctr) {
+    constexpr int NC = 1024 / R5;
+    __shared__ uint32_t part[NC][R5];
+    const uint32_t d6 = blockIdx.x, d5 = threadIdx.x % R5, c = threadIdx.x / R5;
+    const uint32_t gpc = (ngroups + NC - 1) / NC, g0 = min(c * gpc, ngroups), g1 = min(g0 + gpc, ngroups);
+    uint32_t* row = gcnt + (uint64_t)d6 * ngroups * R5 + d5;
+    uint32_t acc = 0;
+    for (uint32_t g = g0; g < g1; g++) acc += row[(uint64_t)g * R5];
+    part[c][d5] = acc;
+    __syncthreads();
+    if (c == 0) {
+        uint32_t a = 0;
+        for (int q = 0; q < NC; q++) { const uint32_t v = part[q][d5]; part[q][d5] = a; a += v; }
+        const uint32_t d0 = (d5 << 6) | d6;
+        if (d0 < D) hist[d0] = a;
+        else if (a) set_err(ctr, ERR_L0_RANGE);
+    }
+    __syncthreads();
+    acc = part[c][d5];
+    for (uint32_t g = g0; g < g1; g++) {
+        const uint32_t v = row[(uint64_t)g * R5];
+        row[(uint64_t)g * R5] = acc;
+        acc += v;
+    }
+}
+
+// Level-0 dense id from the level-1 quotients (exact halving, see l1_dense) and
+// the point's child slab among the slab's 24 (octant * 3 + layer select, as
+// k_l0_dcap_from1 numbers them); -1 outside the grid.
+__device__ __forceinline__ int64_t l0_dense_dest(const L0Params& P, float x, float y, float z, uint32_t& dest) {
+    const int32_t ix1 = cell_index1(x, P.csc), iy1 = cell_index1(y, P.csc), iz1 = cell_index1(z, P.csc);
+    const int32_t u1 = sat_i32(z / P.crc);
+    const int32_t iz0 = iz1 >> 1, t0 = u1 / 2;
+    const int32_t gx0 = (ix1 >> 1) - P.lo[0], gy0 = (iy1 >> 1) - P.lo[1], gz0 = iz0 - P.lo[2];
+    const int64_t ll0 = (int64_t)t0 - ((int64_t)P.dim2 * iz0 - 2);
+    const int64_t ll1 = (int64_t)u1 - ((int64_t)P.dim2 * iz1 - 2);
+    dest = (uint32_t)(((ix1 & 1) | ((iy1 & 1) << 1) | ((iz1 & 1) << 2)) * 3 + (u1 - (2 * t0 - 1)));
+    const bool ok = gx0 >= 0 && gy0 >= 0 && gz0 >= 0 && gx0 < P.g[0] && gy0 < P.g[1] && gz0 < P.g[2] && ll0 >= 0 &&
+                    ll0 < P.nl && ll1 >= 0 && ll1 < (int64_t)kL0Layers;
+    return ok ? (((int64_t)gz0 * P.g[1] + gy0) * P.g[0] + gx0) * kL0Layers + ll0 : -1;
+}
+
+// Pass 2 over one unit (consecutive segments of one d6 bucket), running
+// offsets per d5 kept in wave-0 registers; the same pipelining as pass 1.
+template <int R5>
+__global__ __launch_bounds__(kL0BS, 8) void k_l0_down5g(Arena S, Arena O, L0Params P, const L0Unit* __restrict__ units,
+                                                        const uint32_t* __restrict__ starts, uint32_t ngroups,
+                                                        const uint32_t* __restrict__ gpre,
+                                                        const uint32_t* __restrict__ cnt_scan,
+                                                        const uint32_t* __restrict__ sid, uint32_t D,
+                                                        uint32_t* __restrict__ dcap, Arena dummy, Counters* ctr) {
+    constexpr int R = R5, RB = R5 == 32 ? 5 : R5 == 16 ? 4 : R5 == 8 ? 3 : 2;
+    static_assert((1 << RB) == R5, "R5 is a power of two in 4..32");
+    __shared__ float4 sp[kL0Tile];
+    __shared__ uint32_t sk[kL0Tile];
+    __shared__ uint8_t sd[kL0Tile];
+    __shared__ alignas(16) uint8_t wcnt[R][kL0RW];
+    __shared__ alignas(16) uint16_t wpre[R][kL0RW];
+    __shared__ uint32_t dbase[R], gofs[R];
+    __shared__ uint32_t hc[R * kDests];
+    const uint32_t tid = threadIdx.x, w = tid / 64, lane = tid & 63;
+    const L0Unit U = units[blockIdx.x];
+    const uint32_t a = starts[U.d6 * (ngroups + 1) + U.g0], b = starts[U.d6 * (ngroups + 1) + U.g1];
+    uint32_t runr = 0;   // wave 0, lane t < R: next output position of digit t
+    if (w == 0 && lane < (uint32_t)R) {
+        const uint32_t d0 = (lane << 6) | U.d6;
+        runr = d0 < D ? cnt_scan[d0] + gpre[((uint64_t)U.d6 * ngroups + U.g0) * R + lane] : 0u;
+    }
+    gofs[lane & (R - 1)] = runr;   // (an LDS write of runr: its load is complete before the loop)
+    for (int i = tid; i < R * kDests; i += kL0BS) hc[i] = 0;
+    for (int i = tid; i < kL0RW * R / 4; i += kL0BS) reinterpret_cast<uint32_t*>(&wcnt[0][0])[i] = 0;
+    const uint64_t lt = lanemask_lt();
+    uint32_t err = 0;
+    float4 v[kL0IPT];
+    uint32_t kk[kL0IPT];
+    auto load_tile = [&](uint32_t base) {   // unconditional, clamped (see k_l0_down6g)
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int r = 0; r < kL0IPT; r++) {
+            const uint32_t i = min(base + (uint32_t)r * kL0BS + tid, b - 1);
+            v[r] = S.p[i];
+            kk[r] = S.k[i];
+        }
+        asm volatile("" ::: "memory");   // keep the loads ahead of the tile's stores
+    };
+    if (a >= b) return;   // (units are never empty)
+    load_tile(a);
+    l0_dummy_stores(dummy, v);
+    for (uint32_t base = a; base < b; base += kL0Tile) {
+        const uint32_t tn = min(b - base, (uint32_t)kL0Tile);
+        lds_barrier();
+        uint32_t dgp = 0, rwp = 0;
+#pragma unroll
+        for (int r = 0; r < kL0IPT; r++) {
+            const uint32_t j = (uint32_t)r * kL0BS + tid;
+            const bool valid = j < tn;
+            uint32_t d5 = 0;
+            if (valid) {
+                uint32_t dest;
+                const int64_t d = l0_dense_dest(P, v[r].x, v[r].y, v[r].z, dest);
+                if (d < 0 || ((uint32_t)d & 63u) != U.d6 || dest >= (uint32_t)kDests) {
+                    err = ERR_L0_RANGE;
+                } else {
+                    d5 = ((uint32_t)d >> 6) & (R - 1);
+                    atomicAdd(&hc[d5 * kDests + dest], 1u);
+                }
+            }
+            const uint64_t same = wave_peers<RB>(d5, valid);
+            const uint32_t rw = (uint32_t)__popcll(same & lt);
+            if (valid && rw == 0) wcnt[d5][r * kL0W + w] = (uint8_t)__popcll(same);
+            dgp |= d5 << (8 * r);
+            rwp |= rw << (8 * r);
+        }
+        lds_barrier();
+        if (w == 0) {
+            uint32_t ex;
+            const uint32_t tot = l0_tile_prefix<R>(wcnt, wpre, lane, ex);
+            if (lane < (uint32_t)R) {
+                dbase[lane] = ex;
+                gofs[lane] = runr - ex;
+                runr += tot;
+            }
+        }
+        lds_barrier();
+#pragma unroll
+        for (int r = 0; r < kL0IPT; r++) {
+            const uint32_t j = (uint32_t)r * kL0BS + tid;
+            if (j < tn) {
+                const uint32_t d5 = (dgp >> (8 * r)) & 0xFFu;
+                const uint32_t q = dbase[d5] + wpre[d5][r * kL0W + w] + ((rwp >> (8 * r)) & 0xFFu);
+                sp[q] = v[r];
+                sk[q] = kk[r];
+                sd[q] = (uint8_t)d5;
+            }
+        }
+        load_tile(b - base > (uint32_t)kL0Tile ? base + kL0Tile : base);
+        lds_barrier();
+#pragma unroll
+        for (int r = 0; r < kL0IPT; r++) {   // past tn: a duplicate of the last store
+            const uint32_t j = min((uint32_t)r * kL0BS + tid, tn - 1);
+            const uint32_t dst = gofs[sd[j]] + j;
+            O.p[dst] = sp[j];
+            O.k[dst] = sk[j];
+        }
+    }
+    lds_barrier();
+    for (int i = tid; i < R * kDests; i += kL0BS) {
+        const uint32_t c = hc[i];
+        if (!c) continue;
+        const uint32_t d0 = ((uint32_t)(i / kDests) << 6) | U.d6;
+        if (d0 < D) atomicAdd(&dcap[(uint64_t)sid[d0] * kDests + (uint32_t)(i % kDests)], c);
+    }
+    if (err) set_err(ctr, err);
+}
+
 // per dense slab: non-empty flag; per grid cell: non-empty flag
 __global__ void k_l0_flags(const uint32_t* hist, uint32_t D, int32_t nl, uint32_t* sflag, uint32_t* cflag, uint32_t G) {
     uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
@@ -3195,11 +3541,22 @@ int Engine::level0_bin() {
     uint32_t* cscan = static_cast<uint32_t*>(dev_->get(G * 4));
     uint32_t* d_tot = static_cast<uint32_t*>(dev_->get(16));
     HIP_CHECK(hipMemsetAsync(hist, 0, D * 4, stream_));
+    int cbits = 0;
+    while ((1ull << cbits) < G) cbits++;
+    const int rem = kL0LayerBits - 6 + cbits;
+    const int passes = std::max(1, (rem + 7) / 8);
+    const int per = std::max(1, (rem + passes - 1) / passes);
+    // one upsweep (k_l0_down6g / k_l0_down5g) when the rest of the dense id fits one 5-bit pass
+    // (with external keys staged beside the points the pair table must stay <= 16 wide)
+    const bool l0keys = src_keys_ != nullptr;
+    bool g1up = !P.hashed && passes == 1 && per <= (l0keys ? 4 : 5) && ntiles > 0 &&
+                getenv("PCC_L0_TWO_UPSWEEPS") == nullptr;
+    const uint32_t r5 = l0keys ? 16u : 32u;
     // capacities fused into the pass-1 upsweep when the level-1 slab grid fits LDS
     L1Grid Q;
     for (int a = 0; a < 3; a++) { Q.lo[a] = 2 * P.lo[a]; Q.g[a] = 2 * P.g[a]; }
     const uint64_t D1w = 8ull * G * kL0Layers;
-    const bool fuse_dcap = !P.hashed && D1w <= (uint64_t)kHist1Lds && getenv("PCC_NO_FUSED_DCAP") == nullptr;
+    const bool fuse_dcap = !g1up && !P.hashed && D1w <= (uint64_t)kHist1Lds && getenv("PCC_NO_FUSED_DCAP") == nullptr;
     const uint32_t D1 = fuse_dcap ? (uint32_t)D1w : 0u;
     uint32_t* H1 = nullptr;
     if (fuse_dcap) {
@@ -3210,22 +3567,86 @@ int Engine::level0_bin() {
     // pass): pass 0 on the low 6 layer bits (upsweep done above), then the rest
     // of the layer and the cell bits in passes of at most 8 bits; the first of
     // those also builds the dense histogram.
-    int cbits = 0;
-    while ((1ull << cbits) < G) cbits++;
-    const int rem = kL0LayerBits - 6 + cbits;
-    const int passes = std::max(1, (rem + 7) / 8);
-    const int per = std::max(1, (rem + passes - 1) / passes);
-    uint32_t* counts = static_cast<uint32_t*>(dev_->get(((uint64_t)ntiles << per) * 4 + 64));
     Arena A0 = dev_->ar[0], A1 = dev_->ar[1];
     // the final pass must land in arena 0
     Arena dst = (passes % 2) ? A1 : A0;
     scan_excl_u32(counts0, counts0, (uint32_t)((uint64_t)ntiles << 6), nullptr, dev_->scan, stream_);
-    k_l0_down<6, true, false><<<ntiles, kL0BS, 0, stream_>>>(src_, src_keys_, A1, dst, nsrc_, P, 0, counts0, ntiles,
-                                                              nullptr, 0);
+    uint32_t ngroups = 0, *gcnt = nullptr, *starts = nullptr;
+    Arena l0dummy{nullptr, nullptr};
+    L0Unit* dunits = nullptr;
+    uint32_t nunits = 0;
+    if (g1up) {
+        const char* gq = getenv("PCC_L0_GROUPS");
+        ngroups = std::min<uint32_t>(gq ? std::max<uint32_t>(1, (uint32_t)strtoul(gq, nullptr, 10)) : kL0Groups, ntiles);
+        const uint32_t tpg = (ntiles + ngroups - 1) / ngroups;
+        ngroups = (ntiles + tpg - 1) / tpg;
+        gcnt = static_cast<uint32_t*>(dev_->get(64ull * ngroups * r5 * 4));
+        l0dummy.p = static_cast<float4*>(dev_->get(256ull * kL0BS * kL0IPT * 16));
+        l0dummy.k = static_cast<uint32_t*>(dev_->get(256ull * kL0BS * kL0IPT * 4));
+        starts = static_cast<uint32_t*>(dev_->get(64ull * (ngroups + 1) * 4));
+        if (l0keys) {
+            k_l0_down6g<16, true><<<ngroups, kL0BS, 0, stream_>>>(src_, src_keys_, dst, nsrc_, P, counts0, ntiles, tpg,
+                                                                   ngroups, gcnt, l0dummy, dev_->ctr);
+            k_l0_gprefix<16><<<64, 1024, 0, stream_>>>(gcnt, ngroups, (uint32_t)D, hist, dev_->ctr);
+        } else {
+            k_l0_down6g<32, false><<<ngroups, kL0BS, 0, stream_>>>(src_, nullptr, dst, nsrc_, P, counts0, ntiles, tpg,
+                                                                    ngroups, gcnt, l0dummy, dev_->ctr);
+            k_l0_gprefix<32><<<64, 1024, 0, stream_>>>(gcnt, ngroups, (uint32_t)D, hist, dev_->ctr);
+        }
+        k_l0_gstarts<<<grid_for(64ull * (ngroups + 1), 256, 1u << 30), 256, 0, stream_>>>(counts0, ntiles, tpg, ngroups,
+                                                                                          nsrc_, starts);
+        HIP_CHECK(hipGetLastError());
+        // pass-2 units: runs of consecutive segments of one d6 bucket, about
+        // nsrc / 2048 points each (a segment is never split)
+        std::vector<uint32_t> st(64ull * (ngroups + 1));
+        HIP_CHECK(hipMemcpyAsync(st.data(), starts, st.size() * 4, hipMemcpyDeviceToHost, stream_));
+        HIP_CHECK(hipStreamSynchronize(stream_));
+        const char* udiv = getenv("PCC_L0_UNIT_DIV");
+        const uint64_t ud = udiv ? std::max<uint64_t>(1, strtoull(udiv, nullptr, 10)) : 8192;
+        const uint64_t target = std::max<uint64_t>(nsrc_ / ud, 4ull * kL0Tile);
+        std::vector<L0Unit> units;
+        uint64_t maxseg = 0;
+        for (uint32_t d6 = 0; d6 < 64; d6++) {
+            const uint32_t* row = st.data() + (uint64_t)d6 * (ngroups + 1);
+            uint32_t g0 = 0;
+            uint64_t acc = 0;
+            for (uint32_t gg = 0; gg < ngroups; gg++) {
+                const uint64_t sz = row[gg + 1] - row[gg];
+                maxseg = std::max(maxseg, sz);
+                if (acc && acc + sz > target) {
+                    units.push_back(L0Unit{d6, g0, gg, 0});
+                    g0 = gg;
+                    acc = 0;
+                }
+                acc += sz;
+            }
+            if (acc) units.push_back(L0Unit{d6, g0, ngroups, 0});
+        }
+        if (getenv("PCC_L0_UNIT_SORT")) std::stable_sort(units.begin(), units.end(), [&](const L0Unit& x, const L0Unit& y) {
+            const uint32_t* rx = st.data() + (uint64_t)x.d6 * (ngroups + 1);
+            const uint32_t* ry = st.data() + (uint64_t)y.d6 * (ngroups + 1);
+            return rx[x.g1] - rx[x.g0] > ry[y.g1] - ry[y.g0];
+        });
+        if (maxseg > 16 * target) {
+            // a few segments hold most points (the layers' low bits are skewed):
+            // units cannot balance, take the two-upsweep pass below
+            g1up = false;
+            HIP_CHECK(hipMemsetAsync(hist, 0, D * 4, stream_));
+        } else {
+            nunits = (uint32_t)units.size();
+            dunits = static_cast<L0Unit*>(dev_->get(std::max<uint64_t>(nunits, 1) * sizeof(L0Unit)));
+            if (nunits)
+                HIP_CHECK(hipMemcpyAsync(dunits, units.data(), nunits * sizeof(L0Unit), hipMemcpyHostToDevice, stream_));
+        }
+    } else {
+        k_l0_down<6, true, false><<<ntiles, kL0BS, 0, stream_>>>(src_, src_keys_, A1, dst, nsrc_, P, 0, counts0, ntiles,
+                                                                  nullptr, 0);
+    }
     HIP_CHECK(hipGetLastError());
     Arena src = dst;
     dst = (dst.p == A0.p) ? A1 : A0;
-    for (int p = 0, shift = 6; p < passes; p++, shift += per) {
+    uint32_t* counts = g1up ? nullptr : static_cast<uint32_t*>(dev_->get(((uint64_t)ntiles << per) * 4 + 64));
+    for (int p = 0, shift = 6; p < passes && !g1up; p++, shift += per) {
         switch (per) {
             case 1: l0_pass<1>(p, passes, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, Q, H1, D1, dev_->scan, stream_); break;
             case 2: l0_pass<2>(p, passes, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, Q, H1, D1, dev_->scan, stream_); break;
@@ -3273,6 +3694,16 @@ int Engine::level0_bin() {
         hist, cnt_scan, sflag, cflag, cscan, (uint32_t)D, (uint32_t)G, P, L->cell_idx, L->cell_sb, L->cell_slab0,
         L->slab_cell, L->slab_layer, L->slab_off, L->slab_n);
     k_set_u32<<<1, 1, 0, stream_>>>(L->cell_slab0 + L->ncells, L->nslabs);
+    if (g1up) {   // pass 2 into arena 0, with the capacities
+        HIP_CHECK(hipMemsetAsync(L->dcap, 0, (uint64_t)L->nslabs * kDests * 4, stream_));
+        if (nunits && r5 == 16)
+            k_l0_down5g<16><<<nunits, kL0BS, 0, stream_>>>(src, dst, P, dunits, starts, ngroups, gcnt, cnt_scan, sflag,
+                                                            (uint32_t)D, L->dcap, l0dummy, dev_->ctr);
+        else if (nunits)
+            k_l0_down5g<32><<<nunits, kL0BS, 0, stream_>>>(src, dst, P, dunits, starts, ngroups, gcnt, cnt_scan, sflag,
+                                                            (uint32_t)D, L->dcap, l0dummy, dev_->ctr);
+        HIP_CHECK(hipGetLastError());
+    }
     if (!root_xyz_.empty() && L->ncells) {   // sub-tree build: the roots' spill batches
         int32_t* rx = static_cast<int32_t*>(dev_->get(root_xyz_.size() * 4));
         uint32_t* rs = static_cast<uint32_t*>(dev_->get(root_sb_.size() * 4));
@@ -3293,7 +3724,9 @@ int Engine::level0_bin() {
         HIP_CHECK(hipMemcpyAsync(&hc, dev_->ctr, sizeof hc, hipMemcpyDeviceToHost, stream_));
         HIP_CHECK(hipStreamSynchronize(stream_));
         L->max_slab = hc.max_slab;
-        if (fuse_dcap) {
+        if (g1up) {
+            // capacities counted by k_l0_down5g
+        } else if (fuse_dcap) {
             const uint64_t nd = (uint64_t)L->nslabs * kDests;
             k_l0_dcap_from1<<<grid_for(nd, 256, 1u << 30), 256, 0, stream_>>>(H1, P, Q, L->cell_idx, L->slab_cell,
                                                                               L->slab_layer, L->nslabs, L->dcap);
@@ -3898,34 +4331,95 @@ __global__ __launch_bounds__(kShBS) void k_shard_hist(const Point* __restrict__ 
             if (h[i]) atomicAdd(&hist[i], h[i]);
 }
 
-// owner rank per point (sort key) and its local index (payload)
-__global__ __launch_bounds__(kShBS) void k_shard_owner(const Point* __restrict__ in, uint32_t n, ShardGrid g,
-                                                       ShardSlabs m, const uint32_t* __restrict__ owner, uint32_t nranks,
-                                                       uint32_t* ow, uint32_t* idx, uint32_t* cnt, uint32_t* bad) {
+// Stable partition by destination rank in two passes over the points (no sort,
+// no random gather): per 4096-point tile the points per destination
+// (k_route_count), an exclusive scan over (destination, tile), then every tile
+// writes its points in index order to its runs (k_route_scatter).  Ranks inside
+// a 256-point chunk come from wave peer masks and per-wave counts in LDS.
+constexpr int kRtBS = 256, kRtIPT = 16, kRtTile = kRtBS * kRtIPT, kRtW = kRtBS / 64;
+__device__ __forceinline__ uint32_t route_dest_rank(const ShardGrid& g, const ShardSlabs& m, const uint32_t* owner,
+                                                    uint32_t nranks, const float4& v, uint32_t& bad) {
+    const uint32_t u = shard_unit(g, m, v.x, v.y, v.z);
+    uint32_t o = u == 0xFFFFFFFFu ? 0xFFFFFFFFu : owner[u];
+    if (o >= nranks) { bad = 1u; o = 0; }
+    return o;
+}
+
+__global__ __launch_bounds__(kRtBS) void k_route_count(const Point* __restrict__ in, uint32_t n, ShardGrid g,
+                                                       ShardSlabs m, const uint32_t* __restrict__ owner,
+                                                       uint32_t nranks, uint32_t ntiles, uint32_t* counts,
+                                                       uint32_t* flag) {
     __shared__ uint32_t c[64];
     if (threadIdx.x < 64) c[threadIdx.x] = 0;
     __syncthreads();
     const float4* p4 = reinterpret_cast<const float4*>(in);
-    for (uint32_t i = blockIdx.x * kShBS + threadIdx.x; i < n; i += gridDim.x * kShBS) {
-        const float4 v = p4[i];
-        const uint32_t cl = shard_unit(g, m, v.x, v.y, v.z);
-        uint32_t r = cl == 0xFFFFFFFFu ? 0xFFFFFFFFu : owner[cl];
-        if (r >= nranks) { atomicOr(bad, 1u); r = 0; }
-        ow[i] = r;
-        idx[i] = i;
-        atomicAdd(&c[r], 1u);
+    const uint32_t tile = blockIdx.x;
+    uint32_t bad = 0;
+#pragma unroll 4
+    for (int r = 0; r < kRtIPT; r++) {
+        const uint32_t i = tile * (uint32_t)kRtTile + (uint32_t)r * kRtBS + threadIdx.x;
+        const bool valid = i < n;
+        uint32_t o = 64;
+        if (valid) o = route_dest_rank(g, m, owner, nranks, p4[i], bad);
+        const uint64_t peers = wave_peers<7>(o, valid);
+        if (valid && mask_rank(peers) == 0) atomicAdd(&c[o], (uint32_t)__popcll(peers));
     }
+    if (bad) atomicOr(flag, 1u);
     __syncthreads();
-    if (threadIdx.x < nranks && c[threadIdx.x]) atomicAdd(&cnt[threadIdx.x], c[threadIdx.x]);
+    if (threadIdx.x < nranks) counts[(uint64_t)threadIdx.x * ntiles + tile] = c[threadIdx.x];
 }
 
-__global__ __launch_bounds__(kShBS) void k_shard_gather(const Point* __restrict__ in, uint32_t n, const uint32_t* __restrict__ idx,
-                                                        uint32_t key0, Point* out, uint32_t* keys) {
-    for (uint32_t j = blockIdx.x * kShBS + threadIdx.x; j < n; j += gridDim.x * kShBS) {
-        const uint32_t i = idx[j];
-        reinterpret_cast<float4*>(out)[j] = reinterpret_cast<const float4*>(in)[i];
-        keys[j] = key0 + i;
+__global__ __launch_bounds__(kRtBS) void k_route_scatter(const Point* __restrict__ in, uint32_t n, ShardGrid g,
+                                                         ShardSlabs m, const uint32_t* __restrict__ owner,
+                                                         uint32_t nranks, uint32_t ntiles,
+                                                         const uint32_t* __restrict__ base, uint32_t key0,
+                                                         Point* __restrict__ out, uint32_t* __restrict__ keys) {
+    __shared__ uint32_t run[64];
+    __shared__ uint32_t wc[2][kRtW][64];
+    const uint32_t tid = threadIdx.x, w = tid / 64, lane = tid & 63;
+    const uint32_t tile = blockIdx.x;
+    if (tid < nranks) run[tid] = base[(uint64_t)tid * ntiles + tile];
+    const float4* p4 = reinterpret_cast<const float4*>(in);
+    float4* o4 = reinterpret_cast<float4*>(out);
+    uint32_t bad = 0;
+    for (int r = 0; r < kRtIPT; r++) {
+        const uint32_t par = (uint32_t)r & 1u;
+        const uint32_t i = tile * (uint32_t)kRtTile + (uint32_t)r * kRtBS + tid;
+        const bool valid = i < n;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        uint32_t o = 64;
+        if (valid) {
+            v = p4[i];
+            o = route_dest_rank(g, m, owner, nranks, v, bad);
+        }
+        const uint64_t peers = wave_peers<7>(o, valid);
+        const uint32_t rk = mask_rank(peers);
+        wc[par][w][lane] = 0;   // this wave's row (the other parity is still read by the run update)
+        __builtin_amdgcn_wave_barrier();
+        if (valid && rk == 0) wc[par][w][o] = (uint32_t)__popcll(peers);
+        __syncthreads();
+        if (valid) {
+            uint32_t pos = run[o] + rk;
+            for (uint32_t q = 0; q < w; q++) pos += wc[par][q][o];
+            o4[pos] = v;
+            keys[pos] = key0 + i;
+        }
+        __syncthreads();
+        if (tid < nranks) {
+            uint32_t t = 0;
+            for (uint32_t q = 0; q < (uint32_t)kRtW; q++) t += wc[par][q][tid];
+            run[tid] += t;
+        }
     }
+    (void)bad;
+}
+
+// per destination: its first position (scan value at (r, tile 0)); the end from the total
+__global__ void k_route_totals(const uint32_t* base, uint32_t ntiles, uint32_t nranks, const uint32_t* total,
+                               uint32_t* first) {
+    const uint32_t r = threadIdx.x;
+    if (r < nranks) first[r] = base[(uint64_t)r * ntiles];
+    if (r == nranks) first[r] = *total;
 }
 }  // namespace
 
@@ -3982,29 +4476,28 @@ int shard_route(const Point* d, uint64_t n, uint32_t key0, const ShardGrid& g, c
     ShardScratch& S = shard_scratch(device);
     if (nranks == 0 || nranks > 64) return -EINVAL;
     if (n >= (1ull << 32)) return -EOVERFLOW;
-    if (S.cap < n) {
-        for (auto*& b : S.buf) { (void)hipFree(b); b = nullptr; HIP_CHECK(hipMalloc(&b, std::max<uint64_t>(n, 1) * 4)); }
-        S.cap = n;
+    const uint32_t n32 = (uint32_t)n;
+    const uint32_t ntiles = (uint32_t)((n + kRtTile - 1) / kRtTile);
+    const uint64_t nc = (uint64_t)ntiles * nranks;
+    if (S.cap < nc + 2 * 65) {
+        for (auto*& b : S.buf) { (void)hipFree(b); b = nullptr; HIP_CHECK(hipMalloc(&b, std::max<uint64_t>(nc + 2 * 65, 1) * 4)); }
+        S.cap = nc + 2 * 65;
     }
-    HIP_CHECK(hipMemsetAsync(S.cnt, 0, 64 * 4, S.st));
     HIP_CHECK(hipMemsetAsync(S.flag, 0, 4, S.st));
-    uint32_t hc[64] = {};
+    uint32_t first[65] = {};
     if (n) {
-        const uint32_t n32 = (uint32_t)n;
-        k_shard_owner<<<grid_for(n, kShBS, 4096), kShBS, 0, S.st>>>(d, n32, g, shard_slabs(g, dim), downer, nranks,
-                                                                     S.buf[0], S.buf[1], S.cnt, S.flag);
-        int bits = 0;
-        while ((1u << bits) < nranks) bits++;
-        int which = 0;
-        if (bits) which = radix_sort_pairs(S.buf[0], S.buf[1], S.buf[2], S.buf[3], n32, bits, S.sort, S.st);
-        k_shard_gather<<<grid_for(n, kShBS, 8192), kShBS, 0, S.st>>>(d, n32, which ? S.buf[3] : S.buf[1], key0, dsend, dkeys);
+        const ShardSlabs m = shard_slabs(g, dim);
+        k_route_count<<<ntiles, kRtBS, 0, S.st>>>(d, n32, g, m, downer, nranks, ntiles, S.buf[0], S.flag);
+        scan_excl_u32(S.buf[0], S.buf[1], (uint32_t)nc, S.buf[2], S.sort.scan, S.st);
+        k_route_scatter<<<ntiles, kRtBS, 0, S.st>>>(d, n32, g, m, downer, nranks, ntiles, S.buf[1], key0, dsend, dkeys);
+        k_route_totals<<<1, 128, 0, S.st>>>(S.buf[1], ntiles, nranks, S.buf[2], S.buf[3]);
         HIP_CHECK(hipGetLastError());
-        HIP_CHECK(hipMemcpyAsync(hc, S.cnt, 64 * 4, hipMemcpyDeviceToHost, S.st));
+        HIP_CHECK(hipMemcpyAsync(first, S.buf[3], (nranks + 1) * 4, hipMemcpyDeviceToHost, S.st));
     }
     uint32_t bad = 0;
     HIP_CHECK(hipMemcpyAsync(&bad, S.flag, 4, hipMemcpyDeviceToHost, S.st));
     HIP_CHECK(hipStreamSynchronize(S.st));
-    for (uint32_t r = 0; r < nranks; r++) counts[r] = hc[r];
+    for (uint32_t r = 0; r < nranks; r++) counts[r] = n ? (uint64_t)(first[r + 1] - first[r]) : 0;
     return bad ? -ERANGE : 0;
 }
 

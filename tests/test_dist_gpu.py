@@ -71,6 +71,38 @@ def test_shard_histogram_and_route_match_numpy():
         assert counts == c2
         assert torch.equal(send.cpu(), s2)
         assert torch.equal(keys.cpu(), k2)
+    # a destination past nranks is an error, not a silent drop
+    bad = torch.full((g.ncells,), 3, dtype=torch.int32, device=DEV)
+    with pytest.raises(Exception):
+        pcconv.shard_route(pts.data_ptr(), len(pts_np), 0, g, bad.data_ptr(), 3, send.data_ptr(), keys.data_ptr())
+
+
+def test_shard_slab_histogram_and_route_match_numpy():
+    """Slab mode (cell, hex z-layer) units: histogram and the stable partition
+    (tile count -> scan -> scatter) against numpy, up to 64 destinations."""
+    pts_np = synth(29, 2, 300_007, lo=-2500.0, ext=5000.0)
+    pts = as_tensor(pts_np).to(DEV)
+    ref = NumpyShardOps("/nonexistent")
+    gmin, gmax = ref.bbox(as_tensor(pts_np))
+    g = pcconv.shard_grid_from_bbox(gmin, gmax)
+    dim = int(ref.cfg_full()["sub_grid_dimension"])
+    nu = g.ncells * pcconv.SHARD_LAYERS
+    h = torch.empty(nu, dtype=torch.int32, device=DEV)
+    torch.cuda.synchronize()
+    pcconv.shard_slab_histogram(pts.data_ptr(), len(pts_np), g, dim, h.data_ptr())
+    assert torch.equal(h.cpu(), ref.slab_histogram(as_tensor(pts_np), g))
+    for world in (4, 64):
+        table = torch.from_numpy((np.arange(nu) * 11 % world).astype(np.int32))
+        send = torch.empty_like(pts)
+        keys = torch.empty(len(pts_np), dtype=torch.int32, device=DEV)
+        td = table.to(DEV)
+        torch.cuda.synchronize()
+        counts = pcconv.shard_route_slabs(pts.data_ptr(), len(pts_np), 77, g, dim, td.data_ptr(), world,
+                                          send.data_ptr(), keys.data_ptr())
+        s2, k2, c2 = ref.route_slabs(as_tensor(pts_np), 77, g, table, world)
+        assert counts == c2
+        assert torch.equal(send.cpu(), s2)
+        assert torch.equal(keys.cpu(), k2)
 
 
 def test_synth_device_matches_oracle_stream():
