@@ -53,7 +53,13 @@ constexpr uint32_t kEmpty32 = 0xFFFFFFFFu;
 constexpr int kDenseBS = 1024;
 constexpr int kDenseTab = 116 * 132;  // one z-layer of a dim-96 cell (slab_geom)
 constexpr int kDenseClaim = 2048;
-constexpr uint32_t kDenseStreamMax = 24576;   // k_slab: stream (not gather) the grid points up to this many arrivals
+#ifndef PCC_STREAM_MAX
+#define PCC_STREAM_MAX 24576
+#endif
+#ifndef PCC_STREAM_V
+#define PCC_STREAM_V 4
+#endif
+constexpr uint32_t kDenseStreamMax = PCC_STREAM_MAX;   // k_slab: stream (not gather) the grid points up to this many arrivals
 constexpr int kSmallBS = 256;
 constexpr uint32_t kSmallMax = 1024;  // slabs with fewer arrivals use the hashed kernel
 constexpr int kSmallTab = 2048;
@@ -1511,7 +1517,7 @@ __device__ __forceinline__ void dense_grid_points(const SlabParams& P, L& S, uin
             }
         }
         __syncthreads();
-        constexpr int V = 4;
+        constexpr int V = PCC_STREAM_V;
         for (uint32_t j0 = 0; j0 < n; j0 += V * BS) {
             u32x4 pv[V];
 #pragma unroll

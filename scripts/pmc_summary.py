@@ -7,6 +7,7 @@ gfx950, so it is doubled.  Per-launch values are averages over the launches of
 one build (bench.py --steps 1 --warmup 0)."""
 import csv
 import json
+import re
 import sys
 from collections import OrderedDict
 
@@ -35,7 +36,19 @@ def main(out_dir, name, bench_json):
         e["hbm_bytes"] = 2.0 * e["fetch_bytes_raw"] + e["write_bytes"]
         e["hbm_bytes_per_launch"] = e["hbm_bytes"] / max(e["launches"], 1)
     bench = json.load(open(bench_json))
-    dense = next(v for n, v in k.items() if n.startswith("pcc::k_slab("))
+    dense = next(v for n, v in k.items() if n.startswith(("pcc::k_slab(", "void pcc::k_slab<false>(")))
+    # level-0 binning: every build kernel launched before the first slab kernel, against
+    # one 16-B read and one 20-B write (point + key) per input point
+    l0 = {"hbm_bytes": 0.0, "ns": 0, "kernels": []}
+    for n, v in k.items():
+        if "k_slab" in n:
+            break
+        if n.startswith(("pcc::k_synth", "__amd_rocclr")):   # bench input generation, runtime copies
+            continue
+        l0["hbm_bytes"] += v["hbm_bytes"]
+        l0["ns"] += v["ns"]
+        l0["kernels"].append(n.split("(")[0])
+    npts = float(re.search(r"(\d+) ", bench["config"]["workload"]).group(1))
     arr = bench["stage_ms"]["dense_arrivals"]
     summary = {
         "workload": bench["config"]["workload"],
@@ -44,10 +57,13 @@ def main(out_dir, name, bench_json):
         "dense_kernel": {"launches": dense["launches"], "hbm_bytes_per_launch": dense["hbm_bytes_per_launch"],
                          "alg_bytes_per_launch": 32.0 * arr / dense["launches"],
                          "traffic_over_alg": dense["hbm_bytes"] / (32.0 * arr)},
+        "level0": {"kernels": l0["kernels"], "hbm_bytes": l0["hbm_bytes"], "alg_bytes": 36.0 * npts,
+                   "traffic_over_alg": l0["hbm_bytes"] / (36.0 * npts), "ms": l0["ns"] / 1e6},
         "kernels": k,
     }
     json.dump(summary, open(f"profiles/{name}.json", "w"), indent=1)
     print(json.dumps(summary["dense_kernel"]))
+    print(json.dumps({a: b for a, b in summary["level0"].items() if a != "kernels"}))
 
 
 if __name__ == "__main__":
