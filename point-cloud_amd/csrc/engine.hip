@@ -53,6 +53,9 @@ constexpr uint32_t kEmpty32 = 0xFFFFFFFFu;
 constexpr int kDenseBS = 1024;
 constexpr int kDenseTab = 116 * 132;  // one z-layer of a dim-96 cell (slab_geom)
 constexpr int kDenseClaim = 2048;
+#ifndef PCC_SLAB_PF
+#define PCC_SLAB_PF 2
+#endif
 #ifndef PCC_STREAM_MAX
 #define PCC_STREAM_MAX 24576
 #endif
@@ -1652,11 +1655,12 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
     // emission store (step i+1), so no loaded register is ever copied (a copy
     // would wait for the load, and vmcnt also counts the stores issued since).
     struct Pre { u32x4 p; uint32_t k; };
-    Pre pre[4];
+    constexpr int PF = PCC_SLAB_PF;   // chunks loaded ahead; the ring holds PF + 2
+    Pre pre[PF + 2];
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
+    for (int q = 0; q < PF + 2; q++) {
         const uint32_t jo = min((uint32_t)(q * BS) + tid, nm1);
-        if (q < 2) {
+        if (q < PF) {
             pre[q].p = rP.p(jo * 16);
             pre[q].k = rP.k(jo * 4);
         } else {
@@ -1687,7 +1691,7 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
         const bool valid = j < n;
         const bool forced = valid && mine.k - P.kf_lo < P.kf_n;
         {   // prefetch chunk i+2 (clamped)
-            const uint32_t jo = min(j + 2 * BS, nm1);
+            const uint32_t jo = min(j + PF * BS, nm1);
             pf.p = rP.p(jo * 16);
             pf.k = rP.k(jo * 4);
         }
@@ -1855,15 +1859,28 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
         STAMP(5);
         STAMP_COUNT(10, 1);
     };
-    // nchunks + 1 steps (the last one only emits)
-    for (uint32_t ci = 0; ci <= nchunks; ci += 4) {
-        step(ci, A, B, pre[0], pre[3], pre[2]);
-        if (ci + 1 > nchunks) break;
-        step(ci + 1, B, A, pre[1], pre[0], pre[3]);
-        if (ci + 2 > nchunks) break;
-        step(ci + 2, A, B, pre[2], pre[1], pre[0]);
-        if (ci + 3 > nchunks) break;
-        step(ci + 3, B, A, pre[3], pre[2], pre[1]);
+    // nchunks + 1 steps (the last one only emits).  Chunk i lives in
+    // pre[i % (PF + 2)] from its load (step i - PF) to its emission store (step i + 1).
+    if constexpr (PF == 2) {
+        for (uint32_t ci = 0; ci <= nchunks; ci += 4) {
+            step(ci, A, B, pre[0], pre[3], pre[2]);
+            if (ci + 1 > nchunks) break;
+            step(ci + 1, B, A, pre[1], pre[0], pre[3]);
+            if (ci + 2 > nchunks) break;
+            step(ci + 2, A, B, pre[2], pre[1], pre[0]);
+            if (ci + 3 > nchunks) break;
+            step(ci + 3, B, A, pre[3], pre[2], pre[1]);
+        }
+    } else {
+        static_assert(PF == 3, "prefetch depth 2 or 3");
+        for (uint32_t ci = 0; ci <= nchunks; ci += 10) {
+#define PCC_STEP10(k, X, Y)                                                    \
+    if (ci + (k) > nchunks) break;                                             \
+    step(ci + (k), X, Y, pre[(k) % 5], pre[((k) + 4) % 5], pre[((k) + 3) % 5]);
+            PCC_STEP10(0, A, B) PCC_STEP10(1, B, A) PCC_STEP10(2, A, B) PCC_STEP10(3, B, A) PCC_STEP10(4, A, B)
+            PCC_STEP10(5, B, A) PCC_STEP10(6, A, B) PCC_STEP10(7, B, A) PCC_STEP10(8, A, B) PCC_STEP10(9, B, A)
+#undef PCC_STEP10
+        }
     }
     STAMP(7);
     __syncthreads();
@@ -4317,18 +4334,29 @@ constexpr int kShBS = 256;
 constexpr uint32_t kShLds = 16384;
 __global__ __launch_bounds__(kShBS) void k_shard_hist(const Point* __restrict__ in, uint64_t n, ShardGrid g,
                                                       ShardSlabs m, uint32_t ncells, uint32_t* hist, uint32_t* bad) {
-    __shared__ uint32_t h[kShLds];
+    extern __shared__ uint32_t h[];   // ncells words when ncells <= kShLds (dynamic: small grids keep occupancy)
     const bool lds = ncells <= kShLds;
     if (lds)
         for (uint32_t i = threadIdx.x; i < ncells; i += kShBS) h[i] = 0;
     __syncthreads();
     const float4* p4 = reinterpret_cast<const float4*>(in);
     uint32_t nbad = 0;
-    for (uint64_t i = blockIdx.x * (uint64_t)kShBS + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kShBS) {
-        const float4 v = p4[i];
-        const uint32_t c = shard_unit(g, m, v.x, v.y, v.z);
-        if (c == 0xFFFFFFFFu) { nbad++; continue; }
-        if (lds) atomicAdd(&h[c], 1u); else wave_aggregated_add(hist, c);
+    constexpr int U = 4;   // loads in flight per thread
+    const uint64_t stride = (uint64_t)gridDim.x * kShBS;
+    for (uint64_t i0 = blockIdx.x * (uint64_t)kShBS + threadIdx.x; i0 < n; i0 += U * stride) {
+        float4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint64_t i = i0 + u * stride;
+            v[u] = p4[i < n ? i : n - 1];
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            if (i0 + u * stride >= n) break;
+            const uint32_t c = shard_unit(g, m, v[u].x, v[u].y, v[u].z);
+            if (c == 0xFFFFFFFFu) { nbad++; continue; }
+            if (lds) atomicAdd(&h[c], 1u); else wave_aggregated_add(hist, c);
+        }
     }
     if (nbad) atomicAdd(bad, nbad);
     __syncthreads();
@@ -4469,7 +4497,8 @@ int shard_histogram(const Point* d, uint64_t n, const ShardGrid& g, uint32_t* dh
     if (nc >= (1ull << 32)) return -EOVERFLOW;
     HIP_CHECK(hipMemsetAsync(dhist, 0, nc * 4, S.st));
     HIP_CHECK(hipMemsetAsync(S.flag, 0, 4, S.st));
-    if (n) k_shard_hist<<<grid_for(n, kShBS, 1024), kShBS, 0, S.st>>>(d, n, g, shard_slabs(g, dim), (uint32_t)nc, dhist, S.flag);
+    const size_t smem = nc <= kShLds ? (size_t)nc * 4 : 0;
+    if (n) k_shard_hist<<<grid_for(n, kShBS, 2048), kShBS, smem, S.st>>>(d, n, g, shard_slabs(g, dim), (uint32_t)nc, dhist, S.flag);
     HIP_CHECK(hipGetLastError());
     uint32_t bad = 0;
     HIP_CHECK(hipMemcpyAsync(&bad, S.flag, 4, hipMemcpyDeviceToHost, S.st));

@@ -38,4 +38,19 @@ for _ in range(5):
     st = c.build()
 out["octant_build_ms"] = (time.perf_counter() - t0) / 5 * 1e3
 c.close()
+# the same octant handed over with keys, as a rank receives it after the exchange
+oct_pts = torch.empty((n, 4), dtype=torch.int32, device=dev)
+pcconv.synth_device(oct_pts.data_ptr(), 0, n, 4, 0, 0.0, 1000.0, 0)
+oct_keys = torch.arange(n, dtype=torch.int32, device=dev) * 8
+torch.cuda.synchronize()
+c = pcconv.Converter("/tmp/pcc_rank_n8k")
+c.declare_files([8 * n])
+c.set_keyed_points_device(oct_pts.data_ptr(), oct_keys.data_ptr(), n)
+c.build()
+t0 = time.perf_counter()
+for _ in range(5):
+    st = c.build()
+out["octant_build_keyed_ms"] = (time.perf_counter() - t0) / 5 * 1e3
+
+c.close()
 print(json.dumps(out))
