@@ -233,6 +233,22 @@ int pcc_shard_route_slabs(const pcc_point* dev_pts, uint64_t n, uint32_t key0, c
                           uint32_t sub_grid_dimension, const uint32_t* dev_owner, uint32_t nranks, pcc_point* dev_send,
                           uint32_t* dev_keys, uint64_t* counts, int device);
 
+/* Exchange-lean form of pcc_shard_route / pcc_shard_route_slabs
+ * (sub_grid_dimension 0: cell units, else slab units): no key per routed point;
+ * instead dev_bitmaps[r * ceil(n/64) + w] bit b is set iff local point 64 w + b
+ * goes to rank r (u64 words, written in full by the call).  A receiver gets row
+ * r of every sender (4 B per routed point become 1 bit per sender point) and
+ * rebuilds the keys with pcc_shard_keys_from_bitmaps. */
+int pcc_shard_route_bitmaps(const pcc_point* dev_pts, uint64_t n, const pcc_shard_grid* g,
+                            uint32_t sub_grid_dimension, const uint32_t* dev_owner, uint32_t nranks,
+                            pcc_point* dev_send, uint64_t* dev_bitmaps, uint64_t* counts, int device);
+/* Keys of the points received from nsrc senders (sender order, each ascending):
+ * dev_bitmaps = the senders' rows for this rank concatenated (nwords[s] words
+ * each), key0[s] = sender s's first global key.  nkeys must equal the number of
+ * set bits (= received points), else -EBADMSG. */
+int pcc_shard_keys_from_bitmaps(const uint64_t* dev_bitmaps, const uint64_t* nwords, const uint64_t* key0,
+                                uint32_t nsrc, uint32_t* dev_keys, uint64_t nkeys, int device);
+
 /* Writes one cell file h_{hierarchy}/c_x_y_z.bin under out_dir from a view
  * (Cell::write_to cell.rs:155-181): a cell assembled by the caller from the
  * pieces several ranks built. */

@@ -535,6 +535,32 @@ int pcc_shard_route_slabs(const pcc_point* d, uint64_t n, uint32_t key0, const p
     GUARD_END
 }
 
+int pcc_shard_route_bitmaps(const pcc_point* d, uint64_t n, const pcc_shard_grid* g, uint32_t sub_grid_dimension,
+                            const uint32_t* downer, uint32_t nranks, pcc_point* dsend, uint64_t* dbitmaps,
+                            uint64_t* counts, int device) {
+    if ((!d || !dsend || !dbitmaps) && n) return set_err(-EINVAL, "null argument");
+    if (!g || !downer || !counts) return set_err(-EINVAL, "null argument");
+    if (sub_grid_dimension != 0 && 2 * sub_grid_dimension + 2 > PCC_SHARD_LAYERS)
+        return set_err(-EINVAL, "sub_grid_dimension out of range for slab sharding");
+    GUARD_BEGIN
+    const int rc = shard_route(reinterpret_cast<const Point*>(d), n, 0, to_grid(g), downer, nranks,
+                               reinterpret_cast<Point*>(dsend), nullptr, counts, device, sub_grid_dimension, dbitmaps);
+    return rc ? set_err(rc, "routing failed (nranks > 64, point outside grid, or owner >= nranks)") : 0;
+    GUARD_END
+}
+
+int pcc_shard_keys_from_bitmaps(const uint64_t* dbitmaps, const uint64_t* nwords, const uint64_t* key0, uint32_t nsrc,
+                                uint32_t* dkeys, uint64_t nkeys, int device) {
+    if (!nwords || !key0 || (nkeys && (!dkeys || !dbitmaps))) return set_err(-EINVAL, "null argument");
+    for (uint32_t s = 0; s < nsrc; s++)
+        if (key0[s] + 64 * nwords[s] > (1ull << 32) + 63) return set_err(-EOVERFLOW, "global keys must fit in 32 bits");
+    GUARD_BEGIN
+    const int rc = shard_keys_from_bitmaps(dbitmaps, nwords, key0, nsrc, dkeys, nkeys, device);
+    if (rc == -EBADMSG) return set_err(rc, "bitmaps do not match the number of received points");
+    return rc ? set_err(rc, "key rebuild failed (nsrc outside 1..64 or too many words)") : 0;
+    GUARD_END
+}
+
 int pcc_write_cell_view(const char* out_dir, const pcc_cell_view* v) {
     if (!out_dir || !v) return set_err(-EINVAL, "null argument");
     if (v->entries > 8) return set_err(-EINVAL, "a cell has at most 8 overflow entries");

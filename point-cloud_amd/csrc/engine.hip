@@ -4284,10 +4284,11 @@ struct ShardScratch {
     float* part = nullptr;
     uint32_t* flag = nullptr;
     uint32_t* cnt = nullptr;
+    uint64_t* tab = nullptr;
     SortTemp sort;
     ~ShardScratch() {
         for (auto* b : buf) (void)hipFree(b);
-        (void)hipFree(part); (void)hipFree(flag); (void)hipFree(cnt);
+        (void)hipFree(part); (void)hipFree(flag); (void)hipFree(cnt); (void)hipFree(tab);
         (void)hipFree(sort.counts); (void)hipFree(sort.scan.bsums);
         if (st) (void)hipStreamDestroy(st);
     }
@@ -4303,6 +4304,7 @@ ShardScratch& shard_scratch(int device) {
         HIP_CHECK(hipMalloc(&t_shard->part, kBBoxBlocks * 6 * sizeof(float)));
         HIP_CHECK(hipMalloc(&t_shard->flag, 4));
         HIP_CHECK(hipMalloc(&t_shard->cnt, 64 * 4));
+        HIP_CHECK(hipMalloc(&t_shard->tab, 132 * 8));
     }
     return *t_shard;
 }
@@ -4407,7 +4409,8 @@ __global__ __launch_bounds__(kRtBS) void k_route_scatter(const Point* __restrict
                                                          ShardSlabs m, const uint32_t* __restrict__ owner,
                                                          uint32_t nranks, uint32_t ntiles,
                                                          const uint32_t* __restrict__ base, uint32_t key0,
-                                                         Point* __restrict__ out, uint32_t* __restrict__ keys) {
+                                                         Point* __restrict__ out, uint32_t* __restrict__ keys,
+                                                         unsigned long long* __restrict__ bm, uint32_t nwords) {
     __shared__ uint32_t run[64];
     __shared__ uint32_t wc[2][kRtW][64];
     const uint32_t tid = threadIdx.x, w = tid / 64, lane = tid & 63;
@@ -4436,7 +4439,9 @@ __global__ __launch_bounds__(kRtBS) void k_route_scatter(const Point* __restrict
             uint32_t pos = run[o] + rk;
             for (uint32_t q = 0; q < w; q++) pos += wc[par][q][o];
             o4[pos] = v;
-            keys[pos] = key0 + i;
+            if (keys) keys[pos] = key0 + i;
+            // membership bitmap: the wave's 64 indices are one aligned word
+            if (bm && rk == 0) bm[(uint64_t)o * nwords + (i >> 6)] = peers;
         }
         __syncthreads();
         if (tid < nranks) {
@@ -4455,7 +4460,64 @@ __global__ void k_route_totals(const uint32_t* base, uint32_t ntiles, uint32_t n
     if (r < nranks) first[r] = base[(uint64_t)r * ntiles];
     if (r == nranks) first[r] = *total;
 }
+// Keys of received points from the senders' membership bitmaps (concatenated in
+// sender order): word popcounts, their exclusive scan (= the received rows'
+// positions), then every word writes the keys of its set bits in order.
+__global__ void k_bm_pop(const unsigned long long* __restrict__ bm, uint32_t nw, uint32_t* __restrict__ pc) {
+    const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w < nw) pc[w] = (uint32_t)__popcll(bm[w]);
+}
+__global__ void k_bm_keys(const unsigned long long* __restrict__ bm, uint32_t nw, const uint32_t* __restrict__ pos,
+                          const uint64_t* __restrict__ wstart, const uint64_t* __restrict__ key0, uint32_t nsrc,
+                          uint32_t* __restrict__ keys, uint32_t nkeys) {
+    const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= nw) return;
+    uint32_t sidx = 0;
+    while (sidx + 1 < nsrc && wstart[sidx + 1] <= w) sidx++;
+    const uint32_t kb = (uint32_t)(key0[sidx] + 64ull * (w - wstart[sidx]));
+    unsigned long long m = bm[w];
+    uint32_t p = pos[w];
+    while (m && p < nkeys) {   // (more bits than received rows: the caller reports the mismatch)
+        const uint32_t b = (uint32_t)__ffsll((long long)m) - 1u;
+        keys[p++] = kb + b;
+        m &= m - 1ull;
+    }
+}
+
 }  // namespace
+
+int shard_keys_from_bitmaps(const uint64_t* dbm, const uint64_t* nwords, const uint64_t* key0, uint32_t nsrc,
+                            uint32_t* dkeys, uint64_t nkeys, int device) {
+    ShardScratch& S = shard_scratch(device);
+    if (nsrc == 0 || nsrc > 64) return -EINVAL;
+    std::vector<uint64_t> tab(2 * nsrc + 1);
+    uint64_t nw = 0;
+    for (uint32_t s = 0; s < nsrc; s++) {
+        tab[s] = nw;
+        tab[nsrc + 1 + s] = key0[s];
+        nw += nwords[s];
+    }
+    tab[nsrc] = nw;
+    if (nw >= (1ull << 32) || nkeys >= (1ull << 32)) return -EOVERFLOW;
+    if (S.cap < nw + 2 * 65) {
+        for (auto*& b : S.buf) { (void)hipFree(b); b = nullptr; HIP_CHECK(hipMalloc(&b, std::max<uint64_t>(nw + 2 * 65, 1) * 4)); }
+        S.cap = nw + 2 * 65;
+    }
+    uint64_t* dtab = S.tab;   // word start per sender, the end, first key per sender (<= 129 words)
+    HIP_CHECK(hipMemcpyAsync(dtab, tab.data(), tab.size() * 8, hipMemcpyHostToDevice, S.st));
+    uint32_t total = 0;
+    if (nw) {
+        const auto* bm = reinterpret_cast<const unsigned long long*>(dbm);
+        k_bm_pop<<<(uint32_t)((nw + 255) / 256), 256, 0, S.st>>>(bm, (uint32_t)nw, S.buf[0]);
+        scan_excl_u32(S.buf[0], S.buf[0], (uint32_t)nw, S.buf[1], S.sort.scan, S.st);
+        k_bm_keys<<<(uint32_t)((nw + 255) / 256), 256, 0, S.st>>>(bm, (uint32_t)nw, S.buf[0], dtab, dtab + nsrc + 1,
+                                                                  nsrc, dkeys, (uint32_t)nkeys);
+        HIP_CHECK(hipGetLastError());
+        HIP_CHECK(hipMemcpyAsync(&total, S.buf[1], 4, hipMemcpyDeviceToHost, S.st));
+    }
+    HIP_CHECK(hipStreamSynchronize(S.st));
+    return total == nkeys ? 0 : -EBADMSG;
+}
 
 int shard_synth(Point* dst, uint64_t idx0, uint64_t n, uint64_t seed, int kind, float lo, float ext, int device) {
     ShardScratch& S = shard_scratch(device);
@@ -4507,7 +4569,7 @@ int shard_histogram(const Point* d, uint64_t n, const ShardGrid& g, uint32_t* dh
 }
 
 int shard_route(const Point* d, uint64_t n, uint32_t key0, const ShardGrid& g, const uint32_t* downer, uint32_t nranks,
-                Point* dsend, uint32_t* dkeys, uint64_t* counts, int device, uint32_t dim) {
+                Point* dsend, uint32_t* dkeys, uint64_t* counts, int device, uint32_t dim, uint64_t* dbm) {
     ShardScratch& S = shard_scratch(device);
     if (nranks == 0 || nranks > 64) return -EINVAL;
     if (n >= (1ull << 32)) return -EOVERFLOW;
@@ -4524,7 +4586,10 @@ int shard_route(const Point* d, uint64_t n, uint32_t key0, const ShardGrid& g, c
         const ShardSlabs m = shard_slabs(g, dim);
         k_route_count<<<ntiles, kRtBS, 0, S.st>>>(d, n32, g, m, downer, nranks, ntiles, S.buf[0], S.flag);
         scan_excl_u32(S.buf[0], S.buf[1], (uint32_t)nc, S.buf[2], S.sort.scan, S.st);
-        k_route_scatter<<<ntiles, kRtBS, 0, S.st>>>(d, n32, g, m, downer, nranks, ntiles, S.buf[1], key0, dsend, dkeys);
+        const uint32_t nwords = (uint32_t)((n + 63) / 64);
+        if (dbm) HIP_CHECK(hipMemsetAsync(dbm, 0, (uint64_t)nranks * nwords * 8, S.st));
+        k_route_scatter<<<ntiles, kRtBS, 0, S.st>>>(d, n32, g, m, downer, nranks, ntiles, S.buf[1], key0, dsend, dkeys,
+                                                    reinterpret_cast<unsigned long long*>(dbm), nwords);
         k_route_totals<<<1, 128, 0, S.st>>>(S.buf[1], ntiles, nranks, S.buf[2], S.buf[3]);
         HIP_CHECK(hipGetLastError());
         HIP_CHECK(hipMemcpyAsync(first, S.buf[3], (nranks + 1) * 4, hipMemcpyDeviceToHost, S.st));

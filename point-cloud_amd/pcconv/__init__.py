@@ -37,7 +37,7 @@ EXPORTS = ["pcc_abi_version", "pcc_last_error", "pcc_options_default", "pcc_open
            "pcc_pending_cells", "pcc_export_pending", "pcc_shard_slab_histogram", "pcc_shard_route_slabs",
            "pcc_write_cell_view", "pcc_begin_file", "pcc_append_points", "pcc_end_file", "pcc_cancel_file",
            "pcc_set_summary", "pcc_write_cells", "pcc_write_metadata", "pcc_clear_input", "pcc_adopt_prior",
-           "pcc_open_subtrees", "pcc_visit_cells"]
+           "pcc_open_subtrees", "pcc_visit_cells", "pcc_shard_route_bitmaps", "pcc_shard_keys_from_bitmaps"]
 
 
 class Options(C.Structure):
@@ -153,6 +153,10 @@ def lib():
         L.pcc_shard_slab_histogram.argtypes = [vp, C.c_uint64, C.POINTER(ShardGrid), C.c_uint32, vp, C.c_int]
         L.pcc_shard_route_slabs.argtypes = [vp, C.c_uint64, C.c_uint32, C.POINTER(ShardGrid), C.c_uint32, vp,
                                             C.c_uint32, vp, vp, C.POINTER(C.c_uint64), C.c_int]
+        L.pcc_shard_route_bitmaps.argtypes = [vp, C.c_uint64, C.POINTER(ShardGrid), C.c_uint32, vp, C.c_uint32, vp,
+                                              vp, C.POINTER(C.c_uint64), C.c_int]
+        L.pcc_shard_keys_from_bitmaps.argtypes = [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.c_uint32, vp,
+                                                  C.c_uint64, C.c_int]
         L.pcc_write_cell_view.argtypes = [C.c_char_p, vp]
         L.pcc_begin_file.argtypes = [vp, C.c_uint64]
         L.pcc_append_points.argtypes = [vp, vp, C.c_uint64]
@@ -386,6 +390,26 @@ def shard_route_slabs(pts_ptr: int, n: int, key0: int, grid: ShardGrid, sub_grid
                                        C.c_void_p(owner_ptr), nranks, C.c_void_p(send_ptr), C.c_void_p(keys_ptr),
                                        counts, device))
     return [int(c) for c in counts]
+
+
+def shard_route_bitmaps(pts_ptr: int, n: int, grid: ShardGrid, sub_grid_dimension: int, owner_ptr: int, nranks: int,
+                        send_ptr: int, bitmaps_ptr: int, device: int = 0):
+    """Route without keys: bitmaps_ptr receives nranks rows of ceil(n/64) u64
+    membership words (pcc_shard_route_bitmaps); returns the counts per rank."""
+    counts = (C.c_uint64 * nranks)()
+    _check(lib().pcc_shard_route_bitmaps(C.c_void_p(pts_ptr), n, C.byref(grid), sub_grid_dimension,
+                                         C.c_void_p(owner_ptr), nranks, C.c_void_p(send_ptr), C.c_void_p(bitmaps_ptr),
+                                         counts, device))
+    return [int(c) for c in counts]
+
+
+def shard_keys_from_bitmaps(bitmaps_ptr: int, nwords, key0, keys_ptr: int, nkeys: int, device: int = 0):
+    """Global keys of received points from the senders' bitmap rows (pcc_shard_keys_from_bitmaps)."""
+    ns = len(nwords)
+    nw = (C.c_uint64 * ns)(*[int(v) for v in nwords])
+    k0 = (C.c_uint64 * ns)(*[int(v) for v in key0])
+    _check(lib().pcc_shard_keys_from_bitmaps(C.c_void_p(bitmaps_ptr), nw, k0, ns, C.c_void_p(keys_ptr), nkeys,
+                                             device))
 
 
 def write_cell_view(out_dir: str, view: "CellView"):

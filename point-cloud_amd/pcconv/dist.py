@@ -88,6 +88,14 @@ class TorchComm:
         in out[ro[p]:ro[p]+recv_counts[p]] (source-rank order).  One grouped
         batch of point-to-point transfers straight into those slices, each at
         most `max_msg_bytes`; the own segment is a local device copy."""
+        ops = self._p2p_ops(send, send_counts, recv_counts, out)
+        if ops:
+            for req in self.dist.batch_isend_irecv(ops):
+                req.wait()
+        return out
+
+    def _p2p_ops(self, send, send_counts, recv_counts, out) -> list:
+        """The own segment copied locally; the point-to-point ops of the rest."""
         row = send.element_size() * max(1, int(np.prod(send.shape[1:])))
         mr = max(1, self.max_msg_bytes // row)
         so = np.concatenate([[0], np.cumsum(send_counts)]).astype(np.int64)
@@ -106,10 +114,17 @@ class TorchComm:
             for b in range(0, int(recv_counts[p_from]), mr):
                 ops.append(self.dist.P2POp(self.dist.irecv, out.narrow(0, int(ro[p_from]) + b,
                                                                        min(mr, int(recv_counts[p_from]) - b)), p_from))
+        return ops
+
+    def alltoallv_many(self, specs):
+        """alltoallv_into for several (send, send_counts, recv_counts, out) in ONE
+        grouped batch of point-to-point transfers (one round trip, not one each)."""
+        ops = []
+        for send, sc, rc, out in specs:
+            ops.extend(self._p2p_ops(send, sc, rc, out))
         if ops:
             for req in self.dist.batch_isend_irecv(ops):
                 req.wait()
-        return out
 
     def barrier(self):
         self.dist.barrier()
@@ -646,6 +661,27 @@ class HipShardOps:
                                     keys.data_ptr(), self.dev)
         return send, keys, counts
 
+    # the exchange carries membership bitmaps instead of keys (route_bitmaps / keys_from_bitmaps)
+    bitmap_keys = True
+
+    def route_bitmaps(self, pts: torch.Tensor, grid, table: torch.Tensor, nranks: int, slabs: bool):
+        """(send, bitmaps (nranks, ceil(n/64)) int64, counts): pcc_shard_route_bitmaps
+        on cell units (table = owner per cell) or slab units (table per slab)."""
+        n = pts.shape[0]
+        send = torch.empty_like(pts)
+        bm = torch.empty((nranks, (n + 63) // 64), dtype=torch.int64, device=pts.device)
+        self._ready()
+        dim = int(self.cfg_full()["sub_grid_dimension"]) if slabs else 0
+        counts = pcconv.shard_route_bitmaps(pts.data_ptr(), n, grid, dim, table.data_ptr(), nranks, send.data_ptr(),
+                                            bm.data_ptr(), self.dev)
+        return send, bm, counts
+
+    def keys_from_bitmaps(self, bm: torch.Tensor, nwords, key0, nkeys: int) -> torch.Tensor:
+        keys = torch.empty(nkeys, dtype=torch.int32, device=bm.device)
+        self._ready()
+        pcconv.shard_keys_from_bitmaps(bm.data_ptr(), nwords, key0, keys.data_ptr(), nkeys, self.dev)
+        return keys
+
     def build(self, file_points, pts: torch.Tensor, keys: torch.Tensor | None) -> dict:
         """keys None: this rank holds the whole input in key order (keys 0..n-1).
         The build reads `pts`/`keys` in place (borrowed until it returns)."""
@@ -772,6 +808,22 @@ def _exchange(comm, send: torch.Tensor, counts, rcounts, dev) -> torch.Tensor:
     return out.to(dev)
 
 
+def _exchange_many(comm, specs, dev) -> list:
+    """Several all-to-all-v exchanges (send, counts, recv counts) in one grouped
+    batch when the communicator offers it (alltoallv_many), else one by one."""
+    outs = []
+    for send, counts, rcounts in specs:
+        n = int(sum(int(v) for v in rcounts))
+        outs.append(torch.empty((n,) + tuple(send.shape[1:]), dtype=send.dtype, device=comm.device))
+    sends = [sp[0] if comm.device == dev else sp[0].to(comm.device) for sp in specs]
+    if hasattr(comm, "alltoallv_many"):
+        comm.alltoallv_many([(sd, sp[1], sp[2], o) for sd, sp, o in zip(sends, specs, outs)])
+    else:
+        for sd, sp, o in zip(sends, specs, outs):
+            comm.alltoallv_into(sd, sp[1], sp[2], o)
+    return [o if comm.device == dev else o.to(dev) for o in outs]
+
+
 def _combine(parts: list[dict]) -> dict:
     out = dict(parts[-1])
     for k in ("arrivals", "cells", "slabs"):
@@ -859,6 +911,29 @@ def shard_build(comm, ops, pts: torch.Tensor, key0: int, file_points, write: boo
         if W == 1:   # one rank owns every cell: the partition is the identity
             recv, keys = pts, None
             mark("route")
+        elif getattr(ops, "bitmap_keys", False):
+            # the points travel with one membership bit per sender point instead
+            # of a 4-B key each; every receiver rebuilds its keys in rank order
+            nd = 2 * W if nsplit else W
+            tab = torch.from_numpy((route_table(plan, W) if nsplit else owner_h).astype(np.int32)).to(dev)
+            send, bm, counts = ops.route_bitmaps(pts, grid, tab, nd, nsplit)
+            mark("route")
+            nwl = int(bm.shape[1])
+            rw = comm.alltoall_counts([nwl] * W)
+            k0 = comm.alltoall_counts([int(key0)] * W)
+            streams = [(0, [int(v) for v in counts[:W]], 0)]
+            if nsplit:
+                streams.append((sum(int(v) for v in counts[:W]), [int(v) for v in counts[W:]], W))
+            got = []
+            for off, cw, row in streams:
+                rc = comm.alltoall_counts(cw)
+                rp, rbm = _exchange_many(comm, [(send.narrow(0, off, sum(cw)), cw, rc),
+                                                (bm.narrow(0, row, W).reshape(-1), [nwl] * W, rw)], dev)
+                got.append((rp, ops.keys_from_bitmaps(rbm, rw, k0, sum(rc))))
+            recv, keys = got[0]
+            if nsplit:
+                lrecv, lkeys = got[1]
+            del send, bm
         else:
             if nsplit:
                 tab = torch.from_numpy(route_table(plan, W).astype(np.int32)).to(dev)

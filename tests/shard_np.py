@@ -143,6 +143,39 @@ class NumpyShardOps:
         keys = (key0 + order).astype(np.uint32).view(np.int32)
         return as_tensor(p[order]), torch.from_numpy(keys.copy()), [int(c) for c in counts]
 
+    # membership bitmaps instead of keys on the exchange (HipShardOps.bitmap_keys);
+    # a test may set it False to run the keyed exchange
+    bitmap_keys = True
+
+    def route_bitmaps(self, pts, grid, table, nranks, slabs):
+        """numpy restatement of pcc_shard_route_bitmaps: stable partition by
+        destination plus a (nranks, ceil(n/64)) int64 membership bitmap."""
+        p = as_points(pts)
+        unit = self._slabs(p, grid) if slabs else self._cells(p, grid)
+        own = table.cpu().numpy().astype(np.int64)[unit]
+        order = np.argsort(own, kind="stable")
+        counts = np.bincount(own, minlength=nranks)[:nranks]
+        nw = (len(p) + 63) // 64
+        bits = np.zeros((nranks, nw * 64), dtype=np.uint8)
+        bits[own, np.arange(len(p))] = 1
+        words = np.packbits(bits.reshape(nranks, nw, 64)[:, :, ::-1], axis=2, bitorder="big").view(">u8")
+        bm = words.reshape(nranks, nw).astype(np.uint64).view(np.int64)
+        return as_tensor(p[order]), torch.from_numpy(np.ascontiguousarray(bm)), [int(c) for c in counts]
+
+    def keys_from_bitmaps(self, bm, nwords, key0, nkeys):
+        w = bm.cpu().numpy().view(np.uint64)
+        out, o = [], 0
+        for nwd, k0 in zip(nwords, key0):
+            seg = w[o:o + nwd]
+            o += nwd
+            bits = np.unpackbits(seg.astype(">u8").view(np.uint8).reshape(-1, 8), axis=1, bitorder="big")[:, ::-1]
+            bits = bits.reshape(-1, 64)
+            idx = np.flatnonzero(bits.reshape(-1))
+            out.append((k0 + idx).astype(np.uint64))
+        keys = np.concatenate(out) if out else np.zeros(0, np.uint64)
+        assert len(keys) == nkeys, (len(keys), nkeys)
+        return torch.from_numpy(keys.astype(np.uint32).view(np.int32).copy())
+
     def _feed_global_batches(self, o, file_points, p, k):
         g = 0
         for fp in file_points:

@@ -82,8 +82,11 @@ def test_assign_owners_many_cells_prefix_split():
 
 
 # ------------------------------------------------------------- thread ranks
-@pytest.mark.parametrize("case,world", [("uniform", 1), ("uniform", 2), ("files", 3), ("clustered", 4)])
-def test_thread_ranks_match_oracle(tmp_path, case, world):
+# bitmap: the exchange carries membership bitmaps (keys rebuilt by the receiver),
+# else a 4-B key per routed point
+@pytest.mark.parametrize("case,world,bitmap", [("uniform", 1, True), ("uniform", 2, True), ("uniform", 2, False),
+                                               ("files", 3, True), ("files", 3, False), ("clustered", 4, True)])
+def test_thread_ranks_match_oracle(tmp_path, case, world, bitmap):
     import threading
     files = make_input(case)
     fp = [len(f) for f in files]
@@ -95,6 +98,7 @@ def test_thread_ranks_match_oracle(tmp_path, case, world):
         try:
             pts, key0 = rank_slice(files, r, world)
             ops = NumpyShardOps(out)
+            ops.bitmap_keys = bitmap
             res[r] = shard_build(ThreadComm(grp, r, torch.device("cpu")), ops, as_tensor(pts), key0, fp, write=True)
             ops.close()
         except BaseException as e:  # noqa: BLE001
@@ -323,8 +327,9 @@ def make_skewed(case):
     raise KeyError(case)
 
 
-@pytest.mark.parametrize("case,world", [("gauss", 3), ("gauss", 8), ("gauss_files", 5)])
-def test_thread_ranks_split_cells_match_oracle(tmp_path, case, world):
+@pytest.mark.parametrize("case,world,bitmap", [("gauss", 3, True), ("gauss", 3, False), ("gauss", 8, True),
+                                               ("gauss_files", 5, True)])
+def test_thread_ranks_split_cells_match_oracle(tmp_path, case, world, bitmap):
     """Heavy level-0 cells built by a leader (level 0) and the owners of their
     level-1 sub-trees (plan_split) == the sequential oracle."""
     import threading
@@ -338,6 +343,7 @@ def test_thread_ranks_split_cells_match_oracle(tmp_path, case, world):
         try:
             pts, key0 = rank_slice(files, r, world)
             ops = NumpyShardOps(out, config=SKEW_CFG)
+            ops.bitmap_keys = bitmap
             res[r] = shard_build(ThreadComm(grp, r, torch.device("cpu")), ops, as_tensor(pts), key0, fp, write=True)
             ops.close()
         except BaseException as e:  # noqa: BLE001

@@ -105,6 +105,42 @@ def test_shard_slab_histogram_and_route_match_numpy():
         assert torch.equal(keys.cpu(), k2)
 
 
+@pytest.mark.parametrize("slabs,world", [(False, 3), (False, 8), (True, 16), (True, 64)])
+def test_route_bitmaps_and_key_rebuild_match_numpy(slabs, world):
+    """pcc_shard_route_bitmaps == the numpy restatement (points, counts, every
+    bitmap word), and pcc_shard_keys_from_bitmaps rebuilds each receiver's keys
+    from the senders' rows (three senders of different sizes and key offsets)."""
+    ref = NumpyShardOps("/nonexistent")
+    senders = [synth(31 + q, 1 + (q % 2), m, lo=-2500.0, ext=5000.0) for q, m in enumerate((100_003, 64, 77_777))]
+    allp = np.concatenate(senders)
+    gmin, gmax = ref.bbox(as_tensor(allp))
+    g = pcconv.shard_grid_from_bbox(gmin, gmax)
+    nu = g.ncells * (pcconv.SHARD_LAYERS if slabs else 1)
+    table = torch.from_numpy((np.arange(nu) * 13 % world).astype(np.int32))
+    td = table.to(DEV)
+    rows, key0, k = [], [], 0
+    for sp in senders:
+        pts = as_tensor(sp).to(DEV)
+        ops = HipShardOps.__new__(HipShardOps)
+        ops.dev, ops.cfg = 0, {}
+        send, bm, counts = ops.route_bitmaps(pts, g, td, world, slabs)
+        s2, b2, c2 = ref.route_bitmaps(as_tensor(sp), g, table, world, slabs)
+        assert counts == c2
+        assert torch.equal(send.cpu(), s2)
+        assert torch.equal(bm.cpu(), b2)
+        rows.append(bm)
+        key0.append(k)
+        k += len(sp) + 1000
+    for r in (0, world - 1):
+        cat = torch.cat([b[r] for b in rows])
+        nw = [int(b.shape[1]) for b in rows]
+        nk = int(sum(bin(int(v) & (2**64 - 1)).count("1") for b in rows for v in b[r].cpu().tolist()))
+        keys = HipShardOps.keys_from_bitmaps(ops, cat, nw, key0, nk)
+        assert torch.equal(keys.cpu(), ref.keys_from_bitmaps(cat, nw, key0, nk))
+        with pytest.raises(pcconv.PccError):   # a receive count that disagrees with the bits
+            HipShardOps.keys_from_bitmaps(ops, cat, nw, key0, nk + 1)
+
+
 def test_synth_device_matches_oracle_stream():
     p = torch.empty((77_777, 4), dtype=torch.int32, device=DEV)
     pcconv.synth_device(p.data_ptr(), 123_456, 77_777, 9, 1)
