@@ -588,43 +588,42 @@ constexpr int kL0BS = PCC_L0BS, kL0IPT = PCC_L0IPT, kL0Tile = kL0BS * kL0IPT, kL
 constexpr int kHistLds = 16384;   // dense level-0 slabs counted in LDS (64 KB): 64 cells x 256 layers
 constexpr uint32_t kL0DownGrid = 512;   // persistent blocks of the fused upsweep (2 per CU)
 
-// Pass-0 upsweep from the AoS input, fused with the bounding box
-// (converter.rs:96-104, bounding-volume/src/lib.rs:38-52): per-tile histogram of
-// the low 6 bits of the layer (no bbox needed) and per-block min/max partials
-// (finished by k_bbox_final).  Grid-stride over the tiles.
-__global__ __launch_bounds__(kL0BS) void k_l0_up0_bbox(const Point* __restrict__ in, uint64_t n, L0Params P,
-                                                       uint32_t* __restrict__ counts, uint32_t ntiles, float* part,
-                                                       uint32_t* flag) {
-    constexpr int R = 1 << 6;
+// Pass 0 over the tile groups of k_l0_down6g, fused with the bounding box
+// (converter.rs:96-104, bounding-volume/src/lib.rs:38-52): per group the
+// histogram of the low 6 layer bits (a function of z alone, no bbox needed) and
+// the group's min/max partials (finished by k_bbox_final).  Nothing per tile, so
+// the loop is a plain stream with 4 loads in flight per thread.
+__global__ __launch_bounds__(kL0BS) void k_l0_up0g(const Point* __restrict__ in, uint64_t n, L0Params P, uint32_t tpg,
+                                                   uint32_t ngroups, uint32_t* __restrict__ gcnt0, float* part,
+                                                   uint32_t* flag) {
+    constexpr int R = 1 << 6, U = 4;
     __shared__ uint32_t dh[R];
     __shared__ float sb[kL0BS / 64][6];
     const float4* p4 = reinterpret_cast<const float4*>(in);
+    if (threadIdx.x < (uint32_t)R) dh[threadIdx.x] = 0;
+    __syncthreads();
     float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
     bool bad = false;
-    for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        for (int i = threadIdx.x; i < R; i += kL0BS) dh[i] = 0;
-        __syncthreads();
-        const uint64_t base = (uint64_t)tile * kL0Tile;
-        float4 v[kL0IPT];
+    const uint64_t lo = (uint64_t)blockIdx.x * tpg * kL0Tile;
+    const uint64_t hi = min((uint64_t)(blockIdx.x + 1) * tpg * kL0Tile, n);
+    for (uint64_t i0 = lo + threadIdx.x; i0 < hi; i0 += (uint64_t)U * kL0BS) {
+        float4 v[U];
 #pragma unroll
-        for (int r = 0; r < kL0IPT; r++) {
-            const uint64_t i = base + (uint64_t)r * kL0BS + threadIdx.x;
-            if (i < n) v[r] = p4[i];
-        }
+        for (int u = 0; u < U; u++) v[u] = p4[min(i0 + (uint64_t)u * kL0BS, hi - 1)];
 #pragma unroll
-        for (int r = 0; r < kL0IPT; r++) {
-            const uint64_t i = base + (uint64_t)r * kL0BS + threadIdx.x;
-            if (i < n) {
-                bad |= !(isfinite(v[r].x) && isfinite(v[r].y) && isfinite(v[r].z));
-                mn[0] = fminf(mn[0], v[r].x); mn[1] = fminf(mn[1], v[r].y); mn[2] = fminf(mn[2], v[r].z);
-                mx[0] = fmaxf(mx[0], v[r].x); mx[1] = fmaxf(mx[1], v[r].y); mx[2] = fmaxf(mx[2], v[r].z);
+        for (int u = 0; u < U; u++) {
+            const bool valid = i0 + (uint64_t)u * kL0BS < hi;
+            uint32_t d6 = 0;
+            if (valid) {
+                bad |= !(isfinite(v[u].x) && isfinite(v[u].y) && isfinite(v[u].z));
+                mn[0] = fminf(mn[0], v[u].x); mn[1] = fminf(mn[1], v[u].y); mn[2] = fminf(mn[2], v[u].z);
+                mx[0] = fmaxf(mx[0], v[u].x); mx[1] = fmaxf(mx[1], v[u].y); mx[2] = fmaxf(mx[2], v[u].z);
                 int32_t iz;
-                const int64_t ll = l0_layer(P, v[r].z, iz);
-                atomicAdd(&dh[(uint32_t)ll & (R - 1)], 1u);
+                d6 = (uint32_t)l0_layer(P, v[u].z, iz) & (R - 1);
             }
+            const uint64_t peers = wave_peers<6>(d6, valid);   // one LDS add per distinct digit of the wave
+            if (valid && mask_rank(peers) == 0) atomicAdd(&dh[d6], (uint32_t)__popcll(peers));
         }
-        __syncthreads();
-        for (int d = threadIdx.x; d < R; d += kL0BS) counts[(uint64_t)d * ntiles + tile] = dh[d];
     }
     for (int d = 32; d > 0; d >>= 1)
         for (int a = 0; a < 3; a++) {
@@ -641,6 +640,7 @@ __global__ __launch_bounds__(kL0BS) void k_l0_up0_bbox(const Point* __restrict__
         for (int q = 1; q < kL0BS / 64; q++) r = threadIdx.x < 3 ? fminf(r, sb[q][threadIdx.x]) : fmaxf(r, sb[q][threadIdx.x]);
         part[blockIdx.x * 6 + threadIdx.x] = r;
     }
+    if (threadIdx.x < (uint32_t)R) gcnt0[(uint64_t)threadIdx.x * ngroups + blockIdx.x] = dh[threadIdx.x];
 }
 
 // Pass-1 upsweep from the arena: per-tile digit histogram + the full dense-slab
@@ -995,8 +995,8 @@ template <int R5, bool KEYS>
 __global__ __launch_bounds__(kL0BS, 8) void k_l0_down6g(const Point* __restrict__ in, const uint32_t* __restrict__ keys,
                                                         Arena O, uint64_t n, L0Params P,
                                                         const uint32_t* __restrict__ offs, uint32_t ntiles, uint32_t tpg,
-                                                        uint32_t ngroups, uint32_t* __restrict__ gcnt, Arena dummy,
-                                                        Counters* ctr) {
+                                                        uint32_t ngroups, uint32_t* __restrict__ gcnt, int pairs,
+                                                        Arena dummy, Counters* ctr) {
     constexpr int R = 64;
     using KT = typename std::conditional<KEYS, uint32_t, uint16_t>::type;
     __shared__ float4 sp[kL0Tile];
@@ -1016,9 +1016,9 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_down6g(const Point* __restrict_
     float4 v[kL0IPT];
     uint32_t kk[kL0IPT];
     // wave 0, lane d: output position of digit d for the current tile (the
-    // group's tiles are consecutive: the upsweep's scanned count of the first
-    // tile, then + each tile's total)
-    uint32_t goffr = w == 0 ? offs[(uint64_t)lane * ntiles + t0] : 0u;
+    // group's tiles are consecutive: the scanned pass-0 group count, then + each
+    // tile's total)
+    uint32_t goffr = w == 0 ? offs[(uint64_t)lane * ngroups + g] : 0u;
     gofs[lane] = goffr;   // (an LDS write: the load is complete before the loop)
     // every load and store below is issued unconditionally (indices clamped to
     // the tile), so the number of memory ops per tile is static and the waits
@@ -1045,11 +1045,14 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_down6g(const Point* __restrict_
             const uint64_t i = base + (uint64_t)r * kL0BS + tid;
             const bool valid = i < n;
             uint32_t d6 = 0;
-            if (valid) {
+            if (valid && pairs) {
                 int64_t d = l0_dense<0>(P, v[r].x, v[r].y, v[r].z);
                 if (d < 0) { err = ERR_L0_RANGE; d = 0; }
                 d6 = (uint32_t)d & (R - 1);
                 atomicAdd(&h[d6 * R5 + (((uint32_t)d >> 6) & (R5 - 1))], 1u);
+            } else if (valid) {   // the digit alone (a later pass checks the grid)
+                int32_t iz;
+                d6 = (uint32_t)l0_layer(P, v[r].z, iz) & (R - 1);
             }
             const uint64_t same = wave_peers<6>(d6, valid);
             const uint32_t rw = (uint32_t)__popcll(same & lt);
@@ -1091,19 +1094,20 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_down6g(const Point* __restrict_
         }
     }
     lds_barrier();
-    for (int i = tid; i < R * R5; i += kL0BS)
-        gcnt[((uint64_t)(i / R5) * ngroups + g) * R5 + (i % R5)] = h[i];
+    if (pairs)
+        for (int i = tid; i < R * R5; i += kL0BS)
+            gcnt[((uint64_t)(i / R5) * ngroups + g) * R5 + (i % R5)] = h[i];
     if (err) set_err(ctr, err);
 }
 
 // start of segment (d6, g) of the pass-1 output, g = 0..ngroups (the end)
-__global__ void k_l0_gstarts(const uint32_t* __restrict__ offs, uint32_t ntiles, uint32_t tpg, uint32_t ngroups,
-                             uint64_t n, uint32_t* __restrict__ starts) {
+__global__ void k_l0_gstarts(const uint32_t* __restrict__ offs, uint32_t ngroups, uint64_t n,
+                             uint32_t* __restrict__ starts) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= 64 * (ngroups + 1)) return;
     const uint32_t d6 = i / (ngroups + 1), g = i % (ngroups + 1);
-    const uint64_t idx = (uint64_t)d6 * ntiles + min(g * tpg, ntiles);
-    starts[i] = idx < 64ull * ntiles ? offs[idx] : (uint32_t)n;
+    const uint64_t idx = (uint64_t)d6 * ngroups + g;   // (d6, ngroups) = (d6 + 1, 0)
+    starts[i] = idx < 64ull * ngroups ? offs[idx] : (uint32_t)n;
 }
 
 // per (d6, d5): exclusive prefix of the group counts (in place) and the dense
@@ -3498,15 +3502,20 @@ int Engine::level0_bin() {
     P.hkeys = nullptr;
     P.hcid = nullptr;
     P.ckeys = nullptr;
-    // pass 0 of the LSD sort (low 6 bits of the layer: no grid needed) fused
-    // with the bounding box
+    // Pass 0 (low 6 bits of the layer: no grid needed) fused with the bounding
+    // box, per group of consecutive tiles: k_l0_down6g's blocks walk the same
+    // groups with running offsets, so no per-tile counts exist.
     const uint32_t ntiles = (uint32_t)((nsrc_ + kL0Tile - 1) / kL0Tile);
-    uint32_t* counts0 = static_cast<uint32_t*>(dev_->get(((uint64_t)ntiles << 6) * 4 + 64));
+    const char* gq = getenv("PCC_L0_GROUPS");
+    uint32_t ngroups = std::max<uint32_t>(1, std::min<uint32_t>(gq ? std::max<uint32_t>(1, (uint32_t)strtoul(gq, nullptr, 10))
+                                                                   : kL0Groups, std::min<uint32_t>(ntiles, kBBoxBlocks)));
+    const uint32_t tpg = std::max<uint32_t>(1, (ntiles + ngroups - 1) / ngroups);
+    ngroups = std::max<uint32_t>(1, (ntiles + tpg - 1) / tpg);
+    uint32_t* gcnt0 = static_cast<uint32_t*>(dev_->get(64ull * ngroups * 4 + 64));
     {
         HIP_CHECK(hipMemsetAsync(dev_->bbox_flag, 0, 4, stream_));
-        const uint32_t nbb = std::min<uint32_t>(ntiles, kBBoxBlocks);
-        k_l0_up0_bbox<<<nbb, kL0BS, 0, stream_>>>(src_, nsrc_, P, counts0, ntiles, dev_->bbox_part, dev_->bbox_flag);
-        k_bbox_final<<<1, 256, 0, stream_>>>(dev_->bbox_part, nbb);
+        k_l0_up0g<<<ngroups, kL0BS, 0, stream_>>>(src_, nsrc_, P, tpg, ngroups, gcnt0, dev_->bbox_part, dev_->bbox_flag);
+        k_bbox_final<<<1, 256, 0, stream_>>>(dev_->bbox_part, ngroups);
         HIP_CHECK(hipGetLastError());
         float bb[6];
         uint32_t bad = 0;
@@ -3569,8 +3578,9 @@ int Engine::level0_bin() {
     const int rem = kL0LayerBits - 6 + cbits;
     const int passes = std::max(1, (rem + 7) / 8);
     const int per = std::max(1, (rem + passes - 1) / passes);
-    // one upsweep (k_l0_down6g / k_l0_down5g) when the rest of the dense id fits one 5-bit pass
-    // (with external keys staged beside the points the pair table must stay <= 16 wide)
+    // pass 2 without an upsweep (k_l0_down5g) when the rest of the dense id fits
+    // one 5-bit pass: pass 1 then counts the (d6, d5) pairs per group (with
+    // external keys staged beside the points the pair table must stay <= 16 wide)
     const bool l0keys = src_keys_ != nullptr;
     bool g1up = !P.hashed && passes == 1 && per <= (l0keys ? 4 : 5) && ntiles > 0 &&
                 getenv("PCC_L0_TWO_UPSWEEPS") == nullptr;
@@ -3587,40 +3597,36 @@ int Engine::level0_bin() {
         HIP_CHECK(hipMemsetAsync(H1, 0, (uint64_t)D1 * 4, stream_));
     }
     // LSD passes over the dense slab id (key recomputed from positions every
-    // pass): pass 0 on the low 6 layer bits (upsweep done above), then the rest
-    // of the layer and the cell bits in passes of at most 8 bits; the first of
-    // those also builds the dense histogram.
+    // pass): pass 1 on the low 6 layer bits (k_l0_down6g, offsets from pass 0),
+    // then either the one-upsweep pass 2 (k_l0_down5g) or the rest of the layer
+    // and the cell bits in passes of at most 8 bits, the first of which also
+    // builds the dense histogram.
     Arena A0 = dev_->ar[0], A1 = dev_->ar[1];
     // the final pass must land in arena 0
     Arena dst = (passes % 2) ? A1 : A0;
-    scan_excl_u32(counts0, counts0, (uint32_t)((uint64_t)ntiles << 6), nullptr, dev_->scan, stream_);
-    uint32_t ngroups = 0, *gcnt = nullptr, *starts = nullptr;
-    Arena l0dummy{nullptr, nullptr};
+    scan_excl_u32(gcnt0, gcnt0, 64u * ngroups, nullptr, dev_->scan, stream_);
+    uint32_t* gcnt = g1up ? static_cast<uint32_t*>(dev_->get(64ull * ngroups * r5 * 4)) : nullptr;
+    Arena l0dummy{static_cast<float4*>(dev_->get(256ull * kL0BS * kL0IPT * 16)),
+                  static_cast<uint32_t*>(dev_->get(256ull * kL0BS * kL0IPT * 4))};
+    if (ntiles) {
+        if (l0keys)
+            k_l0_down6g<16, true><<<ngroups, kL0BS, 0, stream_>>>(src_, src_keys_, dst, nsrc_, P, gcnt0, ntiles, tpg,
+                                                                   ngroups, gcnt, g1up ? 1 : 0, l0dummy, dev_->ctr);
+        else
+            k_l0_down6g<32, false><<<ngroups, kL0BS, 0, stream_>>>(src_, nullptr, dst, nsrc_, P, gcnt0, ntiles, tpg,
+                                                                    ngroups, gcnt, g1up ? 1 : 0, l0dummy, dev_->ctr);
+    }
+    uint32_t* starts = nullptr;
     L0Unit* dunits = nullptr;
     uint32_t nunits = 0;
     if (g1up) {
-        const char* gq = getenv("PCC_L0_GROUPS");
-        ngroups = std::min<uint32_t>(gq ? std::max<uint32_t>(1, (uint32_t)strtoul(gq, nullptr, 10)) : kL0Groups, ntiles);
-        const uint32_t tpg = (ntiles + ngroups - 1) / ngroups;
-        ngroups = (ntiles + tpg - 1) / tpg;
-        gcnt = static_cast<uint32_t*>(dev_->get(64ull * ngroups * r5 * 4));
-        l0dummy.p = static_cast<float4*>(dev_->get(256ull * kL0BS * kL0IPT * 16));
-        l0dummy.k = static_cast<uint32_t*>(dev_->get(256ull * kL0BS * kL0IPT * 4));
         starts = static_cast<uint32_t*>(dev_->get(64ull * (ngroups + 1) * 4));
-        if (l0keys) {
-            k_l0_down6g<16, true><<<ngroups, kL0BS, 0, stream_>>>(src_, src_keys_, dst, nsrc_, P, counts0, ntiles, tpg,
-                                                                   ngroups, gcnt, l0dummy, dev_->ctr);
-            k_l0_gprefix<16><<<64, 1024, 0, stream_>>>(gcnt, ngroups, (uint32_t)D, hist, dev_->ctr);
-        } else {
-            k_l0_down6g<32, false><<<ngroups, kL0BS, 0, stream_>>>(src_, nullptr, dst, nsrc_, P, counts0, ntiles, tpg,
-                                                                    ngroups, gcnt, l0dummy, dev_->ctr);
-            k_l0_gprefix<32><<<64, 1024, 0, stream_>>>(gcnt, ngroups, (uint32_t)D, hist, dev_->ctr);
-        }
-        k_l0_gstarts<<<grid_for(64ull * (ngroups + 1), 256, 1u << 30), 256, 0, stream_>>>(counts0, ntiles, tpg, ngroups,
-                                                                                          nsrc_, starts);
+        if (l0keys) k_l0_gprefix<16><<<64, 1024, 0, stream_>>>(gcnt, ngroups, (uint32_t)D, hist, dev_->ctr);
+        else k_l0_gprefix<32><<<64, 1024, 0, stream_>>>(gcnt, ngroups, (uint32_t)D, hist, dev_->ctr);
+        k_l0_gstarts<<<grid_for(64ull * (ngroups + 1), 256, 1u << 30), 256, 0, stream_>>>(gcnt0, ngroups, nsrc_, starts);
         HIP_CHECK(hipGetLastError());
         // pass-2 units: runs of consecutive segments of one d6 bucket, about
-        // nsrc / 2048 points each (a segment is never split)
+        // nsrc / 8192 points each (a segment is never split), in bucket order
         std::vector<uint32_t> st(64ull * (ngroups + 1));
         HIP_CHECK(hipMemcpyAsync(st.data(), starts, st.size() * 4, hipMemcpyDeviceToHost, stream_));
         HIP_CHECK(hipStreamSynchronize(stream_));
@@ -3645,14 +3651,9 @@ int Engine::level0_bin() {
             }
             if (acc) units.push_back(L0Unit{d6, g0, ngroups, 0});
         }
-        if (getenv("PCC_L0_UNIT_SORT")) std::stable_sort(units.begin(), units.end(), [&](const L0Unit& x, const L0Unit& y) {
-            const uint32_t* rx = st.data() + (uint64_t)x.d6 * (ngroups + 1);
-            const uint32_t* ry = st.data() + (uint64_t)y.d6 * (ngroups + 1);
-            return rx[x.g1] - rx[x.g0] > ry[y.g1] - ry[y.g0];
-        });
         if (maxseg > 16 * target) {
             // a few segments hold most points (the layers' low bits are skewed):
-            // units cannot balance, take the two-upsweep pass below
+            // units cannot balance, take the upsweep pass below
             g1up = false;
             HIP_CHECK(hipMemsetAsync(hist, 0, D * 4, stream_));
         } else {
@@ -3661,9 +3662,6 @@ int Engine::level0_bin() {
             if (nunits)
                 HIP_CHECK(hipMemcpyAsync(dunits, units.data(), nunits * sizeof(L0Unit), hipMemcpyHostToDevice, stream_));
         }
-    } else {
-        k_l0_down<6, true, false><<<ntiles, kL0BS, 0, stream_>>>(src_, src_keys_, A1, dst, nsrc_, P, 0, counts0, ntiles,
-                                                                  nullptr, 0);
     }
     HIP_CHECK(hipGetLastError());
     Arena src = dst;
