@@ -81,6 +81,35 @@ def test_clustered_1m():
     assert st["levels"] >= 3
 
 
+def _thin_layer_points(n, seed):
+    """x, y uniform over a 2 x 2 cell footprint, z inside one level-0 hex layer
+    (trunc(z / r0) constant, r0 = 1000/96/2): every point has the same low 6
+    layer bits, so one pass-1 bucket holds the whole input."""
+    p = synth(seed, 0, n, lo=-1000.0, ext=2000.0)
+    p["z"] = (np.float32(100.5) + (p["z"] - np.float32(-1000.0)) * np.float32(3.0 / 2000.0)).astype(np.float32)
+    return p
+
+
+@pytest.mark.parametrize("env", [{}, {"PCC_L0_GROUPS": "1"}, {"PCC_L0_TWO_UPSWEEPS": "1"}],
+                         ids=["units", "one-group-fallback", "two-upsweeps"])
+def test_level0_paths_thin_layer(env):
+    """Level-0 binning paths on input whose points all share one low-6-bit layer
+    digit: the one-upsweep path (pass-2 units cut from one bucket); one tile group
+    (a segment far above the unit target: the run-time fallback to the upsweep
+    pass); and the upsweep pass forced (PCC_L0_TWO_UPSWEEPS)."""
+    pts = _thin_layer_points(1_000_003, 41)
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        _check([pts[:400_000], pts[400_000:]], fast=True)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
 def test_config2_uniform_10m_synthetic_on_device():
     """Config 2: 10M uniform points generated in HBM; the oracle generates the same
     points on the host with its own copy of the generator."""
