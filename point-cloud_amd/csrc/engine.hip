@@ -110,6 +110,8 @@ struct Engine::Dev {
     Counters* ctr = nullptr;
     float* bbox_part = nullptr;     // per-block min/max partials
     uint32_t* bbox_flag = nullptr;
+    uint32_t* hst = nullptr;        // pinned host staging of the level-0 segment starts
+    uint64_t hst_cap = 0;
     uint32_t* files = nullptr;      // per file: start_lo, start_hi, eb0, batch
     ScanTemp scan;
     uint64_t cap = 0;
@@ -3106,6 +3108,7 @@ void Engine::free_all() {
         (void)hipFree(dev_->ctr);
         (void)hipFree(dev_->bbox_part);
         (void)hipFree(dev_->bbox_flag);
+        if (dev_->hst) (void)hipHostFree(dev_->hst);
         (void)hipFree(dev_->scan.bsums);
         for (auto& c : dev_->chunks) (void)hipFree(c.first);
         delete dev_;
@@ -3625,73 +3628,52 @@ int Engine::level0_bin() {
         else k_l0_gprefix<32><<<64, 1024, 0, stream_>>>(gcnt, ngroups, (uint32_t)D, hist, dev_->ctr);
         k_l0_gstarts<<<grid_for(64ull * (ngroups + 1), 256, 1u << 30), 256, 0, stream_>>>(gcnt0, ngroups, nsrc_, starts);
         HIP_CHECK(hipGetLastError());
-        // pass-2 units: runs of consecutive segments of one d6 bucket, about
-        // nsrc / 8192 points each (a segment is never split), in bucket order
-        std::vector<uint32_t> st(64ull * (ngroups + 1));
-        HIP_CHECK(hipMemcpyAsync(st.data(), starts, st.size() * 4, hipMemcpyDeviceToHost, stream_));
-        HIP_CHECK(hipStreamSynchronize(stream_));
-        const char* udiv = getenv("PCC_L0_UNIT_DIV");
-        const uint64_t ud = udiv ? std::max<uint64_t>(1, strtoull(udiv, nullptr, 10)) : 8192;
-        const uint64_t target = std::max<uint64_t>(nsrc_ / ud, 4ull * kL0Tile);
-        std::vector<L0Unit> units;
-        uint64_t maxseg = 0;
-        for (uint32_t d6 = 0; d6 < 64; d6++) {
-            const uint32_t* row = st.data() + (uint64_t)d6 * (ngroups + 1);
-            uint32_t g0 = 0;
-            uint64_t acc = 0;
-            for (uint32_t gg = 0; gg < ngroups; gg++) {
-                const uint64_t sz = row[gg + 1] - row[gg];
-                maxseg = std::max(maxseg, sz);
-                if (acc && acc + sz > target) {
-                    units.push_back(L0Unit{d6, g0, gg, 0});
-                    g0 = gg;
-                    acc = 0;
-                }
-                acc += sz;
-            }
-            if (acc) units.push_back(L0Unit{d6, g0, ngroups, 0});
+        // the segment starts go to pinned host memory now; the unit plan is made
+        // after the one host sync of the level (below)
+        const uint64_t nst = 64ull * (ngroups + 1);
+        if (dev_->hst_cap < nst) {
+            if (dev_->hst) (void)hipHostFree(dev_->hst);
+            HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&dev_->hst), nst * 4, hipHostMallocDefault));
+            dev_->hst_cap = nst;
         }
-        if (maxseg > 16 * target) {
-            // a few segments hold most points (the layers' low bits are skewed):
-            // units cannot balance, take the upsweep pass below
-            g1up = false;
-            HIP_CHECK(hipMemsetAsync(hist, 0, D * 4, stream_));
-        } else {
-            nunits = (uint32_t)units.size();
-            dunits = static_cast<L0Unit*>(dev_->get(std::max<uint64_t>(nunits, 1) * sizeof(L0Unit)));
-            if (nunits)
-                HIP_CHECK(hipMemcpyAsync(dunits, units.data(), nunits * sizeof(L0Unit), hipMemcpyHostToDevice, stream_));
-        }
+        HIP_CHECK(hipMemcpyAsync(dev_->hst, starts, nst * 4, hipMemcpyDeviceToHost, stream_));
     }
     HIP_CHECK(hipGetLastError());
     Arena src = dst;
     dst = (dst.p == A0.p) ? A1 : A0;
-    uint32_t* counts = g1up ? nullptr : static_cast<uint32_t*>(dev_->get(((uint64_t)ntiles << per) * 4 + 64));
-    for (int p = 0, shift = 6; p < passes && !g1up; p++, shift += per) {
-        switch (per) {
-            case 1: l0_pass<1>(p, passes, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, Q, H1, D1, dev_->scan, stream_); break;
-            case 2: l0_pass<2>(p, passes, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, Q, H1, D1, dev_->scan, stream_); break;
-            case 3: l0_pass<3>(p, passes, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, Q, H1, D1, dev_->scan, stream_); break;
-            case 4: l0_pass<4>(p, passes, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, Q, H1, D1, dev_->scan, stream_); break;
-            case 5: l0_pass<5>(p, passes, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, Q, H1, D1, dev_->scan, stream_); break;
-            case 6: l0_pass<6>(p, passes, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, Q, H1, D1, dev_->scan, stream_); break;
-            case 7: l0_pass<7>(p, passes, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, Q, H1, D1, dev_->scan, stream_); break;
-            default: l0_pass<8>(p, passes, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, Q, H1, D1, dev_->scan, stream_); break;
-        }
-        src = dst;
-        dst = (dst.p == A0.p) ? A1 : A0;
-    }
-    // slab / cell tables from the dense histogram
-    k_l0_flags<<<grid_for(std::max<uint64_t>(D, G), 256, 1u << 30), 256, 0, stream_>>>(hist, (uint32_t)D, P.nl, sflag, cflag, (uint32_t)G);
-    scan_excl_u32(hist, cnt_scan, (uint32_t)D, d_tot + 0, dev_->scan, stream_);
-    scan_excl_u32(sflag, sflag, (uint32_t)D, d_tot + 1, dev_->scan, stream_);
-    scan_excl_u32(cflag, cscan, (uint32_t)G, d_tot + 2, dev_->scan, stream_);
+    const Arena p1out = src, p2dst = dst;
     uint32_t tots[3];
     Counters hc;
-    HIP_CHECK(hipMemcpyAsync(tots, d_tot, 12, hipMemcpyDeviceToHost, stream_));
-    HIP_CHECK(hipMemcpyAsync(&hc, dev_->ctr, sizeof hc, hipMemcpyDeviceToHost, stream_));
-    HIP_CHECK(hipStreamSynchronize(stream_));
-    if (hc.err) return fail(-34, "level-0 binning: point outside the bounding grid (internal error)");
+    // the upsweep passes (when pass 2 is not the one-upsweep kernel), tables, the
+    // level's host sync
+    {
+        src = p1out;
+        dst = p2dst;
+        uint32_t* counts = g1up ? nullptr : static_cast<uint32_t*>(dev_->get(((uint64_t)ntiles << per) * 4 + 64));
+        for (int p = 0, shift = 6; p < passes && !g1up; p++, shift += per) {
+            switch (per) {
+                case 1: l0_pass<1>(p, passes, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, Q, H1, D1, dev_->scan, stream_); break;
+                case 2: l0_pass<2>(p, passes, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, Q, H1, D1, dev_->scan, stream_); break;
+                case 3: l0_pass<3>(p, passes, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, Q, H1, D1, dev_->scan, stream_); break;
+                case 4: l0_pass<4>(p, passes, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, Q, H1, D1, dev_->scan, stream_); break;
+                case 5: l0_pass<5>(p, passes, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, Q, H1, D1, dev_->scan, stream_); break;
+                case 6: l0_pass<6>(p, passes, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, Q, H1, D1, dev_->scan, stream_); break;
+                case 7: l0_pass<7>(p, passes, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, Q, H1, D1, dev_->scan, stream_); break;
+                default: l0_pass<8>(p, passes, src, dst, nsrc_, P, shift, counts, ntiles, hist, (uint32_t)D, dev_->ctr, Q, H1, D1, dev_->scan, stream_); break;
+            }
+            src = dst;
+            dst = (dst.p == A0.p) ? A1 : A0;
+        }
+        // slab / cell tables from the dense histogram
+        k_l0_flags<<<grid_for(std::max<uint64_t>(D, G), 256, 1u << 30), 256, 0, stream_>>>(hist, (uint32_t)D, P.nl, sflag, cflag, (uint32_t)G);
+        scan_excl_u32(hist, cnt_scan, (uint32_t)D, d_tot + 0, dev_->scan, stream_);
+        scan_excl_u32(sflag, sflag, (uint32_t)D, d_tot + 1, dev_->scan, stream_);
+        scan_excl_u32(cflag, cscan, (uint32_t)G, d_tot + 2, dev_->scan, stream_);
+        HIP_CHECK(hipMemcpyAsync(tots, d_tot, 12, hipMemcpyDeviceToHost, stream_));
+        HIP_CHECK(hipMemcpyAsync(&hc, dev_->ctr, sizeof hc, hipMemcpyDeviceToHost, stream_));
+        HIP_CHECK(hipStreamSynchronize(stream_));
+        if (hc.err) return fail(-34, "level-0 binning: point outside the bounding grid (internal error)");
+    }
     if (tots[0] != nsrc_) return fail(-5, "level-0 histogram mismatch");
     Level* L = new Level();
     L->dev = dev_;
@@ -3716,6 +3698,35 @@ int Engine::level0_bin() {
         L->slab_cell, L->slab_layer, L->slab_off, L->slab_n);
     k_set_u32<<<1, 1, 0, stream_>>>(L->cell_slab0 + L->ncells, L->nslabs);
     if (g1up) {   // pass 2 into arena 0, with the capacities
+        // Units: runs of consecutive segments of one d6 bucket, about nsrc / 8192
+        // points each, in bucket order (a segment is never split; with the default
+        // groups a segment is at most 4 x the target).  Planned on the host while
+        // the table kernels above run.
+        const uint32_t* st = dev_->hst;
+        const char* udiv = getenv("PCC_L0_UNIT_DIV");
+        const uint64_t ud = udiv ? std::max<uint64_t>(1, strtoull(udiv, nullptr, 10)) : 8192;
+        const uint64_t target = std::max<uint64_t>(nsrc_ / ud, 4ull * kL0Tile);
+        std::vector<L0Unit> units;
+        units.reserve(ud + 128);
+        for (uint32_t d6 = 0; d6 < 64; d6++) {
+            const uint32_t* row = st + (uint64_t)d6 * (ngroups + 1);
+            uint32_t g0 = 0;
+            uint64_t acc = 0;
+            for (uint32_t gg = 0; gg < ngroups; gg++) {
+                const uint64_t sz = row[gg + 1] - row[gg];
+                if (acc && acc + sz > target) {
+                    units.push_back(L0Unit{d6, g0, gg, 0});
+                    g0 = gg;
+                    acc = 0;
+                }
+                acc += sz;
+            }
+            if (acc) units.push_back(L0Unit{d6, g0, ngroups, 0});
+        }
+        nunits = (uint32_t)units.size();
+        dunits = static_cast<L0Unit*>(dev_->get(std::max<uint64_t>(nunits, 1) * sizeof(L0Unit)));
+        if (nunits)
+            HIP_CHECK(hipMemcpyAsync(dunits, units.data(), nunits * sizeof(L0Unit), hipMemcpyHostToDevice, stream_));
         HIP_CHECK(hipMemsetAsync(L->dcap, 0, (uint64_t)L->nslabs * kDests * 4, stream_));
         if (nunits && r5 == 16)
             k_l0_down5g<16><<<nunits, kL0BS, 0, stream_>>>(src, dst, P, dunits, starts, ngroups, gcnt, cnt_scan, sflag,

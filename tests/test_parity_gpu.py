@@ -91,12 +91,12 @@ def _thin_layer_points(n, seed):
 
 
 @pytest.mark.parametrize("env", [{}, {"PCC_L0_GROUPS": "1"}, {"PCC_L0_TWO_UPSWEEPS": "1"}],
-                         ids=["units", "one-group-fallback", "two-upsweeps"])
+                         ids=["units", "one-group", "two-upsweeps"])
 def test_level0_paths_thin_layer(env):
     """Level-0 binning paths on input whose points all share one low-6-bit layer
     digit: the one-upsweep path (pass-2 units cut from one bucket); one tile group
-    (a segment far above the unit target: the run-time fallback to the upsweep
-    pass); and the upsweep pass forced (PCC_L0_TWO_UPSWEEPS)."""
+    (one segment holds the whole input: a single pass-2 unit); and the upsweep
+    passes forced (PCC_L0_TWO_UPSWEEPS)."""
     pts = _thin_layer_points(1_000_003, 41)
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
