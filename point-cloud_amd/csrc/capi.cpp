@@ -77,6 +77,10 @@ struct pcc_converter {
     bool prior_on_disk = false;         // they are the files in out_dir (nothing to rewrite)
     std::vector<uint8_t> prior_touched; // per prior cell, after a build
     uint64_t untouched_grid = 0, untouched_kept = 0, untouched_cells = 0;
+    // the merge state's host arrays (tens of GB at config 5), kept until the
+    // converter closes: unmapping them takes about a second and blocks the
+    // process's other memory mappings meanwhile
+    std::unique_ptr<PriorState> prior_host;
 };
 
 namespace {
@@ -199,13 +203,23 @@ static int open_impl(const char* out_dir, const pcc_options* opt, const std::vec
     c->eng = std::make_unique<Engine>(c->meta.config, c->opt.device);
     if (c->merge) {   // converter.rs:187-207: existing cells are the starting state
         std::string err;
+        const auto t0 = std::chrono::steady_clock::now();
         int rc = read_cloud(c->out_dir, 31, c->prior_cells, err, subtrees);
         if (rc) return set_err(rc, err);
+        const auto t1 = std::chrono::steady_clock::now();
         PriorState ps;
         rc = prior_from_cells(c->prior_cells, c->meta.config, ps, err);
         if (rc) return set_err(rc, err);
+        const auto t2 = std::chrono::steady_clock::now();
         c->eng->set_prior(ps);
         c->prior_on_disk = true;
+        c->prior_host = std::make_unique<PriorState>(std::move(ps));
+        if (getenv("PCC_VERBOSE")) {
+            const auto t3 = std::chrono::steady_clock::now();
+            auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+            fprintf(stderr, "[pcc] open: %zu cells read %.1f ms, merge state %.1f ms, upload %.1f ms\n",
+                    c->prior_cells.size(), ms(t0, t1), ms(t1, t2), ms(t2, t3));
+        }
     }
     *out = c.release();
     return 0;

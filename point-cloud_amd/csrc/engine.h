@@ -9,7 +9,10 @@
 #pragma once
 #include <stdint.h>
 #include <stddef.h>
+#include <memory>
 #include <string>
+#include <type_traits>
+#include <utility>
 #include <vector>
 
 #include <hip/hip_runtime.h>
@@ -86,11 +89,25 @@ struct PriorLevel {
     std::vector<int32_t> slab_layer;
     std::vector<PriorSlabRec> slabs;
 };
+// std::allocator that default-initialises: large host arrays that are filled
+// right after their allocation (by several threads) are not zero-filled first
+template <class T>
+struct DefaultInitAlloc : std::allocator<T> {
+    template <class U> struct rebind { using other = DefaultInitAlloc<U>; };
+    DefaultInitAlloc() = default;
+    template <class U> DefaultInitAlloc(const DefaultInitAlloc<U>&) noexcept {}
+    template <class U> void construct(U* p) noexcept(std::is_nothrow_default_constructible<U>::value) {
+        ::new (static_cast<void*>(p)) U;
+    }
+    template <class U, class... A> void construct(U* p, A&&... a) { ::new (static_cast<void*>(p)) U(std::forward<A>(a)...); }
+};
+template <class T> using HostVec = std::vector<T, DefaultInitAlloc<T>>;
+
 struct PriorState {
     uint64_t nseeds = 0;                               // S: every existing point
-    std::vector<Point> seeds0;                         // level-0 seeds, key order (keys 0 .. seeds0.size()-1)
-    std::vector<Point> inj;                            // levels >= 1, grouped by level, cell, slab: grid then kept
-    std::vector<uint32_t> inj_keys;
+    HostVec<Point> seeds0;                             // level-0 seeds, key order (keys 0 .. seeds0.size()-1)
+    HostVec<Point> inj;                                // levels >= 1, grouped by level, cell, slab: grid then kept
+    HostVec<uint32_t> inj_keys;
     std::vector<uint64_t> forced_lo;                   // per prior level
     std::vector<PriorLevel> levels;
 };

@@ -3292,8 +3292,8 @@ void Engine::add_keyed_device(const Point* dpts, const uint32_t* dkeys, uint64_t
     comb_ok_ = false;
 }
 
-template <class T>
-static T* upload(const std::vector<T>& v) {
+template <class T, class A>
+static T* upload(const std::vector<T, A>& v) {
     T* d = nullptr;
     HIP_CHECK(hipMalloc(&d, std::max<size_t>(v.size(), 1) * sizeof(T)));
     if (!v.empty()) HIP_CHECK(hipMemcpy(d, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));

@@ -2,7 +2,9 @@
 #include "format.h"
 
 #include <dirent.h>
+#include <fcntl.h>
 #include <sys/stat.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <array>
@@ -388,43 +390,57 @@ int write_metadata(const std::string& dir, const Metadata& meta, std::string& er
 
 // ------------------------------------------------------------------ existing cloud
 bool read_cell_file(const std::string& path, CellFile& out, std::string& err) {
-    FILE* f = fopen(path.c_str(), "rb");
-    if (!f) { err = "cannot open " + path; return false; }
-    std::string b;
-    char tmp[1 << 16];
-    size_t r;
-    while ((r = fread(tmp, 1, sizeof tmp, f)) > 0) b.append(tmp, r);
-    fclose(f);
-    auto bad = [&](const char* what) { err = path + ": " + what; return false; };
-    if (b.size() < 49) return bad("truncated header");
-    const char* p = b.data();
-    auto u32 = [&](size_t o) { uint32_t v; memcpy(&v, p + o, 4); return v; };
-    auto i32 = [&](size_t o) { int32_t v; memcpy(&v, p + o, 4); return v; };
-    out.h = u32(0);
-    out.idx[0] = i32(4); out.idx[1] = i32(8); out.idx[2] = i32(12);
-    out.total = u32(16); out.number = u32(20); out.overflow = u32(24);
-    size_t off = 48;
-    if (off + 16ull * out.number + 1 > b.size()) return bad("truncated grid");
+    // header, grid points straight into the cell's array, then the overflow
+    // entries (cell.rs:183-229): no zero fill, no intermediate copy
+    const int fd = open(path.c_str(), O_RDONLY);
+    if (fd < 0) { err = "cannot open " + path; return false; }
+    struct stat sb;
+    if (fstat(fd, &sb) != 0) { close(fd); err = "cannot stat " + path; return false; }
+    const uint64_t size = (uint64_t)sb.st_size;
+    auto rd = [&](void* dst, uint64_t n) {
+        uint64_t got = 0;
+        while (got < n) {
+            const ssize_t r = read(fd, static_cast<char*>(dst) + got, n - got);
+            if (r <= 0) return false;
+            got += (uint64_t)r;
+        }
+        return true;
+    };
+    auto bad = [&](const char* what) { close(fd); err = path + ": " + what; return false; };
+    char hb[48];
+    if (size < 49 || !rd(hb, 48)) return bad("truncated header");
+    auto u32 = [](const char* q) { uint32_t v; memcpy(&v, q, 4); return v; };
+    auto i32 = [](const char* q) { int32_t v; memcpy(&v, q, 4); return v; };
+    out.h = u32(hb);
+    out.idx[0] = i32(hb + 4); out.idx[1] = i32(hb + 8); out.idx[2] = i32(hb + 12);
+    out.total = u32(hb + 16); out.number = u32(hb + 20); out.overflow = u32(hb + 24);
+    if (48 + 16ull * out.number + 1 > size) return bad("truncated grid");
     out.grid.resize(out.number);
-    memcpy(out.grid.data(), p + off, 16ull * out.number);
-    off += 16ull * out.number;
+    if (out.number && !rd(out.grid.data(), 16ull * out.number)) return bad("truncated grid");
+    HostVec<char> tb(size - 48 - 16ull * out.number);
+    if (!rd(tb.data(), tb.size())) return bad("truncated overflow entries");
+    close(fd);
+    const char* p = tb.data();
+    const uint64_t len = tb.size();
+    auto bad2 = [&](const char* what) { err = path + ": " + what; return false; };
+    uint64_t off = 0;
     const uint32_t nb = (uint8_t)p[off++];
-    if (nb > 8) return bad("more than 8 overflow entries");
+    if (nb > 8) return bad2("more than 8 overflow entries");
     out.entries.clear();
     for (uint32_t j = 0; j < nb; j++) {
-        if (off + 16 > b.size()) return bad("truncated overflow entry");
+        if (off + 16 > len) return bad2("truncated overflow entry");
         CellFile::Entry e;
-        e.child[0] = i32(off); e.child[1] = i32(off + 4); e.child[2] = i32(off + 8);
-        const uint32_t n = u32(off + 12);
+        e.child[0] = i32(p + off); e.child[1] = i32(p + off + 4); e.child[2] = i32(p + off + 8);
+        const uint32_t n = u32(p + off + 12);
         off += 16;
         e.some = n != 0;
-        if (off + 16ull * n > b.size()) return bad("truncated overflow list");
+        if (off + 16ull * n > len) return bad2("truncated overflow list");
         e.pts.resize(n);
-        memcpy(e.pts.data(), p + off, 16ull * n);
+        if (n) memcpy(e.pts.data(), p + off, 16ull * n);
         off += 16ull * n;
         out.entries.push_back(std::move(e));
     }
-    if (off != b.size()) return bad("trailing bytes");
+    if (off != len) return bad2("trailing bytes");
     return true;
 }
 
@@ -439,6 +455,8 @@ int read_cloud(const std::string& dir, uint32_t hierarchies, std::vector<CellFil
             keep.push_back({(*subtrees)[i], (*subtrees)[i + 1], (*subtrees)[i + 2]});
         std::sort(keep.begin(), keep.end());
     }
+    struct Want { std::string path; uint32_t h; int32_t x, y, z; };
+    std::vector<Want> want;
     for (uint32_t h = 0; h < hierarchies; h++) {
         const std::string hd = dir + "/h_" + std::to_string(h);
         DIR* d = opendir(hd.c_str());
@@ -453,14 +471,41 @@ int read_cloud(const std::string& dir, uint32_t hierarchies, std::vector<CellFil
             if (sscanf(nm.c_str(), "c_%d_%d_%d.%3s", &x, &y, &z, tail) != 4 || strcmp(tail, "bin") != 0) continue;
             if (subtrees && !std::binary_search(keep.begin(), keep.end(), std::array<int32_t, 3>{x >> h, y >> h, z >> h}))
                 continue;
-            CellFile c;
-            if (!read_cell_file(hd + "/" + nm, c, err)) return -EINVAL;
-            if (c.h != h || c.idx[0] != x || c.idx[1] != y || c.idx[2] != z) {
-                err = hd + "/" + nm + ": header does not match the file name";
-                return -EINVAL;
-            }
-            cells.push_back(std::move(c));
+            want.push_back({hd + "/" + nm, h, x, y, z});
         }
+    }
+    // the files in parallel (the same reader pool size as the writer)
+    cells.resize(want.size());
+    std::atomic<size_t> next{0};
+    std::atomic<bool> failed{false};
+    std::mutex em;
+    auto work = [&]() {
+        std::string e;
+        for (;;) {
+            const size_t i = next.fetch_add(1);
+            if (i >= want.size() || failed.load()) return;
+            const Want& w = want[i];
+            CellFile& c = cells[i];
+            bool ok = read_cell_file(w.path, c, e);
+            if (ok && (c.h != w.h || c.idx[0] != w.x || c.idx[1] != w.y || c.idx[2] != w.z)) {
+                e = w.path + ": header does not match the file name";
+                ok = false;
+            }
+            if (!ok) {
+                std::lock_guard<std::mutex> g(em);
+                if (!failed.exchange(true)) err = e;
+                return;
+            }
+        }
+    };
+    const unsigned nt = std::max(1u, std::min<unsigned>(writer_threads(), (unsigned)want.size()));
+    std::vector<std::thread> th;
+    for (unsigned t = 1; t < nt; t++) th.emplace_back(work);
+    work();
+    for (auto& t : th) t.join();
+    if (failed.load()) {
+        cells.clear();
+        return -EINVAL;
     }
     return 0;
 }
@@ -484,7 +529,7 @@ int prior_from_cells(const std::vector<CellFile>& cells, const Config& cfg, Prio
             return a->idx[0] != b->idx[0] ? a->idx[0] < b->idx[0] : (a->idx[1] != b->idx[1] ? a->idx[1] < b->idx[1] : a->idx[2] < b->idx[2]);
         });
     // keys and per-cell offsets
-    struct CellPlan { uint64_t gkey, kkey, inj_off; std::vector<int32_t> layers; std::vector<PriorSlabRec> recs; };
+    struct CellPlan { uint64_t gkey = 0, kkey = 0, inj_off = 0; std::vector<int32_t> layers; std::vector<PriorSlabRec> recs; };
     std::vector<std::vector<CellPlan>> plan(levels);
     uint64_t key = 0, inj = 0;
     for (uint32_t h = 0; h < levels; h++) {
@@ -506,49 +551,97 @@ int prior_from_cells(const std::vector<CellFile>& cells, const Config& cfg, Prio
     out.nseeds = key;
     out.inj.resize(inj);
     out.inj_keys.resize(inj);
-    // level-0 seeds in key order
-    for (const CellFile* c : by.empty() ? std::vector<const CellFile*>() : by[0])
-        out.seeds0.insert(out.seeds0.end(), c->grid.begin(), c->grid.end());
-    for (const CellFile* c : by.empty() ? std::vector<const CellFile*>() : by[0])
-        for (const CellFile::Entry& e : c->entries)
-            if (e.some) out.seeds0.insert(out.seeds0.end(), e.pts.begin(), e.pts.end());
+    const unsigned nt = std::max(1u, std::min<unsigned>(16, std::thread::hardware_concurrency()));
+    auto parallel = [&](auto&& work) {
+        std::vector<std::thread> th;
+        for (unsigned t = 1; t < nt; t++) th.emplace_back(work);
+        work();
+        for (auto& t : th) t.join();
+    };
+    // level-0 seeds in key order (every grid, then every kept list), copied in parallel
+    {
+        std::vector<std::pair<const Point*, size_t>> parts;
+        if (!by.empty()) {
+            for (const CellFile* c : by[0]) parts.push_back({c->grid.data(), c->grid.size()});
+            for (const CellFile* c : by[0])
+                for (const CellFile::Entry& e : c->entries)
+                    if (e.some) parts.push_back({e.pts.data(), e.pts.size()});
+        }
+        std::vector<size_t> at(parts.size() + 1, 0);
+        for (size_t i = 0; i < parts.size(); i++) at[i + 1] = at[i] + parts[i].second;
+        out.seeds0.resize(at.back());
+        std::atomic<size_t> nx{0};
+        parallel([&]() {
+            for (size_t i; (i = nx.fetch_add(1)) < parts.size();)
+                if (parts[i].second) memcpy(out.seeds0.data() + at[i], parts[i].first, parts[i].second * sizeof(Point));
+        });
+    }
     // per cell (threads): slabs by hex layer, seeds grouped by slab, their child slabs
     std::atomic<int> bad{0};
     for (uint32_t h = 0; h < levels; h++) {
         const float cs = cell_size(cfg.max_cell_size, h), cr = hex_radius(sub_cell_size(cs, cfg.sub_grid_dimension));
         const float csc = cell_size(cfg.max_cell_size, h + 1), crc = hex_radius(sub_cell_size(csc, cfg.sub_grid_dimension));
         std::atomic<size_t> next{0};
+        // Per cell: pass 1 takes every seed's hex layer (hex.rs:83) in key order
+        // (grid, then the kept lists), pass 2 scatters the seeds into their
+        // slab's run of inj (a stable counting sort by layer: both passes read
+        // the cell's points in order) and counts each slab's child slabs.
         auto work = [&]() {
-            std::vector<std::pair<int32_t, uint32_t>> lay;   // (layer, point #) ; # < grid: grid, else kept
-            std::vector<const Point*> src;
-            std::vector<uint32_t> keys;
+            std::vector<int32_t> tl;
+            std::vector<uint32_t> cnt, cur;
+            std::vector<int32_t> sid;
             for (;;) {
                 const size_t i = next.fetch_add(1);
                 if (i >= by[h].size()) return;
                 const CellFile* c = by[h][i];
                 CellPlan& P = plan[h][i];
-                src.clear();
-                keys.clear();
-                for (size_t j = 0; j < c->grid.size(); j++) { src.push_back(&c->grid[j]); keys.push_back((uint32_t)(P.gkey + j)); }
-                uint64_t kk = P.kkey;
+                std::vector<std::pair<const Point*, size_t>> parts;   // grid, then the kept (Some) lists
+                parts.push_back({c->grid.data(), c->grid.size()});
                 for (const CellFile::Entry& e : c->entries)
-                    if (e.some)
-                        for (const Point& q : e.pts) { src.push_back(&q); keys.push_back((uint32_t)kk++); }
-                lay.resize(src.size());
-                for (uint32_t j = 0; j < src.size(); j++) lay[j] = {sat_i32(src[j]->z / cr), j};   // hex.rs:83
-                std::stable_sort(lay.begin(), lay.end(),
-                                 [](const std::pair<int32_t, uint32_t>& a, const std::pair<int32_t, uint32_t>& b) { return a.first < b.first; });
+                    if (e.some) parts.push_back({e.pts.data(), e.pts.size()});
+                size_t n = 0;
+                for (const auto& q : parts) n += q.second;
+                tl.resize(n);
+                int32_t tmin = INT32_MAX, tmax = INT32_MIN;
+                {
+                    size_t j = 0;
+                    for (const auto& q : parts)
+                        for (size_t k = 0; k < q.second; k++, j++) {
+                            tl[j] = sat_i32(q.first[k].z / cr);   // hex.rs:83
+                            tmin = std::min(tmin, tl[j]);
+                            tmax = std::max(tmax, tl[j]);
+                        }
+                }
+                if (n == 0) continue;
+                if ((int64_t)tmax - tmin >= (1 << 20)) { bad.store(2); continue; }   // not one cell's layers
+                const size_t nt_ = (size_t)(tmax - tmin) + 1;
+                cnt.assign(nt_, 0);
+                for (size_t j = 0; j < n; j++) cnt[(size_t)(tl[j] - tmin)]++;
+                // one record per occupied layer, in layer order; seeds at w0 + exclusive scan
+                sid.assign(nt_, -1);
+                cur.assign(nt_, 0);
                 uint64_t w = P.inj_off;
-                for (size_t j = 0; j < lay.size();) {
-                    size_t e = j;
-                    while (e < lay.size() && lay[e].first == lay[j].first) e++;
-                    const int32_t t = lay[j].first;
+                for (size_t t = 0; t < nt_; t++) {
+                    if (!cnt[t]) continue;
                     PriorSlabRec R;
                     R.seed_off = (uint32_t)w;
-                    R.nseed = (uint32_t)(e - j);
+                    R.nseed = cnt[t];
                     for (int d = 0; d < 24; d++) { R.child[d] = kNoPriorSlab; R.dcap[d] = 0; }
-                    for (size_t k = j; k < e; k++) {   // grid seeds first (lower keys), then kept: already in key order
-                        const Point* q = src[lay[k].second];
+                    sid[t] = (int32_t)P.recs.size();
+                    cur[t] = (uint32_t)(w - P.inj_off);
+                    P.layers.push_back(tmin + (int32_t)t);
+                    P.recs.push_back(R);
+                    w += cnt[t];
+                }
+                size_t j = 0;
+                uint64_t key = P.gkey;
+                for (size_t pi = 0; pi < parts.size(); pi++) {
+                    if (pi == 1) key = P.kkey;   // kept seeds follow every grid seed of the level
+                    for (size_t k = 0; k < parts[pi].second; k++, j++, key++) {
+                        const Point* q = &parts[pi].first[k];
+                        const size_t tt = (size_t)(tl[j] - tmin);
+                        const int32_t t = tl[j];
+                        PriorSlabRec& R = P.recs[(size_t)sid[tt]];
                         const int32_t bx = cell_index1(q->x, csc) - 2 * c->idx[0], by_ = cell_index1(q->y, csc) - 2 * c->idx[1],
                                       bz = cell_index1(q->z, csc) - 2 * c->idx[2];
                         const int32_t sel = sat_i32(q->z / crc) - 2 * t + 1;
@@ -557,19 +650,16 @@ int prior_from_cells(const std::vector<CellFile>& cells, const Config& cfg, Prio
                         } else {
                             R.dcap[(bx | (by_ << 1) | (bz << 2)) * 3 + sel]++;
                         }
-                        if (h > 0) { out.inj[w] = *q; out.inj_keys[w] = keys[lay[k].second]; w++; }
+                        if (h > 0) {
+                            const uint64_t o = P.inj_off + cur[tt]++;
+                            out.inj[o] = *q;
+                            out.inj_keys[o] = (uint32_t)key;
+                        }
                     }
-                    P.layers.push_back(t);
-                    P.recs.push_back(R);
-                    j = e;
                 }
             }
         };
-        const unsigned nt = std::max(1u, std::min<unsigned>(16, std::thread::hardware_concurrency()));
-        std::vector<std::thread> th;
-        for (unsigned t = 1; t < nt; t++) th.emplace_back(work);
-        work();
-        for (auto& t : th) t.join();
+        parallel(work);
         PriorLevel& L = out.levels[h];
         L.cell_slab0.push_back(0);
         for (size_t i = 0; i < by[h].size(); i++) {
@@ -587,6 +677,7 @@ int prior_from_cells(const std::vector<CellFile>& cells, const Config& cfg, Prio
             std::vector<PriorSlabRec>().swap(plan[h][i].recs);
         }
     }
+    if (bad.load() == 2) { err = "existing cloud: a cell's points span more hex layers than a cell has"; return -EINVAL; }
     if (bad.load()) { err = "existing cloud: a point lies outside its cell's child slabs"; return -EINVAL; }
     // child links: slab (c, t), destination (octant, sel) -> record of (2c + octant bits, 2t - 1 + sel) at h+1
     for (uint32_t h = 0; h + 1 < levels; h++) {

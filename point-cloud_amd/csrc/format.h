@@ -58,11 +58,11 @@ struct CellFile {
     uint32_t h = 0;
     int32_t idx[3] = {0, 0, 0};
     uint32_t total = 0, number = 0, overflow = 0;
-    std::vector<Point> grid;
+    HostVec<Point> grid;
     struct Entry {
         int32_t child[3];
         bool some;
-        std::vector<Point> pts;
+        HostVec<Point> pts;
     };
     std::vector<Entry> entries;
 };

@@ -16,8 +16,14 @@ from test_oracle_xcheck import _case, _to_np  # noqa: E402
 pytestmark = pytest.mark.gpu
 
 
-def _check(files, cfg=None, batch=10_000, fast=False, synth_files=None):
-    with tempfile.TemporaryDirectory() as tg, tempfile.TemporaryDirectory() as to:
+def _shm():
+    """tmpfs for outputs of hundreds of thousands of cell files (creating and
+    deleting them on the box's overlay file system can take minutes)."""
+    return "/dev/shm" if os.path.isdir("/dev/shm") and os.access("/dev/shm", os.W_OK) else None
+
+
+def _check(files, cfg=None, batch=10_000, fast=False, synth_files=None, base=None):
+    with tempfile.TemporaryDirectory(dir=base) as tg, tempfile.TemporaryDirectory(dir=base) as to:
         st = run_gpu(tg, files if not synth_files else [], cfg=cfg, batch=batch, synth=synth_files)
         err, arrivals = run_oracle(to, files, cfg=cfg, batch=batch)
         assert err == 0
@@ -146,9 +152,10 @@ def test_sparse_bbox_far_outliers():
 
 
 def test_sparse_bbox_small_cells_many_occupied():
-    """Tiny max_cell_size: ~10^6 occupied level-0 cells over a 2^30-cell box."""
-    pts = synth(52, 0, 400_000, lo=-500.0, ext=1000.0)
-    _check([pts], cfg=dict(cell_point_overflow_limit=4, sub_grid_dimension=2, max_cell_size=1.0), fast=True)
+    """Tiny max_cell_size: ~2.5 * 10^5 occupied level-0 cells over a 2^30-cell box."""
+    pts = synth(52, 0, 250_000, lo=-500.0, ext=1000.0)
+    _check([pts], cfg=dict(cell_point_overflow_limit=4, sub_grid_dimension=2, max_cell_size=1.0), fast=True,
+           base=_shm())
 
 
 def test_bbox_beyond_hashed_range_is_an_error():
