@@ -95,6 +95,38 @@ def test_config5_merge_100m_into_1b():
         conv.close()
 
 
+def test_config5_merge_100m_into_1b_from_disk():
+    """Config 5 as the CLI runs it: the 1B cloud is written as cell files and a new
+    converter opens that directory (pcc_open: read_cloud + prior_from_cells, the
+    existing cells as the starting state, converter.rs:187-207) and merges the
+    +100M points.  Same digests as the in-memory adoption above."""
+    import shutil
+    import tempfile
+    fx = fixture("config5")
+    p, s = fx["prior_synth"], fx["synth"]
+    base = tempfile.mkdtemp(prefix="pcc_cfg5_disk_", dir="/tmp")
+    try:
+        if shutil.disk_usage(base).free < 40e9:
+            pytest.skip("needs 16 GB of cell files under /tmp")
+        prior = pcconv.Converter(base)
+        try:
+            prior.add_synthetic(p["seed"], p["kind"], p["n"])
+            prior.build()
+            prior.write()
+        finally:
+            prior.close()
+        conv = pcconv.Converter(base)   # an existing cloud: merge mode
+        try:
+            conv.add_synthetic(s["seed"], s["kind"], s["n"])
+            st = conv.build()
+            _check(conv, st, fx, p["n"] + s["n"], merge=True)
+            assert st["number_of_points"] == p["n"] + s["n"]
+        finally:
+            conv.close()
+    finally:
+        shutil.rmtree(base, ignore_errors=True)
+
+
 def test_config3_generator_device_equals_host():
     """The kind-2 generator (Box-Muller mixture) gives the same bits on gfx950 and
     in the oracle's independent restatement (the fixtures above rely on it)."""
