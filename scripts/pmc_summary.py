@@ -61,7 +61,33 @@ def main(out_dir, name, bench_json):
                    "traffic_over_alg": l0["hbm_bytes"] / (36.0 * npts), "ms": l0["ns"] / 1e6},
         "kernels": k,
     }
+    # per launch of the dense kernel (one per level, in dispatch order), with the
+    # level's arrivals from the engine's verbose log when the pass ran with PCC_VERBOSE=1
+    lv_arr = []
+    try:
+        for line in open(f"{out_dir}/pmc_fetch.err"):
+            m = re.search(r"\[pcc\] level (\d+): .*\(dense (\d+), small (\d+)\) arrivals (\d+)", line)
+            if m:
+                lv_arr.append((int(m.group(1)), int(m.group(2)), int(m.group(4))))
+    except OSError:
+        pass
+    fd = [(t, v) for nm, v, t in fetch if "k_slab<" in nm and "k_slab_" not in nm]
+    wd = [v for nm, v, t in write if "k_slab<" in nm and "k_slab_" not in nm]
+    per = []
+    dense_levels = [a for a in lv_arr if a[1] > 0]
+    for i, ((t, f), w) in enumerate(zip(fd, wd)):
+        e = {"launch": i, "ms": t / 1e6, "fetch_bytes_raw": f, "write_bytes": w, "hbm_bytes": 2.0 * f + w}
+        if i < len(dense_levels):
+            lvl, _, arrivals = dense_levels[i]
+            e.update({"level": lvl, "arrivals": arrivals, "alg_bytes": 32.0 * arrivals,
+                      "traffic_over_alg": (2.0 * f + w) / (32.0 * arrivals),
+                      "uncorrected_over_alg": (f + w) / (32.0 * arrivals),
+                      "alg_GBps": 32.0 * arrivals / t})
+        per.append(e)
+    summary["dense_kernel"]["per_launch"] = per
     json.dump(summary, open(f"profiles/{name}.json", "w"), indent=1)
+    for e in per:
+        print(json.dumps(e))
     print(json.dumps(summary["dense_kernel"]))
     print(json.dumps({a: b for a, b in summary["level0"].items() if a != "kernels"}))
 
