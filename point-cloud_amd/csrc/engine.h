@@ -9,6 +9,7 @@
 #pragma once
 #include <stdint.h>
 #include <stddef.h>
+#include <sys/mman.h>
 #include <memory>
 #include <string>
 #include <type_traits>
@@ -90,12 +91,35 @@ struct PriorLevel {
     std::vector<PriorSlabRec> slabs;
 };
 // std::allocator that default-initialises: large host arrays that are filled
-// right after their allocation (by several threads) are not zero-filled first
+// right after their allocation (by several threads) are not zero-filled first.
+// Arrays of 2 MB or more are mapped 2 MB-aligned with transparent huge pages
+// advised: the first touch of a 16 GB cloud then takes ~8k page faults, not ~4M.
 template <class T>
 struct DefaultInitAlloc : std::allocator<T> {
     template <class U> struct rebind { using other = DefaultInitAlloc<U>; };
     DefaultInitAlloc() = default;
     template <class U> DefaultInitAlloc(const DefaultInitAlloc<U>&) noexcept {}
+    static constexpr size_t kHuge = size_t(2) << 20;
+    T* allocate(size_t n) {
+        const size_t bytes = n * sizeof(T);
+        if (bytes < kHuge) return std::allocator<T>::allocate(n);
+        const size_t len = (bytes + kHuge - 1) & ~(kHuge - 1);
+        void* q = mmap(nullptr, len + kHuge, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+        if (q == MAP_FAILED) throw std::bad_alloc();
+        const uintptr_t b0 = reinterpret_cast<uintptr_t>(q), a = (b0 + kHuge - 1) & ~uintptr_t(kHuge - 1);
+        if (a > b0) munmap(q, a - b0);
+        if (b0 + len + kHuge > a + len) munmap(reinterpret_cast<void*>(a + len), b0 + len + kHuge - (a + len));
+        madvise(reinterpret_cast<void*>(a), len, MADV_HUGEPAGE);
+        return reinterpret_cast<T*>(a);
+    }
+    void deallocate(T* p, size_t n) noexcept {
+        const size_t bytes = n * sizeof(T);
+        if (bytes < kHuge) {
+            std::allocator<T>::deallocate(p, n);
+            return;
+        }
+        munmap(p, (bytes + kHuge - 1) & ~(kHuge - 1));
+    }
     template <class U> void construct(U* p) noexcept(std::is_nothrow_default_constructible<U>::value) {
         ::new (static_cast<void*>(p)) U;
     }
