@@ -25,11 +25,10 @@ __device__ __forceinline__ uint64_t wave_peers(uint32_t v, bool act) {
     uint32_t lo = (uint32_t)a, hi = (uint32_t)(a >> 32);
 #pragma unroll
     for (int b = 0; b < NB; b++) {
-        const uint32_t bit = (v >> b) & 1u;
-        const uint64_t bb = __builtin_amdgcn_ballot_w64(bit != 0);
-        const uint32_t inv = bit - 1u;   // 0 if the bit is set, ~0 otherwise
-        lo &= (uint32_t)bb ^ inv;
-        hi &= (uint32_t)(bb >> 32) ^ inv;
+        const int32_t sx = ((int32_t)(v << (31 - b))) >> 31;   // ~0 if the bit is set, 0 otherwise (v_bfe_i32)
+        const uint64_t bb = __builtin_amdgcn_ballot_w64(sx != 0);
+        lo &= ~((uint32_t)bb ^ (uint32_t)sx);   // lanes whose bit equals this lane's (one v_bitop3 per half)
+        hi &= ~((uint32_t)(bb >> 32) ^ (uint32_t)sx);
     }
     return ((uint64_t)hi << 32) | lo;
 }
