@@ -81,6 +81,7 @@ struct PriorCell { int32_t x, y, z; uint32_t st; };   // st: 2 bits per octant: 
 constexpr uint32_t kNoPriorSlab = 0xFFFFFFFFu;
 struct PriorSlabRec {                                  // one (cell, hex layer) of the existing cloud
     uint32_t seed_off, nseed;                          // level >= 1: its seeds in PriorState::inj
+    uint32_t ngrid, pad;                               // of them grid points (the first ngrid, one per slot)
     uint32_t child[24];                                // its child slabs' records at level h+1 (kNoPriorSlab: none)
     uint32_t dcap[24];                                 // its seeds per child slab (their capacities)
 };

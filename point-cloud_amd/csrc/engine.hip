@@ -1363,6 +1363,7 @@ struct SmallDesc {
     uint32_t s, off, n, dbase;
     int32_t t, cx, cy, cz;
     uint32_t sb, dlen, pad0, pad1;
+    uint32_t ng;   // merge, dense slabs of levels >= 1: the first ng seeds are grid points (one per slot)
 };
 
 struct SlabParams {
@@ -1620,6 +1621,8 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
     }
     const bool wide = n > kJMaskNarrow;
     const uint32_t jmask = wide ? kJMask : kJMaskNarrow;
+    // merge: the first ng arrivals are the slab's grid seeds (below)
+    const uint32_t ng = SEEDS ? min(D.ng, n) : 0u;
     // reference slot: the one holding the cell centre (metadata.rs:104-106)
     const I3 c0 = hex_from_world(cell_pos1(cx, P.cs), cell_pos1(cy, P.cs), cell_pos1(cz, P.cs), G.cr);
     const int32_t rx = c0.x - P.tx / 2, ry = c0.y - P.ty / 2;
@@ -1665,7 +1668,7 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
     Pre pre[PF + 2];
 #pragma unroll
     for (int q = 0; q < PF + 2; q++) {
-        const uint32_t jo = min((uint32_t)(q * BS) + tid, nm1);
+        const uint32_t jo = min(ng + (uint32_t)(q * BS) + tid, nm1);
         if (q < PF) {
             pre[q].p = rP.p(jo * 16);
             pre[q].k = rP.k(jo * 4);
@@ -1686,14 +1689,48 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
     }
     if (tid == 0) { S.nwin = 0; S.err = 0; }
     __syncthreads();
+    if constexpr (SEEDS) {
+        // Merge: the slab's grid seeds (its first ng arrivals: keys below every
+        // other arrival, one per slot, cell.rs:183-229) are the occupants the
+        // replay would install, with no emission; they go straight into the table.
+        for (uint32_t j0 = 0; j0 < ng; j0 += BS) {
+            const uint32_t jg = j0 + tid;
+            const bool v = jg < ng;
+            const u32x4 q = rP.p(v ? jg * 16 : 0xFFFFFFFFu);
+            const float x = __uint_as_float(q.x), y = __uint_as_float(q.y), z = __uint_as_float(q.z);
+            const SlotRoute sr = slot_route(x, y, z, G);
+            const int32_t lx = sr.sl.x - rx, ly = sr.sl.y - ry;
+            const bool layer_ok = sr.sl.z == t;
+            const bool range_ok = lx >= 0 && ly >= 0 && lx < P.tx && ly < P.ty;
+            const bool slotted = v && layer_ok && range_ok;
+            float X, Y, Z;
+            hex_to_world(sr.sl, G.cr, X, Y, Z);
+            const float d2 = dist2(X, Y, Z, x, y, z);
+            const int d = route_dest_nc(sr.rc, cx, cy, cz, t);
+            int32_t gn = route_dest_nc(sr.rg, sr.rc.ix, sr.rc.iy, sr.rc.iz, sr.rc.u);
+            const bool bad = v && (!layer_ok || !range_ok || d < 0 || (P.check_gchild && gn < 0));
+            if (__ballot(bad)) {
+                if (bad) err |= slot_route_errs(sr, layer_ok, range_ok, cx, cy, cz, t, P.check_gchild);
+            }
+            const uint32_t dn = d < 0 ? 0u : (uint32_t)d;
+            if (d < 0) gn = -1;
+            if (slotted) {
+                const unsigned long long e = ((unsigned long long)f2u(d2) << 33) | ((unsigned long long)dn << kJBits) |
+                                             (wide ? 0u : ((uint32_t)(gn + 1) << 23)) | jg;
+                // two grid points in one slot: not a cell a converter writes
+                if (atomicCAS(&S.tab[(uint32_t)(ly * P.tx + lx)], kEmpty64, e) != kEmpty64) err |= ERR_CLAIM;
+            }
+        }
+        __syncthreads();
+    }
     STAMP(0);
     // child-slab regions of this slab, one per lane < 24, kept in registers
     const uint32_t my_doff = lane < kDests ? S.doff[lane] : 0u, my_dcap = lane < kDests ? S.dcap[lane] : 0u;
-    const uint32_t nchunks = (n + BS - 1) / BS;
+    const uint32_t nchunks = (n - ng + BS - 1) / BS;
     auto step = [&](uint32_t ci, Stage& cur, Stage& prv, const Pre& mine, const Pre& prvb, Pre& pf) {
         const uint32_t par = ci & 1;
         uint32_t* claim = S.claim[par];
-        const uint32_t j = ci * BS + tid;
+        const uint32_t j = ng + ci * BS + tid;
         const bool valid = j < n;
         const bool forced = valid && mine.k - P.kf_lo < P.kf_n;
         {   // prefetch chunk i+2 (clamped)
@@ -1843,7 +1880,7 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
                     em = 1;
                     emd = dg & 31u;
                     emg = (int32_t)(dg >> 5) - 1;
-                    gsrc = (ci * BS + bt) * 16;
+                    gsrc = (ng + ci * BS + bt) * 16;
                 } else if (occ != kEmpty64) {          // first record: displaces the occupant
                     em = 1;
                     emd = (uint32_t)(occ >> kJBits) & 31u;
@@ -1960,6 +1997,7 @@ __device__ __forceinline__ SmallDesc slab_desc(uint32_t s, const uint32_t* slab_
     D.cz = cell_idx[3 * cr_ + 2];
     D.sb = cell_sb[cr_];
     D.pad0 = D.pad1 = 0;
+    D.ng = 0;
     return D;
 }
 
@@ -1972,7 +2010,7 @@ __global__ void k_dense_desc(const uint32_t* list, uint32_t nlist, const uint32_
     SmallDesc D = slab_desc(list[i], slab_cell, slab_layer, slab_off, slab_n, cell_idx, cell_sb, dest_off, dcap);
     if (slab_prior) {   // merge, level >= 1: seeds read in place (pad0 = offset in the seed array, pad1 = count)
         const uint32_t pr = slab_prior[D.s];
-        if (pr != kNoPriorSlab) { D.pad0 = prec[pr].seed_off; D.pad1 = prec[pr].nseed; }
+        if (pr != kNoPriorSlab) { D.pad0 = prec[pr].seed_off; D.pad1 = prec[pr].nseed; D.ng = prec[pr].ngrid; }
     }
     out[i] = D;
 }
@@ -1989,7 +2027,7 @@ __global__ void k_small_desc(const uint32_t* list, uint32_t nlist, const uint32_
                             dest_off, dcap);
     if (slab_prior) {   // merge, level >= 1: the slab's seeds stay in the seed array (pad0 = offset, pad1 = count)
         const uint32_t pr = slab_prior[D.s];
-        if (pr != kNoPriorSlab) { D.pad0 = prec[pr].seed_off; D.pad1 = prec[pr].nseed; }
+        if (pr != kNoPriorSlab) { D.pad0 = prec[pr].seed_off; D.pad1 = prec[pr].nseed; D.ng = prec[pr].ngrid; }
     }
     // size class: 0..2 one wave (< 128, < 256, < 512 arrivals), 3 block; the
     // wave classes share wave_out, class c from offset c * nlist.  One global

@@ -626,6 +626,8 @@ int prior_from_cells(const std::vector<CellFile>& cells, const Config& cfg, Prio
                     PriorSlabRec R;
                     R.seed_off = (uint32_t)w;
                     R.nseed = cnt[t];
+                    R.ngrid = 0;
+                    R.pad = 0;
                     for (int d = 0; d < 24; d++) { R.child[d] = kNoPriorSlab; R.dcap[d] = 0; }
                     sid[t] = (int32_t)P.recs.size();
                     cur[t] = (uint32_t)(w - P.inj_off);
@@ -642,6 +644,7 @@ int prior_from_cells(const std::vector<CellFile>& cells, const Config& cfg, Prio
                         const size_t tt = (size_t)(tl[j] - tmin);
                         const int32_t t = tl[j];
                         PriorSlabRec& R = P.recs[(size_t)sid[tt]];
+                        if (pi == 0) R.ngrid++;   // grid seeds precede the kept ones in every slab (key order)
                         const int32_t bx = cell_index1(q->x, csc) - 2 * c->idx[0], by_ = cell_index1(q->y, csc) - 2 * c->idx[1],
                                       bz = cell_index1(q->z, csc) - 2 * c->idx[2];
                         const int32_t sel = sat_i32(q->z / crc) - 2 * t + 1;
