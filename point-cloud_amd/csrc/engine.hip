@@ -36,6 +36,8 @@
 #include <memory>
 
 #include <algorithm>
+#include <mutex>
+#include <unordered_map>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -46,6 +48,93 @@
 #include "synth.h"
 
 namespace pcc {
+
+// ------------------------------------------------------------------ device memory
+// Large device buffers (arenas, input, pool chunks, merge seeds) are kept in a
+// process-wide cache when a converter releases them and handed to the next
+// converter on the same device: right after hipFree of tens of GB, the next
+// hipMalloc of that size stalled for about 5 s on the MI355X boxes
+// (scripts/second_conv.py).  A failed hipMalloc empties the cache and retries.
+namespace {
+constexpr size_t kCacheMin = size_t(64) << 20;
+constexpr size_t kCacheMax = size_t(96) << 30;     // cached bytes per process, beyond: hipFree
+size_t g_dev_cached = 0;
+struct DevBlock { void* p; size_t bytes; int device; };
+std::mutex g_dev_mu;
+std::vector<DevBlock> g_dev_free;                 // cached, unused
+std::unordered_map<void*, DevBlock> g_dev_live;   // handed out by dev_alloc
+}  // namespace
+
+static void* dev_alloc(size_t bytes) {
+    bytes = std::max<size_t>(bytes, 1);
+    int dev = 0;
+    HIP_CHECK(hipGetDevice(&dev));
+    {
+        std::lock_guard<std::mutex> g(g_dev_mu);
+        size_t best = SIZE_MAX;
+        for (size_t i = 0; i < g_dev_free.size(); i++) {   // the smallest cached block that fits, not far larger
+            const DevBlock& b = g_dev_free[i];
+            if (b.device == dev && b.bytes >= bytes && b.bytes <= bytes + bytes / 4 + kCacheMin &&
+                (best == SIZE_MAX || b.bytes < g_dev_free[best].bytes))
+                best = i;
+        }
+        if (best != SIZE_MAX) {
+            const DevBlock b = g_dev_free[best];
+            g_dev_free.erase(g_dev_free.begin() + (ptrdiff_t)best);
+            g_dev_cached -= b.bytes;
+            g_dev_live[b.p] = b;
+            return b.p;
+        }
+    }
+    void* p = nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess) {   // out of memory: give the cached blocks back and retry
+        (void)hipGetLastError();
+        std::vector<DevBlock> drop;
+        {
+            std::lock_guard<std::mutex> g(g_dev_mu);
+            for (size_t i = 0; i < g_dev_free.size();) {
+                if (g_dev_free[i].device == dev) {
+                    drop.push_back(g_dev_free[i]);
+                    g_dev_cached -= g_dev_free[i].bytes;
+                    g_dev_free.erase(g_dev_free.begin() + (ptrdiff_t)i);
+                } else {
+                    i++;
+                }
+            }
+        }
+        for (const DevBlock& b : drop) (void)hipFree(b.p);
+        HIP_CHECK(hipMalloc(&p, bytes));
+    }
+    std::lock_guard<std::mutex> g(g_dev_mu);
+    g_dev_live[p] = DevBlock{p, bytes, dev};
+    return p;
+}
+
+static void dev_release(void* p) {
+    if (!p) return;
+    DevBlock b{};
+    {
+        std::lock_guard<std::mutex> g(g_dev_mu);
+        auto it = g_dev_live.find(p);
+        if (it == g_dev_live.end()) {   // not ours
+            (void)hipFree(p);
+            return;
+        }
+        b = it->second;
+        g_dev_live.erase(it);
+        if (b.bytes >= kCacheMin && g_dev_cached + b.bytes <= kCacheMax) {
+            g_dev_free.push_back(b);
+            g_dev_cached += b.bytes;
+            return;
+        }
+    }
+    (void)hipFree(b.p);
+}
+
+template <class T>
+static void dev_alloc_t(T*& p, size_t bytes) {
+    p = static_cast<T*>(dev_alloc(bytes));
+}
 
 // ------------------------------------------------------------------ constants
 constexpr uint64_t kEmpty64 = ~0ull;
@@ -126,7 +215,7 @@ struct Engine::Dev {
         if (chunk_i == chunks.size()) {
             uint64_t sz = std::max<uint64_t>(bytes, 256ull << 20);
             uint8_t* p = nullptr;
-            HIP_CHECK(hipMalloc(&p, sz));
+            dev_alloc_t(p, sz);
             chunks.push_back({p, sz});
             chunk_used = 0;
         }
@@ -2951,7 +3040,10 @@ __global__ __launch_bounds__(256) void k_next_emit(NextParams Q) {
                 Q.nslab_prior[sid] = pr;
             }
             const uint32_t* sd = pr != kNoPriorSlab ? Q.prec_next[pr].dcap : nullptr;
-            for (int q = 0; q < kDests; q++) Q.ndcap[(uint64_t)sid * kDests + q] = g[q] + (sd ? sd[q] : 0u);
+            // the slab kernels write a gcap row only for a child slab that received
+            // emissions (dest_n > 0); a child slab of seeds alone has none
+            const bool ge = Q.dest_n[di] != 0;
+            for (int q = 0; q < kDests; q++) Q.ndcap[(uint64_t)sid * kDests + q] = (ge ? g[q] : 0u) + (sd ? sd[q] : 0u);
             if (n >= kSmallMax) Q.nbig_list[s_bigbase + atomicAdd(&s_big, 1u)] = sid;
             else Q.nsmall_list[s_smallbase + atomicAdd(&s_small, 1u)] = sid;
         }
@@ -3141,39 +3233,39 @@ void Engine::free_all() {
     levels_.clear();
     if (dev_) {
         for (int a = 0; a < 2; a++) {
-            (void)hipFree(dev_->ar[a].p); (void)hipFree(dev_->ar[a].k);
+            dev_release(dev_->ar[a].p); dev_release(dev_->ar[a].k);
         }
         (void)hipFree(dev_->ctr);
         (void)hipFree(dev_->bbox_part);
         (void)hipFree(dev_->bbox_flag);
         if (dev_->hst) (void)hipHostFree(dev_->hst);
         (void)hipFree(dev_->scan.bsums);
-        for (auto& c : dev_->chunks) (void)hipFree(c.first);
+        for (auto& c : dev_->chunks) dev_release(c.first);
         delete dev_;
         dev_ = nullptr;
     }
-    (void)hipFree(d_in_);
+    dev_release(d_in_);
     d_in_ = nullptr;
-    (void)hipFree(d_keys_);
+    dev_release(d_keys_);
     d_keys_ = nullptr;
     keys_cap_ = 0;
-    (void)hipFree(d_comb_);
+    dev_release(d_comb_);
     d_comb_ = nullptr;
-    (void)hipFree(d_ckeys_);
+    dev_release(d_ckeys_);
     d_ckeys_ = nullptr;
     ckeys_cap_ = 0;
     free_prior();
 }
 
 void Engine::free_prior() {
-    (void)hipFree(d_seeds_);
+    dev_release(d_seeds_);
     d_seeds_ = nullptr;
-    (void)hipFree(d_inj_);
+    dev_release(d_inj_);
     d_inj_ = nullptr;
-    (void)hipFree(d_inj_keys_);
+    dev_release(d_inj_keys_);
     d_inj_keys_ = nullptr;
     for (PriorDev& d : pdev_) {
-        (void)hipFree(d.cells); (void)hipFree(d.cell_slab0); (void)hipFree(d.slab_layer); (void)hipFree(d.slabs);
+        dev_release(d.cells); dev_release(d.cell_slab0); dev_release(d.slab_layer); dev_release(d.slabs);
     }
     pdev_.clear();
 }
@@ -3188,10 +3280,10 @@ void Engine::reserve(uint64_t n) {
     if (n <= cap_) return;
     if (n >= 0xFFFFFFFFull) throw std::runtime_error("more than 2^32-1 points per build are not supported");
     Point* p = nullptr;
-    HIP_CHECK(hipMalloc(&p, std::max<uint64_t>(n, 1) * sizeof(Point)));
+    dev_alloc_t(p, std::max<uint64_t>(n, 1) * sizeof(Point));
     if (n_) HIP_CHECK(hipMemcpyAsync(p, d_in_, n_ * sizeof(Point), hipMemcpyDeviceToDevice, stream_));
     HIP_CHECK(hipStreamSynchronize(stream_));
-    (void)hipFree(d_in_);
+    dev_release(d_in_);
     d_in_ = p;
     cap_ = n;
 }
@@ -3314,10 +3406,10 @@ void Engine::add_keyed_device(const Point* dpts, const uint32_t* dkeys, uint64_t
     reserve(n_ + n);
     if (keys_cap_ < n_ + n) {
         uint32_t* k = nullptr;
-        HIP_CHECK(hipMalloc(&k, std::max<uint64_t>(cap_, 1) * 4));
+        dev_alloc_t(k, std::max<uint64_t>(cap_, 1) * 4);
         if (n_) HIP_CHECK(hipMemcpyAsync(k, d_keys_, n_ * 4, hipMemcpyDeviceToDevice, stream_));
         HIP_CHECK(hipStreamSynchronize(stream_));
-        (void)hipFree(d_keys_);
+        dev_release(d_keys_);
         d_keys_ = k;
         keys_cap_ = cap_;
     }
@@ -3333,7 +3425,7 @@ void Engine::add_keyed_device(const Point* dpts, const uint32_t* dkeys, uint64_t
 template <class T, class A>
 static T* upload(const std::vector<T, A>& v) {
     T* d = nullptr;
-    HIP_CHECK(hipMalloc(&d, std::max<size_t>(v.size(), 1) * sizeof(T)));
+    dev_alloc_t(d, std::max<size_t>(v.size(), 1) * sizeof(T));
     if (!v.empty()) HIP_CHECK(hipMemcpy(d, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
     return d;
 }
@@ -3407,16 +3499,16 @@ int Engine::build() {
         const uint64_t n0 = nseeds0_;
         if (!comb_ok_) {
             if (comb_cap_ < n0 + n_) {
-                (void)hipFree(d_comb_);
-                HIP_CHECK(hipMalloc(&d_comb_, std::max<uint64_t>(n0 + n_, 1) * sizeof(Point)));
+                dev_release(d_comb_);
+                dev_alloc_t(d_comb_, std::max<uint64_t>(n0 + n_, 1) * sizeof(Point));
                 comb_cap_ = n0 + n_;
             }
             if (n0) HIP_CHECK(hipMemcpyAsync(d_comb_, d_seeds_, n0 * sizeof(Point), hipMemcpyDeviceToDevice, stream_));
             HIP_CHECK(hipMemcpyAsync(d_comb_ + n0, ext_in_ ? ext_in_ : d_in_, n_ * sizeof(Point),
                                      hipMemcpyDeviceToDevice, stream_));
             if (ckeys_cap_ < n0 + n_) {
-                (void)hipFree(d_ckeys_);
-                HIP_CHECK(hipMalloc(&d_ckeys_, std::max<uint64_t>(n0 + n_, 1) * 4));
+                dev_release(d_ckeys_);
+                dev_alloc_t(d_ckeys_, std::max<uint64_t>(n0 + n_, 1) * 4);
                 ckeys_cap_ = n0 + n_;
             }
             k_comb_keys<<<grid_for(n0 + n_, 256), 256, 0, stream_>>>(d_ckeys_, ext_in_ ? ext_keys_ : keyed_ ? d_keys_ : nullptr,
@@ -3441,8 +3533,8 @@ int Engine::build() {
     if (dev_->cap < acap) {
         for (int a = 0; a < 2; a++) {
             Arena& A = dev_->ar[a];
-            (void)hipFree(A.p); (void)hipFree(A.k);
-            HIP_CHECK(hipMalloc(&A.p, acap * 16)); HIP_CHECK(hipMalloc(&A.k, acap * 4));
+            dev_release(A.p); dev_release(A.k);
+            dev_alloc_t(A.p, acap * 16); dev_alloc_t(A.k, acap * 4);
         }
         dev_->cap = acap;
     }
