@@ -137,8 +137,14 @@ int pcc_finish(pcc_converter* c);
  * config 5).  Same config required. */
 int pcc_adopt_prior(pcc_converter* dst, pcc_converter* src);
 
-/* Free without writing anything. */
+/* Free without writing anything.  Large device buffers go to a process-wide
+ * cache and are reused by the next converter on the same device. */
 int pcc_close(pcc_converter* c);
+
+/* Frees the cached device buffers of closed converters (e.g. before the GUI
+ * hands the GPU to the renderer); returns the bytes freed.  No reference
+ * counterpart: the reference's Converter drop frees host memory only. */
+uint64_t pcc_release_device_cache(void);
 
 /* One cell of the built cloud as the reference holds it in memory (cell.rs:33-38
  * Cell, Header cell.rs:238-261): the header values exactly as Cell::write_to

@@ -751,6 +751,14 @@ int pcc_close(pcc_converter* c) {
     return 0;
 }
 
+uint64_t pcc_release_device_cache(void) {
+    try {
+        return (uint64_t)pcc::release_device_cache();
+    } catch (...) {
+        return 0;
+    }
+}
+
 int pcc_get_stats(const pcc_converter* c, pcc_stats* s) {
     if (!c || !s) return set_err(-EINVAL, "null argument");
     memset(s, 0, sizeof *s);

@@ -329,4 +329,8 @@ int shard_route(const Point* d, uint64_t n, uint32_t key0, const ShardGrid& g, c
 int shard_keys_from_bitmaps(const uint64_t* dbm, const uint64_t* nwords, const uint64_t* key0, uint32_t nsrc,
                             uint32_t* dkeys, uint64_t nkeys, int device);
 
+// Frees the device buffers closed converters left in the process-wide cache
+// (engine.hip dev_alloc); returns the bytes freed.  Buffers in use stay.
+size_t release_device_cache();
+
 }  // namespace pcc

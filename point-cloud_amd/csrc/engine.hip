@@ -131,6 +131,25 @@ static void dev_release(void* p) {
     (void)hipFree(b.p);
 }
 
+size_t release_device_cache() {
+    std::vector<DevBlock> drop;
+    {
+        std::lock_guard<std::mutex> g(g_dev_mu);
+        drop.swap(g_dev_free);
+        g_dev_cached = 0;
+    }
+    size_t bytes = 0;
+    int cur = 0;
+    HIP_CHECK(hipGetDevice(&cur));
+    for (const DevBlock& b : drop) {
+        if (b.device != cur) (void)hipSetDevice(b.device);
+        (void)hipFree(b.p);
+        if (b.device != cur) (void)hipSetDevice(cur);
+        bytes += b.bytes;
+    }
+    return bytes;
+}
+
 template <class T>
 static void dev_alloc_t(T*& p, size_t bytes) {
     p = static_cast<T*>(dev_alloc(bytes));

@@ -37,7 +37,8 @@ EXPORTS = ["pcc_abi_version", "pcc_last_error", "pcc_options_default", "pcc_open
            "pcc_pending_cells", "pcc_export_pending", "pcc_shard_slab_histogram", "pcc_shard_route_slabs",
            "pcc_write_cell_view", "pcc_begin_file", "pcc_append_points", "pcc_end_file", "pcc_cancel_file",
            "pcc_set_summary", "pcc_write_cells", "pcc_write_metadata", "pcc_clear_input", "pcc_adopt_prior",
-           "pcc_open_subtrees", "pcc_visit_cells", "pcc_shard_route_bitmaps", "pcc_shard_keys_from_bitmaps"]
+           "pcc_open_subtrees", "pcc_visit_cells", "pcc_shard_route_bitmaps", "pcc_shard_keys_from_bitmaps",
+           "pcc_release_device_cache"]
 
 
 class Options(C.Structure):
@@ -171,6 +172,8 @@ def lib():
         L.pcc_clear_input.argtypes = [vp]
         L.pcc_adopt_prior.argtypes = [vp, vp]
         L.pcc_visit_cells.argtypes = [vp, CELL_VISITOR, vp]
+        L.pcc_release_device_cache.argtypes = []
+        L.pcc_release_device_cache.restype = C.c_uint64
         _lib = L
     return _lib
 
@@ -178,6 +181,11 @@ def lib():
 def _check(rc: int):
     if rc != 0:
         raise PccError(rc, lib().pcc_last_error().decode(errors="replace"))
+
+
+def release_device_cache() -> int:
+    """Frees the device buffers closed converters left cached; returns the bytes freed."""
+    return int(lib().pcc_release_device_cache())
 
 
 def default_options(**kw) -> Options:

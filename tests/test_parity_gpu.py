@@ -125,6 +125,24 @@ def test_config2_uniform_10m_synthetic_on_device():
     assert st["levels"] == 2 and st["cells"] == 72
 
 
+def test_device_cache_reuse_and_release():
+    """A closed converter's large buffers are reused by the next one (same stats),
+    and pcc_release_device_cache frees them (a second call finds nothing)."""
+    import pcconv
+    stats = []
+    with tempfile.TemporaryDirectory() as d:
+        for _ in range(2):
+            c = pcconv.Converter(d, batch_size=10_000)
+            c.add_synthetic(7, 0, 5_000_000)
+            stats.append(c.build())
+            c.close()
+    for s in stats:
+        s.pop("build_ms", None)
+    assert stats[0] == stats[1]
+    assert pcconv.release_device_cache() >= 64 << 20   # at least the 80 MB input
+    assert pcconv.release_device_cache() == 0
+
+
 def test_duplicates_exact_limit_chains():
     """Thousands of exact duplicates (ties everywhere, multi-level spill chains)."""
     base = synth(13, 0, 20_000)
