@@ -243,6 +243,7 @@ private:
     int level0_bin();
     int run_level(uint32_t li);
     void run_dcap(Level* L);
+    void quiesce();
     void free_all();
     void free_prior();
 

@@ -57,8 +57,22 @@ namespace pcc {
 // (scripts/second_conv.py).  A failed hipMalloc empties the cache and retries.
 namespace {
 constexpr size_t kCacheMin = size_t(64) << 20;
-constexpr size_t kCacheMax = size_t(96) << 30;     // cached bytes per process, beyond: hipFree
+constexpr size_t kCacheMaxDefault = size_t(96) << 30;   // cached bytes per process, beyond: hipFree
 size_t g_dev_cached = 0;
+// PCC_DEVICE_CACHE_GB overrides the cap (0 disables the cache)
+size_t cache_max() {
+    static const size_t m = [] {
+        const char* e = getenv("PCC_DEVICE_CACHE_GB");
+        return e ? (size_t)(strtod(e, nullptr) * double(size_t(1) << 30)) : kCacheMaxDefault;
+    }();
+    return m;
+}
+// PCC_POISON_CACHE=1 (debug): a reused block is filled with 0xFF before it is
+// handed out, so a read of memory the build never wrote shows up in parity tests.
+bool poison_cache() {
+    const char* e = getenv("PCC_POISON_CACHE");
+    return e && e[0] == '1';
+}
 struct DevBlock { void* p; size_t bytes; int device; };
 std::mutex g_dev_mu;
 std::vector<DevBlock> g_dev_free;                 // cached, unused
@@ -74,7 +88,7 @@ static void* dev_alloc(size_t bytes) {
         size_t best = SIZE_MAX;
         for (size_t i = 0; i < g_dev_free.size(); i++) {   // the smallest cached block that fits, not far larger
             const DevBlock& b = g_dev_free[i];
-            if (b.device == dev && b.bytes >= bytes && b.bytes <= bytes + bytes / 4 + kCacheMin &&
+            if (b.device == dev && b.bytes >= bytes && b.bytes <= bytes + bytes / 4 + kCacheMin &&   // (not far larger)
                 (best == SIZE_MAX || b.bytes < g_dev_free[best].bytes))
                 best = i;
         }
@@ -83,6 +97,7 @@ static void* dev_alloc(size_t bytes) {
             g_dev_free.erase(g_dev_free.begin() + (ptrdiff_t)best);
             g_dev_cached -= b.bytes;
             g_dev_live[b.p] = b;
+            if (poison_cache()) { HIP_CHECK(hipMemset(b.p, 0xFF, b.bytes)); HIP_CHECK(hipDeviceSynchronize()); }
             return b.p;
         }
     }
@@ -122,7 +137,7 @@ static void dev_release(void* p) {
         }
         b = it->second;
         g_dev_live.erase(it);
-        if (b.bytes >= kCacheMin && g_dev_cached + b.bytes <= kCacheMax) {
+        if ((b.bytes >= kCacheMin || poison_cache()) && g_dev_cached + b.bytes <= cache_max()) {   // poison: cache all
             g_dev_free.push_back(b);
             g_dev_cached += b.bytes;
             return;
@@ -492,6 +507,94 @@ __device__ __forceinline__ uint32_t slot_route_errs(const SlotRoute& sr, bool la
     const int d = route_dest(sr.rc, cx, cy, cz, t, rerr);
     (void)route_dest(sr.rg, sr.rc.ix, sr.rc.iy, sr.rc.iz, sr.rc.u, gerr);
     return e | rerr | ((check_g && d >= 0) ? gerr : 0u);
+}
+
+// Slot, child slab and grandchild slab of a point of one slab (cell c, layer t):
+// the per-arrival routine of the slab kernels.  Same quotients as slot_route,
+// fewer instructions on the common path:
+//  * grandchild indices relative to the cell, lg = floor(q_g) - 4c in [0, 4):
+//    child octant bit lg >> 1 (= floor(q_g) >> 1 - 2c), grandchild bit lg & 1;
+//    grandchild layer u_g = trunc(z / cr_g), child layer u_c = u_g / 2 (C
+//    division truncates), so the grandchild select u_g - 2 u_c + 1 is always in
+//    [0, 2] and a valid child route implies a valid grandchild route;
+//  * the point's own layer trunc(z / cr) = u_g / 4: cr_g = cr / 4 exactly
+//    (metadata.rs:92,96 divide by powers of two), RN(z / cr_g) = 4 RN(z / cr),
+//    and trunc(trunc(a) / 4) = trunc(a / 4);
+//  * the operand range of div_rc from the exponents (frexp) and one max: the
+//    exact IEEE path also takes every non-finite coordinate.
+// Lanes outside the range take the exact divisions of slot_route (one ballot).
+struct SlabCtx {
+    int32_t cx, cy, cz, t;
+    int32_t uglo;    // lowest grandchild layer of the slab's points: u_g in [uglo, uglo + 6]
+    uint32_t uspan;  // 3 (t != 0) or 6 (t == 0): u_g - uglo <= uspan <=> the point's layer is t
+    uint32_t sel;    // per u_g - uglo, 4 bits: child select | grandchild select << 2
+    __device__ __forceinline__ SlabCtx(int32_t cx_, int32_t cy_, int32_t cz_, int32_t t_) : cx(cx_), cy(cy_), cz(cz_), t(t_) {
+        // trunc(z / cr) = t <=> u_g in [4t, 4t+3] (t > 0), [-3, 3] (t = 0), [4t-3, 4t] (t < 0)
+        uglo = t_ > 0 ? 4 * t_ : 4 * t_ - 3;
+        uspan = t_ == 0 ? 6u : 3u;
+        sel = 0;
+        for (uint32_t o = 0; o <= uspan; o++) {
+            const int32_t ug = uglo + (int32_t)o, uc = ug / 2;
+            sel |= (uint32_t)((uc - 2 * t_ + 1) | ((ug - 2 * uc + 1) << 2)) << (4 * o);
+        }
+    }
+};
+struct SlotDest {
+    int32_t ox, oy;   // offset index (hex.rs:45-51)
+    int32_t qa;       // axial q (hex.rs:18-24 to_axial of ox, oy)
+    bool layer_ok;    // the point's z layer is the slab's
+    int32_t d, g;     // child slab 0..23 / grandchild slab 0..23 inside it, -1: no valid route
+};
+__device__ __forceinline__ SlotDest slot_dest(float x, float y, float z, const LevelGeo& G, const SlabCtx& C) {
+    const int32_t ex = __builtin_amdgcn_frexp_expf(x), ey = __builtin_amdgcn_frexp_expf(y),
+                  ez = __builtin_amdgcn_frexp_expf(z);
+    bool amb = G.exact || !(fmaxf(fmaxf(fabsf(x), fabsf(y)), fabsf(z)) < 0x1p60f) || min(min(ex, ey), ez) < -58;
+    SlotDest S;
+    {   // hex.rs:67-85
+        const float xq = div_rc(x, G.crx, G.inv_crx);
+        const float yq = div_rc(y, G.cry, G.inv_cry);
+        const float tt = (kSqrt3 * yq) + 1.0f;
+        const float t1 = floorf(tt + xq);
+        const float t2 = tt - xq;
+        const float t3 = (2.0f * xq) + 1.0f;
+        S.qa = sat_i32(floorf(div_rc(t1 + t3, 3.0f, 0x1.555556p-2f)));
+        S.oy = (int32_t)(0u - (uint32_t)sat_i32(floorf(div_rc(t1 + t2, 3.0f, 0x1.555556p-2f))));
+        S.ox = S.qa + ((S.oy - (S.oy & 1)) >> 1);
+    }
+    const float qx = div_rc(x, G.csg, G.inv_csg), qy = div_rc(y, G.csg, G.inv_csg);
+    const float qz = div_rc(z, G.csg, G.inv_csg), qu = div_rc(z, G.crg, G.inv_crg);
+    amb |= fmaxf(fmaxf(fabsf(qx), fabsf(qy)), fmaxf(fabsf(qz), fabsf(qu))) >= 0x1p30f;
+    const int32_t lgx = sat_i32(floorf(qx)) - 4 * C.cx, lgy = sat_i32(floorf(qy)) - 4 * C.cy,
+                  lgz = sat_i32(floorf(qz)) - 4 * C.cz;
+    const uint32_t off = (uint32_t)(sat_i32(truncf(qu)) - C.uglo);
+    S.layer_ok = off <= C.uspan;
+    const uint32_t sl = __builtin_amdgcn_ubfe(C.sel, (off & 7u) * 4u, 4u);
+    const bool bad = (((lgx | lgy | lgz) & ~3) != 0) || !S.layer_ok;
+    const uint32_t octc = (uint32_t)((lgx >> 1) | (lgy & 2) | ((lgz & 2) << 1));
+    const uint32_t octg = (uint32_t)((lgx & 1) | ((lgy & 1) << 1) | ((lgz & 1) << 2));
+    S.d = bad ? -1 : (int32_t)((octc << 1) + octc + (sl & 3u));
+    S.g = bad ? -1 : (int32_t)((octg << 1) + octg + (sl >> 2));
+    if (__ballot(amb)) {
+        if (amb) {
+            const I3 hs = hex_from_world(x, y, z, G.cr);
+            const RouteIdx rc = route_idx_exact(G.csc, G.crc, x, y, z);
+            const RouteIdx rg = route_idx_exact(G.csg, G.crg, x, y, z);
+            S.ox = hs.x;
+            S.oy = hs.y;
+            S.layer_ok = hs.z == C.t;
+            S.qa = hs.x - (hs.y - (hs.y & 1)) / 2;
+            S.d = route_dest_nc(rc, C.cx, C.cy, C.cz, C.t);
+            S.g = S.d < 0 ? -1 : route_dest_nc(rg, rc.ix, rc.iy, rc.iz, rc.u);
+        }
+    }
+    return S;
+}
+// hex.rs:55-65 centre of the slot (z layer t: the point's own layer when it belongs to the slab)
+__device__ __forceinline__ void slot_centre(const SlotDest& S, float cr, float zt, float& X, float& Y, float& Z) {
+    const float qf = (float)S.qa, rf = (float)S.oy;
+    X = cr * ((kSqrt3 * qf) + ((kSqrt3 / 2.0f) * rf));
+    Y = ((cr * 3.0f) / 2.0f) * rf;
+    Z = zt;
 }
 
 // Buffer descriptor of a wave-uniform range.  Base and size are forced into
@@ -1734,6 +1837,8 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
     // reference slot: the one holding the cell centre (metadata.rs:104-106)
     const I3 c0 = hex_from_world(cell_pos1(cx, P.cs), cell_pos1(cy, P.cs), cell_pos1(cz, P.cs), G.cr);
     const int32_t rx = c0.x - P.tx / 2, ry = c0.y - P.ty / 2;
+    const SlabCtx SC{cx, cy, cz, t};
+    const float zt = (float)t * G.cr;   // slot centre z of the slab's layer (hex.rs:63)
     uint32_t err = 0;
     // buffer descriptors: this slab's arrivals and the contiguous region of its
     // 24 child slabs in the next arena (out-of-range offsets drop a store)
@@ -1806,22 +1911,21 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
             const bool v = jg < ng;
             const u32x4 q = rP.p(v ? jg * 16 : 0xFFFFFFFFu);
             const float x = __uint_as_float(q.x), y = __uint_as_float(q.y), z = __uint_as_float(q.z);
-            const SlotRoute sr = slot_route(x, y, z, G);
-            const int32_t lx = sr.sl.x - rx, ly = sr.sl.y - ry;
-            const bool layer_ok = sr.sl.z == t;
+            const SlotDest sd = slot_dest(x, y, z, G, SC);
+            const int32_t lx = sd.ox - rx, ly = sd.oy - ry;
+            const bool layer_ok = sd.layer_ok;
             const bool range_ok = lx >= 0 && ly >= 0 && lx < P.tx && ly < P.ty;
             const bool slotted = v && layer_ok && range_ok;
             float X, Y, Z;
-            hex_to_world(sr.sl, G.cr, X, Y, Z);
+            slot_centre(sd, G.cr, zt, X, Y, Z);
             const float d2 = dist2(X, Y, Z, x, y, z);
-            const int d = route_dest_nc(sr.rc, cx, cy, cz, t);
-            int32_t gn = route_dest_nc(sr.rg, sr.rc.ix, sr.rc.iy, sr.rc.iz, sr.rc.u);
+            const int d = sd.d;
+            int32_t gn = sd.g;
             const bool bad = v && (!layer_ok || !range_ok || d < 0 || (P.check_gchild && gn < 0));
             if (__ballot(bad)) {
-                if (bad) err |= slot_route_errs(sr, layer_ok, range_ok, cx, cy, cz, t, P.check_gchild);
+                if (bad) err |= slot_route_errs(slot_route(x, y, z, G), layer_ok, range_ok, cx, cy, cz, t, P.check_gchild);
             }
             const uint32_t dn = d < 0 ? 0u : (uint32_t)d;
-            if (d < 0) gn = -1;
             if (slotted) {
                 const unsigned long long e = ((unsigned long long)f2u(d2) << 33) | ((unsigned long long)dn << kJBits) |
                                              (wide ? 0u : ((uint32_t)(gn + 1) << 23)) | jg;
@@ -1855,28 +1959,33 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
         if (own.x == 0x7FC00001u) err |= 1u << 30;   // consume the prefetched loads here
         STAMP(12);
 #endif
-        const SlotRoute sr = slot_route(x, y, z, G);
-        const I3 sl = sr.sl;
-        const int32_t lx = sl.x - rx, ly = sl.y - ry;
-        const bool layer_ok = sl.z == t;
+        SlotDest sd;
+        if (ci < nchunks) {   // block-uniform: the last step only emits
+            sd = slot_dest(x, y, z, G, SC);
+        } else {
+            sd.ox = sd.oy = sd.qa = 0;
+            sd.layer_ok = false;
+            sd.d = sd.g = -1;
+        }
+        const int32_t lx = sd.ox - rx, ly = sd.oy - ry;
+        const bool layer_ok = sd.layer_ok;
         const bool range_ok = lx >= 0 && ly >= 0 && lx < P.tx && ly < P.ty;
         const bool slotted = valid && layer_ok && range_ok;
         const uint32_t local = slotted ? (uint32_t)(ly * P.tx + lx) : 0u;
         float X, Y, Z;
-        hex_to_world(sl, G.cr, X, Y, Z);
+        slot_centre(sd, G.cr, zt, X, Y, Z);
         const float d2 = dist2(X, Y, Z, x, y, z);
         uint32_t dn;
         int32_t gn;
         {
-            const int d = route_dest_nc(sr.rc, cx, cy, cz, t);
-            gn = route_dest_nc(sr.rg, sr.rc.ix, sr.rc.iy, sr.rc.iz, sr.rc.u);
+            const int d = sd.d;
+            gn = sd.g;
             // error codes only on the (never expected) failing lanes
             const bool bad = valid && (!layer_ok || !range_ok || d < 0 || (P.check_gchild && gn < 0));
             if (__ballot(bad)) {
-                if (bad) err |= slot_route_errs(sr, layer_ok, range_ok, cx, cy, cz, t, P.check_gchild);
+                if (bad) err |= slot_route_errs(slot_route(x, y, z, G), layer_ok, range_ok, cx, cy, cz, t, P.check_gchild);
             }
             dn = d < 0 ? 0u : (uint32_t)d;
-            if (d < 0) gn = -1;
         }
 #ifdef PCC_STAMPS
         if (d2 == 12345.0f) err |= 1u << 29;   // finish the math before the stamp
@@ -1912,11 +2021,8 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
         {
             int32_t gg = prv.g;
             if (wide && vd && gg == -2) {   // displaced occupant of a wide slab: route its payload
-                const SlotRoute sr = slot_route(__uint_as_float(prv.gp.x), __uint_as_float(prv.gp.y),
-                                                __uint_as_float(prv.gp.z), G);
-                uint32_t rerr = 0, gerr = 0;
-                const int dd = route_dest(sr.rc, cx, cy, cz, t, rerr);
-                gg = dd >= 0 ? route_dest(sr.rg, sr.rc.ix, sr.rc.iy, sr.rc.iz, sr.rc.u, gerr) : -1;
+                gg = slot_dest(__uint_as_float(prv.gp.x), __uint_as_float(prv.gp.y), __uint_as_float(prv.gp.z), G,
+                               SC).g;
             }
             if (!(PCC_ABL & 8) && vd && gg >= 0) atomicAdd(&S.gcnt[d * kDests + gg], 1u);
         }
@@ -2235,6 +2341,8 @@ __device__ __forceinline__ void small_process(const SlabParams& P, SmallLds& S, 
     // reference slot: the one holding the cell centre (metadata.rs:104-106)
     const I3 c0 = hex_from_world(cell_pos1(cx, P.cs), cell_pos1(cy, P.cs), cell_pos1(cz, P.cs), G.cr);
     const int32_t rx = c0.x - P.tx / 2, ry = c0.y - P.ty / 2;
+    const SlabCtx SC{cx, cy, cz, t};
+    const float zt = (float)t * G.cr;   // slot centre z of the slab's layer (hex.rs:63)
     uint32_t err = 0;
     const uint64_t lt = lanemask_lt();
     __syncthreads();
@@ -2260,9 +2368,9 @@ __device__ __forceinline__ void small_process(const SlabParams& P, SmallLds& S, 
         uint32_t dn = 0;
         if (ci < CH) {
             const float x = __uint_as_float(pp[ci].x), y = __uint_as_float(pp[ci].y), z = __uint_as_float(pp[ci].z);
-            const SlotRoute sr = slot_route(x, y, z, G);
-            const int32_t lx = sr.sl.x - rx, ly = sr.sl.y - ry;
-            const bool layer_ok = sr.sl.z == t;
+            const SlotDest sd = slot_dest(x, y, z, G, SC);
+            const int32_t lx = sd.ox - rx, ly = sd.oy - ry;
+            const bool layer_ok = sd.layer_ok;
             const bool range_ok = lx >= 0 && ly >= 0 && lx < P.tx && ly < P.ty;
             pending = valid && layer_ok && range_ok;
             local = pending ? (uint32_t)(ly * P.tx + lx) : 0u;
@@ -2271,16 +2379,15 @@ __device__ __forceinline__ void small_process(const SlabParams& P, SmallLds& S, 
                 self_em = true;
             }
             float X, Y, Z;
-            hex_to_world(sr.sl, G.cr, X, Y, Z);
+            slot_centre(sd, G.cr, zt, X, Y, Z);
             d2 = dist2(X, Y, Z, x, y, z);
-            const int d = route_dest_nc(sr.rc, cx, cy, cz, t);
-            int g = route_dest_nc(sr.rg, sr.rc.ix, sr.rc.iy, sr.rc.iz, sr.rc.u);
+            const int d = sd.d;
+            int g = sd.g;
             const bool bad = valid && (!layer_ok || !range_ok || d < 0 || (P.check_gchild && g < 0));
             if (__ballot(bad)) {
-                if (bad) err |= slot_route_errs(sr, layer_ok, range_ok, cx, cy, cz, t, P.check_gchild);
+                if (bad) err |= slot_route_errs(slot_route(x, y, z, G), layer_ok, range_ok, cx, cy, cz, t, P.check_gchild);
             }
             dn = d < 0 ? 0u : (uint32_t)d;
-            if (d < 0) g = -1;
             own_d[ci] = (int32_t)dn;
             own_g[ci] = g;
             rec_e[ci] = -1;
@@ -2537,6 +2644,8 @@ __global__ __launch_bounds__(64) void k_slab_wave(SlabParams P) {
         }
         const I3 c0 = hex_from_world(cell_pos1(cx, P.cs), cell_pos1(cy, P.cs), cell_pos1(cz, P.cs), G.cr);
         const int32_t rx = c0.x - P.tx / 2, ry = c0.y - P.ty / 2;
+        const SlabCtx SC{cx, cy, cz, t};
+        const float zt = (float)t * G.cr;   // slot centre z of the slab's layer (hex.rs:63)
         uint32_t* gcap_s = P.gcap + (uint64_t)s * kDests * kDests;
         uint32_t err = 0;
         __syncthreads();   // one wave: orders the LDS initialisation
@@ -2551,23 +2660,22 @@ __global__ __launch_bounds__(64) void k_slab_wave(SlabParams P) {
             const uint32_t j = c * 64 + lane;
             const bool valid = j < n;
             const float x = __uint_as_float(pp[c].x), y = __uint_as_float(pp[c].y), z = __uint_as_float(pp[c].z);
-            const SlotRoute sr = slot_route(x, y, z, G);
-            const int32_t lx = sr.sl.x - rx, ly = sr.sl.y - ry;
-            const bool layer_ok = sr.sl.z == t;
+            const SlotDest sd = slot_dest(x, y, z, G, SC);
+            const int32_t lx = sd.ox - rx, ly = sd.oy - ry;
+            const bool layer_ok = sd.layer_ok;
             const bool range_ok = lx >= 0 && ly >= 0 && lx < P.tx && ly < P.ty;
             bool pending = valid && layer_ok && range_ok;
             const uint32_t local = pending ? (uint32_t)(ly * P.tx + lx) : 0u;
             float X, Y, Z;
-            hex_to_world(sr.sl, G.cr, X, Y, Z);
+            slot_centre(sd, G.cr, zt, X, Y, Z);
             const float d2 = dist2(X, Y, Z, x, y, z);
-            const int d = route_dest_nc(sr.rc, cx, cy, cz, t);
-            int g = route_dest_nc(sr.rg, sr.rc.ix, sr.rc.iy, sr.rc.iz, sr.rc.u);
+            const int d = sd.d;
+            int g = sd.g;
             const bool bad = valid && (!layer_ok || !range_ok || d < 0 || (P.check_gchild && g < 0));
             if (__ballot(bad)) {
-                if (bad) err |= slot_route_errs(sr, layer_ok, range_ok, cx, cy, cz, t, P.check_gchild);
+                if (bad) err |= slot_route_errs(slot_route(x, y, z, G), layer_ok, range_ok, cx, cy, cz, t, P.check_gchild);
             }
             const uint32_t dn = d < 0 ? 0u : (uint32_t)d;
-            if (d < 0) g = -1;
             own_d[c] = (int32_t)dn;
             own_g[c] = g;
             int e = 0;
@@ -3241,7 +3349,16 @@ void Engine::ev_collect() {
     ev_used_.clear();
 }
 
+// Blocks go back to the process-wide cache, where another converter (any
+// stream) can take them at once: nothing queued on this engine's streams may
+// still touch them (hipFree synchronised implicitly, the cache does not).
+void Engine::quiesce() {
+    if (stream_) (void)hipStreamSynchronize(stream_);
+    if (copy_) (void)hipStreamSynchronize(copy_);
+}
+
 void Engine::free_all() {
+    quiesce();
     for (auto& u : ev_used_) { ev_pool_.push_back(u.second.first); ev_pool_.push_back(u.second.second); }
     ev_used_.clear();
     for (hipEvent_t e : ev_pool_) (void)hipEventDestroy(e);
@@ -3277,6 +3394,7 @@ void Engine::free_all() {
 }
 
 void Engine::free_prior() {
+    quiesce();
     dev_release(d_seeds_);
     d_seeds_ = nullptr;
     dev_release(d_inj_);

@@ -865,7 +865,9 @@ bool read_ply(const std::string& path, PlyResult& out, std::string& err, const P
     if (!std::getline(f, line) || line.rfind("ply", 0) != 0) { err = path + ": not a PLY file"; return false; }
     enum { ASCII, LE, BE } enc = LE;
     std::vector<Prop> vprops;
-    bool in_vertex = false, seen_vertex = false, vertex_first = true;
+    // ply.rs:36-73 reads `vertex` records straight after the header, whatever
+    // elements the header declares before it (their bytes are read as vertices)
+    bool in_vertex = false, seen_vertex = false;
     uint64_t nvert = 0;
     while (std::getline(f, line)) {
         if (!line.empty() && line.back() == '\r') line.pop_back();
@@ -883,7 +885,6 @@ bool read_ply(const std::string& path, PlyResult& out, std::string& err, const P
             ls >> name >> cnt;
             in_vertex = name == "vertex";
             if (in_vertex) { nvert = cnt; seen_vertex = true; }
-            else if (!seen_vertex) vertex_first = false;
         } else if (kw == "property" && in_vertex) {
             std::string t;
             ls >> t;
@@ -905,7 +906,6 @@ bool read_ply(const std::string& path, PlyResult& out, std::string& err, const P
         }
     }
     if (!seen_vertex) { err = path + ": no vertex element"; return false; }   // ply.rs:37 unwraps this
-    if (!vertex_first) { err = path + ": vertex must be the first PLY element"; return false; }
     out.vertex_count = nvert;
     out.points.clear();
     if (enc == ASCII) {   // ply.rs:43-51: lines are parsed but never pushed into the batch

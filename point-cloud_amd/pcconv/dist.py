@@ -757,6 +757,8 @@ class HipShardOps:
             if c is not None:
                 c.close()
         self.conv = self.conv_lead = self.conv_sub = None
+        # the library's device cache is invisible to PyTorch's allocator and RCCL
+        pcconv.release_device_cache()
         if self._tmp is not None:
             self._tmp.cleanup()
 

@@ -291,3 +291,35 @@ def test_file_in_pieces_equals_one_call(tmp_path):
     c.build()
     assert gpu_digest(c) == dref
     c.close()
+
+
+def test_ply_vertex_not_first_element():
+    """ply.rs:36-73 reads `vertex` records straight after the header, whatever
+    element the header declares first: the bytes of a leading `extra` element
+    (12-byte records: three finite floats) are read as vertex records (x, y, z
+    float; red, green, blue, alpha uchar), and the last vertex records are never
+    reached.  Parity unpinned: no reference fixture, the expected points come
+    from reinterpreting the file's bytes here."""
+    rng = np.random.default_rng(9)
+    n, k = 40_000, 3_000
+    extra = rng.uniform(-800, 800, (k, 3)).astype("<f4")
+    vert = np.zeros(n, dtype=POINT_DTYPE)
+    for a in "xyz":
+        vert[a] = rng.uniform(-900, 900, n).astype(np.float32)
+    vert["rgba"] = rng.integers(0, 256, (n, 4), dtype=np.uint8)
+    hdr = ("ply\nformat binary_little_endian 1.0\nelement extra %d\nproperty float a\nproperty float b\n"
+           "property float c\nelement vertex %d\nproperty float x\nproperty float y\nproperty float z\n"
+           "property uchar red\nproperty uchar green\nproperty uchar blue\nproperty uchar alpha\n"
+           "element face 0\nproperty list uchar int vertex_indices\nend_header\n") % (k, n)
+    payload = extra.tobytes() + vert.tobytes()
+    expect = np.frombuffer(payload[:16 * n], dtype=POINT_DTYPE).copy()
+    with tempfile.TemporaryDirectory() as td:
+        a = os.path.join(td, "x.ply")
+        with open(a, "wb") as f:
+            f.write(hdr.encode())
+            f.write(payload)
+        out, ref = os.path.join(td, "out"), os.path.join(td, "ref")
+        _cli([a], out)
+        _oracle_dir(ref, [expect])
+        d, mg, mo = compare_dirs(out, ref, fast=False)
+        assert d == [] and mg == mo

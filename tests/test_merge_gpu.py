@@ -133,3 +133,28 @@ def test_stale_cells_merge_like_the_reference(meta):
         assert d == [], d
         assert mg == mo
         assert mg["number_of_points"] == len(new[0])
+
+
+def test_poisoned_device_cache_parity_and_merge():
+    """PCC_POISON_CACHE=1 fills every block the device cache hands out again with
+    0xFF: a read of memory the build never wrote then changes cell contents.  Two
+    rounds of a plain build and a merge (the second round runs on recycled blocks)
+    against the oracle's digests."""
+    import pcconv
+    pcconv.release_device_cache()
+    old = os.environ.get("PCC_POISON_CACHE")
+    os.environ["PCC_POISON_CACHE"] = "1"
+    try:
+        a = synth(25, 1, 300_000)
+        b = synth(26, 0, 200_000)
+        for _ in range(2):
+            _merge_check([a], [b[:120_000], b[120_000:]], prior_by="gpu", fast=True)
+            files, cfg, batch = _case(7)
+            first, second = _split(files, 7)
+            _merge_check([_to_np(f) for f in first], [_to_np(f) for f in second], cfg=cfg, batch=batch)
+    finally:
+        if old is None:
+            os.environ.pop("PCC_POISON_CACHE", None)
+        else:
+            os.environ["PCC_POISON_CACHE"] = old
+        pcconv.release_device_cache()

@@ -170,8 +170,8 @@ def test_sparse_bbox_far_outliers():
 
 
 def test_sparse_bbox_small_cells_many_occupied():
-    """Tiny max_cell_size: ~2.5 * 10^5 occupied level-0 cells over a 2^30-cell box."""
-    pts = synth(52, 0, 250_000, lo=-500.0, ext=1000.0)
+    """Tiny max_cell_size: ~4 * 10^5 occupied level-0 cells over a 2^30-cell box."""
+    pts = synth(52, 0, 400_000, lo=-500.0, ext=1000.0)
     _check([pts], cfg=dict(cell_point_overflow_limit=4, sub_grid_dimension=2, max_cell_size=1.0), fast=True,
            base=_shm())
 
