@@ -42,6 +42,11 @@ def parse():
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--cpu-full", action="store_true",
                     help="cpu_baseline = mode (B) over the WHOLE workload, per level-0 part, summed (minutes of CPU)")
+    ap.add_argument("--cpu-mode-a", action="store_true",
+                    help="also time SURVEY 8d mode (A): the oracle with the reference's LRU-100 cell cache and "
+                         ".bin write-back (converter.rs:92,160-216); full run up to 10M points, else a prefix "
+                         "capped at --cpu-cap seconds")
+    ap.add_argument("--cpu-cap", type=float, default=60.0, help="mode (A) time cap (s) beyond 10M points")
     ap.add_argument("--merge-prior", type=int, default=0,
                     help="config 5: merge --points new points (seed --seed) into a cloud built from this many "
                          "config-4 points (seed 4); 0 = fresh build")
@@ -85,6 +90,66 @@ def cpu_full_mode_b(args):
                 **host_cpu())
 
 
+def cpu_mode_a(args):
+    """SURVEY.md §8d mode (A), the faithful reference configuration: the sequential
+    C restatement with the reference's LRU cache of 100 cells (converter.rs:92),
+    every evicted cell written to a .bin file on the local disk and read back when
+    touched again (converter.rs:160-216), 10 000-point batches.  Up to 10M points
+    the whole run; beyond, the prefix converted within --cpu-cap seconds (points/s
+    over that prefix).  Timed like the reference's "Finished converting" log
+    (lib.rs:56-59): the final flush of the cached cells (converter.rs:241-246) is
+    reported apart.  Config 5: the existing cloud (converted untimed, in memory,
+    and written to the directory) is read lazily from disk, as the reference does."""
+    import shutil
+    import tempfile
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from oracle_ctypes import Oracle, synth
+    tmp = tempfile.mkdtemp(prefix="pcc_mode_a_", dir="/tmp")
+    try:
+        if args.merge_prior:   # the existing cloud: a config-4 prefix, same size ratio as the run
+            n0 = min(args.merge_prior, 10 * 10_000_000)
+            o = Oracle()
+            for a in range(0, n0, 1_000_000):
+                o.add_file(synth(4, 0, min(1_000_000, n0 - a), first=a))
+            o.write(tmp)
+            o.close()
+        full = args.points <= 10_000_000
+        cap = float("inf") if full else args.cpu_cap
+        o = Oracle()
+        o.set_lru(tmp, 100)
+        done, conv = 0, 0.0
+        chunk = 1_000_000
+        while done < args.points and conv < cap:
+            m = min(chunk, args.points - done)
+            pts = synth(args.seed, args.kind, m, first=done)
+            for b in range(0, m, 10_000):
+                t0 = time.perf_counter()
+                o.add_batch(pts[b:b + 10_000])
+                conv += time.perf_counter() - t0
+                done += min(10_000, m - b)
+                if conv >= cap:
+                    break
+        st = o.lru_stats()
+        t0 = time.perf_counter()
+        o.write(tmp)
+        flush = time.perf_counter() - t0
+        err = o.error
+        o.close()
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    what = "whole run" if done == args.points else f"prefix of {done} of {args.points} points ({cap:.0f} s cap)"
+    return dict({"value": done / conv, "unit": "points/s", "cores": 1, "kind": "port", "mode": "A",
+                 "sample": f"mode (A): {what}, seed {args.seed}, sequential C restatement with the LRU-100 cell cache "
+                           f"and .bin write-back to local disk ({st['evictions']} evictions, {st['loads']} reloads), "
+                           f"conversion {conv:.1f} s, final flush {flush:.1f} s (not in the rate, as lib.rs:56-59)"
+                           + (f"; existing cloud of {n0} config-4 points read lazily from disk" if args.merge_prior else ""),
+                 "points_reached": done, "flush_s": flush, "error": err}, **host_cpu())
+
+
+# full-run mode (B) measurement of config 4 on the GPU box (bench.py --cpu-full, round 2)
+FULL_MODE_B = os.path.join(ROOT, "profiles", "r2_cpu_full_mode_b_1b.json")
+
+
 def cpu_baseline(args):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from oracle_ctypes import Oracle, synth
@@ -102,11 +167,24 @@ def cpu_baseline(args):
         dt = time.perf_counter() - t0
         lv = o.hierarchies
         o.close()
-        return dict({"value": n / dt, "unit": "points/s", "cores": 1, "kind": "port",
-                     "sample": f"{n} uniform points (seed {args.seed}) in the level-1 cell [0,500)^3 at the density of "
-                               f"the full {args.points}-point run ({lv} levels, as the full run), sequential C "
-                               f"restatement (oracle/pcc_oracle.c, in-memory cells = mode (B), 10 000-point "
-                               f"batches), {dt:.1f} s"}, **host_cpu())
+        rec = dict({"value": n / dt, "unit": "points/s", "cores": 1, "kind": "port",
+                    "sample": f"{n} uniform points (seed {args.seed}) in the level-1 cell [0,500)^3 at the density of "
+                              f"the full {args.points}-point run ({lv} levels, as the full run), sequential C "
+                              f"restatement (oracle/pcc_oracle.c, in-memory cells = mode (B), 10 000-point "
+                              f"batches), {dt:.1f} s"}, **host_cpu())
+        # the sample is friendlier than the whole run: state the full run's rate beside it
+        try:
+            with open(FULL_MODE_B) as f:
+                fb = json.load(f)
+            if args.points == 1_000_000_000 and args.seed == 4 and "config4" in fb["config"]["workload"]:
+                full = fb["cpu_baseline"]["value"]
+                rec["full_run_mode_b"] = {"value": full, "source": os.path.relpath(FULL_MODE_B, ROOT),
+                                          "sample_over_full": rec["value"] / full,
+                                          "note": "all 1e9 points through mode (B) on the GPU box's host, "
+                                                  "8 level-0 parts timed separately and summed"}
+        except (OSError, ValueError, KeyError):
+            pass
+        return rec
     if args.kind == 0 and args.merge_prior:
         # Config 5's shape at the full run's density: the existing cloud's and the
         # new points' share of one level-1 cell, [0, 500)^3 (1/64 of each, the
@@ -314,6 +392,9 @@ def main():
     elif args.cpu_sample > 0:
         res["cpu_baseline"] = cpu_baseline(args)
         res["speedup_vs_cpu"] = res["value"] / res["cpu_baseline"]["value"]
+    if args.cpu_mode_a:
+        res["cpu_baseline_mode_a"] = cpu_mode_a(args)
+        res["speedup_vs_mode_a"] = res["value"] / res["cpu_baseline_mode_a"]["value"]
     print(json.dumps(res), flush=True)
 
 

@@ -55,6 +55,8 @@ def lib():
         L.orc_hierarchies.restype = C.c_uint32
         L.orc_synth.argtypes = [C.c_uint64, C.c_int, C.c_uint64, C.c_uint64, C.c_float, C.c_float, C.c_void_p]
         L.orc_load.argtypes = [C.c_void_p, C.c_char_p]
+        L.orc_set_lru.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32]
+        L.orc_lru_stats.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
         L.orc_set_level_range.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32]
         L.orc_pending_count.argtypes = [C.c_void_p]
         L.orc_pending_count.restype = C.c_uint64
@@ -102,6 +104,17 @@ class Oracle:
     def add_batch(self, pts: np.ndarray):
         pts = np.ascontiguousarray(pts, dtype=POINT_DTYPE)
         lib().orc_add_batch(self._h, pts.ctypes.data, len(pts))
+
+    def set_lru(self, out_dir: str, capacity: int = 100):
+        """Mode (A): at most `capacity` cells in memory
+        (converter.rs:92), evicted cells written back to out_dir and read back
+        when touched again (converter.rs:160-216).  write() must use out_dir."""
+        lib().orc_set_lru(self._h, out_dir.encode(), capacity)
+
+    def lru_stats(self) -> dict:
+        st = (C.c_uint64 * 2)()
+        lib().orc_lru_stats(self._h, st)
+        return {"loads": int(st[0]), "evictions": int(st[1])}
 
     def set_level_range(self, root: int, max_levels: int):
         """Batches enter at level `root`; with max_levels > 0 the points forwarded

@@ -190,6 +190,8 @@ typedef struct {
     hmap grid;                             /* OffsetIndex -> index into gpts */
     plist gpts;
     bucket b[8]; int nb;
+    int evicted;                           /* mode (A): written back, contents freed */
+    uint64_t last_use;                     /* mode (A): LRU clock of the last access */
 } cell;
 
 typedef struct {
@@ -208,6 +210,13 @@ typedef struct {
     uint32_t batch_no;
     struct pend { orc_point p; uint32_t batch; ivec3 idx; uint32_t key; } *pend;
     size_t npend, cappend;
+    /* mode (A): converter.rs:92 LRU of lru_cap cells, an evicted
+     * cell written back to lru_dir (converter.rs:160-178, 209-216) and read back
+     * when it is touched again (converter.rs:181-207) */
+    char* lru_dir;
+    uint32_t lru_cap;
+    uint64_t lru_clock, lru_loads, lru_evictions;
+    size_t* res; size_t nres;              /* indices of the resident cells */
 } orc_conv;
 
 orc_conv* orc_new(const orc_config* cfg) {
@@ -224,7 +233,7 @@ void orc_free(orc_conv* c) {
         for (int j = 0; j < k->nb; j++) pl_free(&k->b[j].pts);
         free(k);
     }
-    free(c->cellv); hm_free(&c->cells); free(c->pend); free(c);
+    free(c->cellv); hm_free(&c->cells); free(c->pend); free(c->lru_dir); free(c->res); free(c);
 }
 
 void orc_set_level_range(orc_conv* c, uint32_t root, uint32_t maxl) {
@@ -253,12 +262,14 @@ void orc_pending_get(const orc_conv* c, orc_point* p, uint32_t* batch, int32_t* 
     }
 }
 
+static cell* lru_touch(orc_conv* c, uint32_t i, int fresh);
+
 /* converter.rs:187-207 (create branch) + cell.rs:43-49 + Header::new cell.rs:264-274 */
 static cell* get_cell(orc_conv* c, uint32_t h, ivec3 idx) {
     int32_t k[4] = { (int32_t)h, idx.x, idx.y, idx.z };
     int ins;
     uint32_t* v = hm_get_or_insert(&c->cells, k, &ins);
-    if (!ins) return c->cellv[*v];
+    if (!ins) return c->lru_cap ? lru_touch(c, *v, 0) : c->cellv[*v];
     cell* n = (cell*)calloc(1, sizeof(cell));
     n->h = h; n->idx = idx;
     n->size = orc_cell_size(&c->cfg, h);
@@ -271,7 +282,7 @@ static cell* get_cell(orc_conv* c, uint32_t h, ivec3 idx) {
     }
     *v = (uint32_t)c->ncells;
     c->cellv[c->ncells++] = n;
-    return n;
+    return c->lru_cap ? lru_touch(c, *v, 1) : n;
 }
 
 /* cell.rs:70-94 Cell::add_point ; returns 1 and sets *out when a point overflows */
@@ -548,8 +559,10 @@ int orc_write(const orc_conv* c, const char* dir) {
         snprintf(path, sizeof path, "%s/h_%u", dir, h);
         if (mkdir(path, 0755) != 0 && errno != EEXIST) return -errno;
     }
+    if (c->lru_cap && strcmp(dir, c->lru_dir) != 0) return -EINVAL;   /* evicted cells live in lru_dir */
     for (size_t i = 0; i < c->ncells; i++) {
         const cell* k = c->cellv[i];
+        if (k->evicted) continue;   /* converter.rs:218-224 save_cache: the resident cells */
         snprintf(path, sizeof path, "%s/h_%u/c_%d_%d_%d.bin", dir, k->h, k->idx.x, k->idx.y, k->idx.z);
         int r = write_cell(k, path);
         if (r) return r;
@@ -557,6 +570,72 @@ int orc_write(const orc_conv* c, const char* dir) {
     snprintf(path, sizeof path, "%s/metadata.json", dir);
     return write_metadata(c, path);
 }
+
+/* ---------------------------------------------------------------- mode (A) */
+static int parse_cell_file(cell* k, const char* path);
+static void cell_path(const orc_conv* c, const cell* k, char* path, size_t n) {
+    snprintf(path, n, "%s/h_%u/c_%d_%d_%d.bin", c->lru_dir, k->h, k->idx.x, k->idx.y, k->idx.z);
+}
+static void cell_release(cell* k) {
+    hm_free(&k->grid); pl_free(&k->gpts);
+    for (int j = 0; j < k->nb; j++) pl_free(&k->b[j].pts);
+    k->nb = 0;
+}
+/* caches 0.2.8 LRUCache as converter.rs:160-178 uses it: a missing cell is
+ * loaded or created and put (evicting the least recently used one, written
+ * back first when the cache is full), every access makes it the most recent */
+static cell* lru_touch(orc_conv* c, uint32_t i, int fresh) {
+    cell* k = c->cellv[i];
+    if (!fresh && !k->evicted) { k->last_use = ++c->lru_clock; return k; }
+    if (c->nres == c->lru_cap) {
+        size_t m = 0;
+        for (size_t r = 1; r < c->nres; r++)
+            if (c->cellv[c->res[r]]->last_use < c->cellv[c->res[m]]->last_use) m = r;
+        cell* o = c->cellv[c->res[m]];
+        char path[4096];
+        snprintf(path, sizeof path, "%s/h_%u", c->lru_dir, o->h);
+        mkdir(path, 0755);   /* converter.rs:141-158 created it */
+        cell_path(c, o, path, sizeof path);
+        if (write_cell(o, path)) c->error = 2;
+        cell_release(o);
+        o->evicted = 1;
+        c->lru_evictions++;
+        c->res[m] = c->res[--c->nres];
+    }
+    {   /* converter.rs:181-207 load_or_create_cell: the cell's file when there is one */
+        char path[4096];
+        cell_path(c, k, path, sizeof path);
+        if (!fresh) hm_init(&k->grid, 3, 1024);
+        struct stat sb;
+        if (!fresh || stat(path, &sb) == 0) {
+            if (parse_cell_file(k, path)) c->error = 2;
+            c->lru_loads++;
+        }
+        k->evicted = 0;
+    }
+    c->res[c->nres++] = i;
+    k->last_use = ++c->lru_clock;
+    return k;
+}
+/* Mode (A): keep at most `cap` cells in memory, write evicted cells to `dir`
+ * (the output directory) and read them back when touched again.  A cloud
+ * already in `dir` is the starting state, read lazily like the reference
+ * (metadata.json now, each cell file when the cell is first touched); no
+ * orc_load with this mode. */
+static int load_metadata(orc_conv* c, const char* path);
+void orc_set_lru(orc_conv* c, const char* dir, uint32_t cap) {
+    char path[4096];
+    snprintf(path, sizeof path, "%s/metadata.json", dir);
+    struct stat sb;
+    if (stat(path, &sb) == 0 && load_metadata(c, path)) c->error = 2;   /* lib.rs:86-101 */
+    free(c->lru_dir);
+    c->lru_dir = strdup(dir);
+    c->lru_cap = cap;
+    c->res = (size_t*)realloc(c->res, (cap + 1) * sizeof(size_t));
+    c->nres = 0;
+    mkdir(dir, 0755);
+}
+void orc_lru_stats(const orc_conv* c, uint64_t out[2]) { out[0] = c->lru_loads; out[1] = c->lru_evictions; }
 
 /* ---------------------------------------------------------------- existing cloud */
 /* lib.rs:86-101 load_metadata + converter.rs:187-207 load_or_create_cell +
@@ -620,21 +699,14 @@ static int load_metadata(orc_conv* c, const char* path) {
     return ok ? 0 : -EINVAL;
 }
 
-static int load_cell_file(orc_conv* c, const char* path) {
-    char* s; size_t len;
-    int r = read_all(path, &s, &len);
-    if (r) return r;
-    const uint8_t* b = (const uint8_t*)s;
+/* Cell::read_from into an existing cell struct (its id and header geometry set) */
+static int parse_cell_bytes(cell* k, const uint8_t* b, size_t len) {
     size_t off = 48;
-    if (len < 49) { free(s); return -EINVAL; }
-    uint32_t h, total, number, overflow;
-    ivec3 idx;
-    memcpy(&h, b, 4); memcpy(&idx.x, b + 4, 4); memcpy(&idx.y, b + 8, 4); memcpy(&idx.z, b + 12, 4);
-    memcpy(&total, b + 16, 4); memcpy(&number, b + 20, 4); memcpy(&overflow, b + 24, 4);
-    cell* k = get_cell(c, h, idx);
-    k->total = total; k->number = number; k->overflow = overflow;
+    if (len < 49) return -EINVAL;
+    memcpy(&k->total, b + 16, 4); memcpy(&k->number, b + 20, 4); memcpy(&k->overflow, b + 24, 4);
+    uint32_t number = k->number;
     float cr = k->sub / 2.0f; /* cell.rs:276-278 */
-    if (off + 16ull * number + 1 > len) { free(s); return -EINVAL; }
+    if (off + 16ull * number + 1 > len) return -EINVAL;
     for (uint32_t i = 0; i < number; i++, off += 16) {
         orc_point pt;
         memcpy(&pt, b + off, 16);
@@ -645,9 +717,9 @@ static int load_cell_file(orc_conv* c, const char* path) {
         else k->gpts.p[*v] = pt;
     }
     uint8_t nb = b[off++];
-    if (nb > 8) { free(s); return -EINVAL; }
+    if (nb > 8) return -EINVAL;
     for (uint8_t j = 0; j < nb; j++) {
-        if (off + 16 > len) { free(s); return -EINVAL; }
+        if (off + 16 > len) return -EINVAL;
         bucket* bk = &k->b[k->nb++];
         memset(bk, 0, sizeof *bk);
         uint32_t n;
@@ -655,7 +727,7 @@ static int load_cell_file(orc_conv* c, const char* path) {
         memcpy(&n, b + off + 12, 4);
         off += 16;
         if (n == 0) { bk->state = 2; continue; }
-        if (off + 16ull * n > len) { free(s); return -EINVAL; }
+        if (off + 16ull * n > len) return -EINVAL;
         bk->state = 1;
         for (uint32_t i = 0; i < n; i++, off += 16) {
             orc_point pt;
@@ -663,8 +735,30 @@ static int load_cell_file(orc_conv* c, const char* path) {
             pl_push(&bk->pts, pt);
         }
     }
-    free(s);
     return off == len ? 0 : -EINVAL;
+}
+static int parse_cell_file(cell* k, const char* path) {
+    char* s; size_t len;
+    int r = read_all(path, &s, &len);
+    if (r) return r;
+    r = parse_cell_bytes(k, (const uint8_t*)s, len);
+    free(s);
+    return r;
+}
+
+static int load_cell_file(orc_conv* c, const char* path) {
+    char* s; size_t len;
+    int r = read_all(path, &s, &len);
+    if (r) return r;
+    const uint8_t* b = (const uint8_t*)s;
+    if (len < 49) { free(s); return -EINVAL; }
+    uint32_t h;
+    ivec3 idx;
+    memcpy(&h, b, 4); memcpy(&idx.x, b + 4, 4); memcpy(&idx.y, b + 8, 4); memcpy(&idx.z, b + 12, 4);
+    cell* k = get_cell(c, h, idx);
+    r = parse_cell_bytes(k, b, len);
+    free(s);
+    return r;
 }
 
 /* Loads dir/metadata.json (config, counters, bbox) and every h_{h}/c_*.bin for

@@ -179,6 +179,9 @@ constexpr int kDenseClaim = 2048;
 #ifndef PCC_SLAB_PF
 #define PCC_SLAB_PF 2
 #endif
+#ifndef PCC_L0_SWZ
+#define PCC_L0_SWZ 1        // level-0 pass 1: padded pair-count rows
+#endif
 #ifndef PCC_STREAM_MAX
 #define PCC_STREAM_MAX 24576
 #endif
@@ -545,10 +548,12 @@ struct SlotDest {
     bool layer_ok;    // the point's z layer is the slab's
     int32_t d, g;     // child slab 0..23 / grandchild slab 0..23 inside it, -1: no valid route
 };
-__device__ __forceinline__ SlotDest slot_dest(float x, float y, float z, const LevelGeo& G, const SlabCtx& C) {
+// Without the exact path: `amb` flags the lanes slot_dest_exact must redo.
+__device__ __forceinline__ SlotDest slot_dest_fast(float x, float y, float z, const LevelGeo& G, const SlabCtx& C,
+                                                   bool& amb) {
     const int32_t ex = __builtin_amdgcn_frexp_expf(x), ey = __builtin_amdgcn_frexp_expf(y),
                   ez = __builtin_amdgcn_frexp_expf(z);
-    bool amb = G.exact || !(fmaxf(fmaxf(fabsf(x), fabsf(y)), fabsf(z)) < 0x1p60f) || min(min(ex, ey), ez) < -58;
+    amb = G.exact || !(fmaxf(fmaxf(fabsf(x), fabsf(y)), fabsf(z)) < 0x1p60f) || min(min(ex, ey), ez) < -58;
     SlotDest S;
     {   // hex.rs:67-85
         const float xq = div_rc(x, G.crx, G.inv_crx);
@@ -574,18 +579,26 @@ __device__ __forceinline__ SlotDest slot_dest(float x, float y, float z, const L
     const uint32_t octg = (uint32_t)((lgx & 1) | ((lgy & 1) << 1) | ((lgz & 1) << 2));
     S.d = bad ? -1 : (int32_t)((octc << 1) + octc + (sl & 3u));
     S.g = bad ? -1 : (int32_t)((octg << 1) + octg + (sl >> 2));
+    return S;
+}
+// The exact IEEE divisions of slot_route for one lane.
+__device__ __forceinline__ void slot_dest_exact(float x, float y, float z, const LevelGeo& G, const SlabCtx& C,
+                                                SlotDest& S) {
+    const I3 hs = hex_from_world(x, y, z, G.cr);
+    const RouteIdx rc = route_idx_exact(G.csc, G.crc, x, y, z);
+    const RouteIdx rg = route_idx_exact(G.csg, G.crg, x, y, z);
+    S.ox = hs.x;
+    S.oy = hs.y;
+    S.layer_ok = hs.z == C.t;
+    S.qa = hs.x - (hs.y - (hs.y & 1)) / 2;
+    S.d = route_dest_nc(rc, C.cx, C.cy, C.cz, C.t);
+    S.g = S.d < 0 ? -1 : route_dest_nc(rg, rc.ix, rc.iy, rc.iz, rc.u);
+}
+__device__ __forceinline__ SlotDest slot_dest(float x, float y, float z, const LevelGeo& G, const SlabCtx& C) {
+    bool amb;
+    SlotDest S = slot_dest_fast(x, y, z, G, C, amb);
     if (__ballot(amb)) {
-        if (amb) {
-            const I3 hs = hex_from_world(x, y, z, G.cr);
-            const RouteIdx rc = route_idx_exact(G.csc, G.crc, x, y, z);
-            const RouteIdx rg = route_idx_exact(G.csg, G.crg, x, y, z);
-            S.ox = hs.x;
-            S.oy = hs.y;
-            S.layer_ok = hs.z == C.t;
-            S.qa = hs.x - (hs.y - (hs.y & 1)) / 2;
-            S.d = route_dest_nc(rc, C.cx, C.cy, C.cz, C.t);
-            S.g = S.d < 0 ? -1 : route_dest_nc(rg, rc.ix, rc.iy, rc.iz, rc.u);
-        }
+        if (amb) slot_dest_exact(x, y, z, G, C, S);
     }
     return S;
 }
@@ -1218,10 +1231,13 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_down6g(const Point* __restrict_
     __shared__ alignas(16) uint8_t wcnt[R][kL0RW];
     __shared__ alignas(16) uint16_t wpre[R][kL0RW];
     __shared__ uint32_t dbase[R], gofs[R];
-    __shared__ uint32_t h[R * R5];
+    // pair counts, row d6 padded to R5 + 1 words: the lanes of a wave share few
+    // d5 values, and with rows of exactly R5 words they all hit bank d5
+    constexpr int HP = PCC_L0_SWZ ? R5 + 1 : R5;
+    __shared__ uint32_t h[R * HP];
     const uint32_t tid = threadIdx.x, w = tid / 64, lane = tid & 63, g = blockIdx.x;
     const float4* p4 = reinterpret_cast<const float4*>(in);
-    for (int i = tid; i < R * R5; i += kL0BS) h[i] = 0;
+    for (int i = tid; i < R * HP; i += kL0BS) h[i] = 0;
     for (int i = tid; i < kL0RW * R / 4; i += kL0BS) reinterpret_cast<uint32_t*>(&wcnt[0][0])[i] = 0;
     const uint64_t lt = lanemask_lt();
     uint32_t err = 0;
@@ -1262,7 +1278,7 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_down6g(const Point* __restrict_
                 int64_t d = l0_dense<0>(P, v[r].x, v[r].y, v[r].z);
                 if (d < 0) { err = ERR_L0_RANGE; d = 0; }
                 d6 = (uint32_t)d & (R - 1);
-                atomicAdd(&h[d6 * R5 + (((uint32_t)d >> 6) & (R5 - 1))], 1u);
+                atomicAdd(&h[d6 * HP + (((uint32_t)d >> 6) & (R5 - 1))], 1u);
             } else if (valid) {   // the digit alone (a later pass checks the grid)
                 int32_t iz;
                 d6 = (uint32_t)l0_layer(P, v[r].z, iz) & (R - 1);
@@ -1309,7 +1325,7 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_down6g(const Point* __restrict_
     lds_barrier();
     if (pairs)
         for (int i = tid; i < R * R5; i += kL0BS)
-            gcnt[((uint64_t)(i / R5) * ngroups + g) * R5 + (i % R5)] = h[i];
+            gcnt[((uint64_t)(i / R5) * ngroups + g) * R5 + (i % R5)] = h[(i / R5) * HP + (i % R5)];
     if (err) set_err(ctr, err);
 }
 
@@ -1960,18 +1976,34 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
         STAMP(12);
 #endif
         SlotDest sd;
+        bool amb = false;
         if (ci < nchunks) {   // block-uniform: the last step only emits
-            sd = slot_dest(x, y, z, G, SC);
+            sd = slot_dest_fast(x, y, z, G, SC, amb);
         } else {
             sd.ox = sd.oy = sd.qa = 0;
             sd.layer_ok = false;
             sd.d = sd.g = -1;
         }
-        const int32_t lx = sd.ox - rx, ly = sd.oy - ry;
+        int32_t lx = sd.ox - rx, ly = sd.oy - ry;
+        bool range_ok = lx >= 0 && ly >= 0 && lx < P.tx && ly < P.ty;
+        bool slotted = valid && sd.layer_ok && range_ok;
+        uint32_t local = slotted ? (uint32_t)(ly * P.tx + lx) : 0u;
+        // the slot's occupant, read before the rest of the arithmetic so the LDS
+        // latency overlaps it (phase B of the last step wrote the table before
+        // the barrier; local 0 for lanes without a slot)
+        unsigned long long occ = S.tab[local];
+        if (__ballot(amb)) {
+            if (amb) {
+                slot_dest_exact(x, y, z, G, SC, sd);
+                lx = sd.ox - rx;
+                ly = sd.oy - ry;
+                range_ok = lx >= 0 && ly >= 0 && lx < P.tx && ly < P.ty;
+                slotted = valid && sd.layer_ok && range_ok;
+                local = slotted ? (uint32_t)(ly * P.tx + lx) : 0u;
+                occ = S.tab[local];
+            }
+        }
         const bool layer_ok = sd.layer_ok;
-        const bool range_ok = lx >= 0 && ly >= 0 && lx < P.tx && ly < P.ty;
-        const bool slotted = valid && layer_ok && range_ok;
-        const uint32_t local = slotted ? (uint32_t)(ly * P.tx + lx) : 0u;
         float X, Y, Z;
         slot_centre(sd, G.cr, zt, X, Y, Z);
         const float d2 = dist2(X, Y, Z, x, y, z);
@@ -1993,14 +2025,14 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
 #endif
         // Occupant filter (cell.rs:80 strict <: ties keep the old point); the
         // candidates push themselves onto their slot's list.
-        unsigned long long occ = kEmpty64;
         bool cand = false;
         int hc = -1;
         uint32_t myprev = kNil;
         if (slotted && !forced) {
-            occ = S.tab[local];
             cand = occ == kEmpty64 || d2 < __uint_as_float((uint32_t)(occ >> 33));
             if (PCC_ABL & 32) cand = false;
+        } else {
+            occ = kEmpty64;
         }
         if (cand) {
             hc = claim_push<CLAIM>(claim, local, tid, myprev);

@@ -685,6 +685,7 @@ class HipShardOps:
     def build(self, file_points, pts: torch.Tensor, keys: torch.Tensor | None) -> dict:
         """keys None: this rank holds the whole input in key order (keys 0..n-1).
         The build reads `pts`/`keys` in place (borrowed until it returns)."""
+        self.last_inputs = {"build": (file_points, pts, keys)}
         return self._keyed_build(self.conv, file_points, pts, keys)
 
     def _keyed_build(self, c, file_points, pts, keys, roots=None) -> dict:
@@ -704,6 +705,7 @@ class HipShardOps:
         forwarded).  Returns (stats, (level-1 cells (n,3), -, points per cell,
         their emissions (m,4), causing keys), partial level-0 cells [{xyz, grid}])."""
         c = self.conv_lead
+        self.last_inputs["lead"] = (file_points, pts, keys)
         st = self._keyed_build(c, file_points, pts, keys)
         _, m = c.pending_cells()
         P = torch.empty((m, 4), dtype=torch.int32, device=pts.device)
@@ -724,6 +726,7 @@ class HipShardOps:
     def sub_build(self, file_points, pts: torch.Tensor, keys: torch.Tensor, cells_xyz, spill_batch) -> dict:
         """The level-1 sub-trees of split cells this rank owns (their arrivals, cell
         after cell, from the leaders' pcc_export_pending)."""
+        self.last_inputs["sub"] = (file_points, pts, keys, cells_xyz, spill_batch)
         return self._keyed_build(self.conv_sub, file_points, pts, keys, roots=(cells_xyz, spill_batch))
 
     def _outputs(self):
