@@ -880,8 +880,8 @@ int pcc_convert_files(const char* out_dir, const char* const* paths, size_t npat
                 pcc_close(c);
                 return src ? src : set_err(-EIO, err);   // the reference unwraps Reader::from_path (las.rs:16)
             }
-            if (r.laz) {
-                log_line("ERROR", "LAZ-compressed point data is not supported by this build (%s)", p.c_str());
+            if (!r.laz_error.empty()) {
+                log_line("ERROR", "%s", r.laz_error.c_str());
                 continue;
             }
             if (!logged) log_line("INFO", "Converting %llu points", (unsigned long long)r.count);

@@ -1,5 +1,6 @@
 // format.cpp — cell / metadata writers and the PLY reader (see format.h).
 #include "format.h"
+#include "laz.h"
 
 #include <dirent.h>
 #include <fcntl.h>
@@ -733,8 +734,41 @@ bool read_las(const std::string& path, LasResult& out, std::string& err, const P
     if (minor >= 4 && hsize >= 375 && got >= 255) n = u64(247);   // LAS 1.4 64-bit count
     out.count = n;
     out.points.clear();
-    if (fmt_raw & 0x80) { out.laz = true; fclose(f); return true; }   // LAZ-compressed point data
     const uint8_t fmt = fmt_raw & 0x3F;
+    // LAZ (las.rs:14-46 through las + laz [dep]): bit 7 of the format marks
+    // compressed point data, described by the LASzip VLR
+    laz::Reader lz;
+    const bool compressed = (fmt_raw & 0x80) != 0;
+    if (compressed) {
+        out.laz = true;
+        const uint32_t nvlr = u32(100);
+        laz::Vlr lv;
+        bool found = false;
+        long pos = hsize;
+        for (uint32_t i = 0; i < nvlr && !found; i++) {
+            uint8_t vh[54];
+            if (fseek(f, pos, SEEK_SET) != 0 || fread(vh, 1, 54, f) != 54) return bad("truncated VLR");
+            uint16_t rid, len;
+            memcpy(&rid, vh + 18, 2);
+            memcpy(&len, vh + 20, 2);
+            if (memcmp(vh + 2, "laszip encoded", 14) == 0 && rid == 22204) {
+                std::vector<uint8_t> d(len);
+                if (fread(d.data(), 1, len, f) != len) return bad("truncated LASzip VLR");
+                std::string e;
+                if (!laz::parse_vlr(d.data(), d.size(), lv, e)) return bad(e);
+                found = true;
+            }
+            pos += 54 + len;
+        }
+        if (!found) return bad("compressed point data without a LASzip VLR");
+        std::string e;
+        if (fmt > 3 || !lz.open(f, data_off, n, rec, lv, e)) {
+            out.laz_error = path + ": " + (fmt > 3 ? "LAZ point format " + std::to_string(fmt) +
+                                                         " (LASzip layered compression) is not supported" : e);
+            fclose(f);
+            return true;
+        }
+    }
     if (fmt > 10) return bad("unsupported point data format " + std::to_string(fmt));
     static const int kColorOff[11] = {-1, -1, 20, 28, -1, 28, -1, 30, 30, -1, 30};
     static const int kMinLen[11] = {20, 28, 26, 34, 57, 63, 30, 36, 38, 59, 67};
@@ -742,7 +776,7 @@ bool read_las(const std::string& path, LasResult& out, std::string& err, const P
     const double sx = f64(131), sy = f64(139), sz = f64(147);
     const double ox = f64(155), oy = f64(163), oz = f64(171);
     const int co = kColorOff[fmt];
-    if (fseek(f, (long)data_off, SEEK_SET) != 0) return bad("bad offset to point data");
+    if (!compressed && fseek(f, (long)data_off, SEEK_SET) != 0) return bad("bad offset to point data");
     if (!sink) out.points.resize(n);
     std::vector<uint8_t> buf;
     const uint64_t chunk = 1 << 18;
@@ -750,9 +784,10 @@ bool read_las(const std::string& path, LasResult& out, std::string& err, const P
     std::vector<Point> piece(sink ? chunk : 0);
     for (uint64_t base = 0; base < n; base += chunk) {
         uint64_t m = std::min<uint64_t>(chunk, n - base);
-        const uint64_t got_m = fread(buf.data(), rec, m, f);
+        std::string lerr;
+        const uint64_t got_m = compressed ? lz.read(buf.data(), m, lerr) : fread(buf.data(), rec, m, f);
         if (got_m != m) {   // las Reader::read_n fails on the missing records (las.rs:23-46)
-            out.data_error = path + ": truncated point data";
+            out.data_error = path + ": " + (compressed ? lerr : std::string("truncated point data"));
             m = got_m;
             if (!sink) out.points.resize(base + m);
         }

@@ -95,11 +95,13 @@ bool read_ply(const std::string& path, PlyResult& out, std::string& err, const P
 // 1.0-1.4, point formats 0-10.  x = (scale * X + offset) in f64 (las
 // Transform::direct), then `as f32`; colour = u16 `as u8` (low byte), alpha 255;
 // formats without colour give (0, 0, 0, 255) (Color::default).  Compressed
-// point data (LAZ) is reported as unsupported (`laz` = true, no points).
+// point data (LAZ, `laz` = true) is decoded by laz.h for point formats 0-3;
+// other LAZ variants set `laz_error` and give no points.
 struct LasResult {
     std::vector<Point> points;
     uint64_t count = 0;   // header number_of_points
     bool laz = false;
+    std::string laz_error;   // a LAZ variant this build does not decode
     std::string data_error;   // truncated point data: `points` holds the records read before it
 };
 bool read_las(const std::string& path, LasResult& out, std::string& err, const PointSink& sink = nullptr);

@@ -1,0 +1,86 @@
+"""LAS writing helpers shared by the LAS/LAZ tests (the reference ships no LAS
+or LAZ fixture: the tests write their own files)."""
+import struct
+
+import numpy as np
+
+REC = {0: 20, 1: 28, 2: 26, 3: 34, 6: 30, 7: 36, 8: 38}
+COLOR_OFF = {0: None, 1: None, 2: 20, 3: 28, 6: None, 7: 30, 8: 30}
+GPS_OFF = {0: None, 1: 20, 2: None, 3: 20}
+
+
+def write_las_records(path, body, fmt, n, scale, offset, minor=2):
+    """Header (no VLRs) + raw point records `body` (n x record bytes)."""
+    rec = body.shape[1] if n else REC[fmt]
+    hsize = 375 if minor >= 4 else 227
+    h = bytearray(hsize)
+    h[0:4] = b"LASF"
+    h[24] = 1
+    h[25] = minor
+    struct.pack_into("<H", h, 94, hsize)
+    struct.pack_into("<I", h, 96, hsize)
+    struct.pack_into("<I", h, 100, 0)
+    h[104] = fmt
+    struct.pack_into("<H", h, 105, rec)
+    struct.pack_into("<I", h, 107, n if (minor < 4 and n < 2**32) else 0)
+    struct.pack_into("<3d", h, 131, *scale)
+    struct.pack_into("<3d", h, 155, *offset)
+    if minor >= 4:
+        struct.pack_into("<Q", h, 247, n)
+    with open(path, "wb") as f:
+        f.write(bytes(h))
+        f.write(np.ascontiguousarray(body).tobytes())
+
+
+def write_las(path, X, Y, Z, scale, offset, fmt=3, rgb=None, minor=2):
+    """Minimal uncompressed LAS writer (header + point records, no VLRs)."""
+    n = len(X)
+    rec = REC[fmt]
+    body = np.zeros((n, rec), dtype=np.uint8)
+    xyz = np.stack([X, Y, Z], axis=1).astype("<i4")
+    body[:, 0:12] = xyz.view(np.uint8).reshape(n, 12)
+    if COLOR_OFF[fmt] is not None:
+        body[:, COLOR_OFF[fmt]:COLOR_OFF[fmt] + 6] = np.asarray(rgb, dtype="<u2").view(np.uint8).reshape(n, 6)
+    write_las_records(path, body, fmt, n, scale, offset, minor)
+
+
+def survey_records(n, fmt, seed, extra=0):
+    """Point records shaped like an airborne survey (what LAZ is made for):
+    coordinates along scan lines, multiple returns, increasing GPS time with
+    repeats, correlated colour, flags, plus `extra` bytes per record."""
+    rng = np.random.default_rng(seed)
+    rec = REC[fmt] + extra
+    body = np.zeros((n, rec), dtype=np.uint8)
+    t = np.arange(n)
+    x = (np.cumsum(rng.integers(-40, 120, n)) + 1_000_000).astype("<i4")
+    y = (np.cumsum(rng.integers(-3, 4, n)) * 7 + (t // 500) * 900 - 2_000_000).astype("<i4")
+    z = (50_000 + np.cumsum(rng.integers(-30, 31, n)) + rng.integers(-200, 200, n) * (rng.random(n) < 0.05)).astype("<i4")
+    body[:, 0:12] = np.stack([x, y, z], 1).view(np.uint8).reshape(n, 12)
+    inten = (rng.integers(0, 700, n) * (rng.random(n) < 0.9)).astype("<u2")
+    body[:, 12:14] = inten.view(np.uint8).reshape(n, 2)
+    nret = rng.integers(1, 5, n)
+    ret = np.minimum(rng.integers(1, 5, n), nret)
+    sdir = (t // 300) % 2
+    edge = (t % 300 == 299).astype(np.int64)
+    body[:, 14] = (ret | (nret << 3) | (sdir << 6) | (edge << 7)).astype(np.uint8)
+    body[:, 15] = rng.choice([1, 2, 2, 2, 5, 6], n).astype(np.uint8)
+    body[:, 16] = ((t // 40) % 60 - 30).astype(np.int8).view(np.uint8)
+    body[:, 17] = (rng.random(n) < 0.02).astype(np.uint8) * rng.integers(0, 255, n).astype(np.uint8)
+    psid = np.full(n, 17, dtype="<u2")
+    psid[n // 2:] = 18
+    body[:, 18:20] = psid.view(np.uint8).reshape(n, 2)
+    if GPS_OFF.get(fmt) is not None:
+        g = 250_000.0 + np.repeat(np.cumsum(rng.random((n + 1) // 2) * 1e-4), 2)[:n]
+        g[n // 3] += 1e9   # a jump beyond 32-bit differences
+        body[:, 20:28] = g.astype("<f8").view(np.uint8).reshape(n, 8)
+    if COLOR_OFF.get(fmt) is not None:
+        base = np.cumsum(rng.integers(-3, 4, n)) % 65536
+        rgb = np.stack([base, (base + rng.integers(0, 300, n)) % 65536, (base * 3) % 65536], 1).astype("<u2")
+        grey = rng.random(n) < 0.3
+        rgb[grey, 1] = rgb[grey, 0]
+        rgb[grey, 2] = rgb[grey, 0]
+        co = COLOR_OFF[fmt]
+        body[:, co:co + 6] = rgb.view(np.uint8).reshape(n, 6)
+    if extra:
+        body[:, REC[fmt]:] = (np.arange(n)[:, None] * np.arange(1, extra + 1)[None, :] % 251).astype(np.uint8)
+    return body

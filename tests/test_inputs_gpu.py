@@ -19,6 +19,7 @@ import pytest
 
 from gpu_util import compare_dirs, gpu_digest  # noqa: E402
 from oracle_ctypes import POINT_DTYPE, Oracle, synth  # noqa: E402
+from las_util import survey_records, write_las, write_las_records  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 
@@ -26,36 +27,6 @@ pytestmark = pytest.mark.gpu
 def _exe():
     import pcconv
     return os.path.join(os.path.dirname(pcconv.LIB_PATH), "point_converter")
-
-
-def write_las(path, X, Y, Z, scale, offset, fmt=3, rgb=None, minor=2):
-    """Minimal uncompressed LAS writer (header + point records, no VLRs)."""
-    n = len(X)
-    color_off = {0: None, 1: None, 2: 20, 3: 28, 6: None, 7: 30, 8: 30}[fmt]
-    rec = {0: 20, 1: 28, 2: 26, 3: 34, 6: 30, 7: 36, 8: 38}[fmt]
-    hsize = 375 if minor >= 4 else 227
-    h = bytearray(hsize)
-    h[0:4] = b"LASF"
-    h[24] = 1
-    h[25] = minor
-    struct.pack_into("<H", h, 94, hsize)
-    struct.pack_into("<I", h, 96, hsize)
-    struct.pack_into("<I", h, 100, 0)
-    h[104] = fmt
-    struct.pack_into("<H", h, 105, rec)
-    struct.pack_into("<I", h, 107, n if (minor < 4 and n < 2**32) else 0)
-    struct.pack_into("<3d", h, 131, *scale)
-    struct.pack_into("<3d", h, 155, *offset)
-    if minor >= 4:
-        struct.pack_into("<Q", h, 247, n)
-    body = np.zeros((n, rec), dtype=np.uint8)
-    xyz = np.stack([X, Y, Z], axis=1).astype("<i4")
-    body[:, 0:12] = xyz.view(np.uint8).reshape(n, 12)
-    if color_off is not None:
-        body[:, color_off:color_off + 6] = np.asarray(rgb, dtype="<u2").view(np.uint8).reshape(n, 6)
-    with open(path, "wb") as f:
-        f.write(bytes(h))
-        f.write(body.tobytes())
 
 
 def decode(X, Y, Z, scale, offset, rgb=None):
@@ -323,3 +294,27 @@ def test_ply_vertex_not_first_element():
         _oracle_dir(ref, [expect])
         d, mg, mo = compare_dirs(out, ref, fast=False)
         assert d == [] and mg == mo
+
+
+def test_laz_cli_equals_las(tmp_path):
+    """LAZ input (las.rs:14-46 through laz [dep]): a .laz made by laz_tool from a
+    .las converts to exactly the .las's cloud, for point formats 1 and 3 (GPS
+    time, colour), two files in one run.  Parity unpinned: the .laz files come
+    from this repository's own encoder (no reference fixture, no LASzip here)."""
+    tool = os.path.join(os.path.dirname(_exe()), "laz_tool")
+    files_las, files_laz = [], []
+    for k, fmt in enumerate((1, 3)):
+        body = survey_records(120_000 if fmt == 3 else 45_000, fmt, seed=40 + fmt)
+        a = str(tmp_path / f"f{k}.las")
+        z = str(tmp_path / f"f{k}.laz")
+        write_las_records(a, body, fmt, len(body), (0.001, 0.001, 0.0005), (-900.0, 1900.0, -20.0))
+        subprocess.run([tool, "compress", a, z, "50000"], check=True)
+        files_las.append(a)
+        files_laz.append(z)
+    out_las, out_laz = str(tmp_path / "out_las"), str(tmp_path / "out_laz")
+    _cli(files_las, out_las)
+    log = _cli(files_laz, out_laz)
+    assert "not supported" not in log
+    d, ma, mb = compare_dirs(out_las, out_laz, fast=False)
+    assert d == [] and ma == mb
+    assert ma["number_of_points"] == 165_000
