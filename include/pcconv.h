@@ -207,6 +207,12 @@ typedef struct pcc_shard_grid {
 /* Level-0 grid spanned by the global bounding box (host only, no device). */
 int pcc_shard_grid_from_bbox(const float gmin[3], const float gmax[3], float max_cell_size, pcc_shard_grid* out);
 
+/* Largest-first greedy placement (host only, no device): item i of weight w[i]
+ * goes, heaviest first (ties by index), to the least loaded rank (ties by
+ * rank); owner[i] and the final load per rank.  The ownership plan's inner loop
+ * (pcconv/dist.py _lpt / assign_owners), identical on every rank. */
+int pcc_shard_lpt(const double* w, uint64_t n, uint32_t world, uint32_t* owner, double* load);
+
 /* Points first .. first+n-1 of the synthetic stream of pcc_add_synthetic,
  * written to dst[0 .. n) in device memory (each rank generates its key range). */
 int pcc_synth_device(pcc_point* dst, uint64_t first, uint64_t n, uint64_t seed, int kind, float lo, float extent,
@@ -295,6 +301,32 @@ int pcc_pending_cells(pcc_converter* c, uint64_t* ncells, uint64_t* npoints);
  * (x, y, z) and spill batches into host arrays of ncells. */
 int pcc_export_pending(pcc_converter* c, int32_t* cells_xyz, uint32_t* spill_batch, uint64_t* cell_points,
                        pcc_point* dev_pts, uint32_t* dev_keys);
+/* After pcc_build: the grid points (cell.rs:70-94 slot winners) of the cells of
+ * the first built level -- a raw build's partial level-0 cells -- compacted into
+ * device memory, cell after cell in the order pcc_visit_cells walks them, each
+ * cell's points in that walk's order; the cells' (x, y, z) and point counts into
+ * host arrays of ncells.  pcc_grid_cells gives ncells and the total npoints. */
+int pcc_grid_cells(pcc_converter* c, uint64_t* ncells, uint64_t* npoints);
+int pcc_export_grid(pcc_converter* c, int32_t* cells_xyz, uint64_t* cell_points, pcc_point* dev_pts);
+
+/* Owner side of shared level-0 cells' overflow buckets: cell.rs:108-153
+ * add_points_in_overflow resolved over the emissions every rank's raw lead build
+ * forwarded (the numpy statement: pcconv/dist.py resolve_bucket).  The emissions
+ * are nseg segments of dev_pts/dev_keys rows (seg_n[s] rows each, contiguous in
+ * order), segment s belonging to bucket seg_bucket[s] < nbuckets; a segment is
+ * in key order and a bucket's keys are distinct.  file_points / batch_size: the
+ * global file structure (lib.rs:31-52 batching); limit: the overflow limit.
+ * Per bucket (host arrays of nbuckets): state 1 = Some (the list is kept) or
+ * 2 = None (spilled at spill_batch), kept_n = its kept points (0 for None).
+ * dev_kept: the Some buckets' lists, bucket after bucket, each in key order
+ * (*nkept rows); dev_sub_pts/keys: the None buckets' emissions, bucket after
+ * bucket, segments in order (*nsub rows).  Each output needs room for every row.
+ * Host transfers are the tables and the states only. */
+int pcc_shard_resolve_buckets(const uint64_t* seg_n, const uint32_t* seg_bucket, uint64_t nseg, uint32_t nbuckets,
+                              const pcc_point* dev_pts, const uint32_t* dev_keys, const uint64_t* file_points,
+                              uint64_t nfiles, uint32_t batch_size, uint32_t limit, uint32_t* state,
+                              uint32_t* spill_batch, uint64_t* kept_n, pcc_point* dev_kept, pcc_point* dev_sub_pts,
+                              uint32_t* dev_sub_keys, uint64_t* nkept, uint64_t* nsub, int device);
 
 /* Global metadata values after the ranks' all-reduce (converter.rs:96-112,141-158). */
 int pcc_set_summary(pcc_converter* c, uint64_t number_of_points, const float bmin[3], const float bmax[3],

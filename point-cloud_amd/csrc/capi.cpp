@@ -479,6 +479,24 @@ int pcc_shard_grid_from_bbox(const float gmin[3], const float gmax[3], float max
     return 0;
 }
 
+int pcc_shard_lpt(const double* w, uint64_t n, uint32_t world, uint32_t* owner, double* load) {
+    if ((n && (!w || !owner)) || !load || world == 0) return set_err(-EINVAL, "null argument or no ranks");
+    GUARD_BEGIN
+    std::vector<uint64_t> order(n);
+    for (uint64_t i = 0; i < n; i++) order[i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](uint64_t a, uint64_t b) { return w[a] > w[b]; });
+    for (uint32_t r = 0; r < world; r++) load[r] = 0.0;
+    for (uint64_t i : order) {
+        uint32_t best = 0;   // least loaded rank, ties by rank
+        for (uint32_t r = 1; r < world; r++)
+            if (load[r] < load[best]) best = r;
+        owner[i] = best;
+        load[best] += w[i];
+    }
+    return 0;
+    GUARD_END
+}
+
 static ShardGrid to_grid(const pcc_shard_grid* g) {
     ShardGrid s;
     for (int a = 0; a < 3; a++) { s.lo[a] = g->lo[a]; s.dims[a] = g->dims[a]; }
@@ -575,6 +593,27 @@ int pcc_shard_keys_from_bitmaps(const uint64_t* dbitmaps, const uint64_t* nwords
     GUARD_END
 }
 
+int pcc_shard_resolve_buckets(const uint64_t* seg_n, const uint32_t* seg_bucket, uint64_t nseg, uint32_t nbuckets,
+                              const pcc_point* dev_pts, const uint32_t* dev_keys, const uint64_t* file_points,
+                              uint64_t nfiles, uint32_t batch_size, uint32_t limit, uint32_t* state,
+                              uint32_t* spill_batch, uint64_t* kept_n, pcc_point* dev_kept, pcc_point* dev_sub_pts,
+                              uint32_t* dev_sub_keys, uint64_t* nkept, uint64_t* nsub, int device) {
+    if (!nkept || !nsub || (nseg && (!seg_n || !seg_bucket)) || (nbuckets && (!state || !spill_batch || !kept_n)) ||
+        (nfiles && !file_points))
+        return set_err(-EINVAL, "null argument");
+    uint64_t rows = 0;
+    for (uint64_t s = 0; s < nseg; s++) rows += seg_n[s];
+    if (rows && (!dev_pts || !dev_keys || !dev_kept || !dev_sub_pts || !dev_sub_keys))
+        return set_err(-EINVAL, "null argument");
+    GUARD_BEGIN
+    const int rc = shard_resolve_buckets(seg_n, seg_bucket, nseg, nbuckets, reinterpret_cast<const Point*>(dev_pts),
+                                         dev_keys, file_points, nfiles, batch_size, limit, state, spill_batch, kept_n,
+                                         reinterpret_cast<Point*>(dev_kept), reinterpret_cast<Point*>(dev_sub_pts),
+                                         dev_sub_keys, nkept, nsub, device);
+    return rc ? set_err(rc, "bucket resolution failed (no files, no segments, or a segment's bucket out of range)") : 0;
+    GUARD_END
+}
+
 int pcc_write_cell_view(const char* out_dir, const pcc_cell_view* v) {
     if (!out_dir || !v) return set_err(-EINVAL, "null argument");
     if (v->entries > 8) return set_err(-EINVAL, "a cell has at most 8 overflow entries");
@@ -651,6 +690,30 @@ int pcc_export_pending(pcc_converter* c, int32_t* cells_xyz, uint32_t* spill_bat
     if (np && (!dev_pts || !dev_keys)) return set_err(-EINVAL, "null argument");
     GUARD_BEGIN
     return c->eng->export_pending(cells_xyz, spill_batch, cell_points, reinterpret_cast<Point*>(dev_pts), dev_keys);
+    GUARD_END
+}
+
+int pcc_grid_cells(pcc_converter* c, uint64_t* ncells, uint64_t* npoints) {
+    if (!c || !ncells || !npoints) return set_err(-EINVAL, "null argument");
+    if (!c->built) return set_err(-EINVAL, "nothing built");
+    *ncells = *npoints = 0;
+    if (!c->eng->num_levels()) return 0;
+    GUARD_BEGIN
+    return c->eng->grid_cells(0, *ncells, *npoints);
+    GUARD_END
+}
+
+int pcc_export_grid(pcc_converter* c, int32_t* cells_xyz, uint64_t* cell_points, pcc_point* dev_pts) {
+    if (!c) return set_err(-EINVAL, "null argument");
+    if (!c->built) return set_err(-EINVAL, "nothing built");
+    if (!c->eng->num_levels()) return 0;
+    GUARD_BEGIN
+    uint64_t nc = 0, np = 0;
+    int rc = c->eng->grid_cells(0, nc, np);
+    if (rc) return set_err(rc, c->eng->last_error());
+    if ((nc && (!cells_xyz || !cell_points)) || (np && !dev_pts)) return set_err(-EINVAL, "null argument");
+    rc = c->eng->export_grid(0, cells_xyz, cell_points, reinterpret_cast<Point*>(dev_pts));
+    return rc ? set_err(rc, c->eng->last_error()) : 0;
     GUARD_END
 }
 

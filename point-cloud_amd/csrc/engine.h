@@ -213,6 +213,10 @@ public:
     int download(std::vector<LevelHost>& levels, std::vector<Point>& grid, std::vector<Point>& kept);
     // one level (grid winners compacted on the device); H's bases are 0
     int download_level(uint32_t i, LevelHost& H, HostPoints& grid, HostPoints& kept);
+    // level i's grid winners per cell into device memory (cell order, each cell's
+    // slabs in layer order); cells' (x, y, z) and winner counts on the host
+    int grid_cells(uint32_t i, uint64_t& ncells, uint64_t& npoints);
+    int export_grid(uint32_t i, int32_t* xyz, uint64_t* cell_n, Point* dpts);
     uint32_t num_levels() const;
     // (h, x, y, z) of every cell the last build produced (merge: the touched cells)
     int built_cells(std::vector<int32_t>& hxyz);
@@ -329,6 +333,11 @@ int shard_route(const Point* d, uint64_t n, uint32_t key0, const ShardGrid& g, c
                 Point* dsend, uint32_t* dkeys, uint64_t* counts, int device, uint32_t dim = 0, uint64_t* dbm = nullptr);
 int shard_keys_from_bitmaps(const uint64_t* dbm, const uint64_t* nwords, const uint64_t* key0, uint32_t nsrc,
                             uint32_t* dkeys, uint64_t nkeys, int device);
+// pcc_shard_resolve_buckets (pcconv.h)
+int shard_resolve_buckets(const uint64_t* seg_n, const uint32_t* seg_bucket, uint64_t nseg, uint32_t nbuckets,
+                          const Point* dpts, const uint32_t* dkeys, const uint64_t* file_points, uint64_t nfiles,
+                          uint32_t batch, uint32_t limit, uint32_t* state, uint32_t* spill_batch, uint64_t* kept_n,
+                          Point* dkept, Point* dsub, uint32_t* dsub_keys, uint64_t* nkept, uint64_t* nsub, int device);
 
 // Frees the device buffers closed converters left in the process-wide cache
 // (engine.hip dev_alloc); returns the bytes freed.  Buffers in use stay.

@@ -4557,6 +4557,51 @@ int Engine::download_level(uint32_t i, LevelHost& H, HostPoints& grid, HostPoint
     return 0;
 }
 
+// Grid winners of built level i per cell, compacted on the device (the sharded
+// step's partial level-0 cells travel to their writers without a host copy).
+// cgo = exclusive scan of the slabs' winner counts (slab order = cell order).
+int Engine::grid_cells(uint32_t i, uint64_t& ncells, uint64_t& npoints) {
+    if (i >= levels_.size()) return -EINVAL;
+    Level* L = levels_[i];
+    ncells = L->ncells;
+    npoints = 0;
+    if (!L->nslabs) return 0;
+    const uint64_t mk = dev_->mark();
+    uint32_t* cgo = static_cast<uint32_t*>(dev_->get(((uint64_t)L->nslabs + 1) * 4));
+    uint32_t* tot = static_cast<uint32_t*>(dev_->get(4));
+    uint32_t nwin = 0;
+    scan_excl_u32(L->slab_grid_n, cgo, L->nslabs, tot, dev_->scan, stream_);
+    HIP_CHECK(hipMemcpyAsync(&nwin, tot, 4, hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    dev_->release(mk);
+    npoints = nwin;
+    return 0;
+}
+
+int Engine::export_grid(uint32_t i, int32_t* xyz, uint64_t* cell_n, Point* dpts) {
+    if (i >= levels_.size()) return -EINVAL;
+    Level* L = levels_[i];
+    if (!L->ncells) return 0;
+    const uint64_t mk = dev_->mark();
+    uint32_t* cgo = static_cast<uint32_t*>(dev_->get(((uint64_t)L->nslabs + 1) * 4));
+    uint32_t* tot = static_cast<uint32_t*>(dev_->get(4));
+    std::vector<uint32_t> slab0(L->ncells + 1ull), hoff(L->nslabs + 1ull, 0);
+    if (L->nslabs) {
+        scan_excl_u32(L->slab_grid_n, cgo, L->nslabs, tot, dev_->scan, stream_);
+        k_compact_grid<<<std::min<uint32_t>(L->nslabs, 65536), 256, 0, stream_>>>(L->grid, L->grid_off, L->slab_grid_n,
+                                                                                cgo, L->nslabs, dpts);
+        HIP_CHECK(hipGetLastError());
+        HIP_CHECK(hipMemcpyAsync(hoff.data(), cgo, (uint64_t)L->nslabs * 4, hipMemcpyDeviceToHost, stream_));
+        HIP_CHECK(hipMemcpyAsync(hoff.data() + L->nslabs, tot, 4, hipMemcpyDeviceToHost, stream_));
+    }
+    HIP_CHECK(hipMemcpyAsync(xyz, L->cell_idx, 3ull * L->ncells * 4, hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipMemcpyAsync(slab0.data(), L->cell_slab0, slab0.size() * 4, hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    dev_->release(mk);
+    for (uint32_t c = 0; c < L->ncells; c++) cell_n[c] = hoff[slab0[c + 1]] - hoff[slab0[c]];
+    return 0;
+}
+
 int Engine::download(std::vector<LevelHost>& out, std::vector<Point>& grid, std::vector<Point>& kept) {
     out.clear();
     grid.clear();
@@ -4593,10 +4638,14 @@ struct ShardScratch {
     uint32_t* flag = nullptr;
     uint32_t* cnt = nullptr;
     uint64_t* tab = nullptr;
+    uint64_t* rt = nullptr;   // bucket resolution tables and sort buffers (shard_resolve_buckets)
+    uint64_t rt_cap = 0;
+    uint32_t* rb = nullptr;
+    uint64_t rb_cap = 0;
     SortTemp sort;
     ~ShardScratch() {
         for (auto* b : buf) (void)hipFree(b);
-        (void)hipFree(part); (void)hipFree(flag); (void)hipFree(cnt); (void)hipFree(tab);
+        (void)hipFree(part); (void)hipFree(flag); (void)hipFree(cnt); (void)hipFree(tab); (void)hipFree(rt); (void)hipFree(rb);
         (void)hipFree(sort.counts); (void)hipFree(sort.scan.bsums);
         if (st) (void)hipStreamDestroy(st);
     }
@@ -4792,6 +4841,96 @@ __global__ void k_bm_keys(const unsigned long long* __restrict__ bm, uint32_t nw
     }
 }
 
+// ---- shared cells' overflow buckets, resolved over every rank's emissions
+// (cell.rs:108-153; the numpy statement is pcconv/dist.py::resolve_bucket).
+// Emissions arrive in segments (a cell's arrivals from one rank: sorted runs per
+// slab, not sorted as a whole); a bucket's keys are distinct.  The rows are
+// sorted by (bucket, key) on the device (two stable radix passes over a row
+// index), so each bucket's keys are one ascending run of `sk`.
+struct BucketTabs {
+    const uint32_t* files;      // 4 u32 per file: start lo/hi, first batch, batch size
+    uint32_t nfiles;
+    const uint64_t* start;      // per segment: first row, rows, bucket
+    const uint64_t* len;
+    const uint64_t* segb;
+    const uint64_t* bstart;     // per bucket: first position in the sorted order (nbuckets + 1)
+    const uint64_t* base;       // per segment: sub-tree output row base (spilled buckets)
+    const uint64_t* kbase;      // per bucket: kept output row base (kept buckets)
+    uint64_t* out;              // per bucket: state | spill batch << 32
+    uint64_t nseg;
+    uint32_t nbuckets, limit;
+};
+__device__ __forceinline__ uint64_t row_segment(const BucketTabs& T, uint64_t i) {
+    uint64_t lo = 0, hi = T.nseg - 1;   // last segment with start <= i
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi + 1) >> 1;
+        if (T.start[mid] <= i) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+// sort input: (key, row) and the row's bucket
+__global__ void k_bkt_rows(BucketTabs T, const uint32_t* __restrict__ keys, uint32_t nrows, uint32_t* __restrict__ k,
+                           uint32_t* __restrict__ idx, uint32_t* __restrict__ bkt) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nrows) return;
+    k[i] = keys[i];
+    idx[i] = i;
+    bkt[i] = (uint32_t)T.segb[row_segment(T, i)];
+}
+__global__ void k_gather_u32(const uint32_t* __restrict__ src, const uint32_t* __restrict__ idx, uint32_t n,
+                             uint32_t* __restrict__ dst) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dst[i] = src[idx[i]];
+}
+// first position in [lo, hi) of sk with sk >= v
+__device__ __forceinline__ uint64_t lower_bound_u32(const uint32_t* sk, uint64_t lo, uint64_t hi, uint32_t v) {
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (sk[mid] < v) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+// one thread per bucket: state 1 (Some) or 2 (None at the spill batch).  Batch
+// by batch the list stays while it holds at most L points after the first
+// batch / below L after a later one: spilled iff tot > L, or tot == L over more
+// than one batch; then the spill batch is that of the thr-th smallest key with
+// thr = L + (first batch's count == L).
+__global__ void k_bkt_resolve(BucketTabs T, const uint32_t* __restrict__ sk) {
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= T.nbuckets) return;
+    const uint64_t a = T.bstart[b], e = T.bstart[b + 1], tot = e - a;
+    uint64_t st = 1;
+    if (tot) {
+        const uint32_t e0 = event_batch(T.files, T.nfiles, sk[a]), e1 = event_batch(T.files, T.nfiles, sk[e - 1]);
+        const bool spilled = tot > T.limit || (tot == T.limit && e0 != e1);
+        if (spilled) {
+            const uint64_t first = lower_bound_u32(sk, a, e, first_key_after(T.files, T.nfiles, e0)) - a;
+            const uint64_t thr = (uint64_t)T.limit + (first == T.limit ? 1u : 0u);
+            const uint64_t want = thr > 1 ? thr : 1;   // the want-th smallest key (1-based), want <= tot
+            st = 2ull | ((uint64_t)event_batch(T.files, T.nfiles, sk[a + want - 1]) << 32);
+        }
+    }
+    T.out[b] = st;
+}
+// kept buckets: sorted position j -> kept row kbase + (j - bstart)
+__global__ void k_bkt_kept(BucketTabs T, const uint32_t* __restrict__ sb, const uint32_t* __restrict__ idx,
+                           uint32_t nrows, const Point* __restrict__ pts, Point* __restrict__ kept) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= nrows) return;
+    const uint32_t b = sb[j];
+    if ((uint32_t)T.out[b] != 1) return;
+    reinterpret_cast<float4*>(kept)[T.kbase[b] + (j - T.bstart[b])] = reinterpret_cast<const float4*>(pts)[idx[j]];
+}
+// spilled buckets: their rows in segment order (pts + keys) from base[segment]
+__global__ void k_bkt_sub(BucketTabs T, const uint32_t* __restrict__ bkt, uint32_t nrows, const Point* __restrict__ pts,
+                          const uint32_t* __restrict__ keys, Point* __restrict__ sub, uint32_t* __restrict__ sub_keys) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nrows || (uint32_t)T.out[bkt[i]] != 2) return;
+    const uint64_t s = row_segment(T, i), o = T.base[s] + (i - T.start[s]);
+    reinterpret_cast<float4*>(sub)[o] = reinterpret_cast<const float4*>(pts)[i];
+    sub_keys[o] = keys[i];
+}
+
 }  // namespace
 
 int shard_keys_from_bitmaps(const uint64_t* dbm, const uint64_t* nwords, const uint64_t* key0, uint32_t nsrc,
@@ -4825,6 +4964,125 @@ int shard_keys_from_bitmaps(const uint64_t* dbm, const uint64_t* nwords, const u
     }
     HIP_CHECK(hipStreamSynchronize(S.st));
     return total == nkeys ? 0 : -EBADMSG;
+}
+
+int shard_resolve_buckets(const uint64_t* seg_n, const uint32_t* seg_bucket, uint64_t nseg, uint32_t nbuckets,
+                          const Point* dpts, const uint32_t* dkeys, const uint64_t* file_points, uint64_t nfiles,
+                          uint32_t batch, uint32_t limit, uint32_t* state, uint32_t* spill_batch, uint64_t* kept_n,
+                          Point* dkept, Point* dsub, uint32_t* dsub_keys, uint64_t* nkept, uint64_t* nsub, int device) {
+    ShardScratch& S = shard_scratch(device);
+    *nkept = *nsub = 0;
+    if (!nbuckets) return 0;
+    if (!nfiles || nseg == 0) return -EINVAL;
+    batch = std::max<uint32_t>(batch, 1);
+    std::vector<uint64_t> tot(nbuckets, 0), bstart(nbuckets + 1ull, 0), start(nseg), segb(nseg);
+    uint64_t nrows = 0;
+    for (uint64_t s = 0; s < nseg; s++) {
+        if (seg_bucket[s] >= nbuckets) return -EINVAL;
+        start[s] = nrows;
+        nrows += seg_n[s];
+        tot[seg_bucket[s]] += seg_n[s];
+        segb[s] = seg_bucket[s];
+    }
+    if (nrows >= (1ull << 32)) return -EOVERFLOW;
+    for (uint32_t b = 0; b < nbuckets; b++) bstart[b + 1] = bstart[b] + tot[b];
+    // file table as the engine's (lib.rs:31-52: batches restart at every file,
+    // an empty file is one empty batch)
+    std::vector<uint32_t> ft;
+    uint64_t g = 0;
+    uint32_t eb = 0;
+    for (uint64_t f = 0; f < nfiles; f++) {
+        ft.insert(ft.end(), {(uint32_t)g, (uint32_t)(g >> 32), eb, batch});
+        g += file_points[f];
+        eb += (uint32_t)std::max<uint64_t>(1, (file_points[f] + batch - 1) / batch);
+    }
+    const uint64_t wf = (ft.size() + 1) / 2;
+    const uint64_t w_start = wf, w_len = w_start + nseg, w_segb = w_len + nseg, w_bstart = w_segb + nseg,
+                   w_base = w_bstart + nbuckets + 1, w_kbase = w_base + nseg, w_out = w_kbase + nbuckets,
+                   words = w_out + nbuckets;
+    if (S.rt_cap < words) {
+        (void)hipFree(S.rt);
+        S.rt = nullptr;
+        HIP_CHECK(hipMalloc(&S.rt, words * 8));
+        S.rt_cap = words;
+    }
+    if (S.rb_cap < nrows) {   // sort buffers: 2 keys, 2 values, row bucket, sorted keys
+        (void)hipFree(S.rb);
+        S.rb = nullptr;
+        HIP_CHECK(hipMalloc(&S.rb, std::max<uint64_t>(nrows, 1) * 6 * 4));
+        S.rb_cap = std::max<uint64_t>(nrows, 1);
+    }
+    std::vector<uint64_t> blob(w_base, 0);
+    memcpy(blob.data(), ft.data(), ft.size() * 4);
+    memcpy(blob.data() + w_start, start.data(), nseg * 8);
+    memcpy(blob.data() + w_len, seg_n, nseg * 8);
+    memcpy(blob.data() + w_segb, segb.data(), nseg * 8);
+    memcpy(blob.data() + w_bstart, bstart.data(), bstart.size() * 8);
+    BucketTabs T;
+    T.files = reinterpret_cast<const uint32_t*>(S.rt);
+    T.nfiles = (uint32_t)nfiles;
+    T.start = S.rt + w_start;
+    T.len = S.rt + w_len;
+    T.segb = S.rt + w_segb;
+    T.bstart = S.rt + w_bstart;
+    T.base = S.rt + w_base;
+    T.kbase = S.rt + w_kbase;
+    T.out = S.rt + w_out;
+    T.nseg = nseg;
+    T.nbuckets = nbuckets;
+    T.limit = limit;
+    HIP_CHECK(hipMemcpyAsync(S.rt, blob.data(), w_base * 8, hipMemcpyHostToDevice, S.st));
+    const uint32_t n = (uint32_t)nrows, nb = (n + 255) / 256;
+    uint32_t* K[2] = {S.rb, S.rb + S.rb_cap};
+    uint32_t* V[2] = {S.rb + 2 * S.rb_cap, S.rb + 3 * S.rb_cap};
+    uint32_t* bkt = S.rb + 4 * S.rb_cap;
+    uint32_t* sk = S.rb + 5 * S.rb_cap;
+    const uint32_t* sbk = nullptr;   // sorted bucket ids
+    const uint32_t* sidx = nullptr;  // rows in (bucket, key) order
+    if (n) {
+        k_bkt_rows<<<nb, 256, 0, S.st>>>(T, dkeys, n, K[0], V[0], bkt);
+        const int r = radix_sort_pairs(K[0], V[0], K[1], V[1], n, 32, S.sort, S.st);
+        k_gather_u32<<<nb, 256, 0, S.st>>>(bkt, V[r], n, K[1 - r]);
+        int bb = 1;
+        while ((1ull << bb) < nbuckets) bb++;
+        const int r2 = radix_sort_pairs(K[1 - r], V[r], K[r], V[1 - r], n, bb, S.sort, S.st);
+        sbk = r2 == 0 ? K[1 - r] : K[r];
+        sidx = r2 == 0 ? V[r] : V[1 - r];
+        k_gather_u32<<<nb, 256, 0, S.st>>>(dkeys, sidx, n, sk);
+    }
+    k_bkt_resolve<<<(nbuckets + 63) / 64, 64, 0, S.st>>>(T, sk);
+    HIP_CHECK(hipGetLastError());
+    std::vector<uint64_t> out(nbuckets);
+    HIP_CHECK(hipMemcpyAsync(out.data(), T.out, nbuckets * 8ull, hipMemcpyDeviceToHost, S.st));
+    HIP_CHECK(hipStreamSynchronize(S.st));
+    // output bases: kept lists bucket after bucket, the spilled buckets' rows
+    // bucket after bucket (each bucket's segments in order)
+    std::vector<uint64_t> tail(nseg + nbuckets, 0), bsub(nbuckets);
+    uint64_t ok = 0, os = 0;
+    for (uint32_t b = 0; b < nbuckets; b++) {
+        state[b] = (uint32_t)out[b];
+        spill_batch[b] = (uint32_t)(out[b] >> 32);
+        const bool some = state[b] == 1;
+        kept_n[b] = some ? tot[b] : 0;
+        tail[nseg + b] = ok;
+        bsub[b] = os;
+        (some ? ok : os) += tot[b];
+    }
+    for (uint64_t s = 0; s < nseg; s++) {   // segments in order: within a bucket, in order too
+        const uint32_t b = seg_bucket[s];
+        tail[s] = bsub[b];
+        if (state[b] == 2) bsub[b] += seg_n[s];
+    }
+    *nkept = ok;
+    *nsub = os;
+    if (n) {
+        HIP_CHECK(hipMemcpyAsync(S.rt + w_base, tail.data(), tail.size() * 8, hipMemcpyHostToDevice, S.st));
+        k_bkt_kept<<<nb, 256, 0, S.st>>>(T, sbk, sidx, n, dpts, dkept);
+        k_bkt_sub<<<nb, 256, 0, S.st>>>(T, bkt, n, dpts, dkeys, dsub, dsub_keys);
+        HIP_CHECK(hipGetLastError());
+    }
+    HIP_CHECK(hipStreamSynchronize(S.st));
+    return 0;
 }
 
 int shard_synth(Point* dst, uint64_t idx0, uint64_t n, uint64_t seed, int kind, float lo, float ext, int device) {

@@ -706,6 +706,64 @@ struct Gps11 : ItemCodec {
     }
 };
 
+// RGB12 v2 colour model (also RGB14 v3's): which bytes changed, low/high byte
+// differences predicted from the red channel's change
+void rgb_decode(Decoder& d, SymbolModel& used, std::vector<SymbolModel>& md, const uint16_t* last, uint16_t* c) {
+    const uint32_t sym = d.symbol(used);
+    if (sym & 1) c[0] = (uint16_t)u8_fold((int32_t)d.symbol(md[0]) + (last[0] & 255));
+    else c[0] = last[0] & 0xFF;
+    if (sym & 2) c[0] |= (uint16_t)(u8_fold((int32_t)d.symbol(md[1]) + (last[0] >> 8)) << 8);
+    else c[0] |= last[0] & 0xFF00;
+    if (sym & 64) {
+        int32_t diff = (c[0] & 0xFF) - (last[0] & 0xFF);
+        if (sym & 4) c[1] = (uint16_t)u8_fold((int32_t)d.symbol(md[2]) + u8_clamp(diff + (last[1] & 255)));
+        else c[1] = last[1] & 0xFF;
+        if (sym & 16) {
+            diff = (diff + ((c[1] & 0xFF) - (last[1] & 0xFF))) / 2;
+            c[2] = (uint16_t)u8_fold((int32_t)d.symbol(md[4]) + u8_clamp(diff + (last[2] & 255)));
+        } else {
+            c[2] = last[2] & 0xFF;
+        }
+        diff = (c[0] >> 8) - (last[0] >> 8);
+        if (sym & 8) c[1] |= (uint16_t)(u8_fold((int32_t)d.symbol(md[3]) + u8_clamp(diff + (last[1] >> 8))) << 8);
+        else c[1] |= last[1] & 0xFF00;
+        if (sym & 32) {
+            diff = (diff + ((c[1] >> 8) - (last[1] >> 8))) / 2;
+            c[2] |= (uint16_t)(u8_fold((int32_t)d.symbol(md[5]) + u8_clamp(diff + (last[2] >> 8))) << 8);
+        } else {
+            c[2] |= last[2] & 0xFF00;
+        }
+    } else {
+        c[1] = c[0];
+        c[2] = c[0];
+    }
+}
+uint32_t rgb_encode(Encoder& e, SymbolModel& used, std::vector<SymbolModel>& md, const uint16_t* last, const uint16_t* c) {
+    const uint32_t sym = ((last[0] & 0x00FF) != (c[0] & 0x00FF)) | (((last[0] & 0xFF00) != (c[0] & 0xFF00)) << 1) |
+                         (((last[1] & 0x00FF) != (c[1] & 0x00FF)) << 2) | (((last[1] & 0xFF00) != (c[1] & 0xFF00)) << 3) |
+                         (((last[2] & 0x00FF) != (c[2] & 0x00FF)) << 4) | (((last[2] & 0xFF00) != (c[2] & 0xFF00)) << 5) |
+                         (((c[0] & 0x00FF) != (c[1] & 0x00FF) || (c[0] & 0x00FF) != (c[2] & 0x00FF) ||
+                           (c[0] & 0xFF00) != (c[1] & 0xFF00) || (c[0] & 0xFF00) != (c[2] & 0xFF00)) << 6);
+    e.symbol(used, sym);
+    if (sym & 1) e.symbol(md[0], u8_fold((c[0] & 255) - (last[0] & 255)));
+    if (sym & 2) e.symbol(md[1], u8_fold((c[0] >> 8) - (last[0] >> 8)));
+    if (sym & 64) {
+        int32_t diff = (c[0] & 0xFF) - (last[0] & 0xFF);
+        if (sym & 4) e.symbol(md[2], u8_fold((c[1] & 255) - u8_clamp(diff + (last[1] & 255))));
+        if (sym & 16) {
+            diff = (diff + ((c[1] & 0xFF) - (last[1] & 0xFF))) / 2;
+            e.symbol(md[4], u8_fold((c[2] & 255) - u8_clamp(diff + (last[2] & 255))));
+        }
+        diff = (c[0] >> 8) - (last[0] >> 8);
+        if (sym & 8) e.symbol(md[3], u8_fold((c[1] >> 8) - u8_clamp(diff + (last[1] >> 8))));
+        if (sym & 32) {
+            diff = (diff + ((c[1] >> 8) - (last[1] >> 8))) / 2;
+            e.symbol(md[5], u8_fold((c[2] >> 8) - u8_clamp(diff + (last[2] >> 8))));
+        }
+    }
+    return sym;
+}
+
 struct Rgb12 : ItemCodec {
     SymbolModel m_used;
     std::vector<SymbolModel> m_diff;
@@ -720,62 +778,14 @@ struct Rgb12 : ItemCodec {
     }
     void read(Decoder& d, uint8_t* item) override {
         uint16_t c[3];
-        const uint32_t sym = d.symbol(m_used);
-        if (sym & 1) c[0] = (uint16_t)u8_fold((int32_t)d.symbol(m_diff[0]) + (last[0] & 255));
-        else c[0] = last[0] & 0xFF;
-        if (sym & 2) c[0] |= (uint16_t)(u8_fold((int32_t)d.symbol(m_diff[1]) + (last[0] >> 8)) << 8);
-        else c[0] |= last[0] & 0xFF00;
-        if (sym & 64) {
-            int32_t diff = (c[0] & 0xFF) - (last[0] & 0xFF);
-            if (sym & 4) c[1] = (uint16_t)u8_fold((int32_t)d.symbol(m_diff[2]) + u8_clamp(diff + (last[1] & 255)));
-            else c[1] = last[1] & 0xFF;
-            if (sym & 16) {
-                diff = (diff + ((c[1] & 0xFF) - (last[1] & 0xFF))) / 2;
-                c[2] = (uint16_t)u8_fold((int32_t)d.symbol(m_diff[4]) + u8_clamp(diff + (last[2] & 255)));
-            } else {
-                c[2] = last[2] & 0xFF;
-            }
-            diff = (c[0] >> 8) - (last[0] >> 8);
-            if (sym & 8) c[1] |= (uint16_t)(u8_fold((int32_t)d.symbol(m_diff[3]) + u8_clamp(diff + (last[1] >> 8))) << 8);
-            else c[1] |= last[1] & 0xFF00;
-            if (sym & 32) {
-                diff = (diff + ((c[1] >> 8) - (last[1] >> 8))) / 2;
-                c[2] |= (uint16_t)(u8_fold((int32_t)d.symbol(m_diff[5]) + u8_clamp(diff + (last[2] >> 8))) << 8);
-            } else {
-                c[2] |= last[2] & 0xFF00;
-            }
-        } else {
-            c[1] = c[0];
-            c[2] = c[0];
-        }
+        rgb_decode(d, m_used, m_diff, last, c);
         memcpy(last, c, 6);
         memcpy(item, c, 6);
     }
     void write(Encoder& e, const uint8_t* item) override {
         uint16_t c[3];
         memcpy(c, item, 6);
-        uint32_t sym = ((last[0] & 0x00FF) != (c[0] & 0x00FF)) | (((last[0] & 0xFF00) != (c[0] & 0xFF00)) << 1) |
-                       (((last[1] & 0x00FF) != (c[1] & 0x00FF)) << 2) | (((last[1] & 0xFF00) != (c[1] & 0xFF00)) << 3) |
-                       (((last[2] & 0x00FF) != (c[2] & 0x00FF)) << 4) | (((last[2] & 0xFF00) != (c[2] & 0xFF00)) << 5) |
-                       (((c[0] & 0x00FF) != (c[1] & 0x00FF) || (c[0] & 0x00FF) != (c[2] & 0x00FF) ||
-                         (c[0] & 0xFF00) != (c[1] & 0xFF00) || (c[0] & 0xFF00) != (c[2] & 0xFF00)) << 6);
-        e.symbol(m_used, sym);
-        if (sym & 1) e.symbol(m_diff[0], u8_fold((c[0] & 255) - (last[0] & 255)));
-        if (sym & 2) e.symbol(m_diff[1], u8_fold((c[0] >> 8) - (last[0] >> 8)));
-        if (sym & 64) {
-            int32_t diff = (c[0] & 0xFF) - (last[0] & 0xFF);
-            if (sym & 4) e.symbol(m_diff[2], u8_fold((c[1] & 255) - u8_clamp(diff + (last[1] & 255))));
-            if (sym & 16) {
-                diff = (diff + ((c[1] & 0xFF) - (last[1] & 0xFF))) / 2;
-                e.symbol(m_diff[4], u8_fold((c[2] & 255) - u8_clamp(diff + (last[2] & 255))));
-            }
-            diff = (c[0] >> 8) - (last[0] >> 8);
-            if (sym & 8) e.symbol(m_diff[3], u8_fold((c[1] >> 8) - u8_clamp(diff + (last[1] >> 8))));
-            if (sym & 32) {
-                diff = (diff + ((c[1] >> 8) - (last[1] >> 8))) / 2;
-                e.symbol(m_diff[5], u8_fold((c[2] >> 8) - u8_clamp(diff + (last[2] >> 8))));
-            }
-        }
+        rgb_encode(e, m_used, m_diff, last, c);
         memcpy(last, c, 6);
     }
 };
@@ -805,6 +815,610 @@ struct Bytes : ItemCodec {
     }
 };
 
+// ------------------------------------------------------------------ LASzip 3 layered items
+// Point formats 6-8 (LAS 1.4): POINT14 v3, RGB14 v3, RGBNIR14 v3, BYTE14 v3 in
+// "layered chunked" compression.  Every field group is its own arithmetic
+// stream (layer) per chunk, and a layer whose values never change in a chunk
+// is stored empty (the decoder then keeps the chunk's first value).  Models
+// live in one of four contexts, selected by the point's scanner channel; a
+// context is created, from the previous context's last point, when its
+// channel first appears in the chunk.
+struct LayeredItem {
+    virtual ~LayeredItem() = default;
+    virtual uint32_t layers() const = 0;
+    // decoder: the chunk's first point (stored raw) and this item's layers
+    virtual void init_dec(const uint8_t* item, uint32_t& ctx, const uint8_t* const* lp, const uint32_t* ln) = 0;
+    virtual void read(uint8_t* item, uint32_t& ctx) = 0;
+    virtual bool overrun() const = 0;
+    // encoder
+    virtual void init_enc(const uint8_t* item, uint32_t& ctx) = 0;
+    virtual void write(const uint8_t* item, uint32_t& ctx) = 0;
+    virtual void finish(std::vector<std::vector<uint8_t>>& out) = 0;   // layers() streams, empty if unchanged
+};
+
+struct LayerSet {   // a layered item's streams
+    std::vector<Decoder> dec;
+    std::vector<bool> present, changed;
+    std::vector<Encoder> enc;
+    std::vector<std::vector<uint8_t>> buf;
+    explicit LayerSet(uint32_t n) : dec(n), present(n, false), changed(n, false), enc(n), buf(n) {}
+    void init_dec(const uint8_t* const* lp, const uint32_t* ln) {
+        for (size_t i = 0; i < dec.size(); i++) {
+            present[i] = ln[i] > 0;
+            if (present[i]) dec[i].init(lp[i], lp[i] + ln[i]);
+        }
+    }
+    void init_enc() {
+        for (size_t i = 0; i < enc.size(); i++) {
+            buf[i].clear();
+            enc[i].init(&buf[i]);
+            changed[i] = false;
+        }
+    }
+    void finish(std::vector<std::vector<uint8_t>>& out, bool always_first) {
+        for (size_t i = 0; i < enc.size(); i++) {
+            enc[i].done();
+            out.push_back((changed[i] || (always_first && i == 0)) ? buf[i] : std::vector<uint8_t>());
+        }
+    }
+    bool overrun() const {
+        for (const Decoder& d : dec)
+            if (d.overrun) return true;
+        return false;
+    }
+};
+
+inline std::unique_ptr<SymbolModel>& lazy_init(std::unique_ptr<SymbolModel>& m, uint32_t n, bool enc) {
+    if (!m) m.reset(new SymbolModel(n, enc));
+    return m;
+}
+
+// The 30-byte LAS 1.4 point record: x, y, z (i32), intensity (u16), returns
+// byte (return number bits 0-3, number of returns 4-7), flags byte
+// (classification flags 0-3, scanner channel 4-5, scan direction 6, edge of
+// flight line 7), classification, user data, scan angle (i16), point source
+// id (u16), GPS time (f64)
+struct P14 {
+    int32_t x = 0, y = 0, z = 0;
+    uint16_t intensity = 0, psid = 0;
+    uint8_t r = 0, n = 0, cflags = 0, channel = 0, dir = 0, edge = 0, cls = 0, user = 0;
+    int16_t angle = 0;
+    int64_t gps = 0;
+    bool gps_change = false;
+};
+P14 unpack14(const uint8_t* p) {
+    P14 q;
+    q.x = rd_i32(p);
+    q.y = rd_i32(p + 4);
+    q.z = rd_i32(p + 8);
+    q.intensity = rd_u16(p + 12);
+    q.r = p[14] & 15;
+    q.n = p[14] >> 4;
+    q.cflags = p[15] & 15;
+    q.channel = (p[15] >> 4) & 3;
+    q.dir = (p[15] >> 6) & 1;
+    q.edge = p[15] >> 7;
+    q.cls = p[16];
+    q.user = p[17];
+    q.angle = (int16_t)rd_u16(p + 18);
+    q.psid = rd_u16(p + 20);
+    memcpy(&q.gps, p + 22, 8);
+    return q;
+}
+void pack14(const P14& q, uint8_t* p) {
+    wr_i32(p, q.x);
+    wr_i32(p + 4, q.y);
+    wr_i32(p + 8, q.z);
+    wr_u16(p + 12, q.intensity);
+    p[14] = (uint8_t)(q.r | (q.n << 4));
+    p[15] = (uint8_t)(q.cflags | (q.channel << 4) | (q.dir << 6) | (q.edge << 7));
+    p[16] = q.cls;
+    p[17] = q.user;
+    wr_u16(p + 18, (uint16_t)q.angle);
+    wr_u16(p + 20, q.psid);
+    memcpy(p + 22, &q.gps, 8);
+}
+
+// return-type context (6) and return level (8) of (number of returns, return number)
+const uint8_t kReturnMap6[16][16] = {
+    {0, 1, 2, 3, 4, 5, 3, 4, 4, 5, 5, 5, 5, 5, 5, 5}, {1, 0, 1, 3, 4, 5, 3, 4, 4, 5, 5, 5, 5, 5, 5, 5},
+    {2, 1, 2, 4, 4, 5, 4, 4, 4, 5, 5, 5, 5, 5, 5, 5}, {3, 3, 4, 5, 4, 5, 4, 4, 4, 5, 5, 5, 5, 5, 5, 5},
+    {4, 4, 4, 4, 5, 5, 4, 4, 4, 5, 5, 5, 5, 5, 5, 5}, {5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5},
+    {3, 3, 4, 4, 4, 5, 5, 4, 4, 5, 5, 5, 5, 5, 5, 5}, {4, 4, 4, 4, 4, 5, 4, 5, 4, 5, 5, 5, 5, 5, 5, 5},
+    {4, 4, 4, 4, 4, 5, 4, 4, 5, 5, 5, 5, 5, 5, 5, 5}, {5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5},
+    {5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5}, {5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5},
+    {5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5}, {5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5},
+    {5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5}, {5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5}};
+inline uint32_t return_level8(uint32_t n, uint32_t r) { return std::min<uint32_t>(n > r ? n - r : r - n, 7); }
+
+// GPS time codes of the layered coder: no "unchanged" code (the layer is only
+// coded for points whose time changed)
+constexpr uint32_t kGps3CodeFull = kGpsMulti - kGpsMultiMinus + 1;   // 511
+constexpr uint32_t kGps3Total = kGpsMulti - kGpsMultiMinus + 5;      // 515
+
+struct P14Ctx {
+    P14 last;
+    std::vector<SymbolModel> m_changed;
+    SymbolModel m_scanner, m_rn_same, m_gps_multi, m_gps_0diff;
+    std::unique_ptr<SymbolModel> m_nret[16], m_rnum[16], m_class[64], m_flags[64], m_user[64];
+    IntegerCompressor ic_dx, ic_dy, ic_z, ic_int, ic_angle, ic_psid, ic_gps;
+    Median5 mx[12], my[12];
+    int32_t last_z[8];
+    uint16_t last_int[8];
+    uint32_t glast = 0, gnext = 0;
+    int64_t gps[4] = {0, 0, 0, 0};
+    int32_t gdiff[4] = {0, 0, 0, 0}, gext[4] = {0, 0, 0, 0};
+    P14Ctx(bool e, const P14& item)
+        : last(item), m_scanner(3, e), m_rn_same(13, e), m_gps_multi(kGps3Total, e), m_gps_0diff(5, e),
+          ic_dx(e, 32, 2), ic_dy(e, 32, 22), ic_z(e, 32, 20), ic_int(e, 16, 4), ic_angle(e, 16, 2), ic_psid(e, 16, 1),
+          ic_gps(e, 32, 9) {
+        for (int i = 0; i < 8; i++) m_changed.emplace_back(128, e);
+        for (IntegerCompressor* ic : {&ic_dx, &ic_dy, &ic_z, &ic_int, &ic_angle, &ic_psid, &ic_gps}) ic->init();
+        for (int i = 0; i < 8; i++) {
+            last_z[i] = item.z;
+            last_int[i] = item.intensity;
+        }
+        last.gps_change = false;
+        gps[0] = item.gps;
+    }
+};
+
+// LASzip 3 POINT14 (layer order: channel/returns/XY, Z, classification, flags,
+// intensity, scan angle, user data, point source, GPS time)
+struct Point14 : LayeredItem {
+    bool enc;
+    std::unique_ptr<P14Ctx> C[4];
+    uint32_t cur = 0;
+    LayerSet L{9};
+    explicit Point14(bool e) : enc(e) {}
+    uint32_t layers() const override { return 9; }
+    bool overrun() const override { return L.overrun(); }
+    void start(const uint8_t* item, uint32_t& ctx) {
+        const P14 p = unpack14(item);
+        for (auto& c : C) c.reset();
+        cur = p.channel;
+        ctx = cur;
+        C[cur].reset(new P14Ctx(enc, p));
+    }
+    void init_dec(const uint8_t* item, uint32_t& ctx, const uint8_t* const* lp, const uint32_t* ln) override {
+        start(item, ctx);
+        L.init_dec(lp, ln);
+    }
+    void init_enc(const uint8_t* item, uint32_t& ctx) override {
+        start(item, ctx);
+        L.init_enc();
+    }
+    void finish(std::vector<std::vector<uint8_t>>& out) override { L.finish(out, true); }
+    static uint32_t kctx(uint32_t k, uint32_t cap) { return k < cap ? (k & ~1u) : cap; }
+
+    void gps_full(P14Ctx& c, Decoder& d) {
+        c.gnext = (c.gnext + 1) & 3;
+        const uint64_t hi = (uint32_t)c.ic_gps.decompress(d, (int32_t)((uint64_t)c.gps[c.glast] >> 32), 8);
+        c.gps[c.gnext] = (int64_t)((hi << 32) | d.int32());
+        c.glast = c.gnext;
+        c.gdiff[c.glast] = 0;
+        c.gext[c.glast] = 0;
+    }
+    void read_gps(P14Ctx& c, Decoder& d) {
+        for (;;) {
+            uint32_t& l = c.glast;
+            if (c.gdiff[l] == 0) {
+                const uint32_t multi = d.symbol(c.m_gps_0diff);
+                if (multi == 0) {
+                    c.gdiff[l] = c.ic_gps.decompress(d, 0, 0);
+                    c.gps[l] = (int64_t)((uint64_t)c.gps[l] + (uint64_t)(int64_t)c.gdiff[l]);
+                    c.gext[l] = 0;
+                } else if (multi == 1) {
+                    gps_full(c, d);
+                } else {
+                    l = (l + multi - 1) & 3;
+                    continue;
+                }
+            } else {
+                const uint32_t multi = d.symbol(c.m_gps_multi);
+                if (multi == 1) {
+                    c.gps[l] = (int64_t)((uint64_t)c.gps[l] + (uint64_t)(int64_t)c.ic_gps.decompress(d, c.gdiff[l], 1));
+                    c.gext[l] = 0;
+                } else if (multi < kGps3CodeFull) {
+                    int32_t g;
+                    if (multi == 0) {
+                        g = c.ic_gps.decompress(d, 0, 7);
+                        if (++c.gext[l] > 3) { c.gdiff[l] = g; c.gext[l] = 0; }
+                    } else if (multi < (uint32_t)kGpsMulti) {
+                        g = c.ic_gps.decompress(d, (int32_t)(multi * (uint32_t)c.gdiff[l]), multi < 10 ? 2 : 3);
+                    } else if (multi == (uint32_t)kGpsMulti) {
+                        g = c.ic_gps.decompress(d, (int32_t)((uint32_t)kGpsMulti * (uint32_t)c.gdiff[l]), 4);
+                        if (++c.gext[l] > 3) { c.gdiff[l] = g; c.gext[l] = 0; }
+                    } else {
+                        const int32_t mm = kGpsMulti - (int32_t)multi;
+                        if (mm > kGpsMultiMinus) {
+                            g = c.ic_gps.decompress(d, (int32_t)((uint32_t)mm * (uint32_t)c.gdiff[l]), 5);
+                        } else {
+                            g = c.ic_gps.decompress(d, (int32_t)((uint32_t)kGpsMultiMinus * (uint32_t)c.gdiff[l]), 6);
+                            if (++c.gext[l] > 3) { c.gdiff[l] = g; c.gext[l] = 0; }
+                        }
+                    }
+                    c.gps[l] = (int64_t)((uint64_t)c.gps[l] + (uint64_t)(int64_t)g);
+                } else if (multi == kGps3CodeFull) {
+                    gps_full(c, d);
+                } else {
+                    l = (l + multi - kGps3CodeFull) & 3;
+                    continue;
+                }
+            }
+            break;
+        }
+    }
+    // encoder: one time sequence per context (the decoder's four-sequence
+    // switching is never needed to reproduce the input)
+    void write_gps(P14Ctx& c, Encoder& e, int64_t t) {
+        uint32_t& l = c.glast;
+        const int64_t dd = (int64_t)((uint64_t)t - (uint64_t)c.gps[l]);
+        const bool fits = dd >= INT32_MIN && dd <= INT32_MAX;
+        auto full = [&]() {
+            c.gnext = (c.gnext + 1) & 3;
+            c.ic_gps.compress(e, (int32_t)((uint64_t)c.gps[l] >> 32), (int32_t)((uint64_t)t >> 32), 8);
+            e.int32((uint32_t)(uint64_t)t);
+            l = c.gnext;
+            c.gps[l] = t;
+            c.gdiff[l] = 0;
+            c.gext[l] = 0;
+        };
+        if (c.gdiff[l] == 0) {
+            if (fits) {
+                e.symbol(c.m_gps_0diff, 0);
+                c.ic_gps.compress(e, 0, (int32_t)dd, 0);
+                c.gdiff[l] = (int32_t)dd;
+                c.gext[l] = 0;
+                c.gps[l] = t;
+            } else {
+                e.symbol(c.m_gps_0diff, 1);
+                full();
+            }
+            return;
+        }
+        if (!fits) {
+            e.symbol(c.m_gps_multi, kGps3CodeFull);
+            full();
+            return;
+        }
+        const int32_t g = (int32_t)dd, df = c.gdiff[l];
+        const double mf = (double)g / (double)df;
+        const int32_t multi = mf > 1e6 ? 1000000 : mf < -1e6 ? -1000000 : (int32_t)(mf >= 0 ? mf + 0.5 : mf - 0.5);
+        if (multi == 1) {
+            e.symbol(c.m_gps_multi, 1);
+            c.ic_gps.compress(e, df, g, 1);
+            c.gext[l] = 0;
+        } else if (multi > 0 && multi < kGpsMulti) {
+            e.symbol(c.m_gps_multi, (uint32_t)multi);
+            c.ic_gps.compress(e, (int32_t)((uint32_t)multi * (uint32_t)df), g, multi < 10 ? 2 : 3);
+        } else if (multi >= kGpsMulti) {
+            e.symbol(c.m_gps_multi, kGpsMulti);
+            c.ic_gps.compress(e, (int32_t)((uint32_t)kGpsMulti * (uint32_t)df), g, 4);
+            if (++c.gext[l] > 3) { c.gdiff[l] = g; c.gext[l] = 0; }
+        } else if (multi < 0 && multi > kGpsMultiMinus) {
+            e.symbol(c.m_gps_multi, (uint32_t)(kGpsMulti - multi));
+            c.ic_gps.compress(e, (int32_t)((uint32_t)multi * (uint32_t)df), g, 5);
+        } else if (multi < 0) {
+            e.symbol(c.m_gps_multi, (uint32_t)(kGpsMulti - kGpsMultiMinus));
+            c.ic_gps.compress(e, (int32_t)((uint32_t)kGpsMultiMinus * (uint32_t)df), g, 6);
+            if (++c.gext[l] > 3) { c.gdiff[l] = g; c.gext[l] = 0; }
+        } else {
+            e.symbol(c.m_gps_multi, 0);
+            c.ic_gps.compress(e, 0, g, 7);
+            if (++c.gext[l] > 3) { c.gdiff[l] = g; c.gext[l] = 0; }
+        }
+        c.gps[l] = t;
+    }
+
+    void read(uint8_t* item, uint32_t& ctx) override {
+        P14Ctx* c = C[cur].get();
+        P14* q = &c->last;
+        Decoder& d0 = L.dec[0];
+        const uint32_t lpr = (q->r == 1 ? 1u : 0u) + (q->r >= q->n ? 2u : 0u) + (q->gps_change ? 4u : 0u);
+        const uint32_t changed = d0.symbol(c->m_changed[lpr]);
+        if (changed & 64) {   // scanner channel: next = current + diff + 1 (mod 4)
+            const uint32_t nc = (cur + d0.symbol(c->m_scanner) + 1) & 3;
+            if (!C[nc]) C[nc].reset(new P14Ctx(false, *q));
+            cur = nc;
+            c = C[cur].get();
+            q = &c->last;
+            q->channel = (uint8_t)nc;
+        }
+        ctx = cur;
+        const bool psc = (changed & 32) != 0, gpsc = (changed & 16) != 0, angc = (changed & 8) != 0;
+        const uint32_t last_n = q->n, last_r = q->r;
+        const uint32_t n = (changed & 4) ? d0.symbol(*lazy_init(c->m_nret[last_n], 16, false)) : last_n;
+        uint32_t r;
+        switch (changed & 3) {
+            case 0: r = last_r; break;
+            case 1: r = (last_r + 1) & 15; break;
+            case 2: r = (last_r + 15) & 15; break;
+            default:
+                r = gpsc ? d0.symbol(*lazy_init(c->m_rnum[last_r], 16, false))
+                         : (last_r + d0.symbol(c->m_rn_same) + 2) & 15;
+        }
+        q->n = (uint8_t)n;
+        q->r = (uint8_t)r;
+        const uint32_t m = kReturnMap6[n][r], lv = return_level8(n, r);
+        const uint32_t cpr = (r == 1 ? 2u : 0u) + (r >= n ? 1u : 0u);
+        const uint32_t mi = (m << 1) | (gpsc ? 1u : 0u);
+        int32_t diff = c->ic_dx.decompress(d0, c->mx[mi].get(), n == 1);
+        q->x = (int32_t)((uint32_t)q->x + (uint32_t)diff);
+        c->mx[mi].add(diff);
+        diff = c->ic_dy.decompress(d0, c->my[mi].get(), (n == 1) + kctx(c->ic_dx.k, 20));
+        q->y = (int32_t)((uint32_t)q->y + (uint32_t)diff);
+        c->my[mi].add(diff);
+        if (L.present[1]) {
+            const uint32_t kb = (c->ic_dx.k + c->ic_dy.k) / 2;
+            q->z = c->ic_z.decompress(L.dec[1], c->last_z[lv], (n == 1) + kctx(kb, 18));
+            c->last_z[lv] = q->z;
+        }
+        if (L.present[2]) {
+            const uint32_t ccc = ((q->cls & 0x1Fu) << 1) + (cpr == 3 ? 1u : 0u);
+            q->cls = (uint8_t)L.dec[2].symbol(*lazy_init(c->m_class[ccc], 256, false));
+        }
+        if (L.present[3]) {
+            const uint32_t lf = (q->edge << 5) | (q->dir << 4) | q->cflags;
+            const uint32_t f = L.dec[3].symbol(*lazy_init(c->m_flags[lf], 64, false));
+            q->edge = (f >> 5) & 1;
+            q->dir = (f >> 4) & 1;
+            q->cflags = f & 15;
+        }
+        if (L.present[4]) {
+            const uint32_t li = (cpr << 1) | (gpsc ? 1u : 0u);
+            q->intensity = (uint16_t)c->ic_int.decompress(L.dec[4], c->last_int[li], cpr);
+            c->last_int[li] = q->intensity;
+        }
+        if (L.present[5] && angc) q->angle = (int16_t)c->ic_angle.decompress(L.dec[5], q->angle, gpsc ? 1 : 0);
+        if (L.present[6]) q->user = (uint8_t)L.dec[6].symbol(*lazy_init(c->m_user[q->user / 4], 256, false));
+        if (L.present[7] && psc) q->psid = (uint16_t)c->ic_psid.decompress(L.dec[7], q->psid, 0);
+        if (L.present[8] && gpsc) {
+            read_gps(*c, L.dec[8]);
+            q->gps = c->gps[c->glast];
+        }
+        pack14(*q, item);
+        q->gps_change = gpsc;
+    }
+
+    void write(const uint8_t* item, uint32_t& ctx) override {
+        const P14 p = unpack14(item);
+        P14Ctx* c = C[cur].get();
+        const P14& q0 = c->last;
+        const uint32_t lpr = (q0.r == 1 ? 1u : 0u) + (q0.r >= q0.n ? 2u : 0u) + (q0.gps_change ? 4u : 0u);
+        const bool sw = p.channel != cur;
+        P14Ctx* nc = c;
+        if (sw) {
+            if (!C[p.channel]) C[p.channel].reset(new P14Ctx(true, q0));
+            nc = C[p.channel].get();
+        }
+        P14& q = nc->last;
+        const bool psc = p.psid != q.psid, gpsc = p.gps != q.gps, angc = p.angle != q.angle;
+        uint32_t rcode = 3;
+        if (p.r == q.r) rcode = 0;
+        else if (p.r == ((q.r + 1) & 15)) rcode = 1;
+        else if (p.r == ((q.r + 15) & 15)) rcode = 2;
+        const uint32_t changed = (sw ? 64u : 0u) | (psc ? 32u : 0u) | (gpsc ? 16u : 0u) | (angc ? 8u : 0u) |
+                                 (p.n != q.n ? 4u : 0u) | rcode;
+        Encoder& e0 = L.enc[0];
+        e0.symbol(c->m_changed[lpr], changed);
+        if (sw) {
+            e0.symbol(c->m_scanner, (p.channel + 4 - cur - 1) & 3);
+            cur = p.channel;
+            q.channel = p.channel;
+            c = nc;
+        }
+        ctx = cur;
+        if (p.n != q.n) e0.symbol(*lazy_init(c->m_nret[q.n], 16, true), p.n);
+        if (rcode == 3) {
+            if (gpsc) e0.symbol(*lazy_init(c->m_rnum[q.r], 16, true), p.r);
+            else e0.symbol(c->m_rn_same, (p.r + 16 - q.r - 2) & 15);
+        }
+        const uint32_t n = p.n, r = p.r;
+        const uint32_t m = kReturnMap6[n][r], lv = return_level8(n, r);
+        const uint32_t cpr = (r == 1 ? 2u : 0u) + (r >= n ? 1u : 0u);
+        const uint32_t mi = (m << 1) | (gpsc ? 1u : 0u);
+        int32_t diff = (int32_t)((uint32_t)p.x - (uint32_t)q.x);
+        c->ic_dx.compress(e0, c->mx[mi].get(), diff, n == 1);
+        c->mx[mi].add(diff);
+        diff = (int32_t)((uint32_t)p.y - (uint32_t)q.y);
+        c->ic_dy.compress(e0, c->my[mi].get(), diff, (n == 1) + kctx(c->ic_dx.k, 20));
+        c->my[mi].add(diff);
+        const uint32_t kb = (c->ic_dx.k + c->ic_dy.k) / 2;
+        c->ic_z.compress(L.enc[1], c->last_z[lv], p.z, (n == 1) + kctx(kb, 18));
+        c->last_z[lv] = p.z;
+        L.changed[1] = L.changed[1] || p.z != q.z;
+        const uint32_t ccc = ((q.cls & 0x1Fu) << 1) + (cpr == 3 ? 1u : 0u);
+        L.enc[2].symbol(*lazy_init(c->m_class[ccc], 256, true), p.cls);
+        L.changed[2] = L.changed[2] || p.cls != q.cls;
+        const uint32_t lf = (q.edge << 5) | (q.dir << 4) | q.cflags, f = (p.edge << 5) | (p.dir << 4) | p.cflags;
+        L.enc[3].symbol(*lazy_init(c->m_flags[lf], 64, true), f);
+        L.changed[3] = L.changed[3] || f != lf;
+        const uint32_t li = (cpr << 1) | (gpsc ? 1u : 0u);
+        c->ic_int.compress(L.enc[4], c->last_int[li], p.intensity, cpr);
+        c->last_int[li] = p.intensity;
+        L.changed[4] = L.changed[4] || p.intensity != q.intensity;
+        if (angc) {
+            c->ic_angle.compress(L.enc[5], q.angle, p.angle, gpsc ? 1 : 0);
+            L.changed[5] = true;
+        }
+        L.enc[6].symbol(*lazy_init(c->m_user[q.user / 4], 256, true), p.user);
+        L.changed[6] = L.changed[6] || p.user != q.user;
+        if (psc) {
+            c->ic_psid.compress(L.enc[7], q.psid, p.psid, 0);
+            L.changed[7] = true;
+        }
+        if (gpsc) {
+            write_gps(*c, L.enc[8], p.gps);
+            L.changed[8] = true;
+        }
+        q = p;
+        q.gps_change = gpsc;
+    }
+};
+
+// RGB14 v3 (colour layer) and RGBNIR14 v3 (plus a near-infrared layer): the
+// RGB12 v2 model per context
+struct RgbCtx {
+    SymbolModel m_used;
+    std::vector<SymbolModel> m_diff;
+    SymbolModel m_nir_used;
+    std::vector<SymbolModel> m_nir;
+    uint16_t last[4];
+    RgbCtx(bool e, const uint16_t* item) : m_used(128, e), m_nir_used(4, e) {
+        for (int i = 0; i < 6; i++) m_diff.emplace_back(256, e);
+        for (int i = 0; i < 2; i++) m_nir.emplace_back(256, e);
+        memcpy(last, item, 8);
+    }
+};
+
+struct Rgb14 : LayeredItem {
+    bool enc, nir;
+    std::unique_ptr<RgbCtx> C[4];
+    uint32_t cur = 0;
+    LayerSet L;
+    Rgb14(bool e, bool with_nir) : enc(e), nir(with_nir), L(with_nir ? 2 : 1) {}
+    uint32_t layers() const override { return nir ? 2 : 1; }
+    bool overrun() const override { return L.overrun(); }
+    void start(const uint8_t* item, uint32_t ctx) {
+        uint16_t v[4] = {0, 0, 0, 0};
+        memcpy(v, item, nir ? 8 : 6);
+        for (auto& c : C) c.reset();
+        cur = ctx;
+        C[cur].reset(new RgbCtx(enc, v));
+    }
+    void init_dec(const uint8_t* item, uint32_t& ctx, const uint8_t* const* lp, const uint32_t* ln) override {
+        start(item, ctx);
+        L.init_dec(lp, ln);
+    }
+    void init_enc(const uint8_t* item, uint32_t& ctx) override {
+        start(item, ctx);
+        L.init_enc();
+    }
+    void finish(std::vector<std::vector<uint8_t>>& out) override { L.finish(out, false); }
+    RgbCtx* switch_to(uint32_t ctx) {
+        if (ctx != cur) {
+            if (!C[ctx]) C[ctx].reset(new RgbCtx(enc, C[cur]->last));
+            cur = ctx;
+        }
+        return C[cur].get();
+    }
+    void read(uint8_t* item, uint32_t& ctx) override {
+        RgbCtx* c = switch_to(ctx);
+        uint16_t v[4];
+        memcpy(v, c->last, 8);
+        if (L.present[0]) rgb_decode(L.dec[0], c->m_used, c->m_diff, c->last, v);
+        if (nir && L.present[1]) {
+            Decoder& d = L.dec[1];
+            const uint32_t sym = d.symbol(c->m_nir_used);
+            uint16_t w = (sym & 1) ? u8_fold((int32_t)d.symbol(c->m_nir[0]) + (c->last[3] & 255)) : (c->last[3] & 0xFF);
+            w |= (sym & 2) ? (uint16_t)(u8_fold((int32_t)d.symbol(c->m_nir[1]) + (c->last[3] >> 8)) << 8)
+                           : (uint16_t)(c->last[3] & 0xFF00);
+            v[3] = w;
+        }
+        memcpy(c->last, v, 8);
+        memcpy(item, v, nir ? 8 : 6);
+    }
+    void write(const uint8_t* item, uint32_t& ctx) override {
+        RgbCtx* c = switch_to(ctx);
+        uint16_t v[4] = {0, 0, 0, 0};
+        memcpy(v, item, nir ? 8 : 6);
+        if (rgb_encode(L.enc[0], c->m_used, c->m_diff, c->last, v)) L.changed[0] = true;
+        if (nir) {
+            const uint32_t sym = ((c->last[3] & 0xFF) != (v[3] & 0xFF)) | (((c->last[3] & 0xFF00) != (v[3] & 0xFF00)) << 1);
+            Encoder& e = L.enc[1];
+            e.symbol(c->m_nir_used, sym);
+            if (sym & 1) e.symbol(c->m_nir[0], u8_fold((v[3] & 255) - (c->last[3] & 255)));
+            if (sym & 2) e.symbol(c->m_nir[1], u8_fold((v[3] >> 8) - (c->last[3] >> 8)));
+            if (sym) L.changed[1] = true;
+        }
+        memcpy(c->last, v, 8);
+    }
+};
+
+// BYTE14 v3: one layer per extra byte, per-byte differences
+struct Bytes14 : LayeredItem {
+    bool enc;
+    uint32_t nb;
+    struct Ctx {
+        std::vector<SymbolModel> m;
+        std::vector<uint8_t> last;
+    };
+    std::unique_ptr<Ctx> C[4];
+    uint32_t cur = 0;
+    LayerSet L;
+    Bytes14(bool e, uint32_t n) : enc(e), nb(n), L(n) {}
+    uint32_t layers() const override { return nb; }
+    bool overrun() const override { return L.overrun(); }
+    Ctx* make(const uint8_t* item) {
+        Ctx* c = new Ctx();
+        for (uint32_t i = 0; i < nb; i++) c->m.emplace_back(256, enc);
+        c->last.assign(item, item + nb);
+        return c;
+    }
+    void start(const uint8_t* item, uint32_t ctx) {
+        for (auto& c : C) c.reset();
+        cur = ctx;
+        C[cur].reset(make(item));
+    }
+    void init_dec(const uint8_t* item, uint32_t& ctx, const uint8_t* const* lp, const uint32_t* ln) override {
+        start(item, ctx);
+        L.init_dec(lp, ln);
+    }
+    void init_enc(const uint8_t* item, uint32_t& ctx) override {
+        start(item, ctx);
+        L.init_enc();
+    }
+    void finish(std::vector<std::vector<uint8_t>>& out) override { L.finish(out, false); }
+    Ctx* switch_to(uint32_t ctx) {
+        if (ctx != cur) {
+            if (!C[ctx]) C[ctx].reset(make(C[cur]->last.data()));
+            cur = ctx;
+        }
+        return C[cur].get();
+    }
+    void read(uint8_t* item, uint32_t& ctx) override {
+        Ctx* c = switch_to(ctx);
+        for (uint32_t i = 0; i < nb; i++) {
+            if (L.present[i]) c->last[i] = u8_fold((int32_t)c->last[i] + (int32_t)L.dec[i].symbol(c->m[i]));
+            item[i] = c->last[i];
+        }
+    }
+    void write(const uint8_t* item, uint32_t& ctx) override {
+        Ctx* c = switch_to(ctx);
+        for (uint32_t i = 0; i < nb; i++) {
+            const int32_t diff = (int32_t)item[i] - (int32_t)c->last[i];
+            L.enc[i].symbol(c->m[i], u8_fold(diff));
+            if (diff) L.changed[i] = true;
+            c->last[i] = item[i];
+        }
+    }
+};
+
+bool is_layered(const std::vector<Item>& items) { return !items.empty() && items[0].type == POINT14; }
+
+bool make_layered(const std::vector<Item>& items, bool enc, std::vector<std::unique_ptr<LayeredItem>>& out,
+                  std::string& err) {
+    out.clear();
+    for (size_t i = 0; i < items.size(); i++) {
+        const Item& it = items[i];
+        if (it.version != 3) {
+            err = "LAZ item type " + std::to_string(it.type) + " version " + std::to_string(it.version) + " is not supported";
+            return false;
+        }
+        if (i == 0 ? (it.type == POINT14 && it.size == 30) : false) out.emplace_back(new Point14(enc));
+        else if (i > 0 && it.type == RGB14 && it.size == 6) out.emplace_back(new Rgb14(enc, false));
+        else if (i > 0 && it.type == RGBNIR14 && it.size == 8) out.emplace_back(new Rgb14(enc, true));
+        else if (i > 0 && it.type == BYTE14 && it.size >= 1) out.emplace_back(new Bytes14(enc, it.size));
+        else {
+            err = "LAZ item type " + std::to_string(it.type) + " (size " + std::to_string(it.size) +
+                  ") is not supported in layered compression";
+            return false;
+        }
+    }
+    return true;
+}
+
 bool make_codecs(const std::vector<Item>& items, bool enc, std::vector<std::unique_ptr<ItemCodec>>& out,
                  std::string& err) {
     out.clear();
@@ -828,9 +1442,11 @@ bool make_codecs(const std::vector<Item>& items, bool enc, std::vector<std::uniq
 class PointDecoder {
 public:
     std::vector<std::unique_ptr<ItemCodec>> codecs;
+    std::vector<std::unique_ptr<LayeredItem>> layered;   // compressor 3
     std::vector<uint16_t> sizes;
     Decoder dec;
     bool first = true;
+    uint32_t ctx = 0;
 };
 
 bool parse_vlr(const uint8_t* d, size_t n, Vlr& v, std::string& err) {
@@ -877,11 +1493,23 @@ std::vector<uint8_t> write_vlr(const Vlr& v) {
     return d;
 }
 
+uint16_t compressor_for_format(uint8_t format) { return format >= 6 ? 3 : 2; }
+
 bool items_for_format(uint8_t format, uint16_t rec, std::vector<Item>& items, std::string& err) {
-    static const uint16_t base[4] = {20, 28, 26, 34};
-    if (format > 3) { err = "LAZ point format " + std::to_string(format) + " (layered compression) is not supported"; return false; }
+    static const uint16_t base[9] = {20, 28, 26, 34, 0, 0, 30, 36, 38};
+    if (format > 8 || base[format] == 0) {
+        err = "LAZ point format " + std::to_string(format) + " is not supported";
+        return false;
+    }
     if (rec < base[format]) { err = "point record shorter than its format"; return false; }
     items.clear();
+    if (format >= 6) {
+        items.push_back({POINT14, 30, 3});
+        if (format == 7) items.push_back({RGB14, 6, 3});
+        if (format == 8) items.push_back({RGBNIR14, 8, 3});
+        if (rec > base[format]) items.push_back({BYTE14, (uint16_t)(rec - base[format]), 3});
+        return true;
+    }
     items.push_back({POINT10, 20, 2});
     if (format == 1 || format == 3) items.push_back({GPSTIME11, 8, 2});
     if (format == 2 || format == 3) items.push_back({RGB12, 6, 2});
@@ -898,15 +1526,17 @@ bool Reader::open(FILE* f, uint64_t data_off, uint64_t npoints, uint16_t rec, co
     left_ = npoints;
     v_ = v;
     if (v.coder != 0) { err = "LAZ coder " + std::to_string(v.coder) + " is not supported"; return false; }
-    if (v.compressor != 1 && v.compressor != 2) {
-        err = "LAZ compressor " + std::to_string(v.compressor) + " (layered, point formats 6-10) is not supported";
+    const bool layered = is_layered(v.items);
+    if (layered ? v.compressor != 3 : (v.compressor != 1 && v.compressor != 2)) {
+        err = "LAZ compressor " + std::to_string(v.compressor) + " does not match its items";
         return false;
     }
     uint32_t sum = 0;
     for (const Item& it : v.items) sum += it.size;
     if (sum != rec) { err = "LAZ items do not add up to the point record length"; return false; }
     dec_.reset(new PointDecoder());
-    if (!make_codecs(v.items, false, dec_->codecs, err)) return false;
+    if (layered ? !make_layered(v.items, false, dec_->layered, err) : !make_codecs(v.items, false, dec_->codecs, err))
+        return false;
     for (const Item& it : v.items) dec_->sizes.push_back(it.size);
     chunk_start_.clear();
     chunk_pts_.clear();
@@ -977,7 +1607,41 @@ uint64_t Reader::read(uint8_t* out, uint64_t m, std::string& err) {
     while (got < m && left_ > 0) {
         if (in_chunk_ == chunk_n_ && !load_chunk(err)) return got;
         uint8_t* rec = out + got * rec_;
-        if (P.first) {   // the chunk's first point is stored raw, then the coder starts
+        if (!P.layered.empty()) {
+            if (P.first) {
+                // layered chunk: the first point raw, its point count, every
+                // layer's size, then the layers in that order
+                size_t o = rec_ + 4;
+                uint32_t nl = 0;
+                for (auto& it : P.layered) nl += it->layers();
+                if (buf_.size() < o + 4ull * nl) { err = "truncated LAZ chunk"; return got; }
+                memcpy(rec, buf_.data(), rec_);
+                std::vector<uint32_t> ln(nl);
+                memcpy(ln.data(), buf_.data() + o, 4ull * nl);
+                o += 4ull * nl;
+                std::vector<const uint8_t*> lp(nl);
+                for (uint32_t i = 0; i < nl; i++) {
+                    if (o + ln[i] > buf_.size()) { err = "truncated LAZ chunk"; return got; }
+                    lp[i] = buf_.data() + o;
+                    o += ln[i];
+                }
+                size_t io = 0;
+                uint32_t li = 0;
+                for (size_t i = 0; i < P.layered.size(); i++) {
+                    P.layered[i]->init_dec(rec + io, P.ctx, lp.data() + li, ln.data() + li);
+                    li += P.layered[i]->layers();
+                    io += P.sizes[i];
+                }
+                P.first = false;
+            } else {
+                size_t io = 0;
+                for (size_t i = 0; i < P.layered.size(); i++) {
+                    P.layered[i]->read(rec + io, P.ctx);
+                    io += P.sizes[i];
+                    if (P.layered[i]->overrun()) { err = "corrupt LAZ chunk"; return got; }
+                }
+            }
+        } else if (P.first) {   // the chunk's first point is stored raw, then the coder starts
             if (buf_.size() < rec_) { err = "truncated LAZ chunk"; return got; }
             memcpy(rec, buf_.data(), rec_);
             size_t o = 0;
@@ -1008,11 +1672,42 @@ uint64_t Reader::read(uint8_t* out, uint64_t m, std::string& err) {
 std::vector<uint8_t> compress(const uint8_t* recs, uint64_t n, uint16_t rec, const std::vector<Item>& items,
                               uint32_t chunk_size) {
     std::vector<std::unique_ptr<ItemCodec>> codecs;
+    std::vector<std::unique_ptr<LayeredItem>> layered;
     std::string err;
-    if (!make_codecs(items, true, codecs, err)) throw std::runtime_error(err);
+    const bool lay = is_layered(items);
+    if (lay ? !make_layered(items, true, layered, err) : !make_codecs(items, true, codecs, err))
+        throw std::runtime_error(err);
     std::vector<uint8_t> out(8, 0);   // chunk table offset, filled below
     std::vector<uint64_t> sizes;
-    for (uint64_t c0 = 0; c0 < n; c0 += chunk_size) {
+    for (uint64_t c0 = 0; c0 < n && lay; c0 += chunk_size) {
+        const uint64_t c1 = std::min<uint64_t>(n, c0 + chunk_size);
+        const size_t start = out.size();
+        out.insert(out.end(), recs + c0 * rec, recs + (c0 + 1) * rec);   // first point raw
+        const uint32_t count = (uint32_t)(c1 - c0);
+        out.insert(out.end(), reinterpret_cast<const uint8_t*>(&count), reinterpret_cast<const uint8_t*>(&count) + 4);
+        uint32_t ctx = 0;
+        size_t o = 0;
+        for (size_t i = 0; i < layered.size(); i++) {
+            layered[i]->init_enc(recs + c0 * rec + o, ctx);
+            o += items[i].size;
+        }
+        for (uint64_t p = c0 + 1; p < c1; p++) {
+            o = 0;
+            for (size_t i = 0; i < layered.size(); i++) {
+                layered[i]->write(recs + p * rec + o, ctx);
+                o += items[i].size;
+            }
+        }
+        std::vector<std::vector<uint8_t>> ls;
+        for (auto& it : layered) it->finish(ls);
+        for (auto& l : ls) {
+            const uint32_t sz = (uint32_t)l.size();
+            out.insert(out.end(), reinterpret_cast<const uint8_t*>(&sz), reinterpret_cast<const uint8_t*>(&sz) + 4);
+        }
+        for (auto& l : ls) out.insert(out.end(), l.begin(), l.end());
+        sizes.push_back(out.size() - start);
+    }
+    for (uint64_t c0 = 0; c0 < n && !lay; c0 += chunk_size) {
         const uint64_t c1 = std::min<uint64_t>(n, c0 + chunk_size);
         const size_t start = out.size();
         out.insert(out.end(), recs + c0 * rec, recs + (c0 + 1) * rec);   // first point raw

@@ -1,6 +1,6 @@
 // laz_tool — LAS <-> LAZ utility over laz.h (tests and manual checks; not part
 // of the converter).
-//   laz_tool compress   IN.las OUT.laz [chunk_size]   formats 0-3, LASzip pointwise chunked
+//   laz_tool compress   IN.las OUT.laz [chunk_size]   formats 0-3 (pointwise chunked), 6-8 (layered chunked)
 //   laz_tool decompress IN.laz OUT.las
 #include <stdio.h>
 #include <string.h>
@@ -47,10 +47,10 @@ int main(int argc, char** argv) {
         if (fmt_raw & 0x80) { fprintf(stderr, "already compressed\n"); return 1; }
         const uint32_t chunk = argc > 4 ? (uint32_t)strtoul(argv[4], nullptr, 10) : 50000u;
         laz::Vlr v;
-        v.compressor = 2;
+        v.compressor = laz::compressor_for_format(fmt_raw & 0x3F);
         v.coder = 0;
-        v.version_major = 2;
-        v.version_minor = 2;
+        v.version_major = v.compressor == 3 ? 3 : 2;
+        v.version_minor = v.compressor == 3 ? 4 : 2;
         v.chunk_size = chunk;
         std::string err;
         if (!laz::items_for_format(fmt_raw & 0x3F, rec, v.items, err)) { fprintf(stderr, "%s\n", err.c_str()); return 1; }

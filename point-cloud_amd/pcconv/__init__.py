@@ -38,7 +38,7 @@ EXPORTS = ["pcc_abi_version", "pcc_last_error", "pcc_options_default", "pcc_open
            "pcc_write_cell_view", "pcc_begin_file", "pcc_append_points", "pcc_end_file", "pcc_cancel_file",
            "pcc_set_summary", "pcc_write_cells", "pcc_write_metadata", "pcc_clear_input", "pcc_adopt_prior",
            "pcc_open_subtrees", "pcc_visit_cells", "pcc_shard_route_bitmaps", "pcc_shard_keys_from_bitmaps",
-           "pcc_release_device_cache"]
+           "pcc_release_device_cache", "pcc_grid_cells", "pcc_export_grid", "pcc_shard_resolve_buckets", "pcc_shard_lpt"]
 
 
 class Options(C.Structure):
@@ -166,6 +166,12 @@ def lib():
         L.pcc_set_root_spill_batches.argtypes = [vp, vp, vp, C.c_uint64]
         L.pcc_pending_cells.argtypes = [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         L.pcc_export_pending.argtypes = [vp, vp, vp, vp, vp, vp]
+        L.pcc_shard_lpt.argtypes = [vp, C.c_uint64, C.c_uint32, vp, vp]
+        L.pcc_grid_cells.argtypes = [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+        L.pcc_export_grid.argtypes = [vp, vp, vp, vp]
+        L.pcc_shard_resolve_buckets.argtypes = [vp, vp, C.c_uint64, C.c_uint32, vp, vp, vp, C.c_uint64, C.c_uint32,
+                                                C.c_uint32, vp, vp, vp, vp, vp, vp, C.POINTER(C.c_uint64),
+                                                C.POINTER(C.c_uint64), C.c_int]
         L.pcc_set_summary.argtypes = [vp, C.c_uint64, f3, f3, C.c_uint32]
         L.pcc_write_cells.argtypes = [vp]
         L.pcc_write_metadata.argtypes = [vp]
@@ -294,6 +300,20 @@ class Converter:
                                         C.c_void_p(keys_ptr)))
         return xyz, sb, cn
 
+    def grid_cells(self) -> tuple[int, int]:
+        nc, npt = C.c_uint64(0), C.c_uint64(0)
+        _check(lib().pcc_grid_cells(self._h, C.byref(nc), C.byref(npt)))
+        return nc.value, npt.value
+
+    def export_grid(self, pts_ptr: int):
+        """pcc_export_grid: (cells (n,3) int32, grid points per cell (n,) uint64);
+        the points go to the device buffer (grid_cells()[1] rows)."""
+        nc, _ = self.grid_cells()
+        xyz = np.zeros((nc, 3), dtype=np.int32)
+        cn = np.zeros(nc, dtype=np.uint64)
+        _check(lib().pcc_export_grid(self._h, xyz.ctypes.data, cn.ctypes.data, C.c_void_p(pts_ptr)))
+        return xyz, cn
+
     def set_keyed_points_device(self, pts_ptr: int, keys_ptr: int, n: int):
         """Borrow (no copy) this rank's keyed input until build() returns."""
         _check(lib().pcc_set_keyed_points_device(self._h, C.c_void_p(pts_ptr), C.c_void_p(keys_ptr), n))
@@ -418,6 +438,35 @@ def shard_keys_from_bitmaps(bitmaps_ptr: int, nwords, key0, keys_ptr: int, nkeys
     k0 = (C.c_uint64 * ns)(*[int(v) for v in key0])
     _check(lib().pcc_shard_keys_from_bitmaps(C.c_void_p(bitmaps_ptr), nw, k0, ns, C.c_void_p(keys_ptr), nkeys,
                                              device))
+
+
+def shard_resolve_buckets(seg_n, seg_bucket, nbuckets: int, pts_ptr: int, keys_ptr: int, file_points,
+                          batch_size: int, limit: int, kept_ptr: int, sub_pts_ptr: int, sub_keys_ptr: int,
+                          device: int = 0):
+    """pcc_shard_resolve_buckets: returns (state, spill_batch, kept_n) per bucket
+    (numpy) and the row totals (nkept, nsub) written to the device outputs."""
+    sn = np.ascontiguousarray(seg_n, dtype=np.uint64).reshape(-1)
+    sbk = np.ascontiguousarray(seg_bucket, dtype=np.uint32).reshape(-1)
+    fp = np.ascontiguousarray([int(v) for v in file_points], dtype=np.uint64)
+    st = np.zeros(nbuckets, np.uint32)
+    sb = np.zeros(nbuckets, np.uint32)
+    kn = np.zeros(nbuckets, np.uint64)
+    nk, ns = C.c_uint64(0), C.c_uint64(0)
+    _check(lib().pcc_shard_resolve_buckets(sn.ctypes.data, sbk.ctypes.data, len(sn), nbuckets, C.c_void_p(pts_ptr),
+                                           C.c_void_p(keys_ptr), fp.ctypes.data, len(fp), batch_size, limit,
+                                           st.ctypes.data, sb.ctypes.data, kn.ctypes.data, C.c_void_p(kept_ptr),
+                                           C.c_void_p(sub_pts_ptr), C.c_void_p(sub_keys_ptr), C.byref(nk),
+                                           C.byref(ns), device))
+    return st, sb, kn, nk.value, ns.value
+
+
+def shard_lpt(w, world: int):
+    """pcc_shard_lpt: (owner per item uint32, load per rank float64)."""
+    w = np.ascontiguousarray(w, dtype=np.float64).reshape(-1)
+    own = np.zeros(len(w), np.uint32)
+    load = np.zeros(world, np.float64)
+    _check(lib().pcc_shard_lpt(w.ctypes.data, len(w), world, own.ctypes.data, load.ctypes.data))
+    return own, load
 
 
 def write_cell_view(out_dir: str, view: "CellView"):

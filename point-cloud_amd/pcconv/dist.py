@@ -197,13 +197,8 @@ def assign_owners(hist: np.ndarray, world: int, greedy_max: int = 4096) -> np.nd
     nz = np.flatnonzero(hist)
     if world <= 1 or len(nz) == 0:
         return owner
-    if len(nz) <= greedy_max:
-        order = nz[np.lexsort((nz, -hist[nz]))]
-        load = np.zeros(world, dtype=np.int64)
-        for c in order:
-            r = int(np.argmin(load))
-            owner[c] = r
-            load[r] += hist[c]
+    if len(nz) <= greedy_max:   # (counts < 2^53: exact in the float64 loads)
+        owner[nz] = pcconv.shard_lpt(hist[nz].astype(np.float64), world)[0]
         return owner
     before = np.cumsum(hist) - hist
     owner[:] = np.minimum(world - 1, (before * world) // max(int(hist.sum()), 1)).astype(np.uint32)
@@ -223,18 +218,7 @@ L0_COST, DEEP_COST, DEPTH = 2.0, 1.0, 4.0
 def _lpt(w: np.ndarray, world: int):
     """Largest-first greedy: item i (weight w[i], ties by index) to the least
     loaded rank (ties by rank).  Deterministic on every rank."""
-    import heapq
-    w = np.asarray(w, dtype=np.float64)
-    own = np.zeros(len(w), dtype=np.uint32)
-    load = np.zeros(world, dtype=np.float64)
-    heap = [(0.0, r) for r in range(world)]
-    for i in np.lexsort((np.arange(len(w)), -w)).tolist():
-        ld, r = heapq.heappop(heap)
-        own[i] = r
-        ld += float(w[i])
-        load[r] = ld
-        heapq.heappush(heap, (ld, r))
-    return own, load
+    return pcconv.shard_lpt(w, world)   # C++ (pcc_shard_lpt): the plan tries up to 2 * world + 1 of these
 
 
 @dataclass
@@ -404,7 +388,8 @@ def _exchange_segments(comm, dest: np.ndarray, meta: np.ndarray, lens: np.ndarra
     order = np.argsort(dest, kind="stable")
     if len(order) and not np.array_equal(order, np.arange(len(order))):
         starts = np.concatenate([[0], np.cumsum(lens)])[:-1]
-        idx = torch.cat([torch.arange(int(starts[i]), int(starts[i] + lens[i]), dtype=torch.int64) for i in order])
+        ls, ss = lens[order], starts[order]
+        idx = torch.from_numpy(np.repeat(ss - (np.cumsum(ls) - ls), ls) + np.arange(int(ls.sum()), dtype=np.int64))
         tensors = [t.index_select(0, idx.to(t.device)) for t in tensors]
     nseg = [int(v) for v in np.bincount(dest, minlength=W)] if len(dest) else [0] * W
     nrow = [int(v) for v in np.bincount(dest, weights=lens, minlength=W).astype(np.int64)] if len(dest) else [0] * W
@@ -492,6 +477,30 @@ def assemble_cells(rmw: np.ndarray, grid_pts: torch.Tensor, rmk: np.ndarray, kep
                     "size": size, "sub": sub,
                     "pos": [f32(v) * size + size / f32(2.0) for v in (x, y, z)]})
     return out
+
+
+class AssembledCells:
+    """The level-0 cells a writer assembles (assemble_cells), kept as their
+    pieces -- host rows of counts plus the received grid / kept tensors, on the
+    device -- until the cells are walked or written; iterating materialises
+    them once (one device-to-host copy of each tensor)."""
+
+    def __init__(self, rmw, grid_pts: torch.Tensor, rmk, kept_pts: torch.Tensor, cfg: dict):
+        self.rmw = np.asarray(rmw, dtype=np.int64).reshape(-1, 4)
+        self.rmk = np.asarray(rmk, dtype=np.int64).reshape(-1, 5)
+        self.grid_pts, self.kept_pts, self.cfg = grid_pts, kept_pts, cfg
+        self._cells = None
+        xyz = np.concatenate([self.rmw[:, :3], self.rmk[:, :3] >> 1])
+        self._n = len(np.unique(xyz, axis=0)) if len(xyz) else 0
+
+    def __len__(self):
+        return self._n
+
+    def __iter__(self):
+        if self._cells is None:
+            self._cells = assemble_cells(self.rmw, self.grid_pts, self.rmk, self.kept_pts, self.cfg)
+            self.grid_pts = self.kept_pts = None
+        return iter(self._cells)
 
 
 def cell_view(c: dict):
@@ -711,17 +720,43 @@ class HipShardOps:
         P = torch.empty((m, 4), dtype=torch.int32, device=pts.device)
         K = torch.empty(m, dtype=torch.int32, device=pts.device)
         xyz, sb, cn = c.export_pending(P.data_ptr(), K.data_ptr())
-        partial = []
+        # the partial level-0 cells' grid winners stay on the device (pcc_export_grid)
+        _, ng = c.grid_cells()
+        G = torch.empty((ng, 4), dtype=torch.int32, device=pts.device)
+        self._ready()   # G's block may have been freed by pending torch work
+        pxyz, pn = c.export_grid(G.data_ptr())
+        return st, (xyz, sb, cn, P, K), (pxyz.astype(np.int64), pn.astype(np.int64), G)
 
-        def grab(vp):
-            v = pcconv.CellView.from_address(vp)
-            n = int(v.number_of_points)
-            g = (np.frombuffer((C.c_char * (16 * n)).from_address(v.grid), dtype=np.int32).reshape(n, 4).copy()
-                 if n else np.zeros((0, 4), np.int32))
-            partial.append({"xyz": (int(v.x), int(v.y), int(v.z)), "grid": g})
-            return 0
-        c.visit_cells(grab)
-        return st, (xyz, sb, cn, P, K), partial
+    def resolve_level1(self, rmeta: np.ndarray, pts: torch.Tensor, keys: torch.Tensor, file_points) -> dict:
+        """Module resolve_level1 on the device (pcc_shard_resolve_buckets): the
+        same outputs, with only the segment table and the bucket states crossing
+        to the host."""
+        if hasattr(self, "last_inputs"):
+            self.last_inputs["resolve"] = (rmeta, pts, keys, file_points)
+        rmeta = np.asarray(rmeta, dtype=np.int64).reshape(-1, 4)
+        rmeta = rmeta[rmeta[:, 3] > 0]   # empty segments carry no rows
+        dev = pts.device
+        if not len(rmeta):
+            return {"sub_pts": pts[:0], "sub_keys": keys[:0], "roots_xyz": np.zeros((0, 3), np.int32),
+                    "roots_sb": np.zeros(0, np.uint32), "bucket_rows": np.zeros((0, 5), np.int64),
+                    "kept_pts": pts[:0]}
+        cells, inv = np.unique(rmeta[:, :3], axis=0, return_inverse=True)   # sorted (x, y, z) as the numpy statement
+        inv = inv.reshape(-1)
+        nrow = int(rmeta[:, 3].sum())
+        if nrow != int(pts.shape[0]) or nrow != int(keys.shape[0]):
+            raise ValueError("segment rows do not match the received emissions")
+        kept = torch.empty((nrow, 4), dtype=torch.int32, device=dev)
+        sub = torch.empty((nrow, 4), dtype=torch.int32, device=dev)
+        subk = torch.empty(nrow, dtype=torch.int32, device=dev)
+        self._ready()
+        st, sb, _, nk, ns = pcconv.shard_resolve_buckets(rmeta[:, 3], inv, len(cells), pts.data_ptr(),
+                                                         keys.data_ptr(), file_points, self.batch_size, self.limit,
+                                                         kept.data_ptr(), sub.data_ptr(), subk.data_ptr(), self.dev)
+        tot = np.bincount(inv, weights=rmeta[:, 3], minlength=len(cells)).astype(np.int64)
+        spilled = st == 2
+        rows = np.column_stack([cells, st.astype(np.int64), tot]).astype(np.int64).reshape(-1, 5)
+        return {"sub_pts": sub[:ns], "sub_keys": subk[:ns], "roots_xyz": cells[spilled].astype(np.int32).reshape(-1, 3),
+                "roots_sb": sb[spilled].astype(np.uint32), "bucket_rows": rows, "kept_pts": kept[:nk]}
 
     def sub_build(self, file_points, pts: torch.Tensor, keys: torch.Tensor, cells_xyz, spill_batch) -> dict:
         """The level-1 sub-trees of split cells this rank owns (their arrivals, cell
@@ -851,13 +886,19 @@ def shard_build(comm, ops, pts: torch.Tensor, key0: int, file_points, write: boo
     ms = {}
     t0 = time.perf_counter()
 
+    c0 = getattr(comm, "elapsed_ms", None)   # a timing communicator (scripts/rank_stages.py) splits out its calls
+
     def mark(name):
-        nonlocal t0
+        nonlocal t0, c0
         if sync is not None:
             sync()
         t1 = time.perf_counter()
         ms[name] = ms.get(name, 0.0) + (t1 - t0) * 1e3
         t0 = t1
+        if c0 is not None:
+            c1 = comm.elapsed_ms
+            ms[name + "_comm"] = ms.get(name + "_comm", 0.0) + (c1 - c0)
+            c0 = c1
 
     W, dev = comm.world, pts.device
     n_total = int(sum(int(v) for v in file_points))
@@ -892,11 +933,14 @@ def shard_build(comm, ops, pts: torch.Tensor, key0: int, file_points, write: boo
         if grid1 is not None:
             sh = ops.slab_histogram(pts, grid)
             sh_h = comm.allreduce_(sh.to(comm.device).to(torch.int64), "sum").cpu().numpy()
+            mark("hist")
             hist_h = sh_h.reshape(-1, NL).sum(axis=1)
             plan = plan_split(hist_h, None, None, W, allow=False)
             if plan.est["ratio"] > 1.02:   # whole cells unbalanced: consider sharing (level-1 histogram)
+                mark("plan")
                 h1 = ops.histogram(pts, grid1)
                 hist1_h = comm.allreduce_(h1.to(comm.device).to(torch.int64), "sum").cpu().numpy()
+                mark("hist")
                 ch = np.full((len(hist_h), 8), -1, dtype=np.int64)
                 nz = np.flatnonzero(hist_h)
                 ch[nz] = children_ids(nz, grid, grid1)
@@ -904,6 +948,7 @@ def shard_build(comm, ops, pts: torch.Tensor, key0: int, file_points, write: boo
         else:
             hist = ops.histogram(pts, grid)
             hist_h = comm.allreduce_(hist.to(comm.device).to(torch.int64), "sum").cpu().numpy()
+            mark("hist")
             plan = plan_split(hist_h, None, None, W, allow=False)
         owner_h = plan.owner0
         owned = int(np.count_nonzero((owner_h == comm.rank) & (hist_h > 0) & ~plan.split))
@@ -971,7 +1016,7 @@ def shard_build(comm, ops, pts: torch.Tensor, key0: int, file_points, write: boo
     if plan is not None and plan.split.any() and W > 1:
         # ... and the slots of the shared cells' slabs it holds (raw level 0:
         # every emission forwarded with the key of the arrival that caused it)
-        lst, (xyz, _, cn, P, K), partial = ops.lead_build_raw(file_points, lrecv, lkeys)
+        lst, (xyz, _, cn, P, K), (pxyz, pn, gpts) = ops.lead_build_raw(file_points, lrecv, lkeys)
         parts.append(lst)
         phases["lead"] = int(lst["arrivals"])
         mark("lead")
@@ -982,16 +1027,20 @@ def shard_build(comm, ops, pts: torch.Tensor, key0: int, file_points, write: boo
         d1 = plan.owner1[level1_ids(xyz, grid1)].astype(np.int64) if len(xyz) else np.zeros(0, np.int64)
         rm1, (rP, rK) = _exchange_segments(comm, d1, np.column_stack([xyz, cn]), cn, [P, K], dev)
         del P, K
-        pxyz = np.array([q["xyz"] for q in partial], dtype=np.int64).reshape(-1, 3)
-        pn = np.array([len(q["grid"]) for q in partial], dtype=np.int64)
-        gpts = torch.from_numpy(np.concatenate([q["grid"] for q in partial]) if partial
-                                else np.zeros((0, 4), np.int32)).to(dev)
+        pxyz = np.asarray(pxyz, dtype=np.int64).reshape(-1, 3)
+        pn = np.asarray(pn, dtype=np.int64).reshape(-1)
         dw = plan.writer[cell_ids(pxyz, grid)].astype(np.int64) if len(pxyz) else np.zeros(0, np.int64)
-        rmw, (rG,) = _exchange_segments(comm, dw, np.column_stack([pxyz, pn]), pn, [gpts], dev)
+        rmw, (rG,) = _exchange_segments(comm, dw, np.column_stack([pxyz, pn]), pn, [gpts.to(dev)], dev)
+        del gpts
         mark("exchange2")
         # 5c. phase 2: resolve each received level-1 cell's bucket (all ranks'
-        # emissions), build the spilled ones' sub-trees
-        res = resolve_level1(rm1, rP, rK, file_points, ops.batch_size, ops.limit)
+        # emissions; on the device when the ops offer it), build the spilled ones'
+        # sub-trees
+        if hasattr(ops, "resolve_level1"):
+            res = ops.resolve_level1(rm1, rP, rK, file_points)
+        else:
+            res = resolve_level1(rm1, rP, rK, file_points, ops.batch_size, ops.limit)
+        mark("resolve")
         sub_points = int(res["sub_pts"].shape[0])
         sst = ops.sub_build(file_points, res["sub_pts"], res["sub_keys"], res["roots_xyz"], res["roots_sb"])
         parts.append(sst)
@@ -1001,7 +1050,9 @@ def shard_build(comm, ops, pts: torch.Tensor, key0: int, file_points, write: boo
         bx = res["bucket_rows"]
         dk = (plan.writer[cell_ids(bx[:, :3] >> 1, grid)].astype(np.int64) if len(bx) else np.zeros(0, np.int64))
         rmk, (rKP,) = _exchange_segments(comm, dk, bx, bx[:, 4] * (bx[:, 3] == 1), [res["kept_pts"]], dev)
-        assembled = assemble_cells(rmw, rG, rmk, rKP, ops.cfg_full())
+        # the pieces stay where they arrived (device) until the cells are
+        # walked or written (AssembledCells)
+        assembled = AssembledCells(rmw, rG, rmk, rKP, ops.cfg_full())
         ops.set_assembled(assembled)
         mark("assemble")
     local = _combine(parts)

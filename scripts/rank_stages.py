@@ -23,7 +23,51 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "point-cloud_amd"))
 
 BUILD_STAGES = ("build", "lead", "subtrees")
-EXCHANGE_STAGES = ("exchange", "exchange2")
+
+
+class TimedComm:
+    """The communicator with its calls timed (device synced first, so queued
+    device work is not counted as communication); shard_build splits each
+    stage into <stage>_comm (collectives) and the rest (local work)."""
+
+    def __init__(self, comm):
+        self.c = comm
+        self.elapsed_ms = 0.0
+
+    def __getattr__(self, name):
+        import torch
+        a = getattr(self.c, name)
+        if not callable(a):
+            return a
+
+        def timed(*args, **kw):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            r = a(*args, **kw)
+            self.elapsed_ms += (time.perf_counter() - t0) * 1e3
+            return r
+        return timed
+
+
+class RecOps:
+    """The ops with their local device calls recorded (stage, name, args), so a
+    rank can replay them alone on the GPU after the step."""
+    STAGE = {"bbox": "bbox", "slab_histogram": "hist", "histogram": "hist", "route_bitmaps": "route",
+             "route_slabs": "route", "route": "route", "keys_from_bitmaps": "exchange", "resolve_level1": "resolve"}
+
+    def __init__(self, ops):
+        self.o = ops
+        self.calls = []
+
+    def __getattr__(self, name):
+        a = getattr(self.o, name)
+        if name not in self.STAGE or not callable(a):
+            return a
+
+        def rec(*args, **kw):
+            self.calls.append((self.STAGE[name], a, args, kw))
+            return a(*args, **kw)
+        return rec
 
 
 def worker(rank, world, port, args, res_dir):
@@ -41,12 +85,13 @@ def worker(rank, world, port, args, res_dir):
         pts = torch.empty((b - a, 4), dtype=torch.int32, device=dev)
         pcconv.synth_device(pts.data_ptr(), a, b - a, args.seed, args.kind, -1000.0, 2000.0, 0)
         torch.cuda.synchronize()
-        ops = HipShardOps(0, batch_size=10_000)
-        comm = TorchComm(torch.device("cpu"))
+        ops = RecOps(HipShardOps(0, batch_size=10_000))
+        comm = TimedComm(TorchComm(torch.device("cpu")))
         files = [args.points]
         for _ in range(args.warmup):
             shard_build(comm, ops, pts, a, files)
         dist.barrier()
+        ops.calls = []
         r = shard_build(comm, ops, pts, a, files, sync=torch.cuda.synchronize)
         # the same step again, this rank's build stages alone on the GPU: every
         # rank runs the step, but a rank's local builds wait for their turn
@@ -54,19 +99,30 @@ def worker(rank, world, port, args, res_dir):
         for turn in range(world):
             dist.barrier()
             if turn == rank:
-                li = dict(ops.last_inputs)
-                for name, fn in (("build", ops.build), ("lead", ops.lead_build_raw), ("subtrees", ops.sub_build)):
-                    if name == "subtrees":
-                        name_in = "sub"
-                    else:
-                        name_in = name
+                li = dict(ops.o.last_inputs)
+                for stage, fn, fa, fk in ops.calls:   # the recorded local device calls
+                    best = None
+                    for _ in range(2):
+                        torch.cuda.synchronize()
+                        t0 = time.perf_counter()
+                        fn(*fa, **fk)
+                        torch.cuda.synchronize()
+                        t = (time.perf_counter() - t0) * 1e3
+                        best = t if best is None else min(best, t)
+                    alone["dev_" + stage] = alone.get("dev_" + stage, 0.0) + best
+                for name, fn, name_in in (("build", ops.build, "build"), ("lead", ops.lead_build_raw, "lead"),
+                                          ("subtrees", ops.sub_build, "sub")):
                     if name_in not in li:
                         continue
-                    torch.cuda.synchronize()
-                    t0 = time.perf_counter()
-                    fn(*li[name_in])
-                    torch.cuda.synchronize()
-                    alone[name] = (time.perf_counter() - t0) * 1e3
+                    best = None
+                    for _ in range(2):   # the better of two runs (the first may grow buffers)
+                        torch.cuda.synchronize()
+                        t0 = time.perf_counter()
+                        fn(*li[name_in])
+                        torch.cuda.synchronize()
+                        t = (time.perf_counter() - t0) * 1e3
+                        best = t if best is None else min(best, t)
+                    alone[name] = best
         dist.barrier()
         out = {"rank": rank, "ms": r.ms, "recv_points": r.recv_points, "owned_cells": r.owned_cells,
                "sub_points": r.sub_points, "assembled_cells": r.assembled_cells,
@@ -100,18 +156,28 @@ def main():
     ranks = [json.load(open(os.path.join(rd, f"rank{i}.json"))) for i in range(args.world)]
     for r in ranks:
         ms = r["ms"]
-        b = sum(ms.get(k, 0.0) for k in BUILD_STAGES)
-        ex = sum(ms.get(k, 0.0) for k in EXCHANGE_STAGES)
-        other = sum(v for k, v in ms.items() if k not in BUILD_STAGES and k not in EXCHANGE_STAGES)
-        r["build_ms_concurrent"] = b
-        r["exchange_ms_gloo"] = ex
-        r["non_build_non_exchange_ms"] = other
+        stages = [k for k in ms if not k.endswith("_comm")]
+        comm = {k: ms.get(k + "_comm", 0.0) for k in stages}
+        local = {k: max(0.0, ms[k] - comm[k]) for k in stages}
+        r["comm_ms_gloo"] = sum(comm.values())
+        r["local_ms_concurrent"] = local
         ba = sum(r["alone"].get(k, 0.0) for k in BUILD_STAGES)
         r["build_ms_alone"] = ba
-        r["non_build_over_build_alone"] = other / ba if ba else None
+        # local non-build work: the device calls outside the builds replayed alone,
+        # plus the host-only stages (ownership plan, assembly bookkeeping,
+        # summary) as measured; the exchange stages' local part is gloo's host
+        # staging (device <-> host copies), absent with RCCL, and left out
+        dev = {k[4:]: v for k, v in r["alone"].items() if k.startswith("dev_") and k != "dev_exchange"}
+        host = {k: local.get(k, 0.0) for k in ("plan", "assemble", "summary")}
+        nb = sum(dev.values()) + sum(host.values()) + r["alone"].get("dev_exchange", 0.0)
+        r["non_build_device_alone_ms"] = dev
+        r["non_build_host_ms"] = host
+        r["non_build_local_ms"] = nb
+        r["non_build_over_build_alone"] = nb / ba if ba else None
     print(json.dumps({"config": args.config, "world": args.world, "points": args.points,
-                      "note": "one process per rank on ONE MI355X; exchanges over gloo (host), not RCCL/xGMI; "
-                              "'alone' = the rank's whole-cell build re-run while the other ranks wait",
+                      "note": "one process per rank on ONE MI355X; collectives over gloo (host), not RCCL/xGMI, "
+                              "timed apart (<stage>_comm); 'alone' = the rank's builds and bucket resolution "
+                              "re-run (best of 2) while the other ranks wait",
                       "ranks": ranks}))
 
 

@@ -6,7 +6,7 @@ import numpy as np
 
 REC = {0: 20, 1: 28, 2: 26, 3: 34, 6: 30, 7: 36, 8: 38}
 COLOR_OFF = {0: None, 1: None, 2: 20, 3: 28, 6: None, 7: 30, 8: 30}
-GPS_OFF = {0: None, 1: 20, 2: None, 3: 20}
+GPS_OFF = {0: None, 1: 20, 2: None, 3: 20, 6: 22, 7: 22, 8: 22}
 
 
 def write_las_records(path, body, fmt, n, scale, offset, minor=2):
@@ -81,6 +81,56 @@ def survey_records(n, fmt, seed, extra=0):
         rgb[grey, 2] = rgb[grey, 0]
         co = COLOR_OFF[fmt]
         body[:, co:co + 6] = rgb.view(np.uint8).reshape(n, 6)
+    if extra:
+        body[:, REC[fmt]:] = (np.arange(n)[:, None] * np.arange(1, extra + 1)[None, :] % 251).astype(np.uint8)
+    return body
+
+
+def survey_records14(n, fmt, seed, extra=0, channels=4):
+    """LAS 1.4 point records (formats 6-8) shaped like a multi-channel survey:
+    scan lines whose points alternate between `channels` scanner channels in
+    runs, up to 15 returns, classification flags, scan angle in 0.006 degree
+    steps, increasing GPS time with repeats and one large jump, colour and NIR
+    (formats 7 / 8), plus `extra` bytes."""
+    rng = np.random.default_rng(seed)
+    rec = REC[fmt] + extra
+    body = np.zeros((n, rec), dtype=np.uint8)
+    t = np.arange(n)
+    ch = ((t // rng.integers(1, 40)) % channels) if channels > 1 else np.zeros(n, np.int64)
+    x = (np.cumsum(rng.integers(-40, 120, n)) + 1_000_000 + ch * 5000).astype("<i4")
+    y = (np.cumsum(rng.integers(-3, 4, n)) * 7 + (t // 500) * 900 - 2_000_000).astype("<i4")
+    z = (50_000 + np.cumsum(rng.integers(-30, 31, n)) + rng.integers(-200, 200, n) * (rng.random(n) < 0.05)).astype("<i4")
+    body[:, 0:12] = np.stack([x, y, z], 1).view(np.uint8).reshape(n, 12)
+    inten = (rng.integers(0, 700, n) * (rng.random(n) < 0.9)).astype("<u2")
+    body[:, 12:14] = inten.view(np.uint8).reshape(n, 2)
+    nret = rng.choice([1, 1, 2, 3, 4, 7, 15], n)
+    ret = np.minimum(rng.integers(1, 16, n), nret)
+    body[:, 14] = (ret | (nret << 4)).astype(np.uint8)
+    cflags = (rng.random(n) < 0.05) * rng.integers(0, 16, n)
+    sdir = (t // 300) % 2
+    edge = (t % 300 == 299).astype(np.int64)
+    body[:, 15] = (cflags | (ch << 4) | (sdir << 6) | (edge << 7)).astype(np.uint8)
+    body[:, 16] = rng.choice([1, 2, 2, 2, 5, 6, 40, 200], n).astype(np.uint8)
+    body[:, 17] = (rng.random(n) < 0.02).astype(np.uint8) * rng.integers(0, 255, n).astype(np.uint8)
+    ang = (((t // 40) % 600) - 300) * 10
+    ang[rng.random(n) < 0.01] = -30000
+    body[:, 18:20] = ang.astype("<i2").view(np.uint8).reshape(n, 2)
+    psid = np.full(n, 17, dtype="<u2")
+    psid[n // 2:] = 18
+    body[:, 20:22] = psid.view(np.uint8).reshape(n, 2)
+    g = 250_000.0 + np.repeat(np.cumsum(rng.random((n + 1) // 2) * 1e-4), 2)[:n]
+    g[n // 3:] += 1e9   # a jump beyond 32-bit differences
+    body[:, 22:30] = g.astype("<f8").view(np.uint8).reshape(n, 8)
+    if fmt in (7, 8):
+        base = np.cumsum(rng.integers(-3, 4, n)) % 65536
+        rgb = np.stack([base, (base + rng.integers(0, 300, n)) % 65536, (base * 3) % 65536], 1).astype("<u2")
+        grey = rng.random(n) < 0.3
+        rgb[grey, 1] = rgb[grey, 0]
+        rgb[grey, 2] = rgb[grey, 0]
+        body[:, 30:36] = rgb.view(np.uint8).reshape(n, 6)
+    if fmt == 8:
+        nir = ((np.cumsum(rng.integers(-2, 3, n)) + 30000) % 65536).astype("<u2")
+        body[:, 36:38] = nir.view(np.uint8).reshape(n, 2)
     if extra:
         body[:, REC[fmt]:] = (np.arange(n)[:, None] * np.arange(1, extra + 1)[None, :] % 251).astype(np.uint8)
     return body

@@ -240,12 +240,14 @@ class NumpyShardOps:
             cells, order, cn = np.zeros((0, 3), np.int32), np.zeros(0, np.int64), np.zeros(0, np.uint64)
         P = as_tensor(fp_[order])
         K = torch.from_numpy(fk[order].astype(np.uint32).view(np.int32).copy())
-        partial = [{"xyz": xyz, "grid": np.ascontiguousarray(gp).view(np.int32).reshape(-1, 4)}
-                   for h, xyz, gp in o.cells() if h == 0]
+        partial = [(xyz, np.ascontiguousarray(gp).view(np.int32).reshape(-1, 4)) for h, xyz, gp in o.cells() if h == 0]
+        pxyz = np.array([q[0] for q in partial], dtype=np.int64).reshape(-1, 3)
+        pn = np.array([len(q[1]) for q in partial], dtype=np.int64)
+        gpts = torch.from_numpy(np.concatenate([q[1] for q in partial]) if partial else np.zeros((0, 4), np.int32))
         st = self._stats(o)
         o.close()
         self.lead = None
-        return st, (cells.astype(np.int32), np.zeros(len(cells), np.uint32), cn, P, K), partial
+        return st, (cells.astype(np.int32), np.zeros(len(cells), np.uint32), cn, P, K), (pxyz, pn, gpts)
 
     def sub_build(self, file_points, pts, keys, cells_xyz, spill_batch) -> dict:
         """The owned level-1 sub-trees: their arrivals replayed batch by batch, an

@@ -451,3 +451,29 @@ def test_thread_ranks_sparse_wide_cloud_coarse_grid(tmp_path):
     assert not errs, errs
     assert sum(r.recv_points for r in res) == sum(fp)
     check_against_oracle(tmp_path, files, out, res[0].summary, cfg=cfg)
+
+
+def test_lpt_matches_heap_restatement():
+    """pcc_shard_lpt (the plan's C++ inner loop) == the heap formulation of
+    largest-first greedy (heaviest first, ties by index, to the least loaded
+    rank, ties by rank), owners and float64 loads alike."""
+    import heapq
+    import pcconv
+
+    def lpt_py(w, world):
+        own = np.zeros(len(w), dtype=np.uint32)
+        load = np.zeros(world)
+        heap = [(0.0, r) for r in range(world)]
+        for i in np.lexsort((np.arange(len(w)), -w)).tolist():
+            ld, r = heapq.heappop(heap)
+            own[i] = r
+            ld += float(w[i])
+            load[r] = ld
+            heapq.heappush(heap, (ld, r))
+        return own, load
+    rng = np.random.default_rng(1)
+    for _ in range(200):
+        n, world = int(rng.integers(0, 2000)), int(rng.integers(1, 17))
+        w = rng.integers(0, 50, n).astype(np.float64) * rng.choice([1.0, 0.5, 3.0])
+        a, b = lpt_py(w, world), pcconv.shard_lpt(w, world)
+        assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])

@@ -141,6 +141,87 @@ def test_route_bitmaps_and_key_rebuild_match_numpy(slabs, world):
             HipShardOps.keys_from_bitmaps(ops, cat, nw, key0, nk + 1)
 
 
+@pytest.mark.parametrize("limit,batch", [(50, 7), (64, 64), (1, 1000), (300, 13)])
+def test_device_bucket_resolution_matches_numpy(limit, batch):
+    """pcc_shard_resolve_buckets (HipShardOps.resolve_level1) == the numpy
+    statement (dist.resolve_level1): bucket states, spill batches, the kept lists
+    in key order, the spilled buckets' rows in segment order.  Buckets of 0..4
+    segments (empty ones included; each several sorted runs, as a cell's slabs)
+    with totals around the limit, over a file structure with an empty file and a
+    short last batch."""
+    from pcconv.dist import resolve_level1
+    rng = np.random.default_rng(limit * 7 + batch)
+    files = [3 * batch + 5, 0, 40 * batch + 1, 2 * batch]
+    n_keys = sum(files)
+    rows, segs = [], []
+    for b in range(60):
+        cell = (int(rng.integers(-5, 5)), int(rng.integers(-5, 5)), b)
+        tot = int(rng.choice([0, 1, limit - 1, limit, limit + 1, 2 * limit + 3, int(rng.integers(1, 3 * limit + 2))]))
+        tot = max(0, min(tot, n_keys))
+        keys = np.sort(rng.choice(n_keys, size=tot, replace=False))
+        if b % 5 == 0 and tot:   # all in one batch when it fits
+            k0 = int(rng.integers(0, max(1, n_keys - tot)))
+            keys = np.arange(k0, k0 + tot)
+        nseg = int(rng.integers(1, 5))
+        owner = rng.integers(0, nseg, size=tot)
+        for s in range(nseg):
+            k = keys[owner == s]
+            # a segment is a cell's arrivals from one rank: sorted runs (slabs), not sorted as a whole
+            runs = rng.integers(0, 3, size=len(k))
+            segs.append((cell, np.concatenate([k[runs == q] for q in (2, 0, 1)])))
+    order = rng.permutation(len(segs))   # segments of a bucket interleave with others
+    meta, kk = [], []
+    for i in order:
+        cell, k = segs[i]
+        meta.append([*cell, len(k)])
+        kk.append(k)
+    meta = np.array(meta, dtype=np.int64)
+    keys = np.concatenate(kk).astype(np.uint32)
+    pts = np.zeros((len(keys), 4), np.int32)
+    pts[:, 0] = np.arange(len(keys))
+    pts[:, 1] = keys.view(np.int32)
+    pts[:, 3] = rng.integers(-2**31, 2**31 - 1, size=len(keys), dtype=np.int64).astype(np.int32)
+    kt = torch.from_numpy(keys.view(np.int32).copy())
+    ref = resolve_level1(meta, torch.from_numpy(pts), kt, files, batch, limit)
+    ops = HipShardOps.__new__(HipShardOps)
+    ops.dev, ops.cfg, ops.batch_size = 0, {"cell_point_overflow_limit": limit}, batch
+    got = ops.resolve_level1(meta, torch.from_numpy(pts).to(DEV), kt.to(DEV), files)
+    assert np.array_equal(got["bucket_rows"], ref["bucket_rows"])
+    assert set(got["bucket_rows"][:, 3]) == {1, 2}, "both states must occur"
+    assert np.array_equal(got["roots_xyz"], ref["roots_xyz"])
+    assert np.array_equal(got["roots_sb"], ref["roots_sb"])
+    for k in ("kept_pts", "sub_pts", "sub_keys"):
+        assert torch.equal(got[k].cpu(), ref[k]), k
+
+
+def test_export_grid_equals_visited_cells():
+    """pcc_export_grid (a raw level-0 lead build's partial cells on the device)
+    == the cells pcc_visit_cells walks: same cells, order, grid points."""
+    from pcconv.dist import key_range
+    n = 300_000
+    pts = as_tensor(synth(71, 2, n)).to(DEV)
+    a, b = key_range(n, 1, 3)
+    keys = torch.arange(a, b, dtype=torch.int32, device=DEV)
+    ops = HipShardOps(0, batch_size=5000, config=SKEW_CFG)
+    try:
+        ops.begin_step()
+        ops.last_inputs = {}
+        _, _, (pxyz, pn, G) = ops.lead_build_raw([n], pts[a:b], keys)
+        seen = []
+
+        def grab(vp):
+            v = pcconv.CellView.from_address(vp)
+            seen.append(((v.x, v.y, v.z), v.grid_points().view(np.int32).reshape(-1, 4)))
+            return 0
+        ops.conv_lead.visit_cells(grab)
+        assert len(seen) == len(pxyz) > 0
+        assert [s[0] for s in seen] == [tuple(int(q) for q in r) for r in pxyz]
+        assert [len(s[1]) for s in seen] == [int(q) for q in pn]
+        assert np.array_equal(np.concatenate([s[1] for s in seen]), G.cpu().numpy())
+    finally:
+        ops.close()
+
+
 def test_synth_device_matches_oracle_stream():
     p = torch.empty((77_777, 4), dtype=torch.int32, device=DEV)
     pcconv.synth_device(p.data_ptr(), 123_456, 77_777, 9, 1)

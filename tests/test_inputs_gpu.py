@@ -19,7 +19,7 @@ import pytest
 
 from gpu_util import compare_dirs, gpu_digest  # noqa: E402
 from oracle_ctypes import POINT_DTYPE, Oracle, synth  # noqa: E402
-from las_util import survey_records, write_las, write_las_records  # noqa: E402
+from las_util import survey_records, survey_records14, write_las, write_las_records  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 
@@ -296,18 +296,23 @@ def test_ply_vertex_not_first_element():
         assert d == [] and mg == mo
 
 
-def test_laz_cli_equals_las(tmp_path):
+@pytest.mark.parametrize("formats", [(1, 3), (6, 8), (7,)])
+def test_laz_cli_equals_las(tmp_path, formats):
     """LAZ input (las.rs:14-46 through laz [dep]): a .laz made by laz_tool from a
     .las converts to exactly the .las's cloud, for point formats 1 and 3 (GPS
-    time, colour), two files in one run.  Parity unpinned: the .laz files come
+    time, colour; pointwise chunks) and 6, 7, 8 (LAS 1.4, layered chunks, colour
+    from 7 / 8), two files in one run.  Parity unpinned: the .laz files come
     from this repository's own encoder (no reference fixture, no LASzip here)."""
     tool = os.path.join(os.path.dirname(_exe()), "laz_tool")
     files_las, files_laz = [], []
-    for k, fmt in enumerate((1, 3)):
-        body = survey_records(120_000 if fmt == 3 else 45_000, fmt, seed=40 + fmt)
+    sizes = {1: 45_000, 3: 120_000, 6: 45_000, 8: 120_000, 7: 165_000}   # 165k points per run
+    for k, fmt in enumerate(formats):
+        n = sizes[fmt]
+        body = (survey_records(n, fmt, seed=40 + fmt) if fmt < 6 else survey_records14(n, fmt, seed=40 + fmt))
         a = str(tmp_path / f"f{k}.las")
         z = str(tmp_path / f"f{k}.laz")
-        write_las_records(a, body, fmt, len(body), (0.001, 0.001, 0.0005), (-900.0, 1900.0, -20.0))
+        write_las_records(a, body, fmt, len(body), (0.001, 0.001, 0.0005), (-900.0, 1900.0, -20.0),
+                          minor=4 if fmt >= 6 else 2)
         subprocess.run([tool, "compress", a, z, "50000"], check=True)
         files_las.append(a)
         files_laz.append(z)
