@@ -212,6 +212,17 @@ int pcc_shard_grid_from_bbox(const float gmin[3], const float gmax[3], float max
  * rank); owner[i] and the final load per rank.  The ownership plan's inner loop
  * (pcconv/dist.py _lpt / assign_owners), identical on every rank. */
 int pcc_shard_lpt(const double* w, uint64_t n, uint32_t world, uint32_t* owner, double* load);
+/* The plan's shared-cell search (host only; pcconv/dist.py plan_split): the
+ * ncand non-empty level-0 cells, heaviest first, with their whole-cell weights
+ * whole_w[i], their slabs' weights slab_w[slab_off[i] .. slab_off[i+1]) and
+ * their level-1 children's weights child_w[child_off[i] .. child_off[i+1]).
+ * For k = 0 .. kmax the first k cells are shared: phase 1 = LPT of the whole
+ * cells k.. followed by the first k cells' slabs, phase 2 = LPT of their
+ * children; the estimate is max phase-1 load + max phase-2 load.  A larger k
+ * replaces the best one only when it is more than 2 % lower. */
+int pcc_shard_plan_search(const double* whole_w, const uint64_t* slab_off, const double* slab_w,
+                          const uint64_t* child_off, const double* child_w, uint32_t ncand, uint32_t kmax,
+                          uint32_t world, uint32_t* best_k, double* best_t);
 
 /* Points first .. first+n-1 of the synthetic stream of pcc_add_synthetic,
  * written to dst[0 .. n) in device memory (each rank generates its key range). */

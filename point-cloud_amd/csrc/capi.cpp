@@ -479,19 +479,77 @@ int pcc_shard_grid_from_bbox(const float gmin[3], const float gmax[3], float max
     return 0;
 }
 
-int pcc_shard_lpt(const double* w, uint64_t n, uint32_t world, uint32_t* owner, double* load) {
-    if ((n && (!w || !owner)) || !load || world == 0) return set_err(-EINVAL, "null argument or no ranks");
-    GUARD_BEGIN
+// largest first (ties by index) to the least loaded rank (ties by rank)
+static void lpt(const double* w, uint64_t n, uint32_t world, uint32_t* owner, double* load) {
     std::vector<uint64_t> order(n);
     for (uint64_t i = 0; i < n; i++) order[i] = i;
     std::stable_sort(order.begin(), order.end(), [&](uint64_t a, uint64_t b) { return w[a] > w[b]; });
     for (uint32_t r = 0; r < world; r++) load[r] = 0.0;
     for (uint64_t i : order) {
-        uint32_t best = 0;   // least loaded rank, ties by rank
+        uint32_t best = 0;
         for (uint32_t r = 1; r < world; r++)
             if (load[r] < load[best]) best = r;
-        owner[i] = best;
+        if (owner) owner[i] = best;
         load[best] += w[i];
+    }
+}
+
+int pcc_shard_lpt(const double* w, uint64_t n, uint32_t world, uint32_t* owner, double* load) {
+    if ((n && (!w || !owner)) || !load || world == 0) return set_err(-EINVAL, "null argument or no ranks");
+    GUARD_BEGIN
+    lpt(w, n, world, owner, load);
+    return 0;
+    GUARD_END
+}
+
+int pcc_shard_plan_search(const double* whole_w, const uint64_t* slab_off, const double* slab_w,
+                          const uint64_t* child_off, const double* child_w, uint32_t ncand, uint32_t kmax,
+                          uint32_t world, uint32_t* best_k, double* best_t) {
+    if (!best_k || !best_t || world == 0 || kmax > ncand || (ncand && (!whole_w || !slab_off || !child_off)))
+        return set_err(-EINVAL, "null argument, no ranks or kmax > ncand");
+    GUARD_BEGIN
+    // Every k places a subset of one fixed item list in one fixed order: the
+    // phase-1 list of k is [whole cells k..] + [slabs of cells ..k), so by
+    // weight (descending), then whole cells before slabs, then position.  Sort
+    // once, then each k is one filtered greedy pass.
+    struct It { double w; uint32_t type, cell; uint64_t pos; };
+    std::vector<It> p1, p2;
+    for (uint32_t i = 0; i < ncand; i++) {
+        p1.push_back({whole_w[i], 0u, i, i});
+        for (uint64_t q = slab_off[i]; q < slab_off[i + 1]; q++) p1.push_back({slab_w[q], 1u, i, q});
+        for (uint64_t q = child_off[i]; q < child_off[i + 1]; q++) p2.push_back({child_w[q], 1u, i, q});
+    }
+    auto by = [](const It& a, const It& b) {
+        if (a.w != b.w) return a.w > b.w;
+        if (a.type != b.type) return a.type < b.type;
+        return a.pos < b.pos;
+    };
+    std::sort(p1.begin(), p1.end(), by);
+    std::sort(p2.begin(), p2.end(), by);
+    std::vector<double> l1(world), l2(world);
+    auto place = [&](std::vector<double>& load, double w) {
+        uint32_t r = 0;   // least loaded rank, ties by rank
+        for (uint32_t q = 1; q < world; q++)
+            if (load[q] < load[r]) r = q;
+        load[r] += w;
+    };
+    bool have = false;
+    *best_k = 0;
+    *best_t = 0.0;
+    for (uint32_t k = 0; k <= kmax; k++) {
+        std::fill(l1.begin(), l1.end(), 0.0);
+        std::fill(l2.begin(), l2.end(), 0.0);
+        for (const It& it : p1)
+            if (it.type == 0 ? it.cell >= k : it.cell < k) place(l1, it.w);
+        bool any2 = false;
+        for (const It& it : p2)
+            if (it.cell < k) { place(l2, it.w); any2 = true; }
+        const double t = *std::max_element(l1.begin(), l1.end()) + (any2 ? *std::max_element(l2.begin(), l2.end()) : 0.0);
+        if (!have || t < *best_t * 0.98) {
+            have = true;
+            *best_t = t;
+            *best_k = k;
+        }
     }
     return 0;
     GUARD_END

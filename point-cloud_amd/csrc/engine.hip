@@ -4640,12 +4640,10 @@ struct ShardScratch {
     uint64_t* tab = nullptr;
     uint64_t* rt = nullptr;   // bucket resolution tables and sort buffers (shard_resolve_buckets)
     uint64_t rt_cap = 0;
-    uint32_t* rb = nullptr;
-    uint64_t rb_cap = 0;
     SortTemp sort;
     ~ShardScratch() {
         for (auto* b : buf) (void)hipFree(b);
-        (void)hipFree(part); (void)hipFree(flag); (void)hipFree(cnt); (void)hipFree(tab); (void)hipFree(rt); (void)hipFree(rb);
+        (void)hipFree(part); (void)hipFree(flag); (void)hipFree(cnt); (void)hipFree(tab); (void)hipFree(rt);
         (void)hipFree(sort.counts); (void)hipFree(sort.scan.bsums);
         if (st) (void)hipStreamDestroy(st);
     }
@@ -4844,91 +4842,195 @@ __global__ void k_bm_keys(const unsigned long long* __restrict__ bm, uint32_t nw
 // ---- shared cells' overflow buckets, resolved over every rank's emissions
 // (cell.rs:108-153; the numpy statement is pcconv/dist.py::resolve_bucket).
 // Emissions arrive in segments (a cell's arrivals from one rank: sorted runs per
-// slab, not sorted as a whole); a bucket's keys are distinct.  The rows are
-// sorted by (bucket, key) on the device (two stable radix passes over a row
-// index), so each bucket's keys are one ascending run of `sk`.
+// slab, not sorted as a whole); a bucket's keys are distinct.  Nothing is
+// sorted but the kept lists: a bucket of tot > L points spills, at the batch of
+// its want-th smallest key (want = L, or L + 1 when its first batch holds
+// exactly L), found by a 4-pass radix select over the bucket's keys; a bucket of
+// tot <= L keeps its list (unless tot == L over two batches, then it spills at
+// its largest key), ranked by key in LDS.  The rows are walked in chunks of at
+// most kRsChunk rows of one segment (one bucket per workgroup).
+constexpr uint32_t kRsChunk = 4096;   // (kKeptMax: the kept-list capacity, as k_bucket's)
 struct BucketTabs {
     const uint32_t* files;      // 4 u32 per file: start lo/hi, first batch, batch size
     uint32_t nfiles;
     const uint64_t* start;      // per segment: first row, rows, bucket
     const uint64_t* len;
     const uint64_t* segb;
-    const uint64_t* bstart;     // per bucket: first position in the sorted order (nbuckets + 1)
-    const uint64_t* base;       // per segment: sub-tree output row base (spilled buckets)
-    const uint64_t* kbase;      // per bucket: kept output row base (kept buckets)
+    const uint64_t* inoff;      // per segment: rows of the bucket's earlier segments
+    const uint64_t* tot;        // per bucket: rows
+    const uint64_t* boff;       // per bucket: its segments bsegs[boff[b] .. boff[b+1]), in order
+    const uint64_t* bsegs;
+    const uint64_t* chunk;      // per chunk: segment | row offset in it << 32 (rows: min(kRsChunk, rest))
+    uint32_t nchunks;
+    uint32_t* hist;             // per bucket 256 digit counts (radix select)
+    uint32_t* sel;              // per bucket: prefix, rank left, kmin, kmax, fk, first, next key, pad
     uint64_t* out;              // per bucket: state | spill batch << 32
-    uint64_t nseg;
+    uint64_t* base;             // per bucket: kept base, sub base (exclusive scans)
     uint32_t nbuckets, limit;
 };
-__device__ __forceinline__ uint64_t row_segment(const BucketTabs& T, uint64_t i) {
-    uint64_t lo = 0, hi = T.nseg - 1;   // last segment with start <= i
-    while (lo < hi) {
-        const uint64_t mid = (lo + hi + 1) >> 1;
-        if (T.start[mid] <= i) lo = mid; else hi = mid - 1;
+enum { SEL_PREFIX, SEL_RANK, SEL_KMIN, SEL_KMAX, SEL_FK, SEL_FIRST, SEL_NEXT, SEL_PAD, SEL_W };
+static_assert(SEL_W % 2 == 0, "whole u64 words per bucket");
+
+// one pass over a chunk: pass 0 = min / max key of every bucket and the top
+// key byte's histogram; passes 1-3 the next bytes among the keys that match the
+// selected prefix (pass 1 also counts the keys below the first batch's end);
+// pass 4 the least key above the selected one.  Buckets of tot <= L only take
+// part in pass 0.
+__global__ __launch_bounds__(256) void k_rsel(BucketTabs T, const uint32_t* __restrict__ keys, int pass) {
+    __shared__ uint32_t h[256];
+    __shared__ uint32_t red[3];
+    const uint64_t cw = T.chunk[blockIdx.x];
+    const uint32_t sg = (uint32_t)cw, o = (uint32_t)(cw >> 32);
+    const uint32_t b = (uint32_t)T.segb[sg];
+    const bool sel = T.tot[b] > T.limit;
+    if (pass > 0 && !sel) return;   // block-uniform
+    const uint64_t r0 = T.start[sg] + o;
+    const uint32_t n = (uint32_t)min<uint64_t>(kRsChunk, T.len[sg] - o);
+    uint32_t* S = T.sel + (uint64_t)b * SEL_W;
+    const int shift = 24 - 8 * (pass < 4 ? pass : 3);
+    const uint32_t hi = pass == 0 ? 0u : (pass >= 4 ? 0xFFFFFFFFu : 0xFFFFFFFFu << (32 - 8 * pass));
+    const uint32_t pref = S[SEL_PREFIX], fk = S[SEL_FK];
+    h[threadIdx.x] = 0;
+    if (threadIdx.x < 3) red[threadIdx.x] = threadIdx.x == 0 ? 0xFFFFFFFFu : 0u;
+    __syncthreads();
+    uint32_t mn = 0xFFFFFFFFu, mx = 0, below = 0;
+    for (uint32_t i = threadIdx.x; i < n; i += 256) {
+        const uint32_t k = keys[r0 + i];
+        if (pass == 0) {
+            mn = min(mn, k);
+            mx = max(mx, k);
+        }
+        if (pass == 4) {
+            if (k > pref) mn = min(mn, k);
+        } else if (sel && ((k ^ pref) & hi) == 0) {
+            atomicAdd(&h[(k >> shift) & 255u], 1u);
+        }
+        if (pass == 1) below += k < fk ? 1u : 0u;
     }
-    return lo;
-}
-// sort input: (key, row) and the row's bucket
-__global__ void k_bkt_rows(BucketTabs T, const uint32_t* __restrict__ keys, uint32_t nrows, uint32_t* __restrict__ k,
-                           uint32_t* __restrict__ idx, uint32_t* __restrict__ bkt) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nrows) return;
-    k[i] = keys[i];
-    idx[i] = i;
-    bkt[i] = (uint32_t)T.segb[row_segment(T, i)];
-}
-__global__ void k_gather_u32(const uint32_t* __restrict__ src, const uint32_t* __restrict__ idx, uint32_t n,
-                             uint32_t* __restrict__ dst) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) dst[i] = src[idx[i]];
-}
-// first position in [lo, hi) of sk with sk >= v
-__device__ __forceinline__ uint64_t lower_bound_u32(const uint32_t* sk, uint64_t lo, uint64_t hi, uint32_t v) {
-    while (lo < hi) {
-        const uint64_t mid = (lo + hi) >> 1;
-        if (sk[mid] < v) lo = mid + 1; else hi = mid;
+    // wave reductions, then one LDS atomic per wave
+    for (int d = 32; d >= 1; d >>= 1) {
+        mn = min(mn, (uint32_t)__shfl_xor((int)mn, d, 64));
+        mx = max(mx, (uint32_t)__shfl_xor((int)mx, d, 64));
+        below += (uint32_t)__shfl_xor((int)below, d, 64);
     }
-    return lo;
+    if ((threadIdx.x & 63) == 0) {
+        atomicMin(&red[0], mn);
+        atomicMax(&red[1], mx);
+        atomicAdd(&red[2], below);
+    }
+    __syncthreads();
+    if (pass < 4 && sel && h[threadIdx.x]) atomicAdd(&T.hist[(uint64_t)b * 256 + threadIdx.x], h[threadIdx.x]);
+    if (threadIdx.x == 0) {
+        if (pass == 0) {
+            atomicMin(&S[SEL_KMIN], red[0]);
+            atomicMax(&S[SEL_KMAX], red[1]);
+        }
+        if (pass == 1) atomicAdd(&S[SEL_FIRST], red[2]);
+        if (pass == 4) atomicMin(&S[SEL_NEXT], red[0]);
+    }
 }
-// one thread per bucket: state 1 (Some) or 2 (None at the spill batch).  Batch
-// by batch the list stays while it holds at most L points after the first
-// batch / below L after a later one: spilled iff tot > L, or tot == L over more
-// than one batch; then the spill batch is that of the thr-th smallest key with
-// thr = L + (first batch's count == L).
-__global__ void k_bkt_resolve(BucketTabs T, const uint32_t* __restrict__ sk) {
+// per bucket after pass p < 4: the digit holding the rank-th smallest key,
+// appended to the prefix; after pass 0 also the end of the first key's batch
+__global__ void k_rsel_pick(BucketTabs T, int pass) {
     const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= T.nbuckets) return;
-    const uint64_t a = T.bstart[b], e = T.bstart[b + 1], tot = e - a;
-    uint64_t st = 1;
-    if (tot) {
-        const uint32_t e0 = event_batch(T.files, T.nfiles, sk[a]), e1 = event_batch(T.files, T.nfiles, sk[e - 1]);
-        const bool spilled = tot > T.limit || (tot == T.limit && e0 != e1);
-        if (spilled) {
-            const uint64_t first = lower_bound_u32(sk, a, e, first_key_after(T.files, T.nfiles, e0)) - a;
-            const uint64_t thr = (uint64_t)T.limit + (first == T.limit ? 1u : 0u);
-            const uint64_t want = thr > 1 ? thr : 1;   // the want-th smallest key (1-based), want <= tot
-            st = 2ull | ((uint64_t)event_batch(T.files, T.nfiles, sk[a + want - 1]) << 32);
+    uint32_t* S = T.sel + (uint64_t)b * SEL_W;
+    if (pass == 0) S[SEL_FK] = first_key_after(T.files, T.nfiles, event_batch(T.files, T.nfiles, S[SEL_KMIN]));
+    if (T.tot[b] <= T.limit) return;
+    uint32_t* hb = T.hist + (uint64_t)b * 256;
+    uint32_t rank = S[SEL_RANK], d = 0;
+    for (; d < 255; d++) {
+        const uint32_t c = hb[d];
+        if (rank < c) break;
+        rank -= c;
+    }
+    for (uint32_t q = 0; q < 256; q++) hb[q] = 0;
+    S[SEL_RANK] = rank;
+    S[SEL_PREFIX] |= d << (24 - 8 * pass);
+}
+// states, spill batches, and the exclusive scans of kept / spilled rows (one block)
+__global__ __launch_bounds__(1024) void k_bkt_state(BucketTabs T) {
+    __shared__ uint64_t part[1024][2];
+    const uint32_t L = T.limit, per = (T.nbuckets + 1023) / 1024;
+    const uint32_t b0 = threadIdx.x * per, b1 = min(b0 + per, T.nbuckets);
+    uint64_t ak = 0, as = 0;
+    for (uint32_t b = b0; b < b1; b++) {
+        const uint32_t* S = T.sel + (uint64_t)b * SEL_W;
+        const uint64_t tot = T.tot[b];
+        uint64_t st = 1;
+        if (tot > L) {   // want = L, or L + 1 when the first batch holds exactly L
+            const uint32_t k = S[SEL_FIRST] == L ? S[SEL_NEXT] : S[SEL_PREFIX];
+            st = 2ull | ((uint64_t)event_batch(T.files, T.nfiles, k) << 32);
+        } else if (tot == L && tot > 0) {
+            const uint32_t e1 = event_batch(T.files, T.nfiles, S[SEL_KMAX]);
+            if (event_batch(T.files, T.nfiles, S[SEL_KMIN]) != e1) st = 2ull | ((uint64_t)e1 << 32);
+        }
+        T.out[b] = st;
+        if ((uint32_t)st == 1) ak += tot; else as += tot;
+    }
+    part[threadIdx.x][0] = ak;
+    part[threadIdx.x][1] = as;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t k = 0, q = 0;
+        for (int t = 0; t < 1024; t++) {
+            const uint64_t a = part[t][0], c = part[t][1];
+            part[t][0] = k;
+            part[t][1] = q;
+            k += a;
+            q += c;
         }
     }
-    T.out[b] = st;
+    __syncthreads();
+    ak = part[threadIdx.x][0];
+    as = part[threadIdx.x][1];
+    for (uint32_t b = b0; b < b1; b++) {
+        T.base[2 * b] = ak;
+        T.base[2 * b + 1] = as;
+        if ((uint32_t)T.out[b] == 1) ak += T.tot[b]; else as += T.tot[b];
+    }
 }
-// kept buckets: sorted position j -> kept row kbase + (j - bstart)
-__global__ void k_bkt_kept(BucketTabs T, const uint32_t* __restrict__ sb, const uint32_t* __restrict__ idx,
-                           uint32_t nrows, const Point* __restrict__ pts, Point* __restrict__ kept) {
-    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= nrows) return;
-    const uint32_t b = sb[j];
-    if ((uint32_t)T.out[b] != 1) return;
-    reinterpret_cast<float4*>(kept)[T.kbase[b] + (j - T.bstart[b])] = reinterpret_cast<const float4*>(pts)[idx[j]];
+// spilled buckets: every row (pts + keys) to sub base + earlier segments of its bucket + its index
+__global__ void k_bkt_sub(BucketTabs T, const Point* __restrict__ pts, const uint32_t* __restrict__ keys,
+                          Point* __restrict__ sub, uint32_t* __restrict__ sub_keys) {
+    const uint64_t cw = T.chunk[blockIdx.x];
+    const uint32_t sg = (uint32_t)cw, o = (uint32_t)(cw >> 32);
+    const uint32_t b = (uint32_t)T.segb[sg];
+    if ((uint32_t)T.out[b] != 2) return;
+    const uint64_t r0 = T.start[sg] + o, d0 = T.base[2 * b + 1] + T.inoff[sg] + o;
+    const uint32_t n = (uint32_t)min<uint64_t>(kRsChunk, T.len[sg] - o);
+    for (uint32_t i = threadIdx.x; i < n; i += 256) {
+        reinterpret_cast<float4*>(sub)[d0 + i] = reinterpret_cast<const float4*>(pts)[r0 + i];
+        sub_keys[d0 + i] = keys[r0 + i];
+    }
 }
-// spilled buckets: their rows in segment order (pts + keys) from base[segment]
-__global__ void k_bkt_sub(BucketTabs T, const uint32_t* __restrict__ bkt, uint32_t nrows, const Point* __restrict__ pts,
-                          const uint32_t* __restrict__ keys, Point* __restrict__ sub, uint32_t* __restrict__ sub_keys) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nrows || (uint32_t)T.out[bkt[i]] != 2) return;
-    const uint64_t s = row_segment(T, i), o = T.base[s] + (i - T.start[s]);
-    reinterpret_cast<float4*>(sub)[o] = reinterpret_cast<const float4*>(pts)[i];
-    sub_keys[o] = keys[i];
+// kept buckets (one workgroup each): the bucket's keys in LDS, every row's rank
+// = the keys below its own (distinct keys), row to kept base + rank
+__global__ __launch_bounds__(1024) void k_bkt_kept(BucketTabs T, const Point* __restrict__ pts,
+                                                   const uint32_t* __restrict__ keys, Point* __restrict__ kept) {
+    __shared__ uint32_t sk[kKeptMax];
+    __shared__ uint32_t sr[kKeptMax];
+    const uint32_t b = blockIdx.x;
+    if ((uint32_t)T.out[b] != 1 || T.tot[b] == 0) return;
+    const uint32_t tot = (uint32_t)T.tot[b];
+    uint32_t o = 0;
+    for (uint64_t j = T.boff[b]; j < T.boff[b + 1]; j++) {
+        const uint64_t sg = T.bsegs[j], r0 = T.start[sg];
+        const uint32_t n = (uint32_t)T.len[sg];
+        for (uint32_t i = threadIdx.x; i < n; i += 1024) {
+            sk[o + i] = keys[r0 + i];
+            sr[o + i] = (uint32_t)(r0 + i);
+        }
+        o += n;
+    }
+    __syncthreads();
+    const uint64_t kb = T.base[2 * b];
+    for (uint32_t i = threadIdx.x; i < tot; i += 1024) {
+        const uint32_t k = sk[i];
+        uint32_t r = 0;
+        for (uint32_t q = 0; q < tot; q++) r += sk[q] < k ? 1u : 0u;
+        reinterpret_cast<float4*>(kept)[kb + r] = reinterpret_cast<const float4*>(pts)[sr[i]];
+    }
 }
 
 }  // namespace
@@ -4974,18 +5076,26 @@ int shard_resolve_buckets(const uint64_t* seg_n, const uint32_t* seg_bucket, uin
     *nkept = *nsub = 0;
     if (!nbuckets) return 0;
     if (!nfiles || nseg == 0) return -EINVAL;
+    if (limit == 0 || limit > (uint32_t)kKeptMax) return -EINVAL;
     batch = std::max<uint32_t>(batch, 1);
-    std::vector<uint64_t> tot(nbuckets, 0), bstart(nbuckets + 1ull, 0), start(nseg), segb(nseg);
+    std::vector<uint64_t> tot(nbuckets, 0), boff(nbuckets + 1ull, 0), start(nseg), segb(nseg), inoff(nseg), chunks;
     uint64_t nrows = 0;
     for (uint64_t s = 0; s < nseg; s++) {
-        if (seg_bucket[s] >= nbuckets) return -EINVAL;
+        const uint32_t b = seg_bucket[s];
+        if (b >= nbuckets) return -EINVAL;
         start[s] = nrows;
+        inoff[s] = tot[b];
         nrows += seg_n[s];
-        tot[seg_bucket[s]] += seg_n[s];
-        segb[s] = seg_bucket[s];
+        tot[b] += seg_n[s];
+        segb[s] = b;
+        boff[b + 1]++;
+        if (seg_n[s] >= (1ull << 32)) return -EOVERFLOW;
+        for (uint64_t o = 0; o < seg_n[s]; o += kRsChunk) chunks.push_back(s | (o << 32));
     }
-    if (nrows >= (1ull << 32)) return -EOVERFLOW;
-    for (uint32_t b = 0; b < nbuckets; b++) bstart[b + 1] = bstart[b] + tot[b];
+    if (nrows >= (1ull << 32) || nseg >= (1ull << 32)) return -EOVERFLOW;
+    for (uint32_t b = 0; b < nbuckets; b++) boff[b + 1] += boff[b];
+    std::vector<uint64_t> bsegs(nseg), fill(boff.begin(), boff.end() - 1);
+    for (uint64_t s = 0; s < nseg; s++) bsegs[fill[seg_bucket[s]]++] = s;
     // file table as the engine's (lib.rs:31-52: batches restart at every file,
     // an empty file is one empty batch)
     std::vector<uint32_t> ft;
@@ -4996,92 +5106,77 @@ int shard_resolve_buckets(const uint64_t* seg_n, const uint32_t* seg_bucket, uin
         g += file_points[f];
         eb += (uint32_t)std::max<uint64_t>(1, (file_points[f] + batch - 1) / batch);
     }
+    const uint64_t nch = chunks.size();
     const uint64_t wf = (ft.size() + 1) / 2;
-    const uint64_t w_start = wf, w_len = w_start + nseg, w_segb = w_len + nseg, w_bstart = w_segb + nseg,
-                   w_base = w_bstart + nbuckets + 1, w_kbase = w_base + nseg, w_out = w_kbase + nbuckets,
-                   words = w_out + nbuckets;
+    const uint64_t w_start = wf, w_len = w_start + nseg, w_segb = w_len + nseg, w_inoff = w_segb + nseg,
+                   w_tot = w_inoff + nseg, w_boff = w_tot + nbuckets, w_bsegs = w_boff + nbuckets + 1,
+                   w_chunk = w_bsegs + nseg, w_sel = w_chunk + nch,                     // SEL_W u32 per bucket
+                   w_hist = w_sel + (uint64_t)nbuckets * SEL_W / 2,                      // 256 u32 per bucket
+                   w_out = w_hist + (uint64_t)nbuckets * 128, w_base = w_out + nbuckets,
+                   words = w_base + 2ull * nbuckets;
     if (S.rt_cap < words) {
         (void)hipFree(S.rt);
         S.rt = nullptr;
         HIP_CHECK(hipMalloc(&S.rt, words * 8));
         S.rt_cap = words;
     }
-    if (S.rb_cap < nrows) {   // sort buffers: 2 keys, 2 values, row bucket, sorted keys
-        (void)hipFree(S.rb);
-        S.rb = nullptr;
-        HIP_CHECK(hipMalloc(&S.rb, std::max<uint64_t>(nrows, 1) * 6 * 4));
-        S.rb_cap = std::max<uint64_t>(nrows, 1);
-    }
-    std::vector<uint64_t> blob(w_base, 0);
+    std::vector<uint64_t> blob(w_out, 0);
     memcpy(blob.data(), ft.data(), ft.size() * 4);
     memcpy(blob.data() + w_start, start.data(), nseg * 8);
     memcpy(blob.data() + w_len, seg_n, nseg * 8);
     memcpy(blob.data() + w_segb, segb.data(), nseg * 8);
-    memcpy(blob.data() + w_bstart, bstart.data(), bstart.size() * 8);
+    memcpy(blob.data() + w_inoff, inoff.data(), nseg * 8);
+    memcpy(blob.data() + w_tot, tot.data(), nbuckets * 8ull);
+    memcpy(blob.data() + w_boff, boff.data(), boff.size() * 8);
+    memcpy(blob.data() + w_bsegs, bsegs.data(), nseg * 8);
+    if (nch) memcpy(blob.data() + w_chunk, chunks.data(), nch * 8);
+    uint32_t* sel0 = reinterpret_cast<uint32_t*>(blob.data() + w_sel);
+    for (uint32_t b = 0; b < nbuckets; b++) {   // select the L-th smallest key (rank L - 1)
+        uint32_t* q = sel0 + (uint64_t)b * SEL_W;
+        q[SEL_RANK] = limit - 1;
+        q[SEL_KMIN] = 0xFFFFFFFFu;
+        q[SEL_NEXT] = 0xFFFFFFFFu;
+    }
     BucketTabs T;
     T.files = reinterpret_cast<const uint32_t*>(S.rt);
     T.nfiles = (uint32_t)nfiles;
     T.start = S.rt + w_start;
     T.len = S.rt + w_len;
     T.segb = S.rt + w_segb;
-    T.bstart = S.rt + w_bstart;
-    T.base = S.rt + w_base;
-    T.kbase = S.rt + w_kbase;
+    T.inoff = S.rt + w_inoff;
+    T.tot = S.rt + w_tot;
+    T.boff = S.rt + w_boff;
+    T.bsegs = S.rt + w_bsegs;
+    T.chunk = S.rt + w_chunk;
+    T.nchunks = (uint32_t)nch;
+    T.sel = reinterpret_cast<uint32_t*>(S.rt + w_sel);
+    T.hist = reinterpret_cast<uint32_t*>(S.rt + w_hist);
     T.out = S.rt + w_out;
-    T.nseg = nseg;
+    T.base = S.rt + w_base;
     T.nbuckets = nbuckets;
     T.limit = limit;
-    HIP_CHECK(hipMemcpyAsync(S.rt, blob.data(), w_base * 8, hipMemcpyHostToDevice, S.st));
-    const uint32_t n = (uint32_t)nrows, nb = (n + 255) / 256;
-    uint32_t* K[2] = {S.rb, S.rb + S.rb_cap};
-    uint32_t* V[2] = {S.rb + 2 * S.rb_cap, S.rb + 3 * S.rb_cap};
-    uint32_t* bkt = S.rb + 4 * S.rb_cap;
-    uint32_t* sk = S.rb + 5 * S.rb_cap;
-    const uint32_t* sbk = nullptr;   // sorted bucket ids
-    const uint32_t* sidx = nullptr;  // rows in (bucket, key) order
-    if (n) {
-        k_bkt_rows<<<nb, 256, 0, S.st>>>(T, dkeys, n, K[0], V[0], bkt);
-        const int r = radix_sort_pairs(K[0], V[0], K[1], V[1], n, 32, S.sort, S.st);
-        k_gather_u32<<<nb, 256, 0, S.st>>>(bkt, V[r], n, K[1 - r]);
-        int bb = 1;
-        while ((1ull << bb) < nbuckets) bb++;
-        const int r2 = radix_sort_pairs(K[1 - r], V[r], K[r], V[1 - r], n, bb, S.sort, S.st);
-        sbk = r2 == 0 ? K[1 - r] : K[r];
-        sidx = r2 == 0 ? V[r] : V[1 - r];
-        k_gather_u32<<<nb, 256, 0, S.st>>>(dkeys, sidx, n, sk);
+    HIP_CHECK(hipMemcpyAsync(S.rt, blob.data(), w_out * 8, hipMemcpyHostToDevice, S.st));   // (hist: zeros)
+    const uint32_t pb = (nbuckets + 63) / 64;
+    for (int pass = 0; pass <= 4; pass++) {
+        if (nch) k_rsel<<<(uint32_t)nch, 256, 0, S.st>>>(T, dkeys, pass);
+        if (pass < 4) k_rsel_pick<<<pb, 64, 0, S.st>>>(T, pass);
     }
-    k_bkt_resolve<<<(nbuckets + 63) / 64, 64, 0, S.st>>>(T, sk);
+    k_bkt_state<<<1, 1024, 0, S.st>>>(T);
+    if (nch) k_bkt_sub<<<(uint32_t)nch, 256, 0, S.st>>>(T, dpts, dkeys, dsub, dsub_keys);
+    k_bkt_kept<<<nbuckets, 1024, 0, S.st>>>(T, dpts, dkeys, dkept);
     HIP_CHECK(hipGetLastError());
     std::vector<uint64_t> out(nbuckets);
     HIP_CHECK(hipMemcpyAsync(out.data(), T.out, nbuckets * 8ull, hipMemcpyDeviceToHost, S.st));
     HIP_CHECK(hipStreamSynchronize(S.st));
-    // output bases: kept lists bucket after bucket, the spilled buckets' rows
-    // bucket after bucket (each bucket's segments in order)
-    std::vector<uint64_t> tail(nseg + nbuckets, 0), bsub(nbuckets);
     uint64_t ok = 0, os = 0;
     for (uint32_t b = 0; b < nbuckets; b++) {
         state[b] = (uint32_t)out[b];
         spill_batch[b] = (uint32_t)(out[b] >> 32);
-        const bool some = state[b] == 1;
-        kept_n[b] = some ? tot[b] : 0;
-        tail[nseg + b] = ok;
-        bsub[b] = os;
-        (some ? ok : os) += tot[b];
-    }
-    for (uint64_t s = 0; s < nseg; s++) {   // segments in order: within a bucket, in order too
-        const uint32_t b = seg_bucket[s];
-        tail[s] = bsub[b];
-        if (state[b] == 2) bsub[b] += seg_n[s];
+        kept_n[b] = state[b] == 1 ? tot[b] : 0;
+        (state[b] == 1 ? ok : os) += tot[b];
     }
     *nkept = ok;
     *nsub = os;
-    if (n) {
-        HIP_CHECK(hipMemcpyAsync(S.rt + w_base, tail.data(), tail.size() * 8, hipMemcpyHostToDevice, S.st));
-        k_bkt_kept<<<nb, 256, 0, S.st>>>(T, sbk, sidx, n, dpts, dkept);
-        k_bkt_sub<<<nb, 256, 0, S.st>>>(T, bkt, n, dpts, dkeys, dsub, dsub_keys);
-        HIP_CHECK(hipGetLastError());
-    }
-    HIP_CHECK(hipStreamSynchronize(S.st));
     return 0;
 }
 

@@ -38,7 +38,8 @@ EXPORTS = ["pcc_abi_version", "pcc_last_error", "pcc_options_default", "pcc_open
            "pcc_write_cell_view", "pcc_begin_file", "pcc_append_points", "pcc_end_file", "pcc_cancel_file",
            "pcc_set_summary", "pcc_write_cells", "pcc_write_metadata", "pcc_clear_input", "pcc_adopt_prior",
            "pcc_open_subtrees", "pcc_visit_cells", "pcc_shard_route_bitmaps", "pcc_shard_keys_from_bitmaps",
-           "pcc_release_device_cache", "pcc_grid_cells", "pcc_export_grid", "pcc_shard_resolve_buckets", "pcc_shard_lpt"]
+           "pcc_release_device_cache", "pcc_grid_cells", "pcc_export_grid", "pcc_shard_resolve_buckets", "pcc_shard_lpt",
+           "pcc_shard_plan_search"]
 
 
 class Options(C.Structure):
@@ -167,6 +168,8 @@ def lib():
         L.pcc_pending_cells.argtypes = [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         L.pcc_export_pending.argtypes = [vp, vp, vp, vp, vp, vp]
         L.pcc_shard_lpt.argtypes = [vp, C.c_uint64, C.c_uint32, vp, vp]
+        L.pcc_shard_plan_search.argtypes = [vp, vp, vp, vp, vp, C.c_uint32, C.c_uint32, C.c_uint32,
+                                            C.POINTER(C.c_uint32), C.POINTER(C.c_double)]
         L.pcc_grid_cells.argtypes = [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         L.pcc_export_grid.argtypes = [vp, vp, vp, vp]
         L.pcc_shard_resolve_buckets.argtypes = [vp, vp, C.c_uint64, C.c_uint32, vp, vp, vp, C.c_uint64, C.c_uint32,
@@ -467,6 +470,18 @@ def shard_lpt(w, world: int):
     load = np.zeros(world, np.float64)
     _check(lib().pcc_shard_lpt(w.ctypes.data, len(w), world, own.ctypes.data, load.ctypes.data))
     return own, load
+
+
+def shard_plan_search(whole_w, slab_off, slab_w, child_off, child_w, kmax: int, world: int):
+    """pcc_shard_plan_search: (best k, its estimate)."""
+    f = lambda a, t: np.ascontiguousarray(a, dtype=t).reshape(-1)
+    ww, so, sw, co, cw = (f(whole_w, np.float64), f(slab_off, np.uint64), f(slab_w, np.float64),
+                          f(child_off, np.uint64), f(child_w, np.float64))
+    bk, bt = C.c_uint32(0), C.c_double(0.0)
+    _check(lib().pcc_shard_plan_search(ww.ctypes.data, so.ctypes.data, sw.ctypes.data if len(sw) else None,
+                                       co.ctypes.data, cw.ctypes.data if len(cw) else None, len(ww), kmax, world,
+                                       C.byref(bk), C.byref(bt)))
+    return bk.value, bt.value
 
 
 def write_cell_view(out_dir: str, view: "CellView"):

@@ -264,22 +264,29 @@ def plan_split(hist0: np.ndarray, hist1: np.ndarray | None, children: np.ndarray
         return no
     sh = np.asarray(slab_hist, dtype=np.int64).reshape(len(hist0), NL)
     order = nz[np.lexsort((nz, -hist0[nz]))]
-    best, best_t = None, None
-    for k in range(0, min(len(order), 2 * world) + 1):
-        sp = order[:k]
-        whole = order[k:]
-        # phase 1: the whole cells and the shared cells' level-0 slabs
-        sl = np.concatenate([c * NL + np.flatnonzero(sh[c]) for c in sp]) if k else np.zeros(0, np.int64)
-        o1, l1 = _lpt(np.concatenate([whole_w[whole], sh.reshape(-1)[sl] * L0_COST]), world)
-        # phase 2: the level-1 sub-trees of the shared cells
-        ch = children[sp].reshape(-1) if k else np.zeros(0, np.int64)
-        ch = ch[ch >= 0]
-        ch = ch[hist1[ch] > 0] if len(ch) else ch
-        o2, l2 = _lpt(hist1[ch] * DEEP_COST * DEPTH, world)
-        t = float(l1.max() + (l2.max() if len(ch) else 0.0))
-        if best_t is None or t < best_t * 0.98:
-            best_t, best = t, (sp, whole, sl, o1, ch, o2, l1, l2)
-    sp, whole, sl, o1, ch, o2, l1, l2 = best
+    # per candidate (heaviest first): its slabs (cell * NL + layer, non-empty
+    # layers ascending) and its non-empty level-1 children (octant order)
+    slabs = [c * NL + np.flatnonzero(sh[c]) for c in order]
+    kids = []
+    for c in order:
+        q = children[c]
+        q = q[q >= 0]
+        kids.append(q[hist1[q] > 0])
+    slab_off = np.concatenate([[0], np.cumsum([len(a) for a in slabs])]).astype(np.uint64)
+    child_off = np.concatenate([[0], np.cumsum([len(a) for a in kids])]).astype(np.uint64)
+    sl_all = np.concatenate(slabs).astype(np.int64)
+    ch_all = np.concatenate(kids).astype(np.int64) if kids else np.zeros(0, np.int64)
+    # the search over k (C++, pcc_shard_plan_search): phase 1 = the whole cells
+    # and the shared cells' level-0 slabs, phase 2 = the shared cells' level-1
+    # sub-trees, both placed largest first
+    k, best_t = pcconv.shard_plan_search(whole_w[order].astype(np.float64), slab_off,
+                                         sh.reshape(-1)[sl_all] * L0_COST, child_off,
+                                         hist1[ch_all] * DEEP_COST * DEPTH, min(len(order), 2 * world), world)
+    sp, whole = order[:k], order[k:]
+    sl = sl_all[:int(slab_off[k])]
+    o1, l1 = _lpt(np.concatenate([whole_w[whole], sh.reshape(-1)[sl] * L0_COST]), world)
+    ch = ch_all[:int(child_off[k])]
+    o2, l2 = _lpt(hist1[ch] * DEEP_COST * DEPTH, world)
     if len(sp) == 0:
         return no
     owner0 = np.zeros(len(hist0), dtype=np.uint32)
@@ -836,6 +843,11 @@ def cell_triples(ids: np.ndarray, grid) -> np.ndarray:
     return out.astype(np.int32).reshape(-1, 3)
 
 
+def _move(comm, t: torch.Tensor, dev) -> torch.Tensor:
+    """t on `dev`; a communicator may do (and time) the staging copies itself."""
+    return comm.move(t, dev) if hasattr(comm, "move") else t.to(dev)
+
+
 def _exchange(comm, send: torch.Tensor, counts, rcounts, dev) -> torch.Tensor:
     """All-to-all-v of rows into a new tensor on `dev` (straight into it when the
     communicator works on that device, else through the communicator's device)."""
@@ -844,8 +856,8 @@ def _exchange(comm, send: torch.Tensor, counts, rcounts, dev) -> torch.Tensor:
         out = torch.empty((n,) + tuple(send.shape[1:]), dtype=send.dtype, device=dev)
         return comm.alltoallv_into(send, counts, rcounts, out)
     out = torch.empty((n,) + tuple(send.shape[1:]), dtype=send.dtype, device=comm.device)
-    comm.alltoallv_into(send.to(comm.device), counts, rcounts, out)
-    return out.to(dev)
+    comm.alltoallv_into(_move(comm, send, comm.device), counts, rcounts, out)
+    return _move(comm, out, dev)
 
 
 def _exchange_many(comm, specs, dev) -> list:
@@ -855,13 +867,13 @@ def _exchange_many(comm, specs, dev) -> list:
     for send, counts, rcounts in specs:
         n = int(sum(int(v) for v in rcounts))
         outs.append(torch.empty((n,) + tuple(send.shape[1:]), dtype=send.dtype, device=comm.device))
-    sends = [sp[0] if comm.device == dev else sp[0].to(comm.device) for sp in specs]
+    sends = [sp[0] if comm.device == dev else _move(comm, sp[0], comm.device) for sp in specs]
     if hasattr(comm, "alltoallv_many"):
         comm.alltoallv_many([(sd, sp[1], sp[2], o) for sd, sp, o in zip(sends, specs, outs)])
     else:
         for sd, sp, o in zip(sends, specs, outs):
             comm.alltoallv_into(sd, sp[1], sp[2], o)
-    return [o if comm.device == dev else o.to(dev) for o in outs]
+    return [o if comm.device == dev else _move(comm, o, dev) for o in outs]
 
 
 def _combine(parts: list[dict]) -> dict:

@@ -34,6 +34,15 @@ class TimedComm:
         self.c = comm
         self.elapsed_ms = 0.0
 
+    def move(self, t, dev):   # gloo's host staging of device tensors counts as communication
+        import torch
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        r = t.to(dev)
+        torch.cuda.synchronize()
+        self.elapsed_ms += (time.perf_counter() - t0) * 1e3
+        return r
+
     def __getattr__(self, name):
         import torch
         a = getattr(self.c, name)
