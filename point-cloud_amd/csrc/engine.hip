@@ -806,6 +806,9 @@ __global__ void k_l0_hash_ids(const unsigned long long* hkeys, uint32_t cap, uin
     if (i < cap && hkeys[i] != kHashEmpty) ckeys[hcid[i]] = hkeys[i];
 }
 
+#ifndef PCC_L0_PF
+#define PCC_L0_PF 1   // level-0 downsweeps: register tiles in flight ahead (1 or 2)
+#endif
 #ifndef PCC_L0BS
 #define PCC_L0BS 1024
 #define PCC_L0IPT 3
@@ -1242,8 +1245,6 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_down6g(const Point* __restrict_
     const uint64_t lt = lanemask_lt();
     uint32_t err = 0;
     const uint32_t t0 = g * tpg, t1 = min(t0 + tpg, ntiles);
-    float4 v[kL0IPT];
-    uint32_t kk[kL0IPT];
     // wave 0, lane d: output position of digit d for the current tile (the
     // group's tiles are consecutive: the scanned pass-0 group count, then + each
     // tile's total)
@@ -1251,8 +1252,8 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_down6g(const Point* __restrict_
     gofs[lane] = goffr;   // (an LDS write: the load is complete before the loop)
     // every load and store below is issued unconditionally (indices clamped to
     // the tile), so the number of memory ops per tile is static and the waits
-    // for the prefetched tile never cover this tile's stores
-    auto load_tile = [&](uint32_t tile) {
+    // for the prefetched tiles never cover this tile's stores
+    auto load_tile = [&](float4* v, uint32_t* kk, uint32_t tile) {
         const uint64_t base = (uint64_t)tile * kL0Tile;
         asm volatile("" ::: "memory");
 #pragma unroll
@@ -1263,9 +1264,10 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_down6g(const Point* __restrict_
         }
         asm volatile("" ::: "memory");   // keep the loads ahead of the tile's stores
     };
-    load_tile(t0);
-    l0_dummy_stores(dummy, v);   // enter the loop with the back-edge's pending ops
-    for (uint32_t tile = t0; tile < t1; tile++) {
+    // one tile from registers v: digits and wave ranks, the tile's digit
+    // prefix, the LDS partition; then v is refilled with tile `pf` (PCC_L0_PF
+    // tiles ahead) before the partitioned tile is stored
+    auto body = [&](uint32_t tile, float4* v, uint32_t* kk, uint32_t pf) {
         const uint64_t base = (uint64_t)tile * kL0Tile;
         lds_barrier();   // the last tile's stores have read the staging arrays
         uint32_t dgp = 0, rwp = 0;
@@ -1310,7 +1312,7 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_down6g(const Point* __restrict_
                 sd[q] = (uint8_t)d6;
             }
         }
-        load_tile(min(tile + 1, t1 - 1));   // the last tile loads itself again: no branch
+        load_tile(v, kk, pf);   // past the group's end: its last tile again, no branch
         lds_barrier();
         const uint32_t tn = (uint32_t)((n - base) < (uint64_t)kL0Tile ? (n - base) : (uint64_t)kL0Tile);
 #pragma unroll
@@ -1321,7 +1323,27 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_down6g(const Point* __restrict_
             if constexpr (KEYS) O.k[dst] = sk[j];
             else O.k[dst] = (uint32_t)(base + sk[j]);
         }
+    };
+#if PCC_L0_PF == 2
+    // two register tiles: tile t + 2 is loaded while tiles t + 1 and t run
+    float4 va[kL0IPT], vb[kL0IPT];
+    uint32_t ka[kL0IPT], kb[kL0IPT];
+    load_tile(va, ka, t0);
+    l0_dummy_stores(dummy, va);   // enter the loop with the back-edge's pending ops
+    load_tile(vb, kb, min(t0 + 1, t1 - 1));
+    l0_dummy_stores(dummy, vb);
+    for (uint32_t tile = t0; tile < t1; tile += 2) {
+        body(tile, va, ka, min(tile + 2, t1 - 1));
+        if (tile + 1 >= t1) break;
+        body(tile + 1, vb, kb, min(tile + 3, t1 - 1));
     }
+#else
+    float4 v[kL0IPT];
+    uint32_t kk[kL0IPT];
+    load_tile(v, kk, t0);
+    l0_dummy_stores(dummy, v);   // enter the loop with the back-edge's pending ops
+    for (uint32_t tile = t0; tile < t1; tile++) body(tile, v, kk, min(tile + 1, t1 - 1));
+#endif
     lds_barrier();
     if (pairs)
         for (int i = tid; i < R * R5; i += kL0BS)
@@ -1416,9 +1438,7 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_down5g(Arena S, Arena O, L0Para
     for (int i = tid; i < kL0RW * R / 4; i += kL0BS) reinterpret_cast<uint32_t*>(&wcnt[0][0])[i] = 0;
     const uint64_t lt = lanemask_lt();
     uint32_t err = 0;
-    float4 v[kL0IPT];
-    uint32_t kk[kL0IPT];
-    auto load_tile = [&](uint32_t base) {   // unconditional, clamped (see k_l0_down6g)
+    auto load_tile = [&](float4* v, uint32_t* kk, uint32_t base) {   // unconditional, clamped (see k_l0_down6g)
         asm volatile("" ::: "memory");
 #pragma unroll
         for (int r = 0; r < kL0IPT; r++) {
@@ -1429,9 +1449,7 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_down5g(Arena S, Arena O, L0Para
         asm volatile("" ::: "memory");   // keep the loads ahead of the tile's stores
     };
     if (a >= b) return;   // (units are never empty)
-    load_tile(a);
-    l0_dummy_stores(dummy, v);
-    for (uint32_t base = a; base < b; base += kL0Tile) {
+    auto body = [&](uint32_t base, float4* v, uint32_t* kk, uint32_t pf) {
         const uint32_t tn = min(b - base, (uint32_t)kL0Tile);
         lds_barrier();
         uint32_t dgp = 0, rwp = 0;
@@ -1478,7 +1496,7 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_down5g(Arena S, Arena O, L0Para
                 sd[q] = (uint8_t)d5;
             }
         }
-        load_tile(b - base > (uint32_t)kL0Tile ? base + kL0Tile : base);
+        load_tile(v, kk, pf);
         lds_barrier();
 #pragma unroll
         for (int r = 0; r < kL0IPT; r++) {   // past tn: a duplicate of the last store
@@ -1487,7 +1505,31 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_down5g(Arena S, Arena O, L0Para
             O.p[dst] = sp[j];
             O.k[dst] = sk[j];
         }
+    };
+    // the tile `k` tiles after `base`, clamped to the unit's last tile
+    auto ahead = [&](uint32_t base, uint32_t k) {
+        const uint32_t last = a + (b - 1 - a) / kL0Tile * kL0Tile;
+        return min(base + k * (uint32_t)kL0Tile, last);
+    };
+#if PCC_L0_PF == 2
+    float4 va[kL0IPT], vb[kL0IPT];
+    uint32_t ka[kL0IPT], kb[kL0IPT];
+    load_tile(va, ka, a);
+    l0_dummy_stores(dummy, va);
+    load_tile(vb, kb, ahead(a, 1));
+    l0_dummy_stores(dummy, vb);
+    for (uint32_t base = a; base < b; base += 2 * kL0Tile) {
+        body(base, va, ka, ahead(base, 2));
+        if (base + kL0Tile >= b) break;
+        body(base + kL0Tile, vb, kb, ahead(base, 3));
     }
+#else
+    float4 v[kL0IPT];
+    uint32_t kk[kL0IPT];
+    load_tile(v, kk, a);
+    l0_dummy_stores(dummy, v);
+    for (uint32_t base = a; base < b; base += kL0Tile) body(base, v, kk, ahead(base, 1));
+#endif
     lds_barrier();
     for (int i = tid; i < R * kDests; i += kL0BS) {
         const uint32_t c = hc[i];
