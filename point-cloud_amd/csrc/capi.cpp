@@ -1011,16 +1011,31 @@ int pcc_convert_files(const char* out_dir, const char* const* paths, size_t npat
             else if (r.data_error.empty()) rc = pcc_add_points(c, nullptr, 0);   // no points: one empty batch
             if (rc) { pcc_close(c); return rc; }
             if (!r.data_error.empty()) log_line("ERROR", "%s", r.data_error.c_str());
-        } else if (ext == "json") {   // converter/own.rs: another converted cloud as input
-            std::vector<Point> pts;
-            uint64_t total = 0;
+        } else if (ext == "json") {   // converter/own.rs: another converted cloud as input, streamed
+            uint64_t total = 0, pushed = 0;
             std::string err;
-            if (read_cloud_points(p, pts, total, err)) {
-                log_line("ERROR", "%s", err.c_str());   // lib.rs:75-77 unwraps; reported instead
+            bool open = false, logged = false;
+            int src = 0;
+            const PointSink sink = [&](const Point* pts, uint64_t m) -> bool {
+                if (!logged) { log_line("INFO", "Converting %llu points", (unsigned long long)total); logged = true; }
+                if (!open) { if ((src = pcc_begin_file(c, total))) return false; open = true; }
+                if ((src = pcc_append_points(c, reinterpret_cast<const pcc_point*>(pts), m))) return false;
+                pushed += m;
+                return true;
+            };
+            const int r = read_cloud_points(p, total, sink, err);
+            if (src) {   // the converter refused a piece
+                if (open) pcc_cancel_file(c);
+                pcc_close(c);
+                return src;
+            }
+            if (r) {   // lib.rs:75-77 unwraps; reported instead, the file contributes nothing
+                if (open) pcc_cancel_file(c);
+                log_line("ERROR", "%s", err.c_str());
                 continue;
             }
-            log_line("INFO", "Converting %llu points", (unsigned long long)total);
-            rc = pcc_add_points(c, reinterpret_cast<const pcc_point*>(pts.data()), pts.size());
+            if (!logged) log_line("INFO", "Converting %llu points", (unsigned long long)total);
+            rc = open ? pcc_end_file(c, pushed) : pcc_add_points(c, nullptr, 0);   // an empty cloud: one empty batch
             if (rc) { pcc_close(c); return rc; }
         } else {
             log_line("WARN", "Unsupported file format '%s'", ext.c_str());   // lib.rs:78-81

@@ -445,9 +445,11 @@ bool read_cell_file(const std::string& path, CellFile& out, std::string& err) {
     return true;
 }
 
-int read_cloud(const std::string& dir, uint32_t hierarchies, std::vector<CellFile>& cells, std::string& err,
-               const std::vector<int32_t>* subtrees) {
-    cells.clear();
+namespace {
+struct CloudFile { std::string path; uint32_t h; int32_t x, y, z; };
+// The cell files of a cloud in a fixed order: hierarchy by hierarchy, names
+// sorted; optionally only those below the given level-0 cells.
+std::vector<CloudFile> list_cloud(const std::string& dir, uint32_t hierarchies, const std::vector<int32_t>* subtrees) {
     // level-0 subtrees to keep (sorted triples); a level-h cell's level-0
     // ancestor is its index >> h (arithmetic: child = 2 * parent + bit)
     std::vector<std::array<int32_t, 3>> keep;
@@ -456,8 +458,7 @@ int read_cloud(const std::string& dir, uint32_t hierarchies, std::vector<CellFil
             keep.push_back({(*subtrees)[i], (*subtrees)[i + 1], (*subtrees)[i + 2]});
         std::sort(keep.begin(), keep.end());
     }
-    struct Want { std::string path; uint32_t h; int32_t x, y, z; };
-    std::vector<Want> want;
+    std::vector<CloudFile> want;
     for (uint32_t h = 0; h < hierarchies; h++) {
         const std::string hd = dir + "/h_" + std::to_string(h);
         DIR* d = opendir(hd.c_str());
@@ -475,18 +476,22 @@ int read_cloud(const std::string& dir, uint32_t hierarchies, std::vector<CellFil
             want.push_back({hd + "/" + nm, h, x, y, z});
         }
     }
-    // the files in parallel (the same reader pool size as the writer)
-    cells.resize(want.size());
-    std::atomic<size_t> next{0};
+    return want;
+}
+// files want[i0 .. i1) into cells[0 .. i1 - i0), in parallel (the writer's pool size)
+bool read_cloud_files(const std::vector<CloudFile>& want, size_t i0, size_t i1, std::vector<CellFile>& cells,
+                      std::string& err) {
+    cells.resize(i1 - i0);
+    std::atomic<size_t> next{i0};
     std::atomic<bool> failed{false};
     std::mutex em;
     auto work = [&]() {
         std::string e;
         for (;;) {
             const size_t i = next.fetch_add(1);
-            if (i >= want.size() || failed.load()) return;
-            const Want& w = want[i];
-            CellFile& c = cells[i];
+            if (i >= i1 || failed.load()) return;
+            const CloudFile& w = want[i];
+            CellFile& c = cells[i - i0];
             bool ok = read_cell_file(w.path, c, e);
             if (ok && (c.h != w.h || c.idx[0] != w.x || c.idx[1] != w.y || c.idx[2] != w.z)) {
                 e = w.path + ": header does not match the file name";
@@ -499,12 +504,20 @@ int read_cloud(const std::string& dir, uint32_t hierarchies, std::vector<CellFil
             }
         }
     };
-    const unsigned nt = std::max(1u, std::min<unsigned>(writer_threads(), (unsigned)want.size()));
+    const unsigned nt = std::max(1u, std::min<unsigned>(writer_threads(), (unsigned)(i1 - i0)));
     std::vector<std::thread> th;
     for (unsigned t = 1; t < nt; t++) th.emplace_back(work);
     work();
     for (auto& t : th) t.join();
-    if (failed.load()) {
+    return !failed.load();
+}
+}  // namespace
+
+int read_cloud(const std::string& dir, uint32_t hierarchies, std::vector<CellFile>& cells, std::string& err,
+               const std::vector<int32_t>* subtrees) {
+    cells.clear();
+    const std::vector<CloudFile> want = list_cloud(dir, hierarchies, subtrees);
+    if (!read_cloud_files(want, 0, want.size(), cells, err)) {
         cells.clear();
         return -EINVAL;
     }
@@ -816,7 +829,7 @@ bool read_las(const std::string& path, LasResult& out, std::string& err, const P
     return true;
 }
 
-int read_cloud_points(const std::string& metadata_path, std::vector<Point>& pts, uint64_t& number_of_points,
+int read_cloud_points(const std::string& metadata_path, uint64_t& number_of_points, const PointSink& sink,
                       std::string& err) {
     std::ifstream f(metadata_path);
     if (!f) { err = "cannot open " + metadata_path; return -ENOENT; }
@@ -824,18 +837,25 @@ int read_cloud_points(const std::string& metadata_path, std::vector<Point>& pts,
     ss << f.rdbuf();
     Metadata m;
     if (!parse_metadata_json(ss.str(), m, err)) return -EINVAL;   // own.rs:57-60
+    number_of_points = m.number_of_points;
     const size_t slash = metadata_path.find_last_of('/');
     const std::string dir = slash == std::string::npos ? "." : metadata_path.substr(0, slash);
+    // own.rs:16-78 hands out the cloud's points cell by cell; here windows of
+    // cell files are read in parallel and their points handed to the sink in
+    // the fixed order (Cell::all_points cell.rs:66-68: grid, then the kept
+    // lists), so at most one window is in host memory
+    const std::vector<CloudFile> want = list_cloud(dir, m.hierarchies, nullptr);
+    constexpr size_t kWindow = 64;
     std::vector<CellFile> cells;
-    const int rc = read_cloud(dir, m.hierarchies, cells, err);
-    if (rc) return rc;
-    pts.clear();
-    for (const CellFile& c : cells) {   // Cell::all_points cell.rs:66-68
-        pts.insert(pts.end(), c.grid.begin(), c.grid.end());
-        for (const CellFile::Entry& e : c.entries)
-            if (e.some) pts.insert(pts.end(), e.pts.begin(), e.pts.end());
+    for (size_t i0 = 0; i0 < want.size(); i0 += kWindow) {
+        const size_t i1 = std::min(want.size(), i0 + kWindow);
+        if (!read_cloud_files(want, i0, i1, cells, err)) return -EINVAL;
+        for (const CellFile& c : cells) {
+            if (!c.grid.empty() && !sink(c.grid.data(), c.grid.size())) return -ECANCELED;
+            for (const CellFile::Entry& e : c.entries)
+                if (e.some && !e.pts.empty() && !sink(e.pts.data(), e.pts.size())) return -ECANCELED;
+        }
     }
-    number_of_points = m.number_of_points;
     return 0;
 }
 

@@ -111,7 +111,10 @@ bool read_las(const std::string& path, LasResult& out, std::string& err, const P
 // enumerates directories and FxHashMaps in unspecified order; this reader fixes
 // the order (file names sorted, grid and overflow entries in file order), so
 // parity for this input is defined relative to that enumeration.
-int read_cloud_points(const std::string& metadata_path, std::vector<Point>& pts, uint64_t& number_of_points,
+// converter/own.rs: another cloud (its metadata.json) as an input file, its
+// points handed to `sink` cell after cell (grid, then kept lists), streamed
+// through windows of cell files; -ECANCELED when the sink stops it
+int read_cloud_points(const std::string& metadata_path, uint64_t& number_of_points, const PointSink& sink,
                       std::string& err);
 
 }  // namespace pcc

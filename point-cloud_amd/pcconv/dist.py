@@ -614,6 +614,9 @@ class HipShardOps:
             return
         if self.conv is not None:
             self.conv.close()
+            # the closed converter's buffers would sit in the library's device
+            # cache, invisible to PyTorch's allocator and RCCL
+            pcconv.release_device_cache()
         self.conv = pcconv.Converter(self.out_dir, batch_size=self.batch_size, device=self.dev, config=self.cfg,
                                      subtrees=cells)
         self.subtrees = cells
