@@ -173,7 +173,16 @@ static void dev_alloc_t(T*& p, size_t bytes) {
 // ------------------------------------------------------------------ constants
 constexpr uint64_t kEmpty64 = ~0ull;
 constexpr uint32_t kEmpty32 = 0xFFFFFFFFu;
+// Diagnostic build only (-DPCC_HALFX, `make var`): timing of two 512-thread
+// workgroups per dense slab, each replaying half the chunks into a half-size slot
+// table (results wrong; measures what two workgroups per CU would gain).
+#ifdef PCC_HALFX
+constexpr int kHX = PCC_HALFX;   // log2 of the workgroups per slab
+constexpr int kDenseBS = 1024 >> kHX;
+#else
 constexpr int kDenseBS = 1024;
+constexpr int kHX = 0;
+#endif
 constexpr int kDenseTab = 116 * 132;  // one z-layer of a dim-96 cell (slab_geom)
 constexpr int kDenseClaim = 2048;
 #ifndef PCC_SLAB_PF
@@ -1670,7 +1679,7 @@ struct SlabParams {
 // Dense slabs (>= kSmallMax arrivals): one 1024-thread workgroup per slab, the
 // slab's whole hex layer as a direct-mapped slot table in LDS.
 struct DenseLds {
-    static constexpr int BS = kDenseBS, TAB = kDenseTab, CLAIM = kDenseClaim, NW = BS / 64;
+    static constexpr int BS = kDenseBS, TAB = kDenseTab >> kHX, CLAIM = kDenseClaim >> kHX, NW = BS / 64;
     unsigned long long tab[TAB];   // occupant: (d2 bits << 33) | (child slab << 28) | j
     uint32_t claim[2][CLAIM];      // per chunk parity: (slot << 11) | head of the slot's candidate list
     uint32_t cd2[BS];              // candidates of the current chunk, by thread: d2 bits,
@@ -1878,7 +1887,8 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
     __shared__ L S;
     STAMP_DECL
     const uint32_t tid = threadIdx.x, wv = tid / 64, lane = tid & 63;
-    const SmallDesc D = P.ddesc[blockIdx.x];
+    const SmallDesc D = P.ddesc[blockIdx.x >> kHX];
+    const uint32_t hx = blockIdx.x & ((1u << kHX) - 1u);   // PCC_HALFX: this workgroup's chunk residue
     const uint32_t s = D.s;
     const int32_t t = D.t;
     const uint32_t off = D.off, n = D.n, nm1 = n - 1;
@@ -1939,7 +1949,7 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
     Pre pre[PF + 2];
 #pragma unroll
     for (int q = 0; q < PF + 2; q++) {
-        const uint32_t jo = min(ng + (uint32_t)(q * BS) + tid, nm1);
+        const uint32_t jo = min(ng + (uint32_t)(((q << kHX) + hx) * BS) + tid, nm1);
         if (q < PF) {
             pre[q].p = rP.p(jo * 16);
             pre[q].k = rP.k(jo * 4);
@@ -1988,23 +1998,30 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
                 const unsigned long long e = ((unsigned long long)f2u(d2) << 33) | ((unsigned long long)dn << kJBits) |
                                              (wide ? 0u : ((uint32_t)(gn + 1) << 23)) | jg;
                 // two grid points in one slot: not a cell a converter writes
-                if (atomicCAS(&S.tab[(uint32_t)(ly * P.tx + lx)], kEmpty64, e) != kEmpty64) err |= ERR_CLAIM;
+                if (atomicCAS(&S.tab[(uint32_t)(ly * P.tx + lx) >> kHX], kEmpty64, e) != kEmpty64) err |= ERR_CLAIM;
             }
         }
         __syncthreads();
     }
     STAMP(0);
     // child-slab regions of this slab, one per lane < 24, kept in registers
-    const uint32_t my_doff = lane < kDests ? S.doff[lane] : 0u, my_dcap = lane < kDests ? S.dcap[lane] : 0u;
-    const uint32_t nchunks = (n - ng + BS - 1) / BS;
+    uint32_t my_doff = lane < kDests ? S.doff[lane] : 0u, my_dcap = lane < kDests ? S.dcap[lane] : 0u;
+    uint32_t nchunks = (n - ng + BS - 1) / BS;
+    if (kHX) {
+        const uint32_t b0 = (uint32_t)((uint64_t)my_dcap * hx >> kHX), b1 = (uint32_t)((uint64_t)my_dcap * (hx + 1) >> kHX);
+        my_doff += b0;
+        my_dcap = b1 - b0;
+        nchunks = (nchunks + (1u << kHX) - 1u - hx) >> kHX;
+    }
     auto step = [&](uint32_t ci, Stage& cur, Stage& prv, const Pre& mine, const Pre& prvb, Pre& pf) {
         const uint32_t par = ci & 1;
         uint32_t* claim = S.claim[par];
-        const uint32_t j = ng + ci * BS + tid;
+        const uint32_t cg = (ci << kHX) + hx;   // chunk index in the slab
+        const uint32_t j = ng + cg * BS + tid;
         const bool valid = j < n;
         const bool forced = valid && mine.k - P.kf_lo < P.kf_n;
         {   // prefetch chunk i+2 (clamped)
-            const uint32_t jo = min(j + PF * BS, nm1);
+            const uint32_t jo = min(j + ((PF * BS) << kHX), nm1);
             pf.p = rP.p(jo * 16);
             pf.k = rP.k(jo * 4);
         }
@@ -2029,7 +2046,7 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
         int32_t lx = sd.ox - rx, ly = sd.oy - ry;
         bool range_ok = lx >= 0 && ly >= 0 && lx < P.tx && ly < P.ty;
         bool slotted = valid && sd.layer_ok && range_ok;
-        uint32_t local = slotted ? (uint32_t)(ly * P.tx + lx) : 0u;
+        uint32_t local = slotted ? (uint32_t)(ly * P.tx + lx) >> kHX : 0u;
         // the slot's occupant, read before the rest of the arithmetic so the LDS
         // latency overlaps it (phase B of the last step wrote the table before
         // the barrier; local 0 for lanes without a slot)
@@ -2041,7 +2058,7 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
                 ly = sd.oy - ry;
                 range_ok = lx >= 0 && ly >= 0 && lx < P.tx && ly < P.ty;
                 slotted = valid && sd.layer_ok && range_ok;
-                local = slotted ? (uint32_t)(ly * P.tx + lx) : 0u;
+                local = slotted ? (uint32_t)(ly * P.tx + lx) >> kHX : 0u;
                 occ = S.tab[local];
             }
         }
@@ -2112,7 +2129,14 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
             if (lane < kDests) {   // byte sums of the wave counts: earlier waves, all waves
                 pre_l = S.dcur[rp][lane];
                 tot_l = pre_l;
-                const u32x4 w = *reinterpret_cast<const u32x4*>(S.wcnt[lane]);
+                uint32_t w[NW / 4];
+                if constexpr (NW == 16) {
+                    const u32x4 w4 = *reinterpret_cast<const u32x4*>(S.wcnt[lane]);
+                    w[0] = w4.x; w[1] = w4.y; w[2] = w4.z; w[3] = w4.w;
+                } else {
+#pragma unroll
+                    for (int k = 0; k < NW / 4; k++) w[k] = S.wcnt[lane][k];
+                }
 #pragma unroll
                 for (uint32_t k = 0; k < (uint32_t)NW / 4; k++) {
                     const uint32_t nb = wv > 4 * k ? min(wv - 4 * k, 4u) : 0u;   // wave-uniform
@@ -2168,7 +2192,7 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
                     em = 1;
                     emd = dg & 31u;
                     emg = (int32_t)(dg >> 5) - 1;
-                    gsrc = (ng + ci * BS + bt) * 16;
+                    gsrc = (ng + cg * BS + bt) * 16;
                 } else if (occ != kEmpty64) {          // first record: displaces the occupant
                     em = 1;
                     emd = (uint32_t)(occ >> kJBits) & 31u;
@@ -2220,12 +2244,21 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
     dense_grid_points<L>(P, S, &S.claim[0][0], rP, s, n, jmask, tid, lane);
     STAMP(8);
     STAMP_FLUSH(P.stamps);
+    if (kHX) err = 0;
     if (err) atomicOr(&S.err, err);
     __syncthreads();
     const uint32_t fp = nchunks & 1;   // dcur after the last (emit-only) step
-    if (tid == 0) {
+    if (tid == 0 && hx == 0) {
         P.slab_grid_n[s] = S.nwin;
         if (S.err) set_err(P.ctr, S.err);
+    }
+    if (kHX) {   // both halves add (zeroed before the launch)
+        const uint32_t dc = S.dcap[tid % kDests];
+        const uint32_t hcap = (uint32_t)((uint64_t)dc * (hx + 1) >> kHX) - (uint32_t)((uint64_t)dc * hx >> kHX);
+        if (tid < kDests) atomicAdd(&P.dest_n[s * kDests + tid], S.dcur[fp][tid] < hcap ? S.dcur[fp][tid] : hcap);
+        for (int i = tid; i < kDests * kDests; i += BS)
+            if (S.gcnt[i]) atomicAdd(&P.gcap[(uint64_t)s * kDests * kDests + i], S.gcnt[i]);
+        return;
     }
     if (tid < kDests) P.dest_n[s * kDests + tid] = S.dcur[fp][tid] < S.dcap[tid] ? S.dcur[fp][tid] : S.dcap[tid];
     // capacities of the child slabs' own child slabs (only rows that will exist)
@@ -4275,9 +4308,13 @@ int Engine::run_level(uint32_t li) {
 #ifdef PCC_STAMPS
         SP.stamps = stamps;
 #endif
+        if (kHX) {
+            HIP_CHECK(hipMemsetAsync(L->dest_n, 0, (uint64_t)L->nslabs * kDests * 4, stream_));
+            HIP_CHECK(hipMemsetAsync(L->gcap, 0, (uint64_t)L->nslabs * kDests * kDests * 4, stream_));
+        }
         ev_begin(ST_DENSE);
-        if (seeds_in_place) k_slab<true><<<L->nbig, kDenseBS, 0, stream_>>>(SP);
-        else k_slab<false><<<L->nbig, kDenseBS, 0, stream_>>>(SP);
+        if (seeds_in_place) k_slab<true><<<L->nbig << kHX, kDenseBS, 0, stream_>>>(SP);
+        else k_slab<false><<<L->nbig << kHX, kDenseBS, 0, stream_>>>(SP);
         ev_end(ST_DENSE);
         if (verbose) {
             HIP_CHECK(hipStreamSynchronize(stream_));
@@ -4387,7 +4424,7 @@ int Engine::run_level(uint32_t li) {
     L->kept_used = hc.kept_cur;
     stats_.grid_points += hg;
     stats_.kept_points += hc.kept_cur;
-    if (hc.err) {
+    if (hc.err && !kHX) {
         char buf[200];
         snprintf(buf, sizeof buf,
                  "device error flags 0x%x at level %u (1 slot range, 2 layer, 4 octant, 8 sel, 16 kept cap, 64 capacity, "
