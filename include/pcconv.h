@@ -214,15 +214,22 @@ int pcc_shard_grid_from_bbox(const float gmin[3], const float gmax[3], float max
 int pcc_shard_lpt(const double* w, uint64_t n, uint32_t world, uint32_t* owner, double* load);
 /* The plan's shared-cell search (host only; pcconv/dist.py plan_split): the
  * ncand non-empty level-0 cells, heaviest first, with their whole-cell weights
- * whole_w[i], their slabs' weights slab_w[slab_off[i] .. slab_off[i+1]) and
- * their level-1 children's weights child_w[child_off[i] .. child_off[i+1]).
+ * whole_w[i]; the first kmax of them (the only ones that can be shared) with
+ * their slabs' weights slab_w[slab_off[i] .. slab_off[i+1]) and their level-1
+ * children's weights child_w[child_off[i] .. child_off[i+1]) (kmax + 1 offsets
+ * each).
  * For k = 0 .. kmax the first k cells are shared: phase 1 = LPT of the whole
  * cells k.. followed by the first k cells' slabs, phase 2 = LPT of their
  * children; the estimate is max phase-1 load + max phase-2 load.  A larger k
- * replaces the best one only when it is more than 2 % lower. */
+ * replaces the best one only when it is more than 2 % lower.  Optional outputs
+ * (NULL: not wanted) for the best k: whole_owner[i] for cells i >= k (ncand
+ * entries), slab_owner[q] for the slabs of cells < k and child_owner[q] for
+ * their children (slab_off[kmax] / child_off[kmax] entries), and the phase-1 /
+ * phase-2 load per rank (world entries each) -- the LPT of the two lists. */
 int pcc_shard_plan_search(const double* whole_w, const uint64_t* slab_off, const double* slab_w,
                           const uint64_t* child_off, const double* child_w, uint32_t ncand, uint32_t kmax,
-                          uint32_t world, uint32_t* best_k, double* best_t);
+                          uint32_t world, uint32_t* best_k, double* best_t, uint32_t* whole_owner,
+                          uint32_t* slab_owner, uint32_t* child_owner, double* load1, double* load2);
 
 /* Points first .. first+n-1 of the synthetic stream of pcc_add_synthetic,
  * written to dst[0 .. n) in device memory (each rank generates its key range). */
@@ -265,6 +272,16 @@ int pcc_shard_route_slabs(const pcc_point* dev_pts, uint64_t n, uint32_t key0, c
 int pcc_shard_route_bitmaps(const pcc_point* dev_pts, uint64_t n, const pcc_shard_grid* g,
                             uint32_t sub_grid_dimension, const uint32_t* dev_owner, uint32_t nranks,
                             pcc_point* dev_send, uint64_t* dev_bitmaps, uint64_t* counts, int device);
+/* One-pass form of pcc_shard_route_bitmaps (same outputs): dev_hist = this
+ * rank's points per unit (pcc_shard_histogram for cell units,
+ * pcc_shard_slab_histogram for slab units, over the same dev_pts), which gives
+ * every destination's total before the points are read; the points are then
+ * read once (decoupled look-back between 4096-point tiles) instead of twice.
+ * -EBADMSG if the histogram does not match the points. */
+int pcc_shard_route_bitmaps_hist(const pcc_point* dev_pts, uint64_t n, const pcc_shard_grid* g,
+                                 uint32_t sub_grid_dimension, const uint32_t* dev_owner, uint32_t nranks,
+                                 const uint32_t* dev_hist, pcc_point* dev_send, uint64_t* dev_bitmaps,
+                                 uint64_t* counts, int device);
 /* Keys of the points received from nsrc senders (sender order, each ascending):
  * dev_bitmaps = the senders' rows for this rank concatenated (nwords[s] words
  * each), key0[s] = sender s's first global key.  nkeys must equal the number of

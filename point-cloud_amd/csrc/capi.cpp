@@ -479,19 +479,42 @@ int pcc_shard_grid_from_bbox(const float gmin[3], const float gmax[3], float max
     return 0;
 }
 
+// Least loaded rank, ties by rank, in log2(world) compares per placement: a
+// tournament tree over the ranks (leaves padded to a power of two with +inf),
+// each node holding the winner of its two children, the left one on ties.
+struct LeastLoaded {
+    uint32_t m = 1;
+    std::vector<double> load;
+    std::vector<uint32_t> node;   // node[1] = the overall winner
+    explicit LeastLoaded(uint32_t world) {
+        while (m < world) m <<= 1;
+        load.assign(m, INFINITY);
+        for (uint32_t r = 0; r < world; r++) load[r] = 0.0;
+        node.assign(2 * m, 0);
+        for (uint32_t r = 0; r < m; r++) node[m + r] = r;
+        for (uint32_t v = m - 1; v >= 1; v--) node[v] = pick(node[2 * v], node[2 * v + 1]);
+    }
+    uint32_t pick(uint32_t a, uint32_t b) const { return load[b] < load[a] ? b : a; }
+    // adds w to the least loaded rank and returns it
+    uint32_t place(double w) {
+        const uint32_t r = node[1];
+        load[r] += w;
+        for (uint32_t v = (m + r) >> 1; v >= 1; v >>= 1) node[v] = pick(node[2 * v], node[2 * v + 1]);
+        return r;
+    }
+};
+
 // largest first (ties by index) to the least loaded rank (ties by rank)
 static void lpt(const double* w, uint64_t n, uint32_t world, uint32_t* owner, double* load) {
     std::vector<uint64_t> order(n);
     for (uint64_t i = 0; i < n; i++) order[i] = i;
     std::stable_sort(order.begin(), order.end(), [&](uint64_t a, uint64_t b) { return w[a] > w[b]; });
-    for (uint32_t r = 0; r < world; r++) load[r] = 0.0;
+    LeastLoaded ll(world);
     for (uint64_t i : order) {
-        uint32_t best = 0;
-        for (uint32_t r = 1; r < world; r++)
-            if (load[r] < load[best]) best = r;
+        const uint32_t best = ll.place(w[i]);
         if (owner) owner[i] = best;
-        load[best] += w[i];
     }
+    for (uint32_t r = 0; r < world; r++) load[r] = ll.load[r];
 }
 
 int pcc_shard_lpt(const double* w, uint64_t n, uint32_t world, uint32_t* owner, double* load) {
@@ -504,7 +527,8 @@ int pcc_shard_lpt(const double* w, uint64_t n, uint32_t world, uint32_t* owner, 
 
 int pcc_shard_plan_search(const double* whole_w, const uint64_t* slab_off, const double* slab_w,
                           const uint64_t* child_off, const double* child_w, uint32_t ncand, uint32_t kmax,
-                          uint32_t world, uint32_t* best_k, double* best_t) {
+                          uint32_t world, uint32_t* best_k, double* best_t, uint32_t* whole_owner,
+                          uint32_t* slab_owner, uint32_t* child_owner, double* load1, double* load2) {
     if (!best_k || !best_t || world == 0 || kmax > ncand || (ncand && (!whole_w || !slab_off || !child_off)))
         return set_err(-EINVAL, "null argument, no ranks or kmax > ncand");
     GUARD_BEGIN
@@ -514,8 +538,10 @@ int pcc_shard_plan_search(const double* whole_w, const uint64_t* slab_off, const
     // once, then each k is one filtered greedy pass.
     struct It { double w; uint32_t type, cell; uint64_t pos; };
     std::vector<It> p1, p2;
+    // only the first kmax candidates can be shared: their slabs and children alone
     for (uint32_t i = 0; i < ncand; i++) {
         p1.push_back({whole_w[i], 0u, i, i});
+        if (i >= kmax) continue;
         for (uint64_t q = slab_off[i]; q < slab_off[i + 1]; q++) p1.push_back({slab_w[q], 1u, i, q});
         for (uint64_t q = child_off[i]; q < child_off[i + 1]; q++) p2.push_back({child_w[q], 1u, i, q});
     }
@@ -526,29 +552,44 @@ int pcc_shard_plan_search(const double* whole_w, const uint64_t* slab_off, const
     };
     std::sort(p1.begin(), p1.end(), by);
     std::sort(p2.begin(), p2.end(), by);
-    std::vector<double> l1(world), l2(world);
-    auto place = [&](std::vector<double>& load, double w) {
-        uint32_t r = 0;   // least loaded rank, ties by rank
-        for (uint32_t q = 1; q < world; q++)
-            if (load[q] < load[r]) r = q;
-        load[r] += w;
-    };
+    auto in1 = [](const It& it, uint32_t k) { return (it.cell >= k) == (it.type == 0); };
     bool have = false;
     *best_k = 0;
     *best_t = 0.0;
     for (uint32_t k = 0; k <= kmax; k++) {
-        std::fill(l1.begin(), l1.end(), 0.0);
-        std::fill(l2.begin(), l2.end(), 0.0);
+        LeastLoaded l1(world), l2(world);
         for (const It& it : p1)
-            if (it.type == 0 ? it.cell >= k : it.cell < k) place(l1, it.w);
+            if (in1(it, k)) l1.place(it.w);
         bool any2 = false;
         for (const It& it : p2)
-            if (it.cell < k) { place(l2, it.w); any2 = true; }
-        const double t = *std::max_element(l1.begin(), l1.end()) + (any2 ? *std::max_element(l2.begin(), l2.end()) : 0.0);
+            if (it.cell < k) { l2.place(it.w); any2 = true; }
+        const double t = *std::max_element(l1.load.begin(), l1.load.begin() + world) +
+                         (any2 ? *std::max_element(l2.load.begin(), l2.load.begin() + world) : 0.0);
         if (!have || t < *best_t * 0.98) {
             have = true;
             *best_t = t;
             *best_k = k;
+        }
+    }
+    // the best k's placement (= LPT of its two lists, the same order): owners
+    // of the whole cells k.., of the slabs and children of the cells ..k
+    if (whole_owner || slab_owner || child_owner || load1 || load2) {
+        const uint32_t k = *best_k;
+        LeastLoaded l1(world), l2(world);
+        for (const It& it : p1) {
+            if (!in1(it, k)) continue;
+            const uint32_t r = l1.place(it.w);
+            if (it.type == 0 && whole_owner) whole_owner[it.pos] = r;
+            if (it.type == 1 && slab_owner) slab_owner[it.pos] = r;
+        }
+        for (const It& it : p2) {
+            if (it.cell >= k) continue;
+            const uint32_t r = l2.place(it.w);
+            if (child_owner) child_owner[it.pos] = r;
+        }
+        for (uint32_t r = 0; r < world; r++) {
+            if (load1) load1[r] = l1.load[r];
+            if (load2) load2[r] = l2.load[r];
         }
     }
     return 0;
@@ -635,6 +676,21 @@ int pcc_shard_route_bitmaps(const pcc_point* d, uint64_t n, const pcc_shard_grid
     GUARD_BEGIN
     const int rc = shard_route(reinterpret_cast<const Point*>(d), n, 0, to_grid(g), downer, nranks,
                                reinterpret_cast<Point*>(dsend), nullptr, counts, device, sub_grid_dimension, dbitmaps);
+    return rc ? set_err(rc, "routing failed (nranks > 64, point outside grid, or owner >= nranks)") : 0;
+    GUARD_END
+}
+
+int pcc_shard_route_bitmaps_hist(const pcc_point* d, uint64_t n, const pcc_shard_grid* g, uint32_t sub_grid_dimension,
+                                 const uint32_t* downer, uint32_t nranks, const uint32_t* dhist, pcc_point* dsend,
+                                 uint64_t* dbitmaps, uint64_t* counts, int device) {
+    if ((!d || !dsend || !dbitmaps) && n) return set_err(-EINVAL, "null argument");
+    if (!g || !downer || !dhist || !counts) return set_err(-EINVAL, "null argument");
+    if (sub_grid_dimension != 0 && 2 * sub_grid_dimension + 2 > PCC_SHARD_LAYERS)
+        return set_err(-EINVAL, "sub_grid_dimension out of range for slab sharding");
+    GUARD_BEGIN
+    const int rc = shard_route_hist(reinterpret_cast<const Point*>(d), n, to_grid(g), downer, nranks, dhist,
+                                    reinterpret_cast<Point*>(dsend), dbitmaps, counts, device, sub_grid_dimension);
+    if (rc == -EBADMSG) return set_err(rc, "the unit histogram does not match the points");
     return rc ? set_err(rc, "routing failed (nranks > 64, point outside grid, or owner >= nranks)") : 0;
     GUARD_END
 }

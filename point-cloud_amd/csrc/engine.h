@@ -331,6 +331,8 @@ int shard_histogram(const Point* d, uint64_t n, const ShardGrid& g, uint32_t* dh
 // dkeys (global key per routed point) or dbm (nranks x ceil(n/64) membership words), either may be null
 int shard_route(const Point* d, uint64_t n, uint32_t key0, const ShardGrid& g, const uint32_t* downer, uint32_t nranks,
                 Point* dsend, uint32_t* dkeys, uint64_t* counts, int device, uint32_t dim = 0, uint64_t* dbm = nullptr);
+int shard_route_hist(const Point* d, uint64_t n, const ShardGrid& g, const uint32_t* downer, uint32_t nranks,
+                     const uint32_t* dhist, Point* dsend, uint64_t* dbm, uint64_t* counts, int device, uint32_t dim);
 int shard_keys_from_bitmaps(const uint64_t* dbm, const uint64_t* nwords, const uint64_t* key0, uint32_t nsrc,
                             uint32_t* dkeys, uint64_t nkeys, int device);
 // pcc_shard_resolve_buckets (pcconv.h)

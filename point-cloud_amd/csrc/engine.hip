@@ -4894,6 +4894,127 @@ __global__ void k_route_totals(const uint32_t* base, uint32_t ntiles, uint32_t n
     if (r < nranks) first[r] = base[(uint64_t)r * ntiles];
     if (r == nranks) first[r] = *total;
 }
+// One-pass form (pcc_shard_route_bitmaps_hist).  The rank's own unit histogram
+// (the points per unit that pcc_shard_histogram / pcc_shard_slab_histogram counted
+// over the same points, computed anyway for the plan) gives every destination's
+// total, so its first position is known before a point is read; each 4096-point
+// tile then takes its offsets inside the destinations from its predecessors by
+// decoupled look-back (publish the tile's counts, walk back to the nearest
+// inclusive prefix) and scatters in index order as k_route_scatter does: one
+// read of the points instead of two.  Tiles are numbered by a ticket, so every
+// predecessor a tile waits for is already running.  A histogram that does not
+// match the points sets flag bit 2 (prefixes above a total, or the last tile's
+// prefix unequal to it) and no store leaves the send buffer.
+constexpr unsigned long long kLbAgg = 1ull << 62, kLbInc = 2ull << 62, kLbVal = (1ull << 62) - 1;
+
+__global__ __launch_bounds__(256) void k_route_dest_totals(const uint32_t* __restrict__ hist, uint32_t nunits,
+                                                           const uint32_t* __restrict__ owner, uint32_t nranks,
+                                                           unsigned long long* __restrict__ tot, uint32_t* flag) {
+    __shared__ unsigned long long s[64];
+    if (threadIdx.x < 64) s[threadIdx.x] = 0;
+    __syncthreads();
+    for (uint32_t u = blockIdx.x * 256u + threadIdx.x; u < nunits; u += gridDim.x * 256u) {
+        const uint32_t h = hist[u];
+        if (!h) continue;
+        const uint32_t o = owner[u];
+        if (o >= nranks) { atomicOr(flag, 1u); continue; }
+        atomicAdd(&s[o], (unsigned long long)h);
+    }
+    __syncthreads();
+    if (threadIdx.x < nranks && s[threadIdx.x]) atomicAdd(&tot[threadIdx.x], s[threadIdx.x]);
+}
+
+__global__ __launch_bounds__(kRtBS) void k_route_lb(const Point* __restrict__ in, uint32_t n, ShardGrid g, ShardSlabs m,
+                                                    const uint32_t* __restrict__ owner, uint32_t nranks, uint32_t ntiles,
+                                                    const unsigned long long* __restrict__ tot,
+                                                    unsigned long long* __restrict__ status, uint32_t* ticket,
+                                                    Point* __restrict__ out, unsigned long long* __restrict__ bm,
+                                                    uint32_t nwords, uint32_t* flag) {
+    __shared__ uint32_t run[64], cnt[64];
+    __shared__ uint32_t wc[2][kRtW][64];
+    __shared__ uint32_t s_tile;
+    const uint32_t tid = threadIdx.x, w = tid / 64, lane = tid & 63;
+    if (tid == 0) s_tile = atomicAdd(ticket, 1u);
+    if (tid < 64) cnt[tid] = 0;
+    __syncthreads();
+    const uint32_t tile = s_tile;
+    const float4* p4 = reinterpret_cast<const float4*>(in);
+    float4* o4 = reinterpret_cast<float4*>(out);
+    // pass 1 (registers): the tile's points, and per row the destination, wave
+    // rank and wave count (o | rk << 8 | pc << 16; o = 64: no point); bitmap words
+    float4 v[kRtIPT];
+    uint32_t meta[kRtIPT];
+    uint32_t bad = 0;
+#pragma unroll
+    for (int r = 0; r < kRtIPT; r++) {
+        const uint32_t i = tile * (uint32_t)kRtTile + (uint32_t)r * kRtBS + tid;
+        v[r] = p4[i < n ? i : n - 1];
+    }
+#pragma unroll
+    for (int r = 0; r < kRtIPT; r++) {
+        const uint32_t i = tile * (uint32_t)kRtTile + (uint32_t)r * kRtBS + tid;
+        const bool valid = i < n;
+        uint32_t o = 64;
+        if (valid) o = route_dest_rank(g, m, owner, nranks, v[r], bad);
+        const uint64_t peers = wave_peers<7>(o, valid);
+        const uint32_t rk = mask_rank(peers), pc = (uint32_t)__popcll(peers);
+        meta[r] = o | (rk << 8) | (pc << 16);
+        if (valid && rk == 0) {
+            atomicAdd(&cnt[o], pc);
+            bm[(uint64_t)o * nwords + (i >> 6)] = peers;   // the wave's 64 indices: one aligned word
+        }
+    }
+    if (bad) atomicOr(flag, 1u);
+    __syncthreads();
+    // look-back, one thread per destination
+    if (tid < nranks) {
+        const uint32_t c = cnt[tid];
+        unsigned long long* st = status + (uint64_t)tile * nranks + tid;
+        uint64_t excl = 0;
+        if (tile == 0) {
+            __hip_atomic_store(st, kLbInc | c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            __hip_atomic_store(st, kLbAgg | c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (uint32_t p = tile; p-- > 0;) {
+                const unsigned long long* sp = status + (uint64_t)p * nranks + tid;
+                unsigned long long sv;
+                while (((sv = __hip_atomic_load(sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 62) == 0)
+                    __builtin_amdgcn_s_sleep(1);
+                excl += sv & kLbVal;
+                if ((sv >> 62) == 2) break;
+            }
+            __hip_atomic_store(st, kLbInc | (excl + c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        uint64_t start = 0;
+        for (uint32_t q = 0; q < tid; q++) start += tot[q];
+        if (excl + c > tot[tid]) atomicOr(flag, 2u);                             // more points than counted
+        if (tile + 1 == ntiles && excl + c != tot[tid]) atomicOr(flag, 2u);   // fewer
+        run[tid] = (uint32_t)(start + excl);
+    }
+    // pass 2: scatter in index order (k_route_scatter's ranks, from the registers)
+    for (int r = 0; r < kRtIPT; r++) {
+        const uint32_t par = (uint32_t)r & 1u;
+        const uint32_t i = tile * (uint32_t)kRtTile + (uint32_t)r * kRtBS + tid;
+        const uint32_t o = meta[r] & 0xFFu, rk = (meta[r] >> 8) & 0xFFu;
+        const bool valid = i < n && o < nranks;
+        wc[par][w][lane] = 0;   // this wave's row (the other parity is still read by the run update)
+        __builtin_amdgcn_wave_barrier();
+        if (valid && rk == 0) wc[par][w][o] = meta[r] >> 16;
+        __syncthreads();
+        if (valid) {
+            uint32_t pos = run[o] + rk;
+            for (uint32_t q = 0; q < w; q++) pos += wc[par][q][o];
+            if (pos < n) o4[pos] = v[r];
+        }
+        __syncthreads();
+        if (tid < nranks) {
+            uint32_t t = 0;
+            for (uint32_t q = 0; q < (uint32_t)kRtW; q++) t += wc[par][q][tid];
+            run[tid] += t;
+        }
+    }
+}
+
 // Keys of received points from the senders' membership bitmaps (concatenated in
 // sender order): word popcounts, their exclusive scan (= the received rows'
 // positions), then every word writes the keys of its set bits in order.
@@ -5338,6 +5459,47 @@ int shard_route(const Point* d, uint64_t n, uint32_t key0, const ShardGrid& g, c
     HIP_CHECK(hipMemcpyAsync(&bad, S.flag, 4, hipMemcpyDeviceToHost, S.st));
     HIP_CHECK(hipStreamSynchronize(S.st));
     for (uint32_t r = 0; r < nranks; r++) counts[r] = n ? (uint64_t)(first[r + 1] - first[r]) : 0;
+    return bad ? -ERANGE : 0;
+}
+
+int shard_route_hist(const Point* d, uint64_t n, const ShardGrid& g, const uint32_t* downer, uint32_t nranks,
+                     const uint32_t* dhist, Point* dsend, uint64_t* dbm, uint64_t* counts, int device, uint32_t dim) {
+    ShardScratch& S = shard_scratch(device);
+    if (nranks == 0 || nranks > 64) return -EINVAL;
+    if (n >= (1ull << 32)) return -EOVERFLOW;
+    const uint64_t nunits = (uint64_t)g.dims[0] * g.dims[1] * g.dims[2] * (dim ? kL0Layers : 1u);
+    if (nunits >= (1ull << 32)) return -EOVERFLOW;
+    const uint32_t n32 = (uint32_t)n;
+    const uint32_t ntiles = (uint32_t)((n + kRtTile - 1) / kRtTile);
+    // status words (ntiles x nranks u64), the totals (64 u64) and the ticket, in u32 units
+    const uint64_t need = ((uint64_t)ntiles * nranks + 64 + 1) * 2;
+    if (S.cap < need) {
+        for (auto*& b : S.buf) { (void)hipFree(b); b = nullptr; HIP_CHECK(hipMalloc(&b, std::max<uint64_t>(need, 1) * 4)); }
+        S.cap = need;
+    }
+    unsigned long long* status = reinterpret_cast<unsigned long long*>(S.buf[0]);
+    unsigned long long* tot = status + (uint64_t)ntiles * nranks;
+    uint32_t* ticket = reinterpret_cast<uint32_t*>(tot + 64);
+    HIP_CHECK(hipMemsetAsync(S.buf[0], 0, need * 4, S.st));
+    HIP_CHECK(hipMemsetAsync(S.flag, 0, 4, S.st));
+    if (nunits)
+        k_route_dest_totals<<<(uint32_t)std::min<uint64_t>((nunits + 255) / 256, 1024), 256, 0, S.st>>>(
+            dhist, (uint32_t)nunits, downer, nranks, tot, S.flag);
+    if (n) {
+        const uint32_t nwords = (uint32_t)((n + 63) / 64);
+        HIP_CHECK(hipMemsetAsync(dbm, 0, (uint64_t)nranks * nwords * 8, S.st));
+        k_route_lb<<<ntiles, kRtBS, 0, S.st>>>(d, n32, g, shard_slabs(g, dim), downer, nranks, ntiles, tot, status,
+                                              ticket, dsend, reinterpret_cast<unsigned long long*>(dbm), nwords, S.flag);
+    }
+    HIP_CHECK(hipGetLastError());
+    unsigned long long ht[64];
+    uint32_t bad = 0;
+    HIP_CHECK(hipMemcpyAsync(ht, tot, nranks * 8, hipMemcpyDeviceToHost, S.st));
+    HIP_CHECK(hipMemcpyAsync(&bad, S.flag, 4, hipMemcpyDeviceToHost, S.st));
+    HIP_CHECK(hipStreamSynchronize(S.st));
+    uint64_t sum = 0;
+    for (uint32_t r = 0; r < nranks; r++) { counts[r] = ht[r]; sum += ht[r]; }
+    if ((bad & 2u) || sum != n) return -EBADMSG;
     return bad ? -ERANGE : 0;
 }
 

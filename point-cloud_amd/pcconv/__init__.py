@@ -37,7 +37,8 @@ EXPORTS = ["pcc_abi_version", "pcc_last_error", "pcc_options_default", "pcc_open
            "pcc_pending_cells", "pcc_export_pending", "pcc_shard_slab_histogram", "pcc_shard_route_slabs",
            "pcc_write_cell_view", "pcc_begin_file", "pcc_append_points", "pcc_end_file", "pcc_cancel_file",
            "pcc_set_summary", "pcc_write_cells", "pcc_write_metadata", "pcc_clear_input", "pcc_adopt_prior",
-           "pcc_open_subtrees", "pcc_visit_cells", "pcc_shard_route_bitmaps", "pcc_shard_keys_from_bitmaps",
+           "pcc_open_subtrees", "pcc_visit_cells", "pcc_shard_route_bitmaps", "pcc_shard_route_bitmaps_hist",
+           "pcc_shard_keys_from_bitmaps",
            "pcc_release_device_cache", "pcc_grid_cells", "pcc_export_grid", "pcc_shard_resolve_buckets", "pcc_shard_lpt",
            "pcc_shard_plan_search"]
 
@@ -157,6 +158,8 @@ def lib():
                                             C.c_uint32, vp, vp, C.POINTER(C.c_uint64), C.c_int]
         L.pcc_shard_route_bitmaps.argtypes = [vp, C.c_uint64, C.POINTER(ShardGrid), C.c_uint32, vp, C.c_uint32, vp,
                                               vp, C.POINTER(C.c_uint64), C.c_int]
+        L.pcc_shard_route_bitmaps_hist.argtypes = [vp, C.c_uint64, C.POINTER(ShardGrid), C.c_uint32, vp, C.c_uint32,
+                                                   vp, vp, vp, C.POINTER(C.c_uint64), C.c_int]
         L.pcc_shard_keys_from_bitmaps.argtypes = [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.c_uint32, vp,
                                                   C.c_uint64, C.c_int]
         L.pcc_write_cell_view.argtypes = [C.c_char_p, vp]
@@ -169,7 +172,7 @@ def lib():
         L.pcc_export_pending.argtypes = [vp, vp, vp, vp, vp, vp]
         L.pcc_shard_lpt.argtypes = [vp, C.c_uint64, C.c_uint32, vp, vp]
         L.pcc_shard_plan_search.argtypes = [vp, vp, vp, vp, vp, C.c_uint32, C.c_uint32, C.c_uint32,
-                                            C.POINTER(C.c_uint32), C.POINTER(C.c_double)]
+                                            C.POINTER(C.c_uint32), C.POINTER(C.c_double), vp, vp, vp, vp, vp]
         L.pcc_grid_cells.argtypes = [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         L.pcc_export_grid.argtypes = [vp, vp, vp, vp]
         L.pcc_shard_resolve_buckets.argtypes = [vp, vp, C.c_uint64, C.c_uint32, vp, vp, vp, C.c_uint64, C.c_uint32,
@@ -434,6 +437,17 @@ def shard_route_bitmaps(pts_ptr: int, n: int, grid: ShardGrid, sub_grid_dimensio
     return [int(c) for c in counts]
 
 
+def shard_route_bitmaps_hist(pts_ptr: int, n: int, grid: ShardGrid, sub_grid_dimension: int, owner_ptr: int,
+                             nranks: int, hist_ptr: int, send_ptr: int, bitmaps_ptr: int, device: int = 0):
+    """One-pass shard_route_bitmaps (pcc_shard_route_bitmaps_hist): hist_ptr =
+    this rank's points per unit (same units as the route) over the same points."""
+    counts = (C.c_uint64 * nranks)()
+    _check(lib().pcc_shard_route_bitmaps_hist(C.c_void_p(pts_ptr), n, C.byref(grid), sub_grid_dimension,
+                                              C.c_void_p(owner_ptr), nranks, C.c_void_p(hist_ptr),
+                                              C.c_void_p(send_ptr), C.c_void_p(bitmaps_ptr), counts, device))
+    return [int(c) for c in counts]
+
+
 def shard_keys_from_bitmaps(bitmaps_ptr: int, nwords, key0, keys_ptr: int, nkeys: int, device: int = 0):
     """Global keys of received points from the senders' bitmap rows (pcc_shard_keys_from_bitmaps)."""
     ns = len(nwords)
@@ -472,16 +486,22 @@ def shard_lpt(w, world: int):
     return own, load
 
 
-def shard_plan_search(whole_w, slab_off, slab_w, child_off, child_w, kmax: int, world: int):
-    """pcc_shard_plan_search: (best k, its estimate)."""
+def shard_plan_search(whole_w, slab_off, slab_w, child_off, child_w, kmax: int, world: int, owners: bool = False):
+    """pcc_shard_plan_search: (best k, its estimate), and with owners=True also
+    (whole-cell owners, slab owners, child owners, phase-1 loads, phase-2 loads)
+    of the best k's placement."""
     f = lambda a, t: np.ascontiguousarray(a, dtype=t).reshape(-1)
     ww, so, sw, co, cw = (f(whole_w, np.float64), f(slab_off, np.uint64), f(slab_w, np.float64),
                           f(child_off, np.uint64), f(child_w, np.float64))
     bk, bt = C.c_uint32(0), C.c_double(0.0)
-    _check(lib().pcc_shard_plan_search(ww.ctypes.data, so.ctypes.data, sw.ctypes.data if len(sw) else None,
-                                       co.ctypes.data, cw.ctypes.data if len(cw) else None, len(ww), kmax, world,
-                                       C.byref(bk), C.byref(bt)))
-    return bk.value, bt.value
+    out = None
+    if owners:
+        out = (np.zeros(len(ww), np.uint32), np.zeros(len(sw), np.uint32), np.zeros(len(cw), np.uint32),
+               np.zeros(world, np.float64), np.zeros(world, np.float64))
+    ptr = lambda a: a.ctypes.data if (a is not None and len(a)) else None
+    _check(lib().pcc_shard_plan_search(ww.ctypes.data, so.ctypes.data, ptr(sw), co.ctypes.data, ptr(cw), len(ww), kmax,
+                                       world, C.byref(bk), C.byref(bt), *(ptr(a) for a in (out or (None,) * 5))))
+    return (bk.value, bt.value) if not owners else (bk.value, bt.value) + out
 
 
 def write_cell_view(out_dir: str, view: "CellView"):

@@ -264,11 +264,13 @@ def plan_split(hist0: np.ndarray, hist1: np.ndarray | None, children: np.ndarray
         return no
     sh = np.asarray(slab_hist, dtype=np.int64).reshape(len(hist0), NL)
     order = nz[np.lexsort((nz, -hist0[nz]))]
-    # per candidate (heaviest first): its slabs (cell * NL + layer, non-empty
-    # layers ascending) and its non-empty level-1 children (octant order)
-    slabs = [c * NL + np.flatnonzero(sh[c]) for c in order]
+    kmax = min(len(order), 2 * world)
+    # per candidate that may be shared (the kmax heaviest): its slabs (cell * NL
+    # + layer, non-empty layers ascending) and its non-empty level-1 children
+    # (octant order)
+    slabs = [c * NL + np.flatnonzero(sh[c]) for c in order[:kmax]]
     kids = []
-    for c in order:
+    for c in order[:kmax]:
         q = children[c]
         q = q[q >= 0]
         kids.append(q[hist1[q] > 0])
@@ -279,16 +281,17 @@ def plan_split(hist0: np.ndarray, hist1: np.ndarray | None, children: np.ndarray
     # the search over k (C++, pcc_shard_plan_search): phase 1 = the whole cells
     # and the shared cells' level-0 slabs, phase 2 = the shared cells' level-1
     # sub-trees, both placed largest first
-    k, best_t = pcconv.shard_plan_search(whole_w[order].astype(np.float64), slab_off,
-                                         sh.reshape(-1)[sl_all] * L0_COST, child_off,
-                                         hist1[ch_all] * DEEP_COST * DEPTH, min(len(order), 2 * world), world)
+    # and the best k's placement, the LPT of its two lists
+    k, best_t, ow, osl, och, l1, l2 = pcconv.shard_plan_search(
+        whole_w[order].astype(np.float64), slab_off, sh.reshape(-1)[sl_all] * L0_COST, child_off,
+        hist1[ch_all] * DEEP_COST * DEPTH, kmax, world, owners=True)
+    if k == 0:
+        return no
     sp, whole = order[:k], order[k:]
     sl = sl_all[:int(slab_off[k])]
-    o1, l1 = _lpt(np.concatenate([whole_w[whole], sh.reshape(-1)[sl] * L0_COST]), world)
+    o1 = np.concatenate([ow[k:], osl[:len(sl)]])
     ch = ch_all[:int(child_off[k])]
-    o2, l2 = _lpt(hist1[ch] * DEEP_COST * DEPTH, world)
-    if len(sp) == 0:
-        return no
+    o2 = och[:len(ch)]
     owner0 = np.zeros(len(hist0), dtype=np.uint32)
     split = np.zeros(len(hist0), dtype=bool)
     split[sp] = True
@@ -683,16 +686,25 @@ class HipShardOps:
     # the exchange carries membership bitmaps instead of keys (route_bitmaps / keys_from_bitmaps)
     bitmap_keys = True
 
-    def route_bitmaps(self, pts: torch.Tensor, grid, table: torch.Tensor, nranks: int, slabs: bool):
+    def route_bitmaps(self, pts: torch.Tensor, grid, table: torch.Tensor, nranks: int, slabs: bool,
+                      hist: torch.Tensor | None = None):
         """(send, bitmaps (nranks, ceil(n/64)) int64, counts): pcc_shard_route_bitmaps
-        on cell units (table = owner per cell) or slab units (table per slab)."""
+        on cell units (table = owner per cell) or slab units (table per slab).
+        hist: this rank's points per unit of the same kind (the local histogram
+        the plan was made from) -> the one-pass form, pcc_shard_route_bitmaps_hist."""
         n = pts.shape[0]
         send = torch.empty_like(pts)
         bm = torch.empty((nranks, (n + 63) // 64), dtype=torch.int64, device=pts.device)
-        self._ready()
+        if hist is not None:
+            hist = hist.to(device=pts.device, dtype=torch.int32).contiguous()
+        self._ready()   # after every torch op on the inputs
         dim = int(self.cfg_full()["sub_grid_dimension"]) if slabs else 0
-        counts = pcconv.shard_route_bitmaps(pts.data_ptr(), n, grid, dim, table.data_ptr(), nranks, send.data_ptr(),
-                                            bm.data_ptr(), self.dev)
+        if hist is not None:
+            counts = pcconv.shard_route_bitmaps_hist(pts.data_ptr(), n, grid, dim, table.data_ptr(), nranks,
+                                                     hist.data_ptr(), send.data_ptr(), bm.data_ptr(), self.dev)
+        else:
+            counts = pcconv.shard_route_bitmaps(pts.data_ptr(), n, grid, dim, table.data_ptr(), nranks,
+                                                send.data_ptr(), bm.data_ptr(), self.dev)
         return send, bm, counts
 
     def keys_from_bitmaps(self, bm: torch.Tensor, nwords, key0, nkeys: int) -> torch.Tensor:
@@ -947,6 +959,7 @@ def shard_build(comm, ops, pts: torch.Tensor, key0: int, file_points, write: boo
             grid1 = None
         if grid1 is not None:
             sh = ops.slab_histogram(pts, grid)
+            lhist = {"slab": sh}   # this rank's own counts: the one-pass route's totals
             sh_h = comm.allreduce_(sh.to(comm.device).to(torch.int64), "sum").cpu().numpy()
             mark("hist")
             hist_h = sh_h.reshape(-1, NL).sum(axis=1)
@@ -962,6 +975,7 @@ def shard_build(comm, ops, pts: torch.Tensor, key0: int, file_points, write: boo
                 plan = plan_split(hist_h, hist1_h, ch, W, slab_hist=sh_h)
         else:
             hist = ops.histogram(pts, grid)
+            lhist = {"cell": hist}
             hist_h = comm.allreduce_(hist.to(comm.device).to(torch.int64), "sum").cpu().numpy()
             mark("hist")
             plan = plan_split(hist_h, None, None, W, allow=False)
@@ -981,7 +995,13 @@ def shard_build(comm, ops, pts: torch.Tensor, key0: int, file_points, write: boo
             # of a 4-B key each; every receiver rebuilds its keys in rank order
             nd = 2 * W if nsplit else W
             tab = torch.from_numpy((route_table(plan, W) if nsplit else owner_h).astype(np.int32)).to(dev)
-            send, bm, counts = ops.route_bitmaps(pts, grid, tab, nd, nsplit)
+            if nsplit:
+                lh = lhist.get("slab")
+            else:
+                lh = lhist.get("cell")
+                if lh is None:   # cells from the slab histogram
+                    lh = lhist["slab"].view(-1, NL).sum(dim=1)
+            send, bm, counts = ops.route_bitmaps(pts, grid, tab, nd, nsplit, hist=lh)
             mark("route")
             nwl = int(bm.shape[1])
             rw = comm.alltoall_counts([nwl] * W)

@@ -95,12 +95,27 @@ def worker(rank, world, port, args, res_dir):
         pcconv.synth_device(pts.data_ptr(), a, b - a, args.seed, args.kind, -1000.0, 2000.0, 0)
         torch.cuda.synchronize()
         ops = RecOps(HipShardOps(0, batch_size=10_000))
+        # the host-only pieces of the plan and assembly stages, recorded too so
+        # they can be timed alone (measured inside the step they include waits
+        # for a GPU the other ranks share)
+        import pcconv.dist as D
+        host_calls = []
+        HOST = {"plan_split": "plan", "children_ids": "plan", "route_table": "plan"}
+
+        def hrec(stage, fn):
+            def f(*fa, **fk):
+                host_calls.append((stage, fn, fa, fk))
+                return fn(*fa, **fk)
+            return f
+        for name, stage in HOST.items():
+            setattr(D, name, hrec(stage, getattr(D, name)))
         comm = TimedComm(TorchComm(torch.device("cpu")))
         files = [args.points]
         for _ in range(args.warmup):
             shard_build(comm, ops, pts, a, files)
         dist.barrier()
         ops.calls = []
+        host_calls.clear()
         r = shard_build(comm, ops, pts, a, files, sync=torch.cuda.synchronize)
         # the same step again, this rank's build stages alone on the GPU: every
         # rank runs the step, but a rank's local builds wait for their turn
@@ -119,6 +134,14 @@ def worker(rank, world, port, args, res_dir):
                         t = (time.perf_counter() - t0) * 1e3
                         best = t if best is None else min(best, t)
                     alone["dev_" + stage] = alone.get("dev_" + stage, 0.0) + best
+                for stage, fn, fa, fk in host_calls:   # the recorded host-only calls (best of 3)
+                    best = None
+                    for _ in range(3):
+                        t0 = time.perf_counter()
+                        fn(*fa, **fk)
+                        t = (time.perf_counter() - t0) * 1e3
+                        best = t if best is None else min(best, t)
+                    alone["host_" + stage] = alone.get("host_" + stage, 0.0) + best
                 for name, fn, name_in in (("build", ops.build, "build"), ("lead", ops.lead_build_raw, "lead"),
                                           ("subtrees", ops.sub_build, "sub")):
                     if name_in not in li:
@@ -177,7 +200,13 @@ def main():
         # summary) as measured; the exchange stages' local part is gloo's host
         # staging (device <-> host copies), absent with RCCL, and left out
         dev = {k[4:]: v for k, v in r["alone"].items() if k.startswith("dev_") and k != "dev_exchange"}
-        host = {k: local.get(k, 0.0) for k in ("plan", "assemble", "summary")}
+        # plan: its host calls timed alone (plan_split, children_ids,
+        # route_table: the stage's work, the rest is a few numpy lookups);
+        # assembly (with its segment bookkeeping) and summary as measured in
+        # the step, whose sync points may wait for the other ranks' kernels
+        host = {"plan": r["alone"].get("host_plan", local.get("plan", 0.0)),
+                "assemble": local.get("assemble", 0.0), "summary": local.get("summary", 0.0)}
+        r["host_stage_ms_in_step"] = {k: local.get(k, 0.0) for k in ("plan", "assemble", "summary")}
         nb = sum(dev.values()) + sum(host.values()) + r["alone"].get("dev_exchange", 0.0)
         r["non_build_device_alone_ms"] = dev
         r["non_build_host_ms"] = host
@@ -186,7 +215,8 @@ def main():
     print(json.dumps({"config": args.config, "world": args.world, "points": args.points,
                       "note": "one process per rank on ONE MI355X; collectives over gloo (host), not RCCL/xGMI, "
                               "timed apart (<stage>_comm); 'alone' = the rank's builds and bucket resolution "
-                              "re-run (best of 2) while the other ranks wait",
+                              "re-run (best of 2) while the other ranks wait; the plan's host calls timed "
+                              "alone too (best of 3)",
                       "ranks": ranks}))
 
 

@@ -147,7 +147,7 @@ class NumpyShardOps:
     # a test may set it False to run the keyed exchange
     bitmap_keys = True
 
-    def route_bitmaps(self, pts, grid, table, nranks, slabs):
+    def route_bitmaps(self, pts, grid, table, nranks, slabs, hist=None):
         """numpy restatement of pcc_shard_route_bitmaps: stable partition by
         destination plus a (nranks, ceil(n/64)) int64 membership bitmap."""
         p = as_points(pts)

@@ -141,6 +141,46 @@ def test_route_bitmaps_and_key_rebuild_match_numpy(slabs, world):
             HipShardOps.keys_from_bitmaps(ops, cat, nw, key0, nk + 1)
 
 
+@pytest.mark.parametrize("slabs,world,n", [(False, 2, 1), (False, 8, 4096), (False, 8, 1_000_003),
+                                           (True, 16, 300_007), (True, 64, 2_500_001)])
+def test_route_bitmaps_one_pass_matches_two_pass(slabs, world, n):
+    """pcc_shard_route_bitmaps_hist (histogram totals + decoupled look-back
+    between tiles, one read of the points) == pcc_shard_route_bitmaps and the
+    numpy restatement: points in order, counts, every bitmap word; a histogram
+    of other points is rejected."""
+    ref = NumpyShardOps("/nonexistent")
+    sp = synth(41 + world, 1 + int(slabs), n, lo=-2500.0, ext=5000.0)
+    pts = as_tensor(sp).to(DEV)
+    gmin, gmax = ref.bbox(as_tensor(sp))
+    g = pcconv.shard_grid_from_bbox(gmin, gmax)
+    dim = int(ref.cfg_full()["sub_grid_dimension"])
+    nu = g.ncells * (pcconv.SHARD_LAYERS if slabs else 1)
+    table = torch.from_numpy((np.arange(nu) * 13 % world).astype(np.int32))
+    td = table.to(DEV)
+    h = torch.empty(nu, dtype=torch.int32, device=DEV)
+    torch.cuda.synchronize()
+    if slabs:
+        pcconv.shard_slab_histogram(pts.data_ptr(), n, g, dim, h.data_ptr())
+    else:
+        pcconv.shard_histogram(pts.data_ptr(), n, g, h.data_ptr())
+    ops = HipShardOps.__new__(HipShardOps)
+    ops.dev, ops.cfg = 0, {}
+    s1, b1, c1 = ops.route_bitmaps(pts, g, td, world, slabs, hist=h)
+    s2, b2, c2 = ops.route_bitmaps(pts, g, td, world, slabs)
+    assert c1 == c2 and sum(c1) == n
+    assert torch.equal(s1, s2)
+    assert torch.equal(b1, b2)
+    if n < 400_000:
+        s3, b3, c3 = ref.route_bitmaps(as_tensor(sp), g, table, world, slabs)
+        assert c1 == c3
+        assert torch.equal(s1.cpu(), s3)
+        assert torch.equal(b1.cpu(), b3)
+    hb = h.clone()
+    hb[int(torch.argmax(hb))] -= 1   # one point missing from the histogram
+    with pytest.raises(pcconv.PccError):
+        ops.route_bitmaps(pts, g, td, world, slabs, hist=hb)
+
+
 @pytest.mark.parametrize("limit,batch", [(50, 7), (64, 64), (1, 1000), (300, 13)])
 def test_device_bucket_resolution_matches_numpy(limit, batch):
     """pcc_shard_resolve_buckets (HipShardOps.resolve_level1) == the numpy
