@@ -717,6 +717,8 @@ __global__ __launch_bounds__(256) void k_bbox_final(float* part, uint32_t nb) {
 struct L0Params {
     float cs, cr, csc, crc;   // level 0 and level 1 cell size / hex radius
     float inv_cs, inv_cr;     // reciprocals for the fast floor/trunc quotients
+    float inv_csc, inv_crc;
+    int32_t exact;            // a divisor outside div_rc's range: IEEE divisions only
     int32_t lo[3];
     int32_t g[3];
     int32_t nl;
@@ -755,14 +757,53 @@ __device__ __forceinline__ int64_t l0_layer(const L0Params& P, float z, int32_t&
     const int32_t t = sat_i32(z / P.cr);   // hex.rs:83 z slot (truncation)
     return (int64_t)t - ((int64_t)P.dim2 * iz - 2);
 }
+// The same quotients from the correctly rounded reciprocals (div_rc: the IEEE
+// quotient for operands 0 or in [2^-60, 2^60]); `amb` flags a lane whose
+// operand is outside that range or a level whose divisors are, and the caller
+// redoes such lanes with l0_layer / l0_dense / l0_dense_dest behind one ballot.
+#ifndef PCC_L0_RC
+#define PCC_L0_RC 1
+#endif
+__device__ __forceinline__ int64_t l0_layer_rc(const L0Params& P, float z, int32_t& iz, bool& amb) {
+    amb |= P.exact || !rc_ok(z);
+    iz = sat_i32(floorf(div_rc(z, P.cs, P.inv_cs)));
+    const int32_t t = sat_i32(truncf(div_rc(z, P.cr, P.inv_cr)));
+    return (int64_t)t - ((int64_t)P.dim2 * iz - 2);
+}
+// the layer digit of pass 0 / pass 1 (exact either way)
+__device__ __forceinline__ int64_t l0_layer_any(const L0Params& P, float z, int32_t& iz) {
+    if (!PCC_L0_RC) return l0_layer(P, z, iz);
+    bool amb = false;
+    int64_t ll = l0_layer_rc(P, z, iz, amb);
+    if (__ballot(amb)) {
+        if (amb) ll = l0_layer(P, z, iz);
+    }
+    return ll;
+}
 // HASHED: -1 = decided by P.hashed at run time, 0 / 1 = known at compile time
 // (the pipelined downsweep must not carry the hash probe loop: its waits would
 // drain the prefetched tile)
 template <int HASHED = -1>
 __device__ __forceinline__ int64_t l0_dense(const L0Params& P, float x, float y, float z) {
-    int32_t iz;
-    const int64_t ll = l0_layer(P, z, iz);
-    int32_t ix = cell_index1(x, P.cs), iy = cell_index1(y, P.cs);
+    int32_t iz, ix, iy;
+    int64_t ll;
+    if (HASHED == 0 && PCC_L0_RC) {   // reciprocal quotients, exact lanes redone below
+        bool amb = !rc_ok(x) || !rc_ok(y);
+        ll = l0_layer_rc(P, z, iz, amb);
+        ix = sat_i32(floorf(div_rc(x, P.cs, P.inv_cs)));
+        iy = sat_i32(floorf(div_rc(y, P.cs, P.inv_cs)));
+        if (__ballot(amb)) {
+            if (amb) {
+                ll = l0_layer(P, z, iz);
+                ix = cell_index1(x, P.cs);
+                iy = cell_index1(y, P.cs);
+            }
+        }
+    } else {
+        ll = l0_layer(P, z, iz);
+        ix = cell_index1(x, P.cs);
+        iy = cell_index1(y, P.cs);
+    }
     int32_t gx = ix - P.lo[0], gy = iy - P.lo[1], gz = iz - P.lo[2];
     if (gx < 0 || gy < 0 || gz < 0 || gx >= P.g[0] || gy >= P.g[1] || gz >= P.g[2] || ll < 0 || ll >= P.nl) return -1;
     if (HASHED == 1 || (HASHED == -1 && P.hashed)) {
@@ -857,7 +898,7 @@ __global__ __launch_bounds__(kL0BS) void k_l0_up0g(const Point* __restrict__ in,
                 mn[0] = fminf(mn[0], v[u].x); mn[1] = fminf(mn[1], v[u].y); mn[2] = fminf(mn[2], v[u].z);
                 mx[0] = fmaxf(mx[0], v[u].x); mx[1] = fmaxf(mx[1], v[u].y); mx[2] = fmaxf(mx[2], v[u].z);
                 int32_t iz;
-                d6 = (uint32_t)l0_layer(P, v[u].z, iz) & (R - 1);
+                d6 = (uint32_t)l0_layer_any(P, v[u].z, iz) & (R - 1);
             }
             const uint64_t peers = wave_peers<6>(d6, valid);   // one LDS add per distinct digit of the wave
             if (valid && mask_rank(peers) == 0) atomicAdd(&dh[d6], (uint32_t)__popcll(peers));
@@ -1292,7 +1333,7 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_down6g(const Point* __restrict_
                 atomicAdd(&h[d6 * HP + (((uint32_t)d >> 6) & (R5 - 1))], 1u);
             } else if (valid) {   // the digit alone (a later pass checks the grid)
                 int32_t iz;
-                d6 = (uint32_t)l0_layer(P, v[r].z, iz) & (R - 1);
+                d6 = (uint32_t)l0_layer_any(P, v[r].z, iz) & (R - 1);
             }
             const uint64_t same = wave_peers<6>(d6, valid);
             const uint32_t rw = (uint32_t)__popcll(same & lt);
@@ -1404,8 +1445,23 @@ __global__ __launch_bounds__(1024) void k_l0_gprefix(uint32_t* __restrict__ gcnt
 // the point's child slab among the slab's 24 (octant * 3 + layer select, as
 // k_l0_dcap_from1 numbers them); -1 outside the grid.
 __device__ __forceinline__ int64_t l0_dense_dest(const L0Params& P, float x, float y, float z, uint32_t& dest) {
-    const int32_t ix1 = cell_index1(x, P.csc), iy1 = cell_index1(y, P.csc), iz1 = cell_index1(z, P.csc);
-    const int32_t u1 = sat_i32(z / P.crc);
+    int32_t ix1, iy1, iz1, u1;
+    bool amb = !PCC_L0_RC;
+    if (PCC_L0_RC) {   // reciprocal quotients, exact lanes redone below
+        amb = P.exact || !rc_ok(x) || !rc_ok(y) || !rc_ok(z);
+        ix1 = sat_i32(floorf(div_rc(x, P.csc, P.inv_csc)));
+        iy1 = sat_i32(floorf(div_rc(y, P.csc, P.inv_csc)));
+        iz1 = sat_i32(floorf(div_rc(z, P.csc, P.inv_csc)));
+        u1 = sat_i32(truncf(div_rc(z, P.crc, P.inv_crc)));
+    }
+    if (__ballot(amb)) {
+        if (amb) {
+            ix1 = cell_index1(x, P.csc);
+            iy1 = cell_index1(y, P.csc);
+            iz1 = cell_index1(z, P.csc);
+            u1 = sat_i32(z / P.crc);
+        }
+    }
     const int32_t iz0 = iz1 >> 1, t0 = u1 / 2;
     const int32_t gx0 = (ix1 >> 1) - P.lo[0], gy0 = (iy1 >> 1) - P.lo[1], gz0 = iz0 - P.lo[2];
     const int64_t ll0 = (int64_t)t0 - ((int64_t)P.dim2 * iz0 - 2);
@@ -3868,6 +3924,11 @@ int Engine::level0_bin() {
     P.crc = hex_radius(sub_cell_size(csc, dim));
     P.inv_cs = 1.0f / P.cs;
     P.inv_cr = 1.0f / P.cr;
+    P.inv_csc = 1.0f / P.csc;
+    P.inv_crc = 1.0f / P.crc;
+    P.exact = 0;
+    for (float v : {P.cs, P.cr, P.csc, P.crc})   // div_rc's divisor range
+        if (!(std::fabs(v) >= 0x1p-60f && std::fabs(v) <= 0x1p60f)) P.exact = 1;
     const SlabGeom g = slab_geom(dim);
     P.nl = g.nl;
     P.dim2 = 2 * (int32_t)dim;
