@@ -875,12 +875,13 @@ constexpr uint32_t kL0DownGrid = 512;   // persistent blocks of the fused upswee
 __global__ __launch_bounds__(kL0BS) void k_l0_up0g(const Point* __restrict__ in, uint64_t n, L0Params P, uint32_t tpg,
                                                    uint32_t ngroups, uint32_t* __restrict__ gcnt0, float* part,
                                                    uint32_t* flag) {
-    constexpr int R = 1 << 6, U = 4;
-    __shared__ uint32_t dh[R];
+    constexpr int R = 1 << 6, U = 4, NWV = kL0BS / 64;
+    __shared__ uint32_t dh[NWV][R];   // per wave: one LDS add per point, no ranks
     __shared__ float sb[kL0BS / 64][6];
     const float4* p4 = reinterpret_cast<const float4*>(in);
-    if (threadIdx.x < (uint32_t)R) dh[threadIdx.x] = 0;
+    for (uint32_t i = threadIdx.x; i < NWV * R; i += kL0BS) (&dh[0][0])[i] = 0;
     __syncthreads();
+    const uint32_t wv = threadIdx.x / 64;
     float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
     bool bad = false;
     const uint64_t lo = (uint64_t)blockIdx.x * tpg * kL0Tile;
@@ -900,8 +901,7 @@ __global__ __launch_bounds__(kL0BS) void k_l0_up0g(const Point* __restrict__ in,
                 int32_t iz;
                 d6 = (uint32_t)l0_layer_any(P, v[u].z, iz) & (R - 1);
             }
-            const uint64_t peers = wave_peers<6>(d6, valid);   // one LDS add per distinct digit of the wave
-            if (valid && mask_rank(peers) == 0) atomicAdd(&dh[d6], (uint32_t)__popcll(peers));
+            if (valid) atomicAdd(&dh[wv][d6], 1u);
         }
     }
     for (int d = 32; d > 0; d >>= 1)
@@ -919,7 +919,11 @@ __global__ __launch_bounds__(kL0BS) void k_l0_up0g(const Point* __restrict__ in,
         for (int q = 1; q < kL0BS / 64; q++) r = threadIdx.x < 3 ? fminf(r, sb[q][threadIdx.x]) : fmaxf(r, sb[q][threadIdx.x]);
         part[blockIdx.x * 6 + threadIdx.x] = r;
     }
-    if (threadIdx.x < (uint32_t)R) gcnt0[(uint64_t)threadIdx.x * ngroups + blockIdx.x] = dh[threadIdx.x];
+    if (threadIdx.x < (uint32_t)R) {
+        uint32_t c = 0;
+        for (int q = 0; q < NWV; q++) c += dh[q][threadIdx.x];
+        gcnt0[(uint64_t)threadIdx.x * ngroups + blockIdx.x] = c;
+    }
 }
 
 // Pass-1 upsweep from the arena: per-tile digit histogram + the full dense-slab
