@@ -775,10 +775,10 @@ bool read_las(const std::string& path, LasResult& out, std::string& err, const P
         }
         if (!found) return bad("compressed point data without a LASzip VLR");
         std::string e;
-        const bool supported = fmt <= 3 || (fmt >= 6 && fmt <= 8);   // formats 4, 5, 9, 10: wave packets
+        const bool supported = fmt <= 10;
         if (!supported || !lz.open(f, data_off, n, rec, lv, e)) {
             out.laz_error = path + ": " + (!supported ? "LAZ point format " + std::to_string(fmt) +
-                                                            " (wave packets) is not supported" : e);
+                                                            " is not supported" : e);
             fclose(f);
             return true;
         }

@@ -815,6 +815,121 @@ struct Bytes : ItemCodec {
     }
 };
 
+// LASwavepacket13 (29 bytes): descriptor index (u8), then byte offset to the
+// waveform data (u64), packet size (u32), return point location and x(t),
+// y(t), z(t) (f32, coded as their bit patterns).  WAVEPACKET13 v1, the only
+// version LASzip has (point formats 4 / 5 of pointwise-chunked files): the
+// index as a symbol; the offset as "same", "previous offset + previous size",
+// a 32-bit difference (integer compressor, predicted from the last such
+// difference) or a raw 64-bit value, the choice coded with a model selected by
+// the previous choice; every other field by an integer compressor from the
+// previous point (x, y, z sharing one with three contexts).
+struct Wave {
+    uint64_t offset;
+    uint32_t size;
+    int32_t ret, x, y, z;
+};
+inline Wave wave_unpack(const uint8_t* p) {   // the 28 bytes after the index
+    Wave w;
+    memcpy(&w.offset, p, 8);
+    memcpy(&w.size, p + 8, 4);
+    memcpy(&w.ret, p + 12, 4);
+    memcpy(&w.x, p + 16, 4);
+    memcpy(&w.y, p + 20, 4);
+    memcpy(&w.z, p + 24, 4);
+    return w;
+}
+inline void wave_pack(const Wave& w, uint8_t* p) {
+    memcpy(p, &w.offset, 8);
+    memcpy(p + 8, &w.size, 4);
+    memcpy(p + 12, &w.ret, 4);
+    memcpy(p + 16, &w.x, 4);
+    memcpy(p + 20, &w.y, 4);
+    memcpy(p + 24, &w.z, 4);
+}
+struct WaveModels {
+    SymbolModel m_index;
+    std::vector<SymbolModel> m_offset;   // by the previous offset code
+    IntegerCompressor ic_offset, ic_size, ic_ret, ic_xyz;
+    int32_t last_diff = 0;
+    uint32_t last_sym = 0;
+    uint8_t last[29];
+    WaveModels(bool e, const uint8_t* item)
+        : m_index(256, e), ic_offset(e, 32, 1), ic_size(e, 32, 1), ic_ret(e, 32, 1), ic_xyz(e, 32, 3) {
+        for (int i = 0; i < 4; i++) m_offset.emplace_back(4, e);
+        init(item);
+    }
+    void init(const uint8_t* item) {
+        m_index.init();
+        for (auto& m : m_offset) m.init();
+        ic_offset.init();
+        ic_size.init();
+        ic_ret.init();
+        ic_xyz.init();
+        last_diff = 0;
+        last_sym = 0;
+        memcpy(last, item, 29);
+    }
+    void read(Decoder& d, uint8_t* item) {
+        item[0] = (uint8_t)d.symbol(m_index);
+        const Wave lw = wave_unpack(last + 1);
+        Wave w;
+        last_sym = d.symbol(m_offset[last_sym]);
+        if (last_sym == 0) {
+            w.offset = lw.offset;
+        } else if (last_sym == 1) {
+            w.offset = lw.offset + lw.size;
+        } else if (last_sym == 2) {
+            last_diff = ic_offset.decompress(d, last_diff, 0);
+            w.offset = lw.offset + (uint64_t)(int64_t)last_diff;
+        } else {
+            const uint64_t lo = d.int32();
+            const uint64_t hi = d.int32();
+            w.offset = (hi << 32) | lo;
+        }
+        w.size = (uint32_t)ic_size.decompress(d, (int32_t)lw.size, 0);
+        w.ret = ic_ret.decompress(d, lw.ret, 0);
+        w.x = ic_xyz.decompress(d, lw.x, 0);
+        w.y = ic_xyz.decompress(d, lw.y, 1);
+        w.z = ic_xyz.decompress(d, lw.z, 2);
+        wave_pack(w, item + 1);
+        memcpy(last, item, 29);
+    }
+    void write(Encoder& e, const uint8_t* item) {
+        e.symbol(m_index, item[0]);
+        const Wave lw = wave_unpack(last + 1), w = wave_unpack(item + 1);
+        const int64_t d64 = (int64_t)(w.offset - lw.offset);
+        const int32_t d32 = (int32_t)d64;
+        uint32_t sym;
+        if (d64 == (int64_t)d32) sym = d32 == 0 ? 0u : (d32 == (int32_t)lw.size ? 1u : 2u);
+        else sym = 3;
+        e.symbol(m_offset[last_sym], sym);
+        last_sym = sym;
+        if (sym == 2) {
+            ic_offset.compress(e, last_diff, d32, 0);
+            last_diff = d32;
+        } else if (sym == 3) {
+            e.int32((uint32_t)w.offset);
+            e.int32((uint32_t)(w.offset >> 32));
+        }
+        ic_size.compress(e, (int32_t)lw.size, (int32_t)w.size, 0);
+        ic_ret.compress(e, lw.ret, w.ret, 0);
+        ic_xyz.compress(e, lw.x, w.x, 0);
+        ic_xyz.compress(e, lw.y, w.y, 1);
+        ic_xyz.compress(e, lw.z, w.z, 2);
+        memcpy(last, item, 29);
+    }
+};
+
+struct Wave13 : ItemCodec {
+    WaveModels M;
+    explicit Wave13(bool e) : M(e, kZero29) {}
+    static constexpr uint8_t kZero29[29] = {};
+    void init(const uint8_t* item) override { M.init(item); }
+    void read(Decoder& d, uint8_t* item) override { M.read(d, item); }
+    void write(Encoder& e, const uint8_t* item) override { M.write(e, item); }
+};
+
 // ------------------------------------------------------------------ LASzip 3 layered items
 // Point formats 6-8 (LAS 1.4): POINT14 v3, RGB14 v3, RGBNIR14 v3, BYTE14 v3 in
 // "layered chunked" compression.  Every field group is its own arithmetic
@@ -1395,6 +1510,50 @@ struct Bytes14 : LayeredItem {
     }
 };
 
+// WAVEPACKET14 v3 (point formats 9 / 10): one layer, the WAVEPACKET13 model
+// per scanner-channel context (a new context starts from the previous
+// context's last packet); an empty layer keeps the chunk's first packet.
+struct Wave14 : LayeredItem {
+    bool enc;
+    std::unique_ptr<WaveModels> C[4];
+    uint32_t cur = 0;
+    LayerSet L;
+    explicit Wave14(bool e) : enc(e), L(1) {}
+    uint32_t layers() const override { return 1; }
+    bool overrun() const override { return L.overrun(); }
+    void start(const uint8_t* item, uint32_t ctx) {
+        for (auto& c : C) c.reset();
+        cur = ctx;
+        C[cur].reset(new WaveModels(enc, item));
+    }
+    void init_dec(const uint8_t* item, uint32_t& ctx, const uint8_t* const* lp, const uint32_t* ln) override {
+        start(item, ctx);
+        L.init_dec(lp, ln);
+    }
+    void init_enc(const uint8_t* item, uint32_t& ctx) override {
+        start(item, ctx);
+        L.init_enc();
+    }
+    void finish(std::vector<std::vector<uint8_t>>& out) override { L.finish(out, false); }
+    WaveModels* switch_to(uint32_t ctx) {
+        if (ctx != cur) {
+            if (!C[ctx]) C[ctx].reset(new WaveModels(enc, C[cur]->last));
+            cur = ctx;
+        }
+        return C[cur].get();
+    }
+    void read(uint8_t* item, uint32_t& ctx) override {
+        WaveModels* c = switch_to(ctx);
+        if (L.present[0]) c->read(L.dec[0], item);
+        else memcpy(item, c->last, 29);
+    }
+    void write(const uint8_t* item, uint32_t& ctx) override {
+        WaveModels* c = switch_to(ctx);
+        if (memcmp(item, c->last, 29) != 0) L.changed[0] = true;
+        c->write(L.enc[0], item);
+    }
+};
+
 bool is_layered(const std::vector<Item>& items) { return !items.empty() && items[0].type == POINT14; }
 
 bool make_layered(const std::vector<Item>& items, bool enc, std::vector<std::unique_ptr<LayeredItem>>& out,
@@ -1410,6 +1569,7 @@ bool make_layered(const std::vector<Item>& items, bool enc, std::vector<std::uni
         else if (i > 0 && it.type == RGB14 && it.size == 6) out.emplace_back(new Rgb14(enc, false));
         else if (i > 0 && it.type == RGBNIR14 && it.size == 8) out.emplace_back(new Rgb14(enc, true));
         else if (i > 0 && it.type == BYTE14 && it.size >= 1) out.emplace_back(new Bytes14(enc, it.size));
+        else if (i > 0 && it.type == WAVEPACKET14 && it.size == 29) out.emplace_back(new Wave14(enc));
         else {
             err = "LAZ item type " + std::to_string(it.type) + " (size " + std::to_string(it.size) +
                   ") is not supported in layered compression";
@@ -1427,6 +1587,7 @@ bool make_codecs(const std::vector<Item>& items, bool enc, std::vector<std::uniq
         else if (it.type == GPSTIME11 && it.size == 8 && it.version == 2) out.emplace_back(new Gps11(enc));
         else if (it.type == RGB12 && it.size == 6 && it.version == 2) out.emplace_back(new Rgb12(enc));
         else if (it.type == BYTE && it.size >= 1 && it.version == 2) out.emplace_back(new Bytes(enc, it.size));
+        else if (it.type == WAVEPACKET13 && it.size == 29 && it.version == 1) out.emplace_back(new Wave13(enc));
         else {
             err = "LAZ item type " + std::to_string(it.type) + " version " + std::to_string(it.version) +
                   (it.type >= POINT14 ? " (point formats 6-10, layered compression)" : "") + " is not supported";
@@ -1496,8 +1657,8 @@ std::vector<uint8_t> write_vlr(const Vlr& v) {
 uint16_t compressor_for_format(uint8_t format) { return format >= 6 ? 3 : 2; }
 
 bool items_for_format(uint8_t format, uint16_t rec, std::vector<Item>& items, std::string& err) {
-    static const uint16_t base[9] = {20, 28, 26, 34, 0, 0, 30, 36, 38};
-    if (format > 8 || base[format] == 0) {
+    static const uint16_t base[11] = {20, 28, 26, 34, 57, 63, 30, 36, 38, 59, 67};
+    if (format > 10) {
         err = "LAZ point format " + std::to_string(format) + " is not supported";
         return false;
     }
@@ -1506,13 +1667,15 @@ bool items_for_format(uint8_t format, uint16_t rec, std::vector<Item>& items, st
     if (format >= 6) {
         items.push_back({POINT14, 30, 3});
         if (format == 7) items.push_back({RGB14, 6, 3});
-        if (format == 8) items.push_back({RGBNIR14, 8, 3});
+        if (format == 8 || format == 10) items.push_back({RGBNIR14, 8, 3});
+        if (format >= 9) items.push_back({WAVEPACKET14, 29, 3});
         if (rec > base[format]) items.push_back({BYTE14, (uint16_t)(rec - base[format]), 3});
         return true;
     }
     items.push_back({POINT10, 20, 2});
-    if (format == 1 || format == 3) items.push_back({GPSTIME11, 8, 2});
-    if (format == 2 || format == 3) items.push_back({RGB12, 6, 2});
+    if (format == 1 || format == 3 || format == 4 || format == 5) items.push_back({GPSTIME11, 8, 2});
+    if (format == 2 || format == 3 || format == 5) items.push_back({RGB12, 6, 2});
+    if (format == 4 || format == 5) items.push_back({WAVEPACKET13, 29, 1});   // LASzip has no version 2
     if (rec > base[format]) items.push_back({BYTE, (uint16_t)(rec - base[format]), 2});
     return true;
 }

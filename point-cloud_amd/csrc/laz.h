@@ -4,12 +4,12 @@
 // Restated from the published LASzip format (the format of laz-perf / laszip /
 // laz-rs): an adaptive binary arithmetic coder (Amir Said's FastAC model as
 // LASzip uses it), integer compressors with k-bit correctors, and
-//   point formats 0-3: "pointwise chunked" compression with the version-2
-//     item compressors POINT10, GPSTIME11, RGB12 and BYTE;
-//   point formats 6-8: LASzip 3 "layered chunked" compression with the
-//     version-3 items POINT14, RGB14, RGBNIR14 and BYTE14 (one arithmetic
-//     stream per field group, models per scanner channel).
-// Formats 4, 5, 9 and 10 (wave packets) are reported as unsupported.
+//   point formats 0-5: "pointwise chunked" compression with the version-2
+//     item compressors POINT10, GPSTIME11, RGB12 and BYTE, and WAVEPACKET13
+//     version 1 (formats 4 / 5: LASzip has no other version of it);
+//   point formats 6-10: LASzip 3 "layered chunked" compression with the
+//     version-3 items POINT14, RGB14, RGBNIR14, WAVEPACKET14 and BYTE14 (one
+//     arithmetic stream per field group, models per scanner channel).
 //
 // The encoder half exists for tests and the laz_tool utility (LAS -> LAZ),
 // never for the converter.  Parity unpinned: no .laz fixture ships with the
@@ -29,7 +29,8 @@ namespace pcc {
 namespace laz {
 
 enum ItemType : uint16_t {
-    BYTE = 0, POINT10 = 6, GPSTIME11 = 7, RGB12 = 8, POINT14 = 10, RGB14 = 11, RGBNIR14 = 12, BYTE14 = 14
+    BYTE = 0, POINT10 = 6, GPSTIME11 = 7, RGB12 = 8, WAVEPACKET13 = 9, POINT14 = 10, RGB14 = 11, RGBNIR14 = 12,
+    WAVEPACKET14 = 13, BYTE14 = 14
 };
 struct Item { uint16_t type, size, version; };
 
@@ -46,8 +47,8 @@ struct Vlr {
 };
 bool parse_vlr(const uint8_t* d, size_t n, Vlr& v, std::string& err);
 std::vector<uint8_t> write_vlr(const Vlr& v);
-// Items of a LAS point format 0-3 / 6-8 record of `rec` bytes (extra bytes as
-// BYTE / BYTE14); compressor 2 for formats 0-3, 3 (layered) for 6-8
+// Items of a LAS point format 0-10 record of `rec` bytes (extra bytes as
+// BYTE / BYTE14); compressor 2 for formats 0-5, 3 (layered) for 6-10
 uint16_t compressor_for_format(uint8_t format);
 bool items_for_format(uint8_t format, uint16_t rec, std::vector<Item>& items, std::string& err);
 
@@ -76,7 +77,7 @@ private:
     std::unique_ptr<PointDecoder> dec_;
 };
 
-// LAS point records (formats 0-3 or 6-8, `rec` bytes each) -> LASzip point
+// LAS point records (formats 0-10, `rec` bytes each) -> LASzip point
 // data: the 8-byte chunk-table offset, the chunks, the chunk table.
 std::vector<uint8_t> compress(const uint8_t* recs, uint64_t n, uint16_t rec, const std::vector<Item>& items,
                               uint32_t chunk_size);

@@ -4,9 +4,10 @@ import struct
 
 import numpy as np
 
-REC = {0: 20, 1: 28, 2: 26, 3: 34, 6: 30, 7: 36, 8: 38}
-COLOR_OFF = {0: None, 1: None, 2: 20, 3: 28, 6: None, 7: 30, 8: 30}
-GPS_OFF = {0: None, 1: 20, 2: None, 3: 20, 6: 22, 7: 22, 8: 22}
+REC = {0: 20, 1: 28, 2: 26, 3: 34, 4: 57, 5: 63, 6: 30, 7: 36, 8: 38, 9: 59, 10: 67}
+COLOR_OFF = {0: None, 1: None, 2: 20, 3: 28, 4: None, 5: 28, 6: None, 7: 30, 8: 30, 9: None, 10: 30}
+GPS_OFF = {0: None, 1: 20, 2: None, 3: 20, 4: 20, 5: 20, 6: 22, 7: 22, 8: 22, 9: 22, 10: 22}
+WAVE_OFF = {4: 28, 5: 34, 9: 30, 10: 38}   # the 29-byte wave packet record
 
 
 def write_las_records(path, body, fmt, n, scale, offset, minor=2):
@@ -44,6 +45,31 @@ def write_las(path, X, Y, Z, scale, offset, fmt=3, rgb=None, minor=2):
     write_las_records(path, body, fmt, n, scale, offset, minor)
 
 
+def add_wave_packets(body, off, rng):
+    """Wave packet records (LAS formats 4 / 5 / 9 / 10) at byte `off`: descriptor
+    index, waveform data offset (mostly the previous offset + the previous
+    packet size, sometimes repeated, sometimes a 32-bit jump, a few 64-bit
+    jumps), packet size, return point location and x(t), y(t), z(t) floats."""
+    n = body.shape[0]
+    idx = rng.choice([1, 1, 1, 2, 3], n).astype(np.uint8)
+    size = rng.choice([120, 240, 240, 480], n).astype(np.uint64)
+    step = size.copy()
+    r = rng.random(n)
+    step[r < 0.1] = 0
+    jump = (r >= 0.1) & (r < 0.15)
+    step[jump] = rng.integers(1, 2**31, int(jump.sum())).astype(np.uint64)
+    off64 = (np.uint64(60_000) + np.concatenate([[0], np.cumsum(step[:-1])])).astype(np.uint64)
+    big = rng.random(n) < 0.003
+    off64[big] += np.uint64(1 << 40)
+    body[:, off] = idx
+    body[:, off + 1:off + 9] = off64.astype("<u8").view(np.uint8).reshape(n, 8)
+    body[:, off + 9:off + 13] = size.astype("<u4").view(np.uint8).reshape(n, 4)
+    f = np.stack([rng.normal(1000, 50, n), rng.normal(0, 1e-4, n), rng.normal(0, 1e-4, n),
+                  -np.abs(rng.normal(0.5, 0.01, n))], 1).astype("<f4")
+    f[::97] = f[::97] * 3.0
+    body[:, off + 13:off + 29] = f.view(np.uint8).reshape(n, 16)
+
+
 def survey_records(n, fmt, seed, extra=0):
     """Point records shaped like an airborne survey (what LAZ is made for):
     coordinates along scan lines, multiple returns, increasing GPS time with
@@ -73,6 +99,8 @@ def survey_records(n, fmt, seed, extra=0):
         g = 250_000.0 + np.repeat(np.cumsum(rng.random((n + 1) // 2) * 1e-4), 2)[:n]
         g[n // 3] += 1e9   # a jump beyond 32-bit differences
         body[:, 20:28] = g.astype("<f8").view(np.uint8).reshape(n, 8)
+    if fmt in WAVE_OFF:
+        add_wave_packets(body, WAVE_OFF[fmt], rng)
     if COLOR_OFF.get(fmt) is not None:
         base = np.cumsum(rng.integers(-3, 4, n)) % 65536
         rgb = np.stack([base, (base + rng.integers(0, 300, n)) % 65536, (base * 3) % 65536], 1).astype("<u2")
@@ -121,14 +149,16 @@ def survey_records14(n, fmt, seed, extra=0, channels=4):
     g = 250_000.0 + np.repeat(np.cumsum(rng.random((n + 1) // 2) * 1e-4), 2)[:n]
     g[n // 3:] += 1e9   # a jump beyond 32-bit differences
     body[:, 22:30] = g.astype("<f8").view(np.uint8).reshape(n, 8)
-    if fmt in (7, 8):
+    if fmt in WAVE_OFF:
+        add_wave_packets(body, WAVE_OFF[fmt], rng)
+    if fmt in (7, 8, 10):
         base = np.cumsum(rng.integers(-3, 4, n)) % 65536
         rgb = np.stack([base, (base + rng.integers(0, 300, n)) % 65536, (base * 3) % 65536], 1).astype("<u2")
         grey = rng.random(n) < 0.3
         rgb[grey, 1] = rgb[grey, 0]
         rgb[grey, 2] = rgb[grey, 0]
         body[:, 30:36] = rgb.view(np.uint8).reshape(n, 6)
-    if fmt == 8:
+    if fmt in (8, 10):
         nir = ((np.cumsum(rng.integers(-2, 3, n)) + 30000) % 65536).astype("<u2")
         body[:, 36:38] = nir.view(np.uint8).reshape(n, 2)
     if extra:

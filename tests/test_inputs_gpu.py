@@ -296,16 +296,18 @@ def test_ply_vertex_not_first_element():
         assert d == [] and mg == mo
 
 
-@pytest.mark.parametrize("formats", [(1, 3), (6, 8), (7,)])
+@pytest.mark.parametrize("formats", [(1, 3), (6, 8), (7,), (4, 5), (9, 10)])
 def test_laz_cli_equals_las(tmp_path, formats):
     """LAZ input (las.rs:14-46 through laz [dep]): a .laz made by laz_tool from a
     .las converts to exactly the .las's cloud, for point formats 1 and 3 (GPS
-    time, colour; pointwise chunks) and 6, 7, 8 (LAS 1.4, layered chunks, colour
-    from 7 / 8), two files in one run.  Parity unpinned: the .laz files come
+    time, colour; pointwise chunks), 6, 7, 8 (LAS 1.4, layered chunks, colour
+    from 7 / 8) and the wave-packet formats 4, 5 (pointwise) and 9, 10
+    (layered), two files in one run.  Parity unpinned: the .laz files come
     from this repository's own encoder (no reference fixture, no LASzip here)."""
     tool = os.path.join(os.path.dirname(_exe()), "laz_tool")
     files_las, files_laz = [], []
-    sizes = {1: 45_000, 3: 120_000, 6: 45_000, 8: 120_000, 7: 165_000}   # 165k points per run
+    sizes = {1: 45_000, 3: 120_000, 6: 45_000, 8: 120_000, 7: 165_000,   # 165k points per run
+             4: 45_000, 5: 120_000, 9: 45_000, 10: 120_000}
     for k, fmt in enumerate(formats):
         n = sizes[fmt]
         body = (survey_records(n, fmt, seed=40 + fmt) if fmt < 6 else survey_records14(n, fmt, seed=40 + fmt))

@@ -1,5 +1,5 @@
 """LAZ codec (point-cloud_amd/csrc/laz.cpp: the LASzip pointwise-chunked format
-for point formats 0-3, the LASzip 3 layered-chunked format for 6-8) through
+for point formats 0-5, the LASzip 3 layered-chunked format for 6-10) through
 laz_tool: LAS -> LAZ -> LAS restores the point records byte for byte, for every
 item combination, chunk sizes from 1 point up, scanner-channel switches,
 extreme coordinate jumps and GPS time jumps beyond 32-bit differences.
@@ -29,7 +29,7 @@ def _roundtrip(tmp_path, body, fmt, chunk):
     return os.path.getsize(z) / os.path.getsize(a)
 
 
-@pytest.mark.parametrize("fmt,extra", [(0, 0), (1, 0), (2, 0), (3, 0), (1, 3), (3, 5)])
+@pytest.mark.parametrize("fmt,extra", [(0, 0), (1, 0), (2, 0), (3, 0), (1, 3), (3, 5), (4, 0), (5, 0), (5, 2)])
 def test_laz_roundtrip_formats(tmp_path, fmt, extra):
     body = survey_records(60_000, fmt, seed=fmt * 10 + extra, extra=extra)
     ratio = _roundtrip(tmp_path, body, fmt, 50_000)
@@ -56,7 +56,8 @@ def test_laz_roundtrip_extreme_values(tmp_path):
     _roundtrip(tmp_path, body, 1, 333)
 
 
-@pytest.mark.parametrize("fmt,extra,channels", [(6, 0, 1), (6, 0, 4), (7, 0, 2), (8, 0, 4), (6, 3, 3), (8, 2, 4)])
+@pytest.mark.parametrize("fmt,extra,channels", [(6, 0, 1), (6, 0, 4), (7, 0, 2), (8, 0, 4), (6, 3, 3), (8, 2, 4),
+                                                (9, 0, 1), (9, 0, 3), (10, 0, 4), (10, 3, 2)])
 def test_laz_layered_roundtrip_formats(tmp_path, fmt, extra, channels):
     """Point formats 6-8 (LASzip 3 layered chunks): POINT14 + RGB14 / RGBNIR14 +
     BYTE14, points hopping between scanner channels (model contexts)."""
