@@ -477,3 +477,44 @@ def test_lpt_matches_heap_restatement():
         w = rng.integers(0, 50, n).astype(np.float64) * rng.choice([1.0, 0.5, 3.0])
         a, b = lpt_py(w, world), pcconv.shard_lpt(w, world)
         assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+
+
+def test_plan_search_placement_equals_lpt_of_its_lists():
+    """pcc_shard_plan_search's owners and loads for its best k (what plan_split
+    uses) == pcc_shard_lpt over the two lists that k defines: phase 1 = the
+    whole cells k.. then the slabs of cells ..k, phase 2 = those cells'
+    children; and the best k minimises the estimate (a larger k only when more
+    than 2 % lower)."""
+    import pcconv
+    rng = np.random.default_rng(5)
+    for _ in range(120):
+        world = int(rng.integers(2, 17))
+        nc = int(rng.integers(1, 40))
+        kmax = min(nc, 2 * world)
+        whole = np.sort(rng.integers(1, 10_000, nc).astype(np.float64))[::-1].copy()
+        whole[rng.random(nc) < 0.2] *= 20.0
+        whole = np.sort(whole)[::-1].copy()
+        ns = rng.integers(0, 30, kmax)
+        nk = rng.integers(0, 9, kmax)
+        so = np.concatenate([[0], np.cumsum(ns)]).astype(np.uint64)
+        co = np.concatenate([[0], np.cumsum(nk)]).astype(np.uint64)
+        sw = rng.integers(0, 500, int(so[-1])).astype(np.float64)
+        cw = rng.integers(0, 2_000, int(co[-1])).astype(np.float64)
+        k, t, ow, osl, och, l1, l2 = pcconv.shard_plan_search(whole, so, sw, co, cw, kmax, world, owners=True)
+        assert (k, t) == pcconv.shard_plan_search(whole, so, sw, co, cw, kmax, world)
+        s1 = int(so[k])
+        o1, m1 = pcconv.shard_lpt(np.concatenate([whole[k:], sw[:s1]]), world)
+        assert np.array_equal(np.concatenate([ow[k:], osl[:s1]]), o1) and np.array_equal(l1, m1)
+        c1 = int(co[k])
+        o2, m2 = pcconv.shard_lpt(cw[:c1], world)
+        assert np.array_equal(och[:c1], o2) and np.array_equal(l2, m2)
+        est = []
+        for kk in range(kmax + 1):
+            _, a = pcconv.shard_lpt(np.concatenate([whole[kk:], sw[:int(so[kk])]]), world)
+            _, b = pcconv.shard_lpt(cw[:int(co[kk])], world)
+            est.append(a.max() + (b.max() if int(co[kk]) else 0.0))
+        best = 0
+        for kk in range(1, kmax + 1):
+            if est[kk] < est[best] * 0.98:
+                best = kk
+        assert k == best and t == est[best]
