@@ -148,6 +148,7 @@ struct BuildStats {
     uint64_t cells = 0, slabs = 0, arrivals = 0;   // arrivals = W
     uint64_t grid_points = 0, kept_points = 0;
     double ms_total = 0, ms_level0_bin = 0;
+    uint64_t pre0_tiles = 0;                       // level-0 pass-0 tiles counted while the input uploaded
     std::vector<double> ms_level;                  // per level (slab + bucket kernels)
 };
 
@@ -245,6 +246,9 @@ private:
     void ev_end(int stage);
     void ev_collect();
     int level0_bin();
+    // level-0 pass 0 behind the host-to-device copy (add_file_host, streamed files)
+    void pre0_count(uint64_t upto, hipEvent_t after, bool all);
+    void pre0_reset();
     int run_level(uint32_t li);
     void run_dcap(Level* L);
     void quiesce();
@@ -262,6 +266,15 @@ private:
     int stage_i_ = 0;
     hipStream_t copy_ = nullptr;
     uint64_t stream_n_ = 0;                              // points pushed into the open file
+    // level-0 pass 0 of the uploaded prefix: 64 layer-digit counts per tile, the
+    // running bounding box (+ per-block partials) and the non-finite flag
+    static constexpr uint64_t kPrePiece = 32ull << 20;  // points per copy piece of add_file_host (512 MB)
+    static constexpr uint32_t kPreBlocks = 1024;
+    uint16_t* d_tile6_ = nullptr;
+    uint64_t tile6_cap_ = 0, pre_tiles_ = 0;
+    float* d_prepart_ = nullptr;
+    uint32_t* d_preflag_ = nullptr;
+    hipEvent_t pre_ev_ = nullptr;
     uint64_t n_ = 0, cap_ = 0;
     uint32_t nbatches_ = 0;
     std::vector<uint64_t> file_start_;   // first point index per file

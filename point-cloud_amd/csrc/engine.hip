@@ -926,6 +926,74 @@ __global__ __launch_bounds__(kL0BS) void k_l0_up0g(const Point* __restrict__ in,
     }
 }
 
+// Pass 0 while a host input uploads (Engine::pre0_count): per tile of kL0Tile
+// points the histogram of the low 6 layer bits (the digit k_l0_up0g counts per
+// group), per block the bounding box of its tiles behind the running box in
+// part[0..5] (k_bbox_final folds them).  Grid-stride over tiles [t0, t1); the
+// build sums the tiles of each group (k_l0_group_from_tiles) instead of reading
+// the points again.
+__global__ __launch_bounds__(kL0BS) void k_l0_tiles0(const Point* __restrict__ in, uint64_t n, L0Params P, uint64_t t0,
+                                                     uint64_t t1, uint16_t* __restrict__ tile6, float* part,
+                                                     uint32_t* flag) {
+    constexpr int R = 1 << 6, NWV = kL0BS / 64;
+    __shared__ uint32_t dh[NWV][R];
+    __shared__ float sb[NWV][6];
+    const float4* p4 = reinterpret_cast<const float4*>(in);
+    const uint32_t tid = threadIdx.x, wv = tid / 64;
+    float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+    bool bad = false;
+    for (uint64_t t = t0 + blockIdx.x; t < t1; t += gridDim.x) {
+        for (uint32_t i = tid; i < NWV * R; i += kL0BS) (&dh[0][0])[i] = 0;
+        __syncthreads();
+        const uint64_t base = t * kL0Tile;
+        float4 v[kL0IPT];
+#pragma unroll
+        for (int r = 0; r < kL0IPT; r++) v[r] = p4[min(base + (uint64_t)r * kL0BS + tid, n - 1)];
+#pragma unroll
+        for (int r = 0; r < kL0IPT; r++) {
+            if (base + (uint64_t)r * kL0BS + tid >= n) continue;
+            bad |= !(isfinite(v[r].x) && isfinite(v[r].y) && isfinite(v[r].z));
+            mn[0] = fminf(mn[0], v[r].x); mn[1] = fminf(mn[1], v[r].y); mn[2] = fminf(mn[2], v[r].z);
+            mx[0] = fmaxf(mx[0], v[r].x); mx[1] = fmaxf(mx[1], v[r].y); mx[2] = fmaxf(mx[2], v[r].z);
+            int32_t iz;
+            atomicAdd(&dh[wv][(uint32_t)l0_layer_any(P, v[r].z, iz) & (R - 1)], 1u);
+        }
+        __syncthreads();
+        if (tid < (uint32_t)R) {
+            uint32_t c = 0;
+            for (int q = 0; q < NWV; q++) c += dh[q][tid];
+            tile6[t * R + tid] = (uint16_t)c;
+        }
+        __syncthreads();
+    }
+    for (int d = 32; d > 0; d >>= 1)
+        for (int a = 0; a < 3; a++) {
+            mn[a] = fminf(mn[a], __shfl_xor(mn[a], d, 64));
+            mx[a] = fmaxf(mx[a], __shfl_xor(mx[a], d, 64));
+        }
+    if (bad) atomicOr(flag, 1u);
+    if ((tid & 63) == 0)
+        for (int a = 0; a < 3; a++) { sb[wv][a] = mn[a]; sb[wv][3 + a] = mx[a]; }
+    __syncthreads();
+    if (tid < 6) {
+        float r = sb[0][tid];
+        for (int q = 1; q < NWV; q++) r = tid < 3 ? fminf(r, sb[q][tid]) : fmaxf(r, sb[q][tid]);
+        part[(1 + blockIdx.x) * 6 + tid] = r;
+    }
+}
+
+// per (group, digit): the sum of its tiles' counts, as k_l0_up0g's gcnt0
+__global__ void k_l0_group_from_tiles(const uint16_t* __restrict__ tile6, uint64_t ntiles, uint32_t tpg,
+                                      uint32_t ngroups, uint32_t* __restrict__ gcnt0) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;   // g * 64 + digit
+    if (i >= ngroups * 64u) return;
+    const uint32_t g = i / 64, d = i % 64;
+    const uint64_t a = (uint64_t)g * tpg, b = min(a + tpg, ntiles);
+    uint32_t c = 0;
+    for (uint64_t t = a; t < b; t++) c += tile6[t * 64 + d];
+    gcnt0[(uint64_t)d * ngroups + g] = c;
+}
+
 // Pass-1 upsweep from the arena: per-tile digit histogram + the full dense-slab
 // histogram (LDS-privatised when it fits), grid-stride over the tiles.
 // Global histogram increment with one atomic per distinct bin of the active
@@ -3475,6 +3543,10 @@ Engine::~Engine() {
         if (b.done) (void)hipEventDestroy(b.done);
     }
     if (copy_) (void)hipStreamDestroy(copy_);
+    if (pre_ev_) (void)hipEventDestroy(pre_ev_);
+    (void)hipFree(d_tile6_);
+    (void)hipFree(d_prepart_);
+    (void)hipFree(d_preflag_);
 }
 
 enum Stage { ST_L0 = 0, ST_DENSE, ST_SMALL, ST_BUCKET, ST_NEXT };
@@ -3600,7 +3672,18 @@ static uint32_t batches_of(uint64_t n, uint32_t batch) {
 void Engine::add_file_host(const Point* pts, uint64_t n, uint32_t batch) {
     comb_ok_ = false;
     reserve(n_ + n);
-    if (n) HIP_CHECK(hipMemcpyAsync(d_in_ + n_, pts, n * sizeof(Point), hipMemcpyHostToDevice, stream_));
+    // the copy in pieces on the copy stream; behind each piece, on the engine
+    // stream, level-0 pass 0 of the tiles it completes (the host thread blocks
+    // in each copy of pageable memory while the device counts the last piece)
+    if (!copy_) HIP_CHECK(hipStreamCreateWithFlags(&copy_, hipStreamNonBlocking));
+    if (!pre_ev_) HIP_CHECK(hipEventCreateWithFlags(&pre_ev_, hipEventDisableTiming));
+    for (uint64_t off = 0; off < n; off += kPrePiece) {
+        const uint64_t m = std::min<uint64_t>(kPrePiece, n - off);
+        HIP_CHECK(hipMemcpyAsync(d_in_ + n_ + off, pts + off, m * sizeof(Point), hipMemcpyHostToDevice, copy_));
+        HIP_CHECK(hipEventRecord(pre_ev_, copy_));
+        pre0_count(n_ + off + m, pre_ev_, false);
+    }
+    HIP_CHECK(hipStreamSynchronize(copy_));
     file_start_.push_back(n_);
     file_eb0_.push_back(nbatches_);
     file_batch_.push_back(std::max<uint32_t>(batch, 1));
@@ -3636,6 +3719,7 @@ void Engine::stream_push(const Point* pts, uint64_t n) {
         HIP_CHECK(hipEventRecord(b.done, copy_));
         b.busy = true;
         stream_n_ += m;
+        pre0_count(n_ + stream_n_, b.done, false);
         pts += m;
         n -= m;
         stage_i_ = (stage_i_ + 1) % kStages;
@@ -3646,6 +3730,7 @@ uint64_t Engine::stream_end(uint64_t keep, uint32_t batch) {
     if (copy_) HIP_CHECK(hipStreamSynchronize(copy_));
     for (Staging& b : stage_) b.busy = false;
     keep = std::min(keep, stream_n_);
+    if (keep < stream_n_) pre0_reset();   // counted points that are not kept
     file_start_.push_back(n_);
     file_eb0_.push_back(nbatches_);
     file_batch_.push_back(std::max<uint32_t>(batch, 1));
@@ -3658,6 +3743,7 @@ uint64_t Engine::stream_end(uint64_t keep, uint32_t batch) {
 void Engine::stream_cancel() {
     if (copy_) HIP_CHECK(hipStreamSynchronize(copy_));
     for (Staging& b : stage_) b.busy = false;
+    if (stream_n_) pre0_reset();
     stream_n_ = 0;
 }
 
@@ -3770,6 +3856,7 @@ void Engine::clear_input() {
     ext_keys_ = nullptr;
     declared_total_ = 0;
     built_ = false;
+    pre0_reset();
 }
 
 int Engine::build() {
@@ -3918,6 +4005,65 @@ static void l0_pass(int p, int passes, Arena src, Arena dst, uint64_t n, const L
     HIP_CHECK(hipGetLastError());
 }
 
+// The level-0 parameters that do not depend on the bounding box.
+static L0Params l0_base_params(const Config& cfg, uint32_t h0) {
+    const uint32_t dim = cfg.sub_grid_dimension;
+    const float cs = cell_size(cfg.max_cell_size, h0), csc = cell_size(cfg.max_cell_size, h0 + 1);
+    L0Params P{};
+    P.cs = cs;
+    P.cr = hex_radius(sub_cell_size(cs, dim));
+    P.csc = csc;
+    P.crc = hex_radius(sub_cell_size(csc, dim));
+    P.inv_cs = 1.0f / P.cs;
+    P.inv_cr = 1.0f / P.cr;
+    P.inv_csc = 1.0f / P.csc;
+    P.inv_crc = 1.0f / P.crc;
+    P.exact = 0;
+    for (float v : {P.cs, P.cr, P.csc, P.crc})   // div_rc's divisor range
+        if (!(std::fabs(v) >= 0x1p-60f && std::fabs(v) <= 0x1p60f)) P.exact = 1;
+    P.nl = slab_geom(dim).nl;
+    P.dim2 = 2 * (int32_t)dim;
+    return P;
+}
+
+// Level-0 pass 0 of the input uploaded so far (the complete tiles of its first
+// `upto` points, or every tile when `all`), on the engine stream after `after`
+// (the copy that brought them).  Only for a build whose source is the plain
+// input (no merge seeds in front, no keyed input).
+void Engine::pre0_count(uint64_t upto, hipEvent_t after, bool all) {
+    if (prior_ || keyed_ || ext_in_ || h0_ != 0) return;
+    const uint64_t t1 = all ? (upto + kL0Tile - 1) / kL0Tile : upto / kL0Tile;
+    if (t1 <= pre_tiles_) return;
+    if (!d_prepart_) {
+        HIP_CHECK(hipMalloc(&d_prepart_, (1 + kPreBlocks) * 6 * sizeof(float)));
+        HIP_CHECK(hipMalloc(&d_preflag_, 4));
+    }
+    if (pre_tiles_ == 0) {   // a fresh running box and flag
+        static const float init[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
+        HIP_CHECK(hipMemcpyAsync(d_prepart_, init, sizeof init, hipMemcpyHostToDevice, stream_));
+        HIP_CHECK(hipMemsetAsync(d_preflag_, 0, 4, stream_));
+    }
+    if (t1 > tile6_cap_) {   // room for every tile of the reserved input
+        const uint64_t cap = std::max<uint64_t>(t1, (cap_ + kL0Tile - 1) / kL0Tile);
+        uint16_t* p = nullptr;
+        HIP_CHECK(hipMalloc(&p, cap * 64 * sizeof(uint16_t)));
+        if (pre_tiles_) HIP_CHECK(hipMemcpyAsync(p, d_tile6_, pre_tiles_ * 64 * sizeof(uint16_t), hipMemcpyDeviceToDevice, stream_));
+        HIP_CHECK(hipStreamSynchronize(stream_));
+        (void)hipFree(d_tile6_);
+        d_tile6_ = p;
+        tile6_cap_ = cap;
+    }
+    if (after) HIP_CHECK(hipStreamWaitEvent(stream_, after, 0));
+    const uint32_t nb = (uint32_t)std::min<uint64_t>(t1 - pre_tiles_, kPreBlocks);
+    k_l0_tiles0<<<nb, kL0BS, 0, stream_>>>(d_in_, upto, l0_base_params(cfg_, 0), pre_tiles_, t1, d_tile6_, d_prepart_,
+                                           d_preflag_);
+    k_bbox_final<<<1, 256, 0, stream_>>>(d_prepart_, nb + 1);
+    HIP_CHECK(hipGetLastError());
+    pre_tiles_ = t1;
+}
+
+void Engine::pre0_reset() { pre_tiles_ = 0; }
+
 int Engine::level0_bin() {
     const uint32_t dim = cfg_.sub_grid_dimension;
     const float cs = cell_size(cfg_.max_cell_size, h0_), csc = cell_size(cfg_.max_cell_size, h0_ + 1);
@@ -3955,9 +4101,22 @@ int Engine::level0_bin() {
     ngroups = std::max<uint32_t>(1, (ntiles + tpg - 1) / tpg);
     uint32_t* gcnt0 = static_cast<uint32_t*>(dev_->get(64ull * ngroups * 4 + 64));
     {
-        HIP_CHECK(hipMemsetAsync(dev_->bbox_flag, 0, 4, stream_));
-        k_l0_up0g<<<ngroups, kL0BS, 0, stream_>>>(src_, nsrc_, P, tpg, ngroups, gcnt0, dev_->bbox_part, dev_->bbox_flag);
-        k_bbox_final<<<1, 256, 0, stream_>>>(dev_->bbox_part, ngroups);
+        // the input's tiles already counted while it uploaded (pre0_count): count
+        // the rest, then only sum the tiles per group
+        const bool pre = pre_tiles_ > 0 && src_ == d_in_ && nsrc_ == n_ && !prior_ && !keyed_ && h0_ == 0 &&
+                         getenv("PCC_NO_PRE0") == nullptr;
+        if (pre) {
+            pre0_count(n_, nullptr, true);
+            k_l0_group_from_tiles<<<(ngroups * 64 + 255) / 256, 256, 0, stream_>>>(d_tile6_, ntiles, tpg, ngroups, gcnt0);
+            HIP_CHECK(hipMemcpyAsync(dev_->bbox_part, d_prepart_, 6 * sizeof(float), hipMemcpyDeviceToDevice, stream_));
+            HIP_CHECK(hipMemcpyAsync(dev_->bbox_flag, d_preflag_, 4, hipMemcpyDeviceToDevice, stream_));
+            stats_.pre0_tiles = pre_tiles_;
+        } else {
+            HIP_CHECK(hipMemsetAsync(dev_->bbox_flag, 0, 4, stream_));
+            k_l0_up0g<<<ngroups, kL0BS, 0, stream_>>>(src_, nsrc_, P, tpg, ngroups, gcnt0, dev_->bbox_part, dev_->bbox_flag);
+            k_bbox_final<<<1, 256, 0, stream_>>>(dev_->bbox_part, ngroups);
+            stats_.pre0_tiles = 0;
+        }
         HIP_CHECK(hipGetLastError());
         float bb[6];
         uint32_t bad = 0;
