@@ -3657,7 +3657,9 @@ void Engine::reserve(uint64_t n) {
     if (n >= 0xFFFFFFFFull) throw std::runtime_error("more than 2^32-1 points per build are not supported");
     Point* p = nullptr;
     dev_alloc_t(p, std::max<uint64_t>(n, 1) * sizeof(Point));
-    if (n_) HIP_CHECK(hipMemcpyAsync(p, d_in_, n_ * sizeof(Point), hipMemcpyDeviceToDevice, stream_));
+    // the points of the files so far and of the one being streamed in
+    const uint64_t live = n_ + stream_n_;
+    if (live) HIP_CHECK(hipMemcpyAsync(p, d_in_, live * sizeof(Point), hipMemcpyDeviceToDevice, stream_));
     HIP_CHECK(hipStreamSynchronize(stream_));
     dev_release(d_in_);
     d_in_ = p;
@@ -3693,8 +3695,8 @@ void Engine::add_file_host(const Point* pts, uint64_t n, uint32_t batch) {
 }
 
 void Engine::stream_begin(uint64_t expected) {
-    if (!copy_) {
-        HIP_CHECK(hipStreamCreateWithFlags(&copy_, hipStreamNonBlocking));
+    if (!copy_) HIP_CHECK(hipStreamCreateWithFlags(&copy_, hipStreamNonBlocking));   // (add_file_host makes it too)
+    if (!stage_[0].host) {
         for (Staging& b : stage_) {
             HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&b.host), kStagePts * sizeof(Point), hipHostMallocDefault));
             HIP_CHECK(hipEventCreateWithFlags(&b.done, hipEventDisableTiming));

@@ -264,6 +264,32 @@ def test_file_in_pieces_equals_one_call(tmp_path):
     c.close()
 
 
+def test_file_in_pieces_beyond_its_expected_size():
+    """A streamed file that outgrows the size announced to pcc_begin_file: the
+    device input grows while the file is open and keeps the points already
+    pushed (and their level-0 tile counts)."""
+    import ctypes as C
+    import pcconv
+    a, b = synth(93, 0, 300_001), synth(94, 1, 6_000_007)
+    ref = pcconv.Converter(tempfile.mkdtemp(prefix="pcc_ref_"))
+    ref.add_points(a)
+    ref.add_points(b)
+    ref.build()
+    dref = gpu_digest(ref)
+    ref.close()
+    c = pcconv.Converter(tempfile.mkdtemp(prefix="pcc_grow_"))
+    c.add_points(a)
+    lib = pcconv.lib()
+    assert lib.pcc_begin_file(c._h, 1000) == 0
+    for o in range(0, len(b), 1_500_000):
+        p = np.ascontiguousarray(b[o:o + 1_500_000])
+        assert lib.pcc_append_points(c._h, C.c_void_p(p.ctypes.data), len(p)) == 0
+    assert lib.pcc_end_file(c._h, len(b)) == 0
+    c.build()
+    assert gpu_digest(c) == dref
+    c.close()
+
+
 def test_ply_vertex_not_first_element():
     """ply.rs:36-73 reads `vertex` records straight after the header, whatever
     element the header declares first: the bytes of a leading `extra` element
