@@ -184,7 +184,13 @@ constexpr int kDenseBS = 1024;
 constexpr int kHX = 0;
 #endif
 constexpr int kDenseTab = 116 * 132;  // one z-layer of a dim-96 cell (slab_geom)
-constexpr int kDenseClaim = 2048;
+#ifndef PCC_DENSE_CLAIM
+#define PCC_DENSE_CLAIM 3744
+#endif
+constexpr int kDenseClaim = PCC_DENSE_CLAIM;   // claim entries per chunk parity (the LDS left beside the slot table)
+#ifndef PCC_CLAIM1
+#define PCC_CLAIM1 0   // 1: one table of 2 x kDenseClaim entries tagged with the chunk parity
+#endif
 #ifndef PCC_SLAB_PF
 #define PCC_SLAB_PF 2
 #endif
@@ -1825,10 +1831,22 @@ __device__ __forceinline__ uint32_t hash_slot(uint32_t k) { return (k * 26544357
 // Per-chunk claim table keyed by slot: entry = (slot << 11) | min pending thread
 // (0x7FF once that thread has been applied).  Slots < 2^14, threads < 2^10.
 constexpr uint32_t kClaimDone = 0x7FFu;
+// home entry and linear probe of a claim table of CLAIM entries (a power of two:
+// the multiplicative hash's middle bits; otherwise its top bits scaled to CLAIM)
+template <int CLAIM>
+__device__ __forceinline__ uint32_t claim_home(uint32_t local) {
+    if constexpr ((CLAIM & (CLAIM - 1)) == 0) return hash_slot(local) & (CLAIM - 1);
+    else return (uint32_t)(((uint64_t)(local * 2654435761u) * (uint32_t)CLAIM) >> 32);
+}
+template <int CLAIM>
+__device__ __forceinline__ uint32_t claim_next(uint32_t h) {
+    if constexpr ((CLAIM & (CLAIM - 1)) == 0) return (h + 1) & (CLAIM - 1);
+    else return h + 1 == (uint32_t)CLAIM ? 0u : h + 1;
+}
 template <int CLAIM>
 __device__ __forceinline__ int claim_insert(uint32_t* H, uint32_t local, uint32_t tid) {
     const uint32_t mine = (local << 11) | tid;
-    uint32_t h = hash_slot(local) & (CLAIM - 1);
+    uint32_t h = claim_home<CLAIM>(local);
     for (int probe = 0; probe < CLAIM; probe++) {
         const uint32_t e = atomicCAS(&H[h], kEmpty32, mine);   // CAS first (see claim_push)
         if (e == kEmpty32) return (int)h;
@@ -1836,7 +1854,7 @@ __device__ __forceinline__ int claim_insert(uint32_t* H, uint32_t local, uint32_
             atomicMin(&H[h], mine);
             return (int)h;
         }
-        h = (h + 1) & (CLAIM - 1);
+        h = claim_next<CLAIM>(h);
     }
     return -1;
 }
@@ -1847,7 +1865,7 @@ constexpr uint32_t kNil = 0x7FFu;
 template <int CLAIM>
 __device__ __forceinline__ int claim_push(uint32_t* H, uint32_t local, uint32_t tid, uint32_t& prev) {
     const uint32_t mine = (local << 11) | tid;
-    uint32_t h = hash_slot(local) & (CLAIM - 1);
+    uint32_t h = claim_home<CLAIM>(local);
     for (int probe = 0; probe < CLAIM; probe++) {
         // CAS first: an empty entry (the common case) costs one LDS round trip
         const uint32_t e = atomicCAS(&H[h], kEmpty32, mine);
@@ -1856,7 +1874,35 @@ __device__ __forceinline__ int claim_push(uint32_t* H, uint32_t local, uint32_t 
             prev = atomicExch(&H[h], mine) & kNil;
             return (int)h;
         }
-        h = (h + 1) & (CLAIM - 1);
+        h = claim_next<CLAIM>(h);
+    }
+    prev = kNil;
+    return -1;
+}
+
+// One claim table for both chunk parities: entry = (parity << 25) | (slot << 11)
+// | head.  An entry of the other parity is dead (its chunk's walk ended at the
+// last barrier): a push takes it over, and its owners clear it with a CAS that
+// fails harmlessly once it has been taken.  Twice the entries of the per-parity
+// tables in the same LDS, so the probe sequences are shorter.
+template <int CLAIM>
+__device__ __forceinline__ int claim_push1(uint32_t* H, uint32_t local, uint32_t par, uint32_t tid, uint32_t& prev) {
+    const uint32_t tl = (par << 14) | local;
+    const uint32_t mine = (tl << 11) | tid;
+    uint32_t h = claim_home<CLAIM>(local);
+    for (int probe = 0; probe < CLAIM; probe++) {
+        uint32_t e = atomicCAS(&H[h], kEmpty32, mine);
+        while (e != kEmpty32 && (e >> 25) != par) {   // dead entry: take it over
+            const uint32_t e2 = atomicCAS(&H[h], e, mine);
+            if (e2 == e) break;
+            e = e2 == kEmpty32 ? atomicCAS(&H[h], kEmpty32, mine) : e2;
+        }
+        if (e == kEmpty32 || (e >> 25) != par) { prev = kNil; return (int)h; }
+        if ((e >> 11) == tl) {
+            prev = atomicExch(&H[h], mine) & kNil;
+            return (int)h;
+        }
+        h = claim_next<CLAIM>(h);
     }
     prev = kNil;
     return -1;
@@ -2143,7 +2189,7 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
     }
     auto step = [&](uint32_t ci, Stage& cur, Stage& prv, const Pre& mine, const Pre& prvb, Pre& pf) {
         const uint32_t par = ci & 1;
-        uint32_t* claim = S.claim[par];
+        uint32_t* claim = PCC_CLAIM1 ? &S.claim[0][0] : S.claim[par];
         const uint32_t cg = (ci << kHX) + hx;   // chunk index in the slab
         const uint32_t j = ng + cg * BS + tid;
         const bool valid = j < n;
@@ -2154,7 +2200,15 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
             pf.k = rP.k(jo * 4);
         }
         // the claim entries of chunk i-1 (other parity) are dead since the last barrier
-        if (prv.hc >= 0) S.claim[par ^ 1][prv.hc] = kEmpty32;
+        if (PCC_CLAIM1) {
+            if (prv.hc >= 0) {
+                uint32_t* T = &S.claim[0][0];
+                const uint32_t e = T[prv.hc];
+                if ((e >> 25) == (par ^ 1)) atomicCAS(&T[prv.hc], e, kEmpty32);
+            }
+        } else if (prv.hc >= 0) {
+            S.claim[par ^ 1][prv.hc] = kEmpty32;
+        }
         const u32x4 own = mine.p;
         const float x = __uint_as_float(own.x), y = __uint_as_float(own.y), z = __uint_as_float(own.z);
         // ---- phase A (1): slot + distance (hex.rs:67-85, 55-65) + own child / grandchild slab
@@ -2222,7 +2276,8 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
             occ = kEmpty64;
         }
         if (cand) {
-            hc = claim_push<CLAIM>(claim, local, tid, myprev);
+            hc = PCC_CLAIM1 ? claim_push1<2 * CLAIM>(claim, local, par, tid, myprev)
+                            : claim_push<CLAIM>(claim, local, tid, myprev);
             if (hc < 0) { err |= ERR_CLAIM; cand = false; }
             S.cd2[tid] = f2u(d2);
             S.cnext[tid] = (uint16_t)myprev;
