@@ -188,8 +188,12 @@ constexpr int kDenseTab = 116 * 132;  // one z-layer of a dim-96 cell (slab_geom
 #define PCC_DENSE_CLAIM 3744
 #endif
 constexpr int kDenseClaim = PCC_DENSE_CLAIM;   // claim entries per chunk parity (the LDS left beside the slot table)
-#ifndef PCC_CLAIM1
-#define PCC_CLAIM1 0   // 1: one table of 2 x kDenseClaim entries tagged with the chunk parity
+#ifndef PCC_HEADS
+#ifdef PCC_HALFX
+#define PCC_HEADS 0
+#else
+#define PCC_HEADS 1    // k_slab: a 16-bit list head per slot (0: hashed claim tables per chunk parity)
+#endif
 #endif
 #ifndef PCC_SLAB_PF
 #define PCC_SLAB_PF 2
@@ -1815,11 +1819,20 @@ struct SlabParams {
 struct DenseLds {
     static constexpr int BS = kDenseBS, TAB = kDenseTab >> kHX, CLAIM = kDenseClaim >> kHX, NW = BS / 64;
     unsigned long long tab[TAB];   // occupant: (d2 bits << 33) | (child slab << 28) | j
+#if PCC_HEADS
+    static constexpr int HW = (TAB + 1) / 2;
+    uint32_t head[HW];             // per slot, 16 bits: (chunk tag << 11) | head of the slot's candidate list
+#else
     uint32_t claim[2][CLAIM];      // per chunk parity: (slot << 11) | head of the slot's candidate list
+#endif
     uint32_t cd2[BS];              // candidates of the current chunk, by thread: d2 bits,
     uint16_t cnext[BS];            //   next candidate of the same slot (kNil: end),
     uint16_t cdg[BS];              //   own child slab | (grandchild slab + 1) << 5
+#if PCC_HEADS
+    uint32_t gcnt[kDests * kDests / 2];   // 16 bits each, folded into registers every 32 steps
+#else
     uint32_t gcnt[kDests * kDests];
+#endif
     uint32_t doff[kDests], dcap[kDests];
     uint32_t dcur[2][kDests];      // emissions per child slab before chunk c: dcur[c & 1]
     alignas(16) uint32_t wcnt[kDests][NW / 4];   // emissions per child slab and wave, one byte per wave (<= 64)
@@ -1871,34 +1884,6 @@ __device__ __forceinline__ int claim_push(uint32_t* H, uint32_t local, uint32_t 
         const uint32_t e = atomicCAS(&H[h], kEmpty32, mine);
         if (e == kEmpty32) { prev = kNil; return (int)h; }
         if ((e >> 11) == local) {
-            prev = atomicExch(&H[h], mine) & kNil;
-            return (int)h;
-        }
-        h = claim_next<CLAIM>(h);
-    }
-    prev = kNil;
-    return -1;
-}
-
-// One claim table for both chunk parities: entry = (parity << 25) | (slot << 11)
-// | head.  An entry of the other parity is dead (its chunk's walk ended at the
-// last barrier): a push takes it over, and its owners clear it with a CAS that
-// fails harmlessly once it has been taken.  Twice the entries of the per-parity
-// tables in the same LDS, so the probe sequences are shorter.
-template <int CLAIM>
-__device__ __forceinline__ int claim_push1(uint32_t* H, uint32_t local, uint32_t par, uint32_t tid, uint32_t& prev) {
-    const uint32_t tl = (par << 14) | local;
-    const uint32_t mine = (tl << 11) | tid;
-    uint32_t h = claim_home<CLAIM>(local);
-    for (int probe = 0; probe < CLAIM; probe++) {
-        uint32_t e = atomicCAS(&H[h], kEmpty32, mine);
-        while (e != kEmpty32 && (e >> 25) != par) {   // dead entry: take it over
-            const uint32_t e2 = atomicCAS(&H[h], e, mine);
-            if (e2 == e) break;
-            e = e2 == kEmpty32 ? atomicCAS(&H[h], kEmpty32, mine) : e2;
-        }
-        if (e == kEmpty32 || (e >> 25) != par) { prev = kNil; return (int)h; }
-        if ((e >> 11) == tl) {
             prev = atomicExch(&H[h], mine) & kNil;
             return (int)h;
         }
@@ -2057,7 +2042,10 @@ __device__ __forceinline__ void dense_grid_points(const SlabParams& P, L& S, uin
 template <bool SEEDS>
 __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
     using L = DenseLds;
-    constexpr int BS = L::BS, TAB = L::TAB, CLAIM = L::CLAIM, NW = L::NW;
+    constexpr int BS = L::BS, TAB = L::TAB, NW = L::NW;
+#if !PCC_HEADS
+    constexpr int CLAIM = L::CLAIM;
+#endif
     __shared__ L S;
     STAMP_DECL
     const uint32_t tid = threadIdx.x, wv = tid / 64, lane = tid & 63;
@@ -2134,8 +2122,15 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
     }
     // the LDS initialisation overlaps the first two chunks' loads
     for (int i = tid; i < TAB; i += BS) S.tab[i] = kEmpty64;
+#if PCC_HEADS
+    static_assert(kHX == 0, "PCC_HEADS: one workgroup per slab");
+    for (int i = tid; i < L::HW; i += BS) S.head[i] = kEmpty32;   // tag 31, head kNil
+    for (int i = tid; i < kDests * kDests / 2; i += BS) S.gcnt[i] = 0;
+    uint32_t gacc0 = 0, gacc1 = 0;   // thread t < 288: counts of (child, grandchild) pairs 2t, 2t + 1
+#else
     for (int i = tid; i < 2 * CLAIM; i += BS) (&S.claim[0][0])[i] = kEmpty32;
     for (int i = tid; i < kDests * kDests; i += BS) S.gcnt[i] = 0;
+#endif
     if (tid < kDests) {
         S.dcur[0][tid] = 0;
         S.dcur[1][tid] = 0;
@@ -2189,7 +2184,11 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
     }
     auto step = [&](uint32_t ci, Stage& cur, Stage& prv, const Pre& mine, const Pre& prvb, Pre& pf) {
         const uint32_t par = ci & 1;
-        uint32_t* claim = PCC_CLAIM1 ? &S.claim[0][0] : S.claim[par];
+#if PCC_HEADS
+        const uint32_t tag = ci & 31u;
+#else
+        uint32_t* claim = S.claim[par];
+#endif
         const uint32_t cg = (ci << kHX) + hx;   // chunk index in the slab
         const uint32_t j = ng + cg * BS + tid;
         const bool valid = j < n;
@@ -2200,15 +2199,9 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
             pf.k = rP.k(jo * 4);
         }
         // the claim entries of chunk i-1 (other parity) are dead since the last barrier
-        if (PCC_CLAIM1) {
-            if (prv.hc >= 0) {
-                uint32_t* T = &S.claim[0][0];
-                const uint32_t e = T[prv.hc];
-                if ((e >> 25) == (par ^ 1)) atomicCAS(&T[prv.hc], e, kEmpty32);
-            }
-        } else if (prv.hc >= 0) {
-            S.claim[par ^ 1][prv.hc] = kEmpty32;
-        }
+#if !PCC_HEADS
+        if (prv.hc >= 0) S.claim[par ^ 1][prv.hc] = kEmpty32;
+#endif
         const u32x4 own = mine.p;
         const float x = __uint_as_float(own.x), y = __uint_as_float(own.y), z = __uint_as_float(own.z);
         // ---- phase A (1): slot + distance (hex.rs:67-85, 55-65) + own child / grandchild slab
@@ -2233,6 +2226,9 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
         // latency overlaps it (phase B of the last step wrote the table before
         // the barrier; local 0 for lanes without a slot)
         unsigned long long occ = S.tab[local];
+#if PCC_HEADS
+        uint32_t hw = S.head[local >> 1];   // the slot's head word, read with the occupant
+#endif
         if (__ballot(amb)) {
             if (amb) {
                 slot_dest_exact(x, y, z, G, SC, sd);
@@ -2242,6 +2238,9 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
                 slotted = valid && sd.layer_ok && range_ok;
                 local = slotted ? (uint32_t)(ly * P.tx + lx) >> kHX : 0u;
                 occ = S.tab[local];
+#if PCC_HEADS
+                hw = S.head[local >> 1];
+#endif
             }
         }
         const bool layer_ok = sd.layer_ok;
@@ -2276,9 +2275,22 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
             occ = kEmpty64;
         }
         if (cand) {
-            hc = PCC_CLAIM1 ? claim_push1<2 * CLAIM>(claim, local, par, tid, myprev)
-                            : claim_push<CLAIM>(claim, local, tid, myprev);
+#if PCC_HEADS
+            // push onto the slot's list: swap this thread into the head's half of
+            // the word (a CAS retried while other pushes change the word); the
+            // old head belongs to this chunk only if its tag is this chunk's
+            const uint32_t sh = (local & 1u) * 16u, mineh = (tag << 11) | tid;
+            for (;;) {
+                const uint32_t o = atomicCAS(&S.head[local >> 1], hw, (hw & ~(0xFFFFu << sh)) | (mineh << sh));
+                if (o == hw) break;
+                hw = o;
+            }
+            const uint32_t oldh = (hw >> sh) & 0xFFFFu;
+            myprev = (oldh >> 11) == tag ? (oldh & kNil) : kNil;
+#else
+            hc = claim_push<CLAIM>(claim, local, tid, myprev);
             if (hc < 0) { err |= ERR_CLAIM; cand = false; }
+#endif
             S.cd2[tid] = f2u(d2);
             S.cnext[tid] = (uint16_t)myprev;
             S.cdg[tid] = (uint16_t)(dn | ((uint32_t)(gn + 1) << 5));
@@ -2298,11 +2310,37 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
                 gg = slot_dest(__uint_as_float(prv.gp.x), __uint_as_float(prv.gp.y), __uint_as_float(prv.gp.z), G,
                                SC).g;
             }
+#if PCC_HEADS
+            if (!(PCC_ABL & 8) && vd && gg >= 0) {
+                const uint32_t gi = (uint32_t)(d * kDests + gg);
+                atomicAdd(&S.gcnt[gi >> 1], (gi & 1u) ? 0x10000u : 1u);
+            }
+#else
             if (!(PCC_ABL & 8) && vd && gg >= 0) atomicAdd(&S.gcnt[d * kDests + gg], 1u);
+#endif
         }
         STAMP(2);
         lds_barrier();
         STAMP(3);
+#if PCC_HEADS
+        // between the barriers nothing pushes or counts: every 16 steps, heads of
+        // older chunks go back to kNil (tags are 5 bits), and every 32 steps the
+        // 16-bit pair counts move into registers (at most 32 768 adds between)
+        if ((ci & 15u) == 15u) {
+            for (int i = tid; i < L::HW; i += BS) {
+                const uint32_t w = S.head[i];
+                const uint32_t lo = ((w >> 11) & 31u) == tag ? (w & 0xFFFFu) : 0xFFFFu;
+                const uint32_t hi = (w >> 27) == tag ? (w >> 16) : 0xFFFFu;
+                if ((lo | (hi << 16)) != w) S.head[i] = lo | (hi << 16);
+            }
+        }
+        if ((ci & 31u) == 31u && tid < kDests * kDests / 2) {
+            const uint32_t w = S.gcnt[tid];
+            gacc0 += w & 0xFFFFu;
+            gacc1 += w >> 16;
+            S.gcnt[tid] = 0;
+        }
+#endif
         // ---- phase B (1): chunk i-1's emissions.  Position = emissions to the
         // same child slab before the chunk + in earlier waves + earlier lanes.
         {
@@ -2355,7 +2393,11 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
             uint32_t bd = 0xFFFFFFFFu, bt = kNil;
             bool beaten = false;
             // branch-free body; the own entry is skipped (known without LDS reads)
+#if PCC_HEADS
+            uint32_t xk = (S.head[local >> 1] >> ((local & 1u) * 16u)) & kNil;
+#else
             uint32_t xk = claim[hc] & kNil;
+#endif
             if (xk == tid) xk = myprev;
             while (xk != kNil) {
                 const uint32_t dx = S.cd2[xk];
@@ -2423,8 +2465,21 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
     STAMP(7);
     __syncthreads();
     STAMP(11);
-
+#if PCC_HEADS
+    if (tid < kDests * kDests / 2) {
+        const uint32_t w = S.gcnt[tid];
+        gacc0 += w & 0xFFFFu;
+        gacc1 += w >> 16;
+    }
+    // the head words become the winner bitmap over the arrivals (all ones)
+    if (n <= kDenseStreamMax) {
+        for (int i = tid; i < (int)((n + 31) / 32); i += BS) S.head[i] = kEmpty32;
+        __syncthreads();
+    }
+    dense_grid_points<L>(P, S, S.head, rP, s, n, jmask, tid, lane);
+#else
     dense_grid_points<L>(P, S, &S.claim[0][0], rP, s, n, jmask, tid, lane);
+#endif
     STAMP(8);
     STAMP_FLUSH(P.stamps);
     if (kHX) err = 0;
@@ -2445,10 +2500,18 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
     }
     if (tid < kDests) P.dest_n[s * kDests + tid] = S.dcur[fp][tid] < S.dcap[tid] ? S.dcur[fp][tid] : S.dcap[tid];
     // capacities of the child slabs' own child slabs (only rows that will exist)
+#if PCC_HEADS
+    if (tid < kDests * kDests / 2) {
+        const uint32_t i0 = 2 * tid, i1 = 2 * tid + 1;
+        if (S.dcur[fp][i0 / kDests]) P.gcap[(uint64_t)s * kDests * kDests + i0] = gacc0;
+        if (S.dcur[fp][i1 / kDests]) P.gcap[(uint64_t)s * kDests * kDests + i1] = gacc1;
+    }
+#else
     for (int i = tid; i < kDests * kDests; i += BS) {
         const int dd = i / kDests;
         if (S.dcur[fp][dd]) P.gcap[(uint64_t)s * kDests * kDests + i] = S.gcnt[i];
     }
+#endif
 }
 
 // Small slabs (< kSmallMax arrivals): at most kSmallCh chunks of kSmallBS, so a
