@@ -2211,6 +2211,12 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
 #endif
         SlotDest sd;
         bool amb = false;
+#if PCC_HEADS
+        // the last step pushes and walks nothing: the head words become the
+        // winner bitmap over the arrivals (all ones; dense_grid_points)
+        if (ci == nchunks && n <= kDenseStreamMax)
+            for (int i = tid; i < (int)((n + 31) / 32); i += BS) S.head[i] = kEmpty32;
+#endif
         if (ci < nchunks) {   // block-uniform: the last step only emits
             sd = slot_dest_fast(x, y, z, G, SC, amb);
         } else {
@@ -2470,11 +2476,6 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
         const uint32_t w = S.gcnt[tid];
         gacc0 += w & 0xFFFFu;
         gacc1 += w >> 16;
-    }
-    // the head words become the winner bitmap over the arrivals (all ones)
-    if (n <= kDenseStreamMax) {
-        for (int i = tid; i < (int)((n + 31) / 32); i += BS) S.head[i] = kEmpty32;
-        __syncthreads();
     }
     dense_grid_points<L>(P, S, S.head, rP, s, n, jmask, tid, lane);
 #else
