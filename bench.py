@@ -287,8 +287,9 @@ def record(args, n_gpus, ms, st_levels, st_cells, st_slabs, arrivals, k, dense_m
                      "alg_bytes_per_arrival": 32, "kernel_ms_per_step": dense_ms,
                      "whole_build_alg_GBs": whole, "whole_build_frac": whole / HBM_PEAK_GBS,
                      "limiter": "vector-instruction issue, not HBM: the dense launches' VALU alone occupies "
-                                ">= 61 / 52 / 58 % of the SIMD cycles at levels 0 / 1 / 2 (266 / 304 / 441 VALU per "
-                                "64 arrivals at 4 cycles each, 2.4 GHz; profiles/r3_pmc_sq_1b.json, DESIGN.md §4)"},
+                                "67 / 57 / 70 % of the SIMD cycles at levels 0 / 1 / 2 (269 / 291 / 395 VALU per "
+                                "64 arrivals at 4 cycles each, 2.4 GHz, kernel-trace durations; "
+                                "profiles/r3c_pmc_sq_1b.json, DESIGN.md §4)"},
         "stage_ms": k,
     }
 
