@@ -1940,9 +1940,15 @@ struct ArrSrc {
 
 // Grid points of a dense slab: the slot table's occupants, compacted into the
 // slab's grid region (cell.rs:158-160: order inside a cell file is free).
+#ifdef PCC_STAMPS
+#define GSTAMP(ph) do { const unsigned long long st_n = __builtin_amdgcn_s_memtime(); st_acc[ph] += st_n - st_t0; st_t0 = st_n; } while (0)
+#else
+#define GSTAMP(ph) do {} while (0)
+#endif
 template <class L, class SRC>
 __device__ __forceinline__ void dense_grid_points(const SlabParams& P, L& S, uint32_t* bm, const SRC& rP,
-                                                  uint32_t s, uint32_t n, uint32_t jmask, uint32_t tid, uint32_t lane) {
+                                                  uint32_t s, uint32_t n, uint32_t jmask, uint32_t tid, uint32_t lane,
+                                                  unsigned long long* st_acc, unsigned long long& st_t0) {
     constexpr int BS = L::BS, TAB = L::TAB;
     // ---- grid points: the table's occupants, compacted into the slab's grid
     // region (cell.rs:158-160: order inside a cell file is free).
@@ -1952,8 +1958,14 @@ __device__ __forceinline__ void dense_grid_points(const SlabParams& P, L& S, uin
     if (PCC_ABL & 1) {
     } else if (n <= kDenseStreamMax) {
         // Small slab: clear the winners' bits in a bitmap over the arrivals (bm:
-        // the claim tables, all ones after the last step), then stream the arrivals
-        // once in order, coalesced, instead of gathering the winners.
+        // the head words, all ones after the last step), then stream the arrivals
+        // once in order, coalesced, instead of gathering the winners.  The first
+        // V chunks are loaded before the table scan and stay in flight across
+        // the LDS-only barrier.
+        constexpr int V = PCC_STREAM_V;
+        u32x4 pv[V];
+#pragma unroll
+        for (int u = 0; u < V; u++) pv[u] = rP.p((u * BS + tid) * 16);   // past n: zero (buffer range)
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const int i = u * BS + (int)tid;
@@ -1963,12 +1975,14 @@ __device__ __forceinline__ void dense_grid_points(const SlabParams& P, L& S, uin
                 atomicAnd(&bm[jw >> 5], ~(1u << (jw & 31u)));
             }
         }
-        __syncthreads();
-        constexpr int V = PCC_STREAM_V;
+        GSTAMP(14);
+        lds_barrier();
+        GSTAMP(15);
         for (uint32_t j0 = 0; j0 < n; j0 += V * BS) {
-            u32x4 pv[V];
+            if (j0) {
 #pragma unroll
-            for (int u = 0; u < V; u++) pv[u] = rP.p((j0 + u * BS + tid) * 16);   // past n: zero (buffer range)
+                for (int u = 0; u < V; u++) pv[u] = rP.p((j0 + u * BS + tid) * 16);
+            }
             uint64_t m[V];
             uint32_t tot = 0;
 #pragma unroll
@@ -2138,7 +2152,7 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
         S.dcap[tid] = P.dcap[s * kDests + tid];
     }
     if (tid == 0) { S.nwin = 0; S.err = 0; }
-    __syncthreads();
+    lds_barrier();   // LDS only: the first chunks' loads stay in flight
     if constexpr (SEEDS) {
         // Merge: the slab's grid seeds (its first ng arrivals: keys below every
         // other arrival, one per slot, cell.rs:183-229) are the occupants the
@@ -2469,7 +2483,7 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
         }
     }
     STAMP(7);
-    __syncthreads();
+    lds_barrier();   // LDS only: the last emission stores need not land
     STAMP(11);
 #if PCC_HEADS
     if (tid < kDests * kDests / 2) {
@@ -2477,15 +2491,21 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
         gacc0 += w & 0xFFFFu;
         gacc1 += w >> 16;
     }
-    dense_grid_points<L>(P, S, S.head, rP, s, n, jmask, tid, lane);
+#ifndef PCC_STAMPS
+    unsigned long long* st_acc = nullptr, st_t0 = 0;
+#endif
+    dense_grid_points<L>(P, S, S.head, rP, s, n, jmask, tid, lane, st_acc, st_t0);
 #else
-    dense_grid_points<L>(P, S, &S.claim[0][0], rP, s, n, jmask, tid, lane);
+#ifndef PCC_STAMPS
+    unsigned long long* st_acc = nullptr, st_t0 = 0;
+#endif
+    dense_grid_points<L>(P, S, &S.claim[0][0], rP, s, n, jmask, tid, lane, st_acc, st_t0);
 #endif
     STAMP(8);
     STAMP_FLUSH(P.stamps);
     if (kHX) err = 0;
     if (err) atomicOr(&S.err, err);
-    __syncthreads();
+    lds_barrier();
     const uint32_t fp = nchunks & 1;   // dcur after the last (emit-only) step
     if (tid == 0 && hx == 0) {
         P.slab_grid_n[s] = S.nwin;
@@ -4750,11 +4770,11 @@ int Engine::run_level(uint32_t li) {
         HIP_CHECK(hipMemcpyAsync(hs, stamps, sizeof hs, hipMemcpyDeviceToHost, stream_));
         HIP_CHECK(hipStreamSynchronize(stream_));
         const char* nm[16] = {"prologue", "claimA", "routeA", "B0wait", "rounds", "rndwait", "stores", "tail",
-                              "pass2", "#rounds", "#steps", "p2sync", "ldwait/epi", "math", "-", "-"};
+                              "pass2", "#rounds", "#steps", "p2sync", "ldwait/epi", "math", "episcan", "episync"};
         for (int v = 0; v < 2; v++) {
             if (!hs[16 * v + 10]) continue;
             fprintf(stderr, "[stamps] level %u %s waves*steps=%llu  cycles/step:", h, v ? "small" : "dense", hs[16 * v + 10]);
-            for (int q = 0; q < 14; q++)
+            for (int q = 0; q < 16; q++)
                 if (q != 9 && q != 10) fprintf(stderr, " %s=%.0f", nm[q], (double)hs[16 * v + q] / hs[16 * v + 10]);
             fprintf(stderr, " rounds/step=%.2f\n", (double)hs[16 * v + 9] / hs[16 * v + 10]);
         }
