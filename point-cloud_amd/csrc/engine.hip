@@ -1833,7 +1833,7 @@ struct DenseLds {
 #else
     uint32_t gcnt[kDests * kDests];
 #endif
-    uint32_t doff[kDests], dcap[kDests];
+    uint32_t dcap[kDests];         // (PCC_HALFX only)
     uint32_t dcur[2][kDests];      // emissions per child slab before chunk c: dcur[c & 1]
     alignas(16) uint32_t wcnt[kDests][NW / 4];   // emissions per child slab and wave, one byte per wave (<= 64)
     uint32_t nwin, err;
@@ -2103,7 +2103,13 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
     const uint32_t dbase = D.dbase;
     const uint64_t db = (uint64_t)D.dlen * 4;
     const __amdgpu_buffer_rsrc_t oP = srd(P.nx.p + dbase, db * 4), oK = srd(P.nx.k + dbase, db);
-
+    // child-slab regions of this slab, one per lane < 24, kept in registers:
+    // unconditional buffer loads (lanes >= 24 read 0) issued before the first
+    // chunks', so the prologue never waits for them (dbase is subtracted at use)
+    const __amdgpu_buffer_rsrc_t rDo = srd(P.dest_off + (uint64_t)s * kDests, kDests * 4),
+                                 rDc = srd(P.dcap + (uint64_t)s * kDests, kDests * 4);
+    uint32_t my_doff = bld(rDo, lane < kDests ? lane * 4 : 0xFFFFFFFFu);
+    uint32_t my_dcap = bld(rDc, lane < kDests ? lane * 4 : 0xFFFFFFFFu);
 
     struct Stage {
         int32_t em;     // -1 none, 0 self, 1 displaced record / occupant
@@ -2148,8 +2154,7 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
     if (tid < kDests) {
         S.dcur[0][tid] = 0;
         S.dcur[1][tid] = 0;
-        S.doff[tid] = P.dest_off[s * kDests + tid] - dbase;
-        S.dcap[tid] = P.dcap[s * kDests + tid];
+        if (kHX) S.dcap[tid] = my_dcap;   // (the split diagnostic reads it at the end)
     }
     if (tid == 0) { S.nwin = 0; S.err = 0; }
     lds_barrier();   // LDS only: the first chunks' loads stay in flight
@@ -2187,8 +2192,6 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
         __syncthreads();
     }
     STAMP(0);
-    // child-slab regions of this slab, one per lane < 24, kept in registers
-    uint32_t my_doff = lane < kDests ? S.doff[lane] : 0u, my_dcap = lane < kDests ? S.dcap[lane] : 0u;
     uint32_t nchunks = (n - ng + BS - 1) / BS;
     if (kHX) {
         const uint32_t b0 = (uint32_t)((uint64_t)my_dcap * hx >> kHX), b1 = (uint32_t)((uint64_t)my_dcap * (hx + 1) >> kHX);
@@ -2386,7 +2389,8 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
                     tot_l = __builtin_amdgcn_udot4(w[k], 0x01010101u, tot_l, false);
                 }
                 if (wv == 0) S.dcur[par][lane] = tot_l;
-                base_l = my_doff + pre_l;                 // this wave's first position in child slab `lane`
+                asm volatile("" : "+v"(my_doff));         // keeps the load's wait out of the prologue
+                base_l = my_doff - dbase + pre_l;         // this wave's first position in child slab `lane`
                 room_l = (int32_t)(my_dcap - pre_l);      // and the capacity left from there
             }
             // both shuffles with every lane active (a bpermute from an inactive
@@ -2519,7 +2523,7 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
             if (S.gcnt[i]) atomicAdd(&P.gcap[(uint64_t)s * kDests * kDests + i], S.gcnt[i]);
         return;
     }
-    if (tid < kDests) P.dest_n[s * kDests + tid] = S.dcur[fp][tid] < S.dcap[tid] ? S.dcur[fp][tid] : S.dcap[tid];
+    if (tid < kDests) P.dest_n[s * kDests + tid] = S.dcur[fp][tid] < my_dcap ? S.dcur[fp][tid] : my_dcap;   // wave 0: lane = tid
     // capacities of the child slabs' own child slabs (only rows that will exist)
 #if PCC_HEADS
     if (tid < kDests * kDests / 2) {
