@@ -2025,9 +2025,14 @@ __device__ __forceinline__ void dense_grid_points(const SlabParams& P, L& S, uin
             wpos[u] = win ? (wb + (uint32_t)__popcll(m[u] & lt)) * 16 : 0xFFFFFFFFu;
             wb += (uint32_t)__popcll(m[u]);
         }
+        GSTAMP(14);
         u32x4 pv[U];
 #pragma unroll
         for (int u = 0; u < U; u++) pv[u] = rP.p(src[u]);
+#ifdef PCC_STAMPS
+        if (pv[U - 1].x == 0x7FC00001u) S.err = 1u << 28;   // the stamp below waits for the gathers
+        GSTAMP(15);
+#endif
 #pragma unroll
         for (int u = 0; u < U; u++) bst4(rG, wpos[u], pv[u]);
     }
