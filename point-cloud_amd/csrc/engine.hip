@@ -207,6 +207,9 @@ constexpr int kDenseClaim = PCC_DENSE_CLAIM;   // claim entries per chunk parity
 #ifndef PCC_STREAM_V
 #define PCC_STREAM_V 4
 #endif
+#ifndef PCC_LPT
+#define PCC_LPT 1   // dense slabs of skewed levels launched largest first
+#endif
 constexpr uint32_t kDenseStreamMax = PCC_STREAM_MAX;   // k_slab: stream (not gather) the grid points up to this many arrivals
 constexpr int kSmallBS = 256;
 constexpr uint32_t kSmallMax = 1024;  // slabs with fewer arrivals use the hashed kernel
@@ -2598,6 +2601,37 @@ __device__ __forceinline__ SmallDesc slab_desc(uint32_t s, const uint32_t* slab_
     return D;
 }
 
+// Launch order of a level's dense slabs when their sizes are skewed: the
+// largest first (LPT), by 256 size classes; the order inside a class is free
+// (slabs are independent).  One block.
+__global__ __launch_bounds__(1024) void k_lpt_order(const uint32_t* __restrict__ list, uint32_t n,
+                                                    const uint32_t* __restrict__ slab_n, uint32_t maxn,
+                                                    uint32_t* __restrict__ out) {
+    __shared__ uint32_t cnt[256];
+    const uint32_t tid = threadIdx.x;
+    if (tid < 256) cnt[tid] = 0;
+    __syncthreads();
+    auto cls = [&](uint32_t s) { return 255u - (uint32_t)(((uint64_t)slab_n[s] * 256u) / ((uint64_t)maxn + 1u)); };
+    for (uint32_t i = tid; i < n; i += 1024) atomicAdd(&cnt[cls(list[i])], 1u);
+    __syncthreads();
+    if (tid < 64) {   // exclusive prefix over the 256 classes, 4 per lane
+        uint32_t c4[4], t = 0;
+        for (int q = 0; q < 4; q++) { c4[q] = cnt[tid * 4 + q]; t += c4[q]; }
+        uint32_t x = t;
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(x, d, 64);
+            if (tid >= (uint32_t)d) x += y;
+        }
+        uint32_t a = x - t;
+        for (int q = 0; q < 4; q++) { cnt[tid * 4 + q] = a; a += c4[q]; }
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < n; i += 1024) {
+        const uint32_t sl = list[i];
+        out[atomicAdd(&cnt[cls(sl)], 1u)] = sl;
+    }
+}
+
 __global__ void k_dense_desc(const uint32_t* list, uint32_t nlist, const uint32_t* slab_cell, const int32_t* slab_layer,
                              const uint32_t* slab_off, const uint32_t* slab_n, const int32_t* cell_idx,
                              const uint32_t* cell_sb, const uint32_t* dest_off, const uint32_t* dcap, SmallDesc* out,
@@ -4671,8 +4705,16 @@ int Engine::run_level(uint32_t li) {
     }
     if (L->nbig) {
         SP.list = L->big_list;
+        // skewed sizes (the largest slab well above the mean): largest first, so
+        // the big ones do not start last and leave the chip idle behind them
+        const uint32_t* dlist = L->big_list;
+        if (PCC_LPT && L->nbig > 256 && (double)L->max_slab * L->nbig > 1.5 * (double)L->arrivals) {
+            uint32_t* sorted = static_cast<uint32_t*>(dev_->get((uint64_t)L->nbig * 4));
+            k_lpt_order<<<1, 1024, 0, stream_>>>(L->big_list, L->nbig, L->slab_n, L->max_slab, sorted);
+            dlist = sorted;
+        }
         SmallDesc* dd = static_cast<SmallDesc*>(dev_->get((uint64_t)L->nbig * sizeof(SmallDesc)));
-        k_dense_desc<<<grid_for(L->nbig, 256, 1u << 30), 256, 0, stream_>>>(L->big_list, L->nbig, L->slab_cell,
+        k_dense_desc<<<grid_for(L->nbig, 256, 1u << 30), 256, 0, stream_>>>(dlist, L->nbig, L->slab_cell,
                                                                            L->slab_layer, L->slab_off, L->slab_n,
                                                                            L->cell_idx, L->cell_sb, L->dest_off,
                                                                            L->dcap, dd,
