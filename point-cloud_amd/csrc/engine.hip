@@ -4708,7 +4708,8 @@ int Engine::run_level(uint32_t li) {
         // skewed sizes (the largest slab well above the mean): largest first, so
         // the big ones do not start last and leave the chip idle behind them
         const uint32_t* dlist = L->big_list;
-        if (PCC_LPT && L->nbig > 256 && (double)L->max_slab * L->nbig > 1.5 * (double)L->arrivals) {
+        if (PCC_LPT && L->nbig > 256 && L->nbig <= (1u << 17) &&   // (one block: up to ~0.1 ms)
+            (double)L->max_slab * L->nbig > 1.5 * (double)L->arrivals) {
             uint32_t* sorted = static_cast<uint32_t*>(dev_->get((uint64_t)L->nbig * 4));
             k_lpt_order<<<1, 1024, 0, stream_>>>(L->big_list, L->nbig, L->slab_n, L->max_slab, sorted);
             dlist = sorted;
