@@ -4713,6 +4713,7 @@ int Engine::run_level(uint32_t li) {
             uint32_t* sorted = static_cast<uint32_t*>(dev_->get((uint64_t)L->nbig * 4));
             k_lpt_order<<<1, 1024, 0, stream_>>>(L->big_list, L->nbig, L->slab_n, L->max_slab, sorted);
             dlist = sorted;
+            if (verbose) fprintf(stderr, "[pcc]   dense slabs launched largest first\n");
         }
         SmallDesc* dd = static_cast<SmallDesc*>(dev_->get((uint64_t)L->nbig * sizeof(SmallDesc)));
         k_dense_desc<<<grid_for(L->nbig, 256, 1u << 30), 256, 0, stream_>>>(dlist, L->nbig, L->slab_cell,

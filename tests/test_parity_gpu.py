@@ -116,6 +116,17 @@ def test_level0_paths_thin_layer(env):
                 os.environ[k] = v
 
 
+def test_skewed_level_largest_first_order():
+    """A level whose dense slabs are skewed: 2M uniform points (≈ 1 300 arrivals in
+    each of the ≈ 1 536 level-0 slabs) and 1M points in one hex layer over four
+    cells (four slabs of ≈ 250 000).  max_slab x dense slabs ≈ 3.8e8 > 1.5 x 3e6
+    arrivals, so the level's dense slabs are launched largest first (k_lpt_order);
+    the launch order must not change any cell."""
+    uni = synth(43, 0, 2_000_000, lo=-1000.0, ext=2000.0)
+    thin = _thin_layer_points(1_000_000, 44)
+    _check([uni[:1_000_000], thin, uni[1_000_000:]], fast=True)
+
+
 def test_config2_uniform_10m_synthetic_on_device():
     """Config 2: 10M uniform points generated in HBM; the oracle generates the same
     points on the host with its own copy of the generator."""
