@@ -207,6 +207,9 @@ constexpr int kDenseClaim = PCC_DENSE_CLAIM;   // claim entries per chunk parity
 #ifndef PCC_STREAM_V
 #define PCC_STREAM_V 4
 #endif
+#ifndef PCC_WAVE2
+#define PCC_WAVE2 0   // k_slab_wave: slot key inside the table entry (no key table), same-slot lanes ranked by ballots
+#endif
 #ifndef PCC_LPT
 #define PCC_LPT 1   // dense slabs of skewed levels launched largest first
 #endif
@@ -2989,7 +2992,9 @@ template <int CH>
 struct WaveLds {
     static constexpr int TAB = 128 * CH;
     unsigned long long tab[TAB];
+#if !PCC_WAVE2
     uint32_t tkey[TAB];          // (claim lane << 24) | slot, kEmpty32 = empty
+#endif
     uint16_t fate[64 * CH];
     uint32_t doff[kDests], dcap[kDests], dcur[kDests];
     uint32_t gcnt[kDests * kDests / 2];   // (child, grandchild) counts, 16 bits each
@@ -2997,6 +3002,24 @@ struct WaveLds {
 template <class WL>
 __device__ __forceinline__ void wave_gcount(WL& W, bool active, uint32_t key) {
     if (active) atomicAdd(&W.gcnt[key >> 1], (key & 1u) ? 0x10000u : 1u);
+}
+
+// PCC_WAVE2 entry: (d2 bits << 33) | (dest << 28) | (slot << 14) | j, j < 2^14; a
+// slot taken with no occupant yet has d2 bits 0x7FFFFFFF (kEmpty64: no slot)
+constexpr unsigned long long kW2None = 0x7FFFFFFFull << 33;
+__device__ __forceinline__ unsigned long long w2_reserved(uint32_t local) {
+    return kW2None | (31ull << 28) | ((unsigned long long)local << 14) | 0x3FFFull;
+}
+template <class WL>
+__device__ __forceinline__ int wave_entry2(WL& W, uint32_t local, uint32_t mask) {
+    uint32_t h = hash_slot(local) & mask;
+    const unsigned long long res = w2_reserved(local);
+    for (uint32_t probe = 0; probe <= mask; probe++) {
+        const unsigned long long old = atomicCAS(&W.tab[h], kEmpty64, res);
+        if (old == kEmpty64 || (((uint32_t)old >> 14) & 0x3FFFu) == local) return (int)h;
+        h = (h + 1) & mask;
+    }
+    return -1;
 }
 
 template <class WL>
@@ -3011,8 +3034,11 @@ __device__ __forceinline__ int wave_entry(WL& W, uint32_t local, uint32_t mask) 
     return -1;
 }
 
+#ifndef PCC_WAVE_OCC
+#define PCC_WAVE_OCC 1   // k_slab_wave: minimum waves per SIMD asked of the compiler
+#endif
 template <int CH>
-__global__ __launch_bounds__(64) void k_slab_wave(SlabParams P) {
+__global__ __launch_bounds__(64, PCC_WAVE_OCC) void k_slab_wave(SlabParams P) {
     using WL = WaveLds<CH>;
     __shared__ WL W;
     const uint32_t lane = threadIdx.x;
@@ -3052,7 +3078,11 @@ __global__ __launch_bounds__(64) void k_slab_wave(SlabParams P) {
                 pk[c] = bld(rK, v ? j * 4 : 0xFFFFFFFFu);
             }
         }
+#if PCC_WAVE2
+        for (uint32_t i = lane; i < cap; i += 64) W.tab[i] = kEmpty64;
+#else
         for (uint32_t i = lane; i < cap; i += 64) { W.tab[i] = kEmpty64; W.tkey[i] = kEmpty32; }
+#endif
         for (uint32_t i = lane; i < kDests * kDests / 2; i += 64) W.gcnt[i] = 0;
         if (lane < kDests) {
             W.dcur[lane] = 0;
@@ -3067,12 +3097,21 @@ __global__ __launch_bounds__(64) void k_slab_wave(SlabParams P) {
         uint32_t err = 0;
         __syncthreads();   // one wave: orders the LDS initialisation
 
+#if PCC_WAVE2
+        // per chunk, one register: (entry + 1, 0 none) | own child slab << 11 | (own grandchild slab + 1) << 16
+        uint32_t own[CH];
+#else
         int32_t rec_e[CH], own_d[CH], own_g[CH];
+#endif
 #pragma unroll
         for (int c = 0; c < CH; c++) {
+#if PCC_WAVE2
+            own[c] = 0u;
+#else
             rec_e[c] = -1;
             own_d[c] = 0;
             own_g[c] = -1;
+#endif
             if ((uint32_t)c >= nch) continue;   // wave-uniform
             const uint32_t j = c * 64 + lane;
             const bool valid = j < n;
@@ -3093,8 +3132,12 @@ __global__ __launch_bounds__(64) void k_slab_wave(SlabParams P) {
                 if (bad) err |= slot_route_errs(slot_route(x, y, z, G), layer_ok, range_ok, cx, cy, cz, t, P.check_gchild);
             }
             const uint32_t dn = d < 0 ? 0u : (uint32_t)d;
+#if PCC_WAVE2
+            own[c] = (dn << 11) | ((uint32_t)(g + 1) << 16);
+#else
             own_d[c] = (int32_t)dn;
             own_g[c] = g;
+#endif
             int e = 0;
             int32_t em = -1;
             uint32_t emj = 0, emd = 0;
@@ -3103,6 +3146,50 @@ __global__ __launch_bounds__(64) void k_slab_wave(SlabParams P) {
                 em = 0;
                 emd = dn;
             }
+#if PCC_WAVE2
+            if (pending) {
+                e = wave_entry2(W, local, mask);
+                if (e < 0) {
+                    err |= ERR_CLAIM;
+                    pending = false;
+                } else {   // occupant pre-filter (see k_slab)
+                    const unsigned long long occ = W.tab[e];
+                    if ((occ >> 33) != 0x7FFFFFFFull && !(d2 < __uint_as_float((uint32_t)(occ >> 33)))) {
+                        pending = false;
+                        em = 0;
+                        emd = dn;
+                    }
+                }
+            }
+            {   // same-slot lanes applied in lane (= key) order: rank among the
+                // pending lanes of the same entry, one rank per round (one wave:
+                // its LDS operations execute in program order)
+                const uint64_t same = wave_peers<10>((uint32_t)(pending ? e : 0), pending);
+                const uint32_t rk = (uint32_t)__popcll(same & lt);
+                for (uint32_t r = 0; __ballot(pending && rk >= r); r++) {
+                    if (pending && rk == r) {
+                        const unsigned long long occ = W.tab[e];
+                        const unsigned long long mine = ((unsigned long long)f2u(d2) << 33) |
+                                                        ((unsigned long long)dn << 28) |
+                                                        ((unsigned long long)local << 14) | j;
+                        if ((occ >> 33) == 0x7FFFFFFFull) {
+                            W.tab[e] = mine;
+                            own[c] |= (uint32_t)(e + 1);
+                        } else if (d2 < __uint_as_float((uint32_t)(occ >> 33))) {   // strict: ties keep the old point
+                            W.tab[e] = mine;
+                            own[c] |= (uint32_t)(e + 1);
+                            em = 1;
+                            emj = (uint32_t)occ & 0x3FFFu;
+                            emd = (uint32_t)(occ >> 28) & 31u;
+                        } else {
+                            em = 0;
+                            emd = dn;
+                        }
+                        pending = false;
+                    }
+                }
+            }
+#else
             if (pending) {
                 e = wave_entry(W, local, mask);
                 if (e < 0) {
@@ -3117,8 +3204,10 @@ __global__ __launch_bounds__(64) void k_slab_wave(SlabParams P) {
                     }
                 }
             }
+#endif
             // claim rounds inside the wave: the lowest pending lane of each slot is applied
-            while (__ballot(pending)) {
+            while (!PCC_WAVE2 && __ballot(pending)) {
+#if !PCC_WAVE2
                 if (pending) atomicMin(&W.tkey[e], (lane << 24) | local);
                 __syncthreads();
                 const bool win = pending && (W.tkey[e] >> 24) == lane;
@@ -3143,6 +3232,7 @@ __global__ __launch_bounds__(64) void k_slab_wave(SlabParams P) {
                     W.tkey[e] = kNoClaim | local;
                 }
                 __syncthreads();
+#endif
             }
             // emissions of this chunk, in lane order per child slab
             const bool vd = em >= 0;
@@ -3172,16 +3262,27 @@ __global__ __launch_bounds__(64) void k_slab_wave(SlabParams P) {
             if ((uint32_t)c >= nch) break;
             const uint32_t j = c * 64 + lane;
             bool win = false, dsp = false;
+#if PCC_WAVE2
+            const int32_t rec = (int32_t)(own[c] & 0x7FFu) - 1;
+            const int32_t od = (int32_t)((own[c] >> 11) & 31u), og = (int32_t)((own[c] >> 16) & 31u) - 1;
+            if (rec >= 0) {
+                const unsigned long long occ = W.tab[rec];
+                win = ((uint32_t)occ & 0x3FFFu) == j;
+                dsp = !win;
+            }
+#else
+            const int32_t od = own_d[c], og = own_g[c];
             if (rec_e[c] >= 0) {
                 const unsigned long long occ = W.tab[rec_e[c]];
                 win = ((uint32_t)occ & kJMask) == j;
                 dsp = !win;
             }
+#endif
             const uint64_t m = __ballot(win);
             bst4(rG, win ? (nwin + (uint32_t)__popcll(m & lt)) * 16 : 0xFFFFFFFFu, pp[c]);
             nwin += (uint32_t)__popcll(m);
             bst4(oP, dsp ? (uint32_t)W.fate[j] * 16 : 0xFFFFFFFFu, pp[c]);
-            wave_gcount(W, dsp && own_g[c] >= 0, (uint32_t)(own_d[c] * kDests + (own_g[c] < 0 ? 0 : own_g[c])));
+            wave_gcount(W, dsp && og >= 0, (uint32_t)(od * kDests + (og < 0 ? 0 : og)));
         }
         if (lane == 0) {
             P.slab_grid_n[s] = nwin;
