@@ -208,7 +208,7 @@ constexpr int kDenseClaim = PCC_DENSE_CLAIM;   // claim entries per chunk parity
 #define PCC_STREAM_V 4
 #endif
 #ifndef PCC_WAVE2
-#define PCC_WAVE2 0   // k_slab_wave: slot key inside the table entry (no key table), same-slot lanes ranked by ballots
+#define PCC_WAVE2 1   // k_slab_wave: slot key inside the table entry (no key table), same-slot lanes ranked by ballots
 #endif
 #ifndef PCC_LPT
 #define PCC_LPT 1   // dense slabs of skewed levels launched largest first
@@ -3035,7 +3035,7 @@ __device__ __forceinline__ int wave_entry(WL& W, uint32_t local, uint32_t mask) 
 }
 
 #ifndef PCC_WAVE_OCC
-#define PCC_WAVE_OCC 1   // k_slab_wave: minimum waves per SIMD asked of the compiler
+#define PCC_WAVE_OCC 4   // k_slab_wave: minimum waves per SIMD asked of the compiler (115 VGPRs for 8 chunks, no spills)
 #endif
 template <int CH>
 __global__ __launch_bounds__(64, PCC_WAVE_OCC) void k_slab_wave(SlabParams P) {
