@@ -173,28 +173,8 @@ static void dev_alloc_t(T*& p, size_t bytes) {
 // ------------------------------------------------------------------ constants
 constexpr uint64_t kEmpty64 = ~0ull;
 constexpr uint32_t kEmpty32 = 0xFFFFFFFFu;
-// Diagnostic build only (-DPCC_HALFX, `make var`): timing of two 512-thread
-// workgroups per dense slab, each replaying half the chunks into a half-size slot
-// table (results wrong; measures what two workgroups per CU would gain).
-#ifdef PCC_HALFX
-constexpr int kHX = PCC_HALFX;   // log2 of the workgroups per slab
-constexpr int kDenseBS = 1024 >> kHX;
-#else
 constexpr int kDenseBS = 1024;
-constexpr int kHX = 0;
-#endif
 constexpr int kDenseTab = 116 * 132;  // one z-layer of a dim-96 cell (slab_geom)
-#ifndef PCC_DENSE_CLAIM
-#define PCC_DENSE_CLAIM 3744
-#endif
-constexpr int kDenseClaim = PCC_DENSE_CLAIM;   // claim entries per chunk parity (the LDS left beside the slot table)
-#ifndef PCC_HEADS
-#ifdef PCC_HALFX
-#define PCC_HEADS 0
-#else
-#define PCC_HEADS 1    // k_slab: a 16-bit list head per slot (0: hashed claim tables per chunk parity)
-#endif
-#endif
 #ifndef PCC_SLAB_PF
 #define PCC_SLAB_PF 2
 #endif
@@ -206,9 +186,6 @@ constexpr int kDenseClaim = PCC_DENSE_CLAIM;   // claim entries per chunk parity
 #endif
 #ifndef PCC_STREAM_V
 #define PCC_STREAM_V 4
-#endif
-#ifndef PCC_WAVE2
-#define PCC_WAVE2 1   // k_slab_wave: slot key inside the table entry (no key table), same-slot lanes ranked by ballots
 #endif
 #ifndef PCC_LPT
 #define PCC_LPT 1   // dense slabs of skewed levels launched largest first
@@ -330,14 +307,6 @@ struct Engine::Level {
 // ------------------------------------------------------------------ diagnostics
 // Diagnostic build only (-DPCC_STAMPS): per-wave s_memtime phase sums of the
 // slab kernel, added into P.stamps[phase]; never compiled into the product.
-// Diagnostic builds only (-DPCC_ABL=mask, `make abl`): timing ablations of the
-// dense slab kernel that break its results (1: no grid gather, 2: no emission
-// stores, 4: no displaced-payload gathers, 8: no grandchild counts, 16: no
-// emission ranks, 32: no claims (every arrival overflows)).  Only the first
-// level's timing is meaningful under 2..32.  Never compiled into the product.
-#ifndef PCC_ABL
-#define PCC_ABL 0
-#endif
 #ifdef PCC_STAMPS
 #define STAMP_DECL unsigned long long st_t0 = __builtin_amdgcn_s_memtime(), st_acc[16] = {};
 #define STAMP(ph) do { const unsigned long long st_n = __builtin_amdgcn_s_memtime(); st_acc[ph] += st_n - st_t0; st_t0 = st_n; } while (0)
@@ -1823,23 +1792,14 @@ struct SlabParams {
 // Dense slabs (>= kSmallMax arrivals): one 1024-thread workgroup per slab, the
 // slab's whole hex layer as a direct-mapped slot table in LDS.
 struct DenseLds {
-    static constexpr int BS = kDenseBS, TAB = kDenseTab >> kHX, CLAIM = kDenseClaim >> kHX, NW = BS / 64;
+    static constexpr int BS = kDenseBS, TAB = kDenseTab, NW = BS / 64;
     unsigned long long tab[TAB];   // occupant: (d2 bits << 33) | (child slab << 28) | j
-#if PCC_HEADS
     static constexpr int HW = (TAB + 1) / 2;
     uint32_t head[HW];             // per slot, 16 bits: (chunk tag << 11) | head of the slot's candidate list
-#else
-    uint32_t claim[2][CLAIM];      // per chunk parity: (slot << 11) | head of the slot's candidate list
-#endif
     uint32_t cd2[BS];              // candidates of the current chunk, by thread: d2 bits,
     uint16_t cnext[BS];            //   next candidate of the same slot (kNil: end),
     uint16_t cdg[BS];              //   own child slab | (grandchild slab + 1) << 5
-#if PCC_HEADS
     uint32_t gcnt[kDests * kDests / 2];   // 16 bits each, folded into registers every 32 steps
-#else
-    uint32_t gcnt[kDests * kDests];
-#endif
-    uint32_t dcap[kDests];         // (PCC_HALFX only)
     uint32_t dcur[2][kDests];      // emissions per child slab before chunk c: dcur[c & 1]
     alignas(16) uint32_t wcnt[kDests][NW / 4];   // emissions per child slab and wave, one byte per wave (<= 64)
     uint32_t nwin, err;
@@ -1850,54 +1810,28 @@ __device__ __forceinline__ uint32_t hash_slot(uint32_t k) { return (k * 26544357
 // Per-chunk claim table keyed by slot: entry = (slot << 11) | min pending thread
 // (0x7FF once that thread has been applied).  Slots < 2^14, threads < 2^10.
 constexpr uint32_t kClaimDone = 0x7FFu;
-// home entry and linear probe of a claim table of CLAIM entries (a power of two:
-// the multiplicative hash's middle bits; otherwise its top bits scaled to CLAIM)
-template <int CLAIM>
-__device__ __forceinline__ uint32_t claim_home(uint32_t local) {
-    if constexpr ((CLAIM & (CLAIM - 1)) == 0) return hash_slot(local) & (CLAIM - 1);
-    else return (uint32_t)(((uint64_t)(local * 2654435761u) * (uint32_t)CLAIM) >> 32);
-}
-template <int CLAIM>
-__device__ __forceinline__ uint32_t claim_next(uint32_t h) {
-    if constexpr ((CLAIM & (CLAIM - 1)) == 0) return (h + 1) & (CLAIM - 1);
-    else return h + 1 == (uint32_t)CLAIM ? 0u : h + 1;
-}
+// Claim table of CLAIM entries (a power of two), linear probing from the
+// multiplicative hash's middle bits.  CAS first: an empty entry (the common
+// case) costs one LDS round trip.
 template <int CLAIM>
 __device__ __forceinline__ int claim_insert(uint32_t* H, uint32_t local, uint32_t tid) {
+    static_assert((CLAIM & (CLAIM - 1)) == 0, "claim table: a power of two");
     const uint32_t mine = (local << 11) | tid;
-    uint32_t h = claim_home<CLAIM>(local);
+    uint32_t h = hash_slot(local) & (CLAIM - 1);
     for (int probe = 0; probe < CLAIM; probe++) {
-        const uint32_t e = atomicCAS(&H[h], kEmpty32, mine);   // CAS first (see claim_push)
+        const uint32_t e = atomicCAS(&H[h], kEmpty32, mine);
         if (e == kEmpty32) return (int)h;
         if ((e >> 11) == local) {
             atomicMin(&H[h], mine);
             return (int)h;
         }
-        h = claim_next<CLAIM>(h);
+        h = (h + 1) & (CLAIM - 1);
     }
     return -1;
 }
 
-// Same table as a list head per slot: the entry's low 11 bits are the last
-// inserted thread; returns the entry and the previous head (kNil: none).
+// end of a dense slab's per-slot candidate list (k_slab)
 constexpr uint32_t kNil = 0x7FFu;
-template <int CLAIM>
-__device__ __forceinline__ int claim_push(uint32_t* H, uint32_t local, uint32_t tid, uint32_t& prev) {
-    const uint32_t mine = (local << 11) | tid;
-    uint32_t h = claim_home<CLAIM>(local);
-    for (int probe = 0; probe < CLAIM; probe++) {
-        // CAS first: an empty entry (the common case) costs one LDS round trip
-        const uint32_t e = atomicCAS(&H[h], kEmpty32, mine);
-        if (e == kEmpty32) { prev = kNil; return (int)h; }
-        if ((e >> 11) == local) {
-            prev = atomicExch(&H[h], mine) & kNil;
-            return (int)h;
-        }
-        h = claim_next<CLAIM>(h);
-    }
-    prev = kNil;
-    return -1;
-}
 
 // Slot-table entry: (d2 bits << 33) | (dest << 28) | ((g + 1) << 23) | j.  d2 >= +0
 // so its sign bit is free; dest (0..23) and g (grandchild slab inside dest, -1
@@ -1961,8 +1895,7 @@ __device__ __forceinline__ void dense_grid_points(const SlabParams& P, L& S, uin
     constexpr int U = (TAB + BS - 1) / BS;
     const uint64_t lt = lanemask_lt();
     const __amdgpu_buffer_rsrc_t rG = srd(P.grid + P.grid_off[s], (uint64_t)n * 16);
-    if (PCC_ABL & 1) {
-    } else if (n <= kDenseStreamMax) {
+    if (n <= kDenseStreamMax) {
         // Small slab: clear the winners' bits in a bitmap over the arrivals (bm:
         // the head words, all ones after the last step), then stream the arrivals
         // once in order, coalesced, instead of gathering the winners.  The first
@@ -2068,14 +2001,10 @@ template <bool SEEDS>
 __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
     using L = DenseLds;
     constexpr int BS = L::BS, TAB = L::TAB, NW = L::NW;
-#if !PCC_HEADS
-    constexpr int CLAIM = L::CLAIM;
-#endif
     __shared__ L S;
     STAMP_DECL
     const uint32_t tid = threadIdx.x, wv = tid / 64, lane = tid & 63;
-    const SmallDesc D = P.ddesc[blockIdx.x >> kHX];
-    const uint32_t hx = blockIdx.x & ((1u << kHX) - 1u);   // PCC_HALFX: this workgroup's chunk residue
+    const SmallDesc D = P.ddesc[blockIdx.x];
     const uint32_t s = D.s;
     const int32_t t = D.t;
     const uint32_t off = D.off, n = D.n, nm1 = n - 1;
@@ -2142,7 +2071,7 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
     Pre pre[PF + 2];
 #pragma unroll
     for (int q = 0; q < PF + 2; q++) {
-        const uint32_t jo = min(ng + (uint32_t)(((q << kHX) + hx) * BS) + tid, nm1);
+        const uint32_t jo = min(ng + (uint32_t)(q * BS) + tid, nm1);
         if (q < PF) {
             pre[q].p = rP.p(jo * 16);
             pre[q].k = rP.k(jo * 4);
@@ -2153,19 +2082,12 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
     }
     // the LDS initialisation overlaps the first two chunks' loads
     for (int i = tid; i < TAB; i += BS) S.tab[i] = kEmpty64;
-#if PCC_HEADS
-    static_assert(kHX == 0, "PCC_HEADS: one workgroup per slab");
     for (int i = tid; i < L::HW; i += BS) S.head[i] = kEmpty32;   // tag 31, head kNil
     for (int i = tid; i < kDests * kDests / 2; i += BS) S.gcnt[i] = 0;
     uint32_t gacc0 = 0, gacc1 = 0;   // thread t < 288: counts of (child, grandchild) pairs 2t, 2t + 1
-#else
-    for (int i = tid; i < 2 * CLAIM; i += BS) (&S.claim[0][0])[i] = kEmpty32;
-    for (int i = tid; i < kDests * kDests; i += BS) S.gcnt[i] = 0;
-#endif
     if (tid < kDests) {
         S.dcur[0][tid] = 0;
         S.dcur[1][tid] = 0;
-        if (kHX) S.dcap[tid] = my_dcap;   // (the split diagnostic reads it at the end)
     }
     if (tid == 0) { S.nwin = 0; S.err = 0; }
     lds_barrier();   // LDS only: the first chunks' loads stay in flight
@@ -2197,39 +2119,25 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
                 const unsigned long long e = ((unsigned long long)f2u(d2) << 33) | ((unsigned long long)dn << kJBits) |
                                              (wide ? 0u : ((uint32_t)(gn + 1) << 23)) | jg;
                 // two grid points in one slot: not a cell a converter writes
-                if (atomicCAS(&S.tab[(uint32_t)(ly * P.tx + lx) >> kHX], kEmpty64, e) != kEmpty64) err |= ERR_CLAIM;
+                if (atomicCAS(&S.tab[(uint32_t)(ly * P.tx + lx)], kEmpty64, e) != kEmpty64) err |= ERR_CLAIM;
             }
         }
         __syncthreads();
     }
     STAMP(0);
-    uint32_t nchunks = (n - ng + BS - 1) / BS;
-    if (kHX) {
-        const uint32_t b0 = (uint32_t)((uint64_t)my_dcap * hx >> kHX), b1 = (uint32_t)((uint64_t)my_dcap * (hx + 1) >> kHX);
-        my_doff += b0;
-        my_dcap = b1 - b0;
-        nchunks = (nchunks + (1u << kHX) - 1u - hx) >> kHX;
-    }
+    const uint32_t nchunks = (n - ng + BS - 1) / BS;
     auto step = [&](uint32_t ci, Stage& cur, Stage& prv, const Pre& mine, const Pre& prvb, Pre& pf) {
         const uint32_t par = ci & 1;
-#if PCC_HEADS
         const uint32_t tag = ci & 31u;
-#else
-        uint32_t* claim = S.claim[par];
-#endif
-        const uint32_t cg = (ci << kHX) + hx;   // chunk index in the slab
-        const uint32_t j = ng + cg * BS + tid;
+        const uint32_t j = ng + ci * BS + tid;
         const bool valid = j < n;
         const bool forced = valid && mine.k - P.kf_lo < P.kf_n;
         {   // prefetch chunk i+2 (clamped)
-            const uint32_t jo = min(j + ((PF * BS) << kHX), nm1);
+            const uint32_t jo = min(j + PF * BS, nm1);
             pf.p = rP.p(jo * 16);
             pf.k = rP.k(jo * 4);
         }
         // the claim entries of chunk i-1 (other parity) are dead since the last barrier
-#if !PCC_HEADS
-        if (prv.hc >= 0) S.claim[par ^ 1][prv.hc] = kEmpty32;
-#endif
         const u32x4 own = mine.p;
         const float x = __uint_as_float(own.x), y = __uint_as_float(own.y), z = __uint_as_float(own.z);
         // ---- phase A (1): slot + distance (hex.rs:67-85, 55-65) + own child / grandchild slab
@@ -2239,12 +2147,10 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
 #endif
         SlotDest sd;
         bool amb = false;
-#if PCC_HEADS
         // the last step pushes and walks nothing: the head words become the
         // winner bitmap over the arrivals (all ones; dense_grid_points)
         if (ci == nchunks && n <= kDenseStreamMax)
             for (int i = tid; i < (int)((n + 31) / 32); i += BS) S.head[i] = kEmpty32;
-#endif
         if (ci < nchunks) {   // block-uniform: the last step only emits
             sd = slot_dest_fast(x, y, z, G, SC, amb);
         } else {
@@ -2255,14 +2161,12 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
         int32_t lx = sd.ox - rx, ly = sd.oy - ry;
         bool range_ok = lx >= 0 && ly >= 0 && lx < P.tx && ly < P.ty;
         bool slotted = valid && sd.layer_ok && range_ok;
-        uint32_t local = slotted ? (uint32_t)(ly * P.tx + lx) >> kHX : 0u;
+        uint32_t local = slotted ? (uint32_t)(ly * P.tx + lx) : 0u;
         // the slot's occupant, read before the rest of the arithmetic so the LDS
         // latency overlaps it (phase B of the last step wrote the table before
         // the barrier; local 0 for lanes without a slot)
         unsigned long long occ = S.tab[local];
-#if PCC_HEADS
         uint32_t hw = S.head[local >> 1];   // the slot's head word, read with the occupant
-#endif
         if (__ballot(amb)) {
             if (amb) {
                 slot_dest_exact(x, y, z, G, SC, sd);
@@ -2270,11 +2174,9 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
                 ly = sd.oy - ry;
                 range_ok = lx >= 0 && ly >= 0 && lx < P.tx && ly < P.ty;
                 slotted = valid && sd.layer_ok && range_ok;
-                local = slotted ? (uint32_t)(ly * P.tx + lx) >> kHX : 0u;
+                local = slotted ? (uint32_t)(ly * P.tx + lx) : 0u;
                 occ = S.tab[local];
-#if PCC_HEADS
                 hw = S.head[local >> 1];
-#endif
             }
         }
         const bool layer_ok = sd.layer_ok;
@@ -2304,12 +2206,10 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
         uint32_t myprev = kNil;
         if (slotted && !forced) {
             cand = occ == kEmpty64 || d2 < __uint_as_float((uint32_t)(occ >> 33));
-            if (PCC_ABL & 32) cand = false;
         } else {
             occ = kEmpty64;
         }
         if (cand) {
-#if PCC_HEADS
             // push onto the slot's list: swap this thread into the head's half of
             // the word (a CAS retried while other pushes change the word); the
             // old head belongs to this chunk only if its tag is this chunk's
@@ -2321,20 +2221,28 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
             }
             const uint32_t oldh = (hw >> sh) & 0xFFFFu;
             myprev = (oldh >> 11) == tag ? (oldh & kNil) : kNil;
-#else
-            hc = claim_push<CLAIM>(claim, local, tid, myprev);
-            if (hc < 0) { err |= ERR_CLAIM; cand = false; }
-#endif
             S.cd2[tid] = f2u(d2);
             S.cnext[tid] = (uint16_t)myprev;
             S.cdg[tid] = (uint16_t)(dn | ((uint32_t)(gn + 1) << 5));
         }
         STAMP(1);
+#ifdef PCC_XVALU
+        // Diagnostic (issue-bound test): PCC_XVALU independent VALU per step in
+        // four chains, half here and half in phase B, feeding err.
+        uint32_t xv0 = j, xv1 = j ^ 1u, xv2 = j ^ 2u, xv3 = j ^ 3u;
+#pragma unroll
+        for (int xq = 0; xq < PCC_XVALU / 8; xq++) {
+            asm volatile("v_add_u32 %0, %0, %1" : "+v"(xv0) : "v"(tid));
+            asm volatile("v_add_u32 %0, %0, %1" : "+v"(xv1) : "v"(tid));
+            asm volatile("v_add_u32 %0, %0, %1" : "+v"(xv2) : "v"(tid));
+            asm volatile("v_add_u32 %0, %0, %1" : "+v"(xv3) : "v"(tid));
+        }
+#endif
         // ---- phase A (2): wave ranks of chunk i-1's emissions per child slab
         const bool vd = prv.em >= 0;
         const int d = vd ? (int)prv.d : 0;
-        const uint64_t same = (PCC_ABL & 16) ? __ballot(vd) : wave_peers<5>((uint32_t)d, vd);
-        const uint32_t rw = (PCC_ABL & 16) ? 0u : mask_rank(same);
+        const uint64_t same = wave_peers<5>((uint32_t)d, vd);
+        const uint32_t rw = mask_rank(same);
         if (lane < kDests) reinterpret_cast<uint8_t*>(S.wcnt[lane])[wv] = 0;
         if (vd && rw == 0) reinterpret_cast<uint8_t*>(S.wcnt[d])[wv] = (uint8_t)__popcll(same);
         // grandchild capacities: one LDS add per emission
@@ -2344,19 +2252,14 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
                 gg = slot_dest(__uint_as_float(prv.gp.x), __uint_as_float(prv.gp.y), __uint_as_float(prv.gp.z), G,
                                SC).g;
             }
-#if PCC_HEADS
-            if (!(PCC_ABL & 8) && vd && gg >= 0) {
+            if (vd && gg >= 0) {
                 const uint32_t gi = (uint32_t)(d * kDests + gg);
                 atomicAdd(&S.gcnt[gi >> 1], (gi & 1u) ? 0x10000u : 1u);
             }
-#else
-            if (!(PCC_ABL & 8) && vd && gg >= 0) atomicAdd(&S.gcnt[d * kDests + gg], 1u);
-#endif
         }
         STAMP(2);
         lds_barrier();
         STAMP(3);
-#if PCC_HEADS
         // between the barriers nothing pushes or counts: every 16 steps, heads of
         // older chunks go back to kNil (tags are 5 bits), and every 32 steps the
         // 16-bit pair counts move into registers (at most 32 768 adds between)
@@ -2374,7 +2277,6 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
             gacc1 += w >> 16;
             S.gcnt[tid] = 0;
         }
-#endif
         // ---- phase B (1): chunk i-1's emissions.  Position = emissions to the
         // same child slab before the chunk + in earlier waves + earlier lanes.
         {
@@ -2410,14 +2312,12 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
             const int32_t room = __shfl(room_l, d, 64);
             const bool ok = vd && (int32_t)rw < room;
             err |= (vd && !ok) ? (uint32_t)ERR_CAPACITY : 0u;
-            if (!(PCC_ABL & 2)) {
-                bst4(oP, ok ? pos * 16 : 0xFFFFFFFFu, prv.em == 1 ? prv.gp : prvb.p);
-                bst(oK, ok ? pos * 4 : 0xFFFFFFFFu, prvb.k);
-            }
+            bst4(oP, ok ? pos * 16 : 0xFFFFFFFFu, prv.em == 1 ? prv.gp : prvb.p);
+            bst(oK, ok ? pos * 4 : 0xFFFFFFFFu, prvb.k);
             STAMP(6);
         }
         // ---- phase B (2): records of chunk i (walk of the slot's candidate list)
-        int32_t em = (slotted && !cand && (forced || occ != kEmpty64 || (PCC_ABL & 32))) ? 0 : -1;
+        int32_t em = (slotted && !cand && (forced || occ != kEmpty64)) ? 0 : -1;
         uint32_t emd = dn;
         int32_t emg = gn;
         uint32_t gsrc = 0xFFFFFFFFu;   // byte offset of a displaced point's payload
@@ -2428,11 +2328,7 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
             uint32_t bd = 0xFFFFFFFFu, bt = kNil;
             bool beaten = false;
             // branch-free body; the own entry is skipped (known without LDS reads)
-#if PCC_HEADS
             uint32_t xk = (S.head[local >> 1] >> ((local & 1u) * 16u)) & kNil;
-#else
-            uint32_t xk = claim[hc] & kNil;
-#endif
             if (xk == tid) xk = myprev;
             while (xk != kNil) {
                 const uint32_t dx = S.cd2[xk];
@@ -2452,7 +2348,7 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
                     em = 1;
                     emd = dg & 31u;
                     emg = (int32_t)(dg >> 5) - 1;
-                    gsrc = (ng + cg * BS + bt) * 16;
+                    gsrc = (ng + ci * BS + bt) * 16;
                 } else if (occ != kEmpty64) {          // first record: displaces the occupant
                     em = 1;
                     emd = (uint32_t)(occ >> kJBits) & 31u;
@@ -2464,11 +2360,21 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
                                    (wide ? 0u : ((uint32_t)(gn + 1) << 23)) | j;
             }
         }
+#ifdef PCC_XVALU
+#pragma unroll
+        for (int xq = 0; xq < PCC_XVALU / 8; xq++) {
+            asm volatile("v_add_u32 %0, %0, %1" : "+v"(xv0) : "v"(tid));
+            asm volatile("v_add_u32 %0, %0, %1" : "+v"(xv1) : "v"(tid));
+            asm volatile("v_add_u32 %0, %0, %1" : "+v"(xv2) : "v"(tid));
+            asm volatile("v_add_u32 %0, %0, %1" : "+v"(xv3) : "v"(tid));
+        }
+        if ((xv0 ^ xv1 ^ xv2 ^ xv3) == 0x9E3779B9u) err |= 1u << 27;
+#endif
         STAMP(4);
         STAMP_COUNT(9, 1);
         // gather outside the divergent branches (a load into registers that
         // another branch writes would force a full vmcnt drain); stored next step
-        cur.gp = rP.p((PCC_ABL & 4) ? 0xFFFFFFFFu : gsrc);
+        cur.gp = rP.p(gsrc);
         cur.em = em; cur.d = emd; cur.g = emg; cur.hc = hc;
         lds_barrier();
         STAMP(5);
@@ -2500,7 +2406,6 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
     STAMP(7);
     lds_barrier();   // LDS only: the last emission stores need not land
     STAMP(11);
-#if PCC_HEADS
     if (tid < kDests * kDests / 2) {
         const uint32_t w = S.gcnt[tid];
         gacc0 += w & 0xFFFFu;
@@ -2510,44 +2415,22 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
     unsigned long long* st_acc = nullptr, st_t0 = 0;
 #endif
     dense_grid_points<L>(P, S, S.head, rP, s, n, jmask, tid, lane, st_acc, st_t0);
-#else
-#ifndef PCC_STAMPS
-    unsigned long long* st_acc = nullptr, st_t0 = 0;
-#endif
-    dense_grid_points<L>(P, S, &S.claim[0][0], rP, s, n, jmask, tid, lane, st_acc, st_t0);
-#endif
     STAMP(8);
     STAMP_FLUSH(P.stamps);
-    if (kHX) err = 0;
     if (err) atomicOr(&S.err, err);
     lds_barrier();
     const uint32_t fp = nchunks & 1;   // dcur after the last (emit-only) step
-    if (tid == 0 && hx == 0) {
+    if (tid == 0) {
         P.slab_grid_n[s] = S.nwin;
         if (S.err) set_err(P.ctr, S.err);
     }
-    if (kHX) {   // both halves add (zeroed before the launch)
-        const uint32_t dc = S.dcap[tid % kDests];
-        const uint32_t hcap = (uint32_t)((uint64_t)dc * (hx + 1) >> kHX) - (uint32_t)((uint64_t)dc * hx >> kHX);
-        if (tid < kDests) atomicAdd(&P.dest_n[s * kDests + tid], S.dcur[fp][tid] < hcap ? S.dcur[fp][tid] : hcap);
-        for (int i = tid; i < kDests * kDests; i += BS)
-            if (S.gcnt[i]) atomicAdd(&P.gcap[(uint64_t)s * kDests * kDests + i], S.gcnt[i]);
-        return;
-    }
     if (tid < kDests) P.dest_n[s * kDests + tid] = S.dcur[fp][tid] < my_dcap ? S.dcur[fp][tid] : my_dcap;   // wave 0: lane = tid
     // capacities of the child slabs' own child slabs (only rows that will exist)
-#if PCC_HEADS
     if (tid < kDests * kDests / 2) {
         const uint32_t i0 = 2 * tid, i1 = 2 * tid + 1;
         if (S.dcur[fp][i0 / kDests]) P.gcap[(uint64_t)s * kDests * kDests + i0] = gacc0;
         if (S.dcur[fp][i1 / kDests]) P.gcap[(uint64_t)s * kDests * kDests + i1] = gacc1;
     }
-#else
-    for (int i = tid; i < kDests * kDests; i += BS) {
-        const int dd = i / kDests;
-        if (S.dcur[fp][dd]) P.gcap[(uint64_t)s * kDests * kDests + i] = S.gcnt[i];
-    }
-#endif
 }
 
 // Small slabs (< kSmallMax arrivals): at most kSmallCh chunks of kSmallBS, so a
@@ -2979,22 +2862,17 @@ __global__ __launch_bounds__(kSmallBS) void k_slab_small(SlabParams P) {
 // ------------------------------------------------------------------ one wave per slab
 // Slabs of < kWaveMax arrivals (most of the deepest levels): one 64-lane wave
 // per slab, one workgroup per slab, ~13 KB of LDS each so a CU holds ~11
-// slabs at once, and no s_barrier between waves.  Same-slot arrivals of a
-// 64-arrival chunk are applied in lane (= key) order by claim rounds on the slot
-// key word (claim lane in the top byte); LDS operations of one wave execute in
-// program order.  Grandchild capacities are counted in LDS (two 16-bit counters
-// per word: a slab has < 512 arrivals) and stored once per slab.
-// Instantiated per size class (CH chunks of 64: slabs of < 64 * CH arrivals,
-// table 128 * CH entries), so the classes of small slabs hold less LDS and
-// fewer registers and more of them fit on a CU.
-constexpr uint32_t kNoClaim = 0x7Fu << 24;
+// slabs at once, and no s_barrier between waves.  The table entry holds the
+// slot key beside the occupant, and same-slot arrivals of a 64-arrival chunk
+// are applied in lane (= key) order, one ballot rank per round.  Grandchild
+// capacities are counted in LDS (two 16-bit counters per word: a slab has < 512
+// arrivals) and stored once per slab.  Instantiated per size class (CH chunks
+// of 64: slabs of < 64 * CH arrivals, table 128 * CH entries), so the classes of
+// small slabs hold less LDS and fewer registers and more of them fit on a CU.
 template <int CH>
 struct WaveLds {
     static constexpr int TAB = 128 * CH;
     unsigned long long tab[TAB];
-#if !PCC_WAVE2
-    uint32_t tkey[TAB];          // (claim lane << 24) | slot, kEmpty32 = empty
-#endif
     uint16_t fate[64 * CH];
     uint32_t doff[kDests], dcap[kDests], dcur[kDests];
     uint32_t gcnt[kDests * kDests / 2];   // (child, grandchild) counts, 16 bits each
@@ -3004,9 +2882,17 @@ __device__ __forceinline__ void wave_gcount(WL& W, bool active, uint32_t key) {
     if (active) atomicAdd(&W.gcnt[key >> 1], (key & 1u) ? 0x10000u : 1u);
 }
 
-// PCC_WAVE2 entry: (d2 bits << 33) | (dest << 28) | (slot << 14) | j, j < 2^14; a
-// slot taken with no occupant yet has d2 bits 0x7FFFFFFF (kEmpty64: no slot)
+// Entry: (d2 bits << 33) | (dest << 28) | (slot << 14) | j, j < 2^14; a slot
+// taken with no occupant yet has d2 bits 0x7FFFFFFF (kEmpty64: no slot).  The
+// packed fields bound the geometry: slot indices of a dim-96 layer (< kDenseTab)
+// fit 14 bits below the reserved 0x3FFF, dest 0..23 fits 5 bits, and the
+// per-chunk register (entry + 1 in 11 bits, wave_peers<10> of the entry) needs
+// TAB <= 1024 entries.
 constexpr unsigned long long kW2None = 0x7FFFFFFFull << 33;
+static_assert(kDenseTab < (1 << 14) - 1, "wave-kernel entry: slot in 14 bits");
+static_assert(kDests < 31, "wave-kernel entry: dest in 5 bits");
+static_assert(128 * (kWaveMax / 64) <= 1024, "wave-kernel entry index: 10-bit peers, 11-bit entry + 1");
+static_assert(kWaveMax <= (1u << 14), "wave-kernel entry: j in 14 bits");
 __device__ __forceinline__ unsigned long long w2_reserved(uint32_t local) {
     return kW2None | (31ull << 28) | ((unsigned long long)local << 14) | 0x3FFFull;
 }
@@ -3022,20 +2908,8 @@ __device__ __forceinline__ int wave_entry2(WL& W, uint32_t local, uint32_t mask)
     return -1;
 }
 
-template <class WL>
-__device__ __forceinline__ int wave_entry(WL& W, uint32_t local, uint32_t mask) {
-    uint32_t h = hash_slot(local) & mask;
-    for (uint32_t probe = 0; probe <= mask; probe++) {
-        // CAS first: a new or already present slot costs one LDS round trip
-        const uint32_t old = atomicCAS(&W.tkey[h], kEmpty32, kNoClaim | local);
-        if (old == kEmpty32 || (old & 0xFFFFFFu) == local) return (int)h;
-        h = (h + 1) & mask;
-    }
-    return -1;
-}
-
 #ifndef PCC_WAVE_OCC
-#define PCC_WAVE_OCC 4   // k_slab_wave: minimum waves per SIMD asked of the compiler (115 VGPRs for 8 chunks, no spills)
+#define PCC_WAVE_OCC 4   // k_slab_wave: minimum waves per SIMD asked of the compiler (<= 128 VGPRs, no spills)
 #endif
 template <int CH>
 __global__ __launch_bounds__(64, PCC_WAVE_OCC) void k_slab_wave(SlabParams P) {
@@ -3078,11 +2952,7 @@ __global__ __launch_bounds__(64, PCC_WAVE_OCC) void k_slab_wave(SlabParams P) {
                 pk[c] = bld(rK, v ? j * 4 : 0xFFFFFFFFu);
             }
         }
-#if PCC_WAVE2
         for (uint32_t i = lane; i < cap; i += 64) W.tab[i] = kEmpty64;
-#else
-        for (uint32_t i = lane; i < cap; i += 64) { W.tab[i] = kEmpty64; W.tkey[i] = kEmpty32; }
-#endif
         for (uint32_t i = lane; i < kDests * kDests / 2; i += 64) W.gcnt[i] = 0;
         if (lane < kDests) {
             W.dcur[lane] = 0;
@@ -3097,21 +2967,11 @@ __global__ __launch_bounds__(64, PCC_WAVE_OCC) void k_slab_wave(SlabParams P) {
         uint32_t err = 0;
         __syncthreads();   // one wave: orders the LDS initialisation
 
-#if PCC_WAVE2
         // per chunk, one register: (entry + 1, 0 none) | own child slab << 11 | (own grandchild slab + 1) << 16
         uint32_t own[CH];
-#else
-        int32_t rec_e[CH], own_d[CH], own_g[CH];
-#endif
 #pragma unroll
         for (int c = 0; c < CH; c++) {
-#if PCC_WAVE2
             own[c] = 0u;
-#else
-            rec_e[c] = -1;
-            own_d[c] = 0;
-            own_g[c] = -1;
-#endif
             if ((uint32_t)c >= nch) continue;   // wave-uniform
             const uint32_t j = c * 64 + lane;
             const bool valid = j < n;
@@ -3132,12 +2992,7 @@ __global__ __launch_bounds__(64, PCC_WAVE_OCC) void k_slab_wave(SlabParams P) {
                 if (bad) err |= slot_route_errs(slot_route(x, y, z, G), layer_ok, range_ok, cx, cy, cz, t, P.check_gchild);
             }
             const uint32_t dn = d < 0 ? 0u : (uint32_t)d;
-#if PCC_WAVE2
             own[c] = (dn << 11) | ((uint32_t)(g + 1) << 16);
-#else
-            own_d[c] = (int32_t)dn;
-            own_g[c] = g;
-#endif
             int e = 0;
             int32_t em = -1;
             uint32_t emj = 0, emd = 0;
@@ -3146,7 +3001,6 @@ __global__ __launch_bounds__(64, PCC_WAVE_OCC) void k_slab_wave(SlabParams P) {
                 em = 0;
                 emd = dn;
             }
-#if PCC_WAVE2
             if (pending) {
                 e = wave_entry2(W, local, mask);
                 if (e < 0) {
@@ -3162,21 +3016,25 @@ __global__ __launch_bounds__(64, PCC_WAVE_OCC) void k_slab_wave(SlabParams P) {
                 }
             }
             {   // same-slot lanes applied in lane (= key) order: rank among the
-                // pending lanes of the same entry, one rank per round (one wave:
-                // its LDS operations execute in program order)
+                // pending lanes of the same entry, one rank per round.  One wave's
+                // LDS operations execute in program order; the entry is read and
+                // written as wavefront-scope atomics, so the compiler can neither
+                // reuse the pre-filter's load nor reorder a round's store past the
+                // next round's load (lane A writes in round r, lane B reads in r+1)
                 const uint64_t same = wave_peers<10>((uint32_t)(pending ? e : 0), pending);
                 const uint32_t rk = (uint32_t)__popcll(same & lt);
                 for (uint32_t r = 0; __ballot(pending && rk >= r); r++) {
                     if (pending && rk == r) {
-                        const unsigned long long occ = W.tab[e];
+                        const unsigned long long occ =
+                            __hip_atomic_load(&W.tab[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
                         const unsigned long long mine = ((unsigned long long)f2u(d2) << 33) |
                                                         ((unsigned long long)dn << 28) |
                                                         ((unsigned long long)local << 14) | j;
                         if ((occ >> 33) == 0x7FFFFFFFull) {
-                            W.tab[e] = mine;
+                            __hip_atomic_store(&W.tab[e], mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
                             own[c] |= (uint32_t)(e + 1);
                         } else if (d2 < __uint_as_float((uint32_t)(occ >> 33))) {   // strict: ties keep the old point
-                            W.tab[e] = mine;
+                            __hip_atomic_store(&W.tab[e], mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
                             own[c] |= (uint32_t)(e + 1);
                             em = 1;
                             emj = (uint32_t)occ & 0x3FFFu;
@@ -3188,51 +3046,6 @@ __global__ __launch_bounds__(64, PCC_WAVE_OCC) void k_slab_wave(SlabParams P) {
                         pending = false;
                     }
                 }
-            }
-#else
-            if (pending) {
-                e = wave_entry(W, local, mask);
-                if (e < 0) {
-                    err |= ERR_CLAIM;
-                    pending = false;
-                } else {   // occupant pre-filter (see k_slab)
-                    const unsigned long long occ = W.tab[e];
-                    if (occ != kEmpty64 && !(d2 < __uint_as_float((uint32_t)(occ >> 33)))) {
-                        pending = false;
-                        em = 0;
-                        emd = dn;
-                    }
-                }
-            }
-#endif
-            // claim rounds inside the wave: the lowest pending lane of each slot is applied
-            while (!PCC_WAVE2 && __ballot(pending)) {
-#if !PCC_WAVE2
-                if (pending) atomicMin(&W.tkey[e], (lane << 24) | local);
-                __syncthreads();
-                const bool win = pending && (W.tkey[e] >> 24) == lane;
-                if (win) {
-                    const unsigned long long occ = W.tab[e];
-                    const unsigned long long mine =
-                        ((unsigned long long)f2u(d2) << 33) | ((unsigned long long)dn << kJBits) | j;
-                    if (occ == kEmpty64) {
-                        W.tab[e] = mine;
-                        rec_e[c] = e;
-                    } else if (d2 < __uint_as_float((uint32_t)(occ >> 33))) {   // strict: ties keep the old point
-                        W.tab[e] = mine;
-                        rec_e[c] = e;
-                        em = 1;
-                        emj = (uint32_t)occ & kJMask;
-                        emd = (uint32_t)(occ >> kJBits) & 31u;
-                    } else {
-                        em = 0;
-                        emd = dn;
-                    }
-                    pending = false;
-                    W.tkey[e] = kNoClaim | local;
-                }
-                __syncthreads();
-#endif
             }
             // emissions of this chunk, in lane order per child slab
             const bool vd = em >= 0;
@@ -3262,7 +3075,6 @@ __global__ __launch_bounds__(64, PCC_WAVE_OCC) void k_slab_wave(SlabParams P) {
             if ((uint32_t)c >= nch) break;
             const uint32_t j = c * 64 + lane;
             bool win = false, dsp = false;
-#if PCC_WAVE2
             const int32_t rec = (int32_t)(own[c] & 0x7FFu) - 1;
             const int32_t od = (int32_t)((own[c] >> 11) & 31u), og = (int32_t)((own[c] >> 16) & 31u) - 1;
             if (rec >= 0) {
@@ -3270,14 +3082,6 @@ __global__ __launch_bounds__(64, PCC_WAVE_OCC) void k_slab_wave(SlabParams P) {
                 win = ((uint32_t)occ & 0x3FFFu) == j;
                 dsp = !win;
             }
-#else
-            const int32_t od = own_d[c], og = own_g[c];
-            if (rec_e[c] >= 0) {
-                const unsigned long long occ = W.tab[rec_e[c]];
-                win = ((uint32_t)occ & kJMask) == j;
-                dsp = !win;
-            }
-#endif
             const uint64_t m = __ballot(win);
             bst4(rG, win ? (nwin + (uint32_t)__popcll(m & lt)) * 16 : 0xFFFFFFFFu, pp[c]);
             nwin += (uint32_t)__popcll(m);
@@ -4827,13 +4631,9 @@ int Engine::run_level(uint32_t li) {
 #ifdef PCC_STAMPS
         SP.stamps = stamps;
 #endif
-        if (kHX) {
-            HIP_CHECK(hipMemsetAsync(L->dest_n, 0, (uint64_t)L->nslabs * kDests * 4, stream_));
-            HIP_CHECK(hipMemsetAsync(L->gcap, 0, (uint64_t)L->nslabs * kDests * kDests * 4, stream_));
-        }
         ev_begin(ST_DENSE);
-        if (seeds_in_place) k_slab<true><<<L->nbig << kHX, kDenseBS, 0, stream_>>>(SP);
-        else k_slab<false><<<L->nbig << kHX, kDenseBS, 0, stream_>>>(SP);
+        if (seeds_in_place) k_slab<true><<<L->nbig, kDenseBS, 0, stream_>>>(SP);
+        else k_slab<false><<<L->nbig, kDenseBS, 0, stream_>>>(SP);
         ev_end(ST_DENSE);
         if (verbose) {
             HIP_CHECK(hipStreamSynchronize(stream_));
@@ -4943,7 +4743,7 @@ int Engine::run_level(uint32_t li) {
     L->kept_used = hc.kept_cur;
     stats_.grid_points += hg;
     stats_.kept_points += hc.kept_cur;
-    if (hc.err && !kHX) {
+    if (hc.err) {
         char buf[200];
         snprintf(buf, sizeof buf,
                  "device error flags 0x%x at level %u (1 slot range, 2 layer, 4 octant, 8 sel, 16 kept cap, 64 capacity, "

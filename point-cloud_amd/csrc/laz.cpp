@@ -1722,6 +1722,13 @@ bool Reader::open(FILE* f, uint64_t data_off, uint64_t npoints, uint16_t rec, co
         uint32_t hdr[2];
         if (fread(hdr, 4, 2, f) != 2) { err = "truncated LAZ chunk table"; return false; }
         const uint32_t nchunks = hdr[1];
+        const bool variable = v.chunk_size == 0xFFFFFFFFu;
+        // a chunk holds at least one point, and fixed-size chunks exactly
+        // ceil(npoints / chunk_size) of them: anything larger is a corrupt table
+        // (and would size the vectors below from untrusted bytes)
+        const uint64_t max_chunks = variable ? std::max<uint64_t>(npoints, 1)
+                                             : (v.chunk_size ? (npoints + v.chunk_size - 1) / v.chunk_size : 0);
+        if (nchunks > max_chunks) { err = "bad LAZ chunk count"; return false; }
         std::vector<uint8_t> tb((size_t)(fsize - (uint64_t)table - 8));
         if (!tb.empty() && fread(tb.data(), 1, tb.size(), f) != tb.size()) { err = "truncated LAZ chunk table"; return false; }
         Decoder d;
@@ -1729,7 +1736,6 @@ bool Reader::open(FILE* f, uint64_t data_off, uint64_t npoints, uint16_t rec, co
         IntegerCompressor ic(false, 32, 2);
         ic.init();
         std::vector<uint64_t> sizes(nchunks), counts(nchunks);
-        const bool variable = v.chunk_size == 0xFFFFFFFFu;
         int32_t pc = 0, ps = 0;
         for (uint32_t i = 0; i < nchunks; i++) {
             if (variable) counts[i] = (uint32_t)(pc = ic.decompress(d, pc, 0));
@@ -1740,7 +1746,7 @@ bool Reader::open(FILE* f, uint64_t data_off, uint64_t npoints, uint16_t rec, co
         for (uint32_t i = 0; i < nchunks; i++) {
             pos += sizes[i];
             chunk_start_.push_back(pos);
-            const uint64_t c = variable ? counts[i] : std::min<uint64_t>(v.chunk_size, npoints - done);
+            const uint64_t c = std::min<uint64_t>(variable ? counts[i] : v.chunk_size, npoints - done);
             chunk_pts_.push_back(c);
             done += c;
         }

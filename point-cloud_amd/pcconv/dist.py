@@ -716,8 +716,21 @@ class HipShardOps:
     def build(self, file_points, pts: torch.Tensor, keys: torch.Tensor | None) -> dict:
         """keys None: this rank holds the whole input in key order (keys 0..n-1).
         The build reads `pts`/`keys` in place (borrowed until it returns)."""
-        self.last_inputs = {"build": (file_points, pts, keys)}
+        self._record("build", (file_points, pts, keys), first=True)
         return self._keyed_build(self.conv, file_points, pts, keys)
+
+    # Diagnostics only (scripts/rank_stages.py replays a step's local calls): with
+    # record_inputs set, every stage's device inputs are kept in last_inputs until
+    # the next step or close().  Off in the product: they would hold GBs of
+    # device memory per rank into the next step's exchange.
+    record_inputs = False
+
+    def _record(self, stage, args, first=False):
+        if not self.record_inputs:
+            return
+        if first or not hasattr(self, "last_inputs"):
+            self.last_inputs = {}
+        self.last_inputs[stage] = args
 
     def _keyed_build(self, c, file_points, pts, keys, roots=None) -> dict:
         self._ready()
@@ -736,7 +749,7 @@ class HipShardOps:
         forwarded).  Returns (stats, (level-1 cells (n,3), -, points per cell,
         their emissions (m,4), causing keys), partial level-0 cells [{xyz, grid}])."""
         c = self.conv_lead
-        self.last_inputs["lead"] = (file_points, pts, keys)
+        self._record("lead", (file_points, pts, keys))
         st = self._keyed_build(c, file_points, pts, keys)
         _, m = c.pending_cells()
         P = torch.empty((m, 4), dtype=torch.int32, device=pts.device)
@@ -753,8 +766,7 @@ class HipShardOps:
         """Module resolve_level1 on the device (pcc_shard_resolve_buckets): the
         same outputs, with only the segment table and the bucket states crossing
         to the host."""
-        if hasattr(self, "last_inputs"):
-            self.last_inputs["resolve"] = (rmeta, pts, keys, file_points)
+        self._record("resolve", (rmeta, pts, keys, file_points))
         rmeta = np.asarray(rmeta, dtype=np.int64).reshape(-1, 4)
         rmeta = rmeta[rmeta[:, 3] > 0]   # empty segments carry no rows
         dev = pts.device
@@ -783,7 +795,7 @@ class HipShardOps:
     def sub_build(self, file_points, pts: torch.Tensor, keys: torch.Tensor, cells_xyz, spill_batch) -> dict:
         """The level-1 sub-trees of split cells this rank owns (their arrivals, cell
         after cell, from the leaders' pcc_export_pending)."""
-        self.last_inputs["sub"] = (file_points, pts, keys, cells_xyz, spill_batch)
+        self._record("sub", (file_points, pts, keys, cells_xyz, spill_batch))
         return self._keyed_build(self.conv_sub, file_points, pts, keys, roots=(cells_xyz, spill_batch))
 
     def _outputs(self):
@@ -817,6 +829,7 @@ class HipShardOps:
             if c is not None:
                 c.close()
         self.conv = self.conv_lead = self.conv_sub = None
+        self.last_inputs = {}
         # the library's device cache is invisible to PyTorch's allocator and RCCL
         pcconv.release_device_cache()
         if self._tmp is not None:

@@ -95,6 +95,7 @@ def worker(rank, world, port, args, res_dir):
         pcconv.synth_device(pts.data_ptr(), a, b - a, args.seed, args.kind, -1000.0, 2000.0, 0)
         torch.cuda.synchronize()
         ops = RecOps(HipShardOps(0, batch_size=10_000))
+        ops.o.record_inputs = True
         # the host-only pieces of the plan and assembly stages, recorded too so
         # they can be timed alone (measured inside the step they include waits
         # for a GPU the other ranks share)

@@ -245,7 +245,6 @@ def test_export_grid_equals_visited_cells():
     ops = HipShardOps(0, batch_size=5000, config=SKEW_CFG)
     try:
         ops.begin_step()
-        ops.last_inputs = {}
         _, _, (pxyz, pn, G) = ops.lead_build_raw([n], pts[a:b], keys)
         seen = []
 

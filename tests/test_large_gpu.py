@@ -173,6 +173,108 @@ def test_visit_digest_equals_oracle_digest_small():
         assert err == 0 and d == [] and mg == mo
 
 
+def _sharded_synth_threads(world, s, out_dir=None, merge=False):
+    """`world` thread ranks sharing cuda:0 (pcconv.dist.ThreadComm): rank r
+    generates its key range of the synthetic stream `s` in HBM and runs the
+    product's sharded step (HipShardOps -> libpcconv.so).  Returns the per-rank
+    results and the digest of the union of the ranks' cells."""
+    import threading
+
+    import torch
+    from oracle_ctypes import Digest
+    from pcconv.dist import HipShardOps, ThreadComm, ThreadGroup, key_range, shard_build
+    dev = torch.device("cuda", 0)
+    grp = ThreadGroup(world)
+    res, ops, errs = [None] * world, [None] * world, []
+
+    def worker(r):
+        try:
+            torch.cuda.set_device(dev)
+            a, b = key_range(s["n"], r, world)
+            pts = torch.empty((b - a, 4), dtype=torch.int32, device=dev)
+            pcconv.synth_device(pts.data_ptr(), a, b - a, s["seed"], s["kind"], -1000.0, 2000.0, 0)
+            torch.cuda.synchronize()
+            ops[r] = HipShardOps(0, out_dir=out_dir, merge=merge)
+            res[r] = shard_build(ThreadComm(grp, r, dev), ops[r], pts, a, [s["n"]], merge=merge)
+        except BaseException as e:  # noqa: BLE001
+            errs.append(e)
+            grp.bar.abort()
+
+    th = [threading.Thread(target=worker, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    try:
+        assert not errs, errs
+        d = Digest()
+        for o in ops:
+            o.visit_cells(lambda v: d.add_view(v) or 0)
+        got = d.result()
+        d.close()
+    finally:
+        for o in ops:
+            if o is not None:
+                o.close()
+    return res, got
+
+
+def test_config4_sharded_8_ranks_octants():
+    """Config 4 as BASELINE names it (1B uniform, top-octant sharding over 8
+    ranks), here as 8 thread ranks on the box's one GPU: each rank generates its
+    contiguous key range (125M points) in HBM, the points are routed to the owners
+    of their level-0 cells (one octant per rank, nothing shared) and every rank
+    builds its sub-tree.  The union of the ranks' cells must give the oracle's
+    digests (converter.rs:114-139: level-0 sub-trees are independent).  The
+    exchange is ThreadComm's device copies: no RCCL/xGMI run is involved."""
+    fx = fixture("config4")
+    s = fx["synth"]
+    res, got = _sharded_synth_threads(8, s)
+    assert got["subtrees"] == fx["subtrees"]
+    assert (got["grid_points"], got["kept_points"]) == (fx["grid_points"], fx["kept_points"])
+    assert sum(r.local["arrivals"] for r in res) == fx["arrivals"]
+    assert sorted(r.owned_cells for r in res) == [1] * 8
+    assert sum(r.recv_points for r in res) == s["n"]
+    assert res[0].summary["hierarchies"] == fx["hierarchies"]
+    bits = np.array(res[0].summary["bbox_min"] + res[0].summary["bbox_max"], dtype=np.float32).view(np.uint32)
+    assert bits.tolist() == fx["bbox_bits"]
+
+
+def test_config5_sharded_merge_8_ranks_from_disk():
+    """Config 5 as BASELINE names it (+100M merged into the 1B cloud, 8 ranks):
+    the 1B cloud is built and written as cell files, then 8 thread ranks each
+    open the existing cloud for the level-0 sub-tree they own
+    (pcc_open_subtrees, converter.rs:187-207 for their own cells), merge their
+    routed share of the new points and the union of their cells must give the
+    oracle's digests of the merged cloud.  No RCCL/xGMI run is involved."""
+    import shutil
+    import tempfile
+    fx = fixture("config5")
+    p, s = fx["prior_synth"], fx["synth"]
+    base = tempfile.mkdtemp(prefix="pcc_cfg5_shard_", dir="/tmp")
+    try:
+        if shutil.disk_usage(base).free < 40e9:
+            pytest.skip("needs 16 GB of cell files under /tmp")
+        prior = pcconv.Converter(base)
+        try:
+            prior.add_synthetic(p["seed"], p["kind"], p["n"])
+            prior.build()
+            prior.write()
+        finally:
+            prior.close()
+        pcconv.release_device_cache()
+        res, got = _sharded_synth_threads(8, s, out_dir=base, merge=True)
+        assert got["subtrees"] == fx["subtrees"]
+        assert (got["grid_points"], got["kept_points"]) == (fx["grid_points"], fx["kept_points"])
+        assert sum(r.recv_points for r in res) == s["n"]
+        assert res[0].summary["number_of_points"] == p["n"] + s["n"]
+        assert res[0].summary["hierarchies"] == fx["hierarchies"]
+        bits = np.array(res[0].summary["bbox_min"] + res[0].summary["bbox_max"], dtype=np.float32).view(np.uint32)
+        assert bits.tolist() == fx["bbox_bits"]
+    finally:
+        shutil.rmtree(base, ignore_errors=True)
+
+
 def test_config3_sharded_8_ranks_split_cells():
     """Config 3 by 8 ranks (threads sharing cuda:0, pcconv.dist.ThreadComm): each
     rank generates its key range in HBM; the heavy level-0 cells are split at
