@@ -149,6 +149,7 @@ struct BuildStats {
     uint64_t grid_points = 0, kept_points = 0;
     double ms_total = 0, ms_level0_bin = 0;
     uint64_t pre0_tiles = 0;                       // level-0 pass-0 tiles counted while the input uploaded
+    uint32_t l0_fold = 0;                          // level-0 binning with pass 0 folded into pass 1
     std::vector<double> ms_level;                  // per level (slab + bucket kernels)
 };
 
@@ -246,6 +247,7 @@ private:
     void ev_end(int stage);
     void ev_collect();
     int level0_bin();
+    bool fold_hint(float cs);
     // level-0 pass 0 behind the host-to-device copy (add_file_host, streamed files)
     void pre0_count(uint64_t upto, hipEvent_t after, bool all);
     void pre0_reset();

@@ -1458,6 +1458,227 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_down6g(const Point* __restrict_
     if (err) set_err(ctr, err);
 }
 
+// ---- level-0 binning with pass 0 folded into pass 1 (grids of at most two
+// level-0 cells per axis).  k_l0_tile6 writes every tile IN PLACE, partitioned by
+// the low 6 layer bits d6 (tile-major: a tile's output range is its input range,
+// so no global digit offsets and no counting pass are needed), and records per
+// tile its digit counts (cnt6, digit-major: the exclusive scan of cnt6 is the
+// position of each tile's run in the digit-partitioned order k_l0_down6g writes)
+// and its digit starts inside the tile (lp6); per group the (d6, d5) pair counts,
+// with the cell part of d5 taken from the PARITY of the absolute cell indices
+// (the grid is unknown until the bounding box is; parities name the cells of a
+// grid of at most two cells per axis, which the host checks after the pass and
+// otherwise falls back to the three-pass binning); and the bounding box
+// (converter.rs:96-104).  k_l0_down5g<., true> then walks each d6 bucket as the
+// sequence of that digit's runs, tile after tile, i.e. in key order.
+template <bool KEYS>
+__global__ __launch_bounds__(kL0BS, 8) void k_l0_tile6(const Point* __restrict__ in, const uint32_t* __restrict__ keys,
+                                                       Arena O, uint64_t n, L0Params P, uint32_t ntiles, uint32_t tpg,
+                                                       uint32_t ngroups, uint32_t* __restrict__ cnt6,
+                                                       uint16_t* __restrict__ lp6, uint32_t* __restrict__ gcnt,
+                                                       float* __restrict__ part, uint32_t* __restrict__ flag,
+                                                       Arena dummy) {
+    constexpr int R = 64, R5 = 32, HP = R5 + 1;
+    using KT = typename std::conditional<KEYS, uint32_t, uint16_t>::type;
+    __shared__ float4 sp[kL0Tile];
+    __shared__ KT sk[kL0Tile];
+    __shared__ alignas(16) uint8_t wcnt[R][kL0RW];
+    __shared__ alignas(16) uint16_t wpre[R][kL0RW];
+    __shared__ uint32_t dbase[R];
+    __shared__ uint32_t h[R * HP];
+    __shared__ float sb[kL0W][6];
+    const uint32_t tid = threadIdx.x, w = tid / 64, lane = tid & 63, g = blockIdx.x;
+    const float4* p4 = reinterpret_cast<const float4*>(in);
+    for (int i = tid; i < R * HP; i += kL0BS) h[i] = 0;
+    for (int i = tid; i < kL0RW * R / 4; i += kL0BS) reinterpret_cast<uint32_t*>(&wcnt[0][0])[i] = 0;
+    const uint64_t lt = lanemask_lt();
+    float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+    bool bad = false;
+    const uint32_t t0 = g * tpg, t1 = min(t0 + tpg, ntiles);
+    auto load_tile = [&](float4* v, uint32_t* kk, uint32_t tile) {   // unconditional, clamped (see k_l0_down6g)
+        const uint64_t base = (uint64_t)tile * kL0Tile;
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int r = 0; r < kL0IPT; r++) {
+            const uint64_t i = min(base + (uint64_t)r * kL0BS + tid, n - 1);
+            v[r] = p4[i];
+            if constexpr (KEYS) kk[r] = keys[i];
+        }
+        asm volatile("" ::: "memory");
+    };
+    auto body = [&](uint32_t tile, float4* v, uint32_t* kk, uint32_t pf) {
+        const uint64_t base = (uint64_t)tile * kL0Tile;
+        lds_barrier();   // the last tile's stores have read the staging arrays
+        uint32_t dgp = 0, rwp = 0;
+#pragma unroll
+        for (int r = 0; r < kL0IPT; r++) {
+            const uint64_t i = base + (uint64_t)r * kL0BS + tid;
+            const bool valid = i < n;
+            uint32_t d6 = 0;
+            if (valid) {
+                const float x = v[r].x, y = v[r].y, z = v[r].z;
+                bad |= !(isfinite(x) && isfinite(y) && isfinite(z));
+                mn[0] = fminf(mn[0], x); mn[1] = fminf(mn[1], y); mn[2] = fminf(mn[2], z);
+                mx[0] = fmaxf(mx[0], x); mx[1] = fmaxf(mx[1], y); mx[2] = fmaxf(mx[2], z);
+            }
+            // cell indices (metadata.rs:100-102) and the layer relative to the
+            // cell's first one, exact quotients, IEEE lanes behind one ballot
+            bool amb = !rc_ok(v[r].x) || !rc_ok(v[r].y);
+            int32_t iz;
+            int64_t ll = l0_layer_rc(P, v[r].z, iz, amb);
+            int32_t ix = sat_i32(floorf(div_rc(v[r].x, P.cs, P.inv_cs)));
+            int32_t iy = sat_i32(floorf(div_rc(v[r].y, P.cs, P.inv_cs)));
+            if (__ballot(valid && amb)) {
+                if (valid && amb) {
+                    ll = l0_layer(P, v[r].z, iz);
+                    ix = cell_index1(v[r].x, P.cs);
+                    iy = cell_index1(v[r].y, P.cs);
+                }
+            }
+            if (valid) {
+                bad |= ll < 0 || ll >= (int64_t)kL0Layers;
+                d6 = (uint32_t)ll & (R - 1);
+                const uint32_t par = (uint32_t)(ix & 1) | ((uint32_t)(iy & 1) << 1) | ((uint32_t)(iz & 1) << 2);
+                atomicAdd(&h[d6 * HP + ((par << 2) | (((uint32_t)ll >> 6) & 3u))], 1u);
+            }
+            const uint64_t same = wave_peers<6>(d6, valid);
+            const uint32_t rw = (uint32_t)__popcll(same & lt);
+            if (valid && rw == 0) wcnt[d6][r * kL0W + w] = (uint8_t)__popcll(same);
+            dgp |= d6 << (8 * r);
+            rwp |= rw << (8 * r);
+        }
+        lds_barrier();
+        if (w == 0) {
+            uint32_t ex;
+            const uint32_t tot = l0_tile_prefix<R>(wcnt, wpre, lane, ex);
+            dbase[lane] = ex;
+            cnt6[(uint64_t)lane * ntiles + tile] = tot;   // this tile's run of digit `lane`: length and start
+            lp6[(uint64_t)tile * R + lane] = (uint16_t)ex;
+        }
+        lds_barrier();
+#pragma unroll
+        for (int r = 0; r < kL0IPT; r++) {
+            const uint64_t i = base + (uint64_t)r * kL0BS + tid;
+            if (i < n) {
+                const uint32_t d6 = (dgp >> (8 * r)) & 0xFFu;
+                const uint32_t q = dbase[d6] + wpre[d6][r * kL0W + w] + ((rwp >> (8 * r)) & 0xFFu);
+                sp[q] = v[r];
+                if constexpr (KEYS) sk[q] = kk[r];
+                else sk[q] = (uint16_t)(r * kL0BS + tid);
+            }
+        }
+        load_tile(v, kk, pf);   // past the group's end: its last tile again, no branch
+        lds_barrier();
+        const uint32_t tn = (uint32_t)((n - base) < (uint64_t)kL0Tile ? (n - base) : (uint64_t)kL0Tile);
+#pragma unroll
+        for (int r = 0; r < kL0IPT; r++) {   // past tn: a duplicate of the last store
+            const uint32_t j = min((uint32_t)r * kL0BS + tid, tn - 1);
+            O.p[base + j] = sp[j];
+            if constexpr (KEYS) O.k[base + j] = sk[j];
+            else O.k[base + j] = (uint32_t)(base + sk[j]);
+        }
+    };
+    if (t0 < t1) {
+        float4 v[kL0IPT];
+        uint32_t kk[kL0IPT];
+        load_tile(v, kk, t0);
+        l0_dummy_stores(dummy, v);   // enter the loop with the back-edge's pending ops
+        for (uint32_t tile = t0; tile < t1; tile++) body(tile, v, kk, min(tile + 1, t1 - 1));
+    }
+    for (int d = 32; d > 0; d >>= 1)
+        for (int a = 0; a < 3; a++) {
+            mn[a] = fminf(mn[a], __shfl_xor(mn[a], d, 64));
+            mx[a] = fmaxf(mx[a], __shfl_xor(mx[a], d, 64));
+        }
+    if (lane == 0)
+        for (int a = 0; a < 3; a++) { sb[w][a] = mn[a]; sb[w][3 + a] = mx[a]; }
+    if (bad) atomicOr(flag, 1u);
+    __syncthreads();
+    if (tid < 6) {
+        float r = sb[0][tid];
+        for (int q = 1; q < kL0W; q++) r = tid < 3 ? fminf(r, sb[q][tid]) : fmaxf(r, sb[q][tid]);
+        part[g * 6 + tid] = r;
+    }
+    for (int i = tid; i < R * R5; i += kL0BS)
+        gcnt[((uint64_t)(i / R5) * ngroups + g) * R5 + (i % R5)] = h[(i / R5) * HP + (i % R5)];
+}
+
+// Segment starts of the digit-partitioned order from the tile-major pass 1:
+// start of (d6, group g) = the scanned run position of the group's first tile.
+__global__ void k_l0_tstarts(const uint32_t* __restrict__ voff, uint32_t ntiles, uint32_t tpg, uint32_t ngroups,
+                             uint64_t n, uint32_t* __restrict__ starts) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= 64 * (ngroups + 1)) return;
+    const uint32_t d6 = i / (ngroups + 1), g = i % (ngroups + 1);
+    const uint64_t t = (uint64_t)g * tpg;
+    starts[i] = g < ngroups ? voff[(uint64_t)d6 * ntiles + t] : (d6 < 63 ? voff[(uint64_t)(d6 + 1) * ntiles] : (uint32_t)n);
+}
+
+// Per (d6, d5): exclusive prefix over the groups of the pair counts of
+// k_l0_tile6, read from their parity slots (pmap: dense d5 -> parity slot, 0xFF
+// none) into the dense-d5 layout k_l0_down5g reads, and the dense histogram
+// bin (d5 << 6 | d6).  A count in a parity slot no dense d5 names is a point
+// outside the grid (pass 2 reports it).
+struct L0PMap { uint8_t s[32]; };
+__global__ __launch_bounds__(1024) void k_l0_gprefix_par(const uint32_t* __restrict__ gsrc, uint32_t* __restrict__ gdst,
+                                                         uint32_t ngroups, uint32_t D, L0PMap pm,
+                                                         uint32_t* __restrict__ hist, Counters* ctr) {
+    constexpr int R5 = 32, NC = 1024 / R5;
+    __shared__ uint32_t part[NC][R5];
+    const uint32_t d6 = blockIdx.x, d5 = threadIdx.x % R5, c = threadIdx.x / R5;
+    const uint32_t gpc = (ngroups + NC - 1) / NC, g0 = min(c * gpc, ngroups), g1 = min(g0 + gpc, ngroups);
+    const uint32_t ps = pm.s[d5];
+    const uint32_t* row = gsrc + (uint64_t)d6 * ngroups * R5 + (ps < 32u ? ps : 0u);
+    uint32_t* orow = gdst + (uint64_t)d6 * ngroups * R5 + d5;
+    uint32_t acc = 0;
+    if (ps < 32u)
+        for (uint32_t g = g0; g < g1; g++) acc += row[(uint64_t)g * R5];
+    part[c][d5] = acc;
+    __syncthreads();
+    if (c == 0) {
+        uint32_t a = 0;
+        for (int q = 0; q < NC; q++) { const uint32_t v = part[q][d5]; part[q][d5] = a; a += v; }
+        const uint32_t d0 = (d5 << 6) | d6;
+        if (d0 < D) hist[d0] = a;
+        else if (a) set_err(ctr, ERR_L0_RANGE);
+    }
+    __syncthreads();
+    acc = part[c][d5];
+    for (uint32_t g = g0; g < g1; g++) {
+        orow[(uint64_t)g * R5] = acc;
+        if (ps < 32u) acc += row[(uint64_t)g * R5];
+    }
+}
+
+// Pass-2 windows over the tile-major pass-1 output: window k of unit u covers the
+// unit's points [a + k T, min(a + (k+1) T, b)) of its d6 bucket; per window the
+// tiles holding its first and last point (the largest tile whose scanned run
+// start is <= the position), found by binary search over the unit's tiles.
+struct L0UnitW { uint32_t d6, a, b, t0, t1, w0, pad_g0, pad; };   // pad_g0: the unit's first group
+__device__ __forceinline__ uint32_t l0_tile_of(const uint32_t* __restrict__ vrow, uint32_t t0, uint32_t t1, uint32_t v) {
+    uint32_t lo = t0, hi = t1 - 1;   // vrow[t0] <= v (the unit's first run starts at a <= v)
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (vrow[mid] <= v) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+__global__ void k_l0_wplan(const L0UnitW* __restrict__ units, uint32_t nunits, uint32_t nwin,
+                           const uint32_t* __restrict__ voff, uint32_t ntiles, uint2* __restrict__ wt) {
+    const uint32_t wi = blockIdx.x * blockDim.x + threadIdx.x;
+    if (wi >= nwin) return;
+    uint32_t lo = 0, hi = nunits - 1;   // the unit of window wi: last with w0 <= wi
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (units[mid].w0 <= wi) lo = mid; else hi = mid - 1;
+    }
+    const L0UnitW U = units[lo];
+    const uint32_t v0 = U.a + (wi - U.w0) * (uint32_t)kL0Tile;
+    const uint32_t v1 = min(v0 + (uint32_t)kL0Tile, U.b) - 1;
+    const uint32_t* vrow = voff + (uint64_t)U.d6 * ntiles;
+    wt[wi] = make_uint2(l0_tile_of(vrow, U.t0, U.t1, v0), l0_tile_of(vrow, U.t0, U.t1, v1));
+}
+
 // start of segment (d6, g) of the pass-1 output, g = 0..ngroups (the end)
 __global__ void k_l0_gstarts(const uint32_t* __restrict__ offs, uint32_t ngroups, uint64_t n,
                              uint32_t* __restrict__ starts) {
@@ -1531,15 +1752,25 @@ __device__ __forceinline__ int64_t l0_dense_dest(const L0Params& P, float x, flo
 
 // Pass 2 over one unit (consecutive segments of one d6 bucket), running
 // offsets per d5 kept in wave-0 registers; the same pipelining as pass 1.
-template <int R5>
+// TM: the pass-1 output is tile-major (k_l0_tile6).  The unit is then read in
+// windows of one tile's size; window k's positions map to the runs of the tiles
+// wt[k] = (first, last) through a slice of their scanned run starts (voff) and
+// physical starts (tile base + lp6) staged in LDS, fetched one window ahead and
+// stored one step before use.
+struct L0Slice { uint32_t tf, ntl, sv, sp; };
+template <int R5, bool TM>
 __global__ __launch_bounds__(kL0BS, 8) void k_l0_down5g(Arena S, Arena O, L0Params P, const L0Unit* __restrict__ units,
                                                         const uint32_t* __restrict__ starts, uint32_t ngroups,
                                                         const uint32_t* __restrict__ gpre,
                                                         const uint32_t* __restrict__ cnt_scan,
                                                         const uint32_t* __restrict__ sid, uint32_t D,
-                                                        uint32_t* __restrict__ dcap, Arena dummy, Counters* ctr) {
+                                                        uint32_t* __restrict__ dcap, Arena dummy, Counters* ctr,
+                                                        const L0UnitW* __restrict__ uw, const uint2* __restrict__ wt,
+                                                        const uint32_t* __restrict__ voff,
+                                                        const uint16_t* __restrict__ lp6, uint32_t ntiles) {
     constexpr int R = R5, RB = R5 == 32 ? 5 : R5 == 16 ? 4 : R5 == 8 ? 3 : 2;
     static_assert((1 << RB) == R5, "R5 is a power of two in 4..32");
+    constexpr uint32_t kSl = kL0BS;   // slice entries (tiles per window) staged in LDS
     __shared__ float4 sp[kL0Tile];
     __shared__ uint32_t sk[kL0Tile];
     __shared__ uint8_t sd[kL0Tile];
@@ -1547,31 +1778,75 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_down5g(Arena S, Arena O, L0Para
     __shared__ alignas(16) uint16_t wpre[R][kL0RW];
     __shared__ uint32_t dbase[R], gofs[R];
     __shared__ uint32_t hc[R * kDests];
+    __shared__ uint32_t slv[TM ? kSl : 1], slp[TM ? kSl : 1];
     const uint32_t tid = threadIdx.x, w = tid / 64, lane = tid & 63;
-    const L0Unit U = units[blockIdx.x];
-    const uint32_t a = starts[U.d6 * (ngroups + 1) + U.g0], b = starts[U.d6 * (ngroups + 1) + U.g1];
+    uint32_t d6u, a, b, g0u, w0 = 0, nwin = 0;
+    if constexpr (TM) {
+        const L0UnitW U = uw[blockIdx.x];
+        d6u = U.d6; a = U.a; b = U.b; g0u = U.pad_g0; w0 = U.w0;
+        nwin = (b - a + kL0Tile - 1) / kL0Tile;
+    } else {
+        const L0Unit U = units[blockIdx.x];
+        d6u = U.d6; g0u = U.g0;
+        a = starts[U.d6 * (ngroups + 1) + U.g0];
+        b = starts[U.d6 * (ngroups + 1) + U.g1];
+    }
     uint32_t runr = 0;   // wave 0, lane t < R: next output position of digit t
     if (w == 0 && lane < (uint32_t)R) {
-        const uint32_t d0 = (lane << 6) | U.d6;
-        runr = d0 < D ? cnt_scan[d0] + gpre[((uint64_t)U.d6 * ngroups + U.g0) * R + lane] : 0u;
+        const uint32_t d0 = (lane << 6) | d6u;
+        runr = d0 < D ? cnt_scan[d0] + gpre[((uint64_t)d6u * ngroups + g0u) * R + lane] : 0u;
     }
     gofs[lane & (R - 1)] = runr;   // (an LDS write of runr: its load is complete before the loop)
     for (int i = tid; i < R * kDests; i += kL0BS) hc[i] = 0;
     for (int i = tid; i < kL0RW * R / 4; i += kL0BS) reinterpret_cast<uint32_t*>(&wcnt[0][0])[i] = 0;
     const uint64_t lt = lanemask_lt();
     uint32_t err = 0;
-    auto load_tile = [&](float4* v, uint32_t* kk, uint32_t base) {   // unconditional, clamped (see k_l0_down6g)
-        asm volatile("" ::: "memory");
+    const uint32_t* vrow = TM ? voff + (uint64_t)d6u * ntiles : nullptr;
+    // TM: this thread's entry of the slice of window k (run start, physical
+    // start), loaded into registers; the window's tiles come from wt
+    auto slice_fetch = [&](uint32_t k, L0Slice& q) {
+        k = min(k, nwin - 1);
+        const uint2 t = wt[w0 + k];
+        q.tf = t.x;
+        q.ntl = t.y - t.x + 1;
+        const uint32_t tt = t.x + min(tid, q.ntl - 1);
+        q.sv = vrow[tt];
+        q.sp = tt * (uint32_t)kL0Tile + lp6[(uint64_t)tt * 64 + d6u];
+    };
+    auto slice_store = [&](const L0Slice& q) {
+        if (tid < q.ntl && tid < kSl) { slv[tid] = q.sv; slp[tid] = q.sp; }
+    };
+    // physical position of the unit's point at virtual position v (window of q)
+    auto xlate = [&](const L0Slice& q, uint32_t v) -> uint32_t {
+        if (q.ntl <= kSl) {
+            uint32_t lo = 0, hi = q.ntl - 1;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi + 1) >> 1;
+                if (slv[mid] <= v) lo = mid; else hi = mid - 1;
+            }
+            return slp[lo] + (v - slv[lo]);
+        }
+        const uint32_t t = l0_tile_of(vrow, q.tf, q.tf + q.ntl, v);   // a sparse digit: search in memory
+        return t * (uint32_t)kL0Tile + lp6[(uint64_t)t * 64 + d6u] + (v - vrow[t]);
+    };
+    auto load_tile = [&](float4* v, uint32_t* kk, uint32_t base, const L0Slice& q) {   // unconditional, clamped (see k_l0_down6g)
+        uint32_t ix[kL0IPT];
 #pragma unroll
         for (int r = 0; r < kL0IPT; r++) {
             const uint32_t i = min(base + (uint32_t)r * kL0BS + tid, b - 1);
-            v[r] = S.p[i];
-            kk[r] = S.k[i];
+            if constexpr (TM) ix[r] = xlate(q, i);
+            else ix[r] = i;
+        }
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int r = 0; r < kL0IPT; r++) {
+            v[r] = S.p[ix[r]];
+            kk[r] = S.k[ix[r]];
         }
         asm volatile("" ::: "memory");   // keep the loads ahead of the tile's stores
     };
     if (a >= b) return;   // (units are never empty)
-    auto body = [&](uint32_t base, float4* v, uint32_t* kk, uint32_t pf) {
+    auto body = [&](uint32_t base, float4* v, uint32_t* kk, uint32_t pf, L0Slice& qn, L0Slice& qf) {
         const uint32_t tn = min(b - base, (uint32_t)kL0Tile);
         lds_barrier();
         uint32_t dgp = 0, rwp = 0;
@@ -1583,7 +1858,7 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_down5g(Arena S, Arena O, L0Para
             if (valid) {
                 uint32_t dest;
                 const int64_t d = l0_dense_dest(P, v[r].x, v[r].y, v[r].z, dest);
-                if (d < 0 || ((uint32_t)d & 63u) != U.d6 || dest >= (uint32_t)kDests) {
+                if (d < 0 || ((uint32_t)d & 63u) != d6u || dest >= (uint32_t)kDests) {
                     err = ERR_L0_RANGE;
                 } else {
                     d5 = ((uint32_t)d >> 6) & (R - 1);
@@ -1596,6 +1871,7 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_down5g(Arena S, Arena O, L0Para
             dgp |= d5 << (8 * r);
             rwp |= rw << (8 * r);
         }
+        if constexpr (TM) slice_store(qn);   // the next window's slice (the last search of this one is done)
         lds_barrier();
         if (w == 0) {
             uint32_t ex;
@@ -1618,7 +1894,8 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_down5g(Arena S, Arena O, L0Para
                 sd[q] = (uint8_t)d5;
             }
         }
-        load_tile(v, kk, pf);
+        load_tile(v, kk, pf, qn);
+        if constexpr (TM) slice_fetch((pf - a) / kL0Tile + 1, qf);   // the window after it
         lds_barrier();
 #pragma unroll
         for (int r = 0; r < kL0IPT; r++) {   // past tn: a duplicate of the last store
@@ -1633,30 +1910,28 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_down5g(Arena S, Arena O, L0Para
         const uint32_t last = a + (b - 1 - a) / kL0Tile * kL0Tile;
         return min(base + k * (uint32_t)kL0Tile, last);
     };
-#if PCC_L0_PF == 2
-    float4 va[kL0IPT], vb[kL0IPT];
-    uint32_t ka[kL0IPT], kb[kL0IPT];
-    load_tile(va, ka, a);
-    l0_dummy_stores(dummy, va);
-    load_tile(vb, kb, ahead(a, 1));
-    l0_dummy_stores(dummy, vb);
-    for (uint32_t base = a; base < b; base += 2 * kL0Tile) {
-        body(base, va, ka, ahead(base, 2));
-        if (base + kL0Tile >= b) break;
-        body(base + kL0Tile, vb, kb, ahead(base, 3));
-    }
-#else
     float4 v[kL0IPT];
     uint32_t kk[kL0IPT];
-    load_tile(v, kk, a);
+    L0Slice q0{}, q1{};
+    if constexpr (TM) {
+        slice_fetch(0, q0);
+        slice_store(q0);
+        lds_barrier();
+    }
+    load_tile(v, kk, a, q0);
+    if constexpr (TM) slice_fetch(1, q1);
     l0_dummy_stores(dummy, v);
-    for (uint32_t base = a; base < b; base += kL0Tile) body(base, v, kk, ahead(base, 1));
-#endif
+    for (uint32_t base = a; base < b; base += kL0Tile) {   // q1: the slice of the window after `base`
+        body(base, v, kk, ahead(base, 1), q1, q0);
+        if (base + kL0Tile >= b) break;
+        base += kL0Tile;
+        body(base, v, kk, ahead(base, 1), q0, q1);
+    }
     lds_barrier();
     for (int i = tid; i < R * kDests; i += kL0BS) {
         const uint32_t c = hc[i];
         if (!c) continue;
-        const uint32_t d0 = ((uint32_t)(i / kDests) << 6) | U.d6;
+        const uint32_t d0 = ((uint32_t)(i / kDests) << 6) | d6u;
         if (d0 < D) atomicAdd(&dcap[(uint64_t)sid[d0] * kDests + (uint32_t)(i % kDests)], c);
     }
     if (err) set_err(ctr, err);
@@ -4153,6 +4428,54 @@ void Engine::pre0_count(uint64_t upto, hipEvent_t after, bool all) {
 
 void Engine::pre0_reset() { pre_tiles_ = 0; }
 
+// Bounding box of one tile out of every ntiles / nb (block b: tile b * ntiles / nb).
+__global__ __launch_bounds__(256) void k_bbox_sample(const Point* __restrict__ in, uint64_t n, uint64_t ntiles,
+                                                     uint32_t nb, float* part) {
+    const uint64_t t = (uint64_t)blockIdx.x * ntiles / nb;
+    const float4* p4 = reinterpret_cast<const float4*>(in);
+    float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (uint64_t i = t * kL0Tile + threadIdx.x; i < min((t + 1) * kL0Tile, n); i += 256) {
+        const float4 v = p4[i];
+        mn[0] = fminf(mn[0], v.x); mn[1] = fminf(mn[1], v.y); mn[2] = fminf(mn[2], v.z);
+        mx[0] = fmaxf(mx[0], v.x); mx[1] = fmaxf(mx[1], v.y); mx[2] = fmaxf(mx[2], v.z);
+    }
+    __shared__ float s[4][6];
+    for (int d = 32; d > 0; d >>= 1)
+        for (int a = 0; a < 3; a++) {
+            mn[a] = fminf(mn[a], __shfl_xor(mn[a], d, 64));
+            mx[a] = fmaxf(mx[a], __shfl_xor(mx[a], d, 64));
+        }
+    if ((threadIdx.x & 63) == 0)
+        for (int a = 0; a < 3; a++) { s[threadIdx.x / 64][a] = mn[a]; s[threadIdx.x / 64][3 + a] = mx[a]; }
+    __syncthreads();
+    if (threadIdx.x < 6) {
+        float r = s[0][threadIdx.x];
+        for (int q = 1; q < 4; q++) r = threadIdx.x < 3 ? fminf(r, s[q][threadIdx.x]) : fmaxf(r, s[q][threadIdx.x]);
+        part[blockIdx.x * 6 + threadIdx.x] = r;
+    }
+}
+
+// Whether to fold level-0 pass 0 into pass 1 (k_l0_tile6): the grid must have at
+// most two level-0 cells per axis.  Judged from the bounding box of a sample of
+// 512 tiles (the exact box decides after the pass; a wrong guess costs that
+// pass, then the three-pass binning runs).
+bool Engine::fold_hint(float cs) {
+    const uint64_t ntiles = (nsrc_ + kL0Tile - 1) / kL0Tile;
+    if (ntiles == 0) return false;
+    const uint32_t nb = (uint32_t)std::min<uint64_t>(ntiles, 512);
+    k_bbox_sample<<<nb, 256, 0, stream_>>>(src_, nsrc_, ntiles, nb, dev_->bbox_part);
+    k_bbox_final<<<1, 256, 0, stream_>>>(dev_->bbox_part, nb);
+    HIP_CHECK(hipGetLastError());
+    float bb[6];
+    HIP_CHECK(hipMemcpyAsync(bb, dev_->bbox_part, sizeof bb, hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    for (int a = 0; a < 3; a++) {
+        if (!(std::isfinite(bb[a]) && std::isfinite(bb[3 + a]))) return false;
+        if ((int64_t)cell_index1(bb[3 + a], cs) - (int64_t)cell_index1(bb[a], cs) >= 2) return false;
+    }
+    return true;
+}
+
 int Engine::level0_bin() {
     const uint32_t dim = cfg_.sub_grid_dimension;
     const float cs = cell_size(cfg_.max_cell_size, h0_), csc = cell_size(cfg_.max_cell_size, h0_ + 1);
@@ -4189,7 +4512,45 @@ int Engine::level0_bin() {
     const uint32_t tpg = std::max<uint32_t>(1, (ntiles + ngroups - 1) / ngroups);
     ngroups = std::max<uint32_t>(1, (ntiles + tpg - 1) / tpg);
     uint32_t* gcnt0 = static_cast<uint32_t*>(dev_->get(64ull * ngroups * 4 + 64));
-    {
+    Arena l0dummy{static_cast<float4*>(dev_->get(256ull * kL0BS * kL0IPT * 16)),
+                  static_cast<uint32_t*>(dev_->get(256ull * kL0BS * kL0IPT * 4))};
+    const bool l0keys = src_keys_ != nullptr;
+    // Pass 0 folded into pass 1 (k_l0_tile6) when the grid is expected to have at
+    // most two level-0 cells per axis (judged from a sample of the tiles' bounding
+    // box; the full box after the pass decides, else the three-pass binning runs).
+    bool fold = false;
+    uint32_t* cnt6 = nullptr;
+    uint16_t* lp6 = nullptr;
+    uint32_t* gpar = nullptr;
+    if (ntiles && fold_hint(cs) && getenv("PCC_NO_FOLD") == nullptr) {
+        cnt6 = static_cast<uint32_t*>(dev_->get(64ull * ntiles * 4));
+        lp6 = static_cast<uint16_t*>(dev_->get(64ull * ntiles * 2));
+        gpar = static_cast<uint32_t*>(dev_->get(64ull * ngroups * 32 * 4));
+        HIP_CHECK(hipMemsetAsync(dev_->bbox_flag, 0, 4, stream_));
+        if (l0keys)
+            k_l0_tile6<true><<<ngroups, kL0BS, 0, stream_>>>(src_, src_keys_, dev_->ar[1], nsrc_, P, ntiles, tpg, ngroups,
+                                                             cnt6, lp6, gpar, dev_->bbox_part, dev_->bbox_flag, l0dummy);
+        else
+            k_l0_tile6<false><<<ngroups, kL0BS, 0, stream_>>>(src_, nullptr, dev_->ar[1], nsrc_, P, ntiles, tpg, ngroups,
+                                                              cnt6, lp6, gpar, dev_->bbox_part, dev_->bbox_flag, l0dummy);
+        k_bbox_final<<<1, 256, 0, stream_>>>(dev_->bbox_part, ngroups);
+        HIP_CHECK(hipGetLastError());
+        float bb[6];
+        uint32_t bad = 0;
+        HIP_CHECK(hipMemcpyAsync(bb, dev_->bbox_part, sizeof bb, hipMemcpyDeviceToHost, stream_));
+        HIP_CHECK(hipMemcpyAsync(&bad, dev_->bbox_flag, 4, hipMemcpyDeviceToHost, stream_));
+        HIP_CHECK(hipStreamSynchronize(stream_));
+        if (bad) return fail(-22, "input contains NaN or infinite coordinates (unsupported)");
+        fold = true;
+        for (int a = 0; a < 3; a++) {
+            bmin_[a] = bb[a];
+            bmax_[a] = bb[3 + a];
+            fold &= (int64_t)cell_index1(bmax_[a], cs) - (int64_t)cell_index1(bmin_[a], cs) < 2;
+        }
+        stats_.pre0_tiles = 0;
+    }
+    stats_.l0_fold = fold ? 1 : 0;
+    if (!fold) {
         // the input's tiles already counted while it uploaded (pre0_count): count
         // the rest, then only sum the tiles per group
         const bool pre = pre_tiles_ > 0 && src_ == d_in_ && nsrc_ == n_ && !prior_ && !keyed_ && h0_ == 0 &&
@@ -4271,10 +4632,11 @@ int Engine::level0_bin() {
     // pass 2 without an upsweep (k_l0_down5g) when the rest of the dense id fits
     // one 5-bit pass: pass 1 then counts the (d6, d5) pairs per group (with
     // external keys staged beside the points the pair table must stay <= 16 wide)
-    const bool l0keys = src_keys_ != nullptr;
-    bool g1up = !P.hashed && passes == 1 && per <= (l0keys ? 4 : 5) && ntiles > 0 &&
-                getenv("PCC_L0_TWO_UPSWEEPS") == nullptr;
-    const uint32_t r5 = l0keys ? 16u : 32u;
+    // (the folded pass 1 counts 32-wide pairs with keys staged too: its pair table
+    // needs no digit staging array)
+    bool g1up = fold || (!P.hashed && passes == 1 && per <= (l0keys ? 4 : 5) && ntiles > 0 &&
+                         getenv("PCC_L0_TWO_UPSWEEPS") == nullptr);
+    const uint32_t r5 = (l0keys && !fold) ? 16u : 32u;
     // capacities fused into the pass-1 upsweep when the level-1 slab grid fits LDS
     L1Grid Q;
     for (int a = 0; a < 3; a++) { Q.lo[a] = 2 * P.lo[a]; Q.g[a] = 2 * P.g[a]; }
@@ -4294,11 +4656,9 @@ int Engine::level0_bin() {
     Arena A0 = dev_->ar[0], A1 = dev_->ar[1];
     // the final pass must land in arena 0
     Arena dst = (passes % 2) ? A1 : A0;
-    scan_excl_u32(gcnt0, gcnt0, 64u * ngroups, nullptr, dev_->scan, stream_);
+    if (!fold) scan_excl_u32(gcnt0, gcnt0, 64u * ngroups, nullptr, dev_->scan, stream_);
     uint32_t* gcnt = g1up ? static_cast<uint32_t*>(dev_->get(64ull * ngroups * r5 * 4)) : nullptr;
-    Arena l0dummy{static_cast<float4*>(dev_->get(256ull * kL0BS * kL0IPT * 16)),
-                  static_cast<uint32_t*>(dev_->get(256ull * kL0BS * kL0IPT * 4))};
-    if (ntiles) {
+    if (ntiles && !fold) {
         if (l0keys)
             k_l0_down6g<16, true><<<ngroups, kL0BS, 0, stream_>>>(src_, src_keys_, dst, nsrc_, P, gcnt0, ntiles, tpg,
                                                                    ngroups, gcnt, g1up ? 1 : 0, l0dummy, dev_->ctr);
@@ -4311,9 +4671,29 @@ int Engine::level0_bin() {
     uint32_t nunits = 0;
     if (g1up) {
         starts = static_cast<uint32_t*>(dev_->get(64ull * (ngroups + 1) * 4));
-        if (l0keys) k_l0_gprefix<16><<<64, 1024, 0, stream_>>>(gcnt, ngroups, (uint32_t)D, hist, dev_->ctr);
-        else k_l0_gprefix<32><<<64, 1024, 0, stream_>>>(gcnt, ngroups, (uint32_t)D, hist, dev_->ctr);
-        k_l0_gstarts<<<grid_for(64ull * (ngroups + 1), 256, 1u << 30), 256, 0, stream_>>>(gcnt0, ngroups, nsrc_, starts);
+        if (fold) {
+            // run positions of the tile-major output in the digit-partitioned order,
+            // segment starts per (d6, group), pair prefixes from the parity slots
+            scan_excl_u32(cnt6, cnt6, 64u * ntiles, nullptr, dev_->scan, stream_);
+            k_l0_tstarts<<<grid_for(64ull * (ngroups + 1), 256, 1u << 30), 256, 0, stream_>>>(cnt6, ntiles, tpg, ngroups,
+                                                                                              nsrc_, starts);
+            L0PMap pm;
+            for (uint32_t d5 = 0; d5 < 32; d5++) {
+                // dense d5 = cell * 4 + layer-high bits, cell = (gz * g1 + gy) * g0 + gx
+                const uint32_t cell = d5 >> 2, hi = d5 & 3u;
+                const uint32_t gx = cell % (uint32_t)P.g[0], gy = (cell / (uint32_t)P.g[0]) % (uint32_t)P.g[1];
+                const uint32_t gz = cell / ((uint32_t)P.g[0] * (uint32_t)P.g[1]);
+                if (cell >= G) { pm.s[d5] = 0xFF; continue; }
+                const uint32_t par = ((uint32_t)(P.lo[0] + (int32_t)gx) & 1u) | (((uint32_t)(P.lo[1] + (int32_t)gy) & 1u) << 1) |
+                                     (((uint32_t)(P.lo[2] + (int32_t)gz) & 1u) << 2);
+                pm.s[d5] = (uint8_t)((par << 2) | hi);
+            }
+            k_l0_gprefix_par<<<64, 1024, 0, stream_>>>(gpar, gcnt, ngroups, (uint32_t)D, pm, hist, dev_->ctr);
+        } else {
+            if (l0keys) k_l0_gprefix<16><<<64, 1024, 0, stream_>>>(gcnt, ngroups, (uint32_t)D, hist, dev_->ctr);
+            else k_l0_gprefix<32><<<64, 1024, 0, stream_>>>(gcnt, ngroups, (uint32_t)D, hist, dev_->ctr);
+            k_l0_gstarts<<<grid_for(64ull * (ngroups + 1), 256, 1u << 30), 256, 0, stream_>>>(gcnt0, ngroups, nsrc_, starts);
+        }
         HIP_CHECK(hipGetLastError());
         // the segment starts go to pinned host memory now; the unit plan is made
         // after the one host sync of the level (below)
@@ -4415,12 +4795,41 @@ int Engine::level0_bin() {
         if (nunits)
             HIP_CHECK(hipMemcpyAsync(dunits, units.data(), nunits * sizeof(L0Unit), hipMemcpyHostToDevice, stream_));
         HIP_CHECK(hipMemsetAsync(L->dcap, 0, (uint64_t)L->nslabs * kDests * 4, stream_));
-        if (nunits && r5 == 16)
-            k_l0_down5g<16><<<nunits, kL0BS, 0, stream_>>>(src, dst, P, dunits, starts, ngroups, gcnt, cnt_scan, sflag,
-                                                            (uint32_t)D, L->dcap, l0dummy, dev_->ctr);
-        else if (nunits)
-            k_l0_down5g<32><<<nunits, kL0BS, 0, stream_>>>(src, dst, P, dunits, starts, ngroups, gcnt, cnt_scan, sflag,
-                                                            (uint32_t)D, L->dcap, l0dummy, dev_->ctr);
+        L0UnitW* duw = nullptr;
+        uint2* dwt = nullptr;
+        if (fold && nunits) {   // the units' windows over the tile-major runs (k_l0_wplan)
+            std::vector<L0UnitW> uw(nunits);
+            uint32_t nwin = 0;
+            for (uint32_t u = 0; u < nunits; u++) {
+                const L0Unit& U = units[u];
+                const uint32_t* row = st + (uint64_t)U.d6 * (ngroups + 1);
+                L0UnitW& W = uw[u];
+                W.d6 = U.d6;
+                W.a = row[U.g0];
+                W.b = row[U.g1];
+                W.t0 = U.g0 * tpg;
+                W.t1 = std::min<uint32_t>(U.g1 * tpg, ntiles);
+                W.w0 = nwin;
+                W.pad_g0 = U.g0;
+                W.pad = 0;
+                nwin += (W.b - W.a + kL0Tile - 1) / kL0Tile;
+            }
+            duw = static_cast<L0UnitW*>(dev_->get((uint64_t)nunits * sizeof(L0UnitW)));
+            dwt = static_cast<uint2*>(dev_->get(std::max<uint64_t>(nwin, 1) * sizeof(uint2)));
+            HIP_CHECK(hipMemcpyAsync(duw, uw.data(), nunits * sizeof(L0UnitW), hipMemcpyHostToDevice, stream_));
+            k_l0_wplan<<<grid_for(nwin, 256, 1u << 30), 256, 0, stream_>>>(duw, nunits, nwin, cnt6, ntiles, dwt);
+            k_l0_down5g<32, true><<<nunits, kL0BS, 0, stream_>>>(src, dst, P, dunits, starts, ngroups, gcnt, cnt_scan, sflag,
+                                                                  (uint32_t)D, L->dcap, l0dummy, dev_->ctr, duw, dwt,
+                                                                  cnt6, lp6, ntiles);
+        } else if (nunits && r5 == 16) {
+            k_l0_down5g<16, false><<<nunits, kL0BS, 0, stream_>>>(src, dst, P, dunits, starts, ngroups, gcnt, cnt_scan,
+                                                                   sflag, (uint32_t)D, L->dcap, l0dummy, dev_->ctr,
+                                                                   nullptr, nullptr, nullptr, nullptr, 0);
+        } else if (nunits) {
+            k_l0_down5g<32, false><<<nunits, kL0BS, 0, stream_>>>(src, dst, P, dunits, starts, ngroups, gcnt, cnt_scan,
+                                                                   sflag, (uint32_t)D, L->dcap, l0dummy, dev_->ctr,
+                                                                   nullptr, nullptr, nullptr, nullptr, 0);
+        }
         HIP_CHECK(hipGetLastError());
     }
     if (!root_xyz_.empty() && L->ncells) {   // sub-tree build: the roots' spill batches

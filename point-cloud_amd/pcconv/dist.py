@@ -685,6 +685,8 @@ class HipShardOps:
 
     # the exchange carries membership bitmaps instead of keys (route_bitmaps / keys_from_bitmaps)
     bitmap_keys = True
+    # build() returns the bounding box of the points it built (pcc_get_stats)
+    build_reports_bbox = True
 
     def route_bitmaps(self, pts: torch.Tensor, grid, table: torch.Tensor, nranks: int, slabs: bool,
                       hist: torch.Tensor | None = None):
@@ -942,6 +944,26 @@ def shard_build(comm, ops, pts: torch.Tensor, key0: int, file_points, write: boo
 
     W, dev = comm.world, pts.device
     n_total = int(sum(int(v) for v in file_points))
+    if W == 1 and not merge and getattr(ops, "build_reports_bbox", False):
+        # One rank owns every level-0 cell: the ownership plan is the identity, so
+        # neither the bounding-box all-reduce nor the cell histogram has anything
+        # to decide.  The build reads the input in place and computes the bounding
+        # box itself (its level-0 pass 0, converter.rs:96-104).
+        ops.begin_step()
+        mark("plan")
+        local = ops.build(file_points, pts, None)
+        mark("build")
+        local = _combine([local])
+        local["phases"] = {"lead": 0, "sub": 0, "whole": int(local.get("arrivals", 0))}
+        summary = {"number_of_points": n_total, "hierarchies": int(local["hierarchies"]),
+                   "bbox_min": list(local["bbox_min"]) if n_total else [0.0, 0.0, 0.0],
+                   "bbox_max": list(local["bbox_max"]) if n_total else [0.0, 0.0, 0.0]}
+        mark("summary")
+        if write:
+            ops.write(summary, cells=True, metadata=True)
+            mark("write")
+        return ShardResult(summary=summary, local=local, recv_points=int(pts.shape[0]),
+                           owned_cells=int(local.get("level0_cells", -1)), ms=ms)
     # 2. global bounding box (converter.rs:96-104: componentwise min/max)
     if pts.shape[0]:
         bmin, bmax = ops.bbox(pts)

@@ -3,7 +3,7 @@ import csv
 import sys
 
 rows = list(csv.DictReader(open(sys.argv[1])))
-idx = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith(("pcc::k_l0_up0g(", "pcc::k_l0_up0_bbox("))]
+idx = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith(("pcc::k_l0_up0g(", "pcc::k_l0_up0_bbox(", "pcc::k_bbox_sample("))]
 tot = 0.0
 for r in rows[idx[-1]:]:
     d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6

@@ -293,7 +293,8 @@ def _run_threads(files, world, out, cfg=None, batch=10_000, merge=False):
     return res
 
 
-@pytest.mark.parametrize("case,world", [("uniform", 2), ("files", 3), ("clustered", 4), ("uniform", 8)])
+@pytest.mark.parametrize("case,world", [("uniform", 1), ("files", 1), ("uniform", 2), ("files", 3), ("clustered", 4),
+                                        ("uniform", 8)])
 def test_sharded_threads_match_oracle(tmp_path, case, world):
     files = make_input(case)
     out = str(tmp_path / "out")
