@@ -286,10 +286,11 @@ def record(args, n_gpus, ms, st_levels, st_cells, st_slabs, arrivals, k, dense_m
                      "alg_bytes_per_launch": 32.0 * k["dense_arrivals"] / max(k["dense_launches"], 1),
                      "alg_bytes_per_arrival": 32, "kernel_ms_per_step": dense_ms,
                      "whole_build_alg_GBs": whole, "whole_build_frac": whole / HBM_PEAK_GBS,
-                     "limiter": "vector-instruction issue, not HBM: the dense launches' VALU alone occupies "
-                                "67 / 57 / 70 % of the SIMD cycles at levels 0 / 1 / 2 (269 / 291 / 395 VALU per "
-                                "64 arrivals at 4 cycles each, 2.4 GHz, kernel-trace durations; "
-                                "profiles/r3c_pmc_sq_1b.json, DESIGN.md §4)"},
+                     "limiter": "instruction issue in the phases between the two barriers of each 1024-arrival "
+                                "step, not HBM: 100 more independent VALU per step (4 waves per SIMD) cost 4.4 ms "
+                                "of the 34.3 ms, about their issue cost at 2 cycles per wave64 VALU "
+                                "(profiles/r4_xvalu_ab.jsonl); VALU alone fills 25-32 % of the SIMD cycles at that "
+                                "rate, the rest being SALU/LDS issue and barrier waits (DESIGN.md §4)"},
         "stage_ms": k,
     }
 

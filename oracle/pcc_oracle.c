@@ -89,13 +89,14 @@ ivec3 orc_hex_from_world(float px, float py, float pz, float cr) {
     int32_t q = sat_i32(floorf(qf));
     int32_t r = (int32_t)(0u - (uint32_t)sat_i32(floorf(rf))); /* -(x as i32), wrapping */
     int32_t h = sat_i32(pz / cr);
-    ivec3 o = { q + (r - (r & 1)) / 2, r, h };
+    /* i32 `+` wraps in a release build (saturated indices of infinite coordinates) */
+    ivec3 o = { (int32_t)((uint32_t)q + (uint32_t)((r - (r & 1)) / 2)), r, h };
     return o;
 }
 
 /* hex.rs:18-24 to_axial then hex.rs:55-65 AxialIndex::to_world */
 void orc_hex_to_world(ivec3 o, float cr, float out[3]) {
-    int32_t q = o.x - (o.y - (o.y & 1)) / 2;
+    int32_t q = (int32_t)((uint32_t)o.x - (uint32_t)((o.y - (o.y & 1)) / 2)); /* wrapping */
     int32_t r = o.y;
     int32_t h = o.z;
     float qf = (float)q, rf = (float)r, hf = (float)h;
@@ -495,8 +496,9 @@ static int write_cell(const cell* k, const char* path) {
  * unpinned; tests compare parsed values. */
 static void fmt_f32(char* buf, float v) {
     if (v == 0.0f) { strcpy(buf, signbit(v) ? "-0.0" : "0.0"); return; }
-    if (isinf(v)) { strcpy(buf, v < 0 ? "-inf" : "inf"); return; }
-    if (isnan(v)) { strcpy(buf, "NaN"); return; }
+    /* serde_json serializes a non-finite f32 as null (bounding boxes of
+     * inputs with infinite coordinates, bounding-volume/src/lib.rs:23-31) */
+    if (isinf(v) || isnan(v)) { strcpy(buf, "null"); return; }
     char e[48];
     int p = 1;
     for (; p <= 9; p++) {

@@ -1464,18 +1464,20 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_down6g(const Point* __restrict_
 // so no global digit offsets and no counting pass are needed), and records per
 // tile its digit counts (cnt6, digit-major: the exclusive scan of cnt6 is the
 // position of each tile's run in the digit-partitioned order k_l0_down6g writes)
-// and its digit starts inside the tile (lp6); per group the (d6, d5) pair counts,
+// and each run's physical start (ph6, digit-major too); per group the (d6, d5) pair counts,
 // with the cell part of d5 taken from the PARITY of the absolute cell indices
 // (the grid is unknown until the bounding box is; parities name the cells of a
 // grid of at most two cells per axis, which the host checks after the pass and
 // otherwise falls back to the three-pass binning); and the bounding box
 // (converter.rs:96-104).  k_l0_down5g<., true> then walks each d6 bucket as the
-// sequence of that digit's runs, tile after tile, i.e. in key order.
+// sequence of that digit's runs, tile after tile, i.e. in key order.  Without
+// external keys a point's key is its tile's base plus its index in the tile, so
+// pass 1 writes that 16-bit index only.
 template <bool KEYS>
 __global__ __launch_bounds__(kL0BS, 8) void k_l0_tile6(const Point* __restrict__ in, const uint32_t* __restrict__ keys,
                                                        Arena O, uint64_t n, L0Params P, uint32_t ntiles, uint32_t tpg,
                                                        uint32_t ngroups, uint32_t* __restrict__ cnt6,
-                                                       uint16_t* __restrict__ lp6, uint32_t* __restrict__ gcnt,
+                                                       uint32_t* __restrict__ ph6, uint32_t* __restrict__ gcnt,
                                                        float* __restrict__ part, uint32_t* __restrict__ flag,
                                                        Arena dummy) {
     constexpr int R = 64, R5 = 32, HP = R5 + 1;
@@ -1495,6 +1497,8 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_tile6(const Point* __restrict__
     float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
     bool bad = false;
     const uint32_t t0 = g * tpg, t1 = min(t0 + tpg, ntiles);
+    // per-tile run records through buffer descriptors (scalar bases, 32-bit offsets)
+    const __amdgpu_buffer_rsrc_t rC = srd(cnt6, 256ull * ntiles), rH = srd(ph6, 256ull * ntiles);
     auto load_tile = [&](float4* v, uint32_t* kk, uint32_t tile) {   // unconditional, clamped (see k_l0_down6g)
         const uint64_t base = (uint64_t)tile * kL0Tile;
         asm volatile("" ::: "memory");
@@ -1551,9 +1555,12 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_tile6(const Point* __restrict__
         if (w == 0) {
             uint32_t ex;
             const uint32_t tot = l0_tile_prefix<R>(wcnt, wpre, lane, ex);
-            dbase[lane] = ex;
-            cnt6[(uint64_t)lane * ntiles + tile] = tot;   // this tile's run of digit `lane`: length and start
-            lp6[(uint64_t)tile * R + lane] = (uint16_t)ex;
+            uint32_t ln = lane;   // (recomputed addresses: see k_l0_down5g)
+            asm volatile("" : "+v"(ln));
+            dbase[ln] = ex;
+            const uint32_t ro = (ln * ntiles + tile) * 4;   // this tile's run of digit `lane`: length, start
+            bst(rC, ro, tot);
+            bst(rH, ro, tile * (uint32_t)kL0Tile + ex);
         }
         lds_barrier();
 #pragma unroll
@@ -1575,7 +1582,7 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_tile6(const Point* __restrict__
             const uint32_t j = min((uint32_t)r * kL0BS + tid, tn - 1);
             O.p[base + j] = sp[j];
             if constexpr (KEYS) O.k[base + j] = sk[j];
-            else O.k[base + j] = (uint32_t)(base + sk[j]);
+            else reinterpret_cast<uint16_t*>(O.k)[base + j] = sk[j];   // key - tile base (k_l0_down5g adds it back)
         }
     };
     if (t0 < t1) {
@@ -1758,7 +1765,7 @@ __device__ __forceinline__ int64_t l0_dense_dest(const L0Params& P, float x, flo
 // physical starts (tile base + lp6) staged in LDS, fetched one window ahead and
 // stored one step before use.
 struct L0Slice { uint32_t tf, ntl, sv, sp; };
-template <int R5, bool TM>
+template <int R5, bool TM, bool K16 = false>
 __global__ __launch_bounds__(kL0BS, 8) void k_l0_down5g(Arena S, Arena O, L0Params P, const L0Unit* __restrict__ units,
                                                         const uint32_t* __restrict__ starts, uint32_t ngroups,
                                                         const uint32_t* __restrict__ gpre,
@@ -1767,7 +1774,7 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_down5g(Arena S, Arena O, L0Para
                                                         uint32_t* __restrict__ dcap, Arena dummy, Counters* ctr,
                                                         const L0UnitW* __restrict__ uw, const uint2* __restrict__ wt,
                                                         const uint32_t* __restrict__ voff,
-                                                        const uint16_t* __restrict__ lp6, uint32_t ntiles) {
+                                                        const uint32_t* __restrict__ ph6, uint32_t ntiles) {
     constexpr int R = R5, RB = R5 == 32 ? 5 : R5 == 16 ? 4 : R5 == 8 ? 3 : 2;
     static_assert((1 << RB) == R5, "R5 is a power of two in 4..32");
     constexpr uint32_t kSl = kL0BS;   // slice entries (tiles per window) staged in LDS
@@ -1802,46 +1809,70 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_down5g(Arena S, Arena O, L0Para
     const uint64_t lt = lanemask_lt();
     uint32_t err = 0;
     const uint32_t* vrow = TM ? voff + (uint64_t)d6u * ntiles : nullptr;
+    const uint32_t* prow = TM ? ph6 + (uint64_t)d6u * ntiles : nullptr;
+    const __amdgpu_buffer_rsrc_t rV = srd(vrow, TM ? 4ull * ntiles : 0), rPh = srd(prow, TM ? 4ull * ntiles : 0);
     // TM: this thread's entry of the slice of window k (run start, physical
-    // start), loaded into registers; the window's tiles come from wt
+    // start), loaded into registers; the window's tiles come from wt (scalar)
     auto slice_fetch = [&](uint32_t k, L0Slice& q) {
         k = min(k, nwin - 1);
         const uint2 t = wt[w0 + k];
-        q.tf = t.x;
-        q.ntl = t.y - t.x + 1;
-        const uint32_t tt = t.x + min(tid, q.ntl - 1);
-        q.sv = vrow[tt];
-        q.sp = tt * (uint32_t)kL0Tile + lp6[(uint64_t)tt * 64 + d6u];
+        q.tf = __builtin_amdgcn_readfirstlane(t.x);
+        q.ntl = __builtin_amdgcn_readfirstlane(t.y - t.x + 1);
+        const uint32_t o = (q.tf + min(tid, q.ntl - 1)) * 4;
+        q.sv = bld(rV, o);
+        q.sp = bld(rPh, o);
     };
     auto slice_store = [&](const L0Slice& q) {
         if (tid < q.ntl && tid < kSl) { slv[tid] = q.sv; slp[tid] = q.sp; }
     };
     // physical position of the unit's point at virtual position v (window of q)
-    auto xlate = [&](const L0Slice& q, uint32_t v) -> uint32_t {
+    // physical positions of this thread's kL0IPT points of the window at `base`:
+    // one binary search per row over the window's slice, the rows' LDS reads
+    // interleaved (a uniform number of halvings); a sparse digit's window of more
+    // than kSl tiles searches the run starts in memory
+    auto xlate3 = [&](const L0Slice& q, uint32_t base, uint32_t* ix) {
+        uint32_t vv[kL0IPT];
+#pragma unroll
+        for (int r = 0; r < kL0IPT; r++) vv[r] = min(base + (uint32_t)r * kL0BS + tid, b - 1);
         if (q.ntl <= kSl) {
-            uint32_t lo = 0, hi = q.ntl - 1;
-            while (lo < hi) {
-                const uint32_t mid = (lo + hi + 1) >> 1;
-                if (slv[mid] <= v) lo = mid; else hi = mid - 1;
+            uint32_t lo[kL0IPT], step = 1;
+            while (step < q.ntl) step <<= 1;
+#pragma unroll
+            for (int r = 0; r < kL0IPT; r++) lo[r] = 0;
+            for (step >>= 1; step; step >>= 1) {   // largest lo with slv[lo] <= v (slv[0] <= v)
+#pragma unroll
+                for (int r = 0; r < kL0IPT; r++) {
+                    const uint32_t m = lo[r] + step;
+                    lo[r] = (m < q.ntl && slv[m < q.ntl ? m : 0] <= vv[r]) ? m : lo[r];
+                }
             }
-            return slp[lo] + (v - slv[lo]);
+#pragma unroll
+            for (int r = 0; r < kL0IPT; r++) ix[r] = slp[lo[r]] + (vv[r] - slv[lo[r]]);
+        } else {
+#pragma unroll
+            for (int r = 0; r < kL0IPT; r++) {
+                const uint32_t t = l0_tile_of(vrow, q.tf, q.tf + q.ntl, vv[r]);
+                ix[r] = prow[t] + (vv[r] - vrow[t]);
+            }
         }
-        const uint32_t t = l0_tile_of(vrow, q.tf, q.tf + q.ntl, v);   // a sparse digit: search in memory
-        return t * (uint32_t)kL0Tile + lp6[(uint64_t)t * 64 + d6u] + (v - vrow[t]);
     };
-    auto load_tile = [&](float4* v, uint32_t* kk, uint32_t base, const L0Slice& q) {   // unconditional, clamped (see k_l0_down6g)
+    auto load_tile = [&](float4* v, uint32_t* kk, uint32_t base, const uint32_t* ixp) {   // unconditional, clamped (see k_l0_down6g)
         uint32_t ix[kL0IPT];
 #pragma unroll
         for (int r = 0; r < kL0IPT; r++) {
-            const uint32_t i = min(base + (uint32_t)r * kL0BS + tid, b - 1);
-            if constexpr (TM) ix[r] = xlate(q, i);
-            else ix[r] = i;
+            if constexpr (TM) ix[r] = ixp[r];
+            else ix[r] = min(base + (uint32_t)r * kL0BS + tid, b - 1);
         }
         asm volatile("" ::: "memory");
 #pragma unroll
         for (int r = 0; r < kL0IPT; r++) {
             v[r] = S.p[ix[r]];
-            kk[r] = S.k[ix[r]];
+            if constexpr (K16) {   // key = tile base + 16-bit index in the tile (k_l0_tile6)
+                const uint32_t tb = __umulhi(ix[r], 0xAAAAAAABu) >> 11;   // ix / 3072 (ix < 2^32)
+                kk[r] = tb * (uint32_t)kL0Tile + reinterpret_cast<const uint16_t*>(S.k)[ix[r]];
+            } else {
+                kk[r] = S.k[ix[r]];
+            }
         }
         asm volatile("" ::: "memory");   // keep the loads ahead of the tile's stores
     };
@@ -1871,14 +1902,17 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_down5g(Arena S, Arena O, L0Para
             dgp |= d5 << (8 * r);
             rwp |= rw << (8 * r);
         }
-        if constexpr (TM) slice_store(qn);   // the next window's slice (the last search of this one is done)
         lds_barrier();
         if (w == 0) {
             uint32_t ex;
             const uint32_t tot = l0_tile_prefix<R>(wcnt, wpre, lane, ex);
-            if (lane < (uint32_t)R) {
-                dbase[lane] = ex;
-                gofs[lane] = runr - ex;
+            // the LDS addresses are recomputed here, not kept live across the loop
+            // (at the 64-VGPR cap they were spilled, and each reload drained vmcnt)
+            uint32_t ln = lane;
+            asm volatile("" : "+v"(ln));
+            if (ln < (uint32_t)R) {
+                dbase[ln] = ex;
+                gofs[ln] = runr - ex;
                 runr += tot;
             }
         }
@@ -1894,7 +1928,11 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_down5g(Arena S, Arena O, L0Para
                 sd[q] = (uint8_t)d5;
             }
         }
-        load_tile(v, kk, pf, qn);
+        {
+            uint32_t ixn[kL0IPT];   // TM: the next window's physical positions (its slice is in LDS)
+            if constexpr (TM) xlate3(qn, pf, ixn);
+            load_tile(v, kk, pf, ixn);
+        }
         if constexpr (TM) slice_fetch((pf - a) / kL0Tile + 1, qf);   // the window after it
         lds_barrier();
 #pragma unroll
@@ -1904,6 +1942,9 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_down5g(Arena S, Arena O, L0Para
             O.p[dst] = sp[j];
             O.k[dst] = sk[j];
         }
+        // TM: the slice of the window after `pf` (this one's last search is done;
+        // searched in the next body after its third barrier)
+        if constexpr (TM) slice_store(qf);
     };
     // the tile `k` tiles after `base`, clamped to the unit's last tile
     auto ahead = [&](uint32_t base, uint32_t k) {
@@ -1913,13 +1954,19 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_down5g(Arena S, Arena O, L0Para
     float4 v[kL0IPT];
     uint32_t kk[kL0IPT];
     L0Slice q0{}, q1{};
+    uint32_t ix0[kL0IPT] = {};
     if constexpr (TM) {
         slice_fetch(0, q0);
         slice_store(q0);
         lds_barrier();
+        xlate3(q0, a, ix0);
+        lds_barrier();
     }
-    load_tile(v, kk, a, q0);
-    if constexpr (TM) slice_fetch(1, q1);
+    load_tile(v, kk, a, ix0);
+    if constexpr (TM) {
+        slice_fetch(1, q1);
+        slice_store(q1);   // (waits for this fetch, once; the loop stores each slice a body ahead)
+    }
     l0_dummy_stores(dummy, v);
     for (uint32_t base = a; base < b; base += kL0Tile) {   // q1: the slice of the window after `base`
         body(base, v, kk, ahead(base, 1), q1, q0);
@@ -4520,19 +4567,19 @@ int Engine::level0_bin() {
     // box; the full box after the pass decides, else the three-pass binning runs).
     bool fold = false;
     uint32_t* cnt6 = nullptr;
-    uint16_t* lp6 = nullptr;
+    uint32_t* ph6 = nullptr;
     uint32_t* gpar = nullptr;
     if (ntiles && fold_hint(cs) && getenv("PCC_NO_FOLD") == nullptr) {
         cnt6 = static_cast<uint32_t*>(dev_->get(64ull * ntiles * 4));
-        lp6 = static_cast<uint16_t*>(dev_->get(64ull * ntiles * 2));
+        ph6 = static_cast<uint32_t*>(dev_->get(64ull * ntiles * 4));
         gpar = static_cast<uint32_t*>(dev_->get(64ull * ngroups * 32 * 4));
         HIP_CHECK(hipMemsetAsync(dev_->bbox_flag, 0, 4, stream_));
         if (l0keys)
             k_l0_tile6<true><<<ngroups, kL0BS, 0, stream_>>>(src_, src_keys_, dev_->ar[1], nsrc_, P, ntiles, tpg, ngroups,
-                                                             cnt6, lp6, gpar, dev_->bbox_part, dev_->bbox_flag, l0dummy);
+                                                             cnt6, ph6, gpar, dev_->bbox_part, dev_->bbox_flag, l0dummy);
         else
             k_l0_tile6<false><<<ngroups, kL0BS, 0, stream_>>>(src_, nullptr, dev_->ar[1], nsrc_, P, ntiles, tpg, ngroups,
-                                                              cnt6, lp6, gpar, dev_->bbox_part, dev_->bbox_flag, l0dummy);
+                                                              cnt6, ph6, gpar, dev_->bbox_part, dev_->bbox_flag, l0dummy);
         k_bbox_final<<<1, 256, 0, stream_>>>(dev_->bbox_part, ngroups);
         HIP_CHECK(hipGetLastError());
         float bb[6];
@@ -4818,9 +4865,14 @@ int Engine::level0_bin() {
             dwt = static_cast<uint2*>(dev_->get(std::max<uint64_t>(nwin, 1) * sizeof(uint2)));
             HIP_CHECK(hipMemcpyAsync(duw, uw.data(), nunits * sizeof(L0UnitW), hipMemcpyHostToDevice, stream_));
             k_l0_wplan<<<grid_for(nwin, 256, 1u << 30), 256, 0, stream_>>>(duw, nunits, nwin, cnt6, ntiles, dwt);
-            k_l0_down5g<32, true><<<nunits, kL0BS, 0, stream_>>>(src, dst, P, dunits, starts, ngroups, gcnt, cnt_scan, sflag,
-                                                                  (uint32_t)D, L->dcap, l0dummy, dev_->ctr, duw, dwt,
-                                                                  cnt6, lp6, ntiles);
+            if (l0keys)
+                k_l0_down5g<32, true, false><<<nunits, kL0BS, 0, stream_>>>(src, dst, P, dunits, starts, ngroups, gcnt,
+                                                                             cnt_scan, sflag, (uint32_t)D, L->dcap, l0dummy,
+                                                                             dev_->ctr, duw, dwt, cnt6, ph6, ntiles);
+            else
+                k_l0_down5g<32, true, true><<<nunits, kL0BS, 0, stream_>>>(src, dst, P, dunits, starts, ngroups, gcnt,
+                                                                            cnt_scan, sflag, (uint32_t)D, L->dcap, l0dummy,
+                                                                            dev_->ctr, duw, dwt, cnt6, ph6, ntiles);
         } else if (nunits && r5 == 16) {
             k_l0_down5g<16, false><<<nunits, kL0BS, 0, stream_>>>(src, dst, P, dunits, starts, ngroups, gcnt, cnt_scan,
                                                                    sflag, (uint32_t)D, L->dcap, l0dummy, dev_->ctr,

@@ -63,13 +63,15 @@ PCC_HD I3 hex_from_world(float px, float py, float pz, float cr) {
     int32_t q = sat_i32(floorf(qf));
     int32_t r = (int32_t)(0u - (uint32_t)sat_i32(floorf(rf)));
     int32_t h = sat_i32(pz / cr);
-    I3 o = { q + (r - (r & 1)) / 2, r, h };
+    // i32 `+` wraps in the reference's release build; only saturated indices
+    // (infinite coordinates) get near the ends of the range
+    I3 o = { (int32_t)((uint32_t)q + (uint32_t)((r - (r & 1)) / 2)), r, h };
     return o;
 }
 
 // hex.rs:18-24 to_axial, then hex.rs:55-65 AxialIndex::to_world
 PCC_HD void hex_to_world(I3 o, float cr, float& X, float& Y, float& Z) {
-    int32_t q = o.x - (o.y - (o.y & 1)) / 2;
+    int32_t q = (int32_t)((uint32_t)o.x - (uint32_t)((o.y - (o.y & 1)) / 2));   // wrapping, as hex.rs:18-24 in release
     float qf = (float)q, rf = (float)o.y, hf = (float)o.z;
     X = cr * ((kSqrt3 * qf) + ((kSqrt3 / 2.0f) * rf));
     Y = ((cr * 3.0f) / 2.0f) * rf;

@@ -71,11 +71,19 @@ def read_dir(out_dir: str, slots: bool = True):
             assert fn == "c_%d_%d_%d.bin" % c["id"][1:], fn
             assert name == "h_%d" % c["id"][0]
             cells[c["id"]] = dict(header=c["header"], grid=c["grid"], buckets=c["buckets"])
-    m = dict(number_of_points=meta["number_of_points"], hierarchies=meta["hierarchies"],
-             bmin=[float(F(v)) for v in meta["bounding_box"]["min"]],
-             bmax=[float(F(v)) for v in meta["bounding_box"]["max"]],
-             config=dict(meta["config"]))
-    return cells, m
+    return cells, _meta(meta)
+
+
+def _f32_or_null(v):
+    """A metadata float; serde_json writes a non-finite f32 as null."""
+    return None if v is None else float(F(v))
+
+
+def _meta(meta: dict) -> dict:
+    return dict(number_of_points=meta["number_of_points"], hierarchies=meta["hierarchies"],
+                bmin=[_f32_or_null(v) for v in meta["bounding_box"]["min"]],
+                bmax=[_f32_or_null(v) for v in meta["bounding_box"]["max"]],
+                config=dict(meta["config"]))
 
 
 def diff(a, b, limit: int = 10) -> list[str]:
@@ -144,11 +152,7 @@ def read_dir_fast(out_dir: str):
                 off += 16 * n
             assert off == len(data)
             cells[(h, x, y, z)] = (hdr, np.sort(grid).tobytes(), tuple(sorted(buckets, key=lambda t: t[0])))
-    m = dict(number_of_points=meta["number_of_points"], hierarchies=meta["hierarchies"],
-             bmin=[float(F(v)) for v in meta["bounding_box"]["min"]],
-             bmax=[float(F(v)) for v in meta["bounding_box"]["max"]],
-             config=dict(meta["config"]))
-    return cells, m
+    return cells, _meta(meta)
 
 
 def diff_fast(a, b, limit: int = 10) -> list[str]:
