@@ -407,6 +407,10 @@ static int write_impl(pcc_converter* c, bool with_metadata) {
     if (verbose) fprintf(stderr, "[pcc] write: last level's files %.1f ms after the last download\n", ms(tj, clk::now()));
     if (rc) return set_err(rc, c->eng->last_error());
     if (wrc) return set_err(wrc, werr);
+    if (!c->eng->side_cells().empty()) {   // the cells of points with an infinite coordinate
+        rc = write_cell_files(c->out_dir, c->meta.config, c->eng->side_cells(), nullptr, err);
+        if (rc) return set_err(rc, err);
+    }
     if (c->merge && !c->prior_on_disk) {   // adopted cloud: its untouched cells are not on disk here
         rc = write_cell_files(c->out_dir, c->meta.config, c->prior_cells, &c->prior_touched, err);
         if (rc) return set_err(rc, err);
@@ -438,6 +442,11 @@ int pcc_visit_cells(pcc_converter* c, pcc_cell_visitor fn, void* user) {
             const int r = fn(&v, user);
             if (r) return r;
         }
+    }
+    for (const CellFile& f : c->eng->side_cells()) {   // cells of points with an infinite coordinate
+        file_cell_view(c->meta.config, f, v);
+        const int r = fn(&v, user);
+        if (r) return r;
     }
     for (size_t i = 0; i < c->prior_cells.size(); i++) {   // merge: the existing cells no new point reached
         if (i < c->prior_touched.size() && c->prior_touched[i]) continue;
@@ -870,6 +879,8 @@ int pcc_adopt_prior(pcc_converter* dst, pcc_converter* src) {
         const int rc = pcc_build(src);
         if (rc) return rc;
     }
+    if (!src->eng->side_cells().empty())
+        return set_err(-22, "a cloud with infinite coordinates cannot be merged into (merges reject them)");
     GUARD_BEGIN
     std::vector<LevelHost> levels;
     std::vector<Point> grid, kept;

@@ -128,6 +128,23 @@ struct DefaultInitAlloc : std::allocator<T> {
 };
 template <class T> using HostVec = std::vector<T, DefaultInitAlloc<T>>;
 
+// One cell file as Cell::read_from sees it (cell.rs:183-229, Header::read_from
+// cell.rs:300-335): grid points in file order, overflow entries in file order
+// (n == 0 <=> None, cell.rs:210-212).  Also the engine's cells of points with
+// an infinite coordinate (Engine::side_cells).
+struct CellFile {
+    uint32_t h = 0;
+    int32_t idx[3] = {0, 0, 0};
+    uint32_t total = 0, number = 0, overflow = 0;
+    HostVec<Point> grid;
+    struct Entry {
+        int32_t child[3];
+        bool some;
+        HostVec<Point> pts;
+    };
+    std::vector<Entry> entries;
+};
+
 struct PriorState {
     uint64_t nseeds = 0;                               // S: every existing point
     HostVec<Point> seeds0;                             // level-0 seeds, key order (keys 0 .. seeds0.size()-1)
@@ -228,6 +245,9 @@ public:
     const float* bbox_min() const { return bmin_; }
     const float* bbox_max() const { return bmax_; }
     uint32_t hierarchies() const { return hierarchies_; }
+    // The cells of the points with an infinite coordinate (built apart, see
+    // build_infinite()); empty for other inputs.  Not part of any level.
+    const std::vector<CellFile>& side_cells() const { return side_; }
     const BuildStats& stats() const { return stats_; }
     void set_profiling(bool on) { profiling_ = on; }
     const StageProfile& profile() const { return prof_; }
@@ -248,6 +268,8 @@ private:
     void ev_collect();
     int level0_bin();
     bool fold_hint(float cs);
+    int enter_nonfinite(uint32_t flags);
+    int build_infinite();
     // level-0 pass 0 behind the host-to-device copy (add_file_host, streamed files)
     void pre0_count(uint64_t upto, hipEvent_t after, bool all);
     void pre0_reset();
@@ -322,6 +344,19 @@ private:
     Dev* dev_ = nullptr;
     std::vector<Level*> levels_;
     float bmin_[3] = {0, 0, 0}, bmax_[3] = {0, 0, 0};
+    // Inputs with non-finite coordinates (enter_nonfinite): the level-0 grid
+    // spans the points without an infinite coordinate, NaN taken as 0 (gmin_ /
+    // gmax_); when some coordinate is infinite those points are split off with
+    // their keys (d_nf_*) from the infinite ones (d_inf_*, built apart).
+    bool nf_mode_ = false;
+    float gmin_[3] = {0, 0, 0}, gmax_[3] = {0, 0, 0};
+    Point* d_nf_pts_ = nullptr;
+    uint32_t* d_nf_keys_ = nullptr;
+    uint64_t nf_cap_ = 0;
+    Point* d_inf_pts_ = nullptr;
+    uint32_t* d_inf_keys_ = nullptr;
+    uint64_t inf_cap_ = 0, ninf_ = 0;
+    std::vector<CellFile> side_;         // their cells (host copy)
     uint32_t hierarchies_ = 0;
     BuildStats stats_;
     bool profiling_ = false;

@@ -698,6 +698,18 @@ __global__ __launch_bounds__(256) void k_bbox_final(float* part, uint32_t nb) {
     }
 }
 
+// Non-finite coordinates (the reference's semantics: f32::min/max skip NaN,
+// `as i32` saturates with NaN -> 0, a NaN distance never compares less):
+// 1 = a NaN coordinate and no infinite one (such a point enters finite cells:
+// index 0 on the NaN axes), 2 = an infinite coordinate (its cell index
+// saturates on that axis at every level: cells of their own, built apart).
+constexpr uint32_t kNfNan = 1u, kNfInf = 2u, kNfLayer = 4u;
+__device__ __forceinline__ uint32_t nf_class(float x, float y, float z) {
+    const bool inf = isinf(x) || isinf(y) || isinf(z);
+    const bool nan = isnan(x) || isnan(y) || isnan(z);
+    return inf ? kNfInf : (nan ? kNfNan : 0u);
+}
+
 // ------------------------------------------------------------------ level-0 binning
 struct L0Params {
     float cs, cr, csc, crc;   // level 0 and level 1 cell size / hex radius
@@ -868,7 +880,7 @@ __global__ __launch_bounds__(kL0BS) void k_l0_up0g(const Point* __restrict__ in,
     __syncthreads();
     const uint32_t wv = threadIdx.x / 64;
     float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
-    bool bad = false;
+    uint32_t nf = 0;
     const uint64_t lo = (uint64_t)blockIdx.x * tpg * kL0Tile;
     const uint64_t hi = min((uint64_t)(blockIdx.x + 1) * tpg * kL0Tile, n);
     for (uint64_t i0 = lo + threadIdx.x; i0 < hi; i0 += (uint64_t)U * kL0BS) {
@@ -880,7 +892,7 @@ __global__ __launch_bounds__(kL0BS) void k_l0_up0g(const Point* __restrict__ in,
             const bool valid = i0 + (uint64_t)u * kL0BS < hi;
             uint32_t d6 = 0;
             if (valid) {
-                bad |= !(isfinite(v[u].x) && isfinite(v[u].y) && isfinite(v[u].z));
+                nf |= nf_class(v[u].x, v[u].y, v[u].z);
                 mn[0] = fminf(mn[0], v[u].x); mn[1] = fminf(mn[1], v[u].y); mn[2] = fminf(mn[2], v[u].z);
                 mx[0] = fmaxf(mx[0], v[u].x); mx[1] = fmaxf(mx[1], v[u].y); mx[2] = fmaxf(mx[2], v[u].z);
                 int32_t iz;
@@ -895,7 +907,7 @@ __global__ __launch_bounds__(kL0BS) void k_l0_up0g(const Point* __restrict__ in,
             mx[a] = fmaxf(mx[a], __shfl_xor(mx[a], d, 64));
         }
     const int w = threadIdx.x / 64;
-    if (bad) atomicOr(flag, 1u);
+    if (nf) atomicOr(flag, nf);
     if ((threadIdx.x & 63) == 0)
         for (int a = 0; a < 3; a++) { sb[w][a] = mn[a]; sb[w][3 + a] = mx[a]; }
     __syncthreads();
@@ -926,7 +938,7 @@ __global__ __launch_bounds__(kL0BS) void k_l0_tiles0(const Point* __restrict__ i
     const float4* p4 = reinterpret_cast<const float4*>(in);
     const uint32_t tid = threadIdx.x, wv = tid / 64;
     float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
-    bool bad = false;
+    uint32_t nf = 0;
     for (uint64_t t = t0 + blockIdx.x; t < t1; t += gridDim.x) {
         for (uint32_t i = tid; i < NWV * R; i += kL0BS) (&dh[0][0])[i] = 0;
         __syncthreads();
@@ -937,7 +949,7 @@ __global__ __launch_bounds__(kL0BS) void k_l0_tiles0(const Point* __restrict__ i
 #pragma unroll
         for (int r = 0; r < kL0IPT; r++) {
             if (base + (uint64_t)r * kL0BS + tid >= n) continue;
-            bad |= !(isfinite(v[r].x) && isfinite(v[r].y) && isfinite(v[r].z));
+            nf |= nf_class(v[r].x, v[r].y, v[r].z);
             mn[0] = fminf(mn[0], v[r].x); mn[1] = fminf(mn[1], v[r].y); mn[2] = fminf(mn[2], v[r].z);
             mx[0] = fmaxf(mx[0], v[r].x); mx[1] = fmaxf(mx[1], v[r].y); mx[2] = fmaxf(mx[2], v[r].z);
             int32_t iz;
@@ -956,7 +968,7 @@ __global__ __launch_bounds__(kL0BS) void k_l0_tiles0(const Point* __restrict__ i
             mn[a] = fminf(mn[a], __shfl_xor(mn[a], d, 64));
             mx[a] = fmaxf(mx[a], __shfl_xor(mx[a], d, 64));
         }
-    if (bad) atomicOr(flag, 1u);
+    if (nf) atomicOr(flag, nf);
     if ((tid & 63) == 0)
         for (int a = 0; a < 3; a++) { sb[wv][a] = mn[a]; sb[wv][3 + a] = mx[a]; }
     __syncthreads();
@@ -1495,7 +1507,7 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_tile6(const Point* __restrict__
     for (int i = tid; i < kL0RW * R / 4; i += kL0BS) reinterpret_cast<uint32_t*>(&wcnt[0][0])[i] = 0;
     const uint64_t lt = lanemask_lt();
     float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
-    bool bad = false;
+    uint32_t nf = 0;
     const uint32_t t0 = g * tpg, t1 = min(t0 + tpg, ntiles);
     // per-tile run records through buffer descriptors (scalar bases, 32-bit offsets)
     const __amdgpu_buffer_rsrc_t rC = srd(cnt6, 256ull * ntiles), rH = srd(ph6, 256ull * ntiles);
@@ -1521,7 +1533,7 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_tile6(const Point* __restrict__
             uint32_t d6 = 0;
             if (valid) {
                 const float x = v[r].x, y = v[r].y, z = v[r].z;
-                bad |= !(isfinite(x) && isfinite(y) && isfinite(z));
+                nf |= nf_class(x, y, z);
                 mn[0] = fminf(mn[0], x); mn[1] = fminf(mn[1], y); mn[2] = fminf(mn[2], z);
                 mx[0] = fmaxf(mx[0], x); mx[1] = fmaxf(mx[1], y); mx[2] = fmaxf(mx[2], z);
             }
@@ -1540,7 +1552,7 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_tile6(const Point* __restrict__
                 }
             }
             if (valid) {
-                bad |= ll < 0 || ll >= (int64_t)kL0Layers;
+                nf |= (ll < 0 || ll >= (int64_t)kL0Layers) ? kNfLayer : 0u;   // (an infinite z too: rebinned apart)
                 d6 = (uint32_t)ll & (R - 1);
                 const uint32_t par = (uint32_t)(ix & 1) | ((uint32_t)(iy & 1) << 1) | ((uint32_t)(iz & 1) << 2);
                 atomicAdd(&h[d6 * HP + ((par << 2) | (((uint32_t)ll >> 6) & 3u))], 1u);
@@ -1599,7 +1611,7 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_tile6(const Point* __restrict__
         }
     if (lane == 0)
         for (int a = 0; a < 3; a++) { sb[w][a] = mn[a]; sb[w][3 + a] = mx[a]; }
-    if (bad) atomicOr(flag, 1u);
+    if (nf) atomicOr(flag, nf);
     __syncthreads();
     if (tid < 6) {
         float r = sb[0][tid];
@@ -2125,6 +2137,8 @@ struct DenseLds {
     uint32_t dcur[2][kDests];      // emissions per child slab before chunk c: dcur[c & 1]
     alignas(16) uint32_t wcnt[kDests][NW / 4];   // emissions per child slab and wave, one byte per wave (<= 64)
     uint32_t nwin, err;
+    uint32_t fj;                   // NaN points in the slot (0, 0) outside the table: the first one's arrival index
+    uint32_t nanc[2];              // per chunk parity: a NaN-distance candidate pushed (the walk's NaN rules apply)
 };
 
 __device__ __forceinline__ uint32_t hash_slot(uint32_t k) { return (k * 2654435761u) >> 15; }
@@ -2154,6 +2168,17 @@ __device__ __forceinline__ int claim_insert(uint32_t* H, uint32_t local, uint32_
 
 // end of a dense slab's per-slot candidate list (k_slab)
 constexpr uint32_t kNil = 0x7FFu;
+// a NaN distance in the candidate list: never less than another (cell.rs:77-80)
+constexpr uint32_t kNanKey = 0x7FFFFFFFu;
+// The slot key of a foreign slot in the hashed tables of the small-slab
+// kernels: a NaN x or y maps to offset slot (0, 0), outside the cell's slot
+// range unless the cell touches the origin (k_slab's "foreign" slots); above
+// every slot of a dim-96 layer, below the wave kernel's reserved 0x3FFF.
+constexpr uint32_t kForeignSlot = 0x3FFEu;
+static_assert(kDenseTab < (int)kForeignSlot, "foreign slot key above the table");
+// the table key of a distance: a NaN point that takes an empty slot keeps it
+// (nothing compares less than it, cell.rs:77-80), i.e. key 0
+__device__ __forceinline__ uint32_t dist_key(float d2) { return d2 == d2 ? f2u(d2) : 0u; }
 
 // Slot-table entry: (d2 bits << 33) | (dest << 28) | ((g + 1) << 23) | j.  d2 >= +0
 // so its sign bit is free; dest (0..23) and g (grandchild slab inside dest, -1
@@ -2236,6 +2261,7 @@ __device__ __forceinline__ void dense_grid_points(const SlabParams& P, L& S, uin
                 atomicAnd(&bm[jw >> 5], ~(1u << (jw & 31u)));
             }
         }
+        if (tid == 0 && S.fj != kEmpty32) atomicAnd(&bm[S.fj >> 5], ~(1u << (S.fj & 31u)));   // a foreign slot's point
         GSTAMP(14);
         lds_barrier();
         GSTAMP(15);
@@ -2296,6 +2322,10 @@ __device__ __forceinline__ void dense_grid_points(const SlabParams& P, L& S, uin
 #endif
 #pragma unroll
         for (int u = 0; u < U; u++) bst4(rG, wpos[u], pv[u]);
+        if (tid == 0 && S.fj != kEmpty32) {   // the point holding a foreign slot (NaN coordinates)
+            const uint32_t wf = atomicAdd(&S.nwin, 1u);
+            bst4(rG, wf * 16, rP.p(S.fj * 16));
+        }
     }
 }
 
@@ -2411,7 +2441,7 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
         S.dcur[0][tid] = 0;
         S.dcur[1][tid] = 0;
     }
-    if (tid == 0) { S.nwin = 0; S.err = 0; }
+    if (tid == 0) { S.nwin = 0; S.err = 0; S.fj = kEmpty32; S.nanc[0] = S.nanc[1] = 0; }
     lds_barrier();   // LDS only: the first chunks' loads stay in flight
     if constexpr (SEEDS) {
         // Merge: the slab's grid seeds (its first ng arrivals: keys below every
@@ -2438,7 +2468,7 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
             }
             const uint32_t dn = d < 0 ? 0u : (uint32_t)d;
             if (slotted) {
-                const unsigned long long e = ((unsigned long long)f2u(d2) << 33) | ((unsigned long long)dn << kJBits) |
+                const unsigned long long e = ((unsigned long long)dist_key(d2) << 33) | ((unsigned long long)dn << kJBits) |
                                              (wide ? 0u : ((uint32_t)(gn + 1) << 23)) | jg;
                 // two grid points in one slot: not a cell a converter writes
                 if (atomicCAS(&S.tab[(uint32_t)(ly * P.tx + lx)], kEmpty64, e) != kEmpty64) err |= ERR_CLAIM;
@@ -2505,13 +2535,24 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
         float X, Y, Z;
         slot_centre(sd, G.cr, zt, X, Y, Z);
         const float d2 = dist2(X, Y, Z, x, y, z);
+        // A NaN coordinate gives a NaN distance, which never compares less
+        // (cell.rs:77-80), and a NaN x or y gives the slot (0, 0) (hex.rs:67-85,
+        // NaN `as i32` = 0), which can lie outside this cell's table: a "foreign"
+        // slot only NaN points reach, so its first arrival is the grid point and
+        // every later one overflows.
+        const bool isn = d2 != d2;
+        bool foreign = false;
+        if (__ballot(isn && valid && layer_ok && !range_ok)) {
+            foreign = isn && valid && layer_ok && !range_ok;
+            if (foreign && !forced) atomicMin(&S.fj, j);
+        }
         uint32_t dn;
         int32_t gn;
         {
             const int d = sd.d;
             gn = sd.g;
             // error codes only on the (never expected) failing lanes
-            const bool bad = valid && (!layer_ok || !range_ok || d < 0 || (P.check_gchild && gn < 0));
+            const bool bad = valid && (!layer_ok || (!range_ok && !foreign) || d < 0 || (P.check_gchild && gn < 0));
             if (__ballot(bad)) {
                 if (bad) err |= slot_route_errs(slot_route(x, y, z, G), layer_ok, range_ok, cx, cy, cz, t, P.check_gchild);
             }
@@ -2531,6 +2572,8 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
         } else {
             occ = kEmpty64;
         }
+        if (cand && isn) S.nanc[par] = 1u;
+        if (tid == 0) S.nanc[par ^ 1u] = 0u;   // the other parity's flag (read before the last barrier)
         if (cand) {
             // push onto the slot's list: swap this thread into the head's half of
             // the word (a CAS retried while other pushes change the word); the
@@ -2543,7 +2586,7 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
             }
             const uint32_t oldh = (hw >> sh) & 0xFFFFu;
             myprev = (oldh >> 11) == tag ? (oldh & kNil) : kNil;
-            S.cd2[tid] = f2u(d2);
+            S.cd2[tid] = isn ? kNanKey : f2u(d2);
             S.cnext[tid] = (uint16_t)myprev;
             S.cdg[tid] = (uint16_t)(dn | ((uint32_t)(gn + 1) << 5));
         }
@@ -2640,6 +2683,9 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
         }
         // ---- phase B (2): records of chunk i (walk of the slot's candidate list)
         int32_t em = (slotted && !cand && (forced || occ != kEmpty64)) ? 0 : -1;
+        if (__ballot(foreign)) {   // a foreign slot: the first NaN point holds it, the others overflow
+            if (foreign && S.fj != j) em = 0;
+        }
         uint32_t emd = dn;
         int32_t emg = gn;
         uint32_t gsrc = 0xFFFFFFFFu;   // byte offset of a displaced point's payload
@@ -2652,17 +2698,41 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
             // branch-free body; the own entry is skipped (known without LDS reads)
             uint32_t xk = (S.head[local >> 1] >> ((local & 1u) * 16u)) & kNil;
             if (xk == tid) xk = myprev;
-            while (xk != kNil) {
-                const uint32_t dx = S.cd2[xk];
-                const uint32_t nx = S.cnext[xk];
-                const bool earlier = xk < tid;
-                const bool better = earlier && (dx < bd || (dx == bd && xk < bt));
-                bd = better ? dx : bd;
-                bt = better ? xk : bt;
-                beaten |= !earlier && dx < me;
-                xk = nx == tid ? myprev : nx;
+            uint32_t meff = me;
+            if (!S.nanc[par]) {
+                while (xk != kNil) {
+                    const uint32_t dx = S.cd2[xk];
+                    const uint32_t nx = S.cnext[xk];
+                    const bool earlier = xk < tid;
+                    const bool better = earlier && (dx < bd || (dx == bd && xk < bt));
+                    bd = better ? dx : bd;
+                    bt = better ? xk : bt;
+                    beaten |= !earlier && dx < me;
+                    xk = nx == tid ? myprev : nx;
+                }
+            } else {
+                // A NaN-distance candidate (the slot was empty) holds the slot iff it
+                // is the earliest candidate; then nothing displaces it (key 0).  Any
+                // other NaN candidate overflows (key kNanKey: never less).
+                uint32_t mt = kNil;   // the earliest earlier candidate
+                while (xk != kNil) {
+                    const uint32_t dx = S.cd2[xk];
+                    const uint32_t nx = S.cnext[xk];
+                    const bool earlier = xk < tid;
+                    const bool better = earlier && (dx < bd || (dx == bd && xk < bt));
+                    bd = better ? dx : bd;
+                    bt = better ? xk : bt;
+                    beaten |= !earlier && dx < me;
+                    mt = earlier && xk < mt ? xk : mt;
+                    xk = nx == tid ? myprev : nx;
+                }
+                if (mt != kNil && S.cd2[mt] == kNanKey) { bd = 0u; bt = mt; }
+                if (isn) {
+                    meff = bt == kNil ? 0u : kNanKey;
+                    beaten = false;
+                }
             }
-            if (bt != kNil && !(me < bd)) {
+            if (bt != kNil && !(meff < bd)) {
                 em = 0;                                // not a record: overflows at its key
             } else {
                 if (bt != kNil) {                      // displaces the record before it
@@ -2678,7 +2748,7 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
                     gsrc = ((uint32_t)occ & jmask) * 16;
                 }
                 if (!beaten)                           // last record: the new occupant
-                    S.tab[local] = ((unsigned long long)me << 33) | ((unsigned long long)dn << kJBits) |
+                    S.tab[local] = ((unsigned long long)meff << 33) | ((unsigned long long)dn << kJBits) |
                                    (wide ? 0u : ((uint32_t)(gn + 1) << 23)) | j;
             }
         }
@@ -2997,18 +3067,19 @@ __device__ __forceinline__ void small_process(const SlabParams& P, SmallLds& S, 
             const int32_t lx = sd.ox - rx, ly = sd.oy - ry;
             const bool layer_ok = sd.layer_ok;
             const bool range_ok = lx >= 0 && ly >= 0 && lx < P.tx && ly < P.ty;
-            pending = valid && layer_ok && range_ok;
-            local = pending ? (uint32_t)(ly * P.tx + lx) : 0u;
+            float X, Y, Z;
+            slot_centre(sd, G.cr, zt, X, Y, Z);
+            d2 = dist2(X, Y, Z, x, y, z);
+            const bool foreign = !range_ok && d2 != d2;   // NaN x or y: slot (0, 0) outside the table (see k_slab)
+            pending = valid && layer_ok && (range_ok || foreign);
+            local = pending ? (range_ok ? (uint32_t)(ly * P.tx + lx) : kForeignSlot) : 0u;
             if (pending && pk[ci] - P.kf_lo < P.kf_n) {   // merge mode: forced emission
                 pending = false;
                 self_em = true;
             }
-            float X, Y, Z;
-            slot_centre(sd, G.cr, zt, X, Y, Z);
-            d2 = dist2(X, Y, Z, x, y, z);
             const int d = sd.d;
             int g = sd.g;
-            const bool bad = valid && (!layer_ok || !range_ok || d < 0 || (P.check_gchild && g < 0));
+            const bool bad = valid && (!layer_ok || (!range_ok && !foreign) || d < 0 || (P.check_gchild && g < 0));
             if (__ballot(bad)) {
                 if (bad) err |= slot_route_errs(slot_route(x, y, z, G), layer_ok, range_ok, cx, cy, cz, t, P.check_gchild);
             }
@@ -3075,7 +3146,7 @@ __device__ __forceinline__ void small_process(const SlabParams& P, SmallLds& S, 
             if (pending && (claim[hc] & kClaimDone) == tid) {
                 const unsigned long long occ = S.tab[e];
                 const unsigned long long mine =
-                    ((unsigned long long)f2u(d2) << 33) | ((unsigned long long)dn << kJBits) | j;
+                    ((unsigned long long)dist_key(d2) << 33) | ((unsigned long long)dn << kJBits) | j;
                 if (occ == kEmpty64) {
                     S.tab[e] = mine;
                     rec_e[ci] = e;
@@ -3302,14 +3373,15 @@ __global__ __launch_bounds__(64, PCC_WAVE_OCC) void k_slab_wave(SlabParams P) {
             const int32_t lx = sd.ox - rx, ly = sd.oy - ry;
             const bool layer_ok = sd.layer_ok;
             const bool range_ok = lx >= 0 && ly >= 0 && lx < P.tx && ly < P.ty;
-            bool pending = valid && layer_ok && range_ok;
-            const uint32_t local = pending ? (uint32_t)(ly * P.tx + lx) : 0u;
             float X, Y, Z;
             slot_centre(sd, G.cr, zt, X, Y, Z);
             const float d2 = dist2(X, Y, Z, x, y, z);
+            const bool foreign = !range_ok && d2 != d2;   // NaN x or y: slot (0, 0) outside the table (see k_slab)
+            bool pending = valid && layer_ok && (range_ok || foreign);
+            const uint32_t local = pending ? (range_ok ? (uint32_t)(ly * P.tx + lx) : kForeignSlot) : 0u;
             const int d = sd.d;
             int g = sd.g;
-            const bool bad = valid && (!layer_ok || !range_ok || d < 0 || (P.check_gchild && g < 0));
+            const bool bad = valid && (!layer_ok || (!range_ok && !foreign) || d < 0 || (P.check_gchild && g < 0));
             if (__ballot(bad)) {
                 if (bad) err |= slot_route_errs(slot_route(x, y, z, G), layer_ok, range_ok, cx, cy, cz, t, P.check_gchild);
             }
@@ -3349,7 +3421,7 @@ __global__ __launch_bounds__(64, PCC_WAVE_OCC) void k_slab_wave(SlabParams P) {
                     if (pending && rk == r) {
                         const unsigned long long occ =
                             __hip_atomic_load(&W.tab[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-                        const unsigned long long mine = ((unsigned long long)f2u(d2) << 33) |
+                        const unsigned long long mine = ((unsigned long long)dist_key(d2) << 33) |
                                                         ((unsigned long long)dn << 28) |
                                                         ((unsigned long long)local << 14) | j;
                         if ((occ >> 33) == 0x7FFFFFFFull) {
@@ -4289,6 +4361,7 @@ int Engine::build() {
     if (prior_ && (h0_ || max_levels_)) return fail(-22, "a merge cannot be split into level ranges");
     hierarchies_ = nbatches_ > 0 ? 1u : 0u;   // converter.rs:141-158 runs for every batch, even empty
     stats_ = BuildStats();
+    side_.clear();
     if (n_ == 0) return 0;
 
     // Input of the build.  Merge mode: the existing
@@ -4364,11 +4437,13 @@ int Engine::build() {
     }
     HIP_CHECK(hipMemsetAsync(dev_->ctr, 0, sizeof(Counters), stream_));
 
+    nf_mode_ = false;
+    ninf_ = 0;
     ev_begin(ST_L0);
     int rc = level0_bin();   // also computes the bounding box (converter.rs:96-104)
     if (rc) return rc;
     stats_.ms_level0_bin = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    for (uint32_t i = 0;; i++) {
+    for (uint32_t i = 0; !levels_.empty(); i++) {
         if (h0_ + i >= kMaxDepth) return fail(-75, "hierarchy depth limit (31) reached: more than cell_point_overflow_limit duplicate points?");
         const auto tl = std::chrono::steady_clock::now();
         rc = run_level(i);
@@ -4386,6 +4461,8 @@ int Engine::build() {
     }
     hierarchies_ = std::max<uint32_t>(hierarchies_, h0_ + (uint32_t)levels_.size());
     stats_.levels = (uint32_t)levels_.size();
+    rc = build_infinite();
+    if (rc) return rc;
     if (profiling_) {
         ev_collect();
         Counters hc;
@@ -4502,6 +4579,460 @@ __global__ __launch_bounds__(256) void k_bbox_sample(const Point* __restrict__ i
     }
 }
 
+// ---- inputs with non-finite coordinates (kNfNan / kNfInf, see nf_class)
+// Per block 15 floats: [0..5] min / max xyz over the non-NaN values of every
+// point (f32::min/max skip NaN and keep infinities: bounding-volume/src/
+// lib.rs:23-31); [6..8] 1 where the axis has a non-NaN value (otherwise the
+// reference's box stays NaN there); [9..14] min / max over the points with no
+// infinite coordinate, NaN taken as 0: the extent of the cells those points
+// enter (cell index 0 on a NaN axis, metadata.rs:100-102).
+constexpr int kNfParts = 15;
+__global__ __launch_bounds__(256) void k_bbox_nf(const Point* __restrict__ in, uint64_t n, float* part) {
+    float r[kNfParts];
+    for (int a = 0; a < 3; a++) {
+        r[a] = INFINITY; r[3 + a] = -INFINITY; r[6 + a] = 0.f; r[9 + a] = INFINITY; r[12 + a] = -INFINITY;
+    }
+    const float4* p4 = reinterpret_cast<const float4*>(in);
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+        const float4 v = p4[i];
+        const float c[3] = {v.x, v.y, v.z};
+        const bool fin = nf_class(v.x, v.y, v.z) != kNfInf;
+        for (int a = 0; a < 3; a++) {
+            r[a] = fminf(r[a], c[a]);
+            r[3 + a] = fmaxf(r[3 + a], c[a]);
+            r[6 + a] = isnan(c[a]) ? r[6 + a] : 1.f;
+            const float g = isnan(c[a]) ? 0.f : c[a];
+            if (fin) { r[9 + a] = fminf(r[9 + a], g); r[12 + a] = fmaxf(r[12 + a], g); }
+        }
+    }
+    __shared__ float s[4][kNfParts];
+    for (int k = 0; k < kNfParts; k++) {
+        const bool mx = (k >= 3 && k < 9) || k >= 12;   // max-reduced slots (the flags too)
+        for (int d = 32; d > 0; d >>= 1) {
+            const float o = __shfl_xor(r[k], d, 64);
+            r[k] = mx ? fmaxf(r[k], o) : fminf(r[k], o);
+        }
+    }
+    if ((threadIdx.x & 63) == 0)
+        for (int k = 0; k < kNfParts; k++) s[threadIdx.x / 64][k] = r[k];
+    __syncthreads();
+    if (threadIdx.x < (uint32_t)kNfParts) {
+        const int k = threadIdx.x;
+        const bool mx = (k >= 3 && k < 9) || k >= 12;
+        float v = s[0][k];
+        for (int q = 1; q < 4; q++) v = mx ? fmaxf(v, s[q][k]) : fminf(v, s[q][k]);
+        part[blockIdx.x * kNfParts + k] = v;
+    }
+}
+__global__ void k_bbox_nf_final(float* part, uint32_t nb) {   // one thread per slot
+    const int k = threadIdx.x;
+    if (k >= kNfParts) return;
+    const bool mx = (k >= 3 && k < 9) || k >= 12;
+    float v = part[k];
+    for (uint32_t b = 1; b < nb; b++) v = mx ? fmaxf(v, part[b * kNfParts + k]) : fminf(v, part[b * kNfParts + k]);
+    part[k] = v;
+}
+
+// Stable split of an input into the points without an infinite coordinate and
+// those with one, each with its key (keys: the input's, else its index): per
+// block of 1024 points the count of the latter, then the scatter.
+__global__ __launch_bounds__(1024) void k_nf_count(const Point* __restrict__ in, uint64_t n, uint32_t* cnt) {
+    __shared__ uint32_t c;
+    if (threadIdx.x == 0) c = 0;
+    __syncthreads();
+    const uint64_t i = blockIdx.x * 1024ull + threadIdx.x;
+    bool inf = false;
+    if (i < n) { const float4 v = reinterpret_cast<const float4*>(in)[i]; inf = nf_class(v.x, v.y, v.z) == kNfInf; }
+    const uint64_t m = __ballot(inf);
+    if ((threadIdx.x & 63) == 0 && m) atomicAdd(&c, (uint32_t)__popcll(m));
+    __syncthreads();
+    if (threadIdx.x == 0) cnt[blockIdx.x] = c;
+}
+__global__ __launch_bounds__(1024) void k_nf_scatter(const Point* __restrict__ in, const uint32_t* __restrict__ keys,
+                                                     uint64_t n, const uint32_t* __restrict__ ibase, Point* fout,
+                                                     uint32_t* fkeys, Point* iout, uint32_t* ikeys) {
+    __shared__ uint32_t lds[1024 / 64 + 1];
+    const uint64_t i = blockIdx.x * 1024ull + threadIdx.x;
+    bool inf = false;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (i < n) { v = reinterpret_cast<const float4*>(in)[i]; inf = nf_class(v.x, v.y, v.z) == kNfInf; }
+    uint32_t tot;
+    const uint32_t r = block_excl_scan<1024>(inf ? 1u : 0u, lds, &tot);
+    if (i >= n) return;
+    const uint32_t k = keys ? keys[i] : (uint32_t)i;
+    const uint32_t ib = ibase[blockIdx.x];
+    if (inf) {
+        reinterpret_cast<float4*>(iout)[ib + r] = v;
+        ikeys[ib + r] = k;
+    } else {
+        const uint64_t f = blockIdx.x * 1024ull - ib + threadIdx.x - r;
+        reinterpret_cast<float4*>(fout)[f] = v;
+        fkeys[f] = k;
+    }
+}
+
+// ---- the points with an infinite coordinate.  Their cell index on that axis
+// saturates at every level (metadata.rs:100-102, `as i32`), so they share no
+// cell with the other points, their child cells are not 2c + bit on that axis,
+// and within a cell they pile onto a few slots (hex.rs:67-85 with an infinite
+// operand).  One sequential pass over them in key order follows the
+// reference's per-batch recursion literally: converter.rs:114-139 (levels of
+// one batch), cell.rs:70-94 (grid slot, `new < old` keeps the first on ties and
+// NaN), cell.rs:108-153 (overflow entries: Vacant / Some / None per child).
+// Rare by nature (a data error), so no parallel design: one lane, state in HBM.
+constexpr uint32_t kInfNil = 0xFFFFFFFFu;
+constexpr uint64_t kInfMax = 1ull << 18;   // points with an infinite coordinate per build
+struct InfCell {
+    int32_t h, x, y, z;
+    uint32_t total, number, overflow, nb;
+    int32_t child[8][3];
+    uint32_t st[8];                  // 0 Vacant (created by this batch), 1 Some, 2 None
+    uint32_t len[8], head[8], tail[8];
+    uint32_t stamp[8], cnt[8], mode[8];
+};
+struct InfOut {
+    uint32_t ncells, ngrid, nnodes, err, hier;
+    uint32_t pad;
+    unsigned long long arrivals;
+};
+struct InfBufs {
+    const Point* pts;
+    const uint32_t* keys;
+    uint32_t n;
+    const uint32_t* files;
+    uint32_t nfiles;
+    InfCell* cells;
+    int4* ckey;
+    uint32_t* cval;
+    int4* skey;
+    uint32_t* sval;
+    uint32_t hmask;                  // both hash tables: hmask + 1 entries
+    Point* gp;                       // grid points in creation order, and their cells
+    uint32_t* gcell;
+    Point* np;                       // Some-list nodes
+    uint32_t* nnext;
+    Point* A;
+    Point* B;
+    Point* ov;                       // one level's overflow: point, cell, entry
+    uint32_t* ovc;
+    uint32_t* ovb;
+    InfOut* out;
+    float maxcs;
+    uint32_t dim, limit;
+};
+__device__ __forceinline__ uint32_t inf_hash(int32_t a, int32_t b, int32_t c, int32_t d) {
+    uint64_t h = 0x9E3779B97F4A7C15ull;
+    for (int32_t v : {a, b, c, d}) {
+        h ^= (uint32_t)v;
+        h *= 0xBF58476D1CE4E5B9ull;
+        h ^= h >> 31;
+    }
+    return (uint32_t)h;
+}
+// the value slot of key k (inserted with kInfNil when absent: *fresh)
+__device__ __forceinline__ uint32_t* inf_find(int4* keys, uint32_t* vals, uint32_t mask, int4 k, bool& fresh) {
+    uint32_t i = inf_hash(k.x, k.y, k.z, k.w) & mask;
+    for (;;) {
+        if (vals[i] == kInfNil) {
+            keys[i] = k;
+            fresh = true;
+            return &vals[i];
+        }
+        const int4 q = keys[i];
+        if (q.x == k.x && q.y == k.y && q.z == k.z && q.w == k.w) {
+            fresh = false;
+            return &vals[i];
+        }
+        i = (i + 1) & mask;
+    }
+}
+__global__ __launch_bounds__(64) void k_inf_build(InfBufs B) {
+    if (threadIdx.x != 0) return;
+    uint32_t ncells = 0, ngrid = 0, nbump = 0, nfree = kInfNil, err = 0, hier = 0, stamp = 0;
+    unsigned long long arrivals = 0;
+    for (uint32_t i0 = 0; i0 < B.n && !err;) {
+        const uint32_t batch = event_batch(B.files, B.nfiles, B.keys[i0]);
+        uint32_t i1 = i0 + 1;
+        while (i1 < B.n && event_batch(B.files, B.nfiles, B.keys[i1]) == batch) i1++;
+        const Point* cur = B.pts + i0;
+        uint32_t ncur = i1 - i0;
+        Point* nxt = B.A;
+        for (uint32_t h = 0; ncur && !err; h++) {
+            if (h >= kMaxDepth) { err |= 1u; break; }   // 2u32.pow(h) overflows (converter.rs:141-145)
+            hier = max(hier, h + 1);
+            stamp++;
+            const float cs = cell_size(B.maxcs, h), cr = hex_radius(sub_cell_size(cs, B.dim));
+            const float ccs = cell_size(B.maxcs, h + 1);
+            uint32_t nov = 0;
+            for (uint32_t k = 0; k < ncur; k++) {      // cell.rs:96-106, one cell after another
+                const Point p = cur[k];
+                bool fresh;
+                uint32_t* cv = inf_find(B.ckey, B.cval, B.hmask,
+                                        make_int4((int32_t)h, cell_index1(p.x, cs), cell_index1(p.y, cs), cell_index1(p.z, cs)),
+                                        fresh);
+                if (fresh) {
+                    if (ncells >= B.n) { err |= 2u; break; }
+                    InfCell& C = B.cells[ncells];
+                    C.h = (int32_t)h;
+                    C.x = cell_index1(p.x, cs); C.y = cell_index1(p.y, cs); C.z = cell_index1(p.z, cs);
+                    C.total = C.number = C.overflow = C.nb = 0;
+                    for (int j = 0; j < 8; j++) C.stamp[j] = 0;
+                    *cv = ncells++;
+                }
+                const uint32_t cid = *cv;
+                InfCell& C = B.cells[cid];
+                arrivals++;
+                const I3 o = hex_from_world(p.x, p.y, p.z, cr);
+                uint32_t* sv = inf_find(B.skey, B.sval, B.hmask, make_int4((int32_t)cid, o.x, o.y, o.z), fresh);
+                if (fresh) {
+                    if (ngrid >= B.n) { err |= 2u; break; }
+                    B.gp[ngrid] = p;
+                    B.gcell[ngrid] = cid;
+                    *sv = ngrid++;
+                    C.total++;
+                    C.number++;
+                    continue;
+                }
+                float X, Y, Z;
+                hex_to_world(o, cr, X, Y, Z);
+                const Point old = B.gp[*sv];
+                Point ovp = p;
+                if (dist2(X, Y, Z, p.x, p.y, p.z) < dist2(X, Y, Z, old.x, old.y, old.z)) {
+                    ovp = old;
+                    B.gp[*sv] = p;
+                }
+                B.ov[nov] = ovp;
+                B.ovc[nov] = cid;
+                nov++;
+            }
+            // overflow entries (converter.rs:67-68 -> cell.rs:108-153): this
+            // batch's count per (cell, child) first, then each entry's transition
+            for (uint32_t k = 0; k < nov && !err; k++) {
+                const Point q = B.ov[k];
+                InfCell& C = B.cells[B.ovc[k]];
+                const int32_t cx = cell_index1(q.x, ccs), cy = cell_index1(q.y, ccs), cz = cell_index1(q.z, ccs);
+                uint32_t j = 0;
+                while (j < C.nb && !(C.child[j][0] == cx && C.child[j][1] == cy && C.child[j][2] == cz)) j++;
+                if (j == C.nb) {
+                    if (j == 8) { err |= 4u; break; }
+                    C.child[j][0] = cx; C.child[j][1] = cy; C.child[j][2] = cz;
+                    C.st[j] = 0;
+                    C.len[j] = 0;
+                    C.head[j] = C.tail[j] = kInfNil;
+                    C.stamp[j] = 0;
+                    C.nb++;
+                }
+                if (C.stamp[j] != stamp) { C.stamp[j] = stamp; C.cnt[j] = 0; C.mode[j] = 0; }
+                C.cnt[j]++;
+                B.ovb[k] = j;
+            }
+            uint32_t nn = 0;
+            for (uint32_t k = 0; k < nov && !err; k++) {
+                InfCell& C = B.cells[B.ovc[k]];
+                const uint32_t j = B.ovb[k];
+                if (C.mode[j] == 0) {
+                    const uint32_t c = C.cnt[j];
+                    if (C.st[j] == 0) {                   // Vacant
+                        if (c <= B.limit) { C.st[j] = 1; C.total += c; C.overflow += c; C.mode[j] = 1; }
+                        else { C.st[j] = 2; C.mode[j] = 2; }
+                    } else if (C.st[j] == 2) {            // Occupied(None)
+                        C.mode[j] = 2;
+                    } else if (C.len[j] + c < B.limit) {  // Occupied(Some), still below the limit
+                        C.total += c; C.overflow += c; C.mode[j] = 1;
+                    } else {                              // Some -> None: the old list goes first
+                        C.total -= C.len[j]; C.overflow -= C.len[j];
+                        for (uint32_t e = C.head[j]; e != kInfNil;) {
+                            nxt[nn++] = B.np[e];
+                            const uint32_t f = B.nnext[e];
+                            B.nnext[e] = nfree;
+                            nfree = e;
+                            e = f;
+                        }
+                        C.st[j] = 2;
+                        C.len[j] = 0;
+                        C.head[j] = C.tail[j] = kInfNil;
+                        C.mode[j] = 2;
+                    }
+                }
+                if (C.mode[j] == 2) {
+                    if (nn >= B.n) { err |= 2u; break; }
+                    nxt[nn++] = B.ov[k];
+                    continue;
+                }
+                uint32_t e;
+                if (nfree != kInfNil) { e = nfree; nfree = B.nnext[e]; }
+                else if (nbump < B.n) e = nbump++;
+                else { err |= 2u; break; }
+                B.np[e] = B.ov[k];
+                B.nnext[e] = kInfNil;
+                if (C.tail[j] == kInfNil) C.head[j] = e; else B.nnext[C.tail[j]] = e;
+                C.tail[j] = e;
+                C.len[j]++;
+            }
+            cur = nxt;
+            ncur = nn;
+            nxt = nxt == B.A ? B.B : B.A;
+        }
+        i0 = i1;
+    }
+    B.out->ncells = ncells;
+    B.out->ngrid = ngrid;
+    B.out->nnodes = nbump;
+    B.out->err = err;
+    B.out->hier = hier;
+    B.out->arrivals = arrivals;
+}
+
+// An input with non-finite coordinates (flags from the first level-0 pass):
+// the reference's bounding box (per axis over the non-NaN values, NaN where
+// there are none), the extent of the cells the points without an infinite
+// coordinate enter (NaN as 0), and, if some coordinate is infinite, those
+// points split off from the rest with their keys (the rest are rebinned as
+// keyed input).  Plain builds only: a merge, a keyed (sharded) input and a
+// level-range build return an error as before.
+int Engine::enter_nonfinite(uint32_t flags) {
+    if (prior_ || keyed_ || ext_in_ || h0_ || max_levels_)
+        return fail(-22, "input contains NaN or infinite coordinates (supported in plain builds only, not in merges, "
+                         "sharded or level-range builds)");
+    const uint32_t nb = (uint32_t)std::min<uint64_t>(std::max<uint64_t>((nsrc_ + 255) / 256, 1), kBBoxBlocks);
+    float* part = static_cast<float*>(dev_->get((uint64_t)nb * kNfParts * 4));
+    k_bbox_nf<<<nb, 256, 0, stream_>>>(src_, nsrc_, part);
+    k_bbox_nf_final<<<1, 64, 0, stream_>>>(part, nb);
+    HIP_CHECK(hipGetLastError());
+    float r[kNfParts];
+    HIP_CHECK(hipMemcpyAsync(r, part, sizeof r, hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    for (int a = 0; a < 3; a++) {
+        bmin_[a] = r[6 + a] != 0.f ? r[a] : NAN;
+        bmax_[a] = r[6 + a] != 0.f ? r[3 + a] : NAN;
+        gmin_[a] = r[9 + a];
+        gmax_[a] = r[12 + a];
+    }
+    if (flags & kNfInf) {
+        const uint64_t nbk = (nsrc_ + 1023) / 1024;
+        uint32_t* cnt = static_cast<uint32_t*>(dev_->get(nbk * 4 + 16));
+        uint32_t* tot = cnt + nbk + 1;
+        k_nf_count<<<(uint32_t)nbk, 1024, 0, stream_>>>(src_, nsrc_, cnt);
+        scan_excl_u32(cnt, cnt, (uint32_t)nbk, tot, dev_->scan, stream_);
+        uint32_t ni = 0;
+        HIP_CHECK(hipMemcpyAsync(&ni, tot, 4, hipMemcpyDeviceToHost, stream_));
+        HIP_CHECK(hipStreamSynchronize(stream_));
+        const uint64_t nf = nsrc_ - ni;
+        if (nf_cap_ < nf) {
+            dev_release(d_nf_pts_); dev_release(d_nf_keys_);
+            dev_alloc_t(d_nf_pts_, std::max<uint64_t>(nf, 1) * sizeof(Point));
+            dev_alloc_t(d_nf_keys_, std::max<uint64_t>(nf, 1) * 4);
+            nf_cap_ = nf;
+        }
+        if (inf_cap_ < ni) {
+            dev_release(d_inf_pts_); dev_release(d_inf_keys_);
+            dev_alloc_t(d_inf_pts_, std::max<uint64_t>(ni, 1) * sizeof(Point));
+            dev_alloc_t(d_inf_keys_, std::max<uint64_t>(ni, 1) * 4);
+            inf_cap_ = ni;
+        }
+        k_nf_scatter<<<(uint32_t)nbk, 1024, 0, stream_>>>(src_, src_keys_, nsrc_, cnt, d_nf_pts_, d_nf_keys_, d_inf_pts_,
+                                                          d_inf_keys_);
+        HIP_CHECK(hipGetLastError());
+        src_ = d_nf_pts_;
+        src_keys_ = d_nf_keys_;
+        nsrc_ = nf;
+        ninf_ = ni;
+    }
+    nf_mode_ = true;
+    return 0;
+}
+
+// The cells of the points with an infinite coordinate (k_inf_build) as host
+// cell files.  The other points' cells never saturate an index at the levels
+// built (checked here), so the two sets of cells are disjoint.
+int Engine::build_infinite() {
+    side_.clear();
+    if (ninf_ == 0) return 0;
+    if (ninf_ > kInfMax) return fail(-22, "more than 2^18 points with infinite coordinates in one build are not supported");
+    if (nsrc_) {
+        float m = 0.f;
+        for (int a = 0; a < 3; a++) m = std::max(m, std::max(std::fabs(gmin_[a]), std::fabs(gmax_[a])));
+        const uint32_t hl = h0_ + (uint32_t)std::max<size_t>(levels_.size(), 1) - 1;
+        if (!(m / cell_size(cfg_.max_cell_size, hl) < 1.0e9f))
+            return fail(-22, "finite coordinates that saturate a cell index mixed with infinite ones are not supported");
+    }
+    const uint32_t n = (uint32_t)ninf_;
+    uint32_t hc = 16;
+    while (hc < 2 * n) hc <<= 1;
+    InfBufs B{};
+    B.pts = d_inf_pts_;
+    B.keys = d_inf_keys_;
+    B.n = n;
+    B.files = dev_->files;
+    B.nfiles = nfiles_dev_;
+    B.cells = static_cast<InfCell*>(dev_->get((uint64_t)n * sizeof(InfCell)));
+    B.ckey = static_cast<int4*>(dev_->get((uint64_t)hc * 16));
+    B.cval = static_cast<uint32_t*>(dev_->get((uint64_t)hc * 4));
+    B.skey = static_cast<int4*>(dev_->get((uint64_t)hc * 16));
+    B.sval = static_cast<uint32_t*>(dev_->get((uint64_t)hc * 4));
+    B.hmask = hc - 1;
+    B.gp = static_cast<Point*>(dev_->get((uint64_t)n * 16));
+    B.gcell = static_cast<uint32_t*>(dev_->get((uint64_t)n * 4));
+    B.np = static_cast<Point*>(dev_->get((uint64_t)n * 16));
+    B.nnext = static_cast<uint32_t*>(dev_->get((uint64_t)n * 4));
+    B.A = static_cast<Point*>(dev_->get((uint64_t)n * 16));
+    B.B = static_cast<Point*>(dev_->get((uint64_t)n * 16));
+    B.ov = static_cast<Point*>(dev_->get((uint64_t)n * 16));
+    B.ovc = static_cast<uint32_t*>(dev_->get((uint64_t)n * 4));
+    B.ovb = static_cast<uint32_t*>(dev_->get((uint64_t)n * 4));
+    B.out = static_cast<InfOut*>(dev_->get(sizeof(InfOut)));
+    B.maxcs = cfg_.max_cell_size;
+    B.dim = cfg_.sub_grid_dimension;
+    B.limit = cfg_.cell_point_overflow_limit;
+    HIP_CHECK(hipMemsetAsync(B.cval, 0xFF, (uint64_t)hc * 4, stream_));
+    HIP_CHECK(hipMemsetAsync(B.sval, 0xFF, (uint64_t)hc * 4, stream_));
+    k_inf_build<<<1, 64, 0, stream_>>>(B);
+    HIP_CHECK(hipGetLastError());
+    InfOut o;
+    HIP_CHECK(hipMemcpyAsync(&o, B.out, sizeof o, hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    if (o.err & 1u) return fail(-75, "hierarchy depth limit (31) reached: more than cell_point_overflow_limit duplicate points?");
+    if (o.err) return fail(-34, "infinite-coordinate build: capacity exceeded (internal error)");
+    std::vector<InfCell> cells(o.ncells);
+    std::vector<Point> gp(o.ngrid), np(o.nnodes);
+    std::vector<uint32_t> gcell(o.ngrid), nnext(o.nnodes);
+    if (o.ncells) HIP_CHECK(hipMemcpyAsync(cells.data(), B.cells, (uint64_t)o.ncells * sizeof(InfCell), hipMemcpyDeviceToHost, stream_));
+    if (o.ngrid) {
+        HIP_CHECK(hipMemcpyAsync(gp.data(), B.gp, (uint64_t)o.ngrid * 16, hipMemcpyDeviceToHost, stream_));
+        HIP_CHECK(hipMemcpyAsync(gcell.data(), B.gcell, (uint64_t)o.ngrid * 4, hipMemcpyDeviceToHost, stream_));
+    }
+    if (o.nnodes) {
+        HIP_CHECK(hipMemcpyAsync(np.data(), B.np, (uint64_t)o.nnodes * 16, hipMemcpyDeviceToHost, stream_));
+        HIP_CHECK(hipMemcpyAsync(nnext.data(), B.nnext, (uint64_t)o.nnodes * 4, hipMemcpyDeviceToHost, stream_));
+    }
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    side_.resize(o.ncells);
+    uint64_t kept = 0;
+    for (uint32_t c = 0; c < o.ncells; c++) {
+        const InfCell& C = cells[c];
+        CellFile& f = side_[c];
+        f.h = (uint32_t)C.h;
+        f.idx[0] = C.x; f.idx[1] = C.y; f.idx[2] = C.z;
+        f.total = C.total; f.number = C.number; f.overflow = C.overflow;
+        for (uint32_t j = 0; j < C.nb; j++) {
+            CellFile::Entry e;
+            for (int a = 0; a < 3; a++) e.child[a] = C.child[j][a];
+            e.some = C.st[j] == 1;
+            if (e.some)
+                for (uint32_t q = C.head[j]; q != kInfNil; q = nnext[q]) e.pts.push_back(np[q]);
+            kept += e.pts.size();
+            f.entries.push_back(std::move(e));
+        }
+    }
+    for (uint32_t g = 0; g < o.ngrid; g++) side_[gcell[g]].grid.push_back(gp[g]);
+    stats_.cells += o.ncells;
+    stats_.grid_points += o.ngrid;
+    stats_.kept_points += kept;
+    stats_.arrivals += o.arrivals;
+    hierarchies_ = std::max<uint32_t>(hierarchies_, o.hier);
+    return 0;
+}
+
 // Whether to fold level-0 pass 0 into pass 1 (k_l0_tile6): the grid must have at
 // most two level-0 cells per axis.  Judged from the bounding box of a sample of
 // 512 tiles (the exact box decides after the pass; a wrong guess costs that
@@ -4524,6 +5055,10 @@ bool Engine::fold_hint(float cs) {
 }
 
 int Engine::level0_bin() {
+    if (nf_mode_ && nsrc_ == 0) {   // every point has an infinite coordinate: no finite cells
+        ev_end(ST_L0);
+        return 0;
+    }
     const uint32_t dim = cfg_.sub_grid_dimension;
     const float cs = cell_size(cfg_.max_cell_size, h0_), csc = cell_size(cfg_.max_cell_size, h0_ + 1);
     L0Params P;
@@ -4566,10 +5101,11 @@ int Engine::level0_bin() {
     // most two level-0 cells per axis (judged from a sample of the tiles' bounding
     // box; the full box after the pass decides, else the three-pass binning runs).
     bool fold = false;
+    int rc = 0;
     uint32_t* cnt6 = nullptr;
     uint32_t* ph6 = nullptr;
     uint32_t* gpar = nullptr;
-    if (ntiles && fold_hint(cs) && getenv("PCC_NO_FOLD") == nullptr) {
+    if (ntiles && !nf_mode_ && fold_hint(cs) && getenv("PCC_NO_FOLD") == nullptr) {
         cnt6 = static_cast<uint32_t*>(dev_->get(64ull * ntiles * 4));
         ph6 = static_cast<uint32_t*>(dev_->get(64ull * ntiles * 4));
         gpar = static_cast<uint32_t*>(dev_->get(64ull * ngroups * 32 * 4));
@@ -4587,7 +5123,11 @@ int Engine::level0_bin() {
         HIP_CHECK(hipMemcpyAsync(bb, dev_->bbox_part, sizeof bb, hipMemcpyDeviceToHost, stream_));
         HIP_CHECK(hipMemcpyAsync(&bad, dev_->bbox_flag, 4, hipMemcpyDeviceToHost, stream_));
         HIP_CHECK(hipStreamSynchronize(stream_));
-        if (bad) return fail(-22, "input contains NaN or infinite coordinates (unsupported)");
+        if (bad & ~kNfLayer) {   // non-finite coordinates: the exact boxes, infinite points apart, then again
+            rc = enter_nonfinite(bad);
+            return rc ? rc : level0_bin();
+        }
+        if (bad) return fail(-34, "level-0 binning: layer outside the cell (internal error)");
         fold = true;
         for (int a = 0; a < 3; a++) {
             bmin_[a] = bb[a];
@@ -4620,12 +5160,19 @@ int Engine::level0_bin() {
         HIP_CHECK(hipMemcpyAsync(bb, dev_->bbox_part, sizeof bb, hipMemcpyDeviceToHost, stream_));
         HIP_CHECK(hipMemcpyAsync(&bad, dev_->bbox_flag, 4, hipMemcpyDeviceToHost, stream_));
         HIP_CHECK(hipStreamSynchronize(stream_));
-        if (bad) return fail(-22, "input contains NaN or infinite coordinates (unsupported)");
-        for (int a = 0; a < 3; a++) { bmin_[a] = bb[a]; bmax_[a] = bb[3 + a]; }
+        if (!nf_mode_) {
+            if (bad & ~kNfLayer) {   // non-finite coordinates: the exact boxes, infinite points apart, then again
+                const int rc = enter_nonfinite(bad);
+                return rc ? rc : level0_bin();
+            }
+            for (int a = 0; a < 3; a++) { bmin_[a] = bb[a]; bmax_[a] = bb[3 + a]; }
+        }
     }
+    const float* glo = nf_mode_ ? gmin_ : bmin_;   // the extent the level-0 grid must cover
+    const float* ghi = nf_mode_ ? gmax_ : bmax_;
     for (int a = 0; a < 3; a++) {
-        P.lo[a] = cell_index1(bmin_[a], cs);
-        const int64_t ext = (int64_t)cell_index1(bmax_[a], cs) - P.lo[a] + 1;
+        P.lo[a] = cell_index1(glo[a], cs);
+        const int64_t ext = (int64_t)cell_index1(ghi[a], cs) - P.lo[a] + 1;
         wide |= ext > (1 << 21);
         P.g[a] = (int32_t)std::min<int64_t>(ext, INT32_MAX);
         G *= (uint64_t)ext;

@@ -42,7 +42,6 @@ int write_view_file(const std::string& dir, const pcc_cell_view& v, std::string&
 int write_level_cells(const std::string& dir, const Config& cfg, const LevelHost& L, const Point* grid,
                       const Point* kept, unsigned nthreads, std::string& err);
 unsigned writer_threads();   // PCC_WRITE_THREADS, else min(16, hardware threads)
-struct CellFile;
 // cells as read from disk, written back unchanged (skip[i] != 0: not written)
 int write_cell_files(const std::string& dir, const Config& cfg, const std::vector<CellFile>& cells,
                      const std::vector<uint8_t>* skip, std::string& err);
@@ -51,21 +50,7 @@ int write_output(const std::string& dir, const Metadata& meta, const std::vector
                  bool with_metadata = true);
 int write_metadata(const std::string& dir, const Metadata& meta, std::string& err);
 
-// One cell file as Cell::read_from sees it (cell.rs:183-229, Header::read_from
-// cell.rs:300-335): grid points in file order, overflow entries in file order
-// (n == 0 <=> None, cell.rs:210-212).
-struct CellFile {
-    uint32_t h = 0;
-    int32_t idx[3] = {0, 0, 0};
-    uint32_t total = 0, number = 0, overflow = 0;
-    HostVec<Point> grid;
-    struct Entry {
-        int32_t child[3];
-        bool some;
-        HostVec<Point> pts;
-    };
-    std::vector<Entry> entries;
-};
+// (CellFile: engine.h)
 bool read_cell_file(const std::string& path, CellFile& out, std::string& err);
 // Every h_{h}/c_{x}_{y}_{z}.bin with h < hierarchies (the layout own.rs:16-62 and
 // converter.rs:187-207 read; the order of the returned cells is unspecified).

@@ -215,15 +215,23 @@ def test_depth_limit_is_an_error():
         c.close()
 
 
-def test_nonfinite_input_rejected():
+def test_nonfinite_merge_rejected():
+    """NaN / +-inf coordinates build in plain builds (test_nonfinite_gpu.py); a
+    merge into an existing cloud still rejects them with an error."""
     import pcconv
-    p = synth(1, 0, 100)
-    p["x"][7] = np.nan
     with tempfile.TemporaryDirectory() as tg:
         c = pcconv.Converter(tg)
+        c.add_points(synth(1, 0, 1000))
+        c.build()
+        c.write()
+        c.close()
+        p = synth(2, 0, 100)
+        p["x"][7] = np.nan
+        c = pcconv.Converter(tg)
         c.add_points(p)
-        with pytest.raises(pcconv.PccError):
+        with pytest.raises(pcconv.PccError) as ei:
             c.build()
+        assert "merge" in str(ei.value)
         c.close()
 
 
