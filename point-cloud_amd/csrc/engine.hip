@@ -2232,7 +2232,7 @@ struct ArrSrc {
 #else
 #define GSTAMP(ph) do {} while (0)
 #endif
-template <class L, class SRC>
+template <bool NF, class L, class SRC>
 __device__ __forceinline__ void dense_grid_points(const SlabParams& P, L& S, uint32_t* bm, const SRC& rP,
                                                   uint32_t s, uint32_t n, uint32_t jmask, uint32_t tid, uint32_t lane,
                                                   unsigned long long* st_acc, unsigned long long& st_t0) {
@@ -2261,7 +2261,8 @@ __device__ __forceinline__ void dense_grid_points(const SlabParams& P, L& S, uin
                 atomicAnd(&bm[jw >> 5], ~(1u << (jw & 31u)));
             }
         }
-        if (tid == 0 && S.fj != kEmpty32) atomicAnd(&bm[S.fj >> 5], ~(1u << (S.fj & 31u)));   // a foreign slot's point
+        if constexpr (NF)   // a foreign slot's point
+            if (tid == 0 && S.fj != kEmpty32) atomicAnd(&bm[S.fj >> 5], ~(1u << (S.fj & 31u)));
         GSTAMP(14);
         lds_barrier();
         GSTAMP(15);
@@ -2322,9 +2323,11 @@ __device__ __forceinline__ void dense_grid_points(const SlabParams& P, L& S, uin
 #endif
 #pragma unroll
         for (int u = 0; u < U; u++) bst4(rG, wpos[u], pv[u]);
-        if (tid == 0 && S.fj != kEmpty32) {   // the point holding a foreign slot (NaN coordinates)
-            const uint32_t wf = atomicAdd(&S.nwin, 1u);
-            bst4(rG, wf * 16, rP.p(S.fj * 16));
+        if constexpr (NF) {
+            if (tid == 0 && S.fj != kEmpty32) {   // the point holding a foreign slot (NaN coordinates)
+                const uint32_t wf = atomicAdd(&S.nwin, 1u);
+                bst4(rG, wf * 16, rP.p(S.fj * 16));
+            }
         }
     }
 }
@@ -2349,7 +2352,8 @@ __device__ __forceinline__ void dense_grid_points(const SlabParams& P, L& S, uin
 // chunk the table's occupants are the slab's grid points (cell.rs:158-160:
 // order inside a cell file is free).  Grandchild capacities count every
 // emission's (child, grandchild) slab when its rank is taken.
-template <bool SEEDS>
+// NF: the input has NaN coordinates (the NaN rules below; Engine::nf_mode_).
+template <bool SEEDS, bool NF>
 __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
     using L = DenseLds;
     constexpr int BS = L::BS, TAB = L::TAB, NW = L::NW;
@@ -2540,11 +2544,13 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
         // NaN `as i32` = 0), which can lie outside this cell's table: a "foreign"
         // slot only NaN points reach, so its first arrival is the grid point and
         // every later one overflows.
-        const bool isn = d2 != d2;
+        const bool isn = NF && d2 != d2;
         bool foreign = false;
-        if (__ballot(isn && valid && layer_ok && !range_ok)) {
-            foreign = isn && valid && layer_ok && !range_ok;
-            if (foreign && !forced) atomicMin(&S.fj, j);
+        if constexpr (NF) {
+            if (__ballot(isn && valid && layer_ok && !range_ok)) {
+                foreign = isn && valid && layer_ok && !range_ok;
+                if (foreign && !forced) atomicMin(&S.fj, j);
+            }
         }
         uint32_t dn;
         int32_t gn;
@@ -2572,8 +2578,10 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
         } else {
             occ = kEmpty64;
         }
-        if (cand && isn) S.nanc[par] = 1u;
-        if (tid == 0) S.nanc[par ^ 1u] = 0u;   // the other parity's flag (read before the last barrier)
+        if constexpr (NF) {
+            if (cand && isn) S.nanc[par] = 1u;
+            if (tid == 0) S.nanc[par ^ 1u] = 0u;   // the other parity's flag (read before the last barrier)
+        }
         if (cand) {
             // push onto the slot's list: swap this thread into the head's half of
             // the word (a CAS retried while other pushes change the word); the
@@ -2683,8 +2691,10 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
         }
         // ---- phase B (2): records of chunk i (walk of the slot's candidate list)
         int32_t em = (slotted && !cand && (forced || occ != kEmpty64)) ? 0 : -1;
-        if (__ballot(foreign)) {   // a foreign slot: the first NaN point holds it, the others overflow
-            if (foreign && S.fj != j) em = 0;
+        if constexpr (NF) {
+            if (__ballot(foreign)) {   // a foreign slot: the first NaN point holds it, the others overflow
+                if (foreign && S.fj != j) em = 0;
+            }
         }
         uint32_t emd = dn;
         int32_t emg = gn;
@@ -2699,7 +2709,7 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
             uint32_t xk = (S.head[local >> 1] >> ((local & 1u) * 16u)) & kNil;
             if (xk == tid) xk = myprev;
             uint32_t meff = me;
-            if (!S.nanc[par]) {
+            if (!NF || !S.nanc[par]) {
                 while (xk != kNil) {
                     const uint32_t dx = S.cd2[xk];
                     const uint32_t nx = S.cnext[xk];
@@ -2806,7 +2816,7 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
 #ifndef PCC_STAMPS
     unsigned long long* st_acc = nullptr, st_t0 = 0;
 #endif
-    dense_grid_points<L>(P, S, S.head, rP, s, n, jmask, tid, lane, st_acc, st_t0);
+    dense_grid_points<NF, L>(P, S, S.head, rP, s, n, jmask, tid, lane, st_acc, st_t0);
     STAMP(8);
     STAMP_FLUSH(P.stamps);
     if (err) atomicOr(&S.err, err);
@@ -5640,8 +5650,9 @@ int Engine::run_level(uint32_t li) {
         SP.stamps = stamps;
 #endif
         ev_begin(ST_DENSE);
-        if (seeds_in_place) k_slab<true><<<L->nbig, kDenseBS, 0, stream_>>>(SP);
-        else k_slab<false><<<L->nbig, kDenseBS, 0, stream_>>>(SP);
+        if (seeds_in_place) k_slab<true, false><<<L->nbig, kDenseBS, 0, stream_>>>(SP);
+        else if (nf_mode_) k_slab<false, true><<<L->nbig, kDenseBS, 0, stream_>>>(SP);
+        else k_slab<false, false><<<L->nbig, kDenseBS, 0, stream_>>>(SP);
         ev_end(ST_DENSE);
         if (verbose) {
             HIP_CHECK(hipStreamSynchronize(stream_));
