@@ -1682,9 +1682,12 @@ __device__ __forceinline__ uint32_t l0_tile_of(const uint32_t* __restrict__ vrow
     }
     return lo;
 }
+// (dcnt: the unit and window counts on the device, k_l0_uplan; else the arguments)
 __global__ void k_l0_wplan(const L0UnitW* __restrict__ units, uint32_t nunits, uint32_t nwin,
-                           const uint32_t* __restrict__ voff, uint32_t ntiles, uint2* __restrict__ wt) {
+                           const uint32_t* __restrict__ voff, uint32_t ntiles, uint2* __restrict__ wt,
+                           const uint32_t* __restrict__ dcnt) {
     const uint32_t wi = blockIdx.x * blockDim.x + threadIdx.x;
+    if (dcnt) { nunits = dcnt[0]; nwin = dcnt[1]; }
     if (wi >= nwin) return;
     uint32_t lo = 0, hi = nunits - 1;   // the unit of window wi: last with w0 <= wi
     while (lo < hi) {
@@ -1696,6 +1699,69 @@ __global__ void k_l0_wplan(const L0UnitW* __restrict__ units, uint32_t nunits, u
     const uint32_t v1 = min(v0 + (uint32_t)kL0Tile, U.b) - 1;
     const uint32_t* vrow = voff + (uint64_t)U.d6 * ntiles;
     wt[wi] = make_uint2(l0_tile_of(vrow, U.t0, U.t1, v0), l0_tile_of(vrow, U.t0, U.t1, v1));
+}
+
+// The pass-2 units of the folded binning, planned on the device (no host round
+// trip between the passes): row d6 of the segment starts is cut into
+// ceil(size / target) units, unit k taking the groups whose segment starts at
+// [k target, (k + 1) target) from the row's first point (a segment is never
+// split; a unit no segment starts in is empty and its block exits).  Units are
+// numbered row after row; umax >= their count (64 + n / target) is the launch
+// size.  Also each unit's first window (exclusive prefix of its windows of
+// kL0Tile points) and, in out[0..1], the unit and window totals.
+__global__ __launch_bounds__(1024) void k_l0_uplan(const uint32_t* __restrict__ starts, uint32_t ngroups, uint32_t tpg,
+                                                   uint32_t ntiles, uint32_t target, uint32_t umax,
+                                                   L0UnitW* __restrict__ uw, uint32_t* __restrict__ out) {
+    __shared__ uint32_t ub[65];
+    __shared__ uint32_t lds[1024 / 64 + 1];
+    const uint32_t tid = threadIdx.x;
+    uint32_t tot;
+    {
+        uint32_t nu = 0;
+        if (tid < 64) {
+            const uint32_t* row = starts + (uint64_t)tid * (ngroups + 1);
+            const uint32_t size = row[ngroups] - row[0];
+            nu = (size + target - 1) / target;
+        }
+        const uint32_t e = block_excl_scan<1024>(nu, lds, &tot);
+        if (tid < 64) ub[tid] = e;
+        if (tid == 0) ub[64] = tot;
+    }
+    __syncthreads();
+    const uint32_t nunits = ub[64];
+    const uint32_t per = (umax + 1023) / 1024, u0 = min(tid * per, umax), u1 = min(u0 + per, umax);
+    uint32_t wsum = 0;
+    for (uint32_t u = u0; u < u1; u++) {
+        L0UnitW W{0, 0, 0, 0, 0, 0, 0, 0};
+        if (u < nunits) {
+            uint32_t d = 0;
+            while (ub[d + 1] <= u) d++;   // (64 rows)
+            const uint32_t k = u - ub[d];
+            const uint32_t* row = starts + (uint64_t)d * (ngroups + 1);
+            const uint32_t r0 = row[0];
+            auto first_at = [&](uint64_t off) {   // first group whose segment starts >= r0 + off (ngroups: none)
+                uint32_t lo = 0, hi = ngroups;
+                while (lo < hi) {
+                    const uint32_t m = (lo + hi) >> 1;
+                    if ((uint64_t)(row[m] - r0) >= off) hi = m; else lo = m + 1;
+                }
+                return lo;
+            };
+            const uint32_t g0 = first_at((uint64_t)k * target), g1 = first_at((uint64_t)(k + 1) * target);
+            W.d6 = d;
+            W.a = row[g0];
+            W.b = row[g1];
+            W.t0 = g0 * tpg;
+            W.t1 = min(g1 * tpg, ntiles);
+            W.pad_g0 = min(g0, ngroups - 1);
+        }
+        W.w0 = wsum;
+        wsum += (W.b - W.a + kL0Tile - 1) / kL0Tile;
+        uw[u] = W;
+    }
+    const uint32_t base = block_excl_scan<1024>(wsum, lds, &tot);
+    for (uint32_t u = u0; u < u1; u++) uw[u].w0 += base;
+    if (tid == 0) { out[0] = nunits; out[1] = tot; }
 }
 
 // start of segment (d6, g) of the pass-1 output, g = 0..ngroups (the end)
@@ -2010,8 +2076,9 @@ __global__ void k_l0_flags(const uint32_t* hist, uint32_t D, int32_t nl, uint32_
 __global__ void k_l0_tables(const uint32_t* hist, const uint32_t* cnt_scan, const uint32_t* sflag_scan,
                             const uint32_t* cflag, const uint32_t* cflag_scan, uint32_t D, uint32_t G, L0Params P,
                             int32_t* cell_idx, uint32_t* cell_sb, uint32_t* cell_slab0, uint32_t* slab_cell,
-                            int32_t* slab_layer, uint32_t* slab_off, uint32_t* slab_n) {
+                            int32_t* slab_layer, uint32_t* slab_off, uint32_t* slab_n, const uint32_t* d_tot) {
     const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+    if (d_tot && d == 0) cell_slab0[d_tot[2]] = d_tot[1];   // (else k_set_u32 from the host totals)
     if (d < G && cflag[d]) {
         const uint32_t r = cflag_scan[d];
         int32_t gx, gy, gz;
@@ -3907,8 +3974,10 @@ __global__ __launch_bounds__(256) void k_next_emit(NextParams Q) {
 }
 
 // big / small slab lists at level 0 (block-aggregated atomics)
+// (dn: the slab count on the device, else nslabs)
 __global__ __launch_bounds__(256) void k_l0_lists(const uint32_t* slab_n, uint32_t nslabs, uint32_t* big,
-                                                  uint32_t* small, Counters* ctr) {
+                                                  uint32_t* small, Counters* ctr, const uint32_t* dn) {
+    if (dn) nslabs = *dn;
     __shared__ uint32_t nb, ns, bb, bs;
     __shared__ unsigned long long ab, as;
     if (threadIdx.x == 0) { nb = 0; ns = 0; ab = 0; as = 0; }
@@ -5273,6 +5342,10 @@ int Engine::level0_bin() {
     uint32_t* starts = nullptr;
     L0Unit* dunits = nullptr;
     uint32_t nunits = 0;
+    // The folded binning runs from the bounding box's sync to the end of pass 2
+    // without a host round trip: tables sized by the grid's slab and cell bounds
+    // (D, G), units planned on the device, the totals read once at the end.
+    const bool defer = fold && root_xyz_.empty() && !prior_ && getenv("PCC_L0_HOSTPLAN") == nullptr;
     if (g1up) {
         starts = static_cast<uint32_t*>(dev_->get(64ull * (ngroups + 1) * 4));
         if (fold) {
@@ -5300,14 +5373,15 @@ int Engine::level0_bin() {
         }
         HIP_CHECK(hipGetLastError());
         // the segment starts go to pinned host memory now; the unit plan is made
-        // after the one host sync of the level (below)
+        // after the one host sync of the level (below).  The folded binning plans
+        // its units on the device (k_l0_uplan).
         const uint64_t nst = 64ull * (ngroups + 1);
-        if (dev_->hst_cap < nst) {
+        if (!defer && dev_->hst_cap < nst) {
             if (dev_->hst) (void)hipHostFree(dev_->hst);
             HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&dev_->hst), nst * 4, hipHostMallocDefault));
             dev_->hst_cap = nst;
         }
-        HIP_CHECK(hipMemcpyAsync(dev_->hst, starts, nst * 4, hipMemcpyDeviceToHost, stream_));
+        if (!defer) HIP_CHECK(hipMemcpyAsync(dev_->hst, starts, nst * 4, hipMemcpyDeviceToHost, stream_));
     }
     HIP_CHECK(hipGetLastError());
     Arena src = dst;
@@ -5340,10 +5414,17 @@ int Engine::level0_bin() {
         scan_excl_u32(hist, cnt_scan, (uint32_t)D, d_tot + 0, dev_->scan, stream_);
         scan_excl_u32(sflag, sflag, (uint32_t)D, d_tot + 1, dev_->scan, stream_);
         scan_excl_u32(cflag, cscan, (uint32_t)G, d_tot + 2, dev_->scan, stream_);
-        HIP_CHECK(hipMemcpyAsync(tots, d_tot, 12, hipMemcpyDeviceToHost, stream_));
-        HIP_CHECK(hipMemcpyAsync(&hc, dev_->ctr, sizeof hc, hipMemcpyDeviceToHost, stream_));
-        HIP_CHECK(hipStreamSynchronize(stream_));
-        if (hc.err) return fail(-34, "level-0 binning: point outside the bounding grid (internal error)");
+        if (!defer) {
+            HIP_CHECK(hipMemcpyAsync(tots, d_tot, 12, hipMemcpyDeviceToHost, stream_));
+            HIP_CHECK(hipMemcpyAsync(&hc, dev_->ctr, sizeof hc, hipMemcpyDeviceToHost, stream_));
+            HIP_CHECK(hipStreamSynchronize(stream_));
+            if (hc.err) return fail(-34, "level-0 binning: point outside the bounding grid (internal error)");
+        }
+    }
+    if (defer) {   // upper bounds until the totals are read (below)
+        tots[0] = (uint32_t)nsrc_;
+        tots[1] = (uint32_t)D;
+        tots[2] = (uint32_t)G;
     }
     if (tots[0] != nsrc_) return fail(-5, "level-0 histogram mismatch");
     Level* L = new Level();
@@ -5366,9 +5447,28 @@ int Engine::level0_bin() {
     L->alloc(L->dcap, (uint64_t)L->nslabs * kDests);
     k_l0_tables<<<grid_for(std::max<uint64_t>(D, G), 256, 1u << 30), 256, 0, stream_>>>(
         hist, cnt_scan, sflag, cflag, cscan, (uint32_t)D, (uint32_t)G, P, L->cell_idx, L->cell_sb, L->cell_slab0,
-        L->slab_cell, L->slab_layer, L->slab_off, L->slab_n);
-    k_set_u32<<<1, 1, 0, stream_>>>(L->cell_slab0 + L->ncells, L->nslabs);
-    if (g1up) {   // pass 2 into arena 0, with the capacities
+        L->slab_cell, L->slab_layer, L->slab_off, L->slab_n, defer ? d_tot : nullptr);
+    if (!defer) k_set_u32<<<1, 1, 0, stream_>>>(L->cell_slab0 + L->ncells, L->nslabs);
+    if (defer) {   // pass 2 of the folded binning, planned on the device
+        const uint64_t target = std::max<uint64_t>(nsrc_ / 8192, 4ull * kL0Tile);
+        const uint32_t umax = (uint32_t)(64 + (nsrc_ + target - 1) / target);
+        const uint32_t wmax = (uint32_t)((nsrc_ + kL0Tile - 1) / kL0Tile) + umax;
+        L0UnitW* duw = static_cast<L0UnitW*>(dev_->get((uint64_t)umax * sizeof(L0UnitW)));
+        uint2* dwt = static_cast<uint2*>(dev_->get((uint64_t)wmax * sizeof(uint2)));
+        uint32_t* dcnt = static_cast<uint32_t*>(dev_->get(16));
+        HIP_CHECK(hipMemsetAsync(L->dcap, 0, (uint64_t)L->nslabs * kDests * 4, stream_));
+        k_l0_uplan<<<1, 1024, 0, stream_>>>(starts, ngroups, tpg, ntiles, (uint32_t)target, umax, duw, dcnt);
+        k_l0_wplan<<<grid_for(wmax, 256, 1u << 30), 256, 0, stream_>>>(duw, 0, 0, cnt6, ntiles, dwt, dcnt);
+        if (l0keys)
+            k_l0_down5g<32, true, false><<<umax, kL0BS, 0, stream_>>>(src, dst, P, nullptr, starts, ngroups, gcnt,
+                                                                       cnt_scan, sflag, (uint32_t)D, L->dcap, l0dummy,
+                                                                       dev_->ctr, duw, dwt, cnt6, ph6, ntiles);
+        else
+            k_l0_down5g<32, true, true><<<umax, kL0BS, 0, stream_>>>(src, dst, P, nullptr, starts, ngroups, gcnt,
+                                                                      cnt_scan, sflag, (uint32_t)D, L->dcap, l0dummy,
+                                                                      dev_->ctr, duw, dwt, cnt6, ph6, ntiles);
+        HIP_CHECK(hipGetLastError());
+    } else if (g1up) {   // pass 2 into arena 0, with the capacities
         // Units: runs of consecutive segments of one d6 bucket, about nsrc / 8192
         // points each, in bucket order (a segment is never split; with the default
         // groups a segment is at most 4 x the target).  Planned on the host while
@@ -5421,7 +5521,7 @@ int Engine::level0_bin() {
             duw = static_cast<L0UnitW*>(dev_->get((uint64_t)nunits * sizeof(L0UnitW)));
             dwt = static_cast<uint2*>(dev_->get(std::max<uint64_t>(nwin, 1) * sizeof(uint2)));
             HIP_CHECK(hipMemcpyAsync(duw, uw.data(), nunits * sizeof(L0UnitW), hipMemcpyHostToDevice, stream_));
-            k_l0_wplan<<<grid_for(nwin, 256, 1u << 30), 256, 0, stream_>>>(duw, nunits, nwin, cnt6, ntiles, dwt);
+            k_l0_wplan<<<grid_for(nwin, 256, 1u << 30), 256, 0, stream_>>>(duw, nunits, nwin, cnt6, ntiles, dwt, nullptr);
             if (l0keys)
                 k_l0_down5g<32, true, false><<<nunits, kL0BS, 0, stream_>>>(src, dst, P, dunits, starts, ngroups, gcnt,
                                                                              cnt_scan, sflag, (uint32_t)D, L->dcap, l0dummy,
@@ -5456,7 +5556,25 @@ int Engine::level0_bin() {
             L->cell_idx, L->slab_cell, L->slab_layer, L->nslabs, pdev_[0].cells, pdev_[0].cell_slab0, pdev_[0].slab_layer,
             pdev_[0].ncells, L->slab_prior);
     }
-    k_l0_lists<<<grid_for(L->nslabs, 256, 1u << 30), 256, 0, stream_>>>(L->slab_n, L->nslabs, L->big_list, L->small_list, dev_->ctr);
+    k_l0_lists<<<grid_for(L->nslabs, 256, 1u << 30), 256, 0, stream_>>>(L->slab_n, L->nslabs, L->big_list,
+                                                                          L->small_list, dev_->ctr, defer ? d_tot + 1 : nullptr);
+    if (defer) {   // the level's one sync after the bounding box's: totals, lists, errors
+        HIP_CHECK(hipMemcpyAsync(tots, d_tot, 12, hipMemcpyDeviceToHost, stream_));
+        HIP_CHECK(hipMemcpyAsync(&hc, dev_->ctr, sizeof hc, hipMemcpyDeviceToHost, stream_));
+        HIP_CHECK(hipStreamSynchronize(stream_));
+        ev_end(ST_L0);
+        if (hc.err) return fail(-34, "level-0 binning: point outside the bounding grid (internal error)");
+        if (tots[0] != nsrc_) return fail(-5, "level-0 histogram mismatch");
+        L->ncells = tots[2];
+        L->nslabs = tots[1];
+        L->max_slab = hc.max_slab;
+        L->nbig = hc.nbig;
+        L->nsmall = hc.nsmall;
+        stats_.cells += L->ncells;
+        stats_.slabs += L->nslabs;
+        stats_.arrivals += nsrc_;
+        return 0;
+    }
     {
         HIP_CHECK(hipMemcpyAsync(&hc, dev_->ctr, sizeof hc, hipMemcpyDeviceToHost, stream_));
         HIP_CHECK(hipStreamSynchronize(stream_));

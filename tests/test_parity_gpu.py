@@ -42,6 +42,17 @@ def test_adversarial_small(seed):
     _check([_to_np(f) for f in files], cfg=cfg, batch=batch)
 
 
+@pytest.mark.parametrize("env", [{}, {"PCC_NO_FOLD": "1"}], ids=["fold", "threepass"])
+def test_single_level0_cell(env, monkeypatch):
+    """Every point in one level-0 cell (a rank's octant after the sharded
+    exchange): a 1 x 1 x 1 level-0 grid through both level-0 binnings."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    pts = synth(41, 0, 2_000_000, lo=0.0, ext=1000.0)
+    st = _check([pts], fast=True)
+    assert st["levels"] >= 2
+
+
 def test_config1_uniform_100k():
     pts = synth(1, 0, 100_000)
     st = _check([pts])
