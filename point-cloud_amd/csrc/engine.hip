@@ -292,6 +292,7 @@ struct Engine::Level {
     Point* grid = nullptr;           // this level's winner region (arrivals entries)
     Point* kept = nullptr;           // this level's kept-list region
     uint64_t kept_cap = 0;
+    unsigned long long* ksort = nullptr;   // limit > kKeptMax: sort scratch of the kept lists (2 words per point)
     uint32_t kept_used = 0;
     uint32_t* bkt_state = nullptr;   // 8 * ncells
     uint32_t* bkt_off = nullptr;
@@ -1706,62 +1707,63 @@ __global__ void k_l0_wplan(const L0UnitW* __restrict__ units, uint32_t nunits, u
 // ceil(size / target) units, unit k taking the groups whose segment starts at
 // [k target, (k + 1) target) from the row's first point (a segment is never
 // split; a unit no segment starts in is empty and its block exits).  Units are
-// numbered row after row; umax >= their count (64 + n / target) is the launch
-// size.  Also each unit's first window (exclusive prefix of its windows of
-// kL0Tile points) and, in out[0..1], the unit and window totals.
-__global__ __launch_bounds__(1024) void k_l0_uplan(const uint32_t* __restrict__ starts, uint32_t ngroups, uint32_t tpg,
-                                                   uint32_t ntiles, uint32_t target, uint32_t umax,
-                                                   L0UnitW* __restrict__ uw, uint32_t* __restrict__ out) {
+// numbered row after row, one thread each; umax >= their count (64 + n /
+// target) is the launch size.  wn[u]: the unit's windows of kL0Tile points,
+// whose exclusive scan is each unit's first window (k_l0_uplan_w0); out[0]: the
+// unit count.
+__global__ __launch_bounds__(256) void k_l0_uplan(const uint32_t* __restrict__ starts, uint32_t ngroups, uint32_t tpg,
+                                                  uint32_t ntiles, uint32_t target, uint32_t umax,
+                                                  L0UnitW* __restrict__ uw, uint32_t* __restrict__ wn,
+                                                  uint32_t* __restrict__ out) {
     __shared__ uint32_t ub[65];
-    __shared__ uint32_t lds[1024 / 64 + 1];
-    const uint32_t tid = threadIdx.x;
-    uint32_t tot;
-    {
-        uint32_t nu = 0;
-        if (tid < 64) {
-            const uint32_t* row = starts + (uint64_t)tid * (ngroups + 1);
-            const uint32_t size = row[ngroups] - row[0];
-            nu = (size + target - 1) / target;
+    const uint32_t tid = threadIdx.x, u = blockIdx.x * 256 + tid;
+    if (tid < 64) {   // units per row, exclusive scan over the rows (wave 0)
+        const uint32_t* row = starts + (uint64_t)tid * (ngroups + 1);
+        const uint32_t nu = (row[ngroups] - row[0] + target - 1) / target;
+        uint32_t x = nu;
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(x, d, 64);
+            if (tid >= (uint32_t)d) x += y;
         }
-        const uint32_t e = block_excl_scan<1024>(nu, lds, &tot);
-        if (tid < 64) ub[tid] = e;
-        if (tid == 0) ub[64] = tot;
+        ub[tid] = x - nu;
+        if (tid == 63) ub[64] = x;
     }
     __syncthreads();
     const uint32_t nunits = ub[64];
-    const uint32_t per = (umax + 1023) / 1024, u0 = min(tid * per, umax), u1 = min(u0 + per, umax);
-    uint32_t wsum = 0;
-    for (uint32_t u = u0; u < u1; u++) {
-        L0UnitW W{0, 0, 0, 0, 0, 0, 0, 0};
-        if (u < nunits) {
-            uint32_t d = 0;
-            while (ub[d + 1] <= u) d++;   // (64 rows)
-            const uint32_t k = u - ub[d];
-            const uint32_t* row = starts + (uint64_t)d * (ngroups + 1);
-            const uint32_t r0 = row[0];
-            auto first_at = [&](uint64_t off) {   // first group whose segment starts >= r0 + off (ngroups: none)
-                uint32_t lo = 0, hi = ngroups;
-                while (lo < hi) {
-                    const uint32_t m = (lo + hi) >> 1;
-                    if ((uint64_t)(row[m] - r0) >= off) hi = m; else lo = m + 1;
-                }
-                return lo;
-            };
-            const uint32_t g0 = first_at((uint64_t)k * target), g1 = first_at((uint64_t)(k + 1) * target);
-            W.d6 = d;
-            W.a = row[g0];
-            W.b = row[g1];
-            W.t0 = g0 * tpg;
-            W.t1 = min(g1 * tpg, ntiles);
-            W.pad_g0 = min(g0, ngroups - 1);
+    if (u == 0) out[0] = nunits;
+    if (u >= umax) return;
+    L0UnitW W{0, 0, 0, 0, 0, 0, 0, 0};
+    if (u < nunits) {
+        uint32_t lo = 0, hi = 63;   // the row: last with ub[d] <= u
+        while (lo < hi) {
+            const uint32_t m = (lo + hi + 1) >> 1;
+            if (ub[m] <= u) lo = m; else hi = m - 1;
         }
-        W.w0 = wsum;
-        wsum += (W.b - W.a + kL0Tile - 1) / kL0Tile;
-        uw[u] = W;
+        const uint32_t d = lo, k = u - ub[d];
+        const uint32_t* row = starts + (uint64_t)d * (ngroups + 1);
+        const uint32_t r0 = row[0];
+        auto first_at = [&](uint64_t off) {   // first group whose segment starts >= r0 + off (ngroups: none)
+            uint32_t a = 0, b = ngroups;
+            while (a < b) {
+                const uint32_t m = (a + b) >> 1;
+                if ((uint64_t)(row[m] - r0) >= off) b = m; else a = m + 1;
+            }
+            return a;
+        };
+        const uint32_t g0 = first_at((uint64_t)k * target), g1 = first_at((uint64_t)(k + 1) * target);
+        W.d6 = d;
+        W.a = row[g0];
+        W.b = row[g1];
+        W.t0 = g0 * tpg;
+        W.t1 = min(g1 * tpg, ntiles);
+        W.pad_g0 = min(g0, ngroups - 1);
     }
-    const uint32_t base = block_excl_scan<1024>(wsum, lds, &tot);
-    for (uint32_t u = u0; u < u1; u++) uw[u].w0 += base;
-    if (tid == 0) { out[0] = nunits; out[1] = tot; }
+    uw[u] = W;
+    wn[u] = (W.b - W.a + kL0Tile - 1) / kL0Tile;
+}
+__global__ void k_l0_uplan_w0(L0UnitW* __restrict__ uw, const uint32_t* __restrict__ w0, uint32_t umax) {
+    const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+    if (u < umax) uw[u].w0 = w0[u];
 }
 
 // start of segment (d6, g) of the pass-1 output, g = 0..ngroups (the end)
@@ -3635,6 +3637,7 @@ struct BucketParams {
     uint32_t nprior;
     Point* kept;
     uint64_t kept_cap;
+    unsigned long long* ksort;   // kept lists above kKeptMax: global sort scratch at 2 x their kept offset
     const uint32_t* cell_slab0;
     const uint32_t* dest_off;
     const uint32_t* dest_n;
@@ -3728,7 +3731,8 @@ __global__ __launch_bounds__(kBktBS) void k_bucket(BucketParams B) {
     const bool spilled = tot > L || (tot == L && emin != emax);
     if (!spilled) {
         // Some(list): the bucket's points in key order, kept in this cell's file
-        if (tot > (uint32_t)kKeptMax) {
+        const bool big = tot > (uint32_t)kKeptMax;   // (limit > kKeptMax): sorted in global memory
+        if (big && !B.ksort) {
             if (threadIdx.x == 0) { set_err(B.ctr, ERR_KEPT_CAP); B.bkt_state[b] = 0; }
             return;
         }
@@ -3739,34 +3743,39 @@ __global__ __launch_bounds__(kBktBS) void k_bucket(BucketParams B) {
         }
         __syncthreads();
         if ((uint64_t)s_off + tot > B.kept_cap) return;
+        // the packed words (key << 32 | arena position) in LDS, or for a list
+        // above the LDS capacity in the scratch at twice its kept offset (a
+        // power-of-two padding below twice the list never reaches the next list's)
+        unsigned long long* sk = big ? B.ksort + 2ull * s_off : skp;
         for (uint32_t i = threadIdx.x; i < nd; i += kBktBS) {
             const uint32_t di = (s0 + i / 3) * kDests + oct * 3 + i % 3;
             const uint32_t n = B.dest_n[di];
             if (n) {
                 const uint32_t o = B.dest_off[di];
                 const uint32_t p = atomicAdd(&s_cnt, n);
-                for (uint32_t q = 0; q < n; q++) skp[p + q] = ((unsigned long long)B.nx.k[o + q] << 32) | (o + q);
+                for (uint32_t q = 0; q < n; q++) sk[p + q] = ((unsigned long long)B.nx.k[o + q] << 32) | (o + q);
             }
         }
         uint32_t np2 = 1;
         while (np2 < tot) np2 <<= 1;
         __syncthreads();
-        for (uint32_t i = tot + threadIdx.x; i < np2; i += kBktBS) skp[i] = ~0ull;
+        for (uint32_t i = tot + threadIdx.x; i < np2; i += kBktBS) sk[i] = ~0ull;
         __syncthreads();
         // bitonic sort by key (keys are unique, so the packed words order by
-        // key); one thread per compare-exchange pair
+        // key); one thread per compare-exchange pair (the workgroup barrier
+        // orders the global scratch's accesses too: one workgroup owns it)
         for (uint32_t kk = 2; kk <= np2; kk <<= 1)
             for (uint32_t jj = kk >> 1; jj > 0; jj >>= 1) {
                 for (uint32_t p = threadIdx.x; p < np2 / 2; p += kBktBS) {
                     const uint32_t i = ((p & ~(jj - 1)) << 1) | (p & (jj - 1)), ix = i | jj;
                     const bool up = (i & kk) == 0;
-                    const unsigned long long a = skp[i], c = skp[ix];
-                    if ((a > c) == up) { skp[i] = c; skp[ix] = a; }
+                    const unsigned long long a = sk[i], c = sk[ix];
+                    if ((a > c) == up) { sk[i] = c; sk[ix] = a; }
                 }
                 __syncthreads();
             }
         for (uint32_t i = threadIdx.x; i < tot; i += kBktBS) {
-            const uint32_t o = (uint32_t)skp[i];
+            const uint32_t o = (uint32_t)sk[i];
             const float4 v = B.nx.p[o];
             reinterpret_cast<float4*>(B.kept)[s_off + i] = v;
         }
@@ -4432,8 +4441,8 @@ int Engine::build() {
     prof_ = StageProfile();
     const auto t0 = std::chrono::steady_clock::now();
     if (cfg_.sub_grid_dimension == 0) return fail(-22, "sub_grid_dimension must be > 0");
-    if (cfg_.cell_point_overflow_limit > (uint32_t)kKeptMax)
-        return fail(-22, "cell_point_overflow_limit > 8192 is not supported by the GPU build");
+    if (cfg_.cell_point_overflow_limit > (1u << 24))
+        return fail(-22, "cell_point_overflow_limit > 2^24 is not supported by the GPU build");
     const SlabGeom g = slab_geom(cfg_.sub_grid_dimension);
     if (g.tx * g.ty > kDenseTab)
         return fail(-22, "sub_grid_dimension too large for the LDS slot table (max 96)");
@@ -5456,8 +5465,12 @@ int Engine::level0_bin() {
         L0UnitW* duw = static_cast<L0UnitW*>(dev_->get((uint64_t)umax * sizeof(L0UnitW)));
         uint2* dwt = static_cast<uint2*>(dev_->get((uint64_t)wmax * sizeof(uint2)));
         uint32_t* dcnt = static_cast<uint32_t*>(dev_->get(16));
+        uint32_t* dwn = static_cast<uint32_t*>(dev_->get((uint64_t)umax * 4));
         HIP_CHECK(hipMemsetAsync(L->dcap, 0, (uint64_t)L->nslabs * kDests * 4, stream_));
-        k_l0_uplan<<<1, 1024, 0, stream_>>>(starts, ngroups, tpg, ntiles, (uint32_t)target, umax, duw, dcnt);
+        k_l0_uplan<<<(umax + 255) / 256, 256, 0, stream_>>>(starts, ngroups, tpg, ntiles, (uint32_t)target, umax, duw,
+                                                            dwn, dcnt);
+        scan_excl_u32(dwn, dwn, umax, dcnt + 1, dev_->scan, stream_);
+        k_l0_uplan_w0<<<(umax + 255) / 256, 256, 0, stream_>>>(duw, dwn, umax);
         k_l0_wplan<<<grid_for(wmax, 256, 1u << 30), 256, 0, stream_>>>(duw, 0, 0, cnt6, ntiles, dwt, dcnt);
         if (l0keys)
             k_l0_down5g<32, true, false><<<umax, kL0BS, 0, stream_>>>(src, dst, P, nullptr, starts, ngroups, gcnt,
@@ -5649,6 +5662,7 @@ int Engine::run_level(uint32_t li) {
     L->alloc(L->grid, L->arrivals);
     L->kept_cap = std::min<uint64_t>(L->arrivals, 8ull * L->ncells * cfg_.cell_point_overflow_limit);
     L->alloc(L->kept, L->kept_cap);
+    if (cfg_.cell_point_overflow_limit > (uint32_t)kKeptMax) L->alloc(L->ksort, 2 * std::max<uint64_t>(L->kept_cap, 1));
     uint32_t* scratch = static_cast<uint32_t*>(dev_->get(16));
     // output regions from exclusive scans (no allocation atomics in the slab kernels).
     // Merge: each child slab's region starts with room for its injected seeds.
@@ -5825,6 +5839,7 @@ int Engine::run_level(uint32_t li) {
     BP.nprior = (prior_ && h < pdev_.size()) ? pdev_[h].ncells : 0u;
     BP.kept = L->kept;
     BP.kept_cap = L->kept_cap;
+    BP.ksort = L->ksort;
     BP.cell_slab0 = L->cell_slab0;
     BP.dest_off = L->dest_off;
     BP.dest_n = L->dest_n;

@@ -84,6 +84,18 @@ def test_max_overflow_limit_kept_lists(n):
            cfg=dict(cell_point_overflow_limit=8192, sub_grid_dimension=4, max_cell_size=8.0))
 
 
+@pytest.mark.parametrize("limit,n", [(20_000, 150_000), (12_000, 95_000)])
+def test_overflow_limit_above_lds_sort(limit, n):
+    """cell_point_overflow_limit above the k_bucket LDS sort capacity (8 192):
+    kept lists of 8 192 < n <= limit points are sorted by key in a global-memory
+    scratch (cell.rs:108-153), the others in LDS; some buckets spill around the
+    threshold."""
+    pts = synth(22, 0, n, lo=0.0, ext=7.999)
+    k = n // 2
+    st = _check([pts[:k], pts[k:]], cfg=dict(cell_point_overflow_limit=limit, sub_grid_dimension=4, max_cell_size=8.0))
+    assert st["kept_points"] > 8192
+
+
 def test_gui_batch_size_50k():
     """The GUI path's default batch size (src/plugins/converter.rs:198-201,604: 50 000 per
     batch) over ragged files: batch boundaries move the event batches."""
