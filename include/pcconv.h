@@ -263,6 +263,19 @@ int pcc_shard_route_slabs(const pcc_point* dev_pts, uint64_t n, uint32_t key0, c
                           uint32_t sub_grid_dimension, const uint32_t* dev_owner, uint32_t nranks, pcc_point* dev_send,
                           uint32_t* dev_keys, uint64_t* counts, int device);
 
+/* The local bounding box and the histogram (sub_grid_dimension > 0: per slab,
+ * as pcc_shard_slab_histogram; 0: per cell) in ONE pass over the points, the
+ * histogram taken over a grid guessed before the global box is known (e.g. from
+ * pcc_shard_bbox_sample all-reduced, one cell of margin); *outside = local
+ * points outside that grid (any on any rank: histogram again on the true grid).
+ * Replaces pcc_shard_bbox + pcc_shard_(slab_)histogram on the sharded step's
+ * critical path (converter.rs:96-104 box, converter.rs:32-47 grouping). */
+int pcc_shard_bbox_histogram(const pcc_point* dev_pts, uint64_t n, const pcc_shard_grid* guess,
+                             uint32_t sub_grid_dimension, uint32_t* dev_hist, float bmin[3], float bmax[3],
+                             uint64_t* outside, int device);
+/* Bounding box of a sample of the points (512 tiles of 3 072): the guess. */
+int pcc_shard_bbox_sample(const pcc_point* dev_pts, uint64_t n, float bmin[3], float bmax[3], int device);
+
 /* Exchange-lean form of pcc_shard_route / pcc_shard_route_slabs
  * (sub_grid_dimension 0: cell units, else slab units): no key per routed point;
  * instead dev_bitmaps[r * ceil(n/64) + w] bit b is set iff local point 64 w + b

@@ -660,6 +660,27 @@ int pcc_shard_slab_histogram(const pcc_point* d, uint64_t n, const pcc_shard_gri
     GUARD_END
 }
 
+int pcc_shard_bbox_histogram(const pcc_point* d, uint64_t n, const pcc_shard_grid* g, uint32_t sub_grid_dimension,
+                             uint32_t* dhist, float bmin[3], float bmax[3], uint64_t* outside, int device) {
+    if ((!d && n) || !g || !dhist || !bmin || !bmax || !outside) return set_err(-EINVAL, "null argument");
+    if (sub_grid_dimension && 2 * sub_grid_dimension + 2 > PCC_SHARD_LAYERS)
+        return set_err(-EINVAL, "sub_grid_dimension out of range for slab sharding");
+    GUARD_BEGIN
+    const int rc = shard_bbox_histogram(reinterpret_cast<const Point*>(d), n, to_grid(g), sub_grid_dimension, dhist,
+                                        bmin, bmax, outside, device);
+    return rc ? set_err(rc, rc == -EINVAL ? "input contains NaN or infinite coordinates (unsupported)"
+                                          : "histogram grid too large") : 0;
+    GUARD_END
+}
+
+int pcc_shard_bbox_sample(const pcc_point* d, uint64_t n, float bmin[3], float bmax[3], int device) {
+    if ((!d && n) || !bmin || !bmax) return set_err(-EINVAL, "null argument");
+    GUARD_BEGIN
+    const int rc = shard_bbox_sample(reinterpret_cast<const Point*>(d), n, bmin, bmax, device);
+    return rc ? set_err(rc, "sample holds NaN or infinite coordinates") : 0;
+    GUARD_END
+}
+
 int pcc_shard_route_slabs(const pcc_point* d, uint64_t n, uint32_t key0, const pcc_shard_grid* g,
                           uint32_t sub_grid_dimension, const uint32_t* downer, uint32_t nranks, pcc_point* dsend,
                           uint32_t* dkeys, uint64_t* counts, int device) {

@@ -378,6 +378,10 @@ int shard_synth(Point* dst, uint64_t idx0, uint64_t n, uint64_t seed, int kind, 
 int shard_bbox(const Point* d, uint64_t n, float bmin[3], float bmax[3], int device);
 // dim > 0: slab mode, unit = cell * 256 + level-0 hex z-layer of a dim sub-grid
 int shard_histogram(const Point* d, uint64_t n, const ShardGrid& g, uint32_t* dhist, int device, uint32_t dim = 0);
+// one pass: local bbox + histogram over a guessed grid (points outside it counted)
+int shard_bbox_histogram(const Point* d, uint64_t n, const ShardGrid& g, uint32_t dim, uint32_t* dhist, float bmin[3],
+                         float bmax[3], uint64_t* outside, int device);
+int shard_bbox_sample(const Point* d, uint64_t n, float bmin[3], float bmax[3], int device);
 // dkeys (global key per routed point) or dbm (nranks x ceil(n/64) membership words), either may be null
 int shard_route(const Point* d, uint64_t n, uint32_t key0, const ShardGrid& g, const uint32_t* downer, uint32_t nranks,
                 Point* dsend, uint32_t* dkeys, uint64_t* counts, int device, uint32_t dim = 0, uint64_t* dbm = nullptr);

@@ -6237,12 +6237,18 @@ __device__ __forceinline__ uint32_t shard_unit(const ShardGrid& g, const ShardSl
 }
 
 constexpr int kShBS = 256;
-// per-block LDS histogram (ncells <= kShLds), else global atomics
+// per-block LDS histogram (ncells <= kShLds), else global atomics.  BBOX: the
+// same pass also takes the block's bounding box (part, as k_bbox) and flags
+// non-finite coordinates (nf); points outside the grid are counted in bad.
 constexpr uint32_t kShLds = 16384;
+template <bool BBOX>
 __global__ __launch_bounds__(kShBS) void k_shard_hist(const Point* __restrict__ in, uint64_t n, ShardGrid g,
-                                                      ShardSlabs m, uint32_t ncells, uint32_t* hist, uint32_t* bad) {
+                                                      ShardSlabs m, uint32_t ncells, uint32_t* hist, uint32_t* bad,
+                                                      float* part, uint32_t* nf) {
     extern __shared__ uint32_t h[];   // ncells words when ncells <= kShLds (dynamic: small grids keep occupancy)
     const bool lds = ncells <= kShLds;
+    float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+    bool nfin = false;
     if (lds)
         for (uint32_t i = threadIdx.x; i < ncells; i += kShBS) h[i] = 0;
     __syncthreads();
@@ -6260,12 +6266,35 @@ __global__ __launch_bounds__(kShBS) void k_shard_hist(const Point* __restrict__ 
 #pragma unroll
         for (int u = 0; u < U; u++) {
             if (i0 + u * stride >= n) break;
+            if constexpr (BBOX) {
+                nfin |= !(isfinite(v[u].x) && isfinite(v[u].y) && isfinite(v[u].z));
+                mn[0] = fminf(mn[0], v[u].x); mn[1] = fminf(mn[1], v[u].y); mn[2] = fminf(mn[2], v[u].z);
+                mx[0] = fmaxf(mx[0], v[u].x); mx[1] = fmaxf(mx[1], v[u].y); mx[2] = fmaxf(mx[2], v[u].z);
+            }
             const uint32_t c = shard_unit(g, m, v[u].x, v[u].y, v[u].z);
             if (c == 0xFFFFFFFFu) { nbad++; continue; }
             if (lds) atomicAdd(&h[c], 1u); else wave_aggregated_add(hist, c);
         }
     }
     if (nbad) atomicAdd(bad, nbad);
+    if constexpr (BBOX) {
+        for (int d = 32; d > 0; d >>= 1)
+            for (int a = 0; a < 3; a++) {
+                mn[a] = fminf(mn[a], __shfl_xor(mn[a], d, 64));
+                mx[a] = fmaxf(mx[a], __shfl_xor(mx[a], d, 64));
+            }
+        __shared__ float sbb[kShBS / 64][6];
+        if (nfin) atomicOr(nf, 1u);
+        if ((threadIdx.x & 63) == 0)
+            for (int a = 0; a < 3; a++) { sbb[threadIdx.x / 64][a] = mn[a]; sbb[threadIdx.x / 64][3 + a] = mx[a]; }
+        __syncthreads();
+        if (threadIdx.x < 6) {
+            float r = sbb[0][threadIdx.x];
+            for (int q = 1; q < kShBS / 64; q++)
+                r = threadIdx.x < 3 ? fminf(r, sbb[q][threadIdx.x]) : fmaxf(r, sbb[q][threadIdx.x]);
+            part[blockIdx.x * 6 + threadIdx.x] = r;
+        }
+    }
     __syncthreads();
     if (lds)
         for (uint32_t i = threadIdx.x; i < ncells; i += kShBS)
@@ -6892,12 +6921,68 @@ int shard_histogram(const Point* d, uint64_t n, const ShardGrid& g, uint32_t* dh
     HIP_CHECK(hipMemsetAsync(dhist, 0, nc * 4, S.st));
     HIP_CHECK(hipMemsetAsync(S.flag, 0, 4, S.st));
     const size_t smem = nc <= kShLds ? (size_t)nc * 4 : 0;
-    if (n) k_shard_hist<<<grid_for(n, kShBS, 2048), kShBS, smem, S.st>>>(d, n, g, shard_slabs(g, dim), (uint32_t)nc, dhist, S.flag);
+    if (n) k_shard_hist<false><<<grid_for(n, kShBS, 2048), kShBS, smem, S.st>>>(d, n, g, shard_slabs(g, dim), (uint32_t)nc,
+                                                                                dhist, S.flag, nullptr, nullptr);
     HIP_CHECK(hipGetLastError());
     uint32_t bad = 0;
     HIP_CHECK(hipMemcpyAsync(&bad, S.flag, 4, hipMemcpyDeviceToHost, S.st));
     HIP_CHECK(hipStreamSynchronize(S.st));
     return bad ? -ERANGE : 0;
+}
+
+// The local bounding box and the slab (dim > 0) or cell histogram over a grid
+// guessed before the box is known, in one pass: points outside the guess are
+// counted in *outside (the caller falls back to shard_histogram on the true
+// grid when any rank has some).  -EINVAL: non-finite coordinates.
+int shard_bbox_histogram(const Point* d, uint64_t n, const ShardGrid& g, uint32_t dim, uint32_t* dhist, float bmin[3],
+                         float bmax[3], uint64_t* outside, int device) {
+    ShardScratch& S = shard_scratch(device);
+    for (int a = 0; a < 3; a++) { bmin[a] = INFINITY; bmax[a] = -INFINITY; }
+    *outside = 0;
+    const uint64_t nc = (uint64_t)g.dims[0] * g.dims[1] * g.dims[2] * (dim ? kL0Layers : 1u);
+    if (nc >= (1ull << 32)) return -EOVERFLOW;
+    HIP_CHECK(hipMemsetAsync(dhist, 0, nc * 4, S.st));
+    if (!n) { HIP_CHECK(hipStreamSynchronize(S.st)); return 0; }
+    HIP_CHECK(hipMemsetAsync(S.flag, 0, 4, S.st));
+    HIP_CHECK(hipMemsetAsync(S.cnt, 0, 4, S.st));
+    const size_t smem = nc <= kShLds ? (size_t)nc * 4 : 0;
+    const uint32_t nb = grid_for(n, kShBS, std::min<uint32_t>(2048, kBBoxBlocks));
+    k_shard_hist<true><<<nb, kShBS, smem, S.st>>>(d, n, g, shard_slabs(g, dim), (uint32_t)nc, dhist, S.cnt, S.part,
+                                                  S.flag);
+    k_bbox_final<<<1, 256, 0, S.st>>>(S.part, nb);
+    HIP_CHECK(hipGetLastError());
+    float bb[6];
+    uint32_t nf = 0, out = 0;
+    HIP_CHECK(hipMemcpyAsync(bb, S.part, sizeof bb, hipMemcpyDeviceToHost, S.st));
+    HIP_CHECK(hipMemcpyAsync(&nf, S.flag, 4, hipMemcpyDeviceToHost, S.st));
+    HIP_CHECK(hipMemcpyAsync(&out, S.cnt, 4, hipMemcpyDeviceToHost, S.st));
+    HIP_CHECK(hipStreamSynchronize(S.st));
+    if (nf) return -EINVAL;
+    for (int a = 0; a < 3; a++) { bmin[a] = bb[a]; bmax[a] = bb[3 + a]; }
+    *outside = out;
+    return 0;
+}
+
+// Bounding box of a sample of the points (one tile of kL0Tile in every
+// ntiles / 512): the guess the fused pass above is made over.
+int shard_bbox_sample(const Point* d, uint64_t n, float bmin[3], float bmax[3], int device) {
+    ShardScratch& S = shard_scratch(device);
+    for (int a = 0; a < 3; a++) { bmin[a] = INFINITY; bmax[a] = -INFINITY; }
+    if (!n) return 0;
+    const uint64_t ntiles = (n + kL0Tile - 1) / kL0Tile;
+    const uint32_t nb = (uint32_t)std::min<uint64_t>(ntiles, 512);
+    k_bbox_sample<<<nb, 256, 0, S.st>>>(d, n, ntiles, nb, S.part);
+    k_bbox_final<<<1, 256, 0, S.st>>>(S.part, nb);
+    HIP_CHECK(hipGetLastError());
+    float bb[6];
+    HIP_CHECK(hipMemcpyAsync(bb, S.part, sizeof bb, hipMemcpyDeviceToHost, S.st));
+    HIP_CHECK(hipStreamSynchronize(S.st));
+    for (int a = 0; a < 3; a++) {
+        if (!(std::isfinite(bb[a]) && std::isfinite(bb[3 + a]))) return -EINVAL;
+        bmin[a] = bb[a];
+        bmax[a] = bb[3 + a];
+    }
+    return 0;
 }
 
 int shard_route(const Point* d, uint64_t n, uint32_t key0, const ShardGrid& g, const uint32_t* downer, uint32_t nranks,

@@ -34,7 +34,7 @@ EXPORTS = ["pcc_abi_version", "pcc_last_error", "pcc_options_default", "pcc_open
            "pcc_convert_files", "pcc_shard_grid_from_bbox", "pcc_synth_device", "pcc_shard_bbox",
            "pcc_shard_histogram", "pcc_shard_route", "pcc_declare_files", "pcc_add_keyed_points_device",
            "pcc_set_keyed_points_device", "pcc_set_level_range", "pcc_set_root_spill_batches",
-           "pcc_pending_cells", "pcc_export_pending", "pcc_shard_slab_histogram", "pcc_shard_route_slabs",
+           "pcc_pending_cells", "pcc_export_pending", "pcc_shard_slab_histogram", "pcc_shard_route_slabs", "pcc_shard_bbox_histogram", "pcc_shard_bbox_sample",
            "pcc_write_cell_view", "pcc_begin_file", "pcc_append_points", "pcc_end_file", "pcc_cancel_file",
            "pcc_set_summary", "pcc_write_cells", "pcc_write_metadata", "pcc_clear_input", "pcc_adopt_prior",
            "pcc_open_subtrees", "pcc_visit_cells", "pcc_shard_route_bitmaps", "pcc_shard_route_bitmaps_hist",
@@ -154,6 +154,9 @@ def lib():
         L.pcc_set_keyed_points_device.argtypes = [vp, vp, vp, C.c_uint64]
         L.pcc_set_level_range.argtypes = [vp, C.c_uint32, C.c_uint32, C.c_int]
         L.pcc_shard_slab_histogram.argtypes = [vp, C.c_uint64, C.POINTER(ShardGrid), C.c_uint32, vp, C.c_int]
+        L.pcc_shard_bbox_histogram.argtypes = [vp, C.c_uint64, C.POINTER(ShardGrid), C.c_uint32, vp, f3, f3,
+                                               C.POINTER(C.c_uint64), C.c_int]
+        L.pcc_shard_bbox_sample.argtypes = [vp, C.c_uint64, f3, f3, C.c_int]
         L.pcc_shard_route_slabs.argtypes = [vp, C.c_uint64, C.c_uint32, C.POINTER(ShardGrid), C.c_uint32, vp,
                                             C.c_uint32, vp, vp, C.POINTER(C.c_uint64), C.c_int]
         L.pcc_shard_route_bitmaps.argtypes = [vp, C.c_uint64, C.POINTER(ShardGrid), C.c_uint32, vp, C.c_uint32, vp,
@@ -415,6 +418,21 @@ def shard_slab_histogram(pts_ptr: int, n: int, grid: ShardGrid, sub_grid_dimensi
                          device: int = 0):
     _check(lib().pcc_shard_slab_histogram(C.c_void_p(pts_ptr), n, C.byref(grid), sub_grid_dimension,
                                           C.c_void_p(hist_ptr), device))
+
+
+def shard_bbox_histogram(pts_ptr: int, n: int, grid: ShardGrid, sub_grid_dimension: int, hist_ptr: int,
+                         device: int = 0):
+    """(bmin, bmax, outside): local box + histogram over a guessed grid, one pass."""
+    bmin, bmax, out = (C.c_float * 3)(), (C.c_float * 3)(), C.c_uint64(0)
+    _check(lib().pcc_shard_bbox_histogram(C.c_void_p(pts_ptr), n, C.byref(grid), sub_grid_dimension,
+                                          C.c_void_p(hist_ptr), bmin, bmax, C.byref(out), device))
+    return list(bmin), list(bmax), int(out.value)
+
+
+def shard_bbox_sample(pts_ptr: int, n: int, device: int = 0):
+    bmin, bmax = (C.c_float * 3)(), (C.c_float * 3)()
+    _check(lib().pcc_shard_bbox_sample(C.c_void_p(pts_ptr), n, bmin, bmax, device))
+    return list(bmin), list(bmax)
 
 
 def shard_route_slabs(pts_ptr: int, n: int, key0: int, grid: ShardGrid, sub_grid_dimension: int, owner_ptr: int,

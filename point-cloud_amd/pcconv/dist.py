@@ -636,6 +636,21 @@ class HipShardOps:
     def grid(self, gmin, gmax, level: int = 0):
         return shard_grid(gmin, gmax, self.max_cell_size, level)
 
+    # the bounding box and the slab histogram in one pass over a guessed grid
+    fused_bbox_hist = True
+
+    def bbox_sample(self, pts: torch.Tensor):
+        self._ready()
+        return pcconv.shard_bbox_sample(pts.data_ptr(), pts.shape[0], self.dev)
+
+    def bbox_slab_histogram(self, pts: torch.Tensor, guess):
+        """(bmin, bmax, slab histogram over `guess`, points outside `guess`)."""
+        h = torch.empty(guess.ncells * pcconv.SHARD_LAYERS, dtype=torch.int32, device=pts.device)
+        self._ready()
+        bmin, bmax, out = pcconv.shard_bbox_histogram(pts.data_ptr(), pts.shape[0], guess,
+                                                      int(self.cfg_full()["sub_grid_dimension"]), h.data_ptr(), self.dev)
+        return bmin, bmax, h, out
+
     def begin_step(self):
         self._built = []
         self.assembled = []
@@ -917,6 +932,18 @@ def _combine(parts: list[dict]) -> dict:
     return out
 
 
+def _sub_grid_hist(h, guess, grid, nl: int):
+    """The slab histogram over `guess` restricted to `grid` (a sub-box of it;
+    cell id = ((ix - lo.x) dims.y + iy - lo.y) dims.z + iz - lo.z), or None when
+    `grid` is not inside `guess`."""
+    o = [int(grid.lo[a]) - int(guess.lo[a]) for a in range(3)]
+    d, dg = [int(v) for v in grid.dims], [int(v) for v in guess.dims]
+    if any(o[a] < 0 or o[a] + d[a] > dg[a] for a in range(3)):
+        return None
+    v = h.view(dg[0], dg[1], dg[2], nl)
+    return v[o[0]:o[0] + d[0], o[1]:o[1] + d[1], o[2]:o[2] + d[2]].contiguous().view(-1)
+
+
 def shard_build(comm, ops, pts: torch.Tensor, key0: int, file_points, write: bool = False,
                 sync=None, merge: bool = False, split: bool = True) -> ShardResult:
     """One sharded conversion step.  `pts` is this rank's (n, 4) int32 view of
@@ -964,16 +991,38 @@ def shard_build(comm, ops, pts: torch.Tensor, key0: int, file_points, write: boo
             mark("write")
         return ShardResult(summary=summary, local=local, recv_points=int(pts.shape[0]),
                            owned_cells=int(local.get("level0_cells", -1)), ms=ms)
-    # 2. global bounding box (converter.rs:96-104: componentwise min/max)
-    if pts.shape[0]:
+    # 2. global bounding box (converter.rs:96-104: componentwise min/max).  With
+    # fused ops the same pass over the points also takes the slab histogram, over
+    # a grid guessed from an all-reduced sample box with one cell of margin; if
+    # a point falls outside it on any rank, the histogram is taken again (step 3).
+    from pcconv import SHARD_LAYERS as NL
+    guess, sh_guess, outside = None, None, 0
+    if getattr(ops, "fused_bbox_hist", False) and not merge and n_total:
+        if pts.shape[0]:
+            smin, smax = ops.bbox_sample(pts)
+        else:
+            smin, smax = [float("inf")] * 3, [float("-inf")] * 3
+        sb = torch.tensor([-smin[0], -smin[1], -smin[2], smax[0], smax[1], smax[2]], dtype=torch.float32,
+                          device=comm.device)
+        comm.allreduce_(sb, "max")
+        sbh = sb.cpu().tolist()
+        cs = float(ops.cfg_full()["max_cell_size"])
+        g0 = ops.grid([-sbh[0] - cs, -sbh[1] - cs, -sbh[2] - cs], [sbh[3] + cs, sbh[4] + cs, sbh[5] + cs])
+        if not int(getattr(g0, "coarse", 0)) and int(g0.ncells) * NL <= (1 << 24):
+            guess = g0
+    if guess is not None:
+        bmin, bmax, sh_guess, outside = ops.bbox_slab_histogram(pts, guess)
+    elif pts.shape[0]:
         bmin, bmax = ops.bbox(pts)
     else:
         bmin, bmax = [float("inf")] * 3, [float("-inf")] * 3
-    bb = torch.tensor([-bmin[0], -bmin[1], -bmin[2], bmax[0], bmax[1], bmax[2]], dtype=torch.float32,
-                      device=comm.device)
+    bb = torch.tensor([-bmin[0], -bmin[1], -bmin[2], bmax[0], bmax[1], bmax[2], 1.0 if outside else 0.0],
+                      dtype=torch.float32, device=comm.device)
     comm.allreduce_(bb, "max")
     bbh = bb.cpu().tolist()
-    gmin, gmax = [-bbh[0], -bbh[1], -bbh[2]], bbh[3:]
+    gmin, gmax = [-bbh[0], -bbh[1], -bbh[2]], bbh[3:6]
+    if bbh[6] > 0:   # the guess missed some point on some rank
+        guess, sh_guess = None, None
     mark("bbox")
     plan = None
     if n_total == 0:
@@ -984,8 +1033,10 @@ def shard_build(comm, ops, pts: torch.Tensor, key0: int, file_points, write: boo
             ops.set_subtrees(np.zeros((0, 3), dtype=np.int32))
     else:
         # 3. ownership: level-0 cells; heavy ones shared slab by slab
-        from pcconv import SHARD_LAYERS as NL
         grid = ops.grid(gmin, gmax)
+        # this rank's slab histogram over the true grid from the fused pass
+        sh_local = (_sub_grid_hist(sh_guess, guess, grid, NL)
+                    if sh_guess is not None and not int(getattr(grid, "coarse", 0)) else None)
         coarse = int(getattr(grid, "coarse", 0))
         if merge and coarse:
             raise ValueError("sharded merge: the existing cloud's bounding box spans more than 2^22 level-0 cells")
@@ -993,7 +1044,7 @@ def shard_build(comm, ops, pts: torch.Tensor, key0: int, file_points, write: boo
         if grid1 is not None and (int(grid1.ncells) > (1 << 22) or int(grid.ncells) * NL > (1 << 24)):
             grid1 = None
         if grid1 is not None:
-            sh = ops.slab_histogram(pts, grid)
+            sh = sh_local if sh_local is not None else ops.slab_histogram(pts, grid)
             lhist = {"slab": sh}   # this rank's own counts: the one-pass route's totals
             sh_h = comm.allreduce_(sh.to(comm.device).to(torch.int64), "sum").cpu().numpy()
             mark("hist")
@@ -1009,7 +1060,8 @@ def shard_build(comm, ops, pts: torch.Tensor, key0: int, file_points, write: boo
                 ch[nz] = children_ids(nz, grid, grid1)
                 plan = plan_split(hist_h, hist1_h, ch, W, slab_hist=sh_h)
         else:
-            hist = ops.histogram(pts, grid)
+            hist = (sh_local.view(-1, NL).sum(dim=1, dtype=torch.int32) if sh_local is not None
+                    else ops.histogram(pts, grid))
             lhist = {"cell": hist}
             hist_h = comm.allreduce_(hist.to(comm.device).to(torch.int64), "sum").cpu().numpy()
             mark("hist")

@@ -117,6 +117,39 @@ class NumpyShardOps:
         u = self._slabs(as_points(pts), grid)
         return torch.from_numpy(np.bincount(u, minlength=grid.ncells * pcconv.SHARD_LAYERS).astype(np.int32))
 
+    # the fused bounding box + slab histogram over a guessed grid (HipShardOps)
+    fused_bbox_hist = True
+
+    def bbox_sample(self, pts):
+        p = as_points(pts)[::97]   # any sample: the fused pass checks the guess
+        return ([float(p[a].min()) for a in "xyz"], [float(p[a].max()) for a in "xyz"])
+
+    def bbox_slab_histogram(self, pts, guess):
+        """numpy restatement of pcc_shard_bbox_histogram: points outside the
+        guessed grid are counted, not binned."""
+        p = as_points(pts)
+        nl = pcconv.SHARD_LAYERS
+        h = np.zeros(guess.ncells * nl, dtype=np.int64)
+        if len(p) == 0:
+            return [float("inf")] * 3, [float("-inf")] * 3, torch.from_numpy(h.astype(np.int32)), 0
+        ix = [cell_index(p[a], guess.cell_size) - guess.lo[i] for i, a in enumerate("xyz")]
+        d = [int(v) for v in guess.dims]
+        inside = np.ones(len(p), dtype=bool)
+        for i in range(3):
+            inside &= (ix[i] >= 0) & (ix[i] < d[i])
+        q = p[inside]
+        if len(q):
+            c = (ix[0][inside] * d[1] + ix[1][inside]) * d[2] + ix[2][inside]
+            dim = int(self.cfg_full()["sub_grid_dimension"])
+            cs = np.float32(guess.cell_size)
+            cr = (cs / np.float32(dim)) / np.float32(2.0)
+            z = q["z"].astype(np.float32)
+            iz = cell_index(z, cs)
+            t = np.clip(np.trunc((z / cr).astype(np.float64)), -2147483648.0, 2147483647.0).astype(np.int64)
+            h = np.bincount(c * nl + (t - (2 * dim * iz - 2)), minlength=guess.ncells * nl)
+        return ([float(p[a].min()) for a in "xyz"], [float(p[a].max()) for a in "xyz"],
+                torch.from_numpy(h.astype(np.int32)), int((~inside).sum()))
+
     def route_slabs(self, pts, key0, grid, table, world):
         p = as_points(pts)
         own = table.cpu().numpy().astype(np.int64)[self._slabs(p, grid)]

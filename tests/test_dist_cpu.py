@@ -84,9 +84,14 @@ def test_assign_owners_many_cells_prefix_split():
 # ------------------------------------------------------------- thread ranks
 # bitmap: the exchange carries membership bitmaps (keys rebuilt by the receiver),
 # else a 4-B key per routed point
-@pytest.mark.parametrize("case,world,bitmap", [("uniform", 1, True), ("uniform", 2, True), ("uniform", 2, False),
-                                               ("files", 3, True), ("files", 3, False), ("clustered", 4, True)])
-def test_thread_ranks_match_oracle(tmp_path, case, world, bitmap):
+# mode: "fused" bounding box + slab histogram in one pass over a guessed grid
+# (the default), "miss" a guess that leaves points outside (histogram again on
+# the true grid), "plain" the separate box and histogram passes
+@pytest.mark.parametrize("case,world,bitmap,mode", [("uniform", 1, True, "fused"), ("uniform", 2, True, "fused"),
+                                                    ("uniform", 2, False, "fused"), ("files", 3, True, "fused"),
+                                                    ("files", 3, False, "fused"), ("clustered", 4, True, "fused"),
+                                                    ("clustered", 3, True, "miss"), ("files", 2, True, "plain")])
+def test_thread_ranks_match_oracle(tmp_path, case, world, bitmap, mode):
     import threading
     files = make_input(case)
     fp = [len(f) for f in files]
@@ -99,6 +104,10 @@ def test_thread_ranks_match_oracle(tmp_path, case, world, bitmap):
             pts, key0 = rank_slice(files, r, world)
             ops = NumpyShardOps(out)
             ops.bitmap_keys = bitmap
+            if mode == "plain":
+                ops.fused_bbox_hist = False
+            elif mode == "miss":   # a sample box of one point: the guessed grid misses the rest
+                ops.bbox_sample = lambda p: ([float(v) for v in p[0, :3].view(torch.float32)],) * 2
             res[r] = shard_build(ThreadComm(grp, r, torch.device("cpu")), ops, as_tensor(pts), key0, fp, write=True)
             ops.close()
         except BaseException as e:  # noqa: BLE001
