@@ -296,6 +296,20 @@ private:
     static constexpr uint32_t kPreBlocks = 1024;
     uint16_t* d_tile6_ = nullptr;
     uint64_t tile6_cap_ = 0, pre_tiles_ = 0;
+    // Folded level-0 pass 1 (k_l0_tile6) behind the upload instead of pass 0,
+    // when the first landed piece's sample box spans at most two level-0 cells
+    // per axis: groups of pre6_tpg_ tiles as their copies land, run records with
+    // a row stride of the reserved capacity's tiles (pre6_tcap_), compacted when
+    // the build takes them over (level0_bin).
+    bool pre_decided_ = false, pre6_ = false;
+    uint32_t pre6_tpg_ = 0, pre6_gdone_ = 0, pre6_gcap_ = 0;
+    uint64_t pre6_tcap_ = 0;
+    uint32_t* d_pre6_cnt_ = nullptr;
+    uint32_t* d_pre6_ph_ = nullptr;
+    uint32_t* d_pre6_gpar_ = nullptr;
+    uint64_t pre6_alloc_tiles_ = 0, pre6_alloc_groups_ = 0;
+    const void* pre6_ar1_ = nullptr;
+    bool pre6_run(uint64_t upto, hipEvent_t after, bool all);
     float* d_prepart_ = nullptr;
     uint32_t* d_preflag_ = nullptr;
     hipEvent_t pre_ev_ = nullptr;

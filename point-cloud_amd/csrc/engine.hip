@@ -1492,7 +1492,7 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_tile6(const Point* __restrict__
                                                        uint32_t ngroups, uint32_t* __restrict__ cnt6,
                                                        uint32_t* __restrict__ ph6, uint32_t* __restrict__ gcnt,
                                                        float* __restrict__ part, uint32_t* __restrict__ flag,
-                                                       Arena dummy) {
+                                                       Arena dummy, uint32_t g0, uint32_t cstride) {
     constexpr int R = 64, R5 = 32, HP = R5 + 1;
     using KT = typename std::conditional<KEYS, uint32_t, uint16_t>::type;
     __shared__ float4 sp[kL0Tile];
@@ -1502,7 +1502,9 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_tile6(const Point* __restrict__
     __shared__ uint32_t dbase[R];
     __shared__ uint32_t h[R * HP];
     __shared__ float sb[kL0W][6];
-    const uint32_t tid = threadIdx.x, w = tid / 64, lane = tid & 63, g = blockIdx.x;
+    // g0: the first group of this launch (uploads, Engine::pre0_count); the run
+    // records' rows are cstride tiles apart and the pair-count rows ngroups groups
+    const uint32_t tid = threadIdx.x, w = tid / 64, lane = tid & 63, g = g0 + blockIdx.x;
     const float4* p4 = reinterpret_cast<const float4*>(in);
     for (int i = tid; i < R * HP; i += kL0BS) h[i] = 0;
     for (int i = tid; i < kL0RW * R / 4; i += kL0BS) reinterpret_cast<uint32_t*>(&wcnt[0][0])[i] = 0;
@@ -1511,7 +1513,7 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_tile6(const Point* __restrict__
     uint32_t nf = 0;
     const uint32_t t0 = g * tpg, t1 = min(t0 + tpg, ntiles);
     // per-tile run records through buffer descriptors (scalar bases, 32-bit offsets)
-    const __amdgpu_buffer_rsrc_t rC = srd(cnt6, 256ull * ntiles), rH = srd(ph6, 256ull * ntiles);
+    const __amdgpu_buffer_rsrc_t rC = srd(cnt6, 256ull * cstride), rH = srd(ph6, 256ull * cstride);
     auto load_tile = [&](float4* v, uint32_t* kk, uint32_t tile) {   // unconditional, clamped (see k_l0_down6g)
         const uint64_t base = (uint64_t)tile * kL0Tile;
         asm volatile("" ::: "memory");
@@ -1571,7 +1573,7 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_tile6(const Point* __restrict__
             uint32_t ln = lane;   // (recomputed addresses: see k_l0_down5g)
             asm volatile("" : "+v"(ln));
             dbase[ln] = ex;
-            const uint32_t ro = (ln * ntiles + tile) * 4;   // this tile's run of digit `lane`: length, start
+            const uint32_t ro = (ln * cstride + tile) * 4;   // this tile's run of digit `lane`: length, start
             bst(rC, ro, tot);
             bst(rH, ro, tile * (uint32_t)kL0Tile + ex);
         }
@@ -4248,8 +4250,10 @@ void Engine::add_file_host(const Point* pts, uint64_t n, uint32_t batch) {
     // in each copy of pageable memory while the device counts the last piece)
     if (!copy_) HIP_CHECK(hipStreamCreateWithFlags(&copy_, hipStreamNonBlocking));
     if (!pre_ev_) HIP_CHECK(hipEventCreateWithFlags(&pre_ev_, hipEventDisableTiming));
-    for (uint64_t off = 0; off < n; off += kPrePiece) {
-        const uint64_t m = std::min<uint64_t>(kPrePiece, n - off);
+    const char* pp = getenv("PCC_PRE_PIECE");   // (tests: smaller pieces)
+    const uint64_t piece = pp ? std::max<uint64_t>(1, strtoull(pp, nullptr, 10)) : kPrePiece;
+    for (uint64_t off = 0; off < n; off += piece) {
+        const uint64_t m = std::min<uint64_t>(piece, n - off);
         HIP_CHECK(hipMemcpyAsync(d_in_ + n_ + off, pts + off, m * sizeof(Point), hipMemcpyHostToDevice, copy_));
         HIP_CHECK(hipEventRecord(pre_ev_, copy_));
         pre0_count(n_ + off + m, pre_ev_, false);
@@ -4602,12 +4606,40 @@ static L0Params l0_base_params(const Config& cfg, uint32_t h0) {
     return P;
 }
 
+// Bounding box of one tile out of every ntiles / nb (block b: tile b * ntiles / nb).
+__global__ __launch_bounds__(256) void k_bbox_sample(const Point* __restrict__ in, uint64_t n, uint64_t ntiles,
+                                                     uint32_t nb, float* part) {
+    const uint64_t t = (uint64_t)blockIdx.x * ntiles / nb;
+    const float4* p4 = reinterpret_cast<const float4*>(in);
+    float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (uint64_t i = t * kL0Tile + threadIdx.x; i < min((t + 1) * kL0Tile, n); i += 256) {
+        const float4 v = p4[i];
+        mn[0] = fminf(mn[0], v.x); mn[1] = fminf(mn[1], v.y); mn[2] = fminf(mn[2], v.z);
+        mx[0] = fmaxf(mx[0], v.x); mx[1] = fmaxf(mx[1], v.y); mx[2] = fmaxf(mx[2], v.z);
+    }
+    __shared__ float s[4][6];
+    for (int d = 32; d > 0; d >>= 1)
+        for (int a = 0; a < 3; a++) {
+            mn[a] = fminf(mn[a], __shfl_xor(mn[a], d, 64));
+            mx[a] = fmaxf(mx[a], __shfl_xor(mx[a], d, 64));
+        }
+    if ((threadIdx.x & 63) == 0)
+        for (int a = 0; a < 3; a++) { s[threadIdx.x / 64][a] = mn[a]; s[threadIdx.x / 64][3 + a] = mx[a]; }
+    __syncthreads();
+    if (threadIdx.x < 6) {
+        float r = s[0][threadIdx.x];
+        for (int q = 1; q < 4; q++) r = threadIdx.x < 3 ? fminf(r, s[q][threadIdx.x]) : fmaxf(r, s[q][threadIdx.x]);
+        part[blockIdx.x * 6 + threadIdx.x] = r;
+    }
+}
+
 // Level-0 pass 0 of the input uploaded so far (the complete tiles of its first
 // `upto` points, or every tile when `all`), on the engine stream after `after`
 // (the copy that brought them).  Only for a build whose source is the plain
 // input (no merge seeds in front, no keyed input).
 void Engine::pre0_count(uint64_t upto, hipEvent_t after, bool all) {
     if (prior_ || keyed_ || ext_in_ || h0_ != 0) return;
+    if (pre6_run(upto, after, all)) return;
     const uint64_t t1 = all ? (upto + kL0Tile - 1) / kL0Tile : upto / kL0Tile;
     if (t1 <= pre_tiles_) return;
     if (!d_prepart_) {
@@ -4638,33 +4670,81 @@ void Engine::pre0_count(uint64_t upto, hipEvent_t after, bool all) {
     pre_tiles_ = t1;
 }
 
-void Engine::pre0_reset() { pre_tiles_ = 0; }
+void Engine::pre0_reset() {
+    pre_tiles_ = 0;
+    pre_decided_ = false;
+    pre6_ = false;
+    pre6_gdone_ = 0;
+}
 
-// Bounding box of one tile out of every ntiles / nb (block b: tile b * ntiles / nb).
-__global__ __launch_bounds__(256) void k_bbox_sample(const Point* __restrict__ in, uint64_t n, uint64_t ntiles,
-                                                     uint32_t nb, float* part) {
-    const uint64_t t = (uint64_t)blockIdx.x * ntiles / nb;
-    const float4* p4 = reinterpret_cast<const float4*>(in);
-    float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
-    for (uint64_t i = t * kL0Tile + threadIdx.x; i < min((t + 1) * kL0Tile, n); i += 256) {
-        const float4 v = p4[i];
-        mn[0] = fminf(mn[0], v.x); mn[1] = fminf(mn[1], v.y); mn[2] = fminf(mn[2], v.z);
-        mx[0] = fmaxf(mx[0], v.x); mx[1] = fmaxf(mx[1], v.y); mx[2] = fmaxf(mx[2], v.z);
-    }
-    __shared__ float s[4][6];
-    for (int d = 32; d > 0; d >>= 1)
+// pre0_count in its folded form: decides on the first landed piece (sample box
+// of at most two level-0 cells per axis), then runs k_l0_tile6 over every group
+// of tiles whose copy has landed.  Returns false when pass 0 runs instead.
+bool Engine::pre6_run(uint64_t upto, hipEvent_t after, bool all) {
+    if (!pre_decided_ && pre_tiles_ == 0) {
+        const uint64_t landed = upto / kL0Tile;
+        if (landed == 0 && !all) return true;   // decide once a tile has landed
+        pre_decided_ = true;
+        pre6_ = false;
+        if (!getenv("PCC_PRE6") || getenv("PCC_NO_PRE6") || getenv("PCC_NO_FOLD") || landed == 0) return false;
+        if (after) HIP_CHECK(hipStreamWaitEvent(stream_, after, 0));
+        const uint32_t nb = (uint32_t)std::min<uint64_t>(landed, 512);
+        k_bbox_sample<<<nb, 256, 0, stream_>>>(d_in_, landed * kL0Tile, landed, nb, dev_->bbox_part);
+        k_bbox_final<<<1, 256, 0, stream_>>>(dev_->bbox_part, nb);
+        HIP_CHECK(hipGetLastError());
+        float bb[6];
+        HIP_CHECK(hipMemcpyAsync(bb, dev_->bbox_part, sizeof bb, hipMemcpyDeviceToHost, stream_));
+        HIP_CHECK(hipStreamSynchronize(stream_));
+        const float cs = cell_size(cfg_.max_cell_size, 0);
         for (int a = 0; a < 3; a++) {
-            mn[a] = fminf(mn[a], __shfl_xor(mn[a], d, 64));
-            mx[a] = fmaxf(mx[a], __shfl_xor(mx[a], d, 64));
+            if (!(std::isfinite(bb[a]) && std::isfinite(bb[3 + a]))) return false;
+            if ((int64_t)cell_index1(bb[3 + a], cs) - (int64_t)cell_index1(bb[a], cs) >= 2) return false;
         }
-    if ((threadIdx.x & 63) == 0)
-        for (int a = 0; a < 3; a++) { s[threadIdx.x / 64][a] = mn[a]; s[threadIdx.x / 64][3 + a] = mx[a]; }
-    __syncthreads();
-    if (threadIdx.x < 6) {
-        float r = s[0][threadIdx.x];
-        for (int q = 1; q < 4; q++) r = threadIdx.x < 3 ? fminf(r, s[q][threadIdx.x]) : fmaxf(r, s[q][threadIdx.x]);
-        part[blockIdx.x * 6 + threadIdx.x] = r;
+        // room for the reserved input: run records, pair counts, the arenas
+        pre6_tcap_ = (cap_ + kL0Tile - 1) / kL0Tile;
+        pre6_tpg_ = (uint32_t)std::max<uint64_t>(1, (pre6_tcap_ + kL0Groups - 1) / kL0Groups);
+        pre6_gcap_ = (uint32_t)((pre6_tcap_ + pre6_tpg_ - 1) / pre6_tpg_);
+        if (pre6_alloc_tiles_ < pre6_tcap_) {
+            dev_release(d_pre6_cnt_); dev_release(d_pre6_ph_);
+            dev_alloc_t(d_pre6_cnt_, 64 * pre6_tcap_ * 4);
+            dev_alloc_t(d_pre6_ph_, 64 * pre6_tcap_ * 4);
+            pre6_alloc_tiles_ = pre6_tcap_;
+        }
+        if (pre6_alloc_groups_ < pre6_gcap_) {
+            dev_release(d_pre6_gpar_);
+            dev_alloc_t(d_pre6_gpar_, 64ull * pre6_gcap_ * 32 * 4);
+            pre6_alloc_groups_ = pre6_gcap_;
+        }
+        if (dev_->cap < cap_) {
+            for (int a = 0; a < 2; a++) {
+                Arena& A = dev_->ar[a];
+                dev_release(A.p); dev_release(A.k);
+                dev_alloc_t(A.p, cap_ * 16); dev_alloc_t(A.k, cap_ * 4);
+            }
+            dev_->cap = cap_;
+        }
+        pre6_ar1_ = dev_->ar[1].p;
+        HIP_CHECK(hipMemsetAsync(dev_->bbox_flag, 0, 4, stream_));
+        pre6_gdone_ = 0;
+        pre6_ = true;
     }
+    if (!pre6_) return false;
+    const uint64_t tl = all ? (upto + kL0Tile - 1) / kL0Tile : upto / kL0Tile;
+    if (tl > pre6_tcap_) { pre6_ = false; return true; }   // beyond the reserved input: the build runs pass 1
+    const uint32_t gend = (uint32_t)(all ? (tl + pre6_tpg_ - 1) / pre6_tpg_ : tl / pre6_tpg_);
+    if (gend <= pre6_gdone_) return true;
+    if (after) HIP_CHECK(hipStreamWaitEvent(stream_, after, 0));
+    const uint32_t ntl = all ? (uint32_t)tl : gend * pre6_tpg_;
+    const uint64_t n = all ? upto : (uint64_t)ntl * kL0Tile;
+    Arena dummy{static_cast<float4*>(dev_->get(256ull * kL0BS * kL0IPT * 16)),
+                static_cast<uint32_t*>(dev_->get(256ull * kL0BS * kL0IPT * 4))};
+    k_l0_tile6<false><<<gend - pre6_gdone_, kL0BS, 0, stream_>>>(d_in_, nullptr, dev_->ar[1], n, l0_base_params(cfg_, 0),
+                                                                ntl, pre6_tpg_, pre6_gcap_, d_pre6_cnt_, d_pre6_ph_,
+                                                                d_pre6_gpar_, dev_->bbox_part, dev_->bbox_flag, dummy,
+                                                                pre6_gdone_, (uint32_t)pre6_tcap_);
+    HIP_CHECK(hipGetLastError());
+    pre6_gdone_ = gend;
+    return true;
 }
 
 // ---- inputs with non-finite coordinates (kNfNan / kNfInf, see nf_class)
@@ -5176,10 +5256,14 @@ int Engine::level0_bin() {
     // box, per group of consecutive tiles: k_l0_down6g's blocks walk the same
     // groups with running offsets, so no per-tile counts exist.
     const uint32_t ntiles = (uint32_t)((nsrc_ + kL0Tile - 1) / kL0Tile);
+    // pass 1 already run behind the upload (pre6_run) for this very input
+    const bool p6 = pre6_ && ntiles && src_ == d_in_ && nsrc_ == n_ && !prior_ && !keyed_ && !ext_in_ && h0_ == 0 &&
+                    !nf_mode_ && dev_->ar[1].p == pre6_ar1_ && ntiles <= pre6_tcap_ && getenv("PCC_NO_FOLD") == nullptr;
+    pre6_ = false;   // (consumed: later levels overwrite the arena)
     const char* gq = getenv("PCC_L0_GROUPS");
     uint32_t ngroups = std::max<uint32_t>(1, std::min<uint32_t>(gq ? std::max<uint32_t>(1, (uint32_t)strtoul(gq, nullptr, 10))
                                                                    : kL0Groups, std::min<uint32_t>(ntiles, kBBoxBlocks)));
-    const uint32_t tpg = std::max<uint32_t>(1, (ntiles + ngroups - 1) / ngroups);
+    const uint32_t tpg = p6 ? pre6_tpg_ : std::max<uint32_t>(1, (ntiles + ngroups - 1) / ngroups);
     ngroups = std::max<uint32_t>(1, (ntiles + tpg - 1) / tpg);
     uint32_t* gcnt0 = static_cast<uint32_t*>(dev_->get(64ull * ngroups * 4 + 64));
     Arena l0dummy{static_cast<float4*>(dev_->get(256ull * kL0BS * kL0IPT * 16)),
@@ -5193,17 +5277,34 @@ int Engine::level0_bin() {
     uint32_t* cnt6 = nullptr;
     uint32_t* ph6 = nullptr;
     uint32_t* gpar = nullptr;
-    if (ntiles && !nf_mode_ && fold_hint(cs) && getenv("PCC_NO_FOLD") == nullptr) {
+    if (ntiles && !nf_mode_ && (p6 || fold_hint(cs)) && getenv("PCC_NO_FOLD") == nullptr) {
         cnt6 = static_cast<uint32_t*>(dev_->get(64ull * ntiles * 4));
         ph6 = static_cast<uint32_t*>(dev_->get(64ull * ntiles * 4));
         gpar = static_cast<uint32_t*>(dev_->get(64ull * ngroups * 32 * 4));
+        if (p6) {
+            // the groups the upload did not complete, then the run records and
+            // pair counts in this build's layout (rows of ntiles / ngroups)
+            if (ngroups > pre6_gdone_)
+                k_l0_tile6<false><<<ngroups - pre6_gdone_, kL0BS, 0, stream_>>>(
+                    src_, nullptr, dev_->ar[1], nsrc_, P, ntiles, tpg, pre6_gcap_, d_pre6_cnt_, d_pre6_ph_, d_pre6_gpar_,
+                    dev_->bbox_part, dev_->bbox_flag, l0dummy, pre6_gdone_, (uint32_t)pre6_tcap_);
+            HIP_CHECK(hipMemcpy2DAsync(cnt6, (size_t)ntiles * 4, d_pre6_cnt_, (size_t)pre6_tcap_ * 4, (size_t)ntiles * 4, 64,
+                                       hipMemcpyDeviceToDevice, stream_));
+            HIP_CHECK(hipMemcpy2DAsync(ph6, (size_t)ntiles * 4, d_pre6_ph_, (size_t)pre6_tcap_ * 4, (size_t)ntiles * 4, 64,
+                                       hipMemcpyDeviceToDevice, stream_));
+            HIP_CHECK(hipMemcpy2DAsync(gpar, (size_t)ngroups * 128, d_pre6_gpar_, (size_t)pre6_gcap_ * 128,
+                                       (size_t)ngroups * 128, 64, hipMemcpyDeviceToDevice, stream_));
+        } else {
         HIP_CHECK(hipMemsetAsync(dev_->bbox_flag, 0, 4, stream_));
         if (l0keys)
             k_l0_tile6<true><<<ngroups, kL0BS, 0, stream_>>>(src_, src_keys_, dev_->ar[1], nsrc_, P, ntiles, tpg, ngroups,
-                                                             cnt6, ph6, gpar, dev_->bbox_part, dev_->bbox_flag, l0dummy);
+                                                             cnt6, ph6, gpar, dev_->bbox_part, dev_->bbox_flag, l0dummy,
+                                                             0, ntiles);
         else
             k_l0_tile6<false><<<ngroups, kL0BS, 0, stream_>>>(src_, nullptr, dev_->ar[1], nsrc_, P, ntiles, tpg, ngroups,
-                                                              cnt6, ph6, gpar, dev_->bbox_part, dev_->bbox_flag, l0dummy);
+                                                              cnt6, ph6, gpar, dev_->bbox_part, dev_->bbox_flag, l0dummy,
+                                                              0, ntiles);
+        }
         k_bbox_final<<<1, 256, 0, stream_>>>(dev_->bbox_part, ngroups);
         HIP_CHECK(hipGetLastError());
         float bb[6];
@@ -5222,7 +5323,7 @@ int Engine::level0_bin() {
             bmax_[a] = bb[3 + a];
             fold &= (int64_t)cell_index1(bmax_[a], cs) - (int64_t)cell_index1(bmin_[a], cs) < 2;
         }
-        stats_.pre0_tiles = 0;
+        stats_.pre0_tiles = p6 ? std::min<uint64_t>((uint64_t)pre6_gdone_ * tpg, ntiles) : 0;
     }
     stats_.l0_fold = fold ? 1 : 0;
     if (!fold) {

@@ -53,6 +53,19 @@ def test_single_level0_cell(env, monkeypatch):
     assert st["levels"] >= 2
 
 
+@pytest.mark.parametrize("env", [{"PCC_PRE_PIECE": "40000"}, {"PCC_PRE_PIECE": "40000", "PCC_NO_PRE6": "1"},
+                                 {"PCC_PRE_PIECE": "3072"}], ids=["pass1", "pass0", "tile_pieces"])
+def test_upload_in_pieces_with_level0_pass_behind(env, monkeypatch):
+    """Host input copied in pieces with level-0 work behind each copy
+    (Engine::pre0_count): the folded pass 1 over the groups each piece completes
+    (pre6_run; the build finishes the rest), or pass 0 (PCC_NO_PRE6); two files,
+    pieces that end mid-tile and mid-group."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    pts = synth(43, 0, 330_001)
+    _check([pts[:200_003], pts[200_003:]], fast=True)
+
+
 def test_config1_uniform_100k():
     pts = synth(1, 0, 100_000)
     st = _check([pts])
