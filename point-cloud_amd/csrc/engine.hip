@@ -209,6 +209,7 @@ enum ErrBits : uint32_t {
     ERR_CAPACITY = 1u << 6,
     ERR_CLAIM = 1u << 7,
     ERR_SLAB_SIZE = 1u << 8,
+    ERR_ARENA = 1u << 9,   // child-slab capacities beyond the next arena (their regions are clamped to it)
 };
 
 struct Counters {
@@ -1486,14 +1487,17 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_down6g(const Point* __restrict_
 // sequence of that digit's runs, tile after tile, i.e. in key order.  Without
 // external keys a point's key is its tile's base plus its index in the tile, so
 // pass 1 writes that 16-bit index only.
-template <bool KEYS>
+// RB1: the low layer bits of pass 1 (6: 64 digits, runs of ~48 points for pass
+// 2; 5: 32 digits, runs of ~96), the pair's high part then the cell parity and
+// the layer's other kL0LayerBits - RB1 bits.
+template <bool KEYS, int RB1 = 6>
 __global__ __launch_bounds__(kL0BS, 8) void k_l0_tile6(const Point* __restrict__ in, const uint32_t* __restrict__ keys,
                                                        Arena O, uint64_t n, L0Params P, uint32_t ntiles, uint32_t tpg,
                                                        uint32_t ngroups, uint32_t* __restrict__ cnt6,
                                                        uint32_t* __restrict__ ph6, uint32_t* __restrict__ gcnt,
                                                        float* __restrict__ part, uint32_t* __restrict__ flag,
                                                        Arena dummy, uint32_t g0, uint32_t cstride) {
-    constexpr int R = 64, R5 = 32, HP = R5 + 1;
+    constexpr int R = 1 << RB1, HB = kL0LayerBits - RB1, R5 = 8 << HB, HP = R5 + 1;
     using KT = typename std::conditional<KEYS, uint32_t, uint16_t>::type;
     __shared__ float4 sp[kL0Tile];
     __shared__ KT sk[kL0Tile];
@@ -1513,7 +1517,7 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_tile6(const Point* __restrict__
     uint32_t nf = 0;
     const uint32_t t0 = g * tpg, t1 = min(t0 + tpg, ntiles);
     // per-tile run records through buffer descriptors (scalar bases, 32-bit offsets)
-    const __amdgpu_buffer_rsrc_t rC = srd(cnt6, 256ull * cstride), rH = srd(ph6, 256ull * cstride);
+    const __amdgpu_buffer_rsrc_t rC = srd(cnt6, 4ull * R * cstride), rH = srd(ph6, 4ull * R * cstride);
     auto load_tile = [&](float4* v, uint32_t* kk, uint32_t tile) {   // unconditional, clamped (see k_l0_down6g)
         const uint64_t base = (uint64_t)tile * kL0Tile;
         asm volatile("" ::: "memory");
@@ -1558,9 +1562,9 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_tile6(const Point* __restrict__
                 nf |= (ll < 0 || ll >= (int64_t)kL0Layers) ? kNfLayer : 0u;   // (an infinite z too: rebinned apart)
                 d6 = (uint32_t)ll & (R - 1);
                 const uint32_t par = (uint32_t)(ix & 1) | ((uint32_t)(iy & 1) << 1) | ((uint32_t)(iz & 1) << 2);
-                atomicAdd(&h[d6 * HP + ((par << 2) | (((uint32_t)ll >> 6) & 3u))], 1u);
+                atomicAdd(&h[d6 * HP + ((par << HB) | (((uint32_t)ll >> RB1) & ((1u << HB) - 1u)))], 1u);
             }
-            const uint64_t same = wave_peers<6>(d6, valid);
+            const uint64_t same = wave_peers<RB1>(d6, valid);
             const uint32_t rw = (uint32_t)__popcll(same & lt);
             if (valid && rw == 0) wcnt[d6][r * kL0W + w] = (uint8_t)__popcll(same);
             dgp |= d6 << (8 * r);
@@ -1572,10 +1576,12 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_tile6(const Point* __restrict__
             const uint32_t tot = l0_tile_prefix<R>(wcnt, wpre, lane, ex);
             uint32_t ln = lane;   // (recomputed addresses: see k_l0_down5g)
             asm volatile("" : "+v"(ln));
-            dbase[ln] = ex;
-            const uint32_t ro = (ln * cstride + tile) * 4;   // this tile's run of digit `lane`: length, start
-            bst(rC, ro, tot);
-            bst(rH, ro, tile * (uint32_t)kL0Tile + ex);
+            if (ln < (uint32_t)R) {
+                dbase[ln] = ex;
+                const uint32_t ro = (ln * cstride + tile) * 4;   // this tile's run of digit `lane`: length, start
+                bst(rC, ro, tot);
+                bst(rH, ro, tile * (uint32_t)kL0Tile + ex);
+            }
         }
         lds_barrier();
 #pragma unroll
@@ -1628,12 +1634,12 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_tile6(const Point* __restrict__
 // Segment starts of the digit-partitioned order from the tile-major pass 1:
 // start of (d6, group g) = the scanned run position of the group's first tile.
 __global__ void k_l0_tstarts(const uint32_t* __restrict__ voff, uint32_t ntiles, uint32_t tpg, uint32_t ngroups,
-                             uint64_t n, uint32_t* __restrict__ starts) {
+                             uint64_t n, uint32_t* __restrict__ starts, uint32_t R1) {   // R1: pass-1 digits
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= 64 * (ngroups + 1)) return;
+    if (i >= R1 * (ngroups + 1)) return;
     const uint32_t d6 = i / (ngroups + 1), g = i % (ngroups + 1);
     const uint64_t t = (uint64_t)g * tpg;
-    starts[i] = g < ngroups ? voff[(uint64_t)d6 * ntiles + t] : (d6 < 63 ? voff[(uint64_t)(d6 + 1) * ntiles] : (uint32_t)n);
+    starts[i] = g < ngroups ? voff[(uint64_t)d6 * ntiles + t] : (d6 + 1 < R1 ? voff[(uint64_t)(d6 + 1) * ntiles] : (uint32_t)n);
 }
 
 // Per (d6, d5): exclusive prefix over the groups of the pair counts of
@@ -1641,26 +1647,27 @@ __global__ void k_l0_tstarts(const uint32_t* __restrict__ voff, uint32_t ntiles,
 // none) into the dense-d5 layout k_l0_down5g reads, and the dense histogram
 // bin (d5 << 6 | d6).  A count in a parity slot no dense d5 names is a point
 // outside the grid (pass 2 reports it).
-struct L0PMap { uint8_t s[32]; };
+struct L0PMap { uint8_t s[64]; };
+template <int LB = 6>
 __global__ __launch_bounds__(1024) void k_l0_gprefix_par(const uint32_t* __restrict__ gsrc, uint32_t* __restrict__ gdst,
                                                          uint32_t ngroups, uint32_t D, L0PMap pm,
                                                          uint32_t* __restrict__ hist, Counters* ctr) {
-    constexpr int R5 = 32, NC = 1024 / R5;
+    constexpr int R5 = 8 << (kL0LayerBits - LB), NC = 1024 / R5;
     __shared__ uint32_t part[NC][R5];
     const uint32_t d6 = blockIdx.x, d5 = threadIdx.x % R5, c = threadIdx.x / R5;
     const uint32_t gpc = (ngroups + NC - 1) / NC, g0 = min(c * gpc, ngroups), g1 = min(g0 + gpc, ngroups);
     const uint32_t ps = pm.s[d5];
-    const uint32_t* row = gsrc + (uint64_t)d6 * ngroups * R5 + (ps < 32u ? ps : 0u);
+    const uint32_t* row = gsrc + (uint64_t)d6 * ngroups * R5 + (ps < (uint32_t)R5 ? ps : 0u);
     uint32_t* orow = gdst + (uint64_t)d6 * ngroups * R5 + d5;
     uint32_t acc = 0;
-    if (ps < 32u)
+    if (ps < (uint32_t)R5)
         for (uint32_t g = g0; g < g1; g++) acc += row[(uint64_t)g * R5];
     part[c][d5] = acc;
     __syncthreads();
     if (c == 0) {
         uint32_t a = 0;
         for (int q = 0; q < NC; q++) { const uint32_t v = part[q][d5]; part[q][d5] = a; a += v; }
-        const uint32_t d0 = (d5 << 6) | d6;
+        const uint32_t d0 = (d5 << LB) | d6;
         if (d0 < D) hist[d0] = a;
         else if (a) set_err(ctr, ERR_L0_RANGE);
     }
@@ -1668,7 +1675,7 @@ __global__ __launch_bounds__(1024) void k_l0_gprefix_par(const uint32_t* __restr
     acc = part[c][d5];
     for (uint32_t g = g0; g < g1; g++) {
         orow[(uint64_t)g * R5] = acc;
-        if (ps < 32u) acc += row[(uint64_t)g * R5];
+        if (ps < (uint32_t)R5) acc += row[(uint64_t)g * R5];
     }
 }
 
@@ -1716,12 +1723,12 @@ __global__ void k_l0_wplan(const L0UnitW* __restrict__ units, uint32_t nunits, u
 __global__ __launch_bounds__(256) void k_l0_uplan(const uint32_t* __restrict__ starts, uint32_t ngroups, uint32_t tpg,
                                                   uint32_t ntiles, uint32_t target, uint32_t umax,
                                                   L0UnitW* __restrict__ uw, uint32_t* __restrict__ wn,
-                                                  uint32_t* __restrict__ out) {
+                                                  uint32_t* __restrict__ out, uint32_t R1) {   // R1 <= 64 rows
     __shared__ uint32_t ub[65];
     const uint32_t tid = threadIdx.x, u = blockIdx.x * 256 + tid;
     if (tid < 64) {   // units per row, exclusive scan over the rows (wave 0)
-        const uint32_t* row = starts + (uint64_t)tid * (ngroups + 1);
-        const uint32_t nu = (row[ngroups] - row[0] + target - 1) / target;
+        const uint32_t* row = starts + (uint64_t)min(tid, R1 - 1) * (ngroups + 1);
+        const uint32_t nu = tid < R1 ? (row[ngroups] - row[0] + target - 1) / target : 0u;
         uint32_t x = nu;
         for (int d = 1; d < 64; d <<= 1) {
             const uint32_t y = __shfl_up(x, d, 64);
@@ -1847,7 +1854,8 @@ __device__ __forceinline__ int64_t l0_dense_dest(const L0Params& P, float x, flo
 // physical starts (tile base + lp6) staged in LDS, fetched one window ahead and
 // stored one step before use.
 struct L0Slice { uint32_t tf, ntl, sv, sp; };
-template <int R5, bool TM, bool K16 = false>
+// LB: the low digit's bits (pass 1: 6, or 5 with R5 = 64 high digits)
+template <int R5, bool TM, bool K16 = false, int LB = 6>
 __global__ __launch_bounds__(kL0BS, 8) void k_l0_down5g(Arena S, Arena O, L0Params P, const L0Unit* __restrict__ units,
                                                         const uint32_t* __restrict__ starts, uint32_t ngroups,
                                                         const uint32_t* __restrict__ gpre,
@@ -1857,9 +1865,12 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_down5g(Arena S, Arena O, L0Para
                                                         const L0UnitW* __restrict__ uw, const uint2* __restrict__ wt,
                                                         const uint32_t* __restrict__ voff,
                                                         const uint32_t* __restrict__ ph6, uint32_t ntiles) {
-    constexpr int R = R5, RB = R5 == 32 ? 5 : R5 == 16 ? 4 : R5 == 8 ? 3 : 2;
-    static_assert((1 << RB) == R5, "R5 is a power of two in 4..32");
-    constexpr uint32_t kSl = kL0BS;   // slice entries (tiles per window) staged in LDS
+    constexpr int R = R5, RB = R5 == 64 ? 6 : R5 == 32 ? 5 : R5 == 16 ? 4 : R5 == 8 ? 3 : 2;
+    static_assert((1 << RB) == R5, "R5 is a power of two in 4..64");
+    constexpr uint32_t LM = (1u << LB) - 1u;
+    // slice entries (tiles per window) staged in LDS; a window over more tiles
+    // (a sparse digit) searches the run starts in memory
+    constexpr uint32_t kSl = R5 == 64 ? 128 : kL0BS;
     __shared__ float4 sp[kL0Tile];
     __shared__ uint32_t sk[kL0Tile];
     __shared__ uint8_t sd[kL0Tile];
@@ -1882,7 +1893,7 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_down5g(Arena S, Arena O, L0Para
     }
     uint32_t runr = 0;   // wave 0, lane t < R: next output position of digit t
     if (w == 0 && lane < (uint32_t)R) {
-        const uint32_t d0 = (lane << 6) | d6u;
+        const uint32_t d0 = (lane << LB) | d6u;
         runr = d0 < D ? cnt_scan[d0] + gpre[((uint64_t)d6u * ngroups + g0u) * R + lane] : 0u;
     }
     gofs[lane & (R - 1)] = runr;   // (an LDS write of runr: its load is complete before the loop)
@@ -1905,7 +1916,12 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_down5g(Arena S, Arena O, L0Para
         q.sp = bld(rPh, o);
     };
     auto slice_store = [&](const L0Slice& q) {
-        if (tid < q.ntl && tid < kSl) { slv[tid] = q.sv; slp[tid] = q.sp; }
+        if (tid < q.ntl && tid < kSl) {
+            uint32_t t = tid;   // the LDS addresses recomputed here, not kept live (spilled at the 64-VGPR cap)
+            asm volatile("" : "+v"(t));
+            slv[t] = q.sv;
+            slp[t] = q.sp;
+        }
     };
     // physical position of the unit's point at virtual position v (window of q)
     // physical positions of this thread's kL0IPT points of the window at `base`:
@@ -1971,10 +1987,10 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_down5g(Arena S, Arena O, L0Para
             if (valid) {
                 uint32_t dest;
                 const int64_t d = l0_dense_dest(P, v[r].x, v[r].y, v[r].z, dest);
-                if (d < 0 || ((uint32_t)d & 63u) != d6u || dest >= (uint32_t)kDests) {
+                if (d < 0 || ((uint32_t)d & LM) != d6u || dest >= (uint32_t)kDests) {
                     err = ERR_L0_RANGE;
                 } else {
-                    d5 = ((uint32_t)d >> 6) & (R - 1);
+                    d5 = ((uint32_t)d >> LB) & (R - 1);
                     atomicAdd(&hc[d5 * kDests + dest], 1u);
                 }
             }
@@ -2060,7 +2076,7 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_down5g(Arena S, Arena O, L0Para
     for (int i = tid; i < R * kDests; i += kL0BS) {
         const uint32_t c = hc[i];
         if (!c) continue;
-        const uint32_t d0 = ((uint32_t)(i / kDests) << 6) | d6u;
+        const uint32_t d0 = ((uint32_t)(i / kDests) << LB) | d6u;
         if (d0 < D) atomicAdd(&dcap[(uint64_t)sid[d0] * kDests + (uint32_t)(i % kDests)], c);
     }
     if (err) set_err(ctr, err);
@@ -2424,7 +2440,8 @@ __device__ __forceinline__ void dense_grid_points(const SlabParams& P, L& S, uin
 // order inside a cell file is free).  Grandchild capacities count every
 // emission's (child, grandchild) slab when its rank is taken.
 // NF: the input has NaN coordinates (the NaN rules below; Engine::nf_mode_).
-template <bool SEEDS, bool NF>
+// KF: a merge level with forced emissions (kept seeds, P.kf_n > 0).
+template <bool SEEDS, bool NF, bool KF>
 __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
     using L = DenseLds;
     constexpr int BS = L::BS, TAB = L::TAB, NW = L::NW;
@@ -2558,7 +2575,7 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
         const uint32_t tag = ci & 31u;
         const uint32_t j = ng + ci * BS + tid;
         const bool valid = j < n;
-        const bool forced = valid && mine.k - P.kf_lo < P.kf_n;
+        const bool forced = KF && valid && mine.k - P.kf_lo < P.kf_n;
         {   // prefetch chunk i+2 (clamped)
             const uint32_t jo = min(j + PF * BS, nm1);
             pf.p = rP.p(jo * 16);
@@ -2755,7 +2772,7 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
             const uint32_t pos = (uint32_t)__shfl((int)base_l, d, 64) + rw;
             const int32_t room = __shfl(room_l, d, 64);
             const bool ok = vd && (int32_t)rw < room;
-            err |= (vd && !ok) ? (uint32_t)ERR_CAPACITY : 0u;
+            if (__ballot(vd && !ok)) err |= ERR_CAPACITY;
             bst4(oP, ok ? pos * 16 : 0xFFFFFFFFu, prv.em == 1 ? prv.gp : prvb.p);
             bst(oK, ok ? pos * 4 : 0xFFFFFFFFu, prvb.k);
             STAMP(6);
@@ -2942,7 +2959,8 @@ __device__ __forceinline__ int small_entry(SmallLds& S, uint32_t local, uint32_t
 constexpr uint32_t kWaveMax = 512;   // small slabs below this size: one wave each (k_slab_wave)
 __device__ __forceinline__ SmallDesc slab_desc(uint32_t s, const uint32_t* slab_cell, const int32_t* slab_layer,
                                                const uint32_t* slab_off, const uint32_t* slab_n, const int32_t* cell_idx,
-                                               const uint32_t* cell_sb, const uint32_t* dest_off, const uint32_t* dcap) {
+                                               const uint32_t* cell_sb, const uint32_t* dest_off, const uint32_t* dcap,
+                                               uint64_t acap) {
     const uint32_t cr_ = slab_cell[s];
     SmallDesc D;
     D.s = s;
@@ -2950,6 +2968,8 @@ __device__ __forceinline__ SmallDesc slab_desc(uint32_t s, const uint32_t* slab_
     D.n = slab_n[s];
     D.dbase = dest_off[s * kDests];
     D.dlen = dest_off[s * kDests + kDests - 1] + dcap[s * kDests + kDests - 1] - D.dbase;
+    // never past the next arena (a capacity sum above it is ERR_ARENA, k_level_begin)
+    D.dlen = (uint32_t)min((uint64_t)D.dlen, acap > D.dbase ? acap - D.dbase : 0ull);
     D.t = slab_layer[s];
     D.cx = cell_idx[3 * cr_];
     D.cy = cell_idx[3 * cr_ + 1];
@@ -2994,10 +3014,10 @@ __global__ __launch_bounds__(1024) void k_lpt_order(const uint32_t* __restrict__
 __global__ void k_dense_desc(const uint32_t* list, uint32_t nlist, const uint32_t* slab_cell, const int32_t* slab_layer,
                              const uint32_t* slab_off, const uint32_t* slab_n, const int32_t* cell_idx,
                              const uint32_t* cell_sb, const uint32_t* dest_off, const uint32_t* dcap, SmallDesc* out,
-                             const uint32_t* slab_prior, const PriorSlabRec* prec) {
+                             const uint32_t* slab_prior, const PriorSlabRec* prec, uint64_t acap) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nlist) return;
-    SmallDesc D = slab_desc(list[i], slab_cell, slab_layer, slab_off, slab_n, cell_idx, cell_sb, dest_off, dcap);
+    SmallDesc D = slab_desc(list[i], slab_cell, slab_layer, slab_off, slab_n, cell_idx, cell_sb, dest_off, dcap, acap);
     if (slab_prior) {   // merge, level >= 1: seeds read in place (pad0 = offset in the seed array, pad1 = count)
         const uint32_t pr = slab_prior[D.s];
         if (pr != kNoPriorSlab) { D.pad0 = prec[pr].seed_off; D.pad1 = prec[pr].nseed; D.ng = prec[pr].ngrid; }
@@ -3009,12 +3029,12 @@ __global__ void k_small_desc(const uint32_t* list, uint32_t nlist, const uint32_
                              const uint32_t* slab_off, const uint32_t* slab_n, const int32_t* cell_idx,
                              const uint32_t* cell_sb, const uint32_t* dest_off, const uint32_t* dcap, SmallDesc* wave_out,
                              SmallDesc* block_out, uint32_t* counts, const uint32_t* slab_prior,
-                             const PriorSlabRec* prec) {
+                             const PriorSlabRec* prec, uint64_t acap) {
     __shared__ uint32_t wc[4][4], bpre[4][4];
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     const bool in = i < nlist;
     SmallDesc D = slab_desc(in ? list[i] : list[0], slab_cell, slab_layer, slab_off, slab_n, cell_idx, cell_sb,
-                            dest_off, dcap);
+                            dest_off, dcap, acap);
     if (slab_prior) {   // merge, level >= 1: the slab's seeds stay in the seed array (pad0 = offset, pad1 = count)
         const uint32_t pr = slab_prior[D.s];
         if (pr != kNoPriorSlab) { D.pad0 = prec[pr].seed_off; D.pad1 = prec[pr].nseed; D.ng = prec[pr].ngrid; }
@@ -4016,6 +4036,15 @@ __global__ __launch_bounds__(256) void k_l0_lists(const uint32_t* slab_n, uint32
 }
 
 __global__ void k_set_u32(uint32_t* p, uint32_t v) { *p = v; }
+// A level's counters back to zero, and the sum of its child-slab capacities
+// checked against the next arena (the slab descriptors clamp every region to it)
+__global__ void k_level_begin(Counters* ctr, const uint32_t* cap_total, uint64_t cap) {
+    ctr->kept_cur = 0;
+    ctr->nbig = ctr->nsmall = 0;
+    ctr->max_slab = 0;
+    ctr->arrivals_next = 0;
+    if (*cap_total > cap) ctr->err |= ERR_ARENA;
+}
 
 // merge: the existing cloud's record of each level-0 slab (cell by binary search
 // over the sorted prior cells, then the layer inside the cell's records)
@@ -4264,7 +4293,8 @@ void Engine::add_file_host(const Point* pts, uint64_t n, uint32_t batch) {
     file_batch_.push_back(std::max<uint32_t>(batch, 1));
     n_ += n;
     nbatches_ += batches_of(n, batch);
-    HIP_CHECK(hipStreamSynchronize(stream_));
+    // (the level-0 work behind the copies may still run on the engine stream:
+    // the build is ordered behind it)
 }
 
 void Engine::stream_begin(uint64_t expected) {
@@ -4686,7 +4716,7 @@ bool Engine::pre6_run(uint64_t upto, hipEvent_t after, bool all) {
         if (landed == 0 && !all) return true;   // decide once a tile has landed
         pre_decided_ = true;
         pre6_ = false;
-        if (!getenv("PCC_PRE6") || getenv("PCC_NO_PRE6") || getenv("PCC_NO_FOLD") || landed == 0) return false;
+        if (getenv("PCC_NO_PRE6") || getenv("PCC_NO_FOLD") || landed == 0) return false;
         if (after) HIP_CHECK(hipStreamWaitEvent(stream_, after, 0));
         const uint32_t nb = (uint32_t)std::min<uint64_t>(landed, 512);
         k_bbox_sample<<<nb, 256, 0, stream_>>>(d_in_, landed * kL0Tile, landed, nb, dev_->bbox_part);
@@ -5257,8 +5287,14 @@ int Engine::level0_bin() {
     // groups with running offsets, so no per-tile counts exist.
     const uint32_t ntiles = (uint32_t)((nsrc_ + kL0Tile - 1) / kL0Tile);
     // pass 1 already run behind the upload (pre6_run) for this very input
-    const bool p6 = pre6_ && ntiles && src_ == d_in_ && nsrc_ == n_ && !prior_ && !keyed_ && !ext_in_ && h0_ == 0 &&
-                    !nf_mode_ && dev_->ar[1].p == pre6_ar1_ && ntiles <= pre6_tcap_ && getenv("PCC_NO_FOLD") == nullptr;
+    // pass-1 digits (the low 6 layer bits) and pass-2 digits (cell parity + 2 layer
+    // bits); a 5 + 6 split (pass-2 runs of ~96 points, 64 pass-2 digits) measured
+    // slower in round 4 (level 0 16.6-17.3 against 16.1-17.0 ms, same boxes)
+    constexpr int lb = 6;
+    constexpr uint32_t R1 = 1u << lb, R2 = 8u << (kL0LayerBits - lb), HB = (uint32_t)(kL0LayerBits - lb);
+    const bool p6 = pre6_ && ntiles && src_ == d_in_ && nsrc_ == n_ && !prior_ && !keyed_ && !ext_in_ &&
+                    h0_ == 0 && !nf_mode_ && dev_->ar[1].p == pre6_ar1_ && ntiles <= pre6_tcap_ &&
+                    getenv("PCC_NO_FOLD") == nullptr;
     pre6_ = false;   // (consumed: later levels overwrite the arena)
     const char* gq = getenv("PCC_L0_GROUPS");
     uint32_t ngroups = std::max<uint32_t>(1, std::min<uint32_t>(gq ? std::max<uint32_t>(1, (uint32_t)strtoul(gq, nullptr, 10))
@@ -5461,21 +5497,22 @@ int Engine::level0_bin() {
         if (fold) {
             // run positions of the tile-major output in the digit-partitioned order,
             // segment starts per (d6, group), pair prefixes from the parity slots
-            scan_excl_u32(cnt6, cnt6, 64u * ntiles, nullptr, dev_->scan, stream_);
-            k_l0_tstarts<<<grid_for(64ull * (ngroups + 1), 256, 1u << 30), 256, 0, stream_>>>(cnt6, ntiles, tpg, ngroups,
-                                                                                              nsrc_, starts);
+            scan_excl_u32(cnt6, cnt6, R1 * ntiles, nullptr, dev_->scan, stream_);
+            k_l0_tstarts<<<grid_for((uint64_t)R1 * (ngroups + 1), 256, 1u << 30), 256, 0, stream_>>>(
+                cnt6, ntiles, tpg, ngroups, nsrc_, starts, R1);
             L0PMap pm;
-            for (uint32_t d5 = 0; d5 < 32; d5++) {
-                // dense d5 = cell * 4 + layer-high bits, cell = (gz * g1 + gy) * g0 + gx
-                const uint32_t cell = d5 >> 2, hi = d5 & 3u;
+            for (uint32_t d5 = 0; d5 < 64; d5++) pm.s[d5] = 0xFF;
+            for (uint32_t d5 = 0; d5 < R2; d5++) {
+                // dense high digit = cell << HB | layer-high bits, cell = (gz * g1 + gy) * g0 + gx
+                const uint32_t cell = d5 >> HB, hi = d5 & ((1u << HB) - 1u);
                 const uint32_t gx = cell % (uint32_t)P.g[0], gy = (cell / (uint32_t)P.g[0]) % (uint32_t)P.g[1];
                 const uint32_t gz = cell / ((uint32_t)P.g[0] * (uint32_t)P.g[1]);
                 if (cell >= G) { pm.s[d5] = 0xFF; continue; }
                 const uint32_t par = ((uint32_t)(P.lo[0] + (int32_t)gx) & 1u) | (((uint32_t)(P.lo[1] + (int32_t)gy) & 1u) << 1) |
                                      (((uint32_t)(P.lo[2] + (int32_t)gz) & 1u) << 2);
-                pm.s[d5] = (uint8_t)((par << 2) | hi);
+                pm.s[d5] = (uint8_t)((par << HB) | hi);
             }
-            k_l0_gprefix_par<<<64, 1024, 0, stream_>>>(gpar, gcnt, ngroups, (uint32_t)D, pm, hist, dev_->ctr);
+            k_l0_gprefix_par<lb><<<R1, 1024, 0, stream_>>>(gpar, gcnt, ngroups, (uint32_t)D, pm, hist, dev_->ctr);
         } else {
             if (l0keys) k_l0_gprefix<16><<<64, 1024, 0, stream_>>>(gcnt, ngroups, (uint32_t)D, hist, dev_->ctr);
             else k_l0_gprefix<32><<<64, 1024, 0, stream_>>>(gcnt, ngroups, (uint32_t)D, hist, dev_->ctr);
@@ -5569,7 +5606,7 @@ int Engine::level0_bin() {
         uint32_t* dwn = static_cast<uint32_t*>(dev_->get((uint64_t)umax * 4));
         HIP_CHECK(hipMemsetAsync(L->dcap, 0, (uint64_t)L->nslabs * kDests * 4, stream_));
         k_l0_uplan<<<(umax + 255) / 256, 256, 0, stream_>>>(starts, ngroups, tpg, ntiles, (uint32_t)target, umax, duw,
-                                                            dwn, dcnt);
+                                                            dwn, dcnt, R1);
         scan_excl_u32(dwn, dwn, umax, dcnt + 1, dev_->scan, stream_);
         k_l0_uplan_w0<<<(umax + 255) / 256, 256, 0, stream_>>>(duw, dwn, umax);
         k_l0_wplan<<<grid_for(wmax, 256, 1u << 30), 256, 0, stream_>>>(duw, 0, 0, cnt6, ntiles, dwt, dcnt);
@@ -5780,21 +5817,9 @@ int Engine::run_level(uint32_t li) {
         scan_excl_u32(L->dcap, L->dest_off, (uint32_t)ND, scratch, dev_->scan, stream_);
     }
     scan_excl_u32(L->slab_n, L->grid_off, L->nslabs, scratch + 1, dev_->scan, stream_);
-    // per-level counters
-    {
-        Counters hc;
-        uint32_t cap_total = 0;   // sum of the child-slab capacities: the next arena must hold them
-        HIP_CHECK(hipMemcpyAsync(&hc, dev_->ctr, sizeof hc, hipMemcpyDeviceToHost, stream_));
-        HIP_CHECK(hipMemcpyAsync(&cap_total, scratch, 4, hipMemcpyDeviceToHost, stream_));
-        HIP_CHECK(hipStreamSynchronize(stream_));
-        if (cap_total > dev_->cap)
-            return fail(-5, "internal error: child-slab capacities exceed the arena (level " + std::to_string(h) + ")");
-        hc.kept_cur = 0;
-        hc.nbig = hc.nsmall = 0;
-        hc.max_slab = 0;
-        hc.arrivals_next = 0;
-        HIP_CHECK(hipMemcpyAsync(dev_->ctr, &hc, sizeof hc, hipMemcpyHostToDevice, stream_));
-    }
+    // per-level counters, and the child-slab capacities against the next arena
+    // (on the device: no host round trip; reported at the level's sync)
+    k_level_begin<<<1, 1, 0, stream_>>>(dev_->ctr, scratch, dev_->cap);
     SlabParams SP;
     SP.in = in;
     SP.nx = nx;
@@ -5877,15 +5902,16 @@ int Engine::run_level(uint32_t li) {
                                                                            L->cell_idx, L->cell_sb, L->dest_off,
                                                                            L->dcap, dd,
                                                                            seeds_in_place ? L->slab_prior : nullptr,
-                                                                           seeds_in_place ? pdev_[h].slabs : nullptr);
+                                                                           seeds_in_place ? pdev_[h].slabs : nullptr, dev_->cap);
         SP.ddesc = dd;
 #ifdef PCC_STAMPS
         SP.stamps = stamps;
 #endif
         ev_begin(ST_DENSE);
-        if (seeds_in_place) k_slab<true, false><<<L->nbig, kDenseBS, 0, stream_>>>(SP);
-        else if (nf_mode_) k_slab<false, true><<<L->nbig, kDenseBS, 0, stream_>>>(SP);
-        else k_slab<false, false><<<L->nbig, kDenseBS, 0, stream_>>>(SP);
+        if (seeds_in_place) k_slab<true, false, true><<<L->nbig, kDenseBS, 0, stream_>>>(SP);
+        else if (SP.kf_n) k_slab<false, false, true><<<L->nbig, kDenseBS, 0, stream_>>>(SP);
+        else if (nf_mode_) k_slab<false, true, false><<<L->nbig, kDenseBS, 0, stream_>>>(SP);
+        else k_slab<false, false, false><<<L->nbig, kDenseBS, 0, stream_>>>(SP);
         ev_end(ST_DENSE);
         if (verbose) {
             HIP_CHECK(hipStreamSynchronize(stream_));
@@ -5906,7 +5932,7 @@ int Engine::run_level(uint32_t li) {
         k_small_desc<<<grid_for(L->nsmall, 256, 1u << 30), 256, 0, stream_>>>(
             L->small_list, L->nsmall, L->slab_cell, L->slab_layer, L->slab_off, L->slab_n, L->cell_idx, L->cell_sb,
             L->dest_off, L->dcap, wd, bd, cnt, seeds_in_place ? L->slab_prior : nullptr,
-            seeds_in_place ? pdev_[h].slabs : nullptr);
+            seeds_in_place ? pdev_[h].slabs : nullptr, dev_->cap);
         uint32_t hcnt[4];
         HIP_CHECK(hipMemcpyAsync(hcnt, cnt, 16, hipMemcpyDeviceToHost, stream_));
         HIP_CHECK(hipStreamSynchronize(stream_));
@@ -6000,7 +6026,7 @@ int Engine::run_level(uint32_t li) {
         char buf[200];
         snprintf(buf, sizeof buf,
                  "device error flags 0x%x at level %u (1 slot range, 2 layer, 4 octant, 8 sel, 16 kept cap, 64 capacity, "
-                 "128 claim, 256 slab > 2^28 arrivals)",
+                 "128 claim, 256 slab > 2^28 arrivals, 512 child capacities beyond the arena)",
                  hc.err, h);
         return fail(-5, buf);
     }

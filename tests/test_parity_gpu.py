@@ -53,8 +53,8 @@ def test_single_level0_cell(env, monkeypatch):
     assert st["levels"] >= 2
 
 
-@pytest.mark.parametrize("env", [{"PCC_PRE_PIECE": "40000", "PCC_PRE6": "1"}, {"PCC_PRE_PIECE": "40000", "PCC_NO_PRE6": "1"},
-                                 {"PCC_PRE_PIECE": "3072", "PCC_PRE6": "1"}], ids=["pass1", "pass0", "tile_pieces"])
+@pytest.mark.parametrize("env", [{"PCC_PRE_PIECE": "40000"}, {"PCC_PRE_PIECE": "40000", "PCC_NO_PRE6": "1"},
+                                 {"PCC_PRE_PIECE": "3072"}], ids=["pass1", "pass0", "tile_pieces"])
 def test_upload_in_pieces_with_level0_pass_behind(env, monkeypatch):
     """Host input copied in pieces with level-0 work behind each copy
     (Engine::pre0_count): the folded pass 1 over the groups each piece completes
