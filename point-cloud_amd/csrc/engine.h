@@ -309,6 +309,7 @@ private:
     uint32_t* d_pre6_gpar_ = nullptr;
     uint64_t pre6_alloc_tiles_ = 0, pre6_alloc_groups_ = 0;
     const void* pre6_ar1_ = nullptr;
+    void* d_pre6_dummy_ = nullptr;       // k_l0_tile6's scratch for its entry stores (persistent, not the build pool)
     bool pre6_run(uint64_t upto, hipEvent_t after, bool all);
     float* d_prepart_ = nullptr;
     uint32_t* d_preflag_ = nullptr;

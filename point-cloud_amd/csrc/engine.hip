@@ -4229,6 +4229,16 @@ void Engine::free_all() {
     dev_release(d_ckeys_);
     d_ckeys_ = nullptr;
     ckeys_cap_ = 0;
+    // non-finite inputs' split copies, the upload-time pass-1 records
+    dev_release(d_nf_pts_); dev_release(d_nf_keys_);
+    d_nf_pts_ = nullptr; d_nf_keys_ = nullptr; nf_cap_ = 0;
+    dev_release(d_inf_pts_); dev_release(d_inf_keys_);
+    d_inf_pts_ = nullptr; d_inf_keys_ = nullptr; inf_cap_ = 0;
+    dev_release(d_pre6_cnt_); dev_release(d_pre6_ph_); dev_release(d_pre6_gpar_); dev_release(d_pre6_dummy_);
+    d_pre6_cnt_ = d_pre6_ph_ = d_pre6_gpar_ = nullptr;
+    d_pre6_dummy_ = nullptr;
+    pre6_alloc_tiles_ = pre6_alloc_groups_ = 0;
+    pre6_ = false;
     free_prior();
 }
 
@@ -4754,6 +4764,7 @@ bool Engine::pre6_run(uint64_t upto, hipEvent_t after, bool all) {
             dev_->cap = cap_;
         }
         pre6_ar1_ = dev_->ar[1].p;
+        if (!d_pre6_dummy_) dev_alloc_t(d_pre6_dummy_, 256ull * kL0BS * kL0IPT * 20);
         HIP_CHECK(hipMemsetAsync(dev_->bbox_flag, 0, 4, stream_));
         pre6_gdone_ = 0;
         pre6_ = true;
@@ -4766,8 +4777,8 @@ bool Engine::pre6_run(uint64_t upto, hipEvent_t after, bool all) {
     if (after) HIP_CHECK(hipStreamWaitEvent(stream_, after, 0));
     const uint32_t ntl = all ? (uint32_t)tl : gend * pre6_tpg_;
     const uint64_t n = all ? upto : (uint64_t)ntl * kL0Tile;
-    Arena dummy{static_cast<float4*>(dev_->get(256ull * kL0BS * kL0IPT * 16)),
-                static_cast<uint32_t*>(dev_->get(256ull * kL0BS * kL0IPT * 4))};
+    Arena dummy{static_cast<float4*>(d_pre6_dummy_),
+                reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(d_pre6_dummy_) + 256ull * kL0BS * kL0IPT * 16)};
     k_l0_tile6<false><<<gend - pre6_gdone_, kL0BS, 0, stream_>>>(d_in_, nullptr, dev_->ar[1], n, l0_base_params(cfg_, 0),
                                                                 ntl, pre6_tpg_, pre6_gcap_, d_pre6_cnt_, d_pre6_ph_,
                                                                 d_pre6_gpar_, dev_->bbox_part, dev_->bbox_flag, dummy,
