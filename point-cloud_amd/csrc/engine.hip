@@ -3671,6 +3671,8 @@ struct BucketParams {
     const uint32_t* room;     // merge: seeds injected into each child slab (a child slab exists if it has any)
     Counters* ctr;
     uint32_t L;
+    uint32_t* dlist;    // buckets deferred to the second launch (k_bucket), and their count
+    uint32_t* dcount;
 };
 
 constexpr int kBktBS = 512;
@@ -3698,18 +3700,28 @@ __device__ __forceinline__ uint32_t first_key_after(const uint32_t* files, uint3
 // cell.rs:108-153 add_points_in_overflow, resolved for all batches at once
 // (SURVEY.md Appendix C.3): bucket = (cell, child octant), emissions key-ordered
 // inside each of its child slabs.
-__global__ __launch_bounds__(kBktBS) void k_bucket(BucketParams B) {
-    __shared__ uint32_t lds[kBktBS / 64 + 1];
-    __shared__ unsigned long long skp[kKeptMax];   // (key << 32) | arena position
+// Two launches per level: k_bucket<kBktSmallBS, kKeptSmall> resolves every
+// bucket except a kept list longer than kKeptSmall, which it appends to a list
+// of deferred buckets (state 4); k_bucket<kBktBS, kKeptMax, true>, a few
+// resident workgroups per CU, then walks that list with the 64 KB sort array.
+// The first launch's 8 KB sort array lets several workgroups share a CU (most
+// kept lists are short: the last level's cells have few emissions).
+constexpr int kBktSmallBS = 256;
+constexpr int kKeptSmall = 1024;
+constexpr uint32_t kBktSplitMin = 8192;   // buckets per level from which the two launches pay
+constexpr uint32_t kBktDeferred = 4;
+template <int BS, int KMAX, bool DEFERRED>
+__device__ __forceinline__ void bucket_one(const BucketParams& B, const uint32_t b, uint32_t* lds,
+                                           unsigned long long* skp) {
     __shared__ uint32_t s_cnt, s_off;
     __shared__ uint32_t s_min, s_max;
-    const uint32_t b = blockIdx.x, cell = b >> 3, oct = b & 7;
+    const uint32_t cell = b >> 3, oct = b & 7;
     const uint32_t s0 = B.cell_slab0[cell], s1 = B.cell_slab0[cell + 1];
     const uint32_t nd = (s1 - s0) * 3;
     const uint32_t L = B.L;
     const uint32_t csb = B.cell_sb[cell];
     uint32_t tot = 0, nne = 0, emin = 0xFFFFFFFFu, emax = 0;
-    for (uint32_t i = threadIdx.x; i < nd; i += kBktBS) {
+    for (uint32_t i = threadIdx.x; i < nd; i += BS) {
         const uint32_t di = (s0 + i / 3) * kDests + oct * 3 + i % 3;
         const uint32_t n = B.dest_n[di];
         nne += (n || (B.room && B.room[di])) ? 1u : 0u;   // slabs of the child cell, if it is built
@@ -3724,8 +3736,8 @@ __global__ __launch_bounds__(kBktBS) void k_bucket(BucketParams B) {
     __syncthreads();
     atomicMin(&s_min, emin);
     atomicMax(&s_max, emax);
-    tot = block_sum<kBktBS>(tot, lds);
-    nne = block_sum<kBktBS>(nne, lds);
+    tot = block_sum<BS>(tot, lds);
+    nne = block_sum<BS>(nne, lds);
     emin = s_min;
     emax = s_max;
     if (B.nprior) {   // merge mode: a bucket that is None on disk forwards everything at once (cell.rs:128-130)
@@ -3753,7 +3765,14 @@ __global__ __launch_bounds__(kBktBS) void k_bucket(BucketParams B) {
     const bool spilled = tot > L || (tot == L && emin != emax);
     if (!spilled) {
         // Some(list): the bucket's points in key order, kept in this cell's file
-        const bool big = tot > (uint32_t)kKeptMax;   // (limit > kKeptMax): sorted in global memory
+        if (!DEFERRED && KMAX < kKeptMax && tot > (uint32_t)KMAX) {   // sorted by the second launch
+            if (threadIdx.x == 0) {
+                B.bkt_state[b] = kBktDeferred;
+                B.dlist[atomicAdd(B.dcount, 1u)] = b;
+            }
+            return;
+        }
+        const bool big = tot > (uint32_t)KMAX;   // (limit > kKeptMax): sorted in global memory
         if (big && !B.ksort) {
             if (threadIdx.x == 0) { set_err(B.ctr, ERR_KEPT_CAP); B.bkt_state[b] = 0; }
             return;
@@ -3769,7 +3788,7 @@ __global__ __launch_bounds__(kBktBS) void k_bucket(BucketParams B) {
         // above the LDS capacity in the scratch at twice its kept offset (a
         // power-of-two padding below twice the list never reaches the next list's)
         unsigned long long* sk = big ? B.ksort + 2ull * s_off : skp;
-        for (uint32_t i = threadIdx.x; i < nd; i += kBktBS) {
+        for (uint32_t i = threadIdx.x; i < nd; i += BS) {
             const uint32_t di = (s0 + i / 3) * kDests + oct * 3 + i % 3;
             const uint32_t n = B.dest_n[di];
             if (n) {
@@ -3781,14 +3800,14 @@ __global__ __launch_bounds__(kBktBS) void k_bucket(BucketParams B) {
         uint32_t np2 = 1;
         while (np2 < tot) np2 <<= 1;
         __syncthreads();
-        for (uint32_t i = tot + threadIdx.x; i < np2; i += kBktBS) sk[i] = ~0ull;
+        for (uint32_t i = tot + threadIdx.x; i < np2; i += BS) sk[i] = ~0ull;
         __syncthreads();
         // bitonic sort by key (keys are unique, so the packed words order by
         // key); one thread per compare-exchange pair (the workgroup barrier
         // orders the global scratch's accesses too: one workgroup owns it)
         for (uint32_t kk = 2; kk <= np2; kk <<= 1)
             for (uint32_t jj = kk >> 1; jj > 0; jj >>= 1) {
-                for (uint32_t p = threadIdx.x; p < np2 / 2; p += kBktBS) {
+                for (uint32_t p = threadIdx.x; p < np2 / 2; p += BS) {
                     const uint32_t i = ((p & ~(jj - 1)) << 1) | (p & (jj - 1)), ix = i | jj;
                     const bool up = (i & kk) == 0;
                     const unsigned long long a = sk[i], c = sk[ix];
@@ -3796,7 +3815,7 @@ __global__ __launch_bounds__(kBktBS) void k_bucket(BucketParams B) {
                 }
                 __syncthreads();
             }
-        for (uint32_t i = threadIdx.x; i < tot; i += kBktBS) {
+        for (uint32_t i = threadIdx.x; i < tot; i += BS) {
             const uint32_t o = (uint32_t)sk[i];
             const float4 v = B.nx.p[o];
             reinterpret_cast<float4*>(B.kept)[s_off + i] = v;
@@ -3810,14 +3829,14 @@ __global__ __launch_bounds__(kBktBS) void k_bucket(BucketParams B) {
     // bound of K(e) = the first key with eb0 > e (0 below the cell's sb).  Binary
     // search over e; each list keeps the window of its count that the search so
     // far allows (counts are monotone in e), so a step costs a few loads per list.
-    constexpr int WL = 4;   // lists per thread with a window (nd <= WL * kBktBS)
+    constexpr int WL = 4;   // lists per thread with a window (nd <= WL * BS)
     __shared__ uint32_t s_k;
-    const bool windowed = nd <= (uint32_t)(WL * kBktBS);
+    const bool windowed = nd <= (uint32_t)(WL * BS);
     uint32_t wlo[WL], whi[WL], woff[WL], wr[WL];
 #pragma unroll
     for (int w = 0; w < WL; w++) {
         wlo[w] = whi[w] = woff[w] = wr[w] = 0;
-        const uint32_t i = threadIdx.x + (uint32_t)w * kBktBS;
+        const uint32_t i = threadIdx.x + (uint32_t)w * BS;
         if (windowed && i < nd) {
             const uint32_t di = (s0 + i / 3) * kDests + oct * 3 + i % 3;
             const uint32_t n = B.dest_n[di];
@@ -3842,7 +3861,7 @@ __global__ __launch_bounds__(kBktBS) void k_bucket(BucketParams B) {
                 c += lo2;
             }
         } else {
-            for (uint32_t i = threadIdx.x; i < nd; i += kBktBS) {
+            for (uint32_t i = threadIdx.x; i < nd; i += BS) {
                 const uint32_t di = (s0 + i / 3) * kDests + oct * 3 + i % 3;
                 const uint32_t n = B.dest_n[di];
                 if (!n) continue;
@@ -3855,7 +3874,7 @@ __global__ __launch_bounds__(kBktBS) void k_bucket(BucketParams B) {
                 c += lo2;
             }
         }
-        return block_sum<kBktBS>(c, lds);
+        return block_sum<BS>(c, lds);
     };
     const uint32_t c0 = eval(emin);
 #pragma unroll
@@ -3875,6 +3894,26 @@ __global__ __launch_bounds__(kBktBS) void k_bucket(BucketParams B) {
         }
     }
     if (threadIdx.x == 0) { B.bkt_state[b] = 2; B.bkt_n[b] = tot; B.bkt_nd[b] = nne; B.bkt_sb[b] = lo; B.bkt_off[b] = 0; }
+}
+template <int BS, int KMAX, bool DEFERRED = false>
+__global__ __launch_bounds__(BS) void k_bucket(BucketParams B) {
+    __shared__ uint32_t lds[BS / 64 + 1];
+    __shared__ unsigned long long skp[KMAX];   // (key << 32) | arena position
+    if constexpr (!DEFERRED) {
+        bucket_one<BS, KMAX, false>(B, blockIdx.x, lds, skp);
+    } else {
+        // the deferred buckets by ticket (their sizes vary)
+        __shared__ uint32_t s_next;
+        const uint32_t nl = *B.dcount;
+        uint32_t i = blockIdx.x;
+        while (i < nl) {
+            bucket_one<BS, KMAX, true>(B, B.dlist[i], lds, skp);
+            if (threadIdx.x == 0) s_next = atomicAdd(B.dcount + 1, 1u) + gridDim.x;
+            __syncthreads();   // (also: the next bucket reuses the LDS)
+            i = s_next;
+            __syncthreads();
+        }
+    }
 }
 
 // ------------------------------------------------------------------ next level tables
@@ -5993,7 +6032,23 @@ int Engine::run_level(uint32_t li) {
     BP.L = (raw_last_ && max_levels_ && li + 1 == max_levels_) ? 0u : cfg_.cell_point_overflow_limit;
     const uint32_t nb = 8 * L->ncells;
     ev_begin(ST_BUCKET);
-    k_bucket<<<nb, kBktBS, 0, stream_>>>(BP);
+    BP.dlist = static_cast<uint32_t*>(dev_->get(nb * 4ull));
+    BP.dcount = static_cast<uint32_t*>(dev_->get(8));   // count, ticket
+    // (PCC_BKT_SPLIT_MIN: another threshold, for tests of the two launches on small inputs)
+    const char* bsm = getenv("PCC_BKT_SPLIT_MIN");
+    const uint32_t split_min = bsm ? (uint32_t)strtoul(bsm, nullptr, 10) : kBktSplitMin;
+    const bool bkt_split = getenv("PCC_BKT_ONE") == nullptr && nb >= split_min;
+    if (bkt_split) HIP_CHECK(hipMemsetAsync(BP.dcount, 0, 8, stream_));
+    // a level of many buckets (most of them short kept lists, e.g. the last
+    // level) in two launches; a few buckets in one (the second launch and its
+    // counter cost more than they save there).  PCC_BKT_ONE: always one (A/B).
+    if (!bkt_split) {
+        k_bucket<kBktBS, kKeptMax><<<nb, kBktBS, 0, stream_>>>(BP);
+    } else {
+        k_bucket<kBktSmallBS, kKeptSmall><<<nb, kBktSmallBS, 0, stream_>>>(BP);
+        if (BP.L > (uint32_t)kKeptSmall)   // two resident workgroups per CU (64 KB of LDS each)
+            k_bucket<kBktBS, kKeptMax, true><<<std::min<uint32_t>(nb, 512), kBktBS, 0, stream_>>>(BP);
+    }
     ev_end(ST_BUCKET);
     HIP_CHECK(hipGetLastError());
     // this level's grid points (one scan instead of per-slab global atomics)

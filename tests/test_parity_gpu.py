@@ -109,6 +109,20 @@ def test_overflow_limit_above_lds_sort(limit, n):
     assert st["kept_points"] > 8192
 
 
+@pytest.mark.parametrize("limit,n", [(8192, 66_000), (20_000, 150_000), (3000, 40_000)])
+def test_bucket_resolution_in_two_launches(limit, n, monkeypatch):
+    """The two-launch bucket resolution that levels of >= 8 192 buckets take
+    (k_bucket: kept lists of <= 1 024 points sorted in an 8 KB LDS array, longer
+    ones deferred to resident 64 KB workgroups, above 8 192 through the global
+    scratch), forced at every level here (PCC_BKT_SPLIT_MIN=1) on inputs whose
+    kept lists span all three sizes; cell.rs:108-153."""
+    monkeypatch.setenv("PCC_BKT_SPLIT_MIN", "1")
+    pts = synth(23, 0, n, lo=0.0, ext=7.999)
+    k = n // 2
+    st = _check([pts[:k], pts[k:]], cfg=dict(cell_point_overflow_limit=limit, sub_grid_dimension=4, max_cell_size=8.0))
+    assert st["kept_points"] > 1024
+
+
 def test_gui_batch_size_50k():
     """The GUI path's default batch size (src/plugins/converter.rs:198-201,604: 50 000 per
     batch) over ragged files: batch boundaries move the event batches."""
