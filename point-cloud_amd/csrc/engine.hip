@@ -3708,13 +3708,15 @@ __device__ __forceinline__ uint32_t first_key_after(const uint32_t* files, uint3
 // kept lists are short: the last level's cells have few emissions).
 constexpr int kBktSmallBS = 256;
 constexpr int kKeptSmall = 1024;
-constexpr uint32_t kBktSplitMin = 8192;   // buckets per level from which the two launches pay
+constexpr uint32_t kBktSplitMin = 8192;
+constexpr int kBktLists = 640;   // a bucket's child-slab lists: 3 per slab of its cell (<= 3 x (2 dim + 5))   // buckets per level from which the two launches pay
 constexpr uint32_t kBktDeferred = 4;
 template <int BS, int KMAX, bool DEFERRED>
 __device__ __forceinline__ void bucket_one(const BucketParams& B, const uint32_t b, uint32_t* lds,
                                            unsigned long long* skp) {
-    __shared__ uint32_t s_cnt, s_off;
+    __shared__ uint32_t s_cnt, s_off, s_nl;
     __shared__ uint32_t s_min, s_max;
+    __shared__ uint32_t s_lo[kBktLists], s_ln[kBktLists], s_lp[kBktLists];   // a kept bucket's lists
     const uint32_t cell = b >> 3, oct = b & 7;
     const uint32_t s0 = B.cell_slab0[cell], s1 = B.cell_slab0[cell + 1];
     const uint32_t nd = (s1 - s0) * 3;
@@ -3779,6 +3781,7 @@ __device__ __forceinline__ void bucket_one(const BucketParams& B, const uint32_t
         }
         if (threadIdx.x == 0) {
             s_cnt = 0;
+            s_nl = 0;
             s_off = atomicAdd(&B.ctr->kept_cur, tot);
             if ((uint64_t)s_off + tot > B.kept_cap) set_err(B.ctr, ERR_KEPT_CAP);
         }
@@ -3788,13 +3791,35 @@ __device__ __forceinline__ void bucket_one(const BucketParams& B, const uint32_t
         // above the LDS capacity in the scratch at twice its kept offset (a
         // power-of-two padding below twice the list never reaches the next list's)
         unsigned long long* sk = big ? B.ksort + 2ull * s_off : skp;
-        for (uint32_t i = threadIdx.x; i < nd; i += BS) {
-            const uint32_t di = (s0 + i / 3) * kDests + oct * 3 + i % 3;
-            const uint32_t n = B.dest_n[di];
-            if (n) {
-                const uint32_t o = B.dest_off[di];
-                const uint32_t p = atomicAdd(&s_cnt, n);
-                for (uint32_t q = 0; q < n; q++) sk[p + q] = ((unsigned long long)B.nx.k[o + q] << 32) | (o + q);
+        if (nd <= (uint32_t)kBktLists) {
+            // the non-empty child-slab lists into an LDS table (threads over
+            // lists), then each list copied by one wave (lanes over its points):
+            // a long list is not one thread's serial loop
+            for (uint32_t i = threadIdx.x; i < nd; i += BS) {
+                const uint32_t di = (s0 + i / 3) * kDests + oct * 3 + i % 3;
+                const uint32_t n = B.dest_n[di];
+                if (n) {
+                    const uint32_t k = atomicAdd(&s_nl, 1u);
+                    s_lo[k] = B.dest_off[di];
+                    s_ln[k] = n;
+                    s_lp[k] = atomicAdd(&s_cnt, n);
+                }
+            }
+            __syncthreads();
+            const uint32_t wv = threadIdx.x / 64, ln = threadIdx.x & 63, nl = s_nl;
+            for (uint32_t k = wv; k < nl; k += BS / 64) {
+                const uint32_t o = s_lo[k], n = s_ln[k], p = s_lp[k];
+                for (uint32_t q = ln; q < n; q += 64) sk[p + q] = ((unsigned long long)B.nx.k[o + q] << 32) | (o + q);
+            }
+        } else {
+            for (uint32_t i = threadIdx.x; i < nd; i += BS) {
+                const uint32_t di = (s0 + i / 3) * kDests + oct * 3 + i % 3;
+                const uint32_t n = B.dest_n[di];
+                if (n) {
+                    const uint32_t o = B.dest_off[di];
+                    const uint32_t p = atomicAdd(&s_cnt, n);
+                    for (uint32_t q = 0; q < n; q++) sk[p + q] = ((unsigned long long)B.nx.k[o + q] << 32) | (o + q);
+                }
             }
         }
         uint32_t np2 = 1;
