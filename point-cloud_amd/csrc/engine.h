@@ -338,6 +338,7 @@ private:
     uint64_t nseeds_ = 0;                // S (all levels)
     Point* d_inj_ = nullptr;             // level >= 1 seeds, grouped by slab
     uint32_t* d_inj_keys_ = nullptr;
+    unsigned long long* d_inj_rec_ = nullptr;   // per grid seed of levels >= 1: its slot-table record (k_seed_rec)
     struct PriorDev {                    // one prior level on the device
         PriorCell* cells = nullptr;
         uint32_t* cell_slab0 = nullptr;

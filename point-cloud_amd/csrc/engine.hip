@@ -2206,6 +2206,7 @@ struct SlabParams {
     int32_t check_gchild;
     uint32_t kf_lo, kf_n;         // merge mode: keys in [kf_lo, kf_lo + kf_n) are forced emissions (engine.h PriorState)
     const float4* inj;            // merge mode: seeds of levels >= 1 (a small slab reads its own in place)
+    const unsigned long long* inj_rec;   // merge mode: per grid seed its slot-table record (k_seed_rec)
     const uint32_t* inj_keys;
     unsigned long long* stamps;   // diagnostic build only
 };
@@ -2524,6 +2525,21 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
             pre[q].k = 0;
         }
     }
+    // merge: the first seed records (below) are loaded before the LDS
+    // initialisation too
+    constexpr int SQ = 4;
+    const __amdgpu_buffer_rsrc_t rR = srd(P.inj_rec + D.pad0, SEEDS ? (uint64_t)ng * 8 : 0ull);
+    uint32_t rl[SQ], rh[SQ];
+    auto seed_batch = [&](uint32_t j0) {
+#pragma unroll
+        for (int k = 0; k < SQ; k++) {
+            const uint32_t jg = j0 + k * BS + tid;
+            const bool v = jg < ng;
+            rl[k] = bld(rR, v ? jg * 8 : 0xFFFFFFFFu);
+            rh[k] = bld(rR, v ? jg * 8 + 4 : 0xFFFFFFFFu);
+        }
+    };
+    if constexpr (SEEDS) seed_batch(0);
     // the LDS initialisation overlaps the first two chunks' loads
     for (int i = tid; i < TAB; i += BS) S.tab[i] = kEmpty64;
     for (int i = tid; i < L::HW; i += BS) S.head[i] = kEmpty32;   // tag 31, head kNil
@@ -2539,8 +2555,9 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
         // Merge: the slab's grid seeds (its first ng arrivals: keys below every
         // other arrival, one per slot, cell.rs:183-229) are the occupants the
         // replay would install, with no emission; they go straight into the table.
-        for (uint32_t j0 = 0; j0 < ng; j0 += BS) {
-            const uint32_t jg = j0 + tid;
+        // a seed whose record (k_seed_rec) is flagged: its slot and route again,
+        // with the error codes (never expected)
+        auto seed_exact = [&](uint32_t jg) {
             const bool v = jg < ng;
             const u32x4 q = rP.p(v ? jg * 16 : 0xFFFFFFFFu);
             const float x = __uint_as_float(q.x), y = __uint_as_float(q.y), z = __uint_as_float(q.z);
@@ -2564,6 +2581,29 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
                                              (wide ? 0u : ((uint32_t)(gn + 1) << 23)) | jg;
                 // two grid points in one slot: not a cell a converter writes
                 if (atomicCAS(&S.tab[(uint32_t)(ly * P.tx + lx)], kEmpty64, e) != kEmpty64) err |= ERR_CLAIM;
+            }
+        };
+        // the seeds' precomputed records, four chunks of loads in flight: one
+        // LDS CAS per seed
+        for (uint32_t j0 = 0; j0 < ng; j0 += SQ * BS) {
+            if (j0) seed_batch(j0);
+            bool flagged = false;
+#pragma unroll
+            for (int k = 0; k < SQ; k++) flagged |= (j0 + k * BS + tid < ng) && (rh[k] >> 31);
+            if (__ballot(flagged)) {
+#pragma unroll 1
+                for (int k = 0; k < SQ; k++) seed_exact(j0 + k * BS + tid);
+                continue;
+            }
+#pragma unroll
+            for (int k = 0; k < SQ; k++) {
+                const uint32_t jg = j0 + k * BS + tid;
+                if (jg < ng) {
+                    const uint32_t local = rh[k] & 0x3FFFu, dn = (rh[k] >> 14) & 31u, g1 = (rh[k] >> 19) & 31u;
+                    const unsigned long long e = ((unsigned long long)rl[k] << 33) | ((unsigned long long)dn << kJBits) |
+                                                 (wide ? 0u : (g1 << 23)) | jg;
+                    if (atomicCAS(&S.tab[local], kEmpty64, e) != kEmpty64) err |= ERR_CLAIM;
+                }
             }
         }
         __syncthreads();
@@ -3069,6 +3109,7 @@ __global__ void k_small_desc(const uint32_t* list, uint32_t nlist, const uint32_
 struct SmallPre {
     u32x4 pp[kSmallCh];
     uint32_t pk[kSmallCh];
+    uint32_t rh[kSmallCh], rl[kSmallCh];   // merge: a grid seed's slot-table record (k_seed_rec), else rh = ~0
     uint32_t doff, dcap;
 };
 
@@ -3090,6 +3131,14 @@ __device__ __forceinline__ void small_prefetch(const SlabParams& P, uint32_t li,
             R.pp[c] = u32x4{a.x | b.x, a.y | b.y, a.z | b.z, a.w | b.w};   // out-of-range loads return 0
             R.pk[c] = bld(rT, sd ? j * 4 : 0xFFFFFFFFu) | bld(rK, (v && !sd) ? j * 4 : 0xFFFFFFFFu);
         }
+        // the grid seeds' records (out of range: 0xFFFFFFFF, i.e. flagged)
+        const __amdgpu_buffer_rsrc_t rR = srd(P.inj_rec + D.pad0, (uint64_t)D.ng * 8);
+#pragma unroll
+        for (int c = 0; c < kSmallCh; c++) {
+            const uint32_t j = c * kSmallBS + tid;
+            R.rl[c] = bld(rR, j < D.ng ? j * 8 : 0xFFFFFFFFu);
+            R.rh[c] = j < D.ng ? bld(rR, j * 8 + 4) : 0xFFFFFFFFu;
+        }
     } else {
 #pragma unroll
         for (int c = 0; c < kSmallCh; c++) {
@@ -3097,6 +3146,8 @@ __device__ __forceinline__ void small_prefetch(const SlabParams& P, uint32_t li,
             const bool v = j < D.n;
             R.pp[c] = bld4(rP, v ? j * 16 : 0xFFFFFFFFu);
             R.pk[c] = bld(rK, v ? j * 4 : 0xFFFFFFFFu);
+            R.rl[c] = 0u;
+            R.rh[c] = 0xFFFFFFFFu;
         }
     }
     const __amdgpu_buffer_rsrc_t rD = srd(P.dest_off + (uint64_t)D.s * kDests, kDests * 4);
@@ -3163,6 +3214,15 @@ __device__ __forceinline__ void small_process(const SlabParams& P, SmallLds& S, 
         float d2 = 0.f;
         uint32_t dn = 0;
         if (ci < CH) {
+            int d, g;
+            if (!__ballot(valid && (R.rh[ci] >> 31))) {
+                // merge: a wave of grid seeds with their records (k_seed_rec)
+                d2 = __uint_as_float(R.rl[ci]);   // (no NaN in a merge)
+                pending = valid;
+                local = valid ? (R.rh[ci] & 0x3FFFu) : 0u;
+                d = (int)((R.rh[ci] >> 14) & 31u);
+                g = (int)((R.rh[ci] >> 19) & 31u) - 1;
+            } else {
             const float x = __uint_as_float(pp[ci].x), y = __uint_as_float(pp[ci].y), z = __uint_as_float(pp[ci].z);
             const SlotDest sd = slot_dest(x, y, z, G, SC);
             const int32_t lx = sd.ox - rx, ly = sd.oy - ry;
@@ -3174,15 +3234,16 @@ __device__ __forceinline__ void small_process(const SlabParams& P, SmallLds& S, 
             const bool foreign = !range_ok && d2 != d2;   // NaN x or y: slot (0, 0) outside the table (see k_slab)
             pending = valid && layer_ok && (range_ok || foreign);
             local = pending ? (range_ok ? (uint32_t)(ly * P.tx + lx) : kForeignSlot) : 0u;
-            if (pending && pk[ci] - P.kf_lo < P.kf_n) {   // merge mode: forced emission
-                pending = false;
-                self_em = true;
-            }
-            const int d = sd.d;
-            int g = sd.g;
+            d = sd.d;
+            g = sd.g;
             const bool bad = valid && (!layer_ok || (!range_ok && !foreign) || d < 0 || (P.check_gchild && g < 0));
             if (__ballot(bad)) {
                 if (bad) err |= slot_route_errs(slot_route(x, y, z, G), layer_ok, range_ok, cx, cy, cz, t, P.check_gchild);
+            }
+            }
+            if (pending && pk[ci] - P.kf_lo < P.kf_n) {   // merge mode: forced emission
+                pending = false;
+                self_em = true;
             }
             dn = d < 0 ? 0u : (uint32_t)d;
             own_d[ci] = (int32_t)dn;
@@ -4314,6 +4375,8 @@ void Engine::free_prior() {
     d_inj_ = nullptr;
     dev_release(d_inj_keys_);
     d_inj_keys_ = nullptr;
+    dev_release(d_inj_rec_);
+    d_inj_rec_ = nullptr;
     for (PriorDev& d : pdev_) {
         dev_release(d.cells); dev_release(d.cell_slab0); dev_release(d.slab_layer); dev_release(d.slabs);
     }
@@ -4499,6 +4562,72 @@ static T* upload(const std::vector<T, A>& v) {
     return d;
 }
 
+// Slot-table geometry of level h (the slab kernels' quotients, hex.rs:67-85,
+// metadata.rs:91-102)
+static LevelGeo level_geo(const Config& cfg, uint32_t h) {
+    const uint32_t dim = cfg.sub_grid_dimension;
+    const float cs = cell_size(cfg.max_cell_size, h), csc = cell_size(cfg.max_cell_size, h + 1),
+                csg = cell_size(cfg.max_cell_size, h + 2);
+    LevelGeo G;
+    G.cr = hex_radius(sub_cell_size(cs, dim));
+    G.crx = G.cr * kSqrt3;
+    G.cry = (-G.cr) * kSqrt3;
+    G.inv_crx = 1.0f / G.crx;
+    G.inv_cry = 1.0f / G.cry;
+    G.inv_cr = 1.0f / G.cr;
+    G.csc = csc;
+    G.inv_csc = 1.0f / csc;
+    G.crc = hex_radius(sub_cell_size(csc, dim));
+    G.inv_crc = 1.0f / G.crc;
+    G.csg = csg;
+    G.inv_csg = 1.0f / csg;
+    G.crg = hex_radius(sub_cell_size(csg, dim));
+    G.inv_crg = 1.0f / G.crg;
+    G.exact = 0;
+    for (float v : {G.cr, G.crx, G.cry, G.csg, G.crg})   // div_rc's divisor range
+        if (!(std::fabs(v) >= 0x1p-60f && std::fabs(v) <= 0x1p60f)) G.exact = 1;
+    return G;
+}
+
+// The slot-table record of every grid seed of the existing cloud's levels >= 1,
+// made once when the cloud is adopted (the reference recomputes each stored
+// point's slot when it reads a cell, cell.rs:183-229): the slab kernel's merge
+// mode then installs a seed with one load and one LDS CAS instead of its slot
+// and route arithmetic.  Record: d2 key (bits 0-31), slot index in the slab's
+// table (32-45), child slab (46-50), grandchild slab + 1 (51-55); bit 63: the
+// seed's slot or route failed (the kernel recomputes it and reports the error).
+__global__ __launch_bounds__(256) void k_seed_rec(const PriorCell* __restrict__ cells, const uint32_t* __restrict__ cell_slab0,
+                                                  const int32_t* __restrict__ slab_layer,
+                                                  const PriorSlabRec* __restrict__ slabs, uint32_t ncells,
+                                                  const float4* __restrict__ inj, LevelGeo G, float cs, int32_t tx, int32_t ty,
+                                                  int32_t check_gchild, unsigned long long* __restrict__ rec) {
+    for (uint32_t c = blockIdx.x; c < ncells; c += gridDim.x) {
+        const int32_t cx = cells[c].x, cy = cells[c].y, cz = cells[c].z;
+        const I3 c0 = hex_from_world(cell_pos1(cx, cs), cell_pos1(cy, cs), cell_pos1(cz, cs), G.cr);
+        const int32_t rx = c0.x - tx / 2, ry = c0.y - ty / 2;
+        for (uint32_t s = cell_slab0[c]; s < cell_slab0[c + 1]; s++) {
+            const int32_t t = slab_layer[s];
+            const SlabCtx SC{cx, cy, cz, t};
+            const float zt = (float)t * G.cr;
+            const uint32_t off = slabs[s].seed_off, ng = slabs[s].ngrid;
+            for (uint32_t j = threadIdx.x; j < ng; j += 256) {
+                const float4 q = inj[off + j];
+                const SlotDest sd = slot_dest(q.x, q.y, q.z, G, SC);
+                const int32_t lx = sd.ox - rx, ly = sd.oy - ry;
+                const bool range_ok = lx >= 0 && ly >= 0 && lx < tx && ly < ty;
+                float X, Y, Z;
+                slot_centre(sd, G.cr, zt, X, Y, Z);
+                const float d2 = dist2(X, Y, Z, q.x, q.y, q.z);
+                const bool bad = !sd.layer_ok || !range_ok || sd.d < 0 || (check_gchild && sd.g < 0) ||
+                                 (uint32_t)(ly * tx + lx) >= (1u << 14);
+                rec[off + j] = bad ? (1ull << 63)
+                                   : ((unsigned long long)dist_key(d2) | ((unsigned long long)(ly * tx + lx) << 32) |
+                                      ((unsigned long long)sd.d << 46) | ((unsigned long long)(sd.g + 1) << 51));
+            }
+        }
+    }
+}
+
 void Engine::set_prior(const PriorState& p) {
     HIP_CHECK(hipStreamSynchronize(stream_));
     free_prior();
@@ -4517,6 +4646,22 @@ void Engine::set_prior(const PriorState& p) {
         d.ncells = (uint32_t)lv.cells.size();
         d.nslabs = (uint32_t)lv.slabs.size();
         pdev_.push_back(d);
+    }
+    // the grid seeds' slot-table records (levels >= 1; level h of the build is
+    // level h of the existing cloud: the config governs both)
+    dev_alloc_t(d_inj_rec_, std::max<size_t>(p.inj.size(), 1) * 8);
+    {
+        const SlabGeom g = slab_geom(cfg_.sub_grid_dimension);
+        for (size_t h = 1; h < pdev_.size(); h++) {
+            const PriorDev& d = pdev_[h];
+            if (!d.ncells) continue;
+            k_seed_rec<<<std::min<uint32_t>(d.ncells, 65536), 256, 0, stream_>>>(
+                d.cells, d.cell_slab0, d.slab_layer, d.slabs, d.ncells, reinterpret_cast<const float4*>(d_inj_),
+                level_geo(cfg_, (uint32_t)h), cell_size(cfg_.max_cell_size, (uint32_t)h), g.tx, g.ty,
+                (h + 2 < kMaxDepth) ? 1 : 0, d_inj_rec_);
+        }
+        HIP_CHECK(hipGetLastError());
+        HIP_CHECK(hipStreamSynchronize(stream_));
     }
     prior_ = true;
     comb_ok_ = false;
@@ -5857,8 +6002,7 @@ int Engine::run_level(uint32_t li) {
     const uint32_t h = L->h;   // absolute level (h0_ + li)
     const uint32_t dim = cfg_.sub_grid_dimension;
     const SlabGeom g = slab_geom(dim);
-    const float cs = cell_size(cfg_.max_cell_size, h), csc = cell_size(cfg_.max_cell_size, h + 1),
-                csg = cell_size(cfg_.max_cell_size, h + 2);
+    const float cs = cell_size(cfg_.max_cell_size, h);
     const Arena& in = dev_->ar[L->arena];
     const Arena& nx = dev_->ar[1 - L->arena];
     const uint64_t ND = (uint64_t)L->nslabs * kDests;
@@ -5922,26 +6066,8 @@ int Engine::run_level(uint32_t li) {
     SP.inj = reinterpret_cast<const float4*>(d_inj_);
     SP.inj_keys = d_inj_keys_;
     SP.cs = cs;
-    {
-        LevelGeo& G = SP.G;
-        G.cr = hex_radius(sub_cell_size(cs, dim));
-        G.crx = G.cr * kSqrt3;
-        G.cry = (-G.cr) * kSqrt3;
-        G.inv_crx = 1.0f / G.crx;
-        G.inv_cry = 1.0f / G.cry;
-        G.inv_cr = 1.0f / G.cr;
-        G.csc = csc;
-        G.inv_csc = 1.0f / csc;
-        G.crc = hex_radius(sub_cell_size(csc, dim));
-        G.inv_crc = 1.0f / G.crc;
-        G.csg = csg;
-        G.inv_csg = 1.0f / csg;
-        G.crg = hex_radius(sub_cell_size(csg, dim));
-        G.inv_crg = 1.0f / G.crg;
-        G.exact = 0;
-        for (float v : {G.cr, G.crx, G.cry, G.csg, G.crg})   // div_rc's divisor range
-            if (!(std::fabs(v) >= 0x1p-60f && std::fabs(v) <= 0x1p60f)) G.exact = 1;
-    }
+    SP.G = level_geo(cfg_, h);
+    SP.inj_rec = d_inj_rec_;
     SP.tx = g.tx;
     SP.ty = g.ty;
     SP.stamps = nullptr;
