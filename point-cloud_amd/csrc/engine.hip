@@ -4611,7 +4611,8 @@ __global__ __launch_bounds__(256) void k_seed_rec(const PriorCell* __restrict__ 
                                                   const int32_t* __restrict__ slab_layer,
                                                   const PriorSlabRec* __restrict__ slabs, uint32_t ncells,
                                                   const float4* __restrict__ inj, LevelGeo G, float cs, int32_t tx, int32_t ty,
-                                                  int32_t check_gchild, unsigned long long* __restrict__ rec) {
+                                                  int32_t check_gchild, uint32_t flag_all,
+                                                  unsigned long long* __restrict__ rec) {
     for (uint32_t c = blockIdx.x; c < ncells; c += gridDim.x) {
         const int32_t cx = cells[c].x, cy = cells[c].y, cz = cells[c].z;
         const I3 c0 = hex_from_world(cell_pos1(cx, cs), cell_pos1(cy, cs), cell_pos1(cz, cs), G.cr);
@@ -4629,7 +4630,7 @@ __global__ __launch_bounds__(256) void k_seed_rec(const PriorCell* __restrict__ 
                 float X, Y, Z;
                 slot_centre(sd, G.cr, zt, X, Y, Z);
                 const float d2 = dist2(X, Y, Z, q.x, q.y, q.z);
-                const bool bad = !sd.layer_ok || !range_ok || sd.d < 0 || (check_gchild && sd.g < 0) ||
+                const bool bad = flag_all || !sd.layer_ok || !range_ok || sd.d < 0 || (check_gchild && sd.g < 0) ||
                                  (uint32_t)(ly * tx + lx) >= (1u << 14);
                 rec[off + j] = bad ? (1ull << 63)
                                    : ((unsigned long long)dist_key(d2) | ((unsigned long long)(ly * tx + lx) << 32) |
@@ -4669,7 +4670,8 @@ void Engine::set_prior(const PriorState& p) {
             k_seed_rec<<<std::min<uint32_t>(d.ncells, 65536), 256, 0, stream_>>>(
                 d.cells, d.cell_slab0, d.slab_layer, d.slabs, d.ncells, reinterpret_cast<const float4*>(d_inj_),
                 level_geo(cfg_, (uint32_t)h), cell_size(cfg_.max_cell_size, (uint32_t)h), g.tx, g.ty,
-                (h + 2 < kMaxDepth) ? 1 : 0, d_inj_rec_);
+                (h + 2 < kMaxDepth) ? 1 : 0, getenv("PCC_NO_SEED_REC") ? 1u : 0u,   // (tests: every seed flagged)
+                d_inj_rec_);
         }
         HIP_CHECK(hipGetLastError());
         HIP_CHECK(hipStreamSynchronize(stream_));

@@ -55,6 +55,20 @@ def test_merge_clustered_deep():
     assert st["levels"] >= 3
 
 
+@pytest.mark.parametrize("seed", [3, 11, 29])
+def test_merge_with_every_seed_record_flagged(seed, monkeypatch):
+    """The grid seeds' slot-table records made at adoption (k_seed_rec) all
+    flagged (PCC_NO_SEED_REC): every seed goes through the kernels' own slot and
+    route arithmetic instead, with the same result (cell.rs:183-229)."""
+    monkeypatch.setenv("PCC_NO_SEED_REC", "1")
+    files, cfg, batch = _case(seed)
+    first, second = _split(files, seed)
+    _merge_check([_to_np(f) for f in first], [_to_np(f) for f in second], cfg=cfg, batch=batch)
+    a = synth(22, 1, 600_000)
+    b = synth(23, 1, 250_000)
+    _merge_check([a], [b], fast=True)
+
+
 def test_merge_small_limit_spills_kept_lists():
     """Tiny limit: existing Some lists spill in the merge, existing None buckets forward."""
     pts = synth(24, 0, 60_000, lo=-40.0, ext=80.0)
