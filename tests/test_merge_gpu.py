@@ -69,6 +69,19 @@ def test_merge_with_every_seed_record_flagged(seed, monkeypatch):
     _merge_check([a], [b], fast=True)
 
 
+@pytest.mark.parametrize("seed", [5, 17])
+def test_merge_with_bucket_resolution_in_two_launches(seed, monkeypatch):
+    """A merge (existing Some / None buckets, cell.rs:108-153) through the
+    two-launch bucket resolution, forced at every level (PCC_BKT_SPLIT_MIN=1)."""
+    monkeypatch.setenv("PCC_BKT_SPLIT_MIN", "1")
+    files, cfg, batch = _case(seed)
+    first, second = _split(files, seed)
+    _merge_check([_to_np(f) for f in first], [_to_np(f) for f in second], cfg=cfg, batch=batch)
+    pts = synth(24, 0, 60_000, lo=-40.0, ext=80.0)
+    cfg = dict(cell_point_overflow_limit=1500, sub_grid_dimension=6, max_cell_size=64.0)
+    _merge_check([pts[:20_000], pts[20_000:30_000]], [pts[30_000:]], cfg=cfg, batch=777)
+
+
 def test_merge_small_limit_spills_kept_lists():
     """Tiny limit: existing Some lists spill in the merge, existing None buckets forward."""
     pts = synth(24, 0, 60_000, lo=-40.0, ext=80.0)
