@@ -3197,12 +3197,46 @@ __device__ __forceinline__ void small_process(const SlabParams& P, SmallLds& S, 
 
     int32_t rec_e[CH];    // table entry of an arrival that became a slot record, else -1
     int32_t own_d[CH], own_g[CH];
+    // Merge: the whole chunks of grid seeds go straight into the table, from
+    // their records (k_seed_rec): one per slot and below every other key, they
+    // claim nothing and emit nothing (as in k_slab's merge mode); the chunk loop
+    // starts after them.
+    uint32_t ci0 = 0;
+    if (D.ng >= (uint32_t)BS) {
+        const uint32_t nfull = min(D.ng / (uint32_t)BS, (uint32_t)CH);
+        bool flagged = false;
+#pragma unroll
+        for (int c = 0; c < CH; c++)
+            if ((uint32_t)c < nfull) flagged |= (R.rh[c] >> 31) != 0u;
+        if (!__syncthreads_or(flagged)) {
+            ci0 = nfull;
+#pragma unroll
+            for (int c = 0; c < CH; c++) {
+                if ((uint32_t)c >= nfull) break;
+                const uint32_t j = c * BS + tid;
+                const uint32_t local = R.rh[c] & 0x3FFFu, dn = (R.rh[c] >> 14) & 31u;
+                own_d[c] = (int32_t)dn;
+                own_g[c] = (int32_t)((R.rh[c] >> 19) & 31u) - 1;
+                rec_e[c] = small_entry(S, local, mask);
+                if (rec_e[c] < 0) {
+                    err |= ERR_CLAIM;
+                } else {
+                    const unsigned long long mine =
+                        ((unsigned long long)R.rl[c] << 33) | ((unsigned long long)dn << kJBits) | j;
+                    // two grid points in one slot: not a cell a converter writes
+                    if (atomicCAS(&S.tab[rec_e[c]], kEmpty64, mine) != kEmpty64) err |= ERR_CLAIM;
+                }
+            }
+            __syncthreads();
+        }
+    }
     // emission of the previous chunk: kind (-1 none, 0 self, 1 displaced), occupant, child slab, grandchild
     int32_t em = -1, emg = -1;
     uint32_t emj = 0, emd = 0;
 #pragma unroll
     for (int ci = 0; ci <= CH; ci++) {
         if ((uint32_t)ci > nch) break;   // block-uniform
+        if ((uint32_t)ci < ci0) continue;   // whole chunks of grid seeds, installed above
         const uint32_t par = ci & 1;
         uint32_t* claim = S.claim[par];
         const bool have = ci < CH && (uint32_t)ci < nch;
