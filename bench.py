@@ -227,9 +227,15 @@ METRIC = "points/sec converted (octree+LOD build), 1B synthetic pts, 1/2/4/8 MI3
 
 
 def _latest_pmc():
-    """The newest round's committed PMC summary (profiles/rNN_pmc_traffic_1b.json)."""
+    """The newest round's committed PMC summary (profiles/rNN_pmc_traffic_1b.json),
+    its final-tree pass (rNN_final_pmc_traffic_1b.json) first."""
     import glob
-    c = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic_1b.json")))
+    import re as _re
+
+    def rank(path):
+        m = _re.match(r"r(\d+)", os.path.basename(path))
+        return (int(m.group(1)) if m else 0, "_final_" in os.path.basename(path), path)
+    c = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic_1b.json")), key=rank)
     return c[-1] if c else os.path.join(ROOT, "profiles", "r1_pmc_traffic_1b.json")
 
 
