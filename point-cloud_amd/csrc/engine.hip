@@ -3500,7 +3500,9 @@ __device__ __forceinline__ int wave_entry2(WL& W, uint32_t local, uint32_t mask)
 #ifndef PCC_WAVE_OCC
 #define PCC_WAVE_OCC 4   // k_slab_wave: minimum waves per SIMD asked of the compiler (<= 128 VGPRs, no spills)
 #endif
-template <int CH>
+// MRG: a merge level (seeds in place): whole chunks of grid seeds go into the
+// table from their records (k_seed_rec)
+template <int CH, bool MRG = false>
 __global__ __launch_bounds__(64, PCC_WAVE_OCC) void k_slab_wave(SlabParams P) {
     using WL = WaveLds<CH>;
     __shared__ WL W;
@@ -3520,16 +3522,24 @@ __global__ __launch_bounds__(64, PCC_WAVE_OCC) void k_slab_wave(SlabParams P) {
         const __amdgpu_buffer_rsrc_t oP = srd(P.nx.p + dbase, db * 4), oK = srd(P.nx.k + dbase, db);
         u32x4 pp[CH];
         uint32_t pk[CH];
+        // merge: whole chunks of grid seeds (nfull) hold their slot-table records
+        // (k_seed_rec) in pp.x / pp.y until pass 2 reloads their payloads
+        const uint32_t nfull = (MRG && D.pad1) ? min(D.ng / 64u, (uint32_t)CH) : 0u;
+        const __amdgpu_buffer_rsrc_t rS = srd(P.inj + D.pad0, (uint64_t)D.pad1 * 16);
         if (D.pad1) {   // merge: the seeds (arrivals 0 .. pad1-1) in place in the seed array
             const uint32_t ns = D.pad1;
-            const __amdgpu_buffer_rsrc_t rS = srd(P.inj + D.pad0, (uint64_t)ns * 16),
-                                         rT = srd(P.inj_keys + D.pad0, (uint64_t)ns * 4);
+            const __amdgpu_buffer_rsrc_t rT = srd(P.inj_keys + D.pad0, (uint64_t)ns * 4),
+                                         rR = srd(P.inj_rec + D.pad0, (uint64_t)D.ng * 8);
 #pragma unroll
             for (int c = 0; c < CH; c++) {
                 const uint32_t j = c * 64 + lane;
                 const bool v = j < n, sd = j < ns;
-                const u32x4 a = bld4(rS, sd ? j * 16 : 0xFFFFFFFFu), b = bld4(rP, (v && !sd) ? j * 16 : 0xFFFFFFFFu);
-                pp[c] = u32x4{a.x | b.x, a.y | b.y, a.z | b.z, a.w | b.w};
+                if (MRG && (uint32_t)c < nfull) {   // wave-uniform
+                    pp[c] = u32x4{bld(rR, j * 8), bld(rR, j * 8 + 4), 0u, 0u};
+                } else {
+                    const u32x4 a = bld4(rS, sd ? j * 16 : 0xFFFFFFFFu), b = bld4(rP, (v && !sd) ? j * 16 : 0xFFFFFFFFu);
+                    pp[c] = u32x4{a.x | b.x, a.y | b.y, a.z | b.z, a.w | b.w};
+                }
                 pk[c] = bld(rT, sd ? j * 4 : 0xFFFFFFFFu) | bld(rK, (v && !sd) ? j * 4 : 0xFFFFFFFFu);
             }
         } else {
@@ -3563,6 +3573,29 @@ __global__ __launch_bounds__(64, PCC_WAVE_OCC) void k_slab_wave(SlabParams P) {
             own[c] = 0u;
             if ((uint32_t)c >= nch) continue;   // wave-uniform
             const uint32_t j = c * 64 + lane;
+            if (MRG && (uint32_t)c < nfull) {   // merge: a whole chunk of grid seeds
+                if (!__ballot(pp[c].y >> 31)) {
+                    // straight into the table from their records: one per slot and
+                    // below every other key, they emit nothing (as k_slab's merge mode)
+                    const uint32_t rh = pp[c].y, local = rh & 0x3FFFu, dn = (rh >> 14) & 31u;
+                    own[c] = (dn << 11) | (((rh >> 19) & 31u) << 16);
+                    const int e = wave_entry2(W, local, mask);
+                    if (e < 0) {
+                        err |= ERR_CLAIM;
+                    } else {
+                        const unsigned long long occ =
+                            __hip_atomic_load(&W.tab[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                        if ((occ >> 33) != 0x7FFFFFFFull) err |= ERR_CLAIM;   // two grid points in one slot
+                        const unsigned long long mine = ((unsigned long long)pp[c].x << 33) |
+                                                        ((unsigned long long)dn << 28) |
+                                                        ((unsigned long long)local << 14) | j;
+                        __hip_atomic_store(&W.tab[e], mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                        own[c] |= (uint32_t)(e + 1);
+                    }
+                    continue;
+                }
+                pp[c] = bld4(rS, j * 16);   // flagged records: the seeds' own arithmetic below
+            }
             const bool valid = j < n;
             const float x = __uint_as_float(pp[c].x), y = __uint_as_float(pp[c].y), z = __uint_as_float(pp[c].z);
             const SlotDest sd = slot_dest(x, y, z, G, SC);
@@ -3657,7 +3690,13 @@ __global__ __launch_bounds__(64, PCC_WAVE_OCC) void k_slab_wave(SlabParams P) {
             wave_gcount(W, ok && em == 0 && g >= 0, (uint32_t)(dd * kDests + (g < 0 ? 0 : g)));
         }
         __syncthreads();
-        // pass 2 from registers: grid points and displaced payloads
+        // pass 2 from registers: grid points and displaced payloads (the
+        // record-installed seed chunks' payloads loaded again first)
+        if constexpr (MRG) {
+#pragma unroll
+            for (int c = 0; c < CH; c++)
+                if ((uint32_t)c < nfull) pp[c] = bld4(rS, (c * 64 + lane) * 16);
+        }
         const __amdgpu_buffer_rsrc_t rG = srd(P.grid + P.grid_off[s], (uint64_t)n * 16);
         uint32_t nwin = 0;
 #pragma unroll
@@ -6192,9 +6231,15 @@ int Engine::run_level(uint32_t li) {
             // CU slot to the next slab (a persistent grid of resident waves
             // walking the list was 1.6x slower at level 3 of config 4)
             const uint32_t gr = hcnt[c];
-            if (c == 0) k_slab_wave<kWaveMax / 256><<<gr, 64, 0, stream_>>>(SP);
-            else if (c == 1) k_slab_wave<kWaveMax / 128><<<gr, 64, 0, stream_>>>(SP);
-            else k_slab_wave<kWaveMax / 64><<<gr, 64, 0, stream_>>>(SP);
+            // (the record path pays for its pass-2 reload only in the largest class:
+            // config 5, 1.95 against 2.34 ms; the 128-255 class was 0.15 ms slower with it)
+            if (seeds_in_place && c == 2) {
+                k_slab_wave<kWaveMax / 64, true><<<gr, 64, 0, stream_>>>(SP);
+            } else {
+                if (c == 0) k_slab_wave<kWaveMax / 256><<<gr, 64, 0, stream_>>>(SP);
+                else if (c == 1) k_slab_wave<kWaveMax / 128><<<gr, 64, 0, stream_>>>(SP);
+                else k_slab_wave<kWaveMax / 64><<<gr, 64, 0, stream_>>>(SP);
+            }
         }
         if (hcnt[3]) {
             SP.sdesc = bd;
