@@ -3522,8 +3522,11 @@ __global__ __launch_bounds__(64, PCC_WAVE_OCC) void k_slab_wave(SlabParams P) {
         const __amdgpu_buffer_rsrc_t oP = srd(P.nx.p + dbase, db * 4), oK = srd(P.nx.k + dbase, db);
         u32x4 pp[CH];
         uint32_t pk[CH];
-        // merge: whole chunks of grid seeds (nfull) hold their slot-table records
-        // (k_seed_rec) in pp.x / pp.y until pass 2 reloads their payloads
+        // merge: whole chunks of grid seeds (nfull) take their slot-table records
+        // (k_seed_rec): beside the payloads when registers allow (KEEP), else in
+        // pp.x / pp.y until pass 2 reloads the payloads
+        constexpr bool KEEP = CH <= 4;
+        uint32_t rlo[KEEP ? CH : 1], rhi[KEEP ? CH : 1];
         const uint32_t nfull = (MRG && D.pad1) ? min(D.ng / 64u, (uint32_t)CH) : 0u;
         const __amdgpu_buffer_rsrc_t rS = srd(P.inj + D.pad0, (uint64_t)D.pad1 * 16);
         if (D.pad1) {   // merge: the seeds (arrivals 0 .. pad1-1) in place in the seed array
@@ -3534,9 +3537,13 @@ __global__ __launch_bounds__(64, PCC_WAVE_OCC) void k_slab_wave(SlabParams P) {
             for (int c = 0; c < CH; c++) {
                 const uint32_t j = c * 64 + lane;
                 const bool v = j < n, sd = j < ns;
-                if (MRG && (uint32_t)c < nfull) {   // wave-uniform
+                if (MRG && !KEEP && (uint32_t)c < nfull) {   // wave-uniform
                     pp[c] = u32x4{bld(rR, j * 8), bld(rR, j * 8 + 4), 0u, 0u};
                 } else {
+                    if constexpr (MRG && KEEP) {
+                        rlo[c] = (uint32_t)c < nfull ? bld(rR, j * 8) : 0u;
+                        rhi[c] = (uint32_t)c < nfull ? bld(rR, j * 8 + 4) : 0xFFFFFFFFu;
+                    }
                     const u32x4 a = bld4(rS, sd ? j * 16 : 0xFFFFFFFFu), b = bld4(rP, (v && !sd) ? j * 16 : 0xFFFFFFFFu);
                     pp[c] = u32x4{a.x | b.x, a.y | b.y, a.z | b.z, a.w | b.w};
                 }
@@ -3574,10 +3581,11 @@ __global__ __launch_bounds__(64, PCC_WAVE_OCC) void k_slab_wave(SlabParams P) {
             if ((uint32_t)c >= nch) continue;   // wave-uniform
             const uint32_t j = c * 64 + lane;
             if (MRG && (uint32_t)c < nfull) {   // merge: a whole chunk of grid seeds
-                if (!__ballot(pp[c].y >> 31)) {
+                const uint32_t rl = KEEP ? rlo[c] : pp[c].x, rh = KEEP ? rhi[c] : pp[c].y;
+                if (!__ballot(rh >> 31)) {
                     // straight into the table from their records: one per slot and
                     // below every other key, they emit nothing (as k_slab's merge mode)
-                    const uint32_t rh = pp[c].y, local = rh & 0x3FFFu, dn = (rh >> 14) & 31u;
+                    const uint32_t local = rh & 0x3FFFu, dn = (rh >> 14) & 31u;
                     own[c] = (dn << 11) | (((rh >> 19) & 31u) << 16);
                     const int e = wave_entry2(W, local, mask);
                     if (e < 0) {
@@ -3586,7 +3594,7 @@ __global__ __launch_bounds__(64, PCC_WAVE_OCC) void k_slab_wave(SlabParams P) {
                         const unsigned long long occ =
                             __hip_atomic_load(&W.tab[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
                         if ((occ >> 33) != 0x7FFFFFFFull) err |= ERR_CLAIM;   // two grid points in one slot
-                        const unsigned long long mine = ((unsigned long long)pp[c].x << 33) |
+                        const unsigned long long mine = ((unsigned long long)rl << 33) |
                                                         ((unsigned long long)dn << 28) |
                                                         ((unsigned long long)local << 14) | j;
                         __hip_atomic_store(&W.tab[e], mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
@@ -3594,7 +3602,7 @@ __global__ __launch_bounds__(64, PCC_WAVE_OCC) void k_slab_wave(SlabParams P) {
                     }
                     continue;
                 }
-                pp[c] = bld4(rS, j * 16);   // flagged records: the seeds' own arithmetic below
+                if constexpr (!KEEP) pp[c] = bld4(rS, j * 16);   // flagged records: the seeds' own arithmetic below
             }
             const bool valid = j < n;
             const float x = __uint_as_float(pp[c].x), y = __uint_as_float(pp[c].y), z = __uint_as_float(pp[c].z);
@@ -3692,7 +3700,7 @@ __global__ __launch_bounds__(64, PCC_WAVE_OCC) void k_slab_wave(SlabParams P) {
         __syncthreads();
         // pass 2 from registers: grid points and displaced payloads (the
         // record-installed seed chunks' payloads loaded again first)
-        if constexpr (MRG) {
+        if constexpr (MRG && !KEEP) {
 #pragma unroll
             for (int c = 0; c < CH; c++)
                 if ((uint32_t)c < nfull) pp[c] = bld4(rS, (c * 64 + lane) * 16);
@@ -6231,10 +6239,11 @@ int Engine::run_level(uint32_t li) {
             // CU slot to the next slab (a persistent grid of resident waves
             // walking the list was 1.6x slower at level 3 of config 4)
             const uint32_t gr = hcnt[c];
-            // (the record path pays for its pass-2 reload only in the largest class:
-            // config 5, 1.95 against 2.34 ms; the 128-255 class was 0.15 ms slower with it)
-            if (seeds_in_place && c == 2) {
-                k_slab_wave<kWaveMax / 64, true><<<gr, 64, 0, stream_>>>(SP);
+            // (merge levels: the classes of 128-511 arrivals install whole chunks of
+            // grid seeds from their records; the smallest class has few whole chunks)
+            if (seeds_in_place && c >= 1) {
+                if (c == 1) k_slab_wave<kWaveMax / 128, true><<<gr, 64, 0, stream_>>>(SP);
+                else k_slab_wave<kWaveMax / 64, true><<<gr, 64, 0, stream_>>>(SP);
             } else {
                 if (c == 0) k_slab_wave<kWaveMax / 256><<<gr, 64, 0, stream_>>>(SP);
                 else if (c == 1) k_slab_wave<kWaveMax / 128><<<gr, 64, 0, stream_>>>(SP);
