@@ -256,6 +256,19 @@ def pmc_traffic(workload):
     return pm["dense_kernel"]["hbm_bytes_per_launch"], os.path.relpath(PMC_SUMMARY, ROOT)
 
 
+def workload_name(args):
+    """BASELINE.json config label of a fresh build: configs 1/2/4 are the uniform
+    clouds of 100k / 10M / 1B points, config 3 the 100M Gaussian mixture; any
+    other size or kind is named by what it is."""
+    if args.kind == 0:
+        cfg = {100_000: "config1: ", 10_000_000: "config2: ", 1_000_000_000: "config4: "}.get(args.points, "")
+        return cfg + "%d uniform points in [-1000,1000)^3, seed %d" % (args.points, args.seed)
+    if args.kind == 2:
+        cfg = "config3: " if args.points == 100_000_000 else ""
+        return cfg + "%d Gaussian-mixture points (32 clusters, SURVEY 8d), seed %d" % (args.points, args.seed)
+    return "clustered blobs: %d points, seed %d" % (args.points, args.seed)
+
+
 def record(args, n_gpus, ms, st_levels, st_cells, st_slabs, arrivals, k, dense_ms, parallelism):
     """The one JSON line (rank 0).  roofline: dense slab kernel k_slab,
     algorithmic bytes = 32 B per arrival it processed over its
@@ -263,9 +276,7 @@ def record(args, n_gpus, ms, st_levels, st_cells, st_slabs, arrivals, k, dense_m
     dense_arr = k["dense_arrivals"]
     achieved = 32.0 * dense_arr / (dense_ms / 1e3) / 1e9 if dense_ms > 0 else 0.0
     whole = 32.0 * arrivals / (ms / 1e3) / 1e9
-    workload = {0: "config4: %d uniform points in [-1000,1000)^3, seed %d",
-                2: "config3: %d Gaussian-mixture points (32 clusters, SURVEY 8d), seed %d"}.get(
-        args.kind, "clustered blobs: %d points, seed %d") % (args.points, args.seed)
+    workload = workload_name(args)
     if args.merge_prior:
         workload = ("config5: +%d %s points (seed %d) merged into the %d-point config-4 cloud (seed 4)" %
                     (args.points, "uniform" if args.kind == 0 else "clustered", args.seed, args.merge_prior))
