@@ -2496,16 +2496,30 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
     uint32_t my_doff = bld(rDo, lane < kDests ? lane * 4 : 0xFFFFFFFFu);
     uint32_t my_dcap = bld(rDc, lane < kDests ? lane * 4 : 0xFFFFFFFFu);
 
+    // Slot of an arrival: computed one step ahead, in the phase B before the
+    // step that replays it (software pipelining: the arithmetic of chunk i+1
+    // fills the LDS latency chains of chunk i's emissions and list walks).
+    struct SlotInfo {
+        uint32_t local;   // slot table index (0 when not slotted)
+        float d2;         // distance to the slot centre
+        uint32_t dn;      // own child slab
+        int32_t gn;       // own grandchild slab
+        bool slotted;     // valid, layer and range ok
+        bool isn;         // NF: NaN distance
+        bool foreign;     // NF: NaN slot outside the table
+    };
     struct Stage {
         int32_t em;     // -1 none, 0 self, 1 displaced record / occupant
         uint32_t d;     // child slab of the emitted point
         int32_t g;      // its grandchild slab (-1 none, -2 unknown: wide slab, from gp)
-        int32_t hc;     // claim entry of a candidate (cleared one step later)
         u32x4 gp;       // gathered payload of a displaced point
+        SlotInfo si;    // slot of this stage's chunk (written one step before its replay)
     };
     Stage A;
-    A.em = -1; A.d = 0; A.g = -1; A.hc = -1;
+    A.em = -1; A.d = 0; A.g = -1;
     A.gp = u32x4{0u, 0u, 0u, 0u};
+    A.si.local = 0; A.si.d2 = 0.0f; A.si.dn = 0; A.si.gn = -1;
+    A.si.slotted = A.si.isn = A.si.foreign = false;
     Stage B = A;
     // Arrivals are prefetched two chunks ahead into a ring of four register
     // buffers: chunk i lives in buf[i % 4] from its load (step i-2) to its
@@ -2608,9 +2622,53 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
         }
         __syncthreads();
     }
-    STAMP(0);
     const uint32_t nchunks = (n - ng + BS - 1) / BS;
-    auto step = [&](uint32_t ci, Stage& cur, Stage& prv, const Pre& mine, const Pre& prvb, Pre& pf) {
+    // Slot, distance (hex.rs:67-85, 55-65) and own child / grandchild slab of
+    // chunk ci's arrival of this thread (payload c): everything of phase A that
+    // does not read the table.  Error codes only on the (never expected) failing
+    // lanes.  A NaN coordinate gives a NaN distance, which never compares less
+    // (cell.rs:77-80), and a NaN x or y gives the slot (0, 0) (hex.rs:67-85, NaN
+    // `as i32` = 0), which can lie outside this cell's table: a "foreign" slot
+    // only NaN points reach, so its first arrival is the grid point and every
+    // later one overflows (S.fj: the least such arrival; a min, so it may be
+    // taken one step early).
+    auto slot_info = [&](uint32_t ci, const Pre& c, SlotInfo& o) {
+        const uint32_t j = ng + ci * BS + tid;
+        const bool valid = j < n;
+        const float x = __uint_as_float(c.p.x), y = __uint_as_float(c.p.y), z = __uint_as_float(c.p.z);
+        bool amb = false;
+        SlotDest sd = slot_dest_fast(x, y, z, G, SC, amb);
+        if (__ballot(amb)) {
+            if (amb) slot_dest_exact(x, y, z, G, SC, sd);
+        }
+        const int32_t lx = sd.ox - rx, ly = sd.oy - ry;
+        const bool range_ok = lx >= 0 && ly >= 0 && lx < P.tx && ly < P.ty;
+        const bool layer_ok = sd.layer_ok;
+        o.slotted = valid && layer_ok && range_ok;
+        o.local = o.slotted ? (uint32_t)(ly * P.tx + lx) : 0u;
+        float X, Y, Z;
+        slot_centre(sd, G.cr, zt, X, Y, Z);
+        o.d2 = dist2(X, Y, Z, x, y, z);
+        o.isn = NF && o.d2 != o.d2;
+        o.foreign = false;
+        if constexpr (NF) {
+            if (__ballot(o.isn && valid && layer_ok && !range_ok)) {
+                o.foreign = o.isn && valid && layer_ok && !range_ok;
+                const bool forced = KF && valid && c.k - P.kf_lo < P.kf_n;
+                if (o.foreign && !forced) atomicMin(&S.fj, j);
+            }
+        }
+        const int d = sd.d;
+        o.gn = sd.g;
+        const bool bad = valid && (!layer_ok || (!range_ok && !o.foreign) || d < 0 || (P.check_gchild && o.gn < 0));
+        if (__ballot(bad)) {
+            if (bad) err |= slot_route_errs(slot_route(x, y, z, G), layer_ok, range_ok, cx, cy, cz, t, P.check_gchild);
+        }
+        o.dn = d < 0 ? 0u : (uint32_t)d;
+    };
+    if (nchunks) slot_info(0, pre[0], A.si);
+    STAMP(0);
+    auto step = [&](uint32_t ci, Stage& cur, Stage& prv, const Pre& mine, const Pre& prvb, const Pre& nxt, Pre& pf) {
         const uint32_t par = ci & 1;
         const uint32_t tag = ci & 31u;
         const uint32_t j = ng + ci * BS + tid;
@@ -2621,85 +2679,28 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
             pf.p = rP.p(jo * 16);
             pf.k = rP.k(jo * 4);
         }
-        // the claim entries of chunk i-1 (other parity) are dead since the last barrier
-        const u32x4 own = mine.p;
-        const float x = __uint_as_float(own.x), y = __uint_as_float(own.y), z = __uint_as_float(own.z);
-        // ---- phase A (1): slot + distance (hex.rs:67-85, 55-65) + own child / grandchild slab
-#ifdef PCC_STAMPS
-        if (own.x == 0x7FC00001u) err |= 1u << 30;   // consume the prefetched loads here
-        STAMP(12);
-#endif
-        SlotDest sd;
-        bool amb = false;
+        // ---- phase A (1): the slot's occupant and list head (the slot itself
+        // was computed in the last phase B; phase B of the last step wrote the
+        // table before the barrier; local 0 for lanes without a slot)
+        const uint32_t local = cur.si.local;
+        const bool slotted = cur.si.slotted;
+        unsigned long long occ = S.tab[local];
+        uint32_t hw = S.head[local >> 1];   // the slot's head word, read with the occupant
         // the last step pushes and walks nothing: the head words become the
         // winner bitmap over the arrivals (all ones; dense_grid_points)
         if (ci == nchunks && n <= kDenseStreamMax)
             for (int i = tid; i < (int)((n + 31) / 32); i += BS) S.head[i] = kEmpty32;
-        if (ci < nchunks) {   // block-uniform: the last step only emits
-            sd = slot_dest_fast(x, y, z, G, SC, amb);
-        } else {
-            sd.ox = sd.oy = sd.qa = 0;
-            sd.layer_ok = false;
-            sd.d = sd.g = -1;
-        }
-        int32_t lx = sd.ox - rx, ly = sd.oy - ry;
-        bool range_ok = lx >= 0 && ly >= 0 && lx < P.tx && ly < P.ty;
-        bool slotted = valid && sd.layer_ok && range_ok;
-        uint32_t local = slotted ? (uint32_t)(ly * P.tx + lx) : 0u;
-        // the slot's occupant, read before the rest of the arithmetic so the LDS
-        // latency overlaps it (phase B of the last step wrote the table before
-        // the barrier; local 0 for lanes without a slot)
-        unsigned long long occ = S.tab[local];
-        uint32_t hw = S.head[local >> 1];   // the slot's head word, read with the occupant
-        if (__ballot(amb)) {
-            if (amb) {
-                slot_dest_exact(x, y, z, G, SC, sd);
-                lx = sd.ox - rx;
-                ly = sd.oy - ry;
-                range_ok = lx >= 0 && ly >= 0 && lx < P.tx && ly < P.ty;
-                slotted = valid && sd.layer_ok && range_ok;
-                local = slotted ? (uint32_t)(ly * P.tx + lx) : 0u;
-                occ = S.tab[local];
-                hw = S.head[local >> 1];
-            }
-        }
-        const bool layer_ok = sd.layer_ok;
-        float X, Y, Z;
-        slot_centre(sd, G.cr, zt, X, Y, Z);
-        const float d2 = dist2(X, Y, Z, x, y, z);
-        // A NaN coordinate gives a NaN distance, which never compares less
-        // (cell.rs:77-80), and a NaN x or y gives the slot (0, 0) (hex.rs:67-85,
-        // NaN `as i32` = 0), which can lie outside this cell's table: a "foreign"
-        // slot only NaN points reach, so its first arrival is the grid point and
-        // every later one overflows.
-        const bool isn = NF && d2 != d2;
-        bool foreign = false;
-        if constexpr (NF) {
-            if (__ballot(isn && valid && layer_ok && !range_ok)) {
-                foreign = isn && valid && layer_ok && !range_ok;
-                if (foreign && !forced) atomicMin(&S.fj, j);
-            }
-        }
-        uint32_t dn;
-        int32_t gn;
-        {
-            const int d = sd.d;
-            gn = sd.g;
-            // error codes only on the (never expected) failing lanes
-            const bool bad = valid && (!layer_ok || (!range_ok && !foreign) || d < 0 || (P.check_gchild && gn < 0));
-            if (__ballot(bad)) {
-                if (bad) err |= slot_route_errs(slot_route(x, y, z, G), layer_ok, range_ok, cx, cy, cz, t, P.check_gchild);
-            }
-            dn = d < 0 ? 0u : (uint32_t)d;
-        }
+        const float d2 = cur.si.d2;
+        const bool isn = cur.si.isn, foreign = cur.si.foreign;
+        const uint32_t dn = cur.si.dn;
+        const int32_t gn = cur.si.gn;
 #ifdef PCC_STAMPS
-        if (d2 == 12345.0f) err |= 1u << 29;   // finish the math before the stamp
+        if (d2 == 12345.0f) err |= 1u << 29;
         STAMP(13);
 #endif
         // Occupant filter (cell.rs:80 strict <: ties keep the old point); the
         // candidates push themselves onto their slot's list.
         bool cand = false;
-        int hc = -1;
         uint32_t myprev = kNil;
         if (slotted && !forced) {
             cand = occ == kEmpty64 || d2 < __uint_as_float((uint32_t)(occ >> 33));
@@ -2782,31 +2783,39 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
         // same child slab before the chunk + in earlier waves + earlier lanes.
         {
             const uint32_t rp = par ^ 1;   // chunk i-1's parity
-            uint32_t pre_l = 0, tot_l = 0, base_l = 0;
-            int32_t room_l = 0;
-            if (lane < kDests) {   // byte sums of the wave counts: earlier waves, all waves
-                pre_l = S.dcur[rp][lane];
-                tot_l = pre_l;
-                uint32_t w[NW / 4];
-                if constexpr (NW == 16) {
-                    const u32x4 w4 = *reinterpret_cast<const u32x4*>(S.wcnt[lane]);
-                    w[0] = w4.x; w[1] = w4.y; w[2] = w4.z; w[3] = w4.w;
-                } else {
+            // byte sums of the wave counts: earlier waves, all waves.  Every lane
+            // reads (lanes >= 24 a copy of lane 0's row), so the reads are issued
+            // before the next chunk's slot arithmetic, which hides their latency.
+            const uint32_t ll = lane < kDests ? lane : 0u;
+            uint32_t pre_l = S.dcur[rp][ll];
+            uint32_t w[NW / 4];
+            if constexpr (NW == 16) {
+                const u32x4 w4 = *reinterpret_cast<const u32x4*>(S.wcnt[ll]);
+                w[0] = w4.x; w[1] = w4.y; w[2] = w4.z; w[3] = w4.w;
+            } else {
 #pragma unroll
-                    for (int k = 0; k < NW / 4; k++) w[k] = S.wcnt[lane][k];
-                }
-#pragma unroll
-                for (uint32_t k = 0; k < (uint32_t)NW / 4; k++) {
-                    const uint32_t nb = wv > 4 * k ? min(wv - 4 * k, 4u) : 0u;   // wave-uniform
-                    const uint32_t m = nb >= 4 ? 0xFFFFFFFFu : ((1u << (8 * nb)) - 1u);
-                    pre_l = __builtin_amdgcn_udot4(w[k] & m, 0x01010101u, pre_l, false);
-                    tot_l = __builtin_amdgcn_udot4(w[k], 0x01010101u, tot_l, false);
-                }
-                if (wv == 0) S.dcur[par][lane] = tot_l;
-                asm volatile("" : "+v"(my_doff));         // keeps the load's wait out of the prologue
-                base_l = my_doff - dbase + pre_l;         // this wave's first position in child slab `lane`
-                room_l = (int32_t)(my_dcap - pre_l);      // and the capacity left from there
+                for (int k = 0; k < NW / 4; k++) w[k] = S.wcnt[ll][k];
             }
+            // ---- the next chunk's slots (into the stage of chunk i-1, whose slot
+            // is dead; its emission fields are read below)
+            if (ci + 1 < nchunks) {   // block-uniform
+                slot_info(ci + 1, nxt, prv.si);
+            } else {
+                prv.si.local = 0; prv.si.d2 = 0.0f; prv.si.dn = 0; prv.si.gn = -1;
+                prv.si.slotted = prv.si.isn = prv.si.foreign = false;
+            }
+            uint32_t tot_l = pre_l;
+#pragma unroll
+            for (uint32_t k = 0; k < (uint32_t)NW / 4; k++) {
+                const uint32_t nb = wv > 4 * k ? min(wv - 4 * k, 4u) : 0u;   // wave-uniform
+                const uint32_t m = nb >= 4 ? 0xFFFFFFFFu : ((1u << (8 * nb)) - 1u);
+                pre_l = __builtin_amdgcn_udot4(w[k] & m, 0x01010101u, pre_l, false);
+                tot_l = __builtin_amdgcn_udot4(w[k], 0x01010101u, tot_l, false);
+            }
+            if (wv == 0 && lane < kDests) S.dcur[par][lane] = tot_l;
+            asm volatile("" : "+v"(my_doff));                   // keeps the load's wait out of the prologue
+            const uint32_t base_l = my_doff - dbase + pre_l;    // this wave's first position in child slab `lane`
+            const int32_t room_l = (int32_t)(my_dcap - pre_l);  // and the capacity left from there
             // both shuffles with every lane active (a bpermute from an inactive
             // lane reads nothing)
             const uint32_t pos = (uint32_t)__shfl((int)base_l, d, 64) + rw;
@@ -2900,38 +2909,40 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
         }
         if ((xv0 ^ xv1 ^ xv2 ^ xv3) == 0x9E3779B9u) err |= 1u << 27;
 #endif
+#ifdef PCC_XSALU
+        {   // Diagnostic: PCC_XSALU independent SALU per step in four chains
+            uint32_t xs0 = ci, xs1 = ci ^ 1u, xs2 = ci ^ 2u, xs3 = ci ^ 3u;
+#pragma unroll
+            for (int xq = 0; xq < PCC_XSALU / 4; xq++) {
+                asm volatile("s_add_u32 %0, %0, 0x9e37" : "+s"(xs0));
+                asm volatile("s_add_u32 %0, %0, 0x79b9" : "+s"(xs1));
+                asm volatile("s_add_u32 %0, %0, 0x3c6e" : "+s"(xs2));
+                asm volatile("s_add_u32 %0, %0, 0xf1bb" : "+s"(xs3));
+            }
+            if ((xs0 ^ xs1 ^ xs2 ^ xs3) == 0x9E3779B9u) err |= 1u << 26;
+        }
+#endif
         STAMP(4);
         STAMP_COUNT(9, 1);
         // gather outside the divergent branches (a load into registers that
         // another branch writes would force a full vmcnt drain); stored next step
         cur.gp = rP.p(gsrc);
-        cur.em = em; cur.d = emd; cur.g = emg; cur.hc = hc;
+        cur.em = em; cur.d = emd; cur.g = emg;
         lds_barrier();
         STAMP(5);
         STAMP_COUNT(10, 1);
     };
     // nchunks + 1 steps (the last one only emits).  Chunk i lives in
     // pre[i % (PF + 2)] from its load (step i - PF) to its emission store (step i + 1).
-    if constexpr (PF == 2) {
-        for (uint32_t ci = 0; ci <= nchunks; ci += 4) {
-            step(ci, A, B, pre[0], pre[3], pre[2]);
-            if (ci + 1 > nchunks) break;
-            step(ci + 1, B, A, pre[1], pre[0], pre[3]);
-            if (ci + 2 > nchunks) break;
-            step(ci + 2, A, B, pre[2], pre[1], pre[0]);
-            if (ci + 3 > nchunks) break;
-            step(ci + 3, B, A, pre[3], pre[2], pre[1]);
-        }
-    } else {
-        static_assert(PF == 3, "prefetch depth 2 or 3");
-        for (uint32_t ci = 0; ci <= nchunks; ci += 10) {
-#define PCC_STEP10(k, X, Y)                                                    \
-    if (ci + (k) > nchunks) break;                                             \
-    step(ci + (k), X, Y, pre[(k) % 5], pre[((k) + 4) % 5], pre[((k) + 3) % 5]);
-            PCC_STEP10(0, A, B) PCC_STEP10(1, B, A) PCC_STEP10(2, A, B) PCC_STEP10(3, B, A) PCC_STEP10(4, A, B)
-            PCC_STEP10(5, B, A) PCC_STEP10(6, A, B) PCC_STEP10(7, B, A) PCC_STEP10(8, A, B) PCC_STEP10(9, B, A)
-#undef PCC_STEP10
-        }
+    static_assert(PF == 2, "prefetch depth 2: a ring of four chunks");
+    for (uint32_t ci = 0; ci <= nchunks; ci += 4) {
+        step(ci, A, B, pre[0], pre[3], pre[1], pre[2]);
+        if (ci + 1 > nchunks) break;
+        step(ci + 1, B, A, pre[1], pre[0], pre[2], pre[3]);
+        if (ci + 2 > nchunks) break;
+        step(ci + 2, A, B, pre[2], pre[1], pre[3], pre[0]);
+        if (ci + 3 > nchunks) break;
+        step(ci + 3, B, A, pre[3], pre[2], pre[0], pre[1]);
     }
     STAMP(7);
     lds_barrier();   // LDS only: the last emission stores need not land
