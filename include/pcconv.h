@@ -236,8 +236,20 @@ int pcc_shard_plan_search(const double* whole_w, const uint64_t* slab_off, const
 int pcc_synth_device(pcc_point* dst, uint64_t first, uint64_t n, uint64_t seed, int kind, float lo, float extent,
                      int device);
 
-/* Local bounding box of n device points (bounding-volume/src/lib.rs:23-52). */
+/* Local bounding box of n device points (bounding-volume/src/lib.rs:23-52).
+ * -EDOM when a coordinate is NaN or infinite: use pcc_shard_bbox_nonfinite. */
 int pcc_shard_bbox(const pcc_point* dev_pts, uint64_t n, float bmin[3], float bmax[3], int device);
+/* The same for an input with NaN / infinite coordinates, as 15 values to
+ * all-reduce: parts[0..2] / [3..5] min / max over the non-NaN values (f32::min /
+ * max skip NaN and keep infinities, bounding-volume/src/lib.rs:23-31);
+ * parts[6..8] 1 where the axis has a non-NaN value (else the reference's box
+ * stays NaN there); parts[9..11] / [12..14] min / max over the points without an
+ * infinite coordinate, NaN taken as 0: the extent of the level-0 cells those
+ * points enter (metadata.rs:100-102, `as i32` maps NaN to 0), i.e. the grid the
+ * ownership plan needs.  A point with an infinite coordinate enters no grid
+ * cell: the histograms and routes below count and send it with unit 0, so one
+ * rank builds every such point (their cells meet no finite point's). */
+int pcc_shard_bbox_nonfinite(const pcc_point* dev_pts, uint64_t n, float parts[15], int device);
 
 /* Points per level-0 cell of the grid (dev_hist: dims.x*dims.y*dims.z u32). */
 int pcc_shard_histogram(const pcc_point* dev_pts, uint64_t n, const pcc_shard_grid* g, uint32_t* dev_hist, int device);
@@ -273,6 +285,9 @@ int pcc_shard_route_slabs(const pcc_point* dev_pts, uint64_t n, uint32_t key0, c
 int pcc_shard_bbox_histogram(const pcc_point* dev_pts, uint64_t n, const pcc_shard_grid* guess,
                              uint32_t sub_grid_dimension, uint32_t* dev_hist, float bmin[3], float bmax[3],
                              uint64_t* outside, int device);
+/* -EDOM (pcc_shard_bbox_histogram, pcc_shard_bbox_sample): NaN or infinite
+ * coordinates; the caller takes pcc_shard_bbox_nonfinite and histograms the
+ * true grid (an infinite point is outside every guessed grid). */
 /* Bounding box of a sample of the points (512 tiles of 3 072): the guess. */
 int pcc_shard_bbox_sample(const pcc_point* dev_pts, uint64_t n, float bmin[3], float bmax[3], int device);
 
@@ -301,6 +316,12 @@ int pcc_shard_route_bitmaps_hist(const pcc_point* dev_pts, uint64_t n, const pcc
  * set bits (= received points), else -EBADMSG. */
 int pcc_shard_keys_from_bitmaps(const uint64_t* dev_bitmaps, const uint64_t* nwords, const uint64_t* key0,
                                 uint32_t nsrc, uint32_t* dev_keys, uint64_t nkeys, int device);
+/* The rank-local start of every global batch: local[b] = the received points
+ * (the senders' rows of dev_bitmaps as in pcc_shard_keys_from_bitmaps) whose
+ * global key is below gstarts[b] (host arrays of nb, gstarts ascending; global
+ * keys are 64-bit here, so clouds of 2^32 points and more shard). */
+int pcc_shard_batch_starts(const uint64_t* dev_bitmaps, const uint64_t* nwords, const uint64_t* key0, uint32_t nsrc,
+                           const uint64_t* gstarts, uint64_t nb, uint64_t* local, int device);
 
 /* Writes one cell file h_{hierarchy}/c_x_y_z.bin under out_dir from a view
  * (Cell::write_to cell.rs:155-181): a cell assembled by the caller from the
@@ -310,6 +331,17 @@ int pcc_write_cell_view(const char* out_dir, const pcc_cell_view* v);
 /* Global file structure (points per input file, CLI order; lib.rs:31-52
  * batching) without points.  Switches the converter to keyed input. */
 int pcc_declare_files(pcc_converter* c, const uint64_t* file_points, uint64_t nfiles);
+/* Rank-local keys (a sharded rank's input of any global size, 2^32 points and
+ * beyond): instead of global keys and the declared files, the event batch
+ * (lib.rs:31-52: the get_batch counter, across files) of each input point i is
+ * batches[k] for the last k with starts[k] <= i.  starts[0] = 0, starts and
+ * batches strictly ascending (one entry per global batch holding some of this
+ * rank's points); total_batches = the global batch count (empty ones included).
+ * The input then comes from pcc_set_keyed_points_device with dev_keys = NULL
+ * (the rank's points in global key order; keys are their indices).  The table
+ * from the exchange bitmaps: pcc_shard_batch_starts. */
+int pcc_set_event_table(pcc_converter* c, const uint64_t* starts, const uint32_t* batches, uint64_t n,
+                        uint64_t total_batches);
 
 /* This rank's points (device memory) with their global keys, ascending. */
 int pcc_add_keyed_points_device(pcc_converter* c, const pcc_point* dev_pts, const uint32_t* dev_keys, uint64_t n);

@@ -625,7 +625,23 @@ int pcc_shard_bbox(const pcc_point* d, uint64_t n, float bmin[3], float bmax[3],
     if ((!d && n) || !bmin || !bmax) return set_err(-EINVAL, "null argument");
     GUARD_BEGIN
     const int rc = shard_bbox(reinterpret_cast<const Point*>(d), n, bmin, bmax, device);
-    return rc ? set_err(rc, "input contains NaN or infinite coordinates (unsupported)") : 0;
+    return rc ? set_err(rc, "input contains NaN or infinite coordinates (pcc_shard_bbox_nonfinite)") : 0;
+    GUARD_END
+}
+
+int pcc_shard_batch_starts(const uint64_t* dbm, const uint64_t* nwords, const uint64_t* key0, uint32_t nsrc,
+                           const uint64_t* gstarts, uint64_t nb, uint64_t* local, int device) {
+    if (!nwords || !key0 || ((!gstarts || !local) && nb)) return set_err(-EINVAL, "null argument");
+    GUARD_BEGIN
+    const int rc = shard_batch_starts(dbm, nwords, key0, nsrc, gstarts, nb, local, device);
+    return rc ? set_err(rc, "batch starts: 1..64 senders in key order, ascending batch starts") : 0;
+    GUARD_END
+}
+
+int pcc_shard_bbox_nonfinite(const pcc_point* d, uint64_t n, float parts[15], int device) {
+    if ((!d && n) || !parts) return set_err(-EINVAL, "null argument");
+    GUARD_BEGIN
+    return shard_bbox_nonfinite(reinterpret_cast<const Point*>(d), n, parts, device);
     GUARD_END
 }
 
@@ -668,8 +684,8 @@ int pcc_shard_bbox_histogram(const pcc_point* d, uint64_t n, const pcc_shard_gri
     GUARD_BEGIN
     const int rc = shard_bbox_histogram(reinterpret_cast<const Point*>(d), n, to_grid(g), sub_grid_dimension, dhist,
                                         bmin, bmax, outside, device);
-    return rc ? set_err(rc, rc == -EINVAL ? "input contains NaN or infinite coordinates (unsupported)"
-                                          : "histogram grid too large") : 0;
+    return rc ? set_err(rc, rc == -EDOM ? "input contains NaN or infinite coordinates (pcc_shard_bbox_nonfinite)"
+                                        : "histogram grid too large") : 0;
     GUARD_END
 }
 
@@ -677,7 +693,7 @@ int pcc_shard_bbox_sample(const pcc_point* d, uint64_t n, float bmin[3], float b
     if ((!d && n) || !bmin || !bmax) return set_err(-EINVAL, "null argument");
     GUARD_BEGIN
     const int rc = shard_bbox_sample(reinterpret_cast<const Point*>(d), n, bmin, bmax, device);
-    return rc ? set_err(rc, "sample holds NaN or infinite coordinates") : 0;
+    return rc ? set_err(rc, "sample box not finite (NaN or infinite coordinates)") : 0;
     GUARD_END
 }
 
@@ -776,6 +792,18 @@ int pcc_declare_files(pcc_converter* c, const uint64_t* file_points, uint64_t nf
     if (tot > (1ull << 32)) return set_err(-EOVERFLOW, "global keys must fit in 32 bits");
     GUARD_BEGIN
     c->eng->declare_files(file_points, nfiles, c->opt.batch_size);
+    c->keyed = true;
+    return 0;
+    GUARD_END
+}
+
+int pcc_set_event_table(pcc_converter* c, const uint64_t* starts, const uint32_t* batches, uint64_t n,
+                        uint64_t total_batches) {
+    if (!c || ((!starts || !batches) && n)) return set_err(-EINVAL, "null argument");
+    if (c->built) return set_err(-EINVAL, "event table after build");
+    if (total_batches > 0xFFFFFFFFull) return set_err(-EOVERFLOW, "more than 2^32-1 batches");
+    GUARD_BEGIN
+    c->eng->set_event_table(starts, batches, n, total_batches);
     c->keyed = true;
     return 0;
     GUARD_END

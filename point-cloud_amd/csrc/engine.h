@@ -152,6 +152,8 @@ struct PriorState {
     HostVec<uint32_t> inj_keys;
     std::vector<uint64_t> forced_lo;                   // per prior level
     std::vector<PriorLevel> levels;
+    bool has_nan = false;                              // some seed has a NaN coordinate (the NaN slot rules apply)
+    float max_abs = 0.f;                               // largest |finite coordinate| of a seed
 };
 
 struct StageProfile {
@@ -201,6 +203,10 @@ public:
     // add_keyed_device() appends this shard's points with their global input
     // indices (keys, ascending).  Event batches come from the global table.
     void declare_files(const uint64_t* file_points, uint64_t nfiles, uint32_t batch);
+    // Rank-local keys: input point i (a borrowed or added device input in key
+    // order, keys = indices) belongs to event batch eb[k] for the last k with
+    // starts[k] <= i; total_batches = the global batch count (lib.rs:31-52).
+    void set_event_table(const uint64_t* starts, const uint32_t* eb, uint64_t n, uint64_t total_batches);
     void add_keyed_device(const Point* dpts, const uint32_t* dkeys, uint64_t n);
     // Zero-copy variant: the build reads this shard's n points and keys straight
     // from caller memory (e.g. the buffers an exchange received into), which must
@@ -335,6 +341,8 @@ private:
     bool prior_ = false;
     Point* d_seeds_ = nullptr;           // level-0 seeds (key order)
     uint64_t nseeds0_ = 0;
+    bool prior_nan_ = false;      // a seed has a NaN coordinate: the slab kernels' NaN rules apply
+    float prior_max_abs_ = 0.f;   // largest |finite coordinate| of a seed
     uint64_t nseeds_ = 0;                // S (all levels)
     Point* d_inj_ = nullptr;             // level >= 1 seeds, grouped by slab
     uint32_t* d_inj_keys_ = nullptr;
@@ -357,6 +365,7 @@ private:
     uint64_t keys_cap_ = 0;
     bool keyed_ = false;
     uint64_t declared_total_ = 0;        // keyed input: global points of the declared files
+    bool event_table_ = false;            // set_event_table: file_* hold the rank-local batch table
     Dev* dev_ = nullptr;
     std::vector<Level*> levels_;
     float bmin_[3] = {0, 0, 0}, bmax_[3] = {0, 0, 0};
@@ -392,6 +401,9 @@ struct ShardGrid {
 };
 int shard_synth(Point* dst, uint64_t idx0, uint64_t n, uint64_t seed, int kind, float lo, float ext, int device);
 int shard_bbox(const Point* d, uint64_t n, float bmin[3], float bmax[3], int device);
+int shard_bbox_nonfinite(const Point* d, uint64_t n, float parts[15], int device);
+int shard_batch_starts(const uint64_t* dbm, const uint64_t* nwords, const uint64_t* key0, uint32_t nsrc,
+                       const uint64_t* gstarts, uint64_t nb, uint64_t* local, int device);
 // dim > 0: slab mode, unit = cell * 256 + level-0 hex z-layer of a dim sub-grid
 int shard_histogram(const Point* d, uint64_t n, const ShardGrid& g, uint32_t* dhist, int device, uint32_t dim = 0);
 // one pass: local bbox + histogram over a guessed grid (points outside it counted)

@@ -2585,7 +2585,11 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
             const float d2 = dist2(X, Y, Z, x, y, z);
             const int d = sd.d;
             int32_t gn = sd.g;
-            const bool bad = v && (!layer_ok || !range_ok || d < 0 || (P.check_gchild && gn < 0));
+            // a NaN grid seed in the foreign slot (0, 0) outside the table holds it
+            const bool foreign = NF && v && layer_ok && !range_ok && d2 != d2;
+            if constexpr (NF)
+                if (foreign) atomicMin(&S.fj, jg);
+            const bool bad = v && (!layer_ok || (!range_ok && !foreign) || d < 0 || (P.check_gchild && gn < 0));
             if (__ballot(bad)) {
                 if (bad) err |= slot_route_errs(slot_route(x, y, z, G), layer_ok, range_ok, cx, cy, cz, t, P.check_gchild);
             }
@@ -2914,10 +2918,10 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
             uint32_t xs0 = ci, xs1 = ci ^ 1u, xs2 = ci ^ 2u, xs3 = ci ^ 3u;
 #pragma unroll
             for (int xq = 0; xq < PCC_XSALU / 4; xq++) {
-                asm volatile("s_add_u32 %0, %0, 0x9e37" : "+s"(xs0));
-                asm volatile("s_add_u32 %0, %0, 0x79b9" : "+s"(xs1));
-                asm volatile("s_add_u32 %0, %0, 0x3c6e" : "+s"(xs2));
-                asm volatile("s_add_u32 %0, %0, 0xf1bb" : "+s"(xs3));
+                asm volatile("s_add_u32 %0, %0, 0x9e37" : "+s"(xs0) : : "scc");
+                asm volatile("s_add_u32 %0, %0, 0x79b9" : "+s"(xs1) : : "scc");
+                asm volatile("s_add_u32 %0, %0, 0x3c6e" : "+s"(xs2) : : "scc");
+                asm volatile("s_add_u32 %0, %0, 0xf1bb" : "+s"(xs3) : : "scc");
             }
             if ((xs0 ^ xs1 ^ xs2 ^ xs3) == 0x9E3779B9u) err |= 1u << 26;
         }
@@ -4628,6 +4632,22 @@ void Engine::declare_files(const uint64_t* file_points, uint64_t nfiles, uint32_
     keyed_ = true;
 }
 
+void Engine::set_event_table(const uint64_t* starts, const uint32_t* eb, uint64_t n, uint64_t total_batches) {
+    if (!file_start_.empty()) throw std::runtime_error("event table after declared files or input");
+    for (uint64_t k = 0; k < n; k++) {
+        if (k && !(starts[k] > starts[k - 1] && eb[k] > eb[k - 1]))
+            throw std::runtime_error("event table: starts and batches must ascend");
+        if (eb[k] >= total_batches) throw std::runtime_error("event table: batch beyond the batch count");
+        file_start_.push_back(starts[k]);
+        file_eb0_.push_back(eb[k]);
+        file_batch_.push_back(0x7FFFFFFFu);   // (i - start) / batch = 0: one batch per entry
+    }
+    if (n && starts[0] != 0) throw std::runtime_error("event table: the first entry must start at point 0");
+    nbatches_ = total_batches;
+    event_table_ = true;
+    keyed_ = true;
+}
+
 void Engine::set_keyed_external(const Point* dpts, const uint32_t* dkeys, uint64_t n) {
     if (n_ || !keyed_) throw std::runtime_error("borrowed keyed input needs declared files and no other input");
     if (n >= 0xFFFFFFFFull) throw std::runtime_error("more than 2^32-1 points per build are not supported");
@@ -4638,6 +4658,7 @@ void Engine::set_keyed_external(const Point* dpts, const uint32_t* dkeys, uint64
 }
 
 void Engine::add_keyed_device(const Point* dpts, const uint32_t* dkeys, uint64_t n) {
+    if (event_table_) throw std::runtime_error("keyed points after an event table (keys are the indices there)");
     reserve(n_ + n);
     if (keys_cap_ < n_ + n) {
         uint32_t* k = nullptr;
@@ -4737,6 +4758,8 @@ void Engine::set_prior(const PriorState& p) {
     free_prior();
     nseeds_ = p.nseeds;
     nseeds0_ = p.seeds0.size();
+    prior_nan_ = p.has_nan;
+    prior_max_abs_ = p.max_abs;
     d_seeds_ = upload(p.seeds0);
     d_inj_ = upload(p.inj);
     d_inj_keys_ = upload(p.inj_keys);
@@ -4784,6 +4807,7 @@ void Engine::clear_input() {
     ext_in_ = nullptr;
     ext_keys_ = nullptr;
     declared_total_ = 0;
+    event_table_ = false;
     built_ = false;
     pre0_reset();
 }
@@ -4814,6 +4838,11 @@ int Engine::build() {
     // cloud's points come first as "seeds" with keys 0 .. S-1, so every one of
     // them precedes every new point in key order, then the new points with keys
     // S + i.  All seeds belong to a pseudo batch 0 before the new batches.
+    if (event_table_) {   // rank-local keys: a borrowed input whose keys are its indices
+        if (n_ && (!ext_in_ || ext_keys_)) return fail(-22, "event table: the input must be borrowed without keys");
+        if (n_ && (file_start_.empty() || file_start_.back() >= n_))
+            return fail(-22, "event table: an entry starts past the input");
+    }
     if (prior_ && keyed_ && nseeds_ + declared_total_ >= 0xFFFFFFFFull)   // keys S + global key (k_comb_keys)
         return fail(-75, "sharded merge: this rank's existing points plus the global new points exceed 2^32-1 keys");
     if (prior_) {   // level-0 input: the level-0 seeds (keys 0 .. n0-1), then the new points (S + key)
@@ -5411,12 +5440,13 @@ __global__ __launch_bounds__(64) void k_inf_build(InfBufs B) {
 // there are none), the extent of the cells the points without an infinite
 // coordinate enter (NaN as 0), and, if some coordinate is infinite, those
 // points split off from the rest with their keys (the rest are rebinned as
-// keyed input).  Plain builds only: a merge, a keyed (sharded) input and a
-// level-range build return an error as before.
+// keyed input).  Plain builds, merges (the existing cloud's seeds take part
+// like any point; an existing cloud never has infinite coordinates: its
+// metadata.json box would be null, which neither the reference nor pcc_open
+// reads back) and keyed (sharded) builds; a level-range build returns an error.
 int Engine::enter_nonfinite(uint32_t flags) {
-    if (prior_ || keyed_ || ext_in_ || h0_ || max_levels_)
-        return fail(-22, "input contains NaN or infinite coordinates (supported in plain builds only, not in merges, "
-                         "sharded or level-range builds)");
+    if (h0_ || max_levels_)
+        return fail(-22, "input contains NaN or infinite coordinates (not supported in level-range builds)");
     const uint32_t nb = (uint32_t)std::min<uint64_t>(std::max<uint64_t>((nsrc_ + 255) / 256, 1), kBBoxBlocks);
     float* part = static_cast<float*>(dev_->get((uint64_t)nb * kNfParts * 4));
     k_bbox_nf<<<nb, 256, 0, stream_>>>(src_, nsrc_, part);
@@ -5472,10 +5502,11 @@ int Engine::build_infinite() {
     side_.clear();
     if (ninf_ == 0) return 0;
     if (ninf_ > kInfMax) return fail(-22, "more than 2^18 points with infinite coordinates in one build are not supported");
-    if (nsrc_) {
-        float m = 0.f;
-        for (int a = 0; a < 3; a++) m = std::max(m, std::max(std::fabs(gmin_[a]), std::fabs(gmax_[a])));
-        const uint32_t hl = h0_ + (uint32_t)std::max<size_t>(levels_.size(), 1) - 1;
+    if (nsrc_ || (prior_ && nseeds_)) {
+        float m = prior_ ? prior_max_abs_ : 0.f;   // a merge: every existing cell too
+        if (nsrc_)
+            for (int a = 0; a < 3; a++) m = std::max(m, std::max(std::fabs(gmin_[a]), std::fabs(gmax_[a])));
+        const uint32_t hl = h0_ + (uint32_t)std::max<size_t>(std::max<size_t>(levels_.size(), prior_ ? pdev_.size() : 0), 1) - 1;
         if (!(m / cell_size(cfg_.max_cell_size, hl) < 1.0e9f))
             return fail(-22, "finite coordinates that saturate a cell index mixed with infinite ones are not supported");
     }
@@ -6214,9 +6245,13 @@ int Engine::run_level(uint32_t li) {
         SP.stamps = stamps;
 #endif
         ev_begin(ST_DENSE);
-        if (seeds_in_place) k_slab<true, false, true><<<L->nbig, kDenseBS, 0, stream_>>>(SP);
+        // NaN rules: NaN input points, or NaN seeds of the existing cloud
+        const bool nf = nf_mode_ || (prior_ && prior_nan_);
+        if (seeds_in_place && nf) k_slab<true, true, true><<<L->nbig, kDenseBS, 0, stream_>>>(SP);
+        else if (seeds_in_place) k_slab<true, false, true><<<L->nbig, kDenseBS, 0, stream_>>>(SP);
+        else if (SP.kf_n && nf) k_slab<false, true, true><<<L->nbig, kDenseBS, 0, stream_>>>(SP);
         else if (SP.kf_n) k_slab<false, false, true><<<L->nbig, kDenseBS, 0, stream_>>>(SP);
-        else if (nf_mode_) k_slab<false, true, false><<<L->nbig, kDenseBS, 0, stream_>>>(SP);
+        else if (nf) k_slab<false, true, false><<<L->nbig, kDenseBS, 0, stream_>>>(SP);
         else k_slab<false, false, false><<<L->nbig, kDenseBS, 0, stream_>>>(SP);
         ev_end(ST_DENSE);
         if (verbose) {
@@ -6641,6 +6676,7 @@ struct ShardScratch {
     uint32_t* buf[4] = {nullptr, nullptr, nullptr, nullptr};
     uint64_t cap = 0;
     float* part = nullptr;
+    float* nfpart = nullptr;   // shard_bbox_nonfinite's per-block partials
     uint32_t* flag = nullptr;
     uint32_t* cnt = nullptr;
     uint64_t* tab = nullptr;
@@ -6649,7 +6685,7 @@ struct ShardScratch {
     SortTemp sort;
     ~ShardScratch() {
         for (auto* b : buf) (void)hipFree(b);
-        (void)hipFree(part); (void)hipFree(flag); (void)hipFree(cnt); (void)hipFree(tab); (void)hipFree(rt);
+        (void)hipFree(part); (void)hipFree(nfpart); (void)hipFree(flag); (void)hipFree(cnt); (void)hipFree(tab); (void)hipFree(rt);
         (void)hipFree(sort.counts); (void)hipFree(sort.scan.bsums);
         if (st) (void)hipStreamDestroy(st);
     }
@@ -6670,6 +6706,12 @@ ShardScratch& shard_scratch(int device) {
     return *t_shard;
 }
 
+// A point with an infinite coordinate (its cells saturate, metadata.rs:100-102,
+// and meet no finite point's: Engine::build_infinite) belongs to no grid cell;
+// with inf0 it is routed with unit 0, so that one rank builds all of them.
+__device__ __forceinline__ bool has_inf(float x, float y, float z) {
+    return isinf(x) || isinf(y) || isinf(z);
+}
 __device__ __forceinline__ uint32_t shard_cell(const ShardGrid& g, float x, float y, float z) {
     const int32_t ix = cell_index1(x, g.cs) - g.lo[0], iy = cell_index1(y, g.cs) - g.lo[1], iz = cell_index1(z, g.cs) - g.lo[2];
     const bool in = ix >= 0 && iy >= 0 && iz >= 0 && (uint32_t)ix < g.dims[0] && (uint32_t)iy < g.dims[1] && (uint32_t)iz < g.dims[2];
@@ -6683,7 +6725,9 @@ struct ShardSlabs {
     float cr;        // level-0 hex radius (0: cell mode)
     int32_t dim2;    // 2 * sub_grid_dimension
 };
+template <bool INF0 = true>
 __device__ __forceinline__ uint32_t shard_unit(const ShardGrid& g, const ShardSlabs& m, float x, float y, float z) {
+    if (has_inf(x, y, z)) return INF0 ? 0u : 0xFFFFFFFFu;
     const uint32_t c = shard_cell(g, x, y, z);
     if (m.dim2 == 0 || c == 0xFFFFFFFFu) return c;
     const int32_t iz = cell_index1(z, g.cs);
@@ -6727,7 +6771,9 @@ __global__ __launch_bounds__(kShBS) void k_shard_hist(const Point* __restrict__ 
                 mn[0] = fminf(mn[0], v[u].x); mn[1] = fminf(mn[1], v[u].y); mn[2] = fminf(mn[2], v[u].z);
                 mx[0] = fmaxf(mx[0], v[u].x); mx[1] = fmaxf(mx[1], v[u].y); mx[2] = fmaxf(mx[2], v[u].z);
             }
-            const uint32_t c = shard_unit(g, m, v[u].x, v[u].y, v[u].z);
+            // the fused pass over a guessed grid counts an infinite point as
+            // outside it (the caller then histograms the true grid)
+            const uint32_t c = shard_unit<!BBOX>(g, m, v[u].x, v[u].y, v[u].z);
             if (c == 0xFFFFFFFFu) { nbad++; continue; }
             if (lds) atomicAdd(&h[c], 1u); else wave_aggregated_add(hist, c);
         }
@@ -6995,6 +7041,29 @@ __global__ void k_bm_keys(const unsigned long long* __restrict__ bm, uint32_t nw
     }
 }
 
+// Rank-local start of global batch start key gs[i]: the received points with a
+// smaller global key (senders in rank = key order; wstart[s] = the first word of
+// sender s's row, wstart[nsrc] = nw; pos = exclusive word popcount prefix,
+// *total its sum).
+__global__ void k_bm_starts(const unsigned long long* __restrict__ bm, const uint32_t* __restrict__ pos,
+                            const uint32_t* __restrict__ total, const uint64_t* __restrict__ wstart,
+                            const uint64_t* __restrict__ key0, uint32_t nsrc, const uint64_t* __restrict__ gs,
+                            uint64_t nb, uint64_t* __restrict__ out) {
+    const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i >= nb) return;
+    const uint64_t g = gs[i];
+    const uint32_t nw = (uint32_t)wstart[nsrc];
+    auto at = [&](uint64_t w) -> uint64_t { return w < nw ? pos[w] : *total; };
+    if (nsrc == 0 || g < key0[0]) { out[i] = 0; return; }
+    uint32_t s = 0;
+    while (s + 1 < nsrc && key0[s + 1] <= g) s++;
+    const uint64_t off = g - key0[s], w = off >> 6, ws = wstart[s], we = wstart[s + 1];
+    if (ws + w >= we) { out[i] = at(we); return; }   // past sender s's points
+    const uint32_t b = (uint32_t)(off & 63u);
+    const unsigned long long below = b ? (bm[ws + w] & ((1ull << b) - 1ull)) : 0ull;
+    out[i] = at(ws + w) + (uint64_t)__popcll(below);
+}
+
 // ---- shared cells' overflow buckets, resolved over every rank's emissions
 // (cell.rs:108-153; the numpy statement is pcconv/dist.py::resolve_bucket).
 // Emissions arrive in segments (a cell's arrivals from one rank: sorted runs per
@@ -7224,6 +7293,47 @@ int shard_keys_from_bitmaps(const uint64_t* dbm, const uint64_t* nwords, const u
     return total == nkeys ? 0 : -EBADMSG;
 }
 
+int shard_batch_starts(const uint64_t* dbm, const uint64_t* nwords, const uint64_t* key0, uint32_t nsrc,
+                       const uint64_t* gstarts, uint64_t nb, uint64_t* local, int device) {
+    ShardScratch& S = shard_scratch(device);
+    if (nsrc == 0 || nsrc > 64) return -EINVAL;
+    std::vector<uint64_t> tab(2 * nsrc + 1);
+    uint64_t nw = 0;
+    for (uint32_t s = 0; s < nsrc; s++) {
+        tab[s] = nw;
+        tab[nsrc + 1 + s] = key0[s];
+        if (s && key0[s] < key0[s - 1]) return -EINVAL;   // senders in key order
+        nw += nwords[s];
+    }
+    tab[nsrc] = nw;
+    if (nw >= (1ull << 32)) return -EOVERFLOW;
+    for (uint64_t b = 1; b < nb; b++)
+        if (gstarts[b] < gstarts[b - 1]) return -EINVAL;
+    if (!nb) return 0;
+    if (S.cap < nw + 2 * 65) {
+        for (auto*& b : S.buf) { (void)hipFree(b); b = nullptr; HIP_CHECK(hipMalloc(&b, std::max<uint64_t>(nw + 2 * 65, 1) * 4)); }
+        S.cap = nw + 2 * 65;
+    }
+    uint64_t* dtab = S.tab;
+    HIP_CHECK(hipMemcpyAsync(dtab, tab.data(), tab.size() * 8, hipMemcpyHostToDevice, S.st));
+    HIP_CHECK(hipMemsetAsync(S.buf[1], 0, 4, S.st));
+    const auto* bm = reinterpret_cast<const unsigned long long*>(dbm);
+    if (nw) {
+        k_bm_pop<<<(uint32_t)((nw + 255) / 256), 256, 0, S.st>>>(bm, (uint32_t)nw, S.buf[0]);
+        scan_excl_u32(S.buf[0], S.buf[0], (uint32_t)nw, S.buf[1], S.sort.scan, S.st);
+    }
+    uint64_t* dgs = nullptr;
+    HIP_CHECK(hipMalloc(&dgs, nb * 16));
+    HIP_CHECK(hipMemcpyAsync(dgs, gstarts, nb * 8, hipMemcpyHostToDevice, S.st));
+    k_bm_starts<<<(uint32_t)((nb + 255) / 256), 256, 0, S.st>>>(bm, S.buf[0], S.buf[1], dtab, dtab + nsrc + 1, nsrc,
+                                                                 dgs, nb, dgs + nb);
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipMemcpyAsync(local, dgs + nb, nb * 8, hipMemcpyDeviceToHost, S.st));
+    HIP_CHECK(hipStreamSynchronize(S.st));
+    HIP_CHECK(hipFree(dgs));
+    return 0;
+}
+
 int shard_resolve_buckets(const uint64_t* seg_n, const uint32_t* seg_bucket, uint64_t nseg, uint32_t nbuckets,
                           const Point* dpts, const uint32_t* dkeys, const uint64_t* file_points, uint64_t nfiles,
                           uint32_t batch, uint32_t limit, uint32_t* state, uint32_t* spill_batch, uint64_t* kept_n,
@@ -7358,8 +7468,27 @@ int shard_bbox(const Point* d, uint64_t n, float bmin[3], float bmax[3], int dev
     HIP_CHECK(hipMemcpyAsync(bb, S.part, sizeof bb, hipMemcpyDeviceToHost, S.st));
     HIP_CHECK(hipMemcpyAsync(&bad, S.flag, 4, hipMemcpyDeviceToHost, S.st));
     HIP_CHECK(hipStreamSynchronize(S.st));
-    if (bad) return -EINVAL;
+    if (bad) return -EDOM;   // non-finite coordinates: shard_bbox_nonfinite
     for (int a = 0; a < 3; a++) { bmin[a] = bb[a]; bmax[a] = bb[3 + a]; }
+    return 0;
+}
+
+// The reference's box and the cell extent of an input with non-finite
+// coordinates (k_bbox_nf's kNfParts values, reduced over the points).
+int shard_bbox_nonfinite(const Point* d, uint64_t n, float parts[15], int device) {
+    ShardScratch& S = shard_scratch(device);
+    for (int a = 0; a < 3; a++) {
+        parts[a] = INFINITY; parts[3 + a] = -INFINITY; parts[6 + a] = 0.f;
+        parts[9 + a] = INFINITY; parts[12 + a] = -INFINITY;
+    }
+    if (!n) return 0;
+    const uint32_t nb = (uint32_t)std::min<uint64_t>((n + 255) / 256, kBBoxBlocks);
+    if (!S.nfpart) HIP_CHECK(hipMalloc(&S.nfpart, (size_t)kBBoxBlocks * kNfParts * 4));
+    k_bbox_nf<<<nb, 256, 0, S.st>>>(d, n, S.nfpart);
+    k_bbox_nf_final<<<1, 64, 0, S.st>>>(S.nfpart, nb);
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipMemcpyAsync(parts, S.nfpart, kNfParts * 4, hipMemcpyDeviceToHost, S.st));
+    HIP_CHECK(hipStreamSynchronize(S.st));
     return 0;
 }
 
@@ -7389,7 +7518,7 @@ int shard_histogram(const Point* d, uint64_t n, const ShardGrid& g, uint32_t* dh
 // The local bounding box and the slab (dim > 0) or cell histogram over a grid
 // guessed before the box is known, in one pass: points outside the guess are
 // counted in *outside (the caller falls back to shard_histogram on the true
-// grid when any rank has some).  -EINVAL: non-finite coordinates.
+// grid when any rank has some).  -EDOM: non-finite coordinates.
 int shard_bbox_histogram(const Point* d, uint64_t n, const ShardGrid& g, uint32_t dim, uint32_t* dhist, float bmin[3],
                          float bmax[3], uint64_t* outside, int device) {
     ShardScratch& S = shard_scratch(device);
@@ -7413,7 +7542,7 @@ int shard_bbox_histogram(const Point* d, uint64_t n, const ShardGrid& g, uint32_
     HIP_CHECK(hipMemcpyAsync(&nf, S.flag, 4, hipMemcpyDeviceToHost, S.st));
     HIP_CHECK(hipMemcpyAsync(&out, S.cnt, 4, hipMemcpyDeviceToHost, S.st));
     HIP_CHECK(hipStreamSynchronize(S.st));
-    if (nf) return -EINVAL;
+    if (nf) return -EDOM;
     for (int a = 0; a < 3; a++) { bmin[a] = bb[a]; bmax[a] = bb[3 + a]; }
     *outside = out;
     return 0;
@@ -7434,7 +7563,7 @@ int shard_bbox_sample(const Point* d, uint64_t n, float bmin[3], float bmax[3], 
     HIP_CHECK(hipMemcpyAsync(bb, S.part, sizeof bb, hipMemcpyDeviceToHost, S.st));
     HIP_CHECK(hipStreamSynchronize(S.st));
     for (int a = 0; a < 3; a++) {
-        if (!(std::isfinite(bb[a]) && std::isfinite(bb[3 + a]))) return -EINVAL;
+        if (!(std::isfinite(bb[a]) && std::isfinite(bb[3 + a]))) return -EDOM;
         bmin[a] = bb[a];
         bmax[a] = bb[3 + a];
     }

@@ -111,10 +111,18 @@ struct J {
         v = (float)d;
         return true;
     }
+    bool null_seen = false;   // a `null` component (serde_json's non-finite f32)
     bool vec3(float* v) {
         if (!eat('[')) return false;
         for (int a = 0; a < 3; a++) {
-            if (!f32num(v[a])) return false;
+            ws();
+            if (s.compare(i, 4, "null") == 0) {   // kept as NaN; the caller reports it
+                i += 4;
+                v[a] = NAN;
+                null_seen = true;
+            } else if (!f32num(v[a])) {
+                return false;
+            }
             if (a < 2 && !eat(',')) return false;
         }
         return eat(']');
@@ -188,6 +196,14 @@ bool parse_metadata_json(const std::string& text, Metadata& m, std::string& err)
             }
         } else ok = j.skip();
         if (!ok) { err = "metadata.json: bad value for " + key; return false; }
+    }
+    if (j.null_seen) {
+        // lib.rs:86-101 reads the file with serde_json, which refuses `null` for
+        // an f32 (the reference panics there): a cloud with infinite coordinates,
+        // or an axis of NaN only, cannot be merged into
+        err = "metadata.json: the existing cloud's bounding box is not finite (null), so it cannot be merged into "
+              "(the reference's serde_json cannot read it back either)";
+        return false;
     }
     return true;
 }
@@ -593,6 +609,9 @@ int prior_from_cells(const std::vector<CellFile>& cells, const Config& cfg, Prio
     }
     // per cell (threads): slabs by hex layer, seeds grouped by slab, their child slabs
     std::atomic<int> bad{0};
+    std::atomic<bool> any_nan{false};
+    std::mutex mx_mu;
+    float mx_abs = 0.f;
     for (uint32_t h = 0; h < levels; h++) {
         const float cs = cell_size(cfg.max_cell_size, h), cr = hex_radius(sub_cell_size(cs, cfg.sub_grid_dimension));
         const float csc = cell_size(cfg.max_cell_size, h + 1), crc = hex_radius(sub_cell_size(csc, cfg.sub_grid_dimension));
@@ -619,13 +638,26 @@ int prior_from_cells(const std::vector<CellFile>& cells, const Config& cfg, Prio
                 tl.resize(n);
                 int32_t tmin = INT32_MAX, tmax = INT32_MIN;
                 {
+                    // also: NaN seeds (the slab kernels' NaN rules) and the largest
+                    // finite magnitude (fmax skips NaN; an infinity fails `< inf`)
+                    bool nan = false;
+                    float m = 0.f;
                     size_t j = 0;
                     for (const auto& q : parts)
                         for (size_t k = 0; k < q.second; k++, j++) {
-                            tl[j] = sat_i32(q.first[k].z / cr);   // hex.rs:83
+                            const Point& pt = q.first[k];
+                            tl[j] = sat_i32(pt.z / cr);   // hex.rs:83
                             tmin = std::min(tmin, tl[j]);
                             tmax = std::max(tmax, tl[j]);
+                            nan |= (pt.x != pt.x) | (pt.y != pt.y) | (pt.z != pt.z);
+                            const float a = std::fmax(std::fmax(std::fabs(pt.x), std::fabs(pt.y)), std::fabs(pt.z));
+                            m = a < INFINITY ? std::fmax(m, a) : m;
                         }
+                    if (nan) any_nan.store(true);
+                    if (n) {
+                        std::lock_guard<std::mutex> lk(mx_mu);
+                        mx_abs = std::max(mx_abs, m);
+                    }
                 }
                 if (n == 0) continue;
                 if ((int64_t)tmax - tmin >= (1 << 20)) { bad.store(2); continue; }   // not one cell's layers
@@ -695,6 +727,8 @@ int prior_from_cells(const std::vector<CellFile>& cells, const Config& cfg, Prio
             std::vector<PriorSlabRec>().swap(plan[h][i].recs);
         }
     }
+    out.has_nan = any_nan.load();
+    out.max_abs = mx_abs;
     if (bad.load() == 2) { err = "existing cloud: a cell's points span more hex layers than a cell has"; return -EINVAL; }
     if (bad.load()) { err = "existing cloud: a point lies outside its cell's child slabs"; return -EINVAL; }
     // child links: slab (c, t), destination (octant, sel) -> record of (2c + octant bits, 2t - 1 + sel) at h+1

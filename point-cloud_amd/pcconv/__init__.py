@@ -32,6 +32,7 @@ EXPORTS = ["pcc_abi_version", "pcc_last_error", "pcc_options_default", "pcc_open
            "pcc_add_points_device", "pcc_add_empty_batches", "pcc_add_synthetic", "pcc_build", "pcc_write",
            "pcc_finish", "pcc_close", "pcc_get_stats", "pcc_set_profiling", "pcc_get_profile", "pcc_device_input",
            "pcc_convert_files", "pcc_shard_grid_from_bbox", "pcc_synth_device", "pcc_shard_bbox",
+           "pcc_shard_bbox_nonfinite", "pcc_set_event_table", "pcc_shard_batch_starts",
            "pcc_shard_histogram", "pcc_shard_route", "pcc_declare_files", "pcc_add_keyed_points_device",
            "pcc_set_keyed_points_device", "pcc_set_level_range", "pcc_set_root_spill_batches",
            "pcc_pending_cells", "pcc_export_pending", "pcc_shard_slab_histogram", "pcc_shard_route_slabs", "pcc_shard_bbox_histogram", "pcc_shard_bbox_sample",
@@ -146,6 +147,9 @@ def lib():
         L.pcc_shard_grid_from_bbox.argtypes = [f3, f3, C.c_float, C.POINTER(ShardGrid)]
         L.pcc_synth_device.argtypes = [vp, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int, C.c_float, C.c_float, C.c_int]
         L.pcc_shard_bbox.argtypes = [vp, C.c_uint64, f3, f3, C.c_int]
+        L.pcc_shard_bbox_nonfinite.argtypes = [vp, C.c_uint64, f3, C.c_int]
+        L.pcc_set_event_table.argtypes = [vp, vp, vp, C.c_uint64, C.c_uint64]
+        L.pcc_shard_batch_starts.argtypes = [vp, vp, vp, C.c_uint32, vp, C.c_uint64, vp, C.c_int]
         L.pcc_shard_histogram.argtypes = [vp, C.c_uint64, C.POINTER(ShardGrid), vp, C.c_int]
         L.pcc_shard_route.argtypes = [vp, C.c_uint64, C.c_uint32, C.POINTER(ShardGrid), vp, C.c_uint32, vp, vp,
                                       C.POINTER(C.c_uint64), C.c_int]
@@ -282,6 +286,13 @@ class Converter:
         arr = (C.c_uint64 * len(file_points))(*[int(v) for v in file_points])
         _check(lib().pcc_declare_files(self._h, arr, len(file_points)))
 
+    def set_event_table(self, starts, batches, total_batches: int):
+        """Rank-local keys: point i's event batch is batches[k] for the last k with
+        starts[k] <= i (pcc_set_event_table); then set_keyed_points_device(ptr, 0, n)."""
+        st = np.ascontiguousarray(starts, dtype=np.uint64)
+        eb = np.ascontiguousarray(batches, dtype=np.uint32)
+        _check(lib().pcc_set_event_table(self._h, st.ctypes.data, eb.ctypes.data, len(st), int(total_batches)))
+
     def add_keyed_points_device(self, pts_ptr: int, keys_ptr: int, n: int):
         _check(lib().pcc_add_keyed_points_device(self._h, C.c_void_p(pts_ptr), C.c_void_p(keys_ptr), n))
 
@@ -401,10 +412,43 @@ def synth_device(dst_ptr: int, first: int, n: int, seed: int, kind: int = 0, lo:
     _check(lib().pcc_synth_device(C.c_void_p(dst_ptr), first, n, seed, kind, lo, extent, device))
 
 
+EDOM = 33   # pcc_shard_bbox*: the input has NaN or infinite coordinates
+
+
+def _check_edom(rc: int) -> bool:
+    """False when rc is -EDOM (NaN / infinite coordinates: shard_bbox_nonfinite)."""
+    if rc == -EDOM:
+        return False
+    _check(rc)
+    return True
+
+
 def shard_bbox(pts_ptr: int, n: int, device: int = 0):
+    """(bmin, bmax), or None when a coordinate is NaN or infinite."""
     bmin, bmax = (C.c_float * 3)(), (C.c_float * 3)()
-    _check(lib().pcc_shard_bbox(C.c_void_p(pts_ptr), n, bmin, bmax, device))
+    if not _check_edom(lib().pcc_shard_bbox(C.c_void_p(pts_ptr), n, bmin, bmax, device)):
+        return None
     return list(bmin), list(bmax)
+
+
+def shard_batch_starts(bm_ptr: int, nwords, key0, gstarts, device: int = 0) -> np.ndarray:
+    """Rank-local start of every global batch start key (pcc_shard_batch_starts)."""
+    nw = np.ascontiguousarray(nwords, dtype=np.uint64)
+    k0 = np.ascontiguousarray(key0, dtype=np.uint64)
+    gs = np.ascontiguousarray(gstarts, dtype=np.uint64)
+    out = np.empty(len(gs), dtype=np.uint64)
+    _check(lib().pcc_shard_batch_starts(C.c_void_p(bm_ptr), nw.ctypes.data, k0.ctypes.data, len(nw), gs.ctypes.data,
+                                        len(gs), out.ctypes.data, device))
+    return out
+
+
+def shard_bbox_nonfinite(pts_ptr: int, n: int, device: int = 0) -> list:
+    """The 15 values of pcc_shard_bbox_nonfinite: the reference's box over the
+    non-NaN values, which axes have one, and the cell extent of the points with
+    no infinite coordinate (NaN as 0)."""
+    parts = (C.c_float * 15)()
+    _check(lib().pcc_shard_bbox_nonfinite(C.c_void_p(pts_ptr), n, parts, device))
+    return list(parts)
 
 
 def shard_histogram(pts_ptr: int, n: int, grid: ShardGrid, hist_ptr: int, device: int = 0):
@@ -422,16 +466,20 @@ def shard_slab_histogram(pts_ptr: int, n: int, grid: ShardGrid, sub_grid_dimensi
 
 def shard_bbox_histogram(pts_ptr: int, n: int, grid: ShardGrid, sub_grid_dimension: int, hist_ptr: int,
                          device: int = 0):
-    """(bmin, bmax, outside): local box + histogram over a guessed grid, one pass."""
+    """(bmin, bmax, outside): local box + histogram over a guessed grid, one pass;
+    None when a coordinate is NaN or infinite."""
     bmin, bmax, out = (C.c_float * 3)(), (C.c_float * 3)(), C.c_uint64(0)
-    _check(lib().pcc_shard_bbox_histogram(C.c_void_p(pts_ptr), n, C.byref(grid), sub_grid_dimension,
-                                          C.c_void_p(hist_ptr), bmin, bmax, C.byref(out), device))
+    if not _check_edom(lib().pcc_shard_bbox_histogram(C.c_void_p(pts_ptr), n, C.byref(grid), sub_grid_dimension,
+                                                      C.c_void_p(hist_ptr), bmin, bmax, C.byref(out), device)):
+        return None
     return list(bmin), list(bmax), int(out.value)
 
 
 def shard_bbox_sample(pts_ptr: int, n: int, device: int = 0):
+    """(bmin, bmax) of the sample, or None when it is not finite."""
     bmin, bmax = (C.c_float * 3)(), (C.c_float * 3)()
-    _check(lib().pcc_shard_bbox_sample(C.c_void_p(pts_ptr), n, bmin, bmax, device))
+    if not _check_edom(lib().pcc_shard_bbox_sample(C.c_void_p(pts_ptr), n, bmin, bmax, device)):
+        return None
     return list(bmin), list(bmax)
 
 

@@ -332,6 +332,29 @@ def event_batches(keys: np.ndarray, file_points, batch: int) -> np.ndarray:
     return eb0[f] + (k - start[f]) // batch
 
 
+def global_batches(file_points, batch: int):
+    """(start key of every non-empty global batch, its event batch number, the
+    global batch count): lib.rs:31-52, an empty file is one empty batch.  Keys
+    are 64-bit: any cloud size."""
+    fp = np.asarray([int(v) for v in file_points], dtype=np.int64)
+    start = np.concatenate([[0], np.cumsum(fp)])[:-1]
+    nb = np.maximum(1, (fp + batch - 1) // batch)
+    eb0 = np.concatenate([[0], np.cumsum(nb)])[:-1]
+    full = (fp + batch - 1) // batch   # batches holding points
+    f = np.repeat(np.arange(len(fp)), full)
+    b = np.arange(int(full.sum()), dtype=np.int64) - np.repeat(np.concatenate([[0], np.cumsum(full)])[:-1], full)
+    return (start[f] + b * batch).astype(np.uint64), (eb0[f] + b).astype(np.int64), int(nb.sum())
+
+
+def event_table(local_starts: np.ndarray, batch_no: np.ndarray, nrecv: int, total: int):
+    """The rank-local event table (pcc_set_event_table) from the local start of
+    every non-empty global batch: the batches with some of this rank's points."""
+    ls = np.asarray(local_starts, dtype=np.int64)
+    nxt = np.concatenate([ls[1:], [nrecv]])
+    keep = ls < nxt
+    return ls[keep].astype(np.uint64), np.asarray(batch_no)[keep].astype(np.uint32), int(total)
+
+
 def resolve_bucket(keys: np.ndarray, file_points, batch: int, limit: int):
     """cell.rs:108-153 for one overflow bucket of a level-0 cell, from all its
     emissions (their causing keys, any order; level 0: event batch = eb0(key)).
@@ -633,6 +656,10 @@ class HipShardOps:
         self._ready()
         return pcconv.shard_bbox(pts.data_ptr(), pts.shape[0], self.dev)
 
+    def bbox_nonfinite(self, pts: torch.Tensor) -> list:
+        self._ready()
+        return pcconv.shard_bbox_nonfinite(pts.data_ptr(), pts.shape[0], self.dev)
+
     def grid(self, gmin, gmax, level: int = 0):
         return shard_grid(gmin, gmax, self.max_cell_size, level)
 
@@ -647,9 +674,11 @@ class HipShardOps:
         """(bmin, bmax, slab histogram over `guess`, points outside `guess`)."""
         h = torch.empty(guess.ncells * pcconv.SHARD_LAYERS, dtype=torch.int32, device=pts.device)
         self._ready()
-        bmin, bmax, out = pcconv.shard_bbox_histogram(pts.data_ptr(), pts.shape[0], guess,
-                                                      int(self.cfg_full()["sub_grid_dimension"]), h.data_ptr(), self.dev)
-        return bmin, bmax, h, out
+        r = pcconv.shard_bbox_histogram(pts.data_ptr(), pts.shape[0], guess,
+                                        int(self.cfg_full()["sub_grid_dimension"]), h.data_ptr(), self.dev)
+        if r is None:   # NaN / infinite coordinates
+            return None
+        return r[0], r[1], h, r[2]
 
     def begin_step(self):
         self._built = []
@@ -724,17 +753,26 @@ class HipShardOps:
                                                 send.data_ptr(), bm.data_ptr(), self.dev)
         return send, bm, counts
 
+    # builds with rank-local keys and an event table (shard_build, no shared cell)
+    local_keys = True
+
+    def batch_starts(self, bm: torch.Tensor, nwords, key0, gstarts) -> np.ndarray:
+        self._ready()
+        return pcconv.shard_batch_starts(bm.data_ptr(), nwords, key0, gstarts, self.dev)
+
     def keys_from_bitmaps(self, bm: torch.Tensor, nwords, key0, nkeys: int) -> torch.Tensor:
         keys = torch.empty(nkeys, dtype=torch.int32, device=bm.device)
         self._ready()
         pcconv.shard_keys_from_bitmaps(bm.data_ptr(), nwords, key0, keys.data_ptr(), nkeys, self.dev)
         return keys
 
-    def build(self, file_points, pts: torch.Tensor, keys: torch.Tensor | None) -> dict:
-        """keys None: this rank holds the whole input in key order (keys 0..n-1).
-        The build reads `pts`/`keys` in place (borrowed until it returns)."""
-        self._record("build", (file_points, pts, keys), first=True)
-        return self._keyed_build(self.conv, file_points, pts, keys)
+    def build(self, file_points, pts: torch.Tensor, keys: torch.Tensor | None, etab=None) -> dict:
+        """keys None: this rank holds the whole input in key order (keys 0..n-1),
+        or, with etab (event_table), its points in global key order with
+        rank-local keys.  The build reads `pts`/`keys` in place (borrowed until
+        it returns)."""
+        self._record("build", (file_points, pts, keys, etab), first=True)
+        return self._keyed_build(self.conv, file_points, pts, keys, etab=etab)
 
     # Diagnostics only (scripts/rank_stages.py replays a step's local calls): with
     # record_inputs set, every stage's device inputs are kept in last_inputs until
@@ -749,10 +787,13 @@ class HipShardOps:
             self.last_inputs = {}
         self.last_inputs[stage] = args
 
-    def _keyed_build(self, c, file_points, pts, keys, roots=None) -> dict:
+    def _keyed_build(self, c, file_points, pts, keys, roots=None, etab=None) -> dict:
         self._ready()
         c.clear_input()
-        c.declare_files(file_points)
+        if etab is not None:
+            c.set_event_table(*etab)
+        else:
+            c.declare_files(file_points)
         if roots is not None:
             c.set_root_spill_batches(*roots)
         c.set_keyed_points_device(pts.data_ptr(), 0 if keys is None else keys.data_ptr(), pts.shape[0])
@@ -944,6 +985,14 @@ def _sub_grid_hist(h, guess, grid, nl: int):
     return v[o[0]:o[0] + d[0], o[1]:o[1] + d[1], o[2]:o[2] + d[2]].contiguous().view(-1)
 
 
+def _fmin(a: float, b: float) -> float:   # f32::min (glam Vec3::min): a NaN operand is skipped
+    return b if a != a else (a if b != b else min(a, b))
+
+
+def _fmax(a: float, b: float) -> float:
+    return b if a != a else (a if b != b else max(a, b))
+
+
 def shard_build(comm, ops, pts: torch.Tensor, key0: int, file_points, write: bool = False,
                 sync=None, merge: bool = False, split: bool = True) -> ShardResult:
     """One sharded conversion step.  `pts` is this rank's (n, 4) int32 view of
@@ -995,36 +1044,63 @@ def shard_build(comm, ops, pts: torch.Tensor, key0: int, file_points, write: boo
     # fused ops the same pass over the points also takes the slab histogram, over
     # a grid guessed from an all-reduced sample box with one cell of margin; if
     # a point falls outside it on any rank, the histogram is taken again (step 3).
+    # NaN / infinite coordinates on any rank ("nonfinite"): the reference's box
+    # skips NaN per axis and keeps infinities (bounding-volume/src/lib.rs:23-31),
+    # the ownership grid spans the cells of the points without an infinite
+    # coordinate (NaN as cell 0, metadata.rs:100-102), and the points with one
+    # travel as unit 0 (one rank builds them all); no cell is shared.
     from pcconv import SHARD_LAYERS as NL
-    guess, sh_guess, outside = None, None, 0
+    inf3, ninf3 = [float("inf")] * 3, [float("-inf")] * 3
+    guess, sh_guess, outside, nf_local = None, None, 0, 0
     if getattr(ops, "fused_bbox_hist", False) and not merge and n_total:
-        if pts.shape[0]:
-            smin, smax = ops.bbox_sample(pts)
-        else:
-            smin, smax = [float("inf")] * 3, [float("-inf")] * 3
-        sb = torch.tensor([-smin[0], -smin[1], -smin[2], smax[0], smax[1], smax[2]], dtype=torch.float32,
-                          device=comm.device)
+        sbox = ops.bbox_sample(pts) if pts.shape[0] else (inf3, ninf3)
+        if sbox is None:
+            nf_local, sbox = 1, (inf3, ninf3)
+        smin, smax = sbox
+        sb = torch.tensor([-smin[0], -smin[1], -smin[2], smax[0], smax[1], smax[2], float(nf_local)],
+                          dtype=torch.float32, device=comm.device)
         comm.allreduce_(sb, "max")
         sbh = sb.cpu().tolist()
         cs = float(ops.cfg_full()["max_cell_size"])
-        g0 = ops.grid([-sbh[0] - cs, -sbh[1] - cs, -sbh[2] - cs], [sbh[3] + cs, sbh[4] + cs, sbh[5] + cs])
-        if not int(getattr(g0, "coarse", 0)) and int(g0.ncells) * NL <= (1 << 24):
-            guess = g0
+        if sbh[6] == 0:
+            g0 = ops.grid([-sbh[0] - cs, -sbh[1] - cs, -sbh[2] - cs], [sbh[3] + cs, sbh[4] + cs, sbh[5] + cs])
+            if not int(getattr(g0, "coarse", 0)) and int(g0.ncells) * NL <= (1 << 24):
+                guess = g0
+    bmin, bmax = inf3, ninf3
     if guess is not None:
-        bmin, bmax, sh_guess, outside = ops.bbox_slab_histogram(pts, guess)
+        r = ops.bbox_slab_histogram(pts, guess)
+        if r is None:
+            nf_local = 1
+        else:
+            bmin, bmax, sh_guess, outside = r
     elif pts.shape[0]:
-        bmin, bmax = ops.bbox(pts)
-    else:
-        bmin, bmax = [float("inf")] * 3, [float("-inf")] * 3
-    bb = torch.tensor([-bmin[0], -bmin[1], -bmin[2], bmax[0], bmax[1], bmax[2], 1.0 if outside else 0.0],
-                      dtype=torch.float32, device=comm.device)
+        r = ops.bbox(pts)
+        if r is None:
+            nf_local = 1
+        else:
+            bmin, bmax = r
+    bb = torch.tensor([-bmin[0], -bmin[1], -bmin[2], bmax[0], bmax[1], bmax[2], 1.0 if outside else 0.0,
+                       float(nf_local)], dtype=torch.float32, device=comm.device)
     comm.allreduce_(bb, "max")
     bbh = bb.cpu().tolist()
     gmin, gmax = [-bbh[0], -bbh[1], -bbh[2]], bbh[3:6]
-    if bbh[6] > 0:   # the guess missed some point on some rank
+    emin, emax = gmin, gmax   # the extent the ownership grid spans
+    nonfinite = bbh[7] > 0
+    if bbh[6] > 0 or nonfinite:   # the guess missed some point on some rank
         guess, sh_guess = None, None
+    if nonfinite:
+        parts = ops.bbox_nonfinite(pts) if pts.shape[0] else inf3 + ninf3 + [0.0] * 3 + inf3 + ninf3
+        v = torch.tensor([-x if (k < 3 or 9 <= k < 12) else x for k, x in enumerate(parts)], dtype=torch.float32,
+                         device=comm.device)
+        comm.allreduce_(v, "max")
+        vh = v.cpu().tolist()
+        gmin = [-vh[a] if vh[6 + a] > 0 else float("nan") for a in range(3)]
+        gmax = [vh[3 + a] if vh[6 + a] > 0 else float("nan") for a in range(3)]
+        emin, emax = [-vh[9 + a] for a in range(3)], [vh[12 + a] for a in range(3)]
+        if not all(a <= b for a, b in zip(emin, emax)):   # every point has an infinite coordinate
+            emin, emax = [0.0] * 3, [0.0] * 3
     mark("bbox")
-    plan = None
+    plan, etab = None, None
     if n_total == 0:
         recv = pts[:0]
         keys = torch.empty(0, dtype=torch.int32, device=dev)
@@ -1033,14 +1109,16 @@ def shard_build(comm, ops, pts: torch.Tensor, key0: int, file_points, write: boo
             ops.set_subtrees(np.zeros((0, 3), dtype=np.int32))
     else:
         # 3. ownership: level-0 cells; heavy ones shared slab by slab
-        grid = ops.grid(gmin, gmax)
+        grid = ops.grid(emin, emax)
         # this rank's slab histogram over the true grid from the fused pass
         sh_local = (_sub_grid_hist(sh_guess, guess, grid, NL)
                     if sh_guess is not None and not int(getattr(grid, "coarse", 0)) else None)
         coarse = int(getattr(grid, "coarse", 0))
         if merge and coarse:
             raise ValueError("sharded merge: the existing cloud's bounding box spans more than 2^22 level-0 cells")
-        grid1 = ops.grid(gmin, gmax, level=1) if (split and not merge and W > 1 and not coarse) else None
+        # (shared cells exchange global u32 keys: none beyond 2^32 points)
+        grid1 = (ops.grid(emin, emax, level=1)
+                 if (split and not merge and W > 1 and not coarse and not nonfinite and n_total < (1 << 32)) else None)
         if grid1 is not None and (int(grid1.ncells) > (1 << 22) or int(grid.ncells) * NL > (1 << 24)):
             grid1 = None
         if grid1 is not None:
@@ -1081,6 +1159,10 @@ def shard_build(comm, ops, pts: torch.Tensor, key0: int, file_points, write: boo
             # the points travel with one membership bit per sender point instead
             # of a 4-B key each; every receiver rebuilds its keys in rank order
             nd = 2 * W if nsplit else W
+            # rank-local keys (no shared cell): the receiver's points keep their
+            # key order, their keys are their indices, and the event batches come
+            # from a table of the batches' local starts (any cloud size)
+            local_keys = getattr(ops, "local_keys", False) and not nsplit
             tab = torch.from_numpy((route_table(plan, W) if nsplit else owner_h).astype(np.int32)).to(dev)
             if nsplit:
                 lh = lhist.get("slab")
@@ -1101,7 +1183,12 @@ def shard_build(comm, ops, pts: torch.Tensor, key0: int, file_points, write: boo
                 rc = comm.alltoall_counts(cw)
                 rp, rbm = _exchange_many(comm, [(send.narrow(0, off, sum(cw)), cw, rc),
                                                 (bm.narrow(0, row, W).reshape(-1), [nwl] * W, rw)], dev)
-                got.append((rp, ops.keys_from_bitmaps(rbm, rw, k0, sum(rc))))
+                if local_keys:
+                    gs, gb, nbt = global_batches(file_points, ops.batch_size)
+                    etab = event_table(ops.batch_starts(rbm, rw, k0, gs), gb, sum(rc), nbt)
+                    got.append((rp, None))
+                else:
+                    got.append((rp, ops.keys_from_bitmaps(rbm, rw, k0, sum(rc))))
             recv, keys = got[0]
             if nsplit:
                 lrecv, lkeys = got[1]
@@ -1130,7 +1217,7 @@ def shard_build(comm, ops, pts: torch.Tensor, key0: int, file_points, write: boo
     phases = {"lead": 0, "sub": 0, "whole": 0}
     sub_points = 0
     # 5a. phase 1: the whole level-0 sub-trees this rank owns ...
-    local = ops.build(file_points, recv, keys)
+    local = ops.build(file_points, recv, keys, etab=etab) if etab is not None else ops.build(file_points, recv, keys)
     parts = [local]
     phases["whole"] = int(local.get("arrivals", 0))
     mark("build")
@@ -1187,9 +1274,9 @@ def shard_build(comm, ops, pts: torch.Tensor, key0: int, file_points, write: boo
     if merge:   # lib.rs:86-101: counters continue; converter.rs:96-104 Aabb::extend_aabb
         pm = ops.prior_meta()
         if pm["number_of_points"] > 0:
-            if n_total:
-                summary["bbox_min"] = [min(a, b) for a, b in zip(gmin, pm["bbox_min"])]
-                summary["bbox_max"] = [max(a, b) for a, b in zip(gmax, pm["bbox_max"])]
+            if n_total:   # f32::min / max: NaN skipped
+                summary["bbox_min"] = [_fmin(a, b) for a, b in zip(gmin, pm["bbox_min"])]
+                summary["bbox_max"] = [_fmax(a, b) for a, b in zip(gmax, pm["bbox_max"])]
             else:
                 summary["bbox_min"], summary["bbox_max"] = pm["bbox_min"], pm["bbox_max"]
         summary["number_of_points"] = n_total + pm["number_of_points"]

@@ -30,9 +30,27 @@ def as_tensor(p: np.ndarray) -> torch.Tensor:
 
 
 def cell_index(v: np.ndarray, cs: float) -> np.ndarray:
-    """metadata.rs:100-102 per axis: (floor(p / cs) as f32) as i32, saturating."""
-    q = np.floor(v.astype(np.float32) / np.float32(cs)).astype(np.float64)
+    """metadata.rs:100-102 per axis: (floor(p / cs) as f32) as i32, saturating, NaN -> 0."""
+    with np.errstate(invalid="ignore"):
+        q = np.floor(v.astype(np.float32) / np.float32(cs)).astype(np.float64)
+    q = np.where(np.isnan(q), 0.0, q)
     return np.clip(q, -2147483648.0, 2147483647.0).astype(np.int64)
+
+
+def _json_f32(v):
+    f = float(np.float32(v))
+    return f if np.isfinite(f) else None
+
+
+def has_inf(p: np.ndarray) -> np.ndarray:
+    return np.isinf(p["x"]) | np.isinf(p["y"]) | np.isinf(p["z"])
+
+
+def finite_box(p: np.ndarray):
+    """(bmin, bmax), or None when a coordinate is NaN or infinite (pcc_shard_bbox's -EDOM)."""
+    if not (np.isfinite(p["x"]).all() and np.isfinite(p["y"]).all() and np.isfinite(p["z"]).all()):
+        return None
+    return [float(p[a].min()) for a in "xyz"], [float(p[a].max()) for a in "xyz"]
 
 
 class NumpyShardOps:
@@ -69,8 +87,23 @@ class NumpyShardOps:
                     shutil.copy(os.path.join(self.out_dir, name, fn), os.path.join(d, name, fn))
 
     def bbox(self, pts):
+        return finite_box(as_points(pts))
+
+    def bbox_nonfinite(self, pts):
+        """numpy restatement of pcc_shard_bbox_nonfinite (k_bbox_nf's 15 values)."""
         p = as_points(pts)
-        return ([float(p[a].min()) for a in "xyz"], [float(p[a].max()) for a in "xyz"])
+        fin = ~has_inf(p)
+        out = [0.0] * 15
+        for i, a in enumerate("xyz"):
+            v = p[a].astype(np.float64)
+            nn = v[~np.isnan(v)]
+            out[i] = float(nn.min()) if len(nn) else float("inf")
+            out[3 + i] = float(nn.max()) if len(nn) else float("-inf")
+            out[6 + i] = 1.0 if len(nn) else 0.0
+            g = np.where(np.isnan(v), 0.0, v)[fin]
+            out[9 + i] = float(g.min()) if len(g) else float("inf")
+            out[12 + i] = float(g.max()) if len(g) else float("-inf")
+        return out
 
     def grid(self, gmin, gmax, level: int = 0):
         from pcconv.dist import shard_grid
@@ -121,8 +154,7 @@ class NumpyShardOps:
     fused_bbox_hist = True
 
     def bbox_sample(self, pts):
-        p = as_points(pts)[::97]   # any sample: the fused pass checks the guess
-        return ([float(p[a].min()) for a in "xyz"], [float(p[a].max()) for a in "xyz"])
+        return finite_box(as_points(pts)[::97])   # any sample: the fused pass checks the guess
 
     def bbox_slab_histogram(self, pts, guess):
         """numpy restatement of pcc_shard_bbox_histogram: points outside the
@@ -130,6 +162,8 @@ class NumpyShardOps:
         p = as_points(pts)
         nl = pcconv.SHARD_LAYERS
         h = np.zeros(guess.ncells * nl, dtype=np.int64)
+        if len(p) and finite_box(p) is None:   # -EDOM
+            return None
         if len(p) == 0:
             return [float("inf")] * 3, [float("-inf")] * 3, torch.from_numpy(h.astype(np.int32)), 0
         ix = [cell_index(p[a], guess.cell_size) - guess.lo[i] for i, a in enumerate("xyz")]
@@ -159,7 +193,9 @@ class NumpyShardOps:
         return as_tensor(p[order]), torch.from_numpy(keys.copy()), [int(c) for c in counts]
 
     def _cells(self, p, grid):
-        ix = [cell_index(p[a], grid.cell_size) - grid.lo[i] for i, a in enumerate("xyz")]
+        """Cell unit of every point; a point with an infinite coordinate: unit 0."""
+        inf = has_inf(p)
+        ix = [np.where(inf, grid.lo[i], cell_index(p[a], grid.cell_size)) - grid.lo[i] for i, a in enumerate("xyz")]
         d = [int(v) for v in grid.dims]
         assert all(((v >= 0) & (v < d[i])).all() for i, v in enumerate(ix))
         return (ix[0] * d[1] + ix[1]) * d[2] + ix[2]
@@ -195,6 +231,21 @@ class NumpyShardOps:
         bm = words.reshape(nranks, nw).astype(np.uint64).view(np.int64)
         return as_tensor(p[order]), torch.from_numpy(np.ascontiguousarray(bm)), [int(c) for c in counts]
 
+    # rank-local keys + an event table (HipShardOps.local_keys); a test may set it False
+    local_keys = True
+
+    def batch_starts(self, bm, nwords, key0, gstarts):
+        """numpy restatement of pcc_shard_batch_starts: received points below each global key."""
+        w = bm.cpu().numpy().view(np.uint64)
+        keys, o = [], 0
+        for nwd, k0 in zip(nwords, key0):
+            seg = w[o:o + nwd]
+            o += nwd
+            bits = np.unpackbits(seg.astype(">u8").view(np.uint8).reshape(-1, 8), axis=1, bitorder="big")[:, ::-1]
+            keys.append(np.uint64(k0) + np.flatnonzero(bits.reshape(-1)).astype(np.uint64))
+        allk = np.concatenate(keys) if keys else np.zeros(0, np.uint64)
+        return np.searchsorted(allk, np.asarray(gstarts, dtype=np.uint64), side="left").astype(np.uint64)
+
     def keys_from_bitmaps(self, bm, nwords, key0, nkeys):
         w = bm.cpu().numpy().view(np.uint64)
         out, o = [], 0
@@ -227,8 +278,35 @@ class NumpyShardOps:
         return {"hierarchies": o.hierarchies, "arrivals": o.arrivals, "cells": o.num_cells, "levels": o.hierarchies,
                 "slabs": 0}
 
-    def build(self, file_points, pts, keys) -> dict:
+    def _feed_table(self, o, p, etab):
+        """Batches of a rank-local event table: entry k's points form batch
+        eb[k]; the global batches without local points are fed empty."""
+        starts, eb, total = etab
+        st = [int(v) for v in starts] + [len(p)]
+        prev = -1
+        for k, e in enumerate(int(v) for v in eb):
+            for _ in range(e - prev - 1):
+                o.add_batch(p[:0])
+            o.add_batch(p[st[k]:st[k + 1]])
+            prev = e
+        for _ in range(total - prev - 1):
+            o.add_batch(p[:0])
+
+    def build(self, file_points, pts, keys, etab=None) -> dict:
         p = as_points(pts)
+        if etab is not None:
+            assert keys is None
+            if self.oracle is not None:
+                if self.oracle in self.oracles:
+                    self.oracles.remove(self.oracle)
+                self.oracle.close()
+            o = self.oracle = Oracle(self.cfg)
+            self.oracles.append(o)
+            if self.merge:
+                o.load(self.subtree_dir)
+            self._feed_table(o, p, etab)
+            assert o.error == 0
+            return self._stats(o)
         k = (np.arange(len(p), dtype=np.int64) if keys is None
              else keys.cpu().numpy().view(np.uint32).astype(np.int64))
         assert (np.diff(k) > 0).all(), "keyed input must arrive in global key order"
@@ -327,8 +405,9 @@ class NumpyShardOps:
             cfg = dict(dict(cell_point_overflow_limit=5000, sub_grid_dimension=96, max_cell_size=1000.0), **self.cfg)
             meta = {"version": "1.0", "name": "Unknown", "number_of_points": summary["number_of_points"],
                     "hierarchies": summary["hierarchies"],
-                    "bounding_box": {"min": [float(np.float32(v)) for v in summary["bbox_min"]],
-                                     "max": [float(np.float32(v)) for v in summary["bbox_max"]]},
+                    # serde_json writes a non-finite f32 as null (as the product's pcc_set_summary)
+                    "bounding_box": {"min": [_json_f32(v) for v in summary["bbox_min"]],
+                                     "max": [_json_f32(v) for v in summary["bbox_max"]]},
                     "config": cfg}
             with open(os.path.join(self.out_dir, "metadata.json"), "w") as f:
                 json.dump(meta, f, indent=2)

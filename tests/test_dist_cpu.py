@@ -527,3 +527,96 @@ def test_plan_search_placement_equals_lpt_of_its_lists():
             if est[kk] < est[best] * 0.98:
                 best = kk
         assert k == best and t == est[best]
+
+
+# ------------------------------------------------------------- NaN / infinite coordinates
+# bounding-volume/src/lib.rs:23-31 (NaN skipped, infinities kept), metadata.rs:100-102
+# (`as i32`: NaN -> cell 0, infinities saturate), cell.rs:77-80 (NaN never less).
+# The ownership grid spans the cells of the points without an infinite
+# coordinate (NaN as 0); the points with one travel as unit 0 (one rank builds
+# them all); no cell is shared.
+def _same_summary(a, b):
+    return json.dumps(a, sort_keys=True) == json.dumps(b, sort_keys=True)   # NaN == NaN
+
+
+def _thread_run(out, files, world, cfg, batch, merge=False, mode="fused"):
+    import threading
+    fp = [len(f) for f in files]
+    grp = ThreadGroup(world)
+    res, errs = [None] * world, []
+
+    def worker(r):
+        try:
+            pts, key0 = rank_slice(files, r, world)
+            ops = NumpyShardOps(out, batch_size=batch, config=None if merge else cfg, merge=merge)
+            if mode == "plain":
+                ops.fused_bbox_hist = False
+            res[r] = shard_build(ThreadComm(grp, r, torch.device("cpu")), ops, as_tensor(pts), key0, fp, write=True,
+                                 merge=merge)
+            ops.close()
+        except BaseException as e:  # noqa: BLE001
+            errs.append(e)
+            grp.bar.abort()
+
+    th = [threading.Thread(target=worker, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs
+    assert all(_same_summary(r.summary, res[0].summary) for r in res)
+    return res
+
+
+@pytest.mark.parametrize("world,kinds,mode", [(2, "mixed", "fused"), (3, "mixed", "plain"), (4, "nan", "fused")])
+def test_thread_ranks_nonfinite_match_oracle(tmp_path, world, kinds, mode):
+    from nonfinite_input import NONFINITE_CFG, nonfinite_files
+    files = nonfinite_files(seed=31, n=60_000, kinds=kinds)
+    out = str(tmp_path / "out")
+    res = _thread_run(out, files, world, NONFINITE_CFG, 5000, mode=mode)
+    assert sum(r.recv_points for r in res) == sum(len(f) for f in files)
+    check_against_oracle(tmp_path, files, out, res[0].summary, cfg=NONFINITE_CFG, batch=5000)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_thread_ranks_nonfinite_merge_matches_oracle(tmp_path, world):
+    """NaN and +-inf points merged by `world` ranks into a cloud holding NaN points."""
+    from nonfinite_input import NONFINITE_CFG, nonfinite_files
+    old = nonfinite_files(seed=32, n=50_000, kinds="nan")
+    new = nonfinite_files(seed=33, n=30_000, kinds="mixed")
+    out = str(tmp_path / "out")
+    assert run_oracle(out, old, NONFINITE_CFG, 5000)[0] == 0
+    res = _thread_run(out, new, world, NONFINITE_CFG, 5000, merge=True)
+    assert sum(r.recv_points for r in res) == sum(len(f) for f in new)
+    check_against_oracle(tmp_path, old + new, out, res[0].summary, cfg=NONFINITE_CFG, batch=5000)
+
+
+def _gloo_nonfinite_worker(rank, world, port, out, res_dir):
+    import torch.distributed as dist
+    from nonfinite_input import NONFINITE_CFG, nonfinite_files
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        files = nonfinite_files(seed=34, n=40_000, kinds="mixed")
+        pts, key0 = rank_slice(files, rank, world)
+        ops = NumpyShardOps(out, batch_size=5000, config=NONFINITE_CFG)
+        r = shard_build(TorchComm(torch.device("cpu")), ops, as_tensor(pts), key0, [len(f) for f in files],
+                        write=True)
+        ops.close()
+        with open(os.path.join(res_dir, f"rank{rank}.json"), "w") as f:
+            json.dump({"summary": r.summary, "recv": r.recv_points}, f)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_nonfinite_matches_oracle(tmp_path):
+    import torch.multiprocessing as mp
+    from nonfinite_input import NONFINITE_CFG, nonfinite_files
+    out, rd = str(tmp_path / "out"), str(tmp_path / "res")
+    os.makedirs(rd)
+    mp.spawn(_gloo_nonfinite_worker, args=(2, _free_port(), out, rd), nprocs=2, join=True)
+    r = [json.load(open(os.path.join(rd, f"rank{i}.json"))) for i in range(2)]
+    files = nonfinite_files(seed=34, n=40_000, kinds="mixed")
+    assert _same_summary(r[0]["summary"], r[1]["summary"])
+    assert r[0]["recv"] + r[1]["recv"] == sum(len(f) for f in files)
+    check_against_oracle(tmp_path, files, out, r[0]["summary"], cfg=NONFINITE_CFG, batch=5000)

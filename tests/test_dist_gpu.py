@@ -434,3 +434,58 @@ def test_gloo_processes_with_hip_ops_match_oracle(tmp_path, case, world):
     if case == "gauss":
         assert r[0]["plan"]["split_cells"] > 0
     check_against_oracle(tmp_path, files, out, r[0]["summary"], cfg=cfg)
+
+
+# NaN / +-inf coordinates through the sharded build (dist.shard_build's
+# "nonfinite" path: the reference's box and the cell extent from
+# pcc_shard_bbox_nonfinite, points with an infinite coordinate routed as unit 0,
+# no shared cells) and through a sharded merge, against the oracle.
+@pytest.mark.parametrize("world,kinds", [(2, "mixed"), (3, "nan"), (4, "mixed")])
+def test_sharded_threads_nonfinite_match_oracle(tmp_path, world, kinds):
+    from nonfinite_input import NONFINITE_CFG, nonfinite_files
+    files = nonfinite_files(seed=41, n=100_000, kinds=kinds)
+    out = str(tmp_path / "out")
+    res = _run_threads(files, world, out, cfg=NONFINITE_CFG, batch=5000)
+    assert sum(r.recv_points for r in res) == sum(len(f) for f in files)
+    check_against_oracle(tmp_path, files, out, res[0].summary, cfg=NONFINITE_CFG, batch=5000)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_merge_nonfinite_match_oracle(tmp_path, world):
+    from nonfinite_input import NONFINITE_CFG, nonfinite_files
+    old = nonfinite_files(seed=42, n=80_000, kinds="nan")
+    new = nonfinite_files(seed=43, n=50_000, kinds="mixed")
+    out = str(tmp_path / "out")
+    assert run_oracle(out, old, NONFINITE_CFG, 5000)[0] == 0
+    res = _run_threads(new, world, out, batch=5000, merge=True)
+    assert sum(r.recv_points for r in res) == sum(len(f) for f in new)
+    check_against_oracle(tmp_path, old + new, out, res[0].summary, cfg=NONFINITE_CFG, batch=5000)
+
+
+def test_shard_ops_nonfinite_units():
+    """pcc_shard_bbox* report NaN / inf input (-EDOM: None in the mirror),
+    pcc_shard_bbox_nonfinite == the numpy statement, and the cell histogram /
+    one-pass route send an infinite point as unit 0 (as the numpy double)."""
+    from nonfinite_input import nonfinite_files
+    p = np.concatenate(nonfinite_files(seed=44, n=50_000, kinds="mixed"))
+    t = as_tensor(p).to(DEV)
+    torch.cuda.synchronize()
+    assert pcconv.shard_bbox(t.data_ptr(), len(p)) is None
+    assert pcconv.shard_bbox_sample(t.data_ptr(), len(p)) is None or np.isfinite(p["x"][::97]).all()
+    ref = NumpyShardOps(None)
+    parts = pcconv.shard_bbox_nonfinite(t.data_ptr(), len(p))
+    want = ref.bbox_nonfinite(as_tensor(p))
+    assert [np.float32(v) for v in parts] == [np.float32(v) for v in want]
+    from pcconv.dist import shard_grid
+    g = shard_grid(parts[9:12], parts[12:15], 1000.0)
+    h = torch.empty(g.ncells, dtype=torch.int32, device=DEV)
+    pcconv.shard_histogram(t.data_ptr(), len(p), g, h.data_ptr())
+    assert np.array_equal(h.cpu().numpy(), ref.histogram(as_tensor(p), g).numpy())
+    world = 3
+    owner = torch.from_numpy((np.arange(g.ncells) % world).astype(np.int32)).to(DEV)
+    ops = HipShardOps.__new__(HipShardOps)
+    ops.dev, ops.cfg = 0, {}
+    s1, b1, c1 = ops.route_bitmaps(t, g, owner, world, False, hist=h)
+    s2, b2, c2 = ref.route_bitmaps(as_tensor(p), g, owner.cpu(), world, False)
+    assert c1 == c2
+    assert torch.equal(s1.cpu(), s2) and torch.equal(b1.cpu(), b2)

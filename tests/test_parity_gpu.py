@@ -265,24 +265,23 @@ def test_depth_limit_is_an_error():
         c.close()
 
 
-def test_nonfinite_merge_rejected():
-    """NaN / +-inf coordinates build in plain builds (test_nonfinite_gpu.py); a
-    merge into an existing cloud still rejects them with an error."""
+def test_merge_into_cloud_with_infinite_bbox_is_an_error():
+    """A cloud with infinite coordinates writes its bounding box as null
+    (serde_json), which the reference cannot read back (lib.rs:86-101 unwraps
+    serde_json's error); a merge into it fails with an explicit error.  NaN and
+    +-inf points merge into a finite cloud: tests/test_nonfinite_gpu.py."""
     import pcconv
     with tempfile.TemporaryDirectory() as tg:
         c = pcconv.Converter(tg)
-        c.add_points(synth(1, 0, 1000))
+        p = synth(1, 0, 1000)
+        p["x"][5] = np.inf
+        c.add_points(p)
         c.build()
         c.write()
         c.close()
-        p = synth(2, 0, 100)
-        p["x"][7] = np.nan
-        c = pcconv.Converter(tg)
-        c.add_points(p)
         with pytest.raises(pcconv.PccError) as ei:
-            c.build()
-        assert "merge" in str(ei.value)
-        c.close()
+            c = pcconv.Converter(tg)
+        assert "not finite" in str(ei.value)
 
 
 def test_ply_cli_roundtrip():
