@@ -56,6 +56,8 @@ typedef struct pcc_stats {
     uint64_t grid_points, kept_points;  /* grid winners + points kept in Some(list) buckets == number_of_points */
     double build_ms;                    /* device build wall time (inputs resident in HBM) */
     float bbox_min[3], bbox_max[3];
+    uint64_t level0_early_tiles;        /* level-0 tiles (3072 points) whose first pass ran before
+                                           pcc_build (behind the upload pieces or pcc_input_landed) */
 } pcc_stats;
 
 /* Per-stage device time of the last pcc_build (HIP events on the engine stream;
@@ -353,6 +355,17 @@ int pcc_add_keyed_points_device(pcc_converter* c, const pcc_point* dev_pts, cons
  * dev_keys may be NULL: the keys are then 0 .. n-1 (one rank holds the whole
  * input in key order, so routing is the identity). */
 int pcc_set_keyed_points_device(pcc_converter* c, const pcc_point* dev_pts, const uint32_t* dev_keys, uint64_t n);
+
+/* Points [first, last) of the borrowed input (pcc_set_keyed_points_device with
+ * dev_keys = NULL after pcc_set_event_table; no merge) are in place, or will be
+ * once the work queued so far on after_stream (a hipStream_t, NULL: none)
+ * completes.  Level-0 pass 1 of the build then runs on every group of tiles
+ * whose points have all landed, on the converter's stream, while the rest of
+ * the input is still arriving (a sharded rank's exchange); the
+ * build runs the groups left.  Ranges may come in any order and overlap.
+ * Optional: without it the build is the same, all of pass 1 inside pcc_build.
+ * The landed points must not change until pcc_build returns. */
+int pcc_input_landed(pcc_converter* c, uint64_t first, uint64_t last, void* after_stream);
 
 /* Level ranges: one heavy level-0 cell built by several ranks (SURVEY §8e/§8f-4;
  * converter.rs:114-139 recursion split at a level boundary, which is exact

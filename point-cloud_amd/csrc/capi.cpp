@@ -829,6 +829,17 @@ int pcc_set_keyed_points_device(pcc_converter* c, const pcc_point* d, const uint
     GUARD_END
 }
 
+int pcc_input_landed(pcc_converter* c, uint64_t first, uint64_t last, void* after_stream) {
+    if (!c) return set_err(-EINVAL, "null argument");
+    if (c->built) return set_err(-EINVAL, "input landed after build");
+    if (c->merge) return set_err(-EINVAL, "input_landed: not for a merge");
+    GUARD_BEGIN
+    const int rc = c->eng->input_landed(first, last, static_cast<hipStream_t>(after_stream));
+    if (rc) return set_err(rc, c->eng->last_error());
+    return 0;
+    GUARD_END
+}
+
 int pcc_set_level_range(pcc_converter* c, uint32_t root_level, uint32_t max_levels, int raw_buckets) {
     if (!c) return set_err(-EINVAL, "null argument");
     if (c->merge) return set_err(-EINVAL, "a merge cannot be split into level ranges");
@@ -1014,6 +1025,7 @@ int pcc_get_stats(const pcc_converter* c, pcc_stats* s) {
     s->kept_points = b.kept_points + c->untouched_kept;
     s->cells += c->untouched_cells;
     s->build_ms = c->build_ms;
+    s->level0_early_tiles = b.pre0_tiles;
     for (int a = 0; a < 3; a++) { s->bbox_min[a] = c->meta.bmin[a]; s->bbox_max[a] = c->meta.bmax[a]; }
     return 0;
 }

@@ -207,6 +207,10 @@ public:
     // order, keys = indices) belongs to event batch eb[k] for the last k with
     // starts[k] <= i; total_batches = the global batch count (lib.rs:31-52).
     void set_event_table(const uint64_t* starts, const uint32_t* eb, uint64_t n, uint64_t total_batches);
+    // Points [first, last) of the borrowed input (set_keyed_external, keys NULL)
+    // are in place: level-0 pass 1 of the groups they complete runs behind.
+    // after: a stream whose work so far wrote those points (NULL: already in place).
+    int input_landed(uint64_t first, uint64_t last, hipStream_t after);
     void add_keyed_device(const Point* dpts, const uint32_t* dkeys, uint64_t n);
     // Zero-copy variant: the build reads this shard's n points and keys straight
     // from caller memory (e.g. the buffers an exchange received into), which must
@@ -317,6 +321,16 @@ private:
     const void* pre6_ar1_ = nullptr;
     void* d_pre6_dummy_ = nullptr;       // k_l0_tile6's scratch for its entry stores (persistent, not the build pool)
     bool pre6_run(uint64_t upto, hipEvent_t after, bool all);
+    // Borrowed device input landing in pieces (a sharded rank's exchange):
+    // level-0 pass 1 runs on every group of tiles whose points have all landed.
+    std::vector<std::pair<uint64_t, uint64_t>> landed_;   // disjoint, sorted point ranges
+    std::vector<uint8_t> pre6_done_;                      // per group: pass 1 run (landing mode)
+    const Point* pre6_src_ = nullptr;                     // the input pass 1 ran on
+    uint32_t* d_pre6_glist_ = nullptr;                    // group lists of the landing launches (in launch order)
+    std::vector<uint32_t> pre6_glist_;                    // (host copy: the async uploads' source)
+    uint64_t pre6_glist_cap_ = 0;
+    uint64_t pre6_ndone_ = 0;                             // groups run
+    hipEvent_t land_ev_ = nullptr;                        // the landing stream's progress
     float* d_prepart_ = nullptr;
     uint32_t* d_preflag_ = nullptr;
     hipEvent_t pre_ev_ = nullptr;

@@ -326,6 +326,20 @@ __device__ __forceinline__ void set_err(Counters* c, uint32_t bit) { atomicOr(&c
 
 __device__ __forceinline__ uint32_t f2u(float f) { return __float_as_uint(f); }
 
+// A per-lane select that stays one v_cndmask: both operands are computed on
+// every lane first.  (A conditional operator with arms of a few instructions
+// is emitted as a branch, i.e. an exec-mask region of 2-3 SALU per wave; the
+// dense slab kernel's 16 waves share the CU's scalar unit.)
+__device__ __forceinline__ uint32_t vsel(bool c, uint32_t t, uint32_t f) {
+    const uint64_t m = __builtin_amdgcn_ballot_w64(c);
+    uint32_t r;
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(f), "v"(t), "s"(m));
+    return r;
+}
+__device__ __forceinline__ int32_t vsel(bool c, int32_t t, int32_t f) {
+    return (int32_t)vsel(c, (uint32_t)t, (uint32_t)f);
+}
+
 // event batch of input index i (lib.rs:31-52: batches restart at every file)
 __device__ __forceinline__ uint32_t event_batch(const uint32_t* files, uint32_t nfiles, uint64_t i) {
     uint32_t lo = 0, hi = nfiles - 1;
@@ -549,7 +563,10 @@ __device__ __forceinline__ SlotDest slot_dest_fast(float x, float y, float z, co
                                                    bool& amb) {
     const int32_t ex = __builtin_amdgcn_frexp_expf(x), ey = __builtin_amdgcn_frexp_expf(y),
                   ez = __builtin_amdgcn_frexp_expf(z);
-    amb = G.exact || !(fmaxf(fmaxf(fabsf(x), fabsf(y)), fabsf(z)) < 0x1p60f) || min(min(ex, ey), ez) < -58;
+    // (non-short-circuit & and |: a && / || chain is emitted as branches, i.e.
+    // exec-mask regions of scalar instructions, in the dense kernel's hot loop)
+    amb = ((int)(G.exact != 0) | (int)!(fmaxf(fmaxf(fabsf(x), fabsf(y)), fabsf(z)) < 0x1p60f) |
+           (int)(min(min(ex, ey), ez) < -58)) != 0;
     SlotDest S;
     {   // hex.rs:67-85
         const float xq = div_rc(x, G.crx, G.inv_crx);
@@ -570,11 +587,11 @@ __device__ __forceinline__ SlotDest slot_dest_fast(float x, float y, float z, co
     const uint32_t off = (uint32_t)(sat_i32(truncf(qu)) - C.uglo);
     S.layer_ok = off <= C.uspan;
     const uint32_t sl = __builtin_amdgcn_ubfe(C.sel, (off & 7u) * 4u, 4u);
-    const bool bad = (((lgx | lgy | lgz) & ~3) != 0) || !S.layer_ok;
+    const bool bad = (((lgx | lgy | lgz) & ~3) != 0) | !S.layer_ok;
     const uint32_t octc = (uint32_t)((lgx >> 1) | (lgy & 2) | ((lgz & 2) << 1));
     const uint32_t octg = (uint32_t)((lgx & 1) | ((lgy & 1) << 1) | ((lgz & 1) << 2));
-    S.d = bad ? -1 : (int32_t)((octc << 1) + octc + (sl & 3u));
-    S.g = bad ? -1 : (int32_t)((octg << 1) + octg + (sl >> 2));
+    S.d = vsel(bad, -1, (int32_t)((octc << 1) + octc + (sl & 3u)));
+    S.g = vsel(bad, -1, (int32_t)((octg << 1) + octg + (sl >> 2)));
     return S;
 }
 // The exact IEEE divisions of slot_route for one lane.
@@ -1496,7 +1513,8 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_tile6(const Point* __restrict__
                                                        uint32_t ngroups, uint32_t* __restrict__ cnt6,
                                                        uint32_t* __restrict__ ph6, uint32_t* __restrict__ gcnt,
                                                        float* __restrict__ part, uint32_t* __restrict__ flag,
-                                                       Arena dummy, uint32_t g0, uint32_t cstride) {
+                                                       Arena dummy, uint32_t g0, uint32_t cstride,
+                                                       const uint32_t* __restrict__ glist = nullptr) {
     constexpr int R = 1 << RB1, HB = kL0LayerBits - RB1, R5 = 8 << HB, HP = R5 + 1;
     using KT = typename std::conditional<KEYS, uint32_t, uint16_t>::type;
     __shared__ float4 sp[kL0Tile];
@@ -1506,9 +1524,11 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_tile6(const Point* __restrict__
     __shared__ uint32_t dbase[R];
     __shared__ uint32_t h[R * HP];
     __shared__ float sb[kL0W][6];
-    // g0: the first group of this launch (uploads, Engine::pre0_count); the run
+    // g0: the first group of this launch (uploads, Engine::pre0_count), or glist:
+    // the launch's groups (input landing in pieces, Engine::input_landed); the run
     // records' rows are cstride tiles apart and the pair-count rows ngroups groups
-    const uint32_t tid = threadIdx.x, w = tid / 64, lane = tid & 63, g = g0 + blockIdx.x;
+    const uint32_t tid = threadIdx.x, w = tid / 64, lane = tid & 63;
+    const uint32_t g = glist ? glist[blockIdx.x] : g0 + blockIdx.x;
     const float4* p4 = reinterpret_cast<const float4*>(in);
     for (int i = tid; i < R * HP; i += kL0BS) h[i] = 0;
     for (int i = tid; i < kL0RW * R / 4; i += kL0BS) reinterpret_cast<uint32_t*>(&wcnt[0][0])[i] = 0;
@@ -2228,6 +2248,7 @@ struct DenseLds {
     uint32_t fj;                   // NaN points in the slot (0, 0) outside the table: the first one's arrival index
     uint32_t nanc[2];              // per chunk parity: a NaN-distance candidate pushed (the walk's NaN rules apply)
 };
+static_assert(sizeof(DenseLds) <= 163840, "the dense slab kernel's LDS");
 
 __device__ __forceinline__ uint32_t hash_slot(uint32_t k) { return (k * 2654435761u) >> 15; }
 
@@ -2267,6 +2288,7 @@ static_assert(kDenseTab < (int)kForeignSlot, "foreign slot key above the table")
 // the table key of a distance: a NaN point that takes an empty slot keeps it
 // (nothing compares less than it, cell.rs:77-80), i.e. key 0
 __device__ __forceinline__ uint32_t dist_key(float d2) { return d2 == d2 ? f2u(d2) : 0u; }
+
 
 // Slot-table entry: (d2 bits << 33) | (dest << 28) | ((g + 1) << 23) | j.  d2 >= +0
 // so its sign bit is free; dest (0..23) and g (grandchild slab inside dest, -1
@@ -2442,13 +2464,16 @@ __device__ __forceinline__ void dense_grid_points(const SlabParams& P, L& S, uin
 // emission's (child, grandchild) slab when its rank is taken.
 // NF: the input has NaN coordinates (the NaN rules below; Engine::nf_mode_).
 // KF: a merge level with forced emissions (kept seeds, P.kf_n > 0).
-template <bool SEEDS, bool NF, bool KF>
+// WIDEOK: a slab of the launch may have 2^23 arrivals or more ("wide"); false
+// compiles the wide paths out of the common launch.
+template <bool SEEDS, bool NF, bool KF, bool WIDEOK = true>
 __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
     using L = DenseLds;
     constexpr int BS = L::BS, TAB = L::TAB, NW = L::NW;
     __shared__ L S;
     STAMP_DECL
-    const uint32_t tid = threadIdx.x, wv = tid / 64, lane = tid & 63;
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(tid / 64);   // (an SGPR)
     const SmallDesc D = P.ddesc[blockIdx.x];
     const uint32_t s = D.s;
     const int32_t t = D.t;
@@ -2459,7 +2484,12 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
         if (tid == 0) set_err(P.ctr, ERR_SLAB_SIZE);
         return;
     }
-    const bool wide = n > kJMaskNarrow;
+    const bool wide = WIDEOK && n > kJMaskNarrow;
+    if (!WIDEOK && n > kJMaskNarrow) {   // (the host launches WIDEOK for such a level)
+        if (tid == 0) set_err(P.ctr, ERR_SLAB_SIZE);
+        return;
+    }
+    const uint32_t wide_u = __builtin_amdgcn_readfirstlane(wide ? 1u : 0u);   // (an SGPR: uniform branches)
     const uint32_t jmask = wide ? kJMask : kJMaskNarrow;
     // merge: the first ng arrivals are the slab's grid seeds (below)
     const uint32_t ng = SEEDS ? min(D.ng, n) : 0u;
@@ -2646,9 +2676,9 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
             if (amb) slot_dest_exact(x, y, z, G, SC, sd);
         }
         const int32_t lx = sd.ox - rx, ly = sd.oy - ry;
-        const bool range_ok = lx >= 0 && ly >= 0 && lx < P.tx && ly < P.ty;
+        const bool range_ok = (lx >= 0) & (ly >= 0) & (lx < P.tx) & (ly < P.ty);
         const bool layer_ok = sd.layer_ok;
-        o.slotted = valid && layer_ok && range_ok;
+        o.slotted = valid & layer_ok & range_ok;
         o.local = o.slotted ? (uint32_t)(ly * P.tx + lx) : 0u;
         float X, Y, Z;
         slot_centre(sd, G.cr, zt, X, Y, Z);
@@ -2664,7 +2694,7 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
         }
         const int d = sd.d;
         o.gn = sd.g;
-        const bool bad = valid && (!layer_ok || (!range_ok && !o.foreign) || d < 0 || (P.check_gchild && o.gn < 0));
+        const bool bad = valid & (!layer_ok | (!range_ok & !o.foreign) | (d < 0) | ((P.check_gchild != 0) & (o.gn < 0)));
         if (__ballot(bad)) {
             if (bad) err |= slot_route_errs(slot_route(x, y, z, G), layer_ok, range_ok, cx, cy, cz, t, P.check_gchild);
         }
@@ -2677,7 +2707,7 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
         const uint32_t tag = ci & 31u;
         const uint32_t j = ng + ci * BS + tid;
         const bool valid = j < n;
-        const bool forced = KF && valid && mine.k - P.kf_lo < P.kf_n;
+        const bool forced = KF && (valid & (mine.k - P.kf_lo < P.kf_n));
         {   // prefetch chunk i+2 (clamped)
             const uint32_t jo = min(j + PF * BS, nm1);
             pf.p = rP.p(jo * 16);
@@ -2691,9 +2721,11 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
         unsigned long long occ = S.tab[local];
         uint32_t hw = S.head[local >> 1];   // the slot's head word, read with the occupant
         // the last step pushes and walks nothing: the head words become the
-        // winner bitmap over the arrivals (all ones; dense_grid_points)
-        if (ci == nchunks && n <= kDenseStreamMax)
-            for (int i = tid; i < (int)((n + 31) / 32); i += BS) S.head[i] = kEmpty32;
+        // winner bitmap over the arrivals (all ones; dense_grid_points).  A
+        // uniform branch and one clamped store per thread (n <= kDenseStreamMax:
+        // at most BS words), so no exec-mask region.
+        static_assert((kDenseStreamMax + 31) / 32 <= (uint32_t)BS, "one bitmap word per thread");
+        if (ci == nchunks && n <= kDenseStreamMax) S.head[min(tid, (n + 31) / 32 - 1)] = kEmpty32;
         const float d2 = cur.si.d2;
         const bool isn = cur.si.isn, foreign = cur.si.foreign;
         const uint32_t dn = cur.si.dn;
@@ -2706,8 +2738,8 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
         // candidates push themselves onto their slot's list.
         bool cand = false;
         uint32_t myprev = kNil;
-        if (slotted && !forced) {
-            cand = occ == kEmpty64 || d2 < __uint_as_float((uint32_t)(occ >> 33));
+        if (slotted & !forced) {
+            cand = (occ == kEmpty64) | (d2 < __uint_as_float((uint32_t)(occ >> 33)));
         } else {
             occ = kEmpty64;
         }
@@ -2715,11 +2747,12 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
             if (cand && isn) S.nanc[par] = 1u;
             if (tid == 0) S.nanc[par ^ 1u] = 0u;   // the other parity's flag (read before the last barrier)
         }
+        const uint32_t sh = (local & 1u) * 16u;
         if (cand) {
             // push onto the slot's list: swap this thread into the head's half of
             // the word (a CAS retried while other pushes change the word); the
             // old head belongs to this chunk only if its tag is this chunk's
-            const uint32_t sh = (local & 1u) * 16u, mineh = (tag << 11) | tid;
+            const uint32_t mineh = (tag << 11) | tid;
             for (;;) {
                 const uint32_t o = atomicCAS(&S.head[local >> 1], hw, (hw & ~(0xFFFFu << sh)) | (mineh << sh));
                 if (o == hw) break;
@@ -2750,15 +2783,16 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
         const uint64_t same = wave_peers<5>((uint32_t)d, vd);
         const uint32_t rw = mask_rank(same);
         if (lane < kDests) reinterpret_cast<uint8_t*>(S.wcnt[lane])[wv] = 0;
-        if (vd && rw == 0) reinterpret_cast<uint8_t*>(S.wcnt[d])[wv] = (uint8_t)__popcll(same);
+        if (vd & (rw == 0)) reinterpret_cast<uint8_t*>(S.wcnt[d])[wv] = (uint8_t)__popcll(same);
         // grandchild capacities: one LDS add per emission
         {
             int32_t gg = prv.g;
-            if (wide && vd && gg == -2) {   // displaced occupant of a wide slab: route its payload
-                gg = slot_dest(__uint_as_float(prv.gp.x), __uint_as_float(prv.gp.y), __uint_as_float(prv.gp.z), G,
-                               SC).g;
+            if (wide_u) {   // block-uniform; a displaced occupant of a wide slab: route its payload
+                if (vd && gg == -2)
+                    gg = slot_dest(__uint_as_float(prv.gp.x), __uint_as_float(prv.gp.y), __uint_as_float(prv.gp.z), G,
+                                   SC).g;
             }
-            if (vd && gg >= 0) {
+            if (vd & (gg >= 0)) {
                 const uint32_t gi = (uint32_t)(d * kDests + gg);
                 atomicAdd(&S.gcnt[gi >> 1], (gi & 1u) ? 0x10000u : 1u);
             }
@@ -2824,85 +2858,91 @@ __global__ __launch_bounds__(kDenseBS) void k_slab(SlabParams P) {
             // lane reads nothing)
             const uint32_t pos = (uint32_t)__shfl((int)base_l, d, 64) + rw;
             const int32_t room = __shfl(room_l, d, 64);
-            const bool ok = vd && (int32_t)rw < room;
-            if (__ballot(vd && !ok)) err |= ERR_CAPACITY;
+            const bool ok = vd & ((int32_t)rw < room);
+            if (__ballot(vd & !ok)) err |= ERR_CAPACITY;
             bst4(oP, ok ? pos * 16 : 0xFFFFFFFFu, prv.em == 1 ? prv.gp : prvb.p);
             bst(oK, ok ? pos * 4 : 0xFFFFFFFFu, prvb.k);
             STAMP(6);
         }
         // ---- phase B (2): records of chunk i (walk of the slot's candidate list)
-        int32_t em = (slotted && !cand && (forced || occ != kEmpty64)) ? 0 : -1;
+        int32_t em = (slotted & !cand & (forced | (occ != kEmpty64))) ? 0 : -1;
         if constexpr (NF) {
             if (__ballot(foreign)) {   // a foreign slot: the first NaN point holds it, the others overflow
                 if (foreign && S.fj != j) em = 0;
             }
         }
-        uint32_t emd = dn;
-        int32_t emg = gn;
-        uint32_t gsrc = 0xFFFFFFFFu;   // byte offset of a displaced point's payload
+        // The decisions after the walk are selects (vsel: each divergent `if`
+        // costs the wave exec-mask SALU, and the scalar unit is shared by the
+        // CU's 16 waves); the LDS accesses stay on the lanes that need them.
+        const uint32_t me = f2u(d2);   // d2 >= +0: the bit patterns order like the values
+        // earliest least earlier candidate (the record before this one, if this
+        // one is a record) and whether a later candidate beats this one
+        uint32_t bd = 0xFFFFFFFFu, bt = kNil;
+        bool beaten = false;
+        // the own entry is skipped (known without LDS reads).  (Both arms of
+        // every select below are computed first: a conditional operator whose
+        // arm is more than a couple of instructions stays a branch.)
+        uint32_t xk = kNil;
         if (cand) {
-            const uint32_t me = f2u(d2);   // d2 >= +0: the bit patterns order like the values
-            // earliest least earlier candidate (the record before this one, if
-            // this one is a record) and whether a later candidate beats this one
-            uint32_t bd = 0xFFFFFFFFu, bt = kNil;
-            bool beaten = false;
-            // branch-free body; the own entry is skipped (known without LDS reads)
-            uint32_t xk = (S.head[local >> 1] >> ((local & 1u) * 16u)) & kNil;
-            if (xk == tid) xk = myprev;
-            uint32_t meff = me;
-            if (!NF || !S.nanc[par]) {
-                while (xk != kNil) {
-                    const uint32_t dx = S.cd2[xk];
-                    const uint32_t nx = S.cnext[xk];
-                    const bool earlier = xk < tid;
-                    const bool better = earlier && (dx < bd || (dx == bd && xk < bt));
-                    bd = better ? dx : bd;
-                    bt = better ? xk : bt;
-                    beaten |= !earlier && dx < me;
-                    xk = nx == tid ? myprev : nx;
-                }
-            } else {
-                // A NaN-distance candidate (the slot was empty) holds the slot iff it
-                // is the earliest candidate; then nothing displaces it (key 0).  Any
-                // other NaN candidate overflows (key kNanKey: never less).
-                uint32_t mt = kNil;   // the earliest earlier candidate
-                while (xk != kNil) {
-                    const uint32_t dx = S.cd2[xk];
-                    const uint32_t nx = S.cnext[xk];
-                    const bool earlier = xk < tid;
-                    const bool better = earlier && (dx < bd || (dx == bd && xk < bt));
-                    bd = better ? dx : bd;
-                    bt = better ? xk : bt;
-                    beaten |= !earlier && dx < me;
-                    mt = earlier && xk < mt ? xk : mt;
-                    xk = nx == tid ? myprev : nx;
-                }
+            xk = (S.head[local >> 1] >> sh) & kNil;
+            xk = xk == tid ? myprev : xk;
+        }
+        uint32_t meff = me;
+        if (!NF || !S.nanc[par]) {
+            while (xk != kNil) {
+                const uint32_t dx = S.cd2[xk];
+                const uint32_t nx = S.cnext[xk];
+                const bool earlier = xk < tid;
+                const bool better = earlier & ((dx < bd) | ((dx == bd) & (xk < bt)));
+                bd = better ? dx : bd;
+                bt = better ? xk : bt;
+                beaten |= !earlier & (dx < me);
+                xk = nx == tid ? myprev : nx;
+            }
+        } else {
+            // A NaN-distance candidate (the slot was empty) holds the slot iff it
+            // is the earliest candidate; then nothing displaces it (key 0).  Any
+            // other NaN candidate overflows (key kNanKey: never less).
+            uint32_t mt = kNil;   // the earliest earlier candidate
+            while (xk != kNil) {
+                const uint32_t dx = S.cd2[xk];
+                const uint32_t nx = S.cnext[xk];
+                const bool earlier = xk < tid;
+                const bool better = earlier && (dx < bd || (dx == bd && xk < bt));
+                bd = better ? dx : bd;
+                bt = better ? xk : bt;
+                beaten |= !earlier && dx < me;
+                mt = earlier && xk < mt ? xk : mt;
+                xk = nx == tid ? myprev : nx;
+            }
+            if (cand) {
                 if (mt != kNil && S.cd2[mt] == kNanKey) { bd = 0u; bt = mt; }
                 if (isn) {
                     meff = bt == kNil ? 0u : kNanKey;
                     beaten = false;
                 }
             }
-            if (bt != kNil && !(meff < bd)) {
-                em = 0;                                // not a record: overflows at its key
-            } else {
-                if (bt != kNil) {                      // displaces the record before it
-                    const uint32_t dg = S.cdg[bt];
-                    em = 1;
-                    emd = dg & 31u;
-                    emg = (int32_t)(dg >> 5) - 1;
-                    gsrc = (ng + ci * BS + bt) * 16;
-                } else if (occ != kEmpty64) {          // first record: displaces the occupant
-                    em = 1;
-                    emd = (uint32_t)(occ >> kJBits) & 31u;
-                    emg = wide ? -2 : (int32_t)(((uint32_t)occ >> 23) & 31u) - 1;
-                    gsrc = ((uint32_t)occ & jmask) * 16;
-                }
-                if (!beaten)                           // last record: the new occupant
-                    S.tab[local] = ((unsigned long long)meff << 33) | ((unsigned long long)dn << kJBits) |
-                                   (wide ? 0u : ((uint32_t)(gn + 1) << 23)) | j;
-            }
         }
+        const bool hasbt = bt != kNil;
+        const bool notrec = hasbt & !(meff < bd);   // not a record: overflows at its key
+        const bool rec = cand & !notrec;
+        uint32_t dg = S.cdg[hasbt ? bt : tid];  // the record before this one (displaced)
+        asm volatile("" : "+v"(dg));            // (not sunk into a branch of its use)
+        const bool dprev = rec & hasbt, docc = rec & !hasbt & (occ != kEmpty64);
+        const int32_t em_c = notrec ? 0 : ((dprev | docc) ? 1 : -1);
+        em = cand ? em_c : em;
+        const uint32_t d_prev = dg & 31u, d_occ = (uint32_t)(occ >> kJBits) & 31u;
+        const int32_t g_prev = (int32_t)(dg >> 5) - 1, g_occ = (int32_t)(((uint32_t)occ >> 23) & 31u) - 1;
+        const int32_t g_occw = wide ? -2 : g_occ;
+        const uint32_t emd = vsel(dprev, d_prev, vsel(docc, d_occ, dn));
+        const int32_t emg = vsel(dprev, g_prev, vsel(docc, g_occw, gn));
+        // byte offset of a displaced point's payload
+        const uint32_t s_prev = (ng + ci * BS + bt) * 16, s_occ = ((uint32_t)occ & jmask) * 16;
+        const uint32_t gsrc = vsel(dprev, s_prev, vsel(docc, s_occ, 0xFFFFFFFFu));
+        // the last record is the new occupant
+        const uint32_t gbits = wide ? 0u : ((uint32_t)(gn + 1) << 23);
+        const unsigned long long ent = ((unsigned long long)meff << 33) | ((unsigned long long)dn << kJBits) | gbits | j;
+        if (rec & !beaten) S.tab[local] = ent;
 #ifdef PCC_XVALU
 #pragma unroll
         for (int xq = 0; xq < PCC_XVALU / 8; xq++) {
@@ -4467,6 +4507,11 @@ void Engine::free_all() {
     dev_release(d_inf_pts_); dev_release(d_inf_keys_);
     d_inf_pts_ = nullptr; d_inf_keys_ = nullptr; inf_cap_ = 0;
     dev_release(d_pre6_cnt_); dev_release(d_pre6_ph_); dev_release(d_pre6_gpar_); dev_release(d_pre6_dummy_);
+    dev_release(d_pre6_glist_);
+    d_pre6_glist_ = nullptr;
+    pre6_glist_cap_ = 0;
+    if (land_ev_) (void)hipEventDestroy(land_ev_);
+    land_ev_ = nullptr;
     d_pre6_cnt_ = d_pre6_ph_ = d_pre6_gpar_ = nullptr;
     d_pre6_dummy_ = nullptr;
     pre6_alloc_tiles_ = pre6_alloc_groups_ = 0;
@@ -5058,6 +5103,9 @@ void Engine::pre0_reset() {
     pre_decided_ = false;
     pre6_ = false;
     pre6_gdone_ = 0;
+    landed_.clear();
+    pre6_done_.clear();
+    pre6_ndone_ = 0;
 }
 
 // pre0_count in its folded form: decides on the first landed piece (sample box
@@ -5110,6 +5158,8 @@ bool Engine::pre6_run(uint64_t upto, hipEvent_t after, bool all) {
         if (!d_pre6_dummy_) dev_alloc_t(d_pre6_dummy_, 256ull * kL0BS * kL0IPT * 20);
         HIP_CHECK(hipMemsetAsync(dev_->bbox_flag, 0, 4, stream_));
         pre6_gdone_ = 0;
+        pre6_src_ = d_in_;
+        pre6_done_.clear();
         pre6_ = true;
     }
     if (!pre6_) return false;
@@ -5129,6 +5179,120 @@ bool Engine::pre6_run(uint64_t upto, hipEvent_t after, bool all) {
     HIP_CHECK(hipGetLastError());
     pre6_gdone_ = gend;
     return true;
+}
+
+// Borrowed device input landing in pieces (a sharded rank's exchange, SURVEY
+// §8e): the same level-0 pass 1 as behind a host upload (pre6_run), on every
+// group of tiles whose points have all landed, in any order (a group's output,
+// run records and pair counts depend on its own tiles only).  The fold is
+// decided once, from the sample box of the first landed range.
+int Engine::input_landed(uint64_t first, uint64_t last, hipStream_t after) {
+    if (!ext_in_ || ext_keys_ || !event_table_ || prior_)   // (keyed input reads keys in pass 1: not this path)
+        return fail(-22, "input_landed: the input must be borrowed with keys NULL and an event table, no merge");
+    last = std::min<uint64_t>(last, n_);
+    if (first >= last) return 0;
+    if (after) {   // the engine's stream waits for the landing stream, the host does not
+        if (!land_ev_) HIP_CHECK(hipEventCreateWithFlags(&land_ev_, hipEventDisableTiming));
+        HIP_CHECK(hipEventRecord(land_ev_, after));
+        HIP_CHECK(hipStreamWaitEvent(stream_, land_ev_, 0));
+    }
+    {   // merge [first, last) into the landed ranges
+        auto& L = landed_;
+        L.push_back({first, last});
+        std::sort(L.begin(), L.end());
+        std::vector<std::pair<uint64_t, uint64_t>> m;
+        for (const auto& r : L) {
+            if (!m.empty() && r.first <= m.back().second) m.back().second = std::max(m.back().second, r.second);
+            else m.push_back(r);
+        }
+        L.swap(m);
+    }
+    const uint64_t ntiles = (n_ + kL0Tile - 1) / kL0Tile;
+    if (!pre_decided_) {
+        // the first range's whole tiles decide the fold (at most two level-0 cells per axis)
+        const uint64_t t0 = (first + kL0Tile - 1) / kL0Tile, t1 = std::min<uint64_t>(last / kL0Tile, ntiles);
+        if (t1 <= t0 && last < n_) return 0;   // decide once a whole tile has landed
+        pre_decided_ = true;
+        pre6_ = false;
+        if (getenv("PCC_NO_PRE6") || getenv("PCC_NO_FOLD") || t1 <= t0) return 0;
+        const uint64_t nt = t1 - t0;
+        const uint32_t nb = (uint32_t)std::min<uint64_t>(nt, 512);
+        k_bbox_sample<<<nb, 256, 0, stream_>>>(ext_in_ + t0 * kL0Tile, nt * kL0Tile, nt, nb, dev_->bbox_part);
+        k_bbox_final<<<1, 256, 0, stream_>>>(dev_->bbox_part, nb);
+        HIP_CHECK(hipGetLastError());
+        float bb[6];
+        HIP_CHECK(hipMemcpyAsync(bb, dev_->bbox_part, sizeof bb, hipMemcpyDeviceToHost, stream_));
+        HIP_CHECK(hipStreamSynchronize(stream_));
+        const float cs = cell_size(cfg_.max_cell_size, 0);
+        for (int a = 0; a < 3; a++) {
+            if (!(std::isfinite(bb[a]) && std::isfinite(bb[3 + a]))) return 0;
+            if ((int64_t)cell_index1(bb[3 + a], cs) - (int64_t)cell_index1(bb[a], cs) >= 2) return 0;
+        }
+        pre6_tcap_ = ntiles;
+        pre6_tpg_ = (uint32_t)std::max<uint64_t>(1, (ntiles + kL0Groups - 1) / kL0Groups);
+        pre6_gcap_ = (uint32_t)((ntiles + pre6_tpg_ - 1) / pre6_tpg_);
+        if (pre6_alloc_tiles_ < pre6_tcap_) {
+            dev_release(d_pre6_cnt_); dev_release(d_pre6_ph_);
+            dev_alloc_t(d_pre6_cnt_, 64 * pre6_tcap_ * 4);
+            dev_alloc_t(d_pre6_ph_, 64 * pre6_tcap_ * 4);
+            pre6_alloc_tiles_ = pre6_tcap_;
+        }
+        if (pre6_alloc_groups_ < pre6_gcap_) {
+            dev_release(d_pre6_gpar_);
+            dev_alloc_t(d_pre6_gpar_, 64ull * pre6_gcap_ * 32 * 4);
+            pre6_alloc_groups_ = pre6_gcap_;
+        }
+        if (pre6_glist_cap_ < pre6_gcap_) {
+            dev_release(d_pre6_glist_);
+            dev_alloc_t(d_pre6_glist_, (uint64_t)pre6_gcap_ * 4);
+            pre6_glist_cap_ = pre6_gcap_;
+        }
+        if (dev_->cap < n_) {
+            for (int a = 0; a < 2; a++) {
+                Arena& A = dev_->ar[a];
+                dev_release(A.p); dev_release(A.k);
+                dev_alloc_t(A.p, n_ * 16); dev_alloc_t(A.k, n_ * 4);
+            }
+            dev_->cap = n_;
+        }
+        pre6_ar1_ = dev_->ar[1].p;
+        if (!d_pre6_dummy_) dev_alloc_t(d_pre6_dummy_, 256ull * kL0BS * kL0IPT * 20);
+        HIP_CHECK(hipMemsetAsync(dev_->bbox_flag, 0, 4, stream_));
+        pre6_src_ = ext_in_;
+        pre6_done_.assign(pre6_gcap_, 0);
+        pre6_glist_.assign(pre6_gcap_, 0);
+        pre6_ndone_ = 0;
+        pre6_gdone_ = 0;
+        pre6_ = true;
+    }
+    if (!pre6_ || pre6_src_ != ext_in_) return 0;
+    // groups whose points have all landed and have not run
+    std::vector<uint32_t> run;
+    for (uint32_t g = 0; g < pre6_gcap_; g++) {
+        if (pre6_done_[g]) continue;
+        const uint64_t a = (uint64_t)g * pre6_tpg_ * kL0Tile;
+        const uint64_t b = std::min<uint64_t>((uint64_t)(g + 1) * pre6_tpg_ * kL0Tile, n_);
+        auto it = std::upper_bound(landed_.begin(), landed_.end(), std::make_pair(a, ~(uint64_t)0));
+        if (it == landed_.begin()) continue;
+        --it;
+        if (it->first <= a && b <= it->second) run.push_back(g);
+    }
+    if (run.empty()) return 0;
+    // every group runs once: the lists go one after another (no reuse, no wait)
+    uint32_t* gl = d_pre6_glist_ + pre6_ndone_;
+    std::copy(run.begin(), run.end(), pre6_glist_.begin() + pre6_ndone_);
+    HIP_CHECK(hipMemcpyAsync(gl, pre6_glist_.data() + pre6_ndone_, run.size() * 4, hipMemcpyHostToDevice, stream_));
+    Arena dummy{static_cast<float4*>(d_pre6_dummy_),
+                reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(d_pre6_dummy_) + 256ull * kL0BS * kL0IPT * 16)};
+    k_l0_tile6<false><<<(uint32_t)run.size(), kL0BS, 0, stream_>>>(ext_in_, nullptr, dev_->ar[1], n_,
+                                                                  l0_base_params(cfg_, 0), (uint32_t)ntiles, pre6_tpg_,
+                                                                  pre6_gcap_, d_pre6_cnt_, d_pre6_ph_, d_pre6_gpar_,
+                                                                  dev_->bbox_part, dev_->bbox_flag, dummy, 0,
+                                                                  (uint32_t)pre6_tcap_, gl);
+    HIP_CHECK(hipGetLastError());
+    for (uint32_t g : run) pre6_done_[g] = 1;
+    pre6_ndone_ += run.size();
+    return 0;
 }
 
 // ---- inputs with non-finite coordinates (kNfNan / kNfInf, see nf_class)
@@ -5648,7 +5812,10 @@ int Engine::level0_bin() {
     // slower in round 4 (level 0 16.6-17.3 against 16.1-17.0 ms, same boxes)
     constexpr int lb = 6;
     constexpr uint32_t R1 = 1u << lb, R2 = 8u << (kL0LayerBits - lb), HB = (uint32_t)(kL0LayerBits - lb);
-    const bool p6 = pre6_ && ntiles && src_ == d_in_ && nsrc_ == n_ && !prior_ && !keyed_ && !ext_in_ &&
+    const bool landing = !pre6_done_.empty();   // pass 1 ran on landed groups of a borrowed input
+    const bool p6 = pre6_ && ntiles && src_ == pre6_src_ && nsrc_ == n_ && !prior_ &&
+                    (landing ? (ext_in_ && !ext_keys_ && event_table_ && ntiles == pre6_tcap_)
+                             : (!keyed_ && !ext_in_ && src_ == d_in_)) &&
                     h0_ == 0 && !nf_mode_ && dev_->ar[1].p == pre6_ar1_ && ntiles <= pre6_tcap_ &&
                     getenv("PCC_NO_FOLD") == nullptr;
     pre6_ = false;   // (consumed: later levels overwrite the arena)
@@ -5676,10 +5843,24 @@ int Engine::level0_bin() {
         if (p6) {
             // the groups the upload did not complete, then the run records and
             // pair counts in this build's layout (rows of ntiles / ngroups)
-            if (ngroups > pre6_gdone_)
+            if (landing) {   // the groups whose points had not all landed
+                const uint64_t n0 = pre6_ndone_;
+                for (uint32_t g = 0; g < ngroups; g++)
+                    if (!pre6_done_[g]) pre6_glist_[pre6_ndone_++] = g;
+                if (pre6_ndone_ > n0) {
+                    HIP_CHECK(hipMemcpyAsync(d_pre6_glist_ + n0, pre6_glist_.data() + n0, (pre6_ndone_ - n0) * 4,
+                                             hipMemcpyHostToDevice, stream_));
+                    k_l0_tile6<false><<<(uint32_t)(pre6_ndone_ - n0), kL0BS, 0, stream_>>>(
+                        src_, nullptr, dev_->ar[1], nsrc_, P, ntiles, tpg, pre6_gcap_, d_pre6_cnt_, d_pre6_ph_,
+                        d_pre6_gpar_, dev_->bbox_part, dev_->bbox_flag, l0dummy, 0, (uint32_t)pre6_tcap_,
+                        d_pre6_glist_ + n0);
+                }
+                pre6_ndone_ = n0;   // (the tiles pass 1 ran on while the input landed)
+            } else if (ngroups > pre6_gdone_) {
                 k_l0_tile6<false><<<ngroups - pre6_gdone_, kL0BS, 0, stream_>>>(
                     src_, nullptr, dev_->ar[1], nsrc_, P, ntiles, tpg, pre6_gcap_, d_pre6_cnt_, d_pre6_ph_, d_pre6_gpar_,
                     dev_->bbox_part, dev_->bbox_flag, l0dummy, pre6_gdone_, (uint32_t)pre6_tcap_);
+            }
             HIP_CHECK(hipMemcpy2DAsync(cnt6, (size_t)ntiles * 4, d_pre6_cnt_, (size_t)pre6_tcap_ * 4, (size_t)ntiles * 4, 64,
                                        hipMemcpyDeviceToDevice, stream_));
             HIP_CHECK(hipMemcpy2DAsync(ph6, (size_t)ntiles * 4, d_pre6_ph_, (size_t)pre6_tcap_ * 4, (size_t)ntiles * 4, 64,
@@ -5715,7 +5896,7 @@ int Engine::level0_bin() {
             bmax_[a] = bb[3 + a];
             fold &= (int64_t)cell_index1(bmax_[a], cs) - (int64_t)cell_index1(bmin_[a], cs) < 2;
         }
-        stats_.pre0_tiles = p6 ? std::min<uint64_t>((uint64_t)pre6_gdone_ * tpg, ntiles) : 0;
+        stats_.pre0_tiles = p6 ? std::min<uint64_t>((uint64_t)(landing ? pre6_ndone_ : pre6_gdone_) * tpg, ntiles) : 0;
     }
     stats_.l0_fold = fold ? 1 : 0;
     if (!fold) {
@@ -6252,7 +6433,8 @@ int Engine::run_level(uint32_t li) {
         else if (SP.kf_n && nf) k_slab<false, true, true><<<L->nbig, kDenseBS, 0, stream_>>>(SP);
         else if (SP.kf_n) k_slab<false, false, true><<<L->nbig, kDenseBS, 0, stream_>>>(SP);
         else if (nf) k_slab<false, true, false><<<L->nbig, kDenseBS, 0, stream_>>>(SP);
-        else k_slab<false, false, false><<<L->nbig, kDenseBS, 0, stream_>>>(SP);
+        else if (L->max_slab > kJMaskNarrow) k_slab<false, false, false><<<L->nbig, kDenseBS, 0, stream_>>>(SP);
+        else k_slab<false, false, false, false><<<L->nbig, kDenseBS, 0, stream_>>>(SP);
         ev_end(ST_DENSE);
         if (verbose) {
             HIP_CHECK(hipStreamSynchronize(stream_));

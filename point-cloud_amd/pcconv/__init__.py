@@ -34,7 +34,7 @@ EXPORTS = ["pcc_abi_version", "pcc_last_error", "pcc_options_default", "pcc_open
            "pcc_convert_files", "pcc_shard_grid_from_bbox", "pcc_synth_device", "pcc_shard_bbox",
            "pcc_shard_bbox_nonfinite", "pcc_set_event_table", "pcc_shard_batch_starts",
            "pcc_shard_histogram", "pcc_shard_route", "pcc_declare_files", "pcc_add_keyed_points_device",
-           "pcc_set_keyed_points_device", "pcc_set_level_range", "pcc_set_root_spill_batches",
+           "pcc_set_keyed_points_device", "pcc_input_landed", "pcc_set_level_range", "pcc_set_root_spill_batches",
            "pcc_pending_cells", "pcc_export_pending", "pcc_shard_slab_histogram", "pcc_shard_route_slabs", "pcc_shard_bbox_histogram", "pcc_shard_bbox_sample",
            "pcc_write_cell_view", "pcc_begin_file", "pcc_append_points", "pcc_end_file", "pcc_cancel_file",
            "pcc_set_summary", "pcc_write_cells", "pcc_write_metadata", "pcc_clear_input", "pcc_adopt_prior",
@@ -53,7 +53,7 @@ class Stats(C.Structure):
     _fields_ = [("number_of_points", C.c_uint64), ("hierarchies", C.c_uint32), ("levels", C.c_uint32),
                 ("cells", C.c_uint64), ("slabs", C.c_uint64), ("arrivals", C.c_uint64),
                 ("grid_points", C.c_uint64), ("kept_points", C.c_uint64), ("build_ms", C.c_double),
-                ("bbox_min", C.c_float * 3), ("bbox_max", C.c_float * 3)]
+                ("bbox_min", C.c_float * 3), ("bbox_max", C.c_float * 3), ("level0_early_tiles", C.c_uint64)]
 
     def as_dict(self) -> dict:
         d = {k: getattr(self, k) for k, _ in self._fields_ if not k.startswith("bbox")}
@@ -156,6 +156,7 @@ def lib():
         L.pcc_declare_files.argtypes = [vp, C.POINTER(C.c_uint64), C.c_uint64]
         L.pcc_add_keyed_points_device.argtypes = [vp, vp, vp, C.c_uint64]
         L.pcc_set_keyed_points_device.argtypes = [vp, vp, vp, C.c_uint64]
+        L.pcc_input_landed.argtypes = [vp, C.c_uint64, C.c_uint64, vp]
         L.pcc_set_level_range.argtypes = [vp, C.c_uint32, C.c_uint32, C.c_int]
         L.pcc_shard_slab_histogram.argtypes = [vp, C.c_uint64, C.POINTER(ShardGrid), C.c_uint32, vp, C.c_int]
         L.pcc_shard_bbox_histogram.argtypes = [vp, C.c_uint64, C.POINTER(ShardGrid), C.c_uint32, vp, f3, f3,
@@ -337,6 +338,12 @@ class Converter:
     def set_keyed_points_device(self, pts_ptr: int, keys_ptr: int, n: int):
         """Borrow (no copy) this rank's keyed input until build() returns."""
         _check(lib().pcc_set_keyed_points_device(self._h, C.c_void_p(pts_ptr), C.c_void_p(keys_ptr), n))
+
+    def input_landed(self, first: int, last: int, after_stream: int = 0):
+        """pcc_input_landed: points [first, last) of the borrowed input are in
+        place once after_stream's queued work completes; level-0 pass 1 of
+        their groups runs behind it (sharded exchange)."""
+        _check(lib().pcc_input_landed(self._h, first, last, C.c_void_p(after_stream or None)))
 
     def set_summary(self, number_of_points: int, bmin, bmax, hierarchies: int):
         _check(lib().pcc_set_summary(self._h, number_of_points, (C.c_float * 3)(*bmin), (C.c_float * 3)(*bmax),

@@ -94,8 +94,10 @@ class TorchComm:
                 req.wait()
         return out
 
-    def _p2p_ops(self, send, send_counts, recv_counts, out) -> list:
-        """The own segment copied locally; the point-to-point ops of the rest."""
+    def _p2p_ops(self, send, send_counts, recv_counts, out, part=(0, 1)) -> list:
+        """The own segment copied locally; the point-to-point ops of the rest.
+        part (r, R): only piece r of R of every segment (round_piece); the own
+        segment is copied whole in piece 0."""
         row = send.element_size() * max(1, int(np.prod(send.shape[1:])))
         mr = max(1, self.max_msg_bytes // row)
         so = np.concatenate([[0], np.cumsum(send_counts)]).astype(np.int64)
@@ -103,18 +105,40 @@ class TorchComm:
         me = self.rank
         if int(send_counts[me]) != int(recv_counts[me]):
             raise ValueError("own segment: send and receive counts differ")
-        if send_counts[me]:
+        if send_counts[me] and part[0] == 0:
             out.narrow(0, int(ro[me]), int(recv_counts[me])).copy_(send.narrow(0, int(so[me]), int(send_counts[me])))
         ops = []
         for k in range(1, self.world):   # peers in ring order from this rank
             p_to, p_from = (me + k) % self.world, (me - k) % self.world
-            for a in range(0, int(send_counts[p_to]), mr):
-                ops.append(self.dist.P2POp(self.dist.isend, send.narrow(0, int(so[p_to]) + a,
-                                                                        min(mr, int(send_counts[p_to]) - a)), p_to))
-            for b in range(0, int(recv_counts[p_from]), mr):
-                ops.append(self.dist.P2POp(self.dist.irecv, out.narrow(0, int(ro[p_from]) + b,
-                                                                       min(mr, int(recv_counts[p_from]) - b)), p_from))
+            a0, a1 = round_piece(int(send_counts[p_to]), *part)
+            for a in range(a0, a1, mr):
+                ops.append(self.dist.P2POp(self.dist.isend, send.narrow(0, int(so[p_to]) + a, min(mr, a1 - a)), p_to))
+            b0, b1 = round_piece(int(recv_counts[p_from]), *part)
+            for b in range(b0, b1, mr):
+                ops.append(self.dist.P2POp(self.dist.irecv, out.narrow(0, int(ro[p_from]) + b, min(mr, b1 - b)),
+                                           p_from))
         return ops
+
+    def alltoallv_rounds(self, send: torch.Tensor, send_counts: list[int], recv_counts: list[int],
+                         out: torch.Tensor, rounds: int, on_landed) -> torch.Tensor:
+        """alltoallv_into in `rounds` grouped batches, piece r of every segment in
+        round r (all peers at once: every xGMI link busy in every round).  Round
+        r + 1 is posted before round r is waited for; after the wait (on the
+        current stream: the host does not block on RCCL) on_landed(ranges,
+        stream) gets round r's received row ranges, so the consumer's work on
+        them queues behind that round while the next one is in flight."""
+        pend = None
+        for r in range(rounds + 1):
+            reqs = None
+            if r < rounds:
+                ops = self._p2p_ops(send, send_counts, recv_counts, out, part=(r, rounds))
+                reqs = self.dist.batch_isend_irecv(ops) if ops else []
+            if pend is not None:
+                for req in pend[0]:
+                    req.wait()
+                on_landed(landed_ranges(recv_counts, self.rank, pend[1], rounds), _stream_handle(out))
+            pend = (reqs, r)
+        return out
 
     def alltoallv_many(self, specs):
         """alltoallv_into for several (send, send_counts, recv_counts, out) in ONE
@@ -182,8 +206,62 @@ class ThreadComm:
         self.g.bar.wait()   # senders may free/reuse their buffers only after every copy
         return out
 
+    def alltoallv_rounds(self, send: torch.Tensor, send_counts: list[int], recv_counts: list[int],
+                         out: torch.Tensor, rounds: int, on_landed) -> torch.Tensor:
+        """TorchComm.alltoallv_rounds between threads: piece r of every segment in
+        round r, then on_landed(round r's row ranges, stream of the copies)."""
+        allv = self._exchange((send, list(send_counts)))
+        ro = np.concatenate([[0], np.cumsum([int(v) for v in recv_counts])]).astype(np.int64)
+        for src in range(self.world):
+            if int(allv[src][1][self.rank]) != int(recv_counts[src]):
+                raise ValueError("receive count differs from the sender's count")
+        for r in range(rounds):
+            for src in range(self.world):
+                t, c = allv[src]
+                o = sum(int(v) for v in c[: self.rank])
+                m = int(c[self.rank])
+                a, b = round_piece(m, r, rounds) if src != self.rank else ((0, m) if r == 0 else (0, 0))
+                if b > a:
+                    out.narrow(0, int(ro[src]) + a, b - a).copy_(t.narrow(0, o + a, b - a))
+            on_landed(landed_ranges(recv_counts, self.rank, r, rounds), _stream_handle(out))
+        if out.is_cuda:   # (the copies read the other threads' buffers)
+            torch.cuda.current_stream(out.device).synchronize()
+        self.g.bar.wait()   # senders may free/reuse their buffers only after every copy
+        return out
+
     def barrier(self):
         self.g.bar.wait()
+
+
+def round_piece(count: int, r: int, rounds: int) -> tuple[int, int]:
+    """Rows [a, b) of a segment of `count` rows that round r of `rounds` carries."""
+    return count * r // rounds, count * (r + 1) // rounds
+
+
+def landed_ranges(recv_counts, me: int, r: int, rounds: int) -> list[tuple[int, int]]:
+    """Row ranges of the receive buffer (segments in source-rank order) that round
+    r of an alltoallv_rounds completes: piece r of every peer's segment, and the
+    own segment (a local copy) in round 0."""
+    ro = np.concatenate([[0], np.cumsum([int(v) for v in recv_counts])]).astype(np.int64)
+    out = []
+    for src, cnt in enumerate(recv_counts):
+        a, b = round_piece(int(cnt), r, rounds) if src != me else ((0, int(cnt)) if r == 0 else (0, 0))
+        if b > a:
+            out.append((int(ro[src]) + a, int(ro[src]) + b))
+    return out
+
+
+def _stream_handle(t: torch.Tensor) -> int:
+    """The current HIP stream of t's device (0 for host tensors).  The null
+    stream cannot be handed to the library (NULL there means "nothing to wait
+    for"), so work on it is waited for here (shard_build exchanges on a side
+    stream instead)."""
+    if not t.is_cuda:
+        return 0
+    s = torch.cuda.current_stream(t.device)
+    if int(s.cuda_stream) == 0:
+        s.synchronize()
+    return int(s.cuda_stream)
 
 
 # ----------------------------------------------------------------- ownership
@@ -771,8 +849,42 @@ class HipShardOps:
         or, with etab (event_table), its points in global key order with
         rank-local keys.  The build reads `pts`/`keys` in place (borrowed until
         it returns)."""
+        self.landing_active = False
         self._record("build", (file_points, pts, keys, etab), first=True)
         return self._keyed_build(self.conv, file_points, pts, keys, etab=etab)
+
+    # the exchange lands the points in this many rounds, level-0 pass 1 running
+    # behind each (pcc_input_landed); 0 or 1: one exchange, then the build
+    landing_rounds = int(os.environ.get("PCC_LAND_ROUNDS", "4"))
+    landing_active = False
+
+    def begin_landing(self, file_points, recv: torch.Tensor, etab):
+        """Borrow `recv` (rank-local keys, etab) before the exchange fills it."""
+        self._ready()
+        c = self.conv
+        c.clear_input()
+        c.set_event_table(*etab)
+        c.set_keyed_points_device(recv.data_ptr(), 0, recv.shape[0])
+        self.landing_active = True
+        self._landing = (file_points, recv, etab, c)
+
+    def landed(self, ranges, stream: int):
+        """Row ranges of the borrowed input that the exchange's work queued on
+        `stream` so far writes: pass 1 of the groups they complete queues behind."""
+        c = self._landing[3]
+        for a, b in ranges:
+            c.input_landed(a, b, stream)
+
+    def build_landed(self) -> dict:
+        file_points, recv, etab, c = self._landing
+        self._landing = None
+        self.landing_active = False
+        self._record("build", (file_points, recv, None, etab), first=True)
+        self._ready()
+        st = c.build()
+        if c not in getattr(self, "_built", []):
+            self._built = getattr(self, "_built", []) + [c]
+        return st
 
     # Diagnostics only (scripts/rank_stages.py replays a step's local calls): with
     # record_inputs set, every stage's device inputs are kept in last_inputs until
@@ -1179,6 +1291,27 @@ def shard_build(comm, ops, pts: torch.Tensor, key0: int, file_points, write: boo
             if nsplit:
                 streams.append((sum(int(v) for v in counts[:W]), [int(v) for v in counts[W:]], W))
             got = []
+            # the points land in rounds while level-0 pass 1 runs on the groups
+            # of tiles each round completes (exchange overlap)
+            rounds = int(getattr(ops, "landing_rounds", 0)) if local_keys and not merge else 0
+            if rounds > 1 and hasattr(comm, "alltoallv_rounds") and comm.device == dev:
+                cw = streams[0][1]
+                rc = comm.alltoall_counts(cw)
+                rbm = _exchange_many(comm, [(bm.narrow(0, 0, W).reshape(-1), [nwl] * W, rw)], dev)[0]
+                gs, gb, nbt = global_batches(file_points, ops.batch_size)
+                etab = event_table(ops.batch_starts(rbm, rw, k0, gs), gb, sum(rc), nbt)
+                recv = torch.empty((sum(rc),) + tuple(send.shape[1:]), dtype=send.dtype, device=dev)
+                ops.begin_landing(file_points, recv, etab)
+                side = torch.cuda.Stream(dev) if recv.is_cuda else None   # (named to the library per round)
+                if side is not None:
+                    side.wait_stream(torch.cuda.current_stream(dev))
+                    with torch.cuda.stream(side):
+                        comm.alltoallv_rounds(send.narrow(0, 0, sum(cw)), cw, rc, recv, rounds, ops.landed)
+                    torch.cuda.current_stream(dev).wait_stream(side)
+                else:
+                    comm.alltoallv_rounds(send.narrow(0, 0, sum(cw)), cw, rc, recv, rounds, ops.landed)
+                streams = []
+                got.append((recv, None))
             for off, cw, row in streams:
                 rc = comm.alltoall_counts(cw)
                 rp, rbm = _exchange_many(comm, [(send.narrow(0, off, sum(cw)), cw, rc),
@@ -1217,7 +1350,11 @@ def shard_build(comm, ops, pts: torch.Tensor, key0: int, file_points, write: boo
     phases = {"lead": 0, "sub": 0, "whole": 0}
     sub_points = 0
     # 5a. phase 1: the whole level-0 sub-trees this rank owns ...
-    local = ops.build(file_points, recv, keys, etab=etab) if etab is not None else ops.build(file_points, recv, keys)
+    if getattr(ops, "landing_active", False):   # the input already borrowed, pass 1 partly run
+        local = ops.build_landed()
+    else:
+        local = (ops.build(file_points, recv, keys, etab=etab) if etab is not None
+                 else ops.build(file_points, recv, keys))
     parts = [local]
     phases["whole"] = int(local.get("arrivals", 0))
     mark("build")

@@ -292,6 +292,28 @@ class NumpyShardOps:
         for _ in range(total - prev - 1):
             o.add_batch(p[:0])
 
+    # the exchange lands in rounds (HipShardOps.landing_rounds); a test may set 0
+    landing_rounds = 3
+    landing_active = False
+
+    def begin_landing(self, file_points, recv, etab):
+        self.landing_active = True
+        self._landing = (file_points, recv, etab)
+        self.landed_log = []
+
+    def landed(self, ranges, stream):
+        self.landed_log.append([(int(a), int(b)) for a, b in ranges])
+
+    def build_landed(self) -> dict:
+        file_points, recv, etab = self._landing
+        self.landing_active = False
+        pos = 0   # the rounds' ranges tile the receive buffer exactly once
+        for a, b in sorted(r for rs in self.landed_log for r in rs):
+            assert a == pos and b > a, (a, b, pos)
+            pos = b
+        assert pos == len(recv), (pos, len(recv))
+        return self.build(file_points, recv, None, etab)
+
     def build(self, file_points, pts, keys, etab=None) -> dict:
         p = as_points(pts)
         if etab is not None:

@@ -304,6 +304,96 @@ def test_gloo_world2_chunked_exchange_matches_oracle(tmp_path):
     check_against_oracle(tmp_path, files, out, r[0]["summary"])
 
 
+# ------------------------------------------------------------- exchange in rounds (pass 1 behind each)
+def test_round_pieces_and_landed_ranges_tile_the_receive_buffer():
+    from pcconv.dist import landed_ranges, round_piece
+    rng = np.random.default_rng(5)
+    for _ in range(200):
+        world, rounds = int(rng.integers(1, 9)), int(rng.integers(1, 9))
+        rc = [int(v) for v in rng.integers(0, 40, size=world)]
+        me = int(rng.integers(0, world))
+        for cnt in rc:
+            assert [round_piece(cnt, r, rounds) for r in range(rounds)][-1][1] == cnt
+            assert all(round_piece(cnt, r, rounds)[1] == round_piece(cnt, r + 1, rounds)[0] for r in range(rounds - 1))
+        got = sorted(x for r in range(rounds) for x in landed_ranges(rc, me, r, rounds))
+        pos = 0
+        for a, b in got:
+            assert a == pos and b > a
+            pos = b
+        assert pos == sum(rc)
+        assert sum(b - a for a, b in landed_ranges(rc, me, 0, rounds)) >= rc[me]   # the own segment first
+
+
+@pytest.mark.parametrize("rounds,world", [(0, 3), (1, 2), (2, 3), (7, 4)])
+def test_thread_ranks_landing_rounds_match_oracle(tmp_path, rounds, world):
+    """The exchange in `rounds` rounds with the build's input borrowed before it
+    (HipShardOps.begin_landing / landed / build_landed; 0: one exchange, then the
+    build): every round reports its ranges, they tile the receive buffer, and
+    the cloud equals the oracle's."""
+    import threading
+    files = make_input("files")
+    fp = [len(f) for f in files]
+    out = str(tmp_path / "out")
+    grp = ThreadGroup(world)
+    res, logs, errs = [None] * world, [None] * world, []
+
+    def worker(r):
+        try:
+            pts, key0 = rank_slice(files, r, world)
+            ops = NumpyShardOps(out)
+            ops.landing_rounds = rounds
+            res[r] = shard_build(ThreadComm(grp, r, torch.device("cpu")), ops, as_tensor(pts), key0, fp, write=True)
+            logs[r] = getattr(ops, "landed_log", None)
+            ops.close()
+        except BaseException as e:  # noqa: BLE001
+            errs.append(e)
+            grp.bar.abort()
+
+    th = [threading.Thread(target=worker, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs
+    for lg in logs:
+        assert (lg is None) if rounds <= 1 else (len(lg) == rounds)
+    assert all(r.summary == res[0].summary for r in res)
+    check_against_oracle(tmp_path, files, out, res[0].summary)
+
+
+def _gloo_rounds_worker(rank, world, port, out, res_dir, rounds):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        files = make_input("files")
+        pts, key0 = rank_slice(files, rank, world)
+        comm = TorchComm(torch.device("cpu"))
+        comm.max_msg_bytes = 1 << 14   # pieces of rounds in several transfers too
+        ops = NumpyShardOps(out)
+        ops.landing_rounds = rounds
+        r = shard_build(comm, ops, as_tensor(pts), key0, [len(f) for f in files], write=True)
+        ops.close()
+        with open(os.path.join(res_dir, f"rank{rank}.json"), "w") as f:
+            json.dump({"summary": r.summary, "recv": r.recv_points, "log": ops.landed_log}, f)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_exchange_rounds_match_oracle(tmp_path):
+    """TorchComm.alltoallv_rounds over gloo: round r + 1 posted before round r is
+    waited for, each round's ranges handed to the ops, the cloud == the oracle's."""
+    import torch.multiprocessing as mp
+    out, rd = str(tmp_path / "out"), str(tmp_path / "res")
+    os.makedirs(rd)
+    mp.spawn(_gloo_rounds_worker, args=(2, _free_port(), out, rd, 5), nprocs=2, join=True)
+    r = [json.load(open(os.path.join(rd, f"rank{i}.json"))) for i in range(2)]
+    files = make_input("files")
+    assert r[0]["recv"] + r[1]["recv"] == sum(len(f) for f in files)
+    assert all(len(x["log"]) == 5 for x in r)
+    check_against_oracle(tmp_path, files, out, r[0]["summary"])
+
+
 def test_hip_shard_ops_config_and_fresh_dir_guards(tmp_path):
     """HipShardOps refuses (before any device work): a merge whose caller config
     differs from the existing cloud's metadata.json, and a non-merge run into a
@@ -620,3 +710,18 @@ def test_gloo_world2_nonfinite_matches_oracle(tmp_path):
     assert _same_summary(r[0]["summary"], r[1]["summary"])
     assert r[0]["recv"] + r[1]["recv"] == sum(len(f) for f in files)
     check_against_oracle(tmp_path, files, out, r[0]["summary"], cfg=NONFINITE_CFG, batch=5000)
+
+
+def test_global_batches_beyond_2p32_keys():
+    """The batch table of a file structure of more than 2^32 points: 64-bit batch
+    starts, an empty file one empty batch (lib.rs:31-52)."""
+    from pcconv.dist import event_batches, global_batches
+    fp = [(1 << 32) + 12_345, 0, 25_000]
+    gs, gb, nbt = global_batches(fp, 10_000)
+    n0 = ((1 << 32) + 12_345 + 9_999) // 10_000
+    assert nbt == n0 + 1 + 3
+    assert len(gs) == len(gb) == n0 + 3
+    assert gs.dtype == np.uint64 and int(gs[n0 - 1]) == (n0 - 1) * 10_000
+    assert int(gs[n0]) == (1 << 32) + 12_345 and int(gb[n0]) == n0 + 1   # after the empty file's batch
+    k = np.array([0, 9_999, 10_000, (1 << 32) + 12_344, (1 << 32) + 12_345, (1 << 32) + 37_344], dtype=np.int64)
+    assert list(event_batches(k, fp, 10_000)) == [0, 0, 1, n0 - 1, n0 + 1, n0 + 3]

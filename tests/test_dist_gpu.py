@@ -489,3 +489,190 @@ def test_shard_ops_nonfinite_units():
     s2, b2, c2 = ref.route_bitmaps(as_tensor(p), g, owner.cpu(), world, False)
     assert c1 == c2
     assert torch.equal(s1.cpu(), s2) and torch.equal(b1.cpu(), b2)
+
+
+# Rank-local keys (clouds of 2^32 points and more): the batch table of a rank
+# from the exchange bitmaps with 64-bit global keys, and a build whose event
+# batches lie beyond 2^32 / batch, against the oracle fed the same batches.
+def test_shard_batch_starts_64bit_keys_match_numpy():
+    rng = np.random.default_rng(5)
+    key0 = [0, (1 << 32) + 7, (1 << 33) + 100_003, (1 << 34) + 1]   # sparse senders beyond 2^32
+    nwords = [37, 0, 129, 64]
+    words = [rng.integers(0, 2**63 - 1, size=n, dtype=np.int64) for n in nwords]
+    bm = torch.from_numpy(np.concatenate(words)).to(DEV)
+    gs = np.sort(np.concatenate([rng.integers(0, (1 << 34) + 10_000, size=2000, dtype=np.int64),
+                                 np.array(key0, dtype=np.int64), np.array(key0, dtype=np.int64) + 64 * np.array(nwords),
+                                 [0, (1 << 35)]])).astype(np.uint64)
+    got = pcconv.shard_batch_starts(bm.data_ptr(), nwords, key0, gs)
+    ref = NumpyShardOps(None).batch_starts(bm.cpu(), nwords, key0, gs)
+    assert np.array_equal(got, ref)
+
+
+def test_event_table_build_beyond_2p32_keys(tmp_path):
+    """A rank's build with rank-local keys whose event batches are those of a
+    cloud of more than 2^32 points (batch numbers near 5e5 of 10 000 points):
+    the cells equal the oracle's when it is fed the same batch sequence."""
+    from gpu_util import compare_dirs
+    from oracle_ctypes import Oracle
+    from pcconv.dist import event_table
+    cfg = dict(cell_point_overflow_limit=40, sub_grid_dimension=8)
+    p = synth(51, 1, 30_000)
+    rng = np.random.default_rng(3)
+    # 30 000 points spread over batches 430 000 .. 430 300 (keys > 4.3e9), some batches skipped
+    eb = np.sort(rng.choice(np.arange(430_000, 430_300), size=len(p)))
+    starts = np.flatnonzero(np.concatenate([[True], eb[1:] != eb[:-1]]))
+    total = 430_400
+    etab = event_table(starts, eb[starts], len(p), total)
+    go, oo = str(tmp_path / "g"), str(tmp_path / "o")
+    c = pcconv.Converter(go, batch_size=10_000, config=cfg)
+    t = as_tensor(p).to(DEV)
+    c.set_event_table(*etab)
+    c.set_keyed_points_device(t.data_ptr(), 0, len(p))
+    torch.cuda.synchronize()
+    c.build()
+    c.write()
+    c.close()
+    o = Oracle(cfg)
+    NumpyShardOps(None)._feed_table(o, p, etab)
+    assert o.error == 0
+    o.write(oo)
+    o.close()
+    d, mg, mo = compare_dirs(go, oo)
+    assert d == [], d[:5]
+    assert mg == mo
+
+
+# ---- exchange overlap: level-0 pass 1 on the groups of tiles whose points have
+# landed (pcc_input_landed), the build running the rest (SURVEY §8e)
+def _landed_build(out, p, cfg, ranges, stream=0):
+    from pcconv.dist import event_table
+    n = len(p)
+    starts = np.arange(0, n, 10_000)
+    etab = event_table(starts, np.arange(len(starts)), n, len(starts))
+    c = pcconv.Converter(out, batch_size=10_000, config=cfg)
+    t = as_tensor(p).to(DEV)
+    torch.cuda.synchronize()
+    c.set_event_table(*etab)
+    c.set_keyed_points_device(t.data_ptr(), 0, n)
+    for a, b in ranges:
+        c.input_landed(a, b, stream)
+    st = c.build()
+    c.write()
+    c.close()
+    return st
+
+
+@pytest.mark.parametrize("order", ["forward", "shuffled", "overlapping", "partial", "none", "nan", "wide"])
+def test_input_landed_matches_oracle(tmp_path, order):
+    """Ranges landed in any order (overlapping, some never: the build runs those
+    groups) give the oracle's cloud; pass 1 ran early on the landed groups when
+    the level-0 grid folds (at most two cells per axis)."""
+    from gpu_util import compare_dirs
+    cfg = dict(cell_point_overflow_limit=500, sub_grid_dimension=32)
+    n = 700_001
+    # "wide": ten level-0 cells per axis, no fold (pass 1 all inside the build)
+    p = synth(71, 0, n) if order != "wide" else synth(72, 0, n, lo=-5000.0, ext=10000.0)
+    if order == "nan":   # NaN coordinates in a late tile: the build redoes level 0 the non-finite way
+        p["x"][n - 5_000:n - 4_990] = np.nan
+    rng = np.random.default_rng(8)
+    cuts = np.unique(np.concatenate([[0, n], rng.integers(0, n, size=40)]))
+    ranges = [(int(a), int(b)) for a, b in zip(cuts[:-1], cuts[1:])]
+    if order == "shuffled" or order == "nan" or order == "wide":
+        rng.shuffle(ranges)
+    elif order == "overlapping":
+        ranges = [(max(0, a - 5000), min(n, b + 7000)) for a, b in ranges]
+        rng.shuffle(ranges)
+    elif order == "partial":
+        ranges = ranges[::3]
+    elif order == "none":
+        ranges = []
+    go, oo = str(tmp_path / "g"), str(tmp_path / "o")
+    st = _landed_build(go, p, cfg, ranges)
+    assert run_oracle(oo, [p], cfg=cfg)[0] == 0
+    d, mg, mo = compare_dirs(go, oo)
+    assert d == [], d[:5]
+    assert mg == mo
+    if order in ("forward", "shuffled", "overlapping", "partial"):
+        assert st["level0_early_tiles"] > 0, st
+    else:
+        assert st["level0_early_tiles"] == 0, st
+
+
+def test_input_landed_behind_a_stream(tmp_path):
+    """The points copied in on another stream, each piece's range handed over
+    with that stream: the engine's pass 1 waits for the copy, not the host."""
+    from gpu_util import compare_dirs
+    from pcconv.dist import event_table
+    cfg = dict(cell_point_overflow_limit=500, sub_grid_dimension=32)
+    n = 500_000
+    p = synth(73, 0, n)
+    src = as_tensor(p).to(DEV)
+    dst = torch.empty_like(src)
+    starts = np.arange(0, n, 10_000)
+    etab = event_table(starts, np.arange(len(starts)), n, len(starts))
+    go, oo = str(tmp_path / "g"), str(tmp_path / "o")
+    c = pcconv.Converter(go, batch_size=10_000, config=cfg)
+    torch.cuda.synchronize()
+    c.set_event_table(*etab)
+    c.set_keyed_points_device(dst.data_ptr(), 0, n)
+    s = torch.cuda.Stream(DEV)
+    with torch.cuda.stream(s):
+        for a in range(0, n, 100_000):
+            b = min(n, a + 100_000)
+            torch.cuda._sleep(2_000_000)   # the copy lands well after the call returns
+            dst[a:b].copy_(src[a:b])
+            c.input_landed(a, b, s.cuda_stream)
+    st = c.build()
+    c.write()
+    c.close()
+    assert st["level0_early_tiles"] > 0
+    assert run_oracle(oo, [p], cfg=cfg)[0] == 0
+    d, mg, mo = compare_dirs(go, oo)
+    assert d == [], d[:5]
+    assert mg == mo
+
+
+def test_input_landed_refused_without_event_table(tmp_path):
+    c = pcconv.Converter(str(tmp_path / "g"))
+    t = as_tensor(synth(74, 0, 1000)).to(DEV)
+    c.declare_files([1000])
+    c.set_keyed_points_device(t.data_ptr(), 0, 1000)
+    with pytest.raises(pcconv.PccError, match="event table"):
+        c.input_landed(0, 1000)
+    c.close()
+
+
+@pytest.mark.parametrize("rounds", [0, 3])
+def test_sharded_threads_exchange_rounds(tmp_path, rounds):
+    """Thread ranks whose exchange lands in rounds with pass 1 behind each (the
+    product default) or in one exchange: both equal the oracle; with rounds the
+    ranks' level-0 pass 1 ran on landed tiles before the build."""
+    files = [synth(75, 0, 1_200_000)]
+    out = str(tmp_path / "out")
+    fp = [len(f) for f in files]
+    world = 2
+    grp = ThreadGroup(world)
+    res, errs = [None] * world, []
+
+    def worker(r):
+        try:
+            torch.cuda.set_device(DEV)
+            pts, key0 = rank_slice(files, r, world)
+            ops = HipShardOps(0, out_dir=out, config=dict(sub_grid_dimension=32))
+            ops.landing_rounds = rounds
+            t = as_tensor(pts).to(DEV)
+            res[r] = shard_build(ThreadComm(grp, r, DEV), ops, t, key0, fp, write=True)
+            ops.close()
+        except BaseException as e:  # noqa: BLE001
+            errs.append(e)
+            grp.bar.abort()
+
+    th = [threading.Thread(target=worker, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs
+    early = [int(r.local.get("level0_early_tiles", 0)) for r in res]
+    assert all(e > 0 for e in early) if rounds > 1 else all(e == 0 for e in early), early
+    check_against_oracle(tmp_path, files, out, res[0].summary, cfg=dict(sub_grid_dimension=32))
