@@ -58,6 +58,9 @@ typedef struct pcc_stats {
     float bbox_min[3], bbox_max[3];
     uint64_t level0_early_tiles;        /* level-0 tiles (3072 points) whose first pass ran before
                                            pcc_build (behind the upload pieces or pcc_input_landed) */
+    uint32_t level0_fold;               /* level-0 binning: 0 the three/four-pass path; 3 / 6 the two-pass
+                                           fold over cells named by their indices modulo 2 / modulo 4 */
+    uint32_t reserved1;
 } pcc_stats;
 
 /* Per-stage device time of the last pcc_build (HIP events on the engine stream;

@@ -277,7 +277,7 @@ private:
     void ev_end(int stage);
     void ev_collect();
     int level0_bin();
-    bool fold_hint(float cs);
+    int fold_hint(float cs);
     int enter_nonfinite(uint32_t flags);
     int build_infinite();
     // level-0 pass 0 behind the host-to-device copy (add_file_host, streamed files)

@@ -1340,6 +1340,50 @@ __device__ __forceinline__ uint32_t l0_tile_prefix(uint8_t (*cnt)[kL0RW], uint16
     return acc;
 }
 
+// l0_tile_prefix for R > 64 digits: lane t handles the R / 64 consecutive digits
+// t * R / 64 + k, their totals and exclusive bases in tot[k], excl[k].
+template <int R>
+__device__ __forceinline__ void l0_tile_prefix_n(uint8_t (*cnt)[kL0RW], uint16_t (*pre)[kL0RW], uint32_t lane,
+                                                 uint32_t* tot, uint32_t* excl) {
+    constexpr int DPL = R / 64;
+    static_assert(R % 64 == 0 && DPL >= 1, "whole digits per lane");
+    uint32_t sum = 0;
+#pragma unroll
+    for (int k = 0; k < DPL; k++) {
+        const uint32_t d = lane * DPL + k;
+        uint2* c2 = reinterpret_cast<uint2*>(cnt[d]);
+        uint4* p4 = reinterpret_cast<uint4*>(pre[d]);
+        uint32_t acc = 0;
+#pragma unroll 2
+        for (int c = 0; c < kL0RW / 8; c++) {
+            const uint2 wv = c2[c];
+            c2[c] = make_uint2(0u, 0u);
+            uint32_t o[4];
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const uint32_t wd = h ? wv.y : wv.x;
+                const uint32_t b0 = wd & 0xFFu, b1 = (wd >> 8) & 0xFFu, b2 = (wd >> 16) & 0xFFu, b3 = wd >> 24;
+                o[2 * h] = acc | ((acc + b0) << 16);
+                acc += b0 + b1;
+                o[2 * h + 1] = acc | ((acc + b2) << 16);
+                acc += b2 + b3;
+            }
+            p4[c] = make_uint4(o[0], o[1], o[2], o[3]);
+        }
+        tot[k] = acc;
+        excl[k] = sum;   // (lane-local so far)
+        sum += acc;
+    }
+    uint32_t x = sum;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= (uint32_t)d) x += y;
+    }
+#pragma unroll
+    for (int k = 0; k < DPL; k++) excl[k] += x - sum;
+}
+
 // Stores shaped like one tile's output stores (kL0IPT x (16 B + 4 B)) into a
 // scratch area: issued once before a tile loop so the loop is entered with the
 // pending memory ops of its back-edge (the compiler's waits at the loop header
@@ -1507,15 +1551,19 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_down6g(const Point* __restrict_
 // RB1: the low layer bits of pass 1 (6: 64 digits, runs of ~48 points for pass
 // 2; 5: 32 digits, runs of ~96), the pair's high part then the cell parity and
 // the layer's other kL0LayerBits - RB1 bits.
-template <bool KEYS, int RB1 = 6>
-__global__ __launch_bounds__(kL0BS, 8) void k_l0_tile6(const Point* __restrict__ in, const uint32_t* __restrict__ keys,
+// CB: the pair's cell bits, the absolute cell indices modulo 2 (CB = 3: a grid
+// of at most two cells per axis) or modulo 4 (CB = 6: at most four, config 3).
+template <bool KEYS, int RB1 = 6, int CB = 3>
+__global__ __launch_bounds__(kL0BS, CB == 3 ? 8 : 1) void k_l0_tile6(const Point* __restrict__ in, const uint32_t* __restrict__ keys,
                                                        Arena O, uint64_t n, L0Params P, uint32_t ntiles, uint32_t tpg,
                                                        uint32_t ngroups, uint32_t* __restrict__ cnt6,
                                                        uint32_t* __restrict__ ph6, uint32_t* __restrict__ gcnt,
                                                        float* __restrict__ part, uint32_t* __restrict__ flag,
                                                        Arena dummy, uint32_t g0, uint32_t cstride,
                                                        const uint32_t* __restrict__ glist = nullptr) {
-    constexpr int R = 1 << RB1, HB = kL0LayerBits - RB1, R5 = 8 << HB, HP = R5 + 1;
+    constexpr int R = 1 << RB1, HB = kL0LayerBits - RB1, R5 = (1 << CB) << HB, HP = R5 + 1;
+    constexpr uint32_t PB = CB / 3, PM = (1u << PB) - 1u;
+    static_assert(CB == 3 || CB == 6, "cell bits: parity or modulo 4 per axis");
     using KT = typename std::conditional<KEYS, uint32_t, uint16_t>::type;
     __shared__ float4 sp[kL0Tile];
     __shared__ KT sk[kL0Tile];
@@ -1581,7 +1629,7 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_tile6(const Point* __restrict__
             if (valid) {
                 nf |= (ll < 0 || ll >= (int64_t)kL0Layers) ? kNfLayer : 0u;   // (an infinite z too: rebinned apart)
                 d6 = (uint32_t)ll & (R - 1);
-                const uint32_t par = (uint32_t)(ix & 1) | ((uint32_t)(iy & 1) << 1) | ((uint32_t)(iz & 1) << 2);
+                const uint32_t par = ((uint32_t)ix & PM) | (((uint32_t)iy & PM) << PB) | (((uint32_t)iz & PM) << (2 * PB));
                 atomicAdd(&h[d6 * HP + ((par << HB) | (((uint32_t)ll >> RB1) & ((1u << HB) - 1u)))], 1u);
             }
             const uint64_t same = wave_peers<RB1>(d6, valid);
@@ -1667,12 +1715,12 @@ __global__ void k_l0_tstarts(const uint32_t* __restrict__ voff, uint32_t ntiles,
 // none) into the dense-d5 layout k_l0_down5g reads, and the dense histogram
 // bin (d5 << 6 | d6).  A count in a parity slot no dense d5 names is a point
 // outside the grid (pass 2 reports it).
-struct L0PMap { uint8_t s[64]; };
-template <int LB = 6>
+struct L0PMap { uint16_t s[256]; };   // 0xFFFF: none
+template <int LB = 6, int CB = 3>
 __global__ __launch_bounds__(1024) void k_l0_gprefix_par(const uint32_t* __restrict__ gsrc, uint32_t* __restrict__ gdst,
                                                          uint32_t ngroups, uint32_t D, L0PMap pm,
                                                          uint32_t* __restrict__ hist, Counters* ctr) {
-    constexpr int R5 = 8 << (kL0LayerBits - LB), NC = 1024 / R5;
+    constexpr int R5 = (1 << CB) << (kL0LayerBits - LB), NC = 1024 / R5;
     __shared__ uint32_t part[NC][R5];
     const uint32_t d6 = blockIdx.x, d5 = threadIdx.x % R5, c = threadIdx.x / R5;
     const uint32_t gpc = (ngroups + NC - 1) / NC, g0 = min(c * gpc, ngroups), g1 = min(g0 + gpc, ngroups);
@@ -1743,7 +1791,7 @@ __global__ void k_l0_wplan(const L0UnitW* __restrict__ units, uint32_t nunits, u
 __global__ __launch_bounds__(256) void k_l0_uplan(const uint32_t* __restrict__ starts, uint32_t ngroups, uint32_t tpg,
                                                   uint32_t ntiles, uint32_t target, uint32_t umax,
                                                   L0UnitW* __restrict__ uw, uint32_t* __restrict__ wn,
-                                                  uint32_t* __restrict__ out, uint32_t R1) {   // R1 <= 64 rows
+                                                  uint32_t* __restrict__ out, uint32_t R1, int cols) {   // R1 <= 64 rows
     __shared__ uint32_t ub[65];
     const uint32_t tid = threadIdx.x, u = blockIdx.x * 256 + tid;
     if (tid < 64) {   // units per row, exclusive scan over the rows (wave 0)
@@ -1787,8 +1835,25 @@ __global__ __launch_bounds__(256) void k_l0_uplan(const uint32_t* __restrict__ s
         W.t1 = min(g1 * tpg, ntiles);
         W.pad_g0 = min(g0, ngroups - 1);
     }
-    uw[u] = W;
-    wn[u] = (W.b - W.a + kL0Tile - 1) / kL0Tile;
+    uint32_t p = u;
+    if (cols && u < nunits) {
+        // launch position column by column: unit k of every row, then unit k + 1
+        // (concurrent blocks read the same tiles' runs of all 64 digits, whose
+        // boundary lines they share), and in a full column the 8 digits 8x .. 8x + 7
+        // on the blocks of one XCD (block i runs on XCD i mod 8), so neighbours
+        // share the XCD's L2
+        const uint32_t d = W.d6, k = u - ub[d];
+        uint32_t base = 0, q = 0, present = 0;
+        for (uint32_t r = 0; r < 64; r++) {
+            const uint32_t nr = ub[r + 1] - ub[r];
+            base += min(nr, k);
+            present += nr > k ? 1u : 0u;
+            q += (r < d && nr > k) ? 1u : 0u;
+        }
+        p = base + (present == 64 ? (d % 8) * 8 + d / 8 : q);
+    }
+    uw[p] = W;
+    wn[p] = (W.b - W.a + kL0Tile - 1) / kL0Tile;
 }
 __global__ void k_l0_uplan_w0(L0UnitW* __restrict__ uw, const uint32_t* __restrict__ w0, uint32_t umax) {
     const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1875,8 +1940,9 @@ __device__ __forceinline__ int64_t l0_dense_dest(const L0Params& P, float x, flo
 // stored one step before use.
 struct L0Slice { uint32_t tf, ntl, sv, sp; };
 // LB: the low digit's bits (pass 1: 6, or 5 with R5 = 64 high digits)
+// R5 = 256 (fold over at most four cells per axis): one workgroup per CU (LDS).
 template <int R5, bool TM, bool K16 = false, int LB = 6>
-__global__ __launch_bounds__(kL0BS, 8) void k_l0_down5g(Arena S, Arena O, L0Params P, const L0Unit* __restrict__ units,
+__global__ __launch_bounds__(kL0BS, R5 > 64 ? 1 : 8) void k_l0_down5g(Arena S, Arena O, L0Params P, const L0Unit* __restrict__ units,
                                                         const uint32_t* __restrict__ starts, uint32_t ngroups,
                                                         const uint32_t* __restrict__ gpre,
                                                         const uint32_t* __restrict__ cnt_scan,
@@ -1885,8 +1951,9 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_down5g(Arena S, Arena O, L0Para
                                                         const L0UnitW* __restrict__ uw, const uint2* __restrict__ wt,
                                                         const uint32_t* __restrict__ voff,
                                                         const uint32_t* __restrict__ ph6, uint32_t ntiles) {
-    constexpr int R = R5, RB = R5 == 64 ? 6 : R5 == 32 ? 5 : R5 == 16 ? 4 : R5 == 8 ? 3 : 2;
-    static_assert((1 << RB) == R5, "R5 is a power of two in 4..64");
+    constexpr int R = R5, RB = R5 == 256 ? 8 : R5 == 64 ? 6 : R5 == 32 ? 5 : R5 == 16 ? 4 : R5 == 8 ? 3 : 2;
+    static_assert((1 << RB) == R5, "R5 is a power of two in 4..64, or 256");
+    constexpr int DPL = R > 64 ? R / 64 : 1;   // wave 0: digits per lane
     constexpr uint32_t LM = (1u << LB) - 1u;
     // slice entries (tiles per window) staged in LDS; a window over more tiles
     // (a sparse digit) searches the run starts in memory
@@ -1911,12 +1978,17 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_down5g(Arena S, Arena O, L0Para
         a = starts[U.d6 * (ngroups + 1) + U.g0];
         b = starts[U.d6 * (ngroups + 1) + U.g1];
     }
-    uint32_t runr = 0;   // wave 0, lane t < R: next output position of digit t
-    if (w == 0 && lane < (uint32_t)R) {
-        const uint32_t d0 = (lane << LB) | d6u;
-        runr = d0 < D ? cnt_scan[d0] + gpre[((uint64_t)d6u * ngroups + g0u) * R + lane] : 0u;
+    uint32_t runr[DPL];   // wave 0, lane t: next output position of digit t (R <= 64) or t * DPL + k
+#pragma unroll
+    for (int k = 0; k < DPL; k++) {
+        const uint32_t dg = R > 64 ? lane * DPL + k : lane;
+        runr[k] = 0;
+        if (w == 0 && dg < (uint32_t)R) {
+            const uint32_t d0 = (dg << LB) | d6u;
+            runr[k] = d0 < D ? cnt_scan[d0] + gpre[((uint64_t)d6u * ngroups + g0u) * R + dg] : 0u;
+        }
+        gofs[dg & (R - 1)] = runr[k];   // (an LDS write of runr: its load is complete before the loop)
     }
-    gofs[lane & (R - 1)] = runr;   // (an LDS write of runr: its load is complete before the loop)
     for (int i = tid; i < R * kDests; i += kL0BS) hc[i] = 0;
     for (int i = tid; i < kL0RW * R / 4; i += kL0BS) reinterpret_cast<uint32_t*>(&wcnt[0][0])[i] = 0;
     const uint64_t lt = lanemask_lt();
@@ -2022,16 +2094,27 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_down5g(Arena S, Arena O, L0Para
         }
         lds_barrier();
         if (w == 0) {
-            uint32_t ex;
-            const uint32_t tot = l0_tile_prefix<R>(wcnt, wpre, lane, ex);
-            // the LDS addresses are recomputed here, not kept live across the loop
-            // (at the 64-VGPR cap they were spilled, and each reload drained vmcnt)
-            uint32_t ln = lane;
-            asm volatile("" : "+v"(ln));
-            if (ln < (uint32_t)R) {
-                dbase[ln] = ex;
-                gofs[ln] = runr - ex;
-                runr += tot;
+            if constexpr (R > 64) {
+                uint32_t tot[DPL], ex[DPL];
+                l0_tile_prefix_n<R>(wcnt, wpre, lane, tot, ex);
+#pragma unroll
+                for (int k = 0; k < DPL; k++) {
+                    dbase[lane * DPL + k] = ex[k];
+                    gofs[lane * DPL + k] = runr[k] - ex[k];
+                    runr[k] += tot[k];
+                }
+            } else {
+                uint32_t ex;
+                const uint32_t tot = l0_tile_prefix<R>(wcnt, wpre, lane, ex);
+                // the LDS addresses are recomputed here, not kept live across the loop
+                // (at the 64-VGPR cap they were spilled, and each reload drained vmcnt)
+                uint32_t ln = lane;
+                asm volatile("" : "+v"(ln));
+                if (ln < (uint32_t)R) {
+                    dbase[ln] = ex;
+                    gofs[ln] = runr[0] - ex;
+                    runr[0] += tot;
+                }
             }
         }
         lds_barrier();
@@ -5755,9 +5838,32 @@ int Engine::build_infinite() {
 // most two level-0 cells per axis.  Judged from the bounding box of a sample of
 // 512 tiles (the exact box decides after the pass; a wrong guess costs that
 // pass, then the three-pass binning runs).
-bool Engine::fold_hint(float cs) {
+// Pass 2 of the folded binning (tile-major pass-1 output): 32 high digits (cell
+// parities) or 256 (cells modulo 4); 16-bit in-tile keys unless keys were given.
+static void l0_pass2_tm(int fcb, bool keys, uint32_t nblocks, Arena src, Arena dst, const L0Params& P,
+                        const L0Unit* units, const uint32_t* starts, uint32_t ngroups, const uint32_t* gcnt,
+                        const uint32_t* cnt_scan, const uint32_t* sflag, uint32_t D, uint32_t* dcap, Arena dummy,
+                        Counters* ctr, const L0UnitW* uw, const uint2* wt, const uint32_t* cnt6, const uint32_t* ph6,
+                        uint32_t ntiles, hipStream_t st) {
+    if (fcb == 6 && keys)
+        k_l0_down5g<256, true, false><<<nblocks, kL0BS, 0, st>>>(src, dst, P, units, starts, ngroups, gcnt, cnt_scan, sflag,
+                                                                 D, dcap, dummy, ctr, uw, wt, cnt6, ph6, ntiles);
+    else if (fcb == 6)
+        k_l0_down5g<256, true, true><<<nblocks, kL0BS, 0, st>>>(src, dst, P, units, starts, ngroups, gcnt, cnt_scan, sflag,
+                                                                D, dcap, dummy, ctr, uw, wt, cnt6, ph6, ntiles);
+    else if (keys)
+        k_l0_down5g<32, true, false><<<nblocks, kL0BS, 0, st>>>(src, dst, P, units, starts, ngroups, gcnt, cnt_scan, sflag,
+                                                                D, dcap, dummy, ctr, uw, wt, cnt6, ph6, ntiles);
+    else
+        k_l0_down5g<32, true, true><<<nblocks, kL0BS, 0, st>>>(src, dst, P, units, starts, ngroups, gcnt, cnt_scan, sflag,
+                                                               D, dcap, dummy, ctr, uw, wt, cnt6, ph6, ntiles);
+}
+
+// The folded binning's cell bits from a sample of the tiles' bounding box: 3
+// (at most two level-0 cells per axis), 6 (at most four), 0 (no fold).
+int Engine::fold_hint(float cs) {
     const uint64_t ntiles = (nsrc_ + kL0Tile - 1) / kL0Tile;
-    if (ntiles == 0) return false;
+    if (ntiles == 0) return 0;
     const uint32_t nb = (uint32_t)std::min<uint64_t>(ntiles, 512);
     k_bbox_sample<<<nb, 256, 0, stream_>>>(src_, nsrc_, ntiles, nb, dev_->bbox_part);
     k_bbox_final<<<1, 256, 0, stream_>>>(dev_->bbox_part, nb);
@@ -5765,11 +5871,12 @@ bool Engine::fold_hint(float cs) {
     float bb[6];
     HIP_CHECK(hipMemcpyAsync(bb, dev_->bbox_part, sizeof bb, hipMemcpyDeviceToHost, stream_));
     HIP_CHECK(hipStreamSynchronize(stream_));
+    int64_t ext = 0;
     for (int a = 0; a < 3; a++) {
-        if (!(std::isfinite(bb[a]) && std::isfinite(bb[3 + a]))) return false;
-        if ((int64_t)cell_index1(bb[3 + a], cs) - (int64_t)cell_index1(bb[a], cs) >= 2) return false;
+        if (!(std::isfinite(bb[a]) && std::isfinite(bb[3 + a]))) return 0;
+        ext = std::max<int64_t>(ext, (int64_t)cell_index1(bb[3 + a], cs) - (int64_t)cell_index1(bb[a], cs));
     }
-    return true;
+    return ext < 2 ? 3 : (ext < 4 && getenv("PCC_NO_FOLD4") == nullptr) ? 6 : 0;
 }
 
 int Engine::level0_bin() {
@@ -5811,7 +5918,7 @@ int Engine::level0_bin() {
     // bits); a 5 + 6 split (pass-2 runs of ~96 points, 64 pass-2 digits) measured
     // slower in round 4 (level 0 16.6-17.3 against 16.1-17.0 ms, same boxes)
     constexpr int lb = 6;
-    constexpr uint32_t R1 = 1u << lb, R2 = 8u << (kL0LayerBits - lb), HB = (uint32_t)(kL0LayerBits - lb);
+    constexpr uint32_t R1 = 1u << lb, HB = (uint32_t)(kL0LayerBits - lb);
     const bool landing = !pre6_done_.empty();   // pass 1 ran on landed groups of a borrowed input
     const bool p6 = pre6_ && ntiles && src_ == pre6_src_ && nsrc_ == n_ && !prior_ &&
                     (landing ? (ext_in_ && !ext_keys_ && event_table_ && ntiles == pre6_tcap_)
@@ -5836,10 +5943,13 @@ int Engine::level0_bin() {
     uint32_t* cnt6 = nullptr;
     uint32_t* ph6 = nullptr;
     uint32_t* gpar = nullptr;
-    if (ntiles && !nf_mode_ && (p6 || fold_hint(cs)) && getenv("PCC_NO_FOLD") == nullptr) {
+    // fcb: the fold's cell bits (k_l0_tile6 CB); pass 2 then has (1 << fcb) << HB digits
+    const int fcb = (ntiles && !nf_mode_ && getenv("PCC_NO_FOLD") == nullptr) ? (p6 ? 3 : fold_hint(cs)) : 0;
+    const uint32_t r2f = fcb ? (1u << fcb) << HB : 0u;
+    if (fcb) {
         cnt6 = static_cast<uint32_t*>(dev_->get(64ull * ntiles * 4));
         ph6 = static_cast<uint32_t*>(dev_->get(64ull * ntiles * 4));
-        gpar = static_cast<uint32_t*>(dev_->get(64ull * ngroups * 32 * 4));
+        gpar = static_cast<uint32_t*>(dev_->get(64ull * ngroups * r2f * 4));
         if (p6) {
             // the groups the upload did not complete, then the run records and
             // pair counts in this build's layout (rows of ntiles / ngroups)
@@ -5869,7 +5979,15 @@ int Engine::level0_bin() {
                                        (size_t)ngroups * 128, 64, hipMemcpyDeviceToDevice, stream_));
         } else {
         HIP_CHECK(hipMemsetAsync(dev_->bbox_flag, 0, 4, stream_));
-        if (l0keys)
+        if (l0keys && fcb == 6)
+            k_l0_tile6<true, 6, 6><<<ngroups, kL0BS, 0, stream_>>>(src_, src_keys_, dev_->ar[1], nsrc_, P, ntiles, tpg,
+                                                                   ngroups, cnt6, ph6, gpar, dev_->bbox_part,
+                                                                   dev_->bbox_flag, l0dummy, 0, ntiles);
+        else if (fcb == 6)
+            k_l0_tile6<false, 6, 6><<<ngroups, kL0BS, 0, stream_>>>(src_, nullptr, dev_->ar[1], nsrc_, P, ntiles, tpg,
+                                                                    ngroups, cnt6, ph6, gpar, dev_->bbox_part,
+                                                                    dev_->bbox_flag, l0dummy, 0, ntiles);
+        else if (l0keys)
             k_l0_tile6<true><<<ngroups, kL0BS, 0, stream_>>>(src_, src_keys_, dev_->ar[1], nsrc_, P, ntiles, tpg, ngroups,
                                                              cnt6, ph6, gpar, dev_->bbox_part, dev_->bbox_flag, l0dummy,
                                                              0, ntiles);
@@ -5894,11 +6012,11 @@ int Engine::level0_bin() {
         for (int a = 0; a < 3; a++) {
             bmin_[a] = bb[a];
             bmax_[a] = bb[3 + a];
-            fold &= (int64_t)cell_index1(bmax_[a], cs) - (int64_t)cell_index1(bmin_[a], cs) < 2;
+            fold &= (int64_t)cell_index1(bmax_[a], cs) - (int64_t)cell_index1(bmin_[a], cs) < (fcb == 3 ? 2 : 4);
         }
         stats_.pre0_tiles = p6 ? std::min<uint64_t>((uint64_t)(landing ? pre6_ndone_ : pre6_gdone_) * tpg, ntiles) : 0;
     }
-    stats_.l0_fold = fold ? 1 : 0;
+    stats_.l0_fold = fold ? (uint32_t)fcb : 0u;
     if (!fold) {
         // the input's tiles already counted while it uploaded (pre0_count): count
         // the rest, then only sum the tiles per group
@@ -5992,7 +6110,7 @@ int Engine::level0_bin() {
     // needs no digit staging array)
     bool g1up = fold || (!P.hashed && passes == 1 && per <= (l0keys ? 4 : 5) && ntiles > 0 &&
                          getenv("PCC_L0_TWO_UPSWEEPS") == nullptr);
-    const uint32_t r5 = (l0keys && !fold) ? 16u : 32u;
+    const uint32_t r5 = fold ? r2f : l0keys ? 16u : 32u;
     // capacities fused into the pass-1 upsweep when the level-1 slab grid fits LDS
     L1Grid Q;
     for (int a = 0; a < 3; a++) { Q.lo[a] = 2 * P.lo[a]; Q.g[a] = 2 * P.g[a]; }
@@ -6038,18 +6156,24 @@ int Engine::level0_bin() {
             k_l0_tstarts<<<grid_for((uint64_t)R1 * (ngroups + 1), 256, 1u << 30), 256, 0, stream_>>>(
                 cnt6, ntiles, tpg, ngroups, nsrc_, starts, R1);
             L0PMap pm;
-            for (uint32_t d5 = 0; d5 < 64; d5++) pm.s[d5] = 0xFF;
-            for (uint32_t d5 = 0; d5 < R2; d5++) {
+            const uint32_t pb = (uint32_t)fcb / 3, pmk = (1u << pb) - 1u;
+            for (uint32_t d5 = 0; d5 < 256; d5++) pm.s[d5] = 0xFFFF;
+            for (uint32_t d5 = 0; d5 < r2f; d5++) {
                 // dense high digit = cell << HB | layer-high bits, cell = (gz * g1 + gy) * g0 + gx
                 const uint32_t cell = d5 >> HB, hi = d5 & ((1u << HB) - 1u);
                 const uint32_t gx = cell % (uint32_t)P.g[0], gy = (cell / (uint32_t)P.g[0]) % (uint32_t)P.g[1];
                 const uint32_t gz = cell / ((uint32_t)P.g[0] * (uint32_t)P.g[1]);
-                if (cell >= G) { pm.s[d5] = 0xFF; continue; }
-                const uint32_t par = ((uint32_t)(P.lo[0] + (int32_t)gx) & 1u) | (((uint32_t)(P.lo[1] + (int32_t)gy) & 1u) << 1) |
-                                     (((uint32_t)(P.lo[2] + (int32_t)gz) & 1u) << 2);
-                pm.s[d5] = (uint8_t)((par << HB) | hi);
+                if (cell >= G) continue;
+                // the cell's slot among the pair counts: absolute indices modulo 2 or 4
+                const uint32_t par = ((uint32_t)(P.lo[0] + (int32_t)gx) & pmk) |
+                                     (((uint32_t)(P.lo[1] + (int32_t)gy) & pmk) << pb) |
+                                     (((uint32_t)(P.lo[2] + (int32_t)gz) & pmk) << (2 * pb));
+                pm.s[d5] = (uint16_t)((par << HB) | hi);
             }
-            k_l0_gprefix_par<lb><<<R1, 1024, 0, stream_>>>(gpar, gcnt, ngroups, (uint32_t)D, pm, hist, dev_->ctr);
+            if (fcb == 6)
+                k_l0_gprefix_par<lb, 6><<<R1, 1024, 0, stream_>>>(gpar, gcnt, ngroups, (uint32_t)D, pm, hist, dev_->ctr);
+            else
+                k_l0_gprefix_par<lb><<<R1, 1024, 0, stream_>>>(gpar, gcnt, ngroups, (uint32_t)D, pm, hist, dev_->ctr);
         } else {
             if (l0keys) k_l0_gprefix<16><<<64, 1024, 0, stream_>>>(gcnt, ngroups, (uint32_t)D, hist, dev_->ctr);
             else k_l0_gprefix<32><<<64, 1024, 0, stream_>>>(gcnt, ngroups, (uint32_t)D, hist, dev_->ctr);
@@ -6143,18 +6267,12 @@ int Engine::level0_bin() {
         uint32_t* dwn = static_cast<uint32_t*>(dev_->get((uint64_t)umax * 4));
         HIP_CHECK(hipMemsetAsync(L->dcap, 0, (uint64_t)L->nslabs * kDests * 4, stream_));
         k_l0_uplan<<<(umax + 255) / 256, 256, 0, stream_>>>(starts, ngroups, tpg, ntiles, (uint32_t)target, umax, duw,
-                                                            dwn, dcnt, R1);
+                                                            dwn, dcnt, R1, getenv("PCC_L0_COLS") ? 1 : 0);
         scan_excl_u32(dwn, dwn, umax, dcnt + 1, dev_->scan, stream_);
         k_l0_uplan_w0<<<(umax + 255) / 256, 256, 0, stream_>>>(duw, dwn, umax);
         k_l0_wplan<<<grid_for(wmax, 256, 1u << 30), 256, 0, stream_>>>(duw, 0, 0, cnt6, ntiles, dwt, dcnt);
-        if (l0keys)
-            k_l0_down5g<32, true, false><<<umax, kL0BS, 0, stream_>>>(src, dst, P, nullptr, starts, ngroups, gcnt,
-                                                                       cnt_scan, sflag, (uint32_t)D, L->dcap, l0dummy,
-                                                                       dev_->ctr, duw, dwt, cnt6, ph6, ntiles);
-        else
-            k_l0_down5g<32, true, true><<<umax, kL0BS, 0, stream_>>>(src, dst, P, nullptr, starts, ngroups, gcnt,
-                                                                      cnt_scan, sflag, (uint32_t)D, L->dcap, l0dummy,
-                                                                      dev_->ctr, duw, dwt, cnt6, ph6, ntiles);
+        l0_pass2_tm(fcb, l0keys, umax, src, dst, P, nullptr, starts, ngroups, gcnt, cnt_scan, sflag, (uint32_t)D,
+                    L->dcap, l0dummy, dev_->ctr, duw, dwt, cnt6, ph6, ntiles, stream_);
         HIP_CHECK(hipGetLastError());
     } else if (g1up) {   // pass 2 into arena 0, with the capacities
         // Units: runs of consecutive segments of one d6 bucket, about nsrc / 8192
@@ -6210,14 +6328,8 @@ int Engine::level0_bin() {
             dwt = static_cast<uint2*>(dev_->get(std::max<uint64_t>(nwin, 1) * sizeof(uint2)));
             HIP_CHECK(hipMemcpyAsync(duw, uw.data(), nunits * sizeof(L0UnitW), hipMemcpyHostToDevice, stream_));
             k_l0_wplan<<<grid_for(nwin, 256, 1u << 30), 256, 0, stream_>>>(duw, nunits, nwin, cnt6, ntiles, dwt, nullptr);
-            if (l0keys)
-                k_l0_down5g<32, true, false><<<nunits, kL0BS, 0, stream_>>>(src, dst, P, dunits, starts, ngroups, gcnt,
-                                                                             cnt_scan, sflag, (uint32_t)D, L->dcap, l0dummy,
-                                                                             dev_->ctr, duw, dwt, cnt6, ph6, ntiles);
-            else
-                k_l0_down5g<32, true, true><<<nunits, kL0BS, 0, stream_>>>(src, dst, P, dunits, starts, ngroups, gcnt,
-                                                                            cnt_scan, sflag, (uint32_t)D, L->dcap, l0dummy,
-                                                                            dev_->ctr, duw, dwt, cnt6, ph6, ntiles);
+            l0_pass2_tm(fcb, l0keys, nunits, src, dst, P, dunits, starts, ngroups, gcnt, cnt_scan, sflag, (uint32_t)D,
+                        L->dcap, l0dummy, dev_->ctr, duw, dwt, cnt6, ph6, ntiles, stream_);
         } else if (nunits && r5 == 16) {
             k_l0_down5g<16, false><<<nunits, kL0BS, 0, stream_>>>(src, dst, P, dunits, starts, ngroups, gcnt, cnt_scan,
                                                                    sflag, (uint32_t)D, L->dcap, l0dummy, dev_->ctr,

@@ -725,3 +725,65 @@ def test_global_batches_beyond_2p32_keys():
     assert int(gs[n0]) == (1 << 32) + 12_345 and int(gb[n0]) == n0 + 1   # after the empty file's batch
     k = np.array([0, 9_999, 10_000, (1 << 32) + 12_344, (1 << 32) + 12_345, (1 << 32) + 37_344], dtype=np.int64)
     assert list(event_batches(k, fp, 10_000)) == [0, 0, 1, n0 - 1, n0 + 1, n0 + 3]
+
+
+# ------------------------------------------------------------- keys past 2^32 on thread ranks
+def phantom_case():
+    """Global keys past 2^32 with synthetic sparse keys: a first file of 2^32
+    points that no rank holds (its batches are empty here), then the real
+    files, whose keys therefore start at 2^32."""
+    real = [synth(81, 0, 60_000), synth(82, 1, 25_001)]
+    return real, [1 << 32] + [len(f) for f in real]
+
+
+def check_phantom_against_oracle(tmp_path, real, fp, out, summary, cfg=None, batch=10_000):
+    """The oracle fed the phantom file's batches empty, then the real files."""
+    from oracle_ctypes import Oracle
+    ref = str(tmp_path / "oracle")
+    o = Oracle(cfg)
+    empty = real[0][:0]
+    for _ in range((fp[0] + batch - 1) // batch):
+        o.add_batch(empty)
+    for f in real:
+        o.add_file(f, batch)
+    assert o.error == 0
+    o.write(ref)
+    o.close()
+    ca, ma = canon.read_dir_fast(ref)
+    cb, mb = canon.read_dir_fast(out)
+    d = canon.diff_fast(ca, cb)
+    assert not d, d[:5]
+    assert summary["number_of_points"] == sum(fp)
+    assert summary["hierarchies"] == ma["hierarchies"] == mb["hierarchies"]
+    assert ma["bmin"] == mb["bmin"] and ma["bmax"] == mb["bmax"]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_thread_ranks_keys_past_2p32_match_oracle(tmp_path, world):
+    """Thread ranks whose global keys start at 2^32 (rank-local keys + event
+    tables over 429 499 global batches) == the oracle fed the same batches."""
+    import threading
+    real, fp = phantom_case()
+    out = str(tmp_path / "out")
+    grp = ThreadGroup(world)
+    res, errs = [None] * world, []
+
+    def worker(r):
+        try:
+            pts, key0 = rank_slice(real, r, world)
+            ops = NumpyShardOps(out)
+            res[r] = shard_build(ThreadComm(grp, r, torch.device("cpu")), ops, as_tensor(pts), key0 + fp[0], fp,
+                                 write=True)
+            ops.close()
+        except BaseException as e:  # noqa: BLE001
+            errs.append(e)
+            grp.bar.abort()
+
+    th = [threading.Thread(target=worker, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs
+    assert all(r.summary == res[0].summary for r in res)
+    check_phantom_against_oracle(tmp_path, real, fp, out, res[0].summary)

@@ -47,6 +47,31 @@ def test_keyed_input_equals_plain_input(tmp_path):
     assert ma == mb
 
 
+@pytest.mark.parametrize("lo,ext,fold", [(-1000.0, 2000.0, 3), (-2000.0, 4000.0, 6)])
+def test_keyed_input_level0_folds(tmp_path, lo, ext, fold):
+    """Keyed device input (pass 1 stages the keys beside the points) through both
+    level-0 folds: 2 and 4 cells per axis, against the plain input's output."""
+    files = [synth(27, 0, 400_000, lo=lo, ext=ext), synth(28, 0, 333_333, lo=lo, ext=ext)]
+    allp = np.concatenate(files)
+    cfg = dict(sub_grid_dimension=48)
+    plain = str(tmp_path / "plain")
+    run_gpu(plain, files, cfg=cfg)
+    keyed = str(tmp_path / "keyed")
+    c = pcconv.Converter(keyed, config=cfg)
+    c.declare_files([len(f) for f in files])
+    pts = as_tensor(allp).to(DEV)
+    keys = torch.arange(len(allp), dtype=torch.int32, device=DEV)
+    torch.cuda.synchronize()
+    c.add_keyed_points_device(pts.data_ptr(), keys.data_ptr(), len(allp))
+    st = c.build()
+    c.write()
+    c.close()
+    assert st["level0_fold"] == fold
+    d, ma, mb = compare_dirs(plain, keyed)
+    assert not d, d
+    assert ma == mb
+
+
 def test_shard_histogram_and_route_match_numpy():
     pts_np = synth(23, 1, 200_001, lo=-2500.0, ext=5000.0)
     pts = as_tensor(pts_np).to(DEV)
@@ -676,3 +701,36 @@ def test_sharded_threads_exchange_rounds(tmp_path, rounds):
     early = [int(r.local.get("level0_early_tiles", 0)) for r in res]
     assert all(e > 0 for e in early) if rounds > 1 else all(e == 0 for e in early), early
     check_against_oracle(tmp_path, files, out, res[0].summary, cfg=dict(sub_grid_dimension=32))
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_threads_keys_past_2p32(tmp_path, world):
+    """Thread ranks with the HIP ops whose global keys start at 2^32 (a first
+    file no rank holds: synthetic sparse keys), rank-local keys and event
+    tables, the exchange in rounds: == the oracle fed the same batches."""
+    from test_dist_cpu import check_phantom_against_oracle, phantom_case
+    real, fp = phantom_case()
+    out = str(tmp_path / "out")
+    grp = ThreadGroup(world)
+    res, errs = [None] * world, []
+
+    def worker(r):
+        try:
+            torch.cuda.set_device(DEV)
+            pts, key0 = rank_slice(real, r, world)
+            ops = HipShardOps(0, out_dir=out)
+            t = as_tensor(pts).to(DEV)
+            res[r] = shard_build(ThreadComm(grp, r, DEV), ops, t, key0 + fp[0], fp, write=True)
+            ops.close()
+        except BaseException as e:  # noqa: BLE001
+            errs.append(e)
+            grp.bar.abort()
+
+    th = [threading.Thread(target=worker, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs
+    assert all(r.summary == res[0].summary for r in res)
+    check_phantom_against_oracle(tmp_path, real, fp, out, res[0].summary)

@@ -327,3 +327,44 @@ def test_wide_slab_over_2_23_arrivals():
     pts["rgba"] = rng.integers(0, 256, (n, 4), dtype=np.uint8)
     st = _check([pts], fast=True)
     assert st["levels"] >= 2
+
+
+def _fold_kind(files, cs=1000.0):
+    """The level-0 binning a cloud takes: 3 (at most two level-0 cells per axis),
+    6 (at most four), 0 (more: the three/four-pass path)."""
+    allp = np.concatenate(files)
+    ext = 0
+    for a in "xyz":
+        v = allp[a].astype(np.float32)
+        ext = max(ext, int(np.floor(v.max() / np.float32(cs))) - int(np.floor(v.min() / np.float32(cs))))
+    return 3 if ext < 2 else 6 if ext < 4 else 0
+
+
+def _reshape(p, sx, ox, sy, oy, sz, oz):
+    q = p.copy()
+    for a, s, o in (("x", sx, ox), ("y", sy, oy), ("z", sz, oz)):
+        q[a] = (q[a] * np.float32(s) + np.float32(o)).astype(np.float32)
+    return q
+
+
+@pytest.mark.parametrize("case,env", [("4x4x4", {}), ("4x4x4", {"PCC_NO_FOLD4": "1"}), ("3x4x2", {}), ("2x3x1", {}),
+                                      ("gauss", {}), ("5x4x4", {})])
+def test_level0_fold_modulo4(case, env, monkeypatch):
+    """The two-pass level-0 fold over grids of up to four cells per axis (cells
+    named by their absolute indices modulo 4, config 3's 64 cells), against the
+    oracle; PCC_NO_FOLD4 and a grid of five cells take the four-pass path."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    if case == "gauss":   # the config-3 generator (Gaussian mixture)
+        files = [synth(91, 2, 900_000), synth(92, 2, 300_001)]
+    else:
+        p = synth(93, 0, 1_200_000, lo=-2000.0, ext=4000.0)   # cells -2 .. 1 on every axis
+        p = {"4x4x4": p, "3x4x2": _reshape(p, 0.75, 500.0, 1.0, 0.0, 0.5, 0.0),
+             "2x3x1": _reshape(p, 0.5, 0.0, 0.75, 500.0, 0.25, 500.0),
+             "5x4x4": _reshape(p, 1.25, 0.0, 1.0, 0.0, 1.0, 0.0)}[case]
+        files = [p[:500_000], p[500_000:]]
+    want = _fold_kind(files)
+    if case.startswith("4") or case.startswith("3"):
+        assert want == 6
+    st = _check(files, cfg=dict(sub_grid_dimension=64, cell_point_overflow_limit=1000), fast=True)
+    assert st["level0_fold"] == (0 if env else want), st
