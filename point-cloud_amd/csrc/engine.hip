@@ -1297,6 +1297,7 @@ __global__ __launch_bounds__(kL0BS) void k_l0_down(const Point* __restrict__ in,
 // counts the level-0 capacities (arrivals per child slab) on the way, which
 // replaces the level-1 histogram pass.
 constexpr uint32_t kL0Groups = 2048;
+constexpr uint32_t kL0Groups6 = 256;   // the modulo-4 fold (k_l0_tile6 CB = 6: 64 KB pair table per group)
 struct L0Unit { uint32_t d6, g0, g1, pad; };
 
 // Per-tile wave counts, digit-major: cnt[d][r * kL0W + q] = lanes of wave q in
@@ -5926,9 +5927,15 @@ int Engine::level0_bin() {
                     h0_ == 0 && !nf_mode_ && dev_->ar[1].p == pre6_ar1_ && ntiles <= pre6_tcap_ &&
                     getenv("PCC_NO_FOLD") == nullptr;
     pre6_ = false;   // (consumed: later levels overwrite the arena)
-    const char* gq = getenv("PCC_L0_GROUPS");
+    // fcb: the fold's cell bits (k_l0_tile6 CB); pass 2 then has (1 << fcb) << HB digits
+    const int fcb = (ntiles && !nf_mode_ && getenv("PCC_NO_FOLD") == nullptr) ? (p6 ? 3 : fold_hint(cs)) : 0;
+    const uint32_t r2f = fcb ? (1u << fcb) << HB : 0u;
+    // (the modulo-4 fold's pair tables are 64 KB per group, written by pass 1 and
+    // scanned over the groups: at most kL0Groups6 groups)
+    const char* gq = getenv(fcb == 6 ? "PCC_L0_GROUPS6" : "PCC_L0_GROUPS");
     uint32_t ngroups = std::max<uint32_t>(1, std::min<uint32_t>(gq ? std::max<uint32_t>(1, (uint32_t)strtoul(gq, nullptr, 10))
-                                                                   : kL0Groups, std::min<uint32_t>(ntiles, kBBoxBlocks)));
+                                                                   : fcb == 6 ? kL0Groups6 : kL0Groups,
+                                                                std::min<uint32_t>(ntiles, kBBoxBlocks)));
     const uint32_t tpg = p6 ? pre6_tpg_ : std::max<uint32_t>(1, (ntiles + ngroups - 1) / ngroups);
     ngroups = std::max<uint32_t>(1, (ntiles + tpg - 1) / tpg);
     uint32_t* gcnt0 = static_cast<uint32_t*>(dev_->get(64ull * ngroups * 4 + 64));
@@ -5943,9 +5950,6 @@ int Engine::level0_bin() {
     uint32_t* cnt6 = nullptr;
     uint32_t* ph6 = nullptr;
     uint32_t* gpar = nullptr;
-    // fcb: the fold's cell bits (k_l0_tile6 CB); pass 2 then has (1 << fcb) << HB digits
-    const int fcb = (ntiles && !nf_mode_ && getenv("PCC_NO_FOLD") == nullptr) ? (p6 ? 3 : fold_hint(cs)) : 0;
-    const uint32_t r2f = fcb ? (1u << fcb) << HB : 0u;
     if (fcb) {
         cnt6 = static_cast<uint32_t*>(dev_->get(64ull * ntiles * 4));
         ph6 = static_cast<uint32_t*>(dev_->get(64ull * ntiles * 4));
@@ -6258,7 +6262,9 @@ int Engine::level0_bin() {
         L->slab_cell, L->slab_layer, L->slab_off, L->slab_n, defer ? d_tot : nullptr);
     if (!defer) k_set_u32<<<1, 1, 0, stream_>>>(L->cell_slab0 + L->ncells, L->nslabs);
     if (defer) {   // pass 2 of the folded binning, planned on the device
-        const uint64_t target = std::max<uint64_t>(nsrc_ / 8192, 4ull * kL0Tile);
+        // units of ~n / 8192 points; with 256 pass-2 digits n / 2048 (each unit
+        // flushes 256 x 24 capacity counters)
+        const uint64_t target = std::max<uint64_t>(nsrc_ / (fcb == 6 ? 2048 : 8192), 4ull * kL0Tile);
         const uint32_t umax = (uint32_t)(64 + (nsrc_ + target - 1) / target);
         const uint32_t wmax = (uint32_t)((nsrc_ + kL0Tile - 1) / kL0Tile) + umax;
         L0UnitW* duw = static_cast<L0UnitW*>(dev_->get((uint64_t)umax * sizeof(L0UnitW)));
@@ -6267,7 +6273,7 @@ int Engine::level0_bin() {
         uint32_t* dwn = static_cast<uint32_t*>(dev_->get((uint64_t)umax * 4));
         HIP_CHECK(hipMemsetAsync(L->dcap, 0, (uint64_t)L->nslabs * kDests * 4, stream_));
         k_l0_uplan<<<(umax + 255) / 256, 256, 0, stream_>>>(starts, ngroups, tpg, ntiles, (uint32_t)target, umax, duw,
-                                                            dwn, dcnt, R1, getenv("PCC_L0_COLS") ? 1 : 0);
+                                                            dwn, dcnt, R1, getenv("PCC_L0_ROWS") ? 0 : 1);
         scan_excl_u32(dwn, dwn, umax, dcnt + 1, dev_->scan, stream_);
         k_l0_uplan_w0<<<(umax + 255) / 256, 256, 0, stream_>>>(duw, dwn, umax);
         k_l0_wplan<<<grid_for(wmax, 256, 1u << 30), 256, 0, stream_>>>(duw, 0, 0, cnt6, ntiles, dwt, dcnt);
@@ -6467,7 +6473,11 @@ int Engine::run_level(uint32_t li) {
     scan_excl_u32(L->slab_n, L->grid_off, L->nslabs, scratch + 1, dev_->scan, stream_);
     // per-level counters, and the child-slab capacities against the next arena
     // (on the device: no host round trip; reported at the level's sync)
-    k_level_begin<<<1, 1, 0, stream_>>>(dev_->ctr, scratch, dev_->cap);
+    // (PCC_TEST_ARENA_CAP: tests shrink the arena seen by the check and the region
+    // clamps, so the clamped kernels and the error path run)
+    uint64_t acap = dev_->cap;
+    if (const char* tc = getenv("PCC_TEST_ARENA_CAP")) acap = std::min<uint64_t>(acap, strtoull(tc, nullptr, 10));
+    k_level_begin<<<1, 1, 0, stream_>>>(dev_->ctr, scratch, acap);
     SlabParams SP;
     SP.in = in;
     SP.nx = nx;
@@ -6532,7 +6542,7 @@ int Engine::run_level(uint32_t li) {
                                                                            L->cell_idx, L->cell_sb, L->dest_off,
                                                                            L->dcap, dd,
                                                                            seeds_in_place ? L->slab_prior : nullptr,
-                                                                           seeds_in_place ? pdev_[h].slabs : nullptr, dev_->cap);
+                                                                           seeds_in_place ? pdev_[h].slabs : nullptr, acap);
         SP.ddesc = dd;
 #ifdef PCC_STAMPS
         SP.stamps = stamps;
@@ -6567,7 +6577,7 @@ int Engine::run_level(uint32_t li) {
         k_small_desc<<<grid_for(L->nsmall, 256, 1u << 30), 256, 0, stream_>>>(
             L->small_list, L->nsmall, L->slab_cell, L->slab_layer, L->slab_off, L->slab_n, L->cell_idx, L->cell_sb,
             L->dest_off, L->dcap, wd, bd, cnt, seeds_in_place ? L->slab_prior : nullptr,
-            seeds_in_place ? pdev_[h].slabs : nullptr, dev_->cap);
+            seeds_in_place ? pdev_[h].slabs : nullptr, acap);
         uint32_t hcnt[4];
         HIP_CHECK(hipMemcpyAsync(hcnt, cnt, 16, hipMemcpyDeviceToHost, stream_));
         HIP_CHECK(hipStreamSynchronize(stream_));
@@ -6680,6 +6690,13 @@ int Engine::run_level(uint32_t li) {
     L->kept_used = hc.kept_cur;
     stats_.grid_points += hg;
     stats_.kept_points += hc.kept_cur;
+    if (hc.err & ERR_ARENA) {
+        char buf[160];
+        snprintf(buf, sizeof buf,
+                 "internal: the child-slab capacities of level %u exceed the next level's arena (their regions "
+                 "were clamped to it; device flags 0x%x)", h, hc.err);
+        return fail(-5, buf);
+    }
     if (hc.err) {
         char buf[200];
         snprintf(buf, sizeof buf,

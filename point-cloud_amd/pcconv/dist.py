@@ -1097,6 +1097,23 @@ def _sub_grid_hist(h, guess, grid, nl: int):
     return v[o[0]:o[0] + d[0], o[1]:o[1] + d[1], o[2]:o[2] + d[2]].contiguous().view(-1)
 
 
+def _attempt(fn, fallback):
+    """(fn(), None), or (fallback, the exception) when this rank's local pass fails."""
+    try:
+        return fn(), None
+    except Exception as e:  # noqa: BLE001 (re-raised by _raise_together after the collective)
+        return fallback, e
+
+
+def _raise_together(err, flag: float, stage: str):
+    """After a collective carrying every rank's error flag: this rank's own error,
+    or an error naming the stage another rank failed in."""
+    if err is not None:
+        raise err
+    if flag > 0:
+        raise RuntimeError(f"shard_build: another rank failed in its {stage} pass")
+
+
 def _fmin(a: float, b: float) -> float:   # f32::min (glam Vec3::min): a NaN operand is skipped
     return b if a != a else (a if b != b else min(a, b))
 
@@ -1164,48 +1181,55 @@ def shard_build(comm, ops, pts: torch.Tensor, key0: int, file_points, write: boo
     from pcconv import SHARD_LAYERS as NL
     inf3, ninf3 = [float("inf")] * 3, [float("-inf")] * 3
     guess, sh_guess, outside, nf_local = None, None, 0, 0
+    # A rank whose local pass fails still joins the collective, with an error flag
+    # in the reduced tensor, so that every rank raises instead of the others
+    # waiting in it forever.
     if getattr(ops, "fused_bbox_hist", False) and not merge and n_total:
-        sbox = ops.bbox_sample(pts) if pts.shape[0] else (inf3, ninf3)
+        sbox, err = _attempt(lambda: ops.bbox_sample(pts) if pts.shape[0] else (inf3, ninf3), (inf3, ninf3))
         if sbox is None:
             nf_local, sbox = 1, (inf3, ninf3)
         smin, smax = sbox
-        sb = torch.tensor([-smin[0], -smin[1], -smin[2], smax[0], smax[1], smax[2], float(nf_local)],
-                          dtype=torch.float32, device=comm.device)
+        sb = torch.tensor([-smin[0], -smin[1], -smin[2], smax[0], smax[1], smax[2], float(nf_local),
+                           1.0 if err else 0.0], dtype=torch.float32, device=comm.device)
         comm.allreduce_(sb, "max")
         sbh = sb.cpu().tolist()
+        _raise_together(err, sbh[7], "bounding-box sample")
         cs = float(ops.cfg_full()["max_cell_size"])
         if sbh[6] == 0:
             g0 = ops.grid([-sbh[0] - cs, -sbh[1] - cs, -sbh[2] - cs], [sbh[3] + cs, sbh[4] + cs, sbh[5] + cs])
             if not int(getattr(g0, "coarse", 0)) and int(g0.ncells) * NL <= (1 << 24):
                 guess = g0
-    bmin, bmax = inf3, ninf3
+    bmin, bmax, err = inf3, ninf3, None
     if guess is not None:
-        r = ops.bbox_slab_histogram(pts, guess)
+        r, err = _attempt(lambda: ops.bbox_slab_histogram(pts, guess), (inf3, ninf3, None, 0))
         if r is None:
             nf_local = 1
         else:
             bmin, bmax, sh_guess, outside = r
     elif pts.shape[0]:
-        r = ops.bbox(pts)
+        r, err = _attempt(lambda: ops.bbox(pts), (inf3, ninf3))
         if r is None:
             nf_local = 1
         else:
             bmin, bmax = r
     bb = torch.tensor([-bmin[0], -bmin[1], -bmin[2], bmax[0], bmax[1], bmax[2], 1.0 if outside else 0.0,
-                       float(nf_local)], dtype=torch.float32, device=comm.device)
+                       float(nf_local), 1.0 if err else 0.0], dtype=torch.float32, device=comm.device)
     comm.allreduce_(bb, "max")
     bbh = bb.cpu().tolist()
+    _raise_together(err, bbh[8], "bounding box")
     gmin, gmax = [-bbh[0], -bbh[1], -bbh[2]], bbh[3:6]
     emin, emax = gmin, gmax   # the extent the ownership grid spans
     nonfinite = bbh[7] > 0
     if bbh[6] > 0 or nonfinite:   # the guess missed some point on some rank
         guess, sh_guess = None, None
     if nonfinite:
-        parts = ops.bbox_nonfinite(pts) if pts.shape[0] else inf3 + ninf3 + [0.0] * 3 + inf3 + ninf3
-        v = torch.tensor([-x if (k < 3 or 9 <= k < 12) else x for k, x in enumerate(parts)], dtype=torch.float32,
-                         device=comm.device)
+        empty_parts = inf3 + ninf3 + [0.0] * 3 + inf3 + ninf3
+        parts, err = _attempt(lambda: ops.bbox_nonfinite(pts) if pts.shape[0] else empty_parts, empty_parts)
+        v = torch.tensor([-x if (k < 3 or 9 <= k < 12) else x for k, x in enumerate(parts)] + [1.0 if err else 0.0],
+                         dtype=torch.float32, device=comm.device)
         comm.allreduce_(v, "max")
         vh = v.cpu().tolist()
+        _raise_together(err, vh[15], "non-finite bounding box")
         gmin = [-vh[a] if vh[6 + a] > 0 else float("nan") for a in range(3)]
         gmax = [vh[3 + a] if vh[6 + a] > 0 else float("nan") for a in range(3)]
         emin, emax = [-vh[9 + a] for a in range(3)], [vh[12 + a] for a in range(3)]

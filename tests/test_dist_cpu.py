@@ -787,3 +787,40 @@ def test_thread_ranks_keys_past_2p32_match_oracle(tmp_path, world):
     assert not errs, errs
     assert all(r.summary == res[0].summary for r in res)
     check_phantom_against_oracle(tmp_path, real, fp, out, res[0].summary)
+
+
+@pytest.mark.parametrize("stage", ["bbox_sample", "bbox_slab_histogram", "bbox"])
+def test_rank_failure_in_bbox_pass_raises_on_every_rank(tmp_path, stage):
+    """One rank's local bounding-box pass raising: every rank raises after the
+    collective (the failing rank its own error, the others a named one) instead
+    of the others waiting in the all-reduce forever."""
+    import threading
+    files = make_input("files")
+    fp = [len(f) for f in files]
+    world = 3
+    grp = ThreadGroup(world)
+    errs = [None] * world
+
+    def worker(r):
+        pts, key0 = rank_slice(files, r, world)
+        ops = NumpyShardOps(str(tmp_path / "out"))
+        if stage == "bbox":
+            ops.fused_bbox_hist = False
+        if r == 1:
+            def boom(*a, **k):
+                raise ValueError("injected failure")
+            setattr(ops, stage, boom)
+        try:
+            shard_build(ThreadComm(grp, r, torch.device("cpu")), ops, as_tensor(pts), key0, fp)
+        except BaseException as e:  # noqa: BLE001
+            errs[r] = e
+
+    th = [threading.Thread(target=worker, args=(r,), daemon=True) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert not any(t.is_alive() for t in th), "a rank is still waiting in a collective"
+    assert isinstance(errs[1], ValueError) and "injected" in str(errs[1])
+    for r in (0, 2):
+        assert isinstance(errs[r], RuntimeError) and "another rank failed" in str(errs[r]), errs[r]

@@ -368,3 +368,17 @@ def test_level0_fold_modulo4(case, env, monkeypatch):
         assert want == 6
     st = _check(files, cfg=dict(sub_grid_dimension=64, cell_point_overflow_limit=1000), fast=True)
     assert st["level0_fold"] == (0 if env else want), st
+
+
+def test_arena_overflow_is_reported(monkeypatch, tmp_path):
+    """Child-slab capacities beyond the next level's arena (forced with a test
+    cap): the clamped kernels run, and the build fails with the arena message."""
+    import pcconv
+    monkeypatch.setenv("PCC_TEST_ARENA_CAP", "1000")
+    c = pcconv.Converter(str(tmp_path / "g"), config=dict(sub_grid_dimension=16, cell_point_overflow_limit=50))
+    try:
+        c.add_points(synth(95, 0, 200_000))
+        with pytest.raises(pcconv.PccError, match="exceed the next level's arena"):
+            c.build()
+    finally:
+        c.close()
