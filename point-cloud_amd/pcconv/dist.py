@@ -251,6 +251,21 @@ def landed_ranges(recv_counts, me: int, r: int, rounds: int) -> list[tuple[int, 
     return out
 
 
+_sides = threading.local()
+
+
+def _side_stream(dev) -> "torch.cuda.Stream":
+    """The calling thread's side stream on `dev` for the exchange rounds (made once:
+    creating a stream per step cost milliseconds)."""
+    d = getattr(_sides, "d", None)
+    if d is None:
+        d = _sides.d = {}
+    key = torch.device(dev).index
+    if key not in d:
+        d[key] = torch.cuda.Stream(dev)
+    return d[key]
+
+
 def _stream_handle(t: torch.Tensor) -> int:
     """The current HIP stream of t's device (0 for host tensors).  The null
     stream cannot be handed to the library (NULL there means "nothing to wait
@@ -1326,7 +1341,7 @@ def shard_build(comm, ops, pts: torch.Tensor, key0: int, file_points, write: boo
                 etab = event_table(ops.batch_starts(rbm, rw, k0, gs), gb, sum(rc), nbt)
                 recv = torch.empty((sum(rc),) + tuple(send.shape[1:]), dtype=send.dtype, device=dev)
                 ops.begin_landing(file_points, recv, etab)
-                side = torch.cuda.Stream(dev) if recv.is_cuda else None   # (named to the library per round)
+                side = _side_stream(dev) if recv.is_cuda else None   # (named to the library per round)
                 if side is not None:
                     side.wait_stream(torch.cuda.current_stream(dev))
                     with torch.cuda.stream(side):
