@@ -280,6 +280,8 @@ private:
     int fold_hint(float cs);
     int enter_nonfinite(uint32_t flags);
     int build_infinite();
+    int build_wide();
+    int replay_seq(const Point* pts, const uint32_t* keys, uint64_t n);
     // level-0 pass 0 behind the host-to-device copy (add_file_host, streamed files)
     void pre0_count(uint64_t upto, hipEvent_t after, bool all);
     void pre0_reset();

@@ -4955,8 +4955,11 @@ int Engine::build() {
     if (cfg_.cell_point_overflow_limit > (1u << 24))
         return fail(-22, "cell_point_overflow_limit > 2^24 is not supported by the GPU build");
     const SlabGeom g = slab_geom(cfg_.sub_grid_dimension);
-    if (g.tx * g.ty > kDenseTab)
-        return fail(-22, "sub_grid_dimension too large for the LDS slot table (max 96)");
+    // sub-grids beyond the LDS slot table or the level-0 layer field (dimension
+    // > 96): the sequential replay (build_wide)
+    const bool wide = g.tx * g.ty > kDenseTab || g.nl > (int32_t)kL0Layers || getenv("PCC_TEST_WIDE") != nullptr;
+    if (wide && (prior_ || h0_ || max_levels_))
+        return fail(-22, "sub_grid_dimension > 96: merges and level ranges are not supported");
     if (prior_ && (h0_ || max_levels_)) return fail(-22, "a merge cannot be split into level ranges");
     hierarchies_ = nbatches_ > 0 ? 1u : 0u;   // converter.rs:141-158 runs for every batch, even empty
     stats_ = BuildStats();
@@ -5043,6 +5046,11 @@ int Engine::build() {
 
     nf_mode_ = false;
     ninf_ = 0;
+    if (wide) {
+        const int rcw = build_wide();
+        stats_.ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        return rcw;
+    }
     ev_begin(ST_L0);
     int rc = level0_bin();   // also computes the bounding box (converter.rs:96-104)
     if (rc) return rc;
@@ -5482,6 +5490,11 @@ __global__ __launch_bounds__(1024) void k_nf_scatter(const Point* __restrict__ i
 // Rare by nature (a data error), so no parallel design: one lane, state in HBM.
 constexpr uint32_t kInfNil = 0xFFFFFFFFu;
 constexpr uint64_t kInfMax = 1ull << 18;   // points with an infinite coordinate per build
+constexpr uint64_t kWideMax = 1ull << 24;  // points per build with a sub-grid beyond the dense table (build_wide)
+__global__ void k_iota_u32(uint32_t* k, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) k[i] = (uint32_t)i;
+}
 struct InfCell {
     int32_t h, x, y, z;
     uint32_t total, number, overflow, nb;
@@ -5758,12 +5771,48 @@ int Engine::build_infinite() {
         if (!(m / cell_size(cfg_.max_cell_size, hl) < 1.0e9f))
             return fail(-22, "finite coordinates that saturate a cell index mixed with infinite ones are not supported");
     }
-    const uint32_t n = (uint32_t)ninf_;
+    return replay_seq(d_inf_pts_, d_inf_keys_, ninf_);
+}
+
+// Sub-grid dimensions beyond the dense slot table (> 96; the reference allows
+// any, metadata.rs:17-18): every point through the sequential replay of the
+// reference's per-batch recursion (k_inf_build: one lane, cell and slot hash
+// tables in HBM), cells as side cells.  A correctness path, not a fast one:
+// about 1 M arrivals per second.  The bounding box in the reference's form
+// (k_bbox_nf: NaN skipped, infinities kept).
+int Engine::build_wide() {
+    if (nsrc_ > kWideMax) return fail(-22, "sub_grid_dimension > 96: more than 2^24 points per build are not supported");
+    const uint32_t nb = (uint32_t)std::min<uint64_t>(std::max<uint64_t>((nsrc_ + 255) / 256, 1), kBBoxBlocks);
+    float* part = static_cast<float*>(dev_->get((uint64_t)nb * kNfParts * 4));
+    k_bbox_nf<<<nb, 256, 0, stream_>>>(src_, nsrc_, part);
+    k_bbox_nf_final<<<1, 64, 0, stream_>>>(part, nb);
+    HIP_CHECK(hipGetLastError());
+    float r[kNfParts];
+    HIP_CHECK(hipMemcpyAsync(r, part, sizeof r, hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    for (int a = 0; a < 3; a++) {
+        bmin_[a] = r[6 + a] != 0.f ? r[a] : NAN;
+        bmax_[a] = r[6 + a] != 0.f ? r[3 + a] : NAN;
+    }
+    const uint32_t* keys = src_keys_;
+    if (!keys) {   // plain or event-table input: the keys are the indices
+        uint32_t* k = static_cast<uint32_t*>(dev_->get(nsrc_ * 4));
+        k_iota_u32<<<grid_for(nsrc_, 256), 256, 0, stream_>>>(k, nsrc_);
+        HIP_CHECK(hipGetLastError());
+        keys = k;
+    }
+    const int rc = replay_seq(src_, keys, nsrc_);
+    stats_.levels = hierarchies_;
+    return rc;
+}
+
+int Engine::replay_seq(const Point* pts, const uint32_t* keys, uint64_t npts) {
+    const uint32_t n = (uint32_t)npts;
     uint32_t hc = 16;
     while (hc < 2 * n) hc <<= 1;
     InfBufs B{};
-    B.pts = d_inf_pts_;
-    B.keys = d_inf_keys_;
+    B.pts = pts;
+    B.keys = keys;
     B.n = n;
     B.files = dev_->files;
     B.nfiles = nfiles_dev_;

@@ -1199,7 +1199,10 @@ def shard_build(comm, ops, pts: torch.Tensor, key0: int, file_points, write: boo
     # A rank whose local pass fails still joins the collective, with an error flag
     # in the reduced tensor, so that every rank raises instead of the others
     # waiting in it forever.
-    if getattr(ops, "fused_bbox_hist", False) and not merge and n_total:
+    # slab units (cell x hex layer) exist for sub-grids of at most 96 (the engine's
+    # level-0 layer field); beyond that, whole cells only
+    wide = int(ops.cfg_full()["sub_grid_dimension"]) > 96 if hasattr(ops, "cfg_full") else False
+    if getattr(ops, "fused_bbox_hist", False) and not merge and n_total and not wide:
         sbox, err = _attempt(lambda: ops.bbox_sample(pts) if pts.shape[0] else (inf3, ninf3), (inf3, ninf3))
         if sbox is None:
             nf_local, sbox = 1, (inf3, ninf3)
@@ -1269,7 +1272,8 @@ def shard_build(comm, ops, pts: torch.Tensor, key0: int, file_points, write: boo
             raise ValueError("sharded merge: the existing cloud's bounding box spans more than 2^22 level-0 cells")
         # (shared cells exchange global u32 keys: none beyond 2^32 points)
         grid1 = (ops.grid(emin, emax, level=1)
-                 if (split and not merge and W > 1 and not coarse and not nonfinite and n_total < (1 << 32)) else None)
+                 if (split and not merge and W > 1 and not coarse and not nonfinite and not wide and n_total < (1 << 32))
+                 else None)
         if grid1 is not None and (int(grid1.ncells) > (1 << 22) or int(grid.ncells) * NL > (1 << 24)):
             grid1 = None
         if grid1 is not None:

@@ -36,7 +36,8 @@ def main(out_dir, name, bench_json):
         e["hbm_bytes"] = 2.0 * e["fetch_bytes_raw"] + e["write_bytes"]
         e["hbm_bytes_per_launch"] = e["hbm_bytes"] / max(e["launches"], 1)
     bench = json.load(open(bench_json))
-    dense = next(v for n, v in k.items() if n.startswith(("pcc::k_slab(", "void pcc::k_slab<false>(", "void pcc::k_slab<false, false>(", "void pcc::k_slab<false, false, false>(")))
+    dense = next(v for n, v in k.items() if n.startswith(("pcc::k_slab(", "void pcc::k_slab<false>(", "void pcc::k_slab<false, false>(", "void pcc::k_slab<false, false, false>(",
+                                                 "void pcc::k_slab<false, false, false, false>(")))
     # level-0 binning: every build kernel launched before the first slab kernel, against
     # one 16-B read and one 20-B write (point + key) per input point
     l0 = {"hbm_bytes": 0.0, "ns": 0, "kernels": []}

@@ -51,6 +51,9 @@ def main(out, subs):
                       "SQ_ACTIVE_INST_LDS", "SQ_WAIT_INST_LDS"):
                 if c in r:
                     d["frac_" + c] = r[c] / wc
+        ns = next((v for k, v in r.items() if k.startswith("ns_")), 0)
+        if wc and ns:   # resident waves per CU over the kernel (quad-cycles x 4, 256 CUs, 2.4 GHz nominal clock)
+            d["waves_per_cu"] = wc * 4.0 / (ns * 2.4 * 256)
         if r.get("SQ_LDS_IDX_ACTIVE"):
             d["lds_bank_conflict_frac"] = r.get("SQ_LDS_BANK_CONFLICT", 0) / r["SQ_LDS_IDX_ACTIVE"]
         if r.get("SQ_INSTS_VALU") and r.get("SQ_INSTS_SALU"):

@@ -824,3 +824,34 @@ def test_rank_failure_in_bbox_pass_raises_on_every_rank(tmp_path, stage):
     assert isinstance(errs[1], ValueError) and "injected" in str(errs[1])
     for r in (0, 2):
         assert isinstance(errs[r], RuntimeError) and "another rank failed" in str(errs[r]), errs[r]
+
+
+def test_thread_ranks_wide_subgrid_match_oracle(tmp_path):
+    """sub_grid_dimension 128 (beyond the slab units): whole cells only, no fused
+    slab histogram, against the oracle."""
+    import threading
+    cfg = dict(sub_grid_dimension=128, cell_point_overflow_limit=300)
+    files = make_input("files")
+    fp = [len(f) for f in files]
+    out = str(tmp_path / "out")
+    world = 3
+    grp = ThreadGroup(world)
+    res, errs = [None] * world, []
+
+    def worker(r):
+        try:
+            pts, key0 = rank_slice(files, r, world)
+            ops = NumpyShardOps(out, config=cfg)
+            res[r] = shard_build(ThreadComm(grp, r, torch.device("cpu")), ops, as_tensor(pts), key0, fp, write=True)
+            ops.close()
+        except BaseException as e:  # noqa: BLE001
+            errs.append(e)
+            grp.bar.abort()
+
+    th = [threading.Thread(target=worker, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs
+    check_against_oracle(tmp_path, files, out, res[0].summary, cfg=cfg)

@@ -734,3 +734,14 @@ def test_sharded_threads_keys_past_2p32(tmp_path, world):
     assert not errs, errs
     assert all(r.summary == res[0].summary for r in res)
     check_phantom_against_oracle(tmp_path, real, fp, out, res[0].summary)
+
+
+def test_sharded_threads_wide_subgrid(tmp_path):
+    """Thread ranks with the HIP ops at sub_grid_dimension 128 (the sequential
+    replay per rank, rank-local keys and event tables): == the oracle."""
+    cfg = dict(sub_grid_dimension=128, cell_point_overflow_limit=300)
+    files = make_input("files")
+    out = str(tmp_path / "out")
+    res = _run_threads(files, 3, out, cfg=cfg)
+    assert sum(r.recv_points for r in res) == sum(len(f) for f in files)
+    check_against_oracle(tmp_path, files, out, res[0].summary, cfg=cfg)

@@ -382,3 +382,23 @@ def test_arena_overflow_is_reported(monkeypatch, tmp_path):
             c.build()
     finally:
         c.close()
+
+
+@pytest.mark.parametrize("dim,n,limit", [(97, 80_000, 200), (128, 120_000, 500), (200, 60_000, 50), (128, 30_001, 1)])
+def test_wide_subgrid_matches_oracle(dim, n, limit):
+    """sub_grid_dimension beyond the dense slot table (> 96, which the
+    reference allows: metadata.rs:17-18) through the sequential replay
+    (build_wide), against the oracle; several files and a ragged batch."""
+    p = synth(96 + dim, 1, n)
+    st = _check([p[: n // 3], p[n // 3:]], cfg=dict(sub_grid_dimension=dim, cell_point_overflow_limit=limit), batch=7_777)
+    assert st["levels"] >= 1
+
+
+def test_wide_path_forced_equals_slab_path(monkeypatch):
+    """The sequential replay forced at a dimension the slab kernels handle
+    (PCC_TEST_WIDE) writes the same cloud as the oracle, NaN and infinite
+    coordinates included."""
+    from nonfinite_input import nonfinite_files
+    monkeypatch.setenv("PCC_TEST_WIDE", "1")
+    _check(nonfinite_files(seed=13, n=20_000, kinds="mixed"), cfg=dict(sub_grid_dimension=16, cell_point_overflow_limit=40))
+    _check([synth(97, 0, 150_000)], cfg=dict(sub_grid_dimension=32, cell_point_overflow_limit=300))
