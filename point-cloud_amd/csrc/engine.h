@@ -13,6 +13,7 @@
 #include <memory>
 #include <string>
 #include <type_traits>
+#include <initializer_list>
 #include <utility>
 #include <vector>
 
@@ -172,6 +173,11 @@ struct BuildStats {
     std::vector<double> ms_level;                  // per level (slab + bucket kernels)
 };
 
+// Engine::readback: up to four small device ranges (multiples of 4 bytes)
+struct RbSrc { const uint32_t* p[4]; uint32_t n[4]; };
+struct RbPart { void* host; const void* dev; size_t bytes; };
+constexpr uint32_t kReadbackWords = 1024;
+
 class Engine {
 public:
     Engine(const Config& cfg, int device, hipStream_t stream = nullptr);
@@ -280,6 +286,11 @@ private:
     int fold_hint(float cs);
     int enter_nonfinite(uint32_t flags);
     int build_infinite();
+    void readback(std::initializer_list<RbPart> parts);
+    void readback_begin(std::initializer_list<RbPart> parts);
+    void readback_end();
+    std::vector<RbPart> rb_parts_;
+    hipEvent_t rb_ev_ = nullptr;
     int build_wide();
     int replay_seq(const Point* pts, const uint32_t* keys, uint64_t n);
     // level-0 pass 0 behind the host-to-device copy (add_file_host, streamed files)

@@ -242,6 +242,8 @@ struct Engine::Dev {
     uint32_t* hst = nullptr;        // pinned host staging of the level-0 segment starts
     uint64_t hst_cap = 0;
     uint32_t* files = nullptr;      // per file: start_lo, start_hi, eb0, batch
+    uint32_t* rb_dev = nullptr;     // readback: small device values gathered into one block,
+    uint32_t* rb_host = nullptr;    //   copied in one transfer to pinned host memory
     ScanTemp scan;
     uint64_t cap = 0;
     // chunked bump allocator for per-build tables and output regions (reset at
@@ -4392,6 +4394,13 @@ __global__ __launch_bounds__(256) void k_l0_lists(const uint32_t* slab_n, uint32
 }
 
 __global__ void k_set_u32(uint32_t* p, uint32_t v) { *p = v; }
+__global__ __launch_bounds__(256) void k_readback(RbSrc r, uint32_t* __restrict__ out) {
+    uint32_t o = 0;
+    for (int k = 0; k < 4; k++) {
+        for (uint32_t i = threadIdx.x; i < r.n[k]; i += 256) out[o + i] = r.p[k][i];
+        o += r.n[k];
+    }
+}
 // A level's counters back to zero, and the sum of its child-slab capacities
 // checked against the next arena (the slab descriptors clamp every region to it)
 __global__ void k_level_begin(Counters* ctr, const uint32_t* cap_total, uint64_t cap) {
@@ -4486,6 +4495,45 @@ Engine::Engine(const Config& cfg, int device, hipStream_t stream) : cfg_(cfg), d
     HIP_CHECK(hipMalloc(&dev_->ctr, sizeof(Counters)));
     HIP_CHECK(hipMalloc(&dev_->bbox_part, kBBoxBlocks * 6 * sizeof(float)));
     HIP_CHECK(hipMalloc(&dev_->bbox_flag, sizeof(uint32_t)));
+    HIP_CHECK(hipMalloc(&dev_->rb_dev, kReadbackWords * 4));
+    HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&dev_->rb_host), kReadbackWords * 4, hipHostMallocDefault));
+}
+
+// Small device values for the host (counters, totals, boxes) in one round trip:
+// a one-block kernel packs up to four word ranges into one device block, one
+// copy moves it to pinned memory, one stream sync, then the host unpacks.
+// (Separate copies into pageable stack variables cost 20-60 us each between
+// kernels, a few per level.)
+void Engine::readback(std::initializer_list<RbPart> parts) {
+    readback_begin(parts);
+    readback_end();
+}
+// begin: queue the pack and the copy, then record an event; end: wait for that
+// event only (work queued after begin keeps running) and unpack
+void Engine::readback_begin(std::initializer_list<RbPart> parts) {
+    RbSrc r{};
+    uint32_t k = 0, words = 0;
+    rb_parts_.assign(parts.begin(), parts.end());
+    for (const RbPart& q : parts) {
+        r.p[k] = static_cast<const uint32_t*>(q.dev);
+        r.n[k] = (uint32_t)(q.bytes / 4);
+        words += r.n[k++];
+    }
+    if (words > kReadbackWords) throw std::runtime_error("readback: too many words");
+    k_readback<<<1, 256, 0, stream_>>>(r, dev_->rb_dev);
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipMemcpyAsync(dev_->rb_host, dev_->rb_dev, (uint64_t)words * 4, hipMemcpyDeviceToHost, stream_));
+    if (!rb_ev_) HIP_CHECK(hipEventCreateWithFlags(&rb_ev_, hipEventDisableTiming));
+    HIP_CHECK(hipEventRecord(rb_ev_, stream_));
+}
+void Engine::readback_end() {
+    HIP_CHECK(hipEventSynchronize(rb_ev_));
+    uint32_t o = 0;
+    for (const RbPart& q : rb_parts_) {
+        std::memcpy(q.host, dev_->rb_host + o, q.bytes);
+        o += (uint32_t)(q.bytes / 4);
+    }
+    rb_parts_.clear();
 }
 
 Engine::~Engine() {
@@ -4569,6 +4617,10 @@ void Engine::free_all() {
         (void)hipFree(dev_->ctr);
         (void)hipFree(dev_->bbox_part);
         (void)hipFree(dev_->bbox_flag);
+        (void)hipFree(dev_->rb_dev);
+        if (rb_ev_) (void)hipEventDestroy(rb_ev_);
+        rb_ev_ = nullptr;
+        if (dev_->rb_host) (void)hipHostFree(dev_->rb_host);
         if (dev_->hst) (void)hipHostFree(dev_->hst);
         (void)hipFree(dev_->scan.bsums);
         for (auto& c : dev_->chunks) dev_release(c.first);
@@ -6053,9 +6105,7 @@ int Engine::level0_bin() {
         HIP_CHECK(hipGetLastError());
         float bb[6];
         uint32_t bad = 0;
-        HIP_CHECK(hipMemcpyAsync(bb, dev_->bbox_part, sizeof bb, hipMemcpyDeviceToHost, stream_));
-        HIP_CHECK(hipMemcpyAsync(&bad, dev_->bbox_flag, 4, hipMemcpyDeviceToHost, stream_));
-        HIP_CHECK(hipStreamSynchronize(stream_));
+        readback({{bb, dev_->bbox_part, sizeof bb}, {&bad, dev_->bbox_flag, 4}});
         if (bad & ~kNfLayer) {   // non-finite coordinates: the exact boxes, infinite points apart, then again
             rc = enter_nonfinite(bad);
             return rc ? rc : level0_bin();
@@ -6090,9 +6140,7 @@ int Engine::level0_bin() {
         HIP_CHECK(hipGetLastError());
         float bb[6];
         uint32_t bad = 0;
-        HIP_CHECK(hipMemcpyAsync(bb, dev_->bbox_part, sizeof bb, hipMemcpyDeviceToHost, stream_));
-        HIP_CHECK(hipMemcpyAsync(&bad, dev_->bbox_flag, 4, hipMemcpyDeviceToHost, stream_));
-        HIP_CHECK(hipStreamSynchronize(stream_));
+        readback({{bb, dev_->bbox_part, sizeof bb}, {&bad, dev_->bbox_flag, 4}});
         if (!nf_mode_) {
             if (bad & ~kNfLayer) {   // non-finite coordinates: the exact boxes, infinite points apart, then again
                 const int rc = enter_nonfinite(bad);
@@ -6276,9 +6324,7 @@ int Engine::level0_bin() {
         scan_excl_u32(sflag, sflag, (uint32_t)D, d_tot + 1, dev_->scan, stream_);
         scan_excl_u32(cflag, cscan, (uint32_t)G, d_tot + 2, dev_->scan, stream_);
         if (!defer) {
-            HIP_CHECK(hipMemcpyAsync(tots, d_tot, 12, hipMemcpyDeviceToHost, stream_));
-            HIP_CHECK(hipMemcpyAsync(&hc, dev_->ctr, sizeof hc, hipMemcpyDeviceToHost, stream_));
-            HIP_CHECK(hipStreamSynchronize(stream_));
+            readback({{tots, d_tot, 12}, {&hc, dev_->ctr, sizeof hc}});
             if (hc.err) return fail(-34, "level-0 binning: point outside the bounding grid (internal error)");
         }
     }
@@ -6414,9 +6460,7 @@ int Engine::level0_bin() {
     k_l0_lists<<<grid_for(L->nslabs, 256, 1u << 30), 256, 0, stream_>>>(L->slab_n, L->nslabs, L->big_list,
                                                                           L->small_list, dev_->ctr, defer ? d_tot + 1 : nullptr);
     if (defer) {   // the level's one sync after the bounding box's: totals, lists, errors
-        HIP_CHECK(hipMemcpyAsync(tots, d_tot, 12, hipMemcpyDeviceToHost, stream_));
-        HIP_CHECK(hipMemcpyAsync(&hc, dev_->ctr, sizeof hc, hipMemcpyDeviceToHost, stream_));
-        HIP_CHECK(hipStreamSynchronize(stream_));
+        readback({{tots, d_tot, 12}, {&hc, dev_->ctr, sizeof hc}});
         ev_end(ST_L0);
         if (hc.err) return fail(-34, "level-0 binning: point outside the bounding grid (internal error)");
         if (tots[0] != nsrc_) return fail(-5, "level-0 histogram mismatch");
@@ -6431,8 +6475,7 @@ int Engine::level0_bin() {
         return 0;
     }
     {
-        HIP_CHECK(hipMemcpyAsync(&hc, dev_->ctr, sizeof hc, hipMemcpyDeviceToHost, stream_));
-        HIP_CHECK(hipStreamSynchronize(stream_));
+        readback({{&hc, dev_->ctr, sizeof hc}});
         L->max_slab = hc.max_slab;
         if (g1up) {
             // capacities counted by k_l0_down5g
@@ -6446,8 +6489,7 @@ int Engine::level0_bin() {
     }
     HIP_CHECK(hipGetLastError());
     ev_end(ST_L0);
-    HIP_CHECK(hipMemcpyAsync(&hc, dev_->ctr, sizeof hc, hipMemcpyDeviceToHost, stream_));
-    HIP_CHECK(hipStreamSynchronize(stream_));
+    readback({{&hc, dev_->ctr, sizeof hc}});
     if (hc.err) return fail(-34, "level-0 capacities: routing error (internal error)");
     L->nbig = hc.nbig;
     L->nsmall = hc.nsmall;
@@ -6573,6 +6615,23 @@ int Engine::run_level(uint32_t li) {
         fprintf(stderr, "[pcc] level %u: cells %u slabs %u (dense %u, small %u) arrivals %llu max_slab %u\n", h, L->ncells,
                 L->nslabs, L->nbig, L->nsmall, (unsigned long long)L->arrivals, L->max_slab);
     }
+    // the small slabs' descriptors and class counts first: their readback
+    // completes while the dense kernel runs, so the small kernels queue behind
+    // it without a host round trip in between
+    SmallDesc* wd = nullptr;
+    SmallDesc* bd = nullptr;
+    uint32_t hcnt[4] = {0, 0, 0, 0};
+    if (L->nsmall) {
+        wd = static_cast<SmallDesc*>(dev_->get((uint64_t)L->nsmall * 3 * sizeof(SmallDesc)));
+        bd = static_cast<SmallDesc*>(dev_->get((uint64_t)L->nsmall * sizeof(SmallDesc)));
+        uint32_t* cnt = static_cast<uint32_t*>(dev_->get(16));
+        HIP_CHECK(hipMemsetAsync(cnt, 0, 16, stream_));
+        k_small_desc<<<grid_for(L->nsmall, 256, 1u << 30), 256, 0, stream_>>>(
+            L->small_list, L->nsmall, L->slab_cell, L->slab_layer, L->slab_off, L->slab_n, L->cell_idx, L->cell_sb,
+            L->dest_off, L->dcap, wd, bd, cnt, seeds_in_place ? L->slab_prior : nullptr,
+            seeds_in_place ? pdev_[h].slabs : nullptr, acap);
+        readback_begin({{hcnt, cnt, 16}});
+    }
     if (L->nbig) {
         SP.list = L->big_list;
         // skewed sizes (the largest slab well above the mean): largest first, so
@@ -6619,17 +6678,7 @@ int Engine::run_level(uint32_t li) {
         SP.stamps = stamps + 16;
 #endif
         ev_begin(ST_SMALL);
-        SmallDesc* wd = static_cast<SmallDesc*>(dev_->get((uint64_t)L->nsmall * 3 * sizeof(SmallDesc)));
-        SmallDesc* bd = static_cast<SmallDesc*>(dev_->get((uint64_t)L->nsmall * sizeof(SmallDesc)));
-        uint32_t* cnt = static_cast<uint32_t*>(dev_->get(16));
-        HIP_CHECK(hipMemsetAsync(cnt, 0, 16, stream_));
-        k_small_desc<<<grid_for(L->nsmall, 256, 1u << 30), 256, 0, stream_>>>(
-            L->small_list, L->nsmall, L->slab_cell, L->slab_layer, L->slab_off, L->slab_n, L->cell_idx, L->cell_sb,
-            L->dest_off, L->dcap, wd, bd, cnt, seeds_in_place ? L->slab_prior : nullptr,
-            seeds_in_place ? pdev_[h].slabs : nullptr, acap);
-        uint32_t hcnt[4];
-        HIP_CHECK(hipMemcpyAsync(hcnt, cnt, 16, hipMemcpyDeviceToHost, stream_));
-        HIP_CHECK(hipStreamSynchronize(stream_));
+        readback_end();
         for (int c = 0; c < 3; c++) {
             if (!hcnt[c]) continue;
             SP.wdesc = wd + (uint64_t)c * L->nsmall;
@@ -6732,10 +6781,7 @@ int Engine::run_level(uint32_t li) {
 #endif
     uint32_t ht[2], hg = 0;
     Counters hc;
-    HIP_CHECK(hipMemcpyAsync(&hg, gtot, 4, hipMemcpyDeviceToHost, stream_));
-    HIP_CHECK(hipMemcpyAsync(ht, tots, 8, hipMemcpyDeviceToHost, stream_));
-    HIP_CHECK(hipMemcpyAsync(&hc, dev_->ctr, sizeof hc, hipMemcpyDeviceToHost, stream_));
-    HIP_CHECK(hipStreamSynchronize(stream_));
+    readback({{&hg, gtot, 4}, {ht, tots, 8}, {&hc, dev_->ctr, sizeof hc}});
     L->kept_used = hc.kept_cur;
     stats_.grid_points += hg;
     stats_.kept_points += hc.kept_cur;
@@ -6809,8 +6855,7 @@ int Engine::run_level(uint32_t li) {
                 d_inj_keys_, dev_->ar[N->arena], N->slab_n);
         ev_end(ST_NEXT);
         HIP_CHECK(hipGetLastError());
-        HIP_CHECK(hipMemcpyAsync(&hc, dev_->ctr, sizeof hc, hipMemcpyDeviceToHost, stream_));
-        HIP_CHECK(hipStreamSynchronize(stream_));
+        readback({{&hc, dev_->ctr, sizeof hc}});
         N->nbig = hc.nbig;
         N->nsmall = hc.nsmall;
         N->arrivals = hc.arrivals_next;
