@@ -75,9 +75,40 @@ __global__ __launch_bounds__(kScanBS) void k_scan_down(const uint32_t* in, uint3
     }
 }
 
+// Small arrays (the per-level tables of deep levels, config 3's levels): one
+// block walks tiles of 16 384 words with a running carry, one launch instead of
+// three (each launch of a few microseconds costs as much again in dispatch gaps).
+constexpr uint32_t kScanSingleMax = 32768;
+__global__ __launch_bounds__(1024) void k_scan_single(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* d_total) {
+    constexpr uint32_t T = 1024 * kScanIPT;
+    __shared__ uint32_t lds[1024 / kWave + 1];
+    uint32_t carry = 0;
+    for (uint32_t t0 = 0; t0 < n; t0 += T) {
+        const uint32_t base = t0 + threadIdx.x * kScanIPT;
+        uint32_t v[kScanIPT], s = 0;
+#pragma unroll
+        for (int i = 0; i < kScanIPT; i++) {
+            v[i] = base + i < n ? in[base + i] : 0u;
+            s += v[i];
+        }
+        uint32_t tot;
+        uint32_t e = block_excl_scan<1024>(s, lds, &tot) + carry;   // (ends with a barrier: in-place safe)
+#pragma unroll
+        for (int i = 0; i < kScanIPT; i++)
+            if (base + i < n) { out[base + i] = e; e += v[i]; }
+        carry += tot;
+    }
+    if (threadIdx.x == 0 && d_total) *d_total = carry;
+}
+
 void scan_excl_u32(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* d_total, ScanTemp& tmp, hipStream_t st) {
     if (n == 0) {
         if (d_total) HIP_CHECK(hipMemsetAsync(d_total, 0, 4, st));
+        return;
+    }
+    if (n <= kScanSingleMax) {
+        k_scan_single<<<1, 1024, 0, st>>>(in, out, n, d_total);
+        HIP_CHECK(hipGetLastError());
         return;
     }
     uint32_t nb = (n + kScanTile - 1) / kScanTile;

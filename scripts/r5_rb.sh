@@ -1,5 +1,6 @@
-# round 5: packed pinned readbacks + the small-slab counts read back behind the dense launch (prod)
-# against the committed engine (build/var_head): parity subset, then config 4 and config 3 A/Bs
+# round 5: an engine change (prod) against the previous build (build/var_head; first use: packed pinned
+# readbacks + the small-slab counts read back behind the dense launch)
+# parity subset, then config 4 and config 3 A/Bs
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$PWD}
 TAG=${1:-r5rb}
