@@ -3959,6 +3959,9 @@ struct BucketParams {
 };
 
 constexpr int kBktBS = 512;
+#ifndef PCC_BKT_ABL
+#define PCC_BKT_ABL 0   // diagnostic builds only: 1 no kept-list sort, 2 no spill-batch search
+#endif
 
 // event batch of an emission of a level-h cell: max(eb0(key), cell's running sb)
 __device__ __forceinline__ uint32_t emission_eb(const BucketParams& B, uint32_t key, uint32_t csb) {
@@ -3994,6 +3997,122 @@ constexpr int kKeptSmall = 1024;
 constexpr uint32_t kBktSplitMin = 8192;
 constexpr int kBktLists = 640;   // a bucket's child-slab lists: 3 per slab of its cell (<= 3 x (2 dim + 5))   // buckets per level from which the two launches pay
 constexpr uint32_t kBktDeferred = 4;
+// A kept list in key order by a stable LSD radix sort, 4 key bits per pass over
+// the bucket's key range (kmax - kmin: config 3's 27 bits in 7 passes).  The
+// child-slab lists are each key-ordered, but a bucket has hundreds of short ones,
+// so merging them gains little; the bitonic network it replaces took 91
+// barrier-separated stages for 8 192 words and was the level's critical path
+// on skewed clouds.  LDS: the keys (u32) and the element indices ping-ponged
+// (u16) in the 64 KB of the packed-word array, plus per-pass digit counts per
+// (row, wave) and their block-scanned bases.  An element's index is its place
+// in the concatenation of the lists in destination order, so its arena
+// position follows from a binary search over the lists' first indices.
+#ifndef PCC_BKT_RADIX
+#define PCC_BKT_RADIX 1
+#endif
+constexpr uint32_t kBktRadixMin = 1024;   // kept lists at least this long: radix sort
+template <int BS, int KMAX>
+__device__ __forceinline__ void bucket_sort_radix(const BucketParams& B, uint32_t b, uint32_t s0, uint32_t oct, uint32_t nd,
+                                                  uint32_t tot, uint32_t s_off, uint32_t* lds, unsigned long long* skp,
+                                                  uint32_t* s_lo, uint32_t* s_ln, uint32_t* s_lp) {
+    constexpr int W = BS / 64, ROWS = KMAX / BS, NRW = KMAX / 64, NC = 16 * NRW, EPT = NC / BS;
+    static_assert(KMAX % BS == 0 && NC % BS == 0 && ROWS <= 32, "radix geometry");
+    __shared__ alignas(16) uint8_t rcnt[NC];
+    __shared__ uint16_t rpre[NC];
+    __shared__ uint32_t r_min, r_max;
+    uint32_t* skey = reinterpret_cast<uint32_t*>(skp);
+    uint16_t* sidx[2] = {reinterpret_cast<uint16_t*>(skey + KMAX), reinterpret_cast<uint16_t*>(skey + KMAX) + KMAX};
+    const uint32_t tid = threadIdx.x, w = tid / 64, lane = tid & 63;
+    // the lists' first indices in destination order (one block scan)
+    constexpr uint32_t LPT = (kBktLists + BS - 1) / BS;
+    uint32_t ln_[LPT], acc = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < LPT; j++) {
+        const uint32_t i = tid * LPT + j;
+        ln_[j] = 0;
+        if (i < nd) {
+            const uint32_t di = (s0 + i / 3) * kDests + oct * 3 + i % 3;
+            ln_[j] = B.dest_n[di];
+            s_lo[i] = B.dest_off[di];
+            s_ln[i] = ln_[j];
+        }
+        acc += ln_[j];
+    }
+    uint32_t t_;
+    uint32_t base = block_excl_scan<BS>(acc, lds, &t_);
+#pragma unroll
+    for (uint32_t j = 0; j < LPT; j++) {
+        const uint32_t i = tid * LPT + j;
+        if (i < nd) s_lp[i] = base;
+        base += ln_[j];
+    }
+    if (tid == 0) { r_min = 0xFFFFFFFFu; r_max = 0; }
+    __syncthreads();
+    // keys in (a wave per list), indices 0 .. tot-1
+    for (uint32_t k = w; k < nd; k += W) {
+        const uint32_t n = s_ln[k], o = s_lo[k], p = s_lp[k];
+        for (uint32_t q = lane; q < n; q += 64) skey[p + q] = B.nx.k[o + q];
+    }
+    for (uint32_t i = tid; i < tot; i += BS) sidx[0][i] = (uint16_t)i;
+    __syncthreads();
+    uint32_t kmn = 0xFFFFFFFFu, kmx = 0;
+    for (uint32_t i = tid; i < tot; i += BS) { kmn = min(kmn, skey[i]); kmx = max(kmx, skey[i]); }
+    atomicMin(&r_min, kmn);
+    atomicMax(&r_max, kmx);
+    __syncthreads();
+    const uint32_t kmin = r_min, span = r_max - r_min;
+    const uint32_t bits = span ? 32u - (uint32_t)__clz(span) : 0u;
+    const uint64_t lt = lanemask_lt();
+    int cur = 0;
+    for (uint32_t sh = 0; sh < bits; sh += 4, cur ^= 1) {
+        for (uint32_t i = tid; i < NC / 4; i += BS) reinterpret_cast<uint32_t*>(rcnt)[i] = 0;
+        __syncthreads();
+        uint32_t reg[ROWS];   // per row: element index | rank << 13 | digit << 19 | valid << 23
+#pragma unroll
+        for (int r = 0; r < ROWS; r++) {
+            const uint32_t i = (uint32_t)r * BS + tid;
+            const bool valid = i < tot;
+            const uint32_t id = valid ? sidx[cur][i] : 0u;
+            const uint32_t d = valid ? ((skey[id] - kmin) >> sh) & 15u : 0u;
+            const uint64_t peers = wave_peers<4>(d, valid);
+            const uint32_t rk = (uint32_t)__popcll(peers & lt);
+            if (valid && rk == 0) rcnt[d * NRW + r * W + w] = (uint8_t)__popcll(peers);
+            reg[r] = id | (rk << 13) | (d << 19) | (valid ? 1u << 23 : 0u);
+        }
+        __syncthreads();
+        // bases: exclusive scan of the counts in (digit, row, wave) order
+        uint32_t c[EPT], sum = 0;
+#pragma unroll
+        for (int e = 0; e < EPT; e++) { c[e] = rcnt[tid * EPT + e]; sum += c[e]; }
+        uint32_t tt;
+        uint32_t pb = block_excl_scan<BS>(sum, lds, &tt);
+#pragma unroll
+        for (int e = 0; e < EPT; e++) { rpre[tid * EPT + e] = (uint16_t)pb; pb += c[e]; }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < ROWS; r++) {
+            const uint32_t v = reg[r];
+            if (v >> 23) {
+                const uint32_t d = (v >> 19) & 15u, rk = (v >> 13) & 63u;
+                sidx[cur ^ 1][rpre[d * NRW + r * W + w] + rk] = (uint16_t)(v & 0x1FFFu);
+            }
+        }
+        __syncthreads();
+    }
+    // the points in key order: element -> its list (last first index <= it) -> arena position
+    for (uint32_t i = tid; i < tot; i += BS) {
+        const uint32_t e = sidx[cur][i];
+        uint32_t lo = 0, hi = nd;   // first list with s_lp > e, minus one
+        while (lo < hi) {
+            const uint32_t m = (lo + hi) >> 1;
+            if (s_lp[m] <= e) lo = m + 1; else hi = m;
+        }
+        const uint32_t k = lo - 1;
+        reinterpret_cast<float4*>(B.kept)[s_off + i] = B.nx.p[s_lo[k] + (e - s_lp[k])];
+    }
+    if (tid == 0) { B.bkt_state[b] = 1; B.bkt_off[b] = s_off; B.bkt_n[b] = tot; B.bkt_nd[b] = 0; B.bkt_sb[b] = 0; }
+}
+
 template <int BS, int KMAX, bool DEFERRED>
 __device__ __forceinline__ void bucket_one(const BucketParams& B, const uint32_t b, uint32_t* lds,
                                            unsigned long long* skp) {
@@ -4070,6 +4189,13 @@ __device__ __forceinline__ void bucket_one(const BucketParams& B, const uint32_t
         }
         __syncthreads();
         if ((uint64_t)s_off + tot > B.kept_cap) return;
+        // long lists by the radix sort (a fixed number of passes), short ones by
+        // the bitonic network (log^2 stages of a small power of two: config 4's
+        // last level of 32 768 mostly short lists ran 0.33 ms slower all radix)
+        if (!big && nd <= (uint32_t)kBktLists && PCC_BKT_RADIX && tot >= kBktRadixMin) {
+            bucket_sort_radix<BS, KMAX>(B, b, s0, oct, nd, tot, s_off, lds, skp, s_lo, s_ln, s_lp);
+            return;
+        }
         // the packed words (key << 32 | arena position) in LDS, or for a list
         // above the LDS capacity in the scratch at twice its kept offset (a
         // power-of-two padding below twice the list never reaches the next list's)
@@ -4113,6 +4239,9 @@ __device__ __forceinline__ void bucket_one(const BucketParams& B, const uint32_t
         // bitonic sort by key (keys are unique, so the packed words order by
         // key); one thread per compare-exchange pair (the workgroup barrier
         // orders the global scratch's accesses too: one workgroup owns it)
+#if PCC_BKT_ABL == 1
+        if (tot > 0xFFFFFFFEu)   // (diagnostic build: the sort skipped, timing only)
+#endif
         for (uint32_t kk = 2; kk <= np2; kk <<= 1)
             for (uint32_t jj = kk >> 1; jj > 0; jj >>= 1) {
                 for (uint32_t p = threadIdx.x; p < np2 / 2; p += BS) {
@@ -4189,6 +4318,9 @@ __device__ __forceinline__ void bucket_one(const BucketParams& B, const uint32_t
     for (int w = 0; w < WL; w++) wlo[w] = wr[w];   // every later e is >= emin
     const uint32_t target = L + (c0 == L ? 1u : 0u);
     uint32_t lo = emin, hi = emax;   // c(emax) = tot >= target
+#if PCC_BKT_ABL == 2
+    hi = lo;   // (diagnostic build: the spill-batch search skipped, timing only)
+#endif
     while (lo < hi) {
         const uint32_t mid = lo + (hi - lo) / 2;
         if (eval(mid) >= target) {
@@ -4204,7 +4336,7 @@ __device__ __forceinline__ void bucket_one(const BucketParams& B, const uint32_t
     if (threadIdx.x == 0) { B.bkt_state[b] = 2; B.bkt_n[b] = tot; B.bkt_nd[b] = nne; B.bkt_sb[b] = lo; B.bkt_off[b] = 0; }
 }
 template <int BS, int KMAX, bool DEFERRED = false>
-__global__ __launch_bounds__(BS) void k_bucket(BucketParams B) {
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_bucket(BucketParams B) {   // (two 512-thread workgroups per CU)
     __shared__ uint32_t lds[BS / 64 + 1];
     __shared__ unsigned long long skp[KMAX];   // (key << 32) | arena position
     if constexpr (!DEFERRED) {

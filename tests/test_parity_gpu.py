@@ -402,3 +402,14 @@ def test_wide_path_forced_equals_slab_path(monkeypatch):
     monkeypatch.setenv("PCC_TEST_WIDE", "1")
     _check(nonfinite_files(seed=13, n=20_000, kinds="mixed"), cfg=dict(sub_grid_dimension=16, cell_point_overflow_limit=40))
     _check([synth(97, 0, 150_000)], cfg=dict(sub_grid_dimension=32, cell_point_overflow_limit=300))
+
+
+@pytest.mark.parametrize("limit", [1024, 1500, 4000, 8192])
+def test_long_kept_lists_radix_sorted(limit):
+    """Kept overflow lists of a thousand points and more (the bucket kernel's
+    radix sort, from kBktRadixMin = 1024 up to the 8 192-word LDS capacity),
+    against the oracle: a small sub-grid sends most points to the overflow,
+    several files and ragged batches interleave their keys."""
+    p = synth(98, 1, 400_000)
+    _check([p[:150_000], p[150_000:151_111], p[151_111:]], cfg=dict(sub_grid_dimension=8, cell_point_overflow_limit=limit),
+           batch=6_000, fast=True)
