@@ -1306,11 +1306,19 @@ struct L0Unit { uint32_t d6, g0, g1, pad; };
 // row r with digit d (<= 64), pre[d][..] = their exclusive prefix in key order.
 constexpr int kL0RW = kL0IPT * kL0W;   // 48 (row, wave) pairs per tile
 static_assert(kL0RW % 16 == 0, "16-byte rows");
+// Row strides of the count (bytes) and prefix (u16) rows: PCC_L0_PAD skews the
+// rows across LDS banks for wave 0's row reads / writes (56 B = 14 words, 112 B =
+// 28 words against 48 B = 12 and 96 B = 24: half the lanes per bank)
+#ifndef PCC_L0_PAD
+#define PCC_L0_PAD 0
+#endif
+constexpr int kL0RC = kL0RW + (PCC_L0_PAD ? 8 : 0), kL0RP = kL0RW + (PCC_L0_PAD ? 8 : 0);
+static_assert(kL0RC % 8 == 0 && (kL0RP * 2) % 16 == 0, "8-byte count rows, 16-byte prefix rows");
 // Wave 0 of a tile: lane t < R reads digit t's 48 counts as 16-byte words,
 // writes their prefixes and clears them for the next tile, then the tile's digit
 // bases by a wave scan; returns the digit's total.
 template <int R>
-__device__ __forceinline__ uint32_t l0_tile_prefix(uint8_t (*cnt)[kL0RW], uint16_t (*pre)[kL0RW], uint32_t lane,
+__device__ __forceinline__ uint32_t l0_tile_prefix(uint8_t (*cnt)[kL0RC], uint16_t (*pre)[kL0RP], uint32_t lane,
                                                    uint32_t& excl) {
     uint32_t acc = 0;
     if (lane < (uint32_t)R) {
@@ -1346,7 +1354,7 @@ __device__ __forceinline__ uint32_t l0_tile_prefix(uint8_t (*cnt)[kL0RW], uint16
 // l0_tile_prefix for R > 64 digits: lane t handles the R / 64 consecutive digits
 // t * R / 64 + k, their totals and exclusive bases in tot[k], excl[k].
 template <int R>
-__device__ __forceinline__ void l0_tile_prefix_n(uint8_t (*cnt)[kL0RW], uint16_t (*pre)[kL0RW], uint32_t lane,
+__device__ __forceinline__ void l0_tile_prefix_n(uint8_t (*cnt)[kL0RC], uint16_t (*pre)[kL0RP], uint32_t lane,
                                                  uint32_t* tot, uint32_t* excl) {
     constexpr int DPL = R / 64;
     static_assert(R % 64 == 0 && DPL >= 1, "whole digits per lane");
@@ -1416,8 +1424,8 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_down6g(const Point* __restrict_
     __shared__ float4 sp[kL0Tile];
     __shared__ KT sk[kL0Tile];
     __shared__ uint8_t sd[kL0Tile];
-    __shared__ alignas(16) uint8_t wcnt[R][kL0RW];
-    __shared__ alignas(16) uint16_t wpre[R][kL0RW];
+    __shared__ alignas(16) uint8_t wcnt[R][kL0RC];
+    __shared__ alignas(16) uint16_t wpre[R][kL0RP];
     __shared__ uint32_t dbase[R], gofs[R];
     // pair counts, row d6 padded to R5 + 1 words: the lanes of a wave share few
     // d5 values, and with rows of exactly R5 words they all hit bank d5
@@ -1426,7 +1434,7 @@ __global__ __launch_bounds__(kL0BS, 8) void k_l0_down6g(const Point* __restrict_
     const uint32_t tid = threadIdx.x, w = tid / 64, lane = tid & 63, g = blockIdx.x;
     const float4* p4 = reinterpret_cast<const float4*>(in);
     for (int i = tid; i < R * HP; i += kL0BS) h[i] = 0;
-    for (int i = tid; i < kL0RW * R / 4; i += kL0BS) reinterpret_cast<uint32_t*>(&wcnt[0][0])[i] = 0;
+    for (int i = tid; i < kL0RC * R / 4; i += kL0BS) reinterpret_cast<uint32_t*>(&wcnt[0][0])[i] = 0;
     const uint64_t lt = lanemask_lt();
     uint32_t err = 0;
     const uint32_t t0 = g * tpg, t1 = min(t0 + tpg, ntiles);
@@ -1570,8 +1578,8 @@ __global__ __launch_bounds__(kL0BS, CB == 3 ? 8 : 1) void k_l0_tile6(const Point
     using KT = typename std::conditional<KEYS, uint32_t, uint16_t>::type;
     __shared__ float4 sp[kL0Tile];
     __shared__ KT sk[kL0Tile];
-    __shared__ alignas(16) uint8_t wcnt[R][kL0RW];
-    __shared__ alignas(16) uint16_t wpre[R][kL0RW];
+    __shared__ alignas(16) uint8_t wcnt[R][kL0RC];
+    __shared__ alignas(16) uint16_t wpre[R][kL0RP];
     __shared__ uint32_t dbase[R];
     __shared__ uint32_t h[R * HP];
     __shared__ float sb[kL0W][6];
@@ -1582,7 +1590,7 @@ __global__ __launch_bounds__(kL0BS, CB == 3 ? 8 : 1) void k_l0_tile6(const Point
     const uint32_t g = glist ? glist[blockIdx.x] : g0 + blockIdx.x;
     const float4* p4 = reinterpret_cast<const float4*>(in);
     for (int i = tid; i < R * HP; i += kL0BS) h[i] = 0;
-    for (int i = tid; i < kL0RW * R / 4; i += kL0BS) reinterpret_cast<uint32_t*>(&wcnt[0][0])[i] = 0;
+    for (int i = tid; i < kL0RC * R / 4; i += kL0BS) reinterpret_cast<uint32_t*>(&wcnt[0][0])[i] = 0;
     const uint64_t lt = lanemask_lt();
     float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
     uint32_t nf = 0;
@@ -1964,8 +1972,8 @@ __global__ __launch_bounds__(kL0BS, R5 > 64 ? 1 : 8) void k_l0_down5g(Arena S, A
     __shared__ float4 sp[kL0Tile];
     __shared__ uint32_t sk[kL0Tile];
     __shared__ uint8_t sd[kL0Tile];
-    __shared__ alignas(16) uint8_t wcnt[R][kL0RW];
-    __shared__ alignas(16) uint16_t wpre[R][kL0RW];
+    __shared__ alignas(16) uint8_t wcnt[R][kL0RC];
+    __shared__ alignas(16) uint16_t wpre[R][kL0RP];
     __shared__ uint32_t dbase[R], gofs[R];
     __shared__ uint32_t hc[R * kDests];
     __shared__ uint32_t slv[TM ? kSl : 1], slp[TM ? kSl : 1];
@@ -1993,7 +2001,7 @@ __global__ __launch_bounds__(kL0BS, R5 > 64 ? 1 : 8) void k_l0_down5g(Arena S, A
         gofs[dg & (R - 1)] = runr[k];   // (an LDS write of runr: its load is complete before the loop)
     }
     for (int i = tid; i < R * kDests; i += kL0BS) hc[i] = 0;
-    for (int i = tid; i < kL0RW * R / 4; i += kL0BS) reinterpret_cast<uint32_t*>(&wcnt[0][0])[i] = 0;
+    for (int i = tid; i < kL0RC * R / 4; i += kL0BS) reinterpret_cast<uint32_t*>(&wcnt[0][0])[i] = 0;
     const uint64_t lt = lanemask_lt();
     uint32_t err = 0;
     const uint32_t* vrow = TM ? voff + (uint64_t)d6u * ntiles : nullptr;
