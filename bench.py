@@ -304,10 +304,10 @@ def record(args, n_gpus, ms, st_levels, st_cells, st_slabs, arrivals, k, dense_m
                      "alg_bytes_per_arrival": 32, "kernel_ms_per_step": dense_ms,
                      "whole_build_alg_GBs": whole, "whole_build_frac": whole / HBM_PEAK_GBS,
                      "limiter": "instruction issue in the phases between the two barriers of each 1024-arrival "
-                                "step, not HBM: 100 more independent VALU per step (4 waves per SIMD) cost 4.4 ms "
-                                "of the 34.3 ms, about their issue cost at 2 cycles per wave64 VALU "
-                                "(profiles/r4_xvalu_ab.jsonl); VALU alone fills 25-32 % of the SIMD cycles at that "
-                                "rate, the rest being SALU/LDS issue and barrier waits (DESIGN.md §4)"},
+                                "step, not HBM: 100 more dependent VALU per wave and step cost +4.4 ms over the "
+                                "three dense launches, 100 more SALU +6.0 ms (profiles/r5_salu_valu_probe.txt); one "
+                                "1024-thread workgroup per CU (13.5-14.7 resident waves of 16, "
+                                "profiles/r5a_pmc_sq_1b.json), 43-46 % of wave-cycles waiting (DESIGN.md §4)"},
         "stage_ms": k,
     }
 
