@@ -464,6 +464,7 @@ def shard_histogram(pts_ptr: int, n: int, grid: ShardGrid, hist_ptr: int, device
 
 
 SHARD_LAYERS = 256   # PCC_SHARD_LAYERS
+SHARD_LDS_UNITS = 16384   # engine.hip kShLds: slab units a fused bbox+histogram pass counts in LDS
 
 
 def shard_slab_histogram(pts_ptr: int, n: int, grid: ShardGrid, sub_grid_dimension: int, hist_ptr: int,

@@ -1193,7 +1193,7 @@ def shard_build(comm, ops, pts: torch.Tensor, key0: int, file_points, write: boo
     # the ownership grid spans the cells of the points without an infinite
     # coordinate (NaN as cell 0, metadata.rs:100-102), and the points with one
     # travel as unit 0 (one rank builds them all); no cell is shared.
-    from pcconv import SHARD_LAYERS as NL
+    from pcconv import SHARD_LAYERS as NL, SHARD_LDS_UNITS
     inf3, ninf3 = [float("inf")] * 3, [float("-inf")] * 3
     guess, sh_guess, outside, nf_local = None, None, 0, 0
     # A rank whose local pass fails still joins the collective, with an error flag
@@ -1214,9 +1214,22 @@ def shard_build(comm, ops, pts: torch.Tensor, key0: int, file_points, write: boo
         _raise_together(err, sbh[7], "bounding-box sample")
         cs = float(ops.cfg_full()["max_cell_size"])
         if sbh[6] == 0:
-            g0 = ops.grid([-sbh[0] - cs, -sbh[1] - cs, -sbh[2] - cs], [sbh[3] + cs, sbh[4] + cs, sbh[5] + cs])
-            if not int(getattr(g0, "coarse", 0)) and int(g0.ncells) * NL <= (1 << 24):
-                guess = g0
+            # a guess whose units fit the fused kernel's LDS histogram is preferred,
+            # even without the margin: beyond it the counts go to global atomics,
+            # which clustered points contend on (config 3: 3.4 ms against 0.3 ms
+            # for the two-pass fallback).  The margin-less guess may miss points
+            # (step 3 then takes the histogram again).
+            def sample_grid(m):
+                g = ops.grid([-sbh[0] - m, -sbh[1] - m, -sbh[2] - m], [sbh[3] + m, sbh[4] + m, sbh[5] + m])
+                return None if int(getattr(g, "coarse", 0)) else g
+            units = lambda g: int(g.ncells) * NL
+            g_m = sample_grid(cs)
+            if g_m is not None and units(g_m) > SHARD_LDS_UNITS:
+                g_0 = sample_grid(0.0)
+                if g_0 is not None and units(g_0) <= SHARD_LDS_UNITS:
+                    g_m = g_0
+            if g_m is not None and units(g_m) <= (1 << 24):
+                guess = g_m
     bmin, bmax, err = inf3, ninf3, None
     if guess is not None:
         r, err = _attempt(lambda: ops.bbox_slab_histogram(pts, guess), (inf3, ninf3, None, 0))

@@ -62,7 +62,8 @@ class RecOps:
     """The ops with their local device calls recorded (stage, name, args), so a
     rank can replay them alone on the GPU after the step."""
     STAGE = {"bbox": "bbox", "bbox_sample": "bbox", "bbox_slab_histogram": "bbox", "slab_histogram": "hist", "histogram": "hist", "route_bitmaps": "route",
-             "route_slabs": "route", "route": "route", "keys_from_bitmaps": "exchange", "resolve_level1": "resolve"}
+             "route_slabs": "route", "route": "route", "keys_from_bitmaps": "exchange", "batch_starts": "exchange",
+             "resolve_level1": "resolve"}
 
     def __init__(self, ops):
         self.o = ops

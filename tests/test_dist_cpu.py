@@ -125,6 +125,47 @@ def test_thread_ranks_match_oracle(tmp_path, case, world, bitmap, mode):
     check_against_oracle(tmp_path, files, out, res[0].summary)
 
 
+@pytest.mark.parametrize("cells,expect", [(4, 4 ** 3), (6, 8 ** 3)])
+def test_guess_grid_prefers_lds_histogram(tmp_path, cells, expect):
+    """A sample box of 4 cells a side: with the one-cell margin the guess would be
+    6^3 cells x 256 layers, past the fused kernel's LDS histogram, so the guess
+    drops the margin (4^3); at 6 cells a side neither fits and the margin stays.
+    Either way the result matches the oracle (points the guess misses are taken
+    again on the true grid)."""
+    import threading
+    files = make_input("uniform")
+    fp = [len(f) for f in files]
+    out = str(tmp_path / "out")
+    grp = ThreadGroup(2)
+    res, errs, seen = [None] * 2, [], []
+
+    def worker(r):
+        try:
+            pts, key0 = rank_slice(files, r, 2)
+            ops = NumpyShardOps(out)
+            cs = float(ops.cfg_full()["max_cell_size"])
+            ops.bbox_sample = lambda p: ([0.25 * cs] * 3, [(cells - 0.75) * cs] * 3)
+            fused = ops.bbox_slab_histogram
+
+            def record(p, guess):
+                seen.append(int(guess.ncells))
+                return fused(p, guess)
+            ops.bbox_slab_histogram = record
+            res[r] = shard_build(ThreadComm(grp, r, torch.device("cpu")), ops, as_tensor(pts), key0, fp, write=True)
+            ops.close()
+        except BaseException as e:  # noqa: BLE001
+            errs.append(e)
+            grp.bar.abort()
+
+    th = [threading.Thread(target=worker, args=(r,)) for r in range(2)]
+    [t.start() for t in th]
+    [t.join() for t in th]
+    assert not errs, errs
+    assert seen == [expect, expect]
+    assert all(r.summary == res[0].summary for r in res)
+    check_against_oracle(tmp_path, files, out, res[0].summary)
+
+
 def test_thread_ranks_empty_input(tmp_path):
     import threading
     grp = ThreadGroup(2)

@@ -745,3 +745,28 @@ def test_sharded_threads_wide_subgrid(tmp_path):
     res = _run_threads(files, 3, out, cfg=cfg)
     assert sum(r.recv_points for r in res) == sum(len(f) for f in files)
     check_against_oracle(tmp_path, files, out, res[0].summary, cfg=cfg)
+
+
+def test_input_landed_refused_for_merge_and_after_build(tmp_path):
+    """pcc_input_landed is for a borrowed, event-table input before its build:
+    a merge (its seeds come first) and a call after the build are refused."""
+    from pcconv.dist import event_table
+    p = synth(76, 0, 50_000)
+    t = as_tensor(p).to(DEV)
+    etab = event_table(np.arange(0, len(p), 10_000), np.arange(5), len(p), 5)
+    c = pcconv.Converter(str(tmp_path / "g"))
+    c.set_event_table(*etab)
+    c.set_keyed_points_device(t.data_ptr(), 0, len(p))
+    torch.cuda.synchronize()
+    c.input_landed(0, 20_000)
+    c.build()
+    with pytest.raises(pcconv.PccError, match="after build"):
+        c.input_landed(20_000, 50_000)
+    c.write()
+    c.close()
+    m = pcconv.Converter(str(tmp_path / "g"))   # reopens the cloud just written: a merge
+    m.set_event_table(*etab)
+    m.set_keyed_points_device(t.data_ptr(), 0, len(p))
+    with pytest.raises(pcconv.PccError, match="merge"):
+        m.input_landed(0, len(p))
+    m.close()
