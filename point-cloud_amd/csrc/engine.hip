@@ -7226,11 +7226,13 @@ struct ShardScratch {
     uint32_t* cnt = nullptr;
     uint64_t* tab = nullptr;
     uint64_t* rt = nullptr;   // bucket resolution tables and sort buffers (shard_resolve_buckets)
+    unsigned long long* ks = nullptr;   // its sort scratch of kept lists above kKeptMax
+    uint64_t ks_cap = 0;
     uint64_t rt_cap = 0;
     SortTemp sort;
     ~ShardScratch() {
         for (auto* b : buf) (void)hipFree(b);
-        (void)hipFree(part); (void)hipFree(nfpart); (void)hipFree(flag); (void)hipFree(cnt); (void)hipFree(tab); (void)hipFree(rt);
+        (void)hipFree(part); (void)hipFree(nfpart); (void)hipFree(flag); (void)hipFree(cnt); (void)hipFree(tab); (void)hipFree(rt); (void)hipFree(ks);
         (void)hipFree(sort.counts); (void)hipFree(sort.scan.bsums);
         if (st) (void)hipStreamDestroy(st);
     }
@@ -7636,6 +7638,8 @@ struct BucketTabs {
     uint32_t* sel;              // per bucket: prefix, rank left, kmin, kmax, fk, first, next key, pad
     uint64_t* out;              // per bucket: state | spill batch << 32
     uint64_t* base;             // per bucket: kept base, sub base (exclusive scans)
+    unsigned long long* ksort;  // limit > kKeptMax: sort scratch of the kept lists above the LDS
+                                // capacity, at twice their kept base (nullptr otherwise)
     uint32_t nbuckets, limit;
 };
 enum { SEL_PREFIX, SEL_RANK, SEL_KMIN, SEL_KMAX, SEL_FK, SEL_FIRST, SEL_NEXT, SEL_PAD, SEL_W };
@@ -7775,7 +7779,11 @@ __global__ void k_bkt_sub(BucketTabs T, const Point* __restrict__ pts, const uin
     }
 }
 // kept buckets (one workgroup each): the bucket's keys in LDS, every row's rank
-// = the keys below its own (distinct keys), row to kept base + rank
+// = the keys below its own (distinct keys), row to kept base + rank.  A list
+// above the LDS capacity (limit > kKeptMax) is bitonic-sorted as packed words
+// (key << 32 | row) in the global scratch at twice its kept base, as k_bucket
+// does (a power-of-two padding below twice the list never reaches the next
+// list's; the workgroup barrier orders the scratch's accesses: one workgroup owns it)
 __global__ __launch_bounds__(1024) void k_bkt_kept(BucketTabs T, const Point* __restrict__ pts,
                                                    const uint32_t* __restrict__ keys, Point* __restrict__ kept) {
     __shared__ uint32_t sk[kKeptMax];
@@ -7783,6 +7791,36 @@ __global__ __launch_bounds__(1024) void k_bkt_kept(BucketTabs T, const Point* __
     const uint32_t b = blockIdx.x;
     if ((uint32_t)T.out[b] != 1 || T.tot[b] == 0) return;
     const uint32_t tot = (uint32_t)T.tot[b];
+    if (tot > (uint32_t)kKeptMax) {
+        if (!T.ksort) return;   // (the host allocates it whenever such a list can be kept)
+        unsigned long long* sw = T.ksort + 2 * T.base[2 * b];
+        uint32_t o = 0;
+        for (uint64_t j = T.boff[b]; j < T.boff[b + 1]; j++) {
+            const uint64_t sg = T.bsegs[j], r0 = T.start[sg];
+            const uint32_t n = (uint32_t)T.len[sg];
+            for (uint32_t i = threadIdx.x; i < n; i += 1024)
+                sw[o + i] = ((unsigned long long)keys[r0 + i] << 32) | (uint32_t)(r0 + i);
+            o += n;
+        }
+        uint32_t np2 = 1;
+        while (np2 < tot) np2 <<= 1;
+        for (uint32_t i = tot + threadIdx.x; i < np2; i += 1024) sw[i] = ~0ull;
+        __syncthreads();
+        for (uint32_t kk = 2; kk <= np2; kk <<= 1)
+            for (uint32_t jj = kk >> 1; jj > 0; jj >>= 1) {
+                for (uint32_t p = threadIdx.x; p < np2 / 2; p += 1024) {
+                    const uint32_t i = ((p & ~(jj - 1)) << 1) | (p & (jj - 1)), ix = i | jj;
+                    const bool up = (i & kk) == 0;
+                    const unsigned long long a = sw[i], c = sw[ix];
+                    if ((a > c) == up) { sw[i] = c; sw[ix] = a; }
+                }
+                __syncthreads();
+            }
+        const uint64_t kb = T.base[2 * b];
+        for (uint32_t i = threadIdx.x; i < tot; i += 1024)
+            reinterpret_cast<float4*>(kept)[kb + i] = reinterpret_cast<const float4*>(pts)[(uint32_t)sw[i]];
+        return;
+    }
     uint32_t o = 0;
     for (uint64_t j = T.boff[b]; j < T.boff[b + 1]; j++) {
         const uint64_t sg = T.bsegs[j], r0 = T.start[sg];
@@ -7887,7 +7925,7 @@ int shard_resolve_buckets(const uint64_t* seg_n, const uint32_t* seg_bucket, uin
     *nkept = *nsub = 0;
     if (!nbuckets) return 0;
     if (!nfiles || nseg == 0) return -EINVAL;
-    if (limit == 0 || limit > (uint32_t)kKeptMax) return -EINVAL;
+    if (limit == 0 || limit > (1u << 24)) return -EINVAL;   // (the engine's limit, Engine::open)
     batch = std::max<uint32_t>(batch, 1);
     std::vector<uint64_t> tot(nbuckets, 0), boff(nbuckets + 1ull, 0), start(nseg), segb(nseg), inoff(nseg), chunks;
     uint64_t nrows = 0;
@@ -7966,6 +8004,25 @@ int shard_resolve_buckets(const uint64_t* seg_n, const uint32_t* seg_bucket, uin
     T.base = S.rt + w_base;
     T.nbuckets = nbuckets;
     T.limit = limit;
+    // kept lists above the LDS capacity: their sort scratch (twice the rows any
+    // kept bucket can hold, i.e. of the buckets with tot <= limit)
+    T.ksort = nullptr;
+    uint64_t kmax_rows = 0;
+    bool big = false;
+    for (uint32_t b = 0; b < nbuckets; b++)
+        if (tot[b] <= limit) {
+            kmax_rows += tot[b];
+            big |= tot[b] > (uint64_t)kKeptMax;
+        }
+    if (big) {
+        if (S.ks_cap < 2 * kmax_rows) {
+            (void)hipFree(S.ks);
+            S.ks = nullptr;
+            HIP_CHECK(hipMalloc(&S.ks, 2 * kmax_rows * 8));
+            S.ks_cap = 2 * kmax_rows;
+        }
+        T.ksort = S.ks;
+    }
     HIP_CHECK(hipMemcpyAsync(S.rt, blob.data(), w_out * 8, hipMemcpyHostToDevice, S.st));   // (hist: zeros)
     const uint32_t pb = (nbuckets + 63) / 64;
     for (int pass = 0; pass <= 4; pass++) {

@@ -510,7 +510,9 @@ def _exchange_segments(comm, dest: np.ndarray, meta: np.ndarray, lens: np.ndarra
     W = comm.world
     dest = np.asarray(dest, dtype=np.int64)
     lens = np.asarray(lens, dtype=np.int64)
-    meta = np.asarray(meta, dtype=np.int64).reshape(len(dest), -1)
+    meta = np.asarray(meta, dtype=np.int64)
+    k = meta.shape[1] if meta.ndim == 2 else (meta.size // len(dest) if len(dest) else 1)
+    meta = meta.reshape(len(dest), k)   # (no segments: 0 rows of k, not reshape(0, -1))
     order = np.argsort(dest, kind="stable")
     if len(order) and not np.array_equal(order, np.arange(len(order))):
         starts = np.concatenate([[0], np.cumsum(lens)])[:-1]
@@ -519,7 +521,6 @@ def _exchange_segments(comm, dest: np.ndarray, meta: np.ndarray, lens: np.ndarra
         tensors = [t.index_select(0, idx.to(t.device)) for t in tensors]
     nseg = [int(v) for v in np.bincount(dest, minlength=W)] if len(dest) else [0] * W
     nrow = [int(v) for v in np.bincount(dest, weights=lens, minlength=W).astype(np.int64)] if len(dest) else [0] * W
-    k = meta.shape[1] if meta.ndim == 2 else 1
     mt = torch.from_numpy(np.ascontiguousarray(meta[order]).reshape(-1, k)).to(comm.device)
     rmeta = _exchange(comm, mt, nseg, comm.alltoall_counts(nseg), comm.device).cpu().numpy().reshape(-1, k)
     rr = comm.alltoall_counts(nrow)

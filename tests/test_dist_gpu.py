@@ -402,6 +402,20 @@ def test_sharded_threads_split_cells_match_oracle(tmp_path, world):
     check_against_oracle(tmp_path, files, out, res[0].summary, cfg=SKEW_CFG)
 
 
+def test_sharded_split_cells_kept_lists_above_lds(tmp_path):
+    """Shared level-0 cells whose octant buckets stay Some with more than 8 192
+    points (a limit of 13 056, above the LDS sort capacity; the randomised
+    sweep's case 7, a plane of 88 099 points over 4 ranks): the device bucket
+    resolution sorts those kept lists in global memory, == the oracle."""
+    from fuzz_cases import mid_case
+    files, cfg, batch, _ = mid_case(7)
+    assert cfg["cell_point_overflow_limit"] > 8192
+    out = str(tmp_path / "out")
+    res = _run_threads(files, 4, out, cfg=cfg, batch=batch)
+    assert res[0].plan["split_cells"] > 0
+    check_against_oracle(tmp_path, files, out, res[0].summary, cfg=cfg, batch=batch)
+
+
 def test_sharded_threads_sparse_wide_cloud_coarse_grid(tmp_path):
     """Level-0 grid beyond the shard grid's 2^22 cells: ownership by blocks of
     level-0 cells (pcconv.dist.shard_grid), hashed level-0 grid per rank."""

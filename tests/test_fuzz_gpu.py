@@ -81,3 +81,45 @@ def test_fuzz_big_matches_oracle(seed):
         assert mg == mo
         assert st["arrivals"] == arrivals
         assert kt["dense_launches"] > 0 and kt["dense_arrivals"] > 0
+
+
+@pytest.mark.parametrize("seed", range(1, 48, 3))
+def test_fuzz_sharded_threads_match_oracle(seed, tmp_path):
+    """The sweep's cases sharded over 2-8 thread ranks on cuda:0 (pcconv.dist:
+    level-0 cells or slabs owned per rank, the exchange in 0 or 2-5 rounds with
+    level-0 pass 1 behind it), merged output against the oracle's one-process run."""
+    import threading
+    import numpy as np
+    import torch
+    from pcconv.dist import HipShardOps, ThreadComm, ThreadGroup, key_range, shard_build
+    from test_dist_cpu import check_against_oracle
+    from shard_np import as_tensor
+    files, cfg, batch, kind = mid_case(seed)
+    world = [2, 3, 4, 5, 8][seed % 5]
+    rounds = [0, 2, 3, 5][seed % 4]
+    fp = [len(f) for f in files]
+    allp = np.concatenate(files)
+    out = str(tmp_path / "out")
+    dev = torch.device("cuda", 0)
+    grp = ThreadGroup(world)
+    res, errs = [None] * world, []
+
+    def worker(r):
+        try:
+            torch.cuda.set_device(dev)
+            a, b = key_range(len(allp), r, world)
+            ops = HipShardOps(0, out_dir=out, batch_size=batch, config=cfg)
+            ops.landing_rounds = rounds
+            t = as_tensor(allp[a:b]).to(dev)
+            res[r] = shard_build(ThreadComm(grp, r, dev), ops, t, a, fp, write=True)
+            ops.close()
+        except BaseException as e:  # noqa: BLE001
+            errs.append(e)
+            grp.bar.abort()
+
+    th = [threading.Thread(target=worker, args=(r,)) for r in range(world)]
+    [t.start() for t in th]
+    [t.join() for t in th]
+    assert not errs, (kind, cfg, batch, world, errs)
+    assert sum(r.recv_points for r in res) == len(allp)
+    check_against_oracle(tmp_path, files, out, res[0].summary, cfg=cfg, batch=batch)
