@@ -1027,6 +1027,7 @@ int pcc_get_stats(const pcc_converter* c, pcc_stats* s) {
     s->build_ms = c->build_ms;
     s->level0_early_tiles = b.pre0_tiles;
     s->level0_fold = b.l0_fold;
+    s->sequential_replay = b.seq_replay;
     for (int a = 0; a < 3; a++) { s->bbox_min[a] = c->meta.bmin[a]; s->bbox_max[a] = c->meta.bmax[a]; }
     return 0;
 }

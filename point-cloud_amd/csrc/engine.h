@@ -170,6 +170,7 @@ struct BuildStats {
     double ms_total = 0, ms_level0_bin = 0;
     uint64_t pre0_tiles = 0;                       // level-0 pass-0 tiles counted while the input uploaded
     uint32_t l0_fold = 0;                          // level-0 binning with pass 0 folded into pass 1
+    uint32_t seq_replay = 0;                       // the whole build ran as the sequential replay
     std::vector<double> ms_level;                  // per level (slab + bucket kernels)
 };
 
@@ -292,6 +293,8 @@ private:
     std::vector<RbPart> rb_parts_;
     hipEvent_t rb_ev_ = nullptr;
     int build_wide();
+    int replay_whole(const Point* src, const uint32_t* keys, uint64_t n, const char* why);
+    bool geom_fault_ = false;   // run_level: only hexagon / slot geometry flags (saturated indices)
     int replay_seq(const Point* pts, const uint32_t* keys, uint64_t n);
     // level-0 pass 0 behind the host-to-device copy (add_file_host, streamed files)
     void pre0_count(uint64_t upto, hipEvent_t after, bool all);

@@ -198,6 +198,8 @@ constexpr int kSmallClaim = 512;
 constexpr int kKeptMax = 8192;        // LDS sort capacity for kept (Some) buckets
 constexpr int kDests = 24;            // 8 octants x 3 child layers per slab
 constexpr uint32_t kMaxDepth = 31;    // 2u32.pow(h) overflows at h = 32 (metadata.rs:92)
+constexpr uint64_t kWideMax = 1ull << 24;  // points per build with a sub-grid beyond the dense table (build_wide)
+constexpr int kInfSaturated = -10022;   // build_infinite: finite cells could meet the infinite ones (-EINVAL to callers)
 
 enum ErrBits : uint32_t {
     ERR_SLOT_RANGE = 1u << 0,
@@ -5238,11 +5240,18 @@ int Engine::build() {
 
     nf_mode_ = false;
     ninf_ = 0;
+    geom_fault_ = false;
     if (wide) {
         const int rcw = build_wide();
         stats_.ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         return rcw;
     }
+    // the input as it stands (enter_nonfinite moves the infinite points apart):
+    // what the sequential replay takes if the levels cannot be built in parallel
+    const Point* src0 = src_;
+    const uint32_t* keys0 = src_keys_;
+    const uint64_t n0 = nsrc_;
+    const bool can_replay = !prior_ && !h0_ && !max_levels_ && n0 <= kWideMax && getenv("PCC_NO_REPLAY") == nullptr;
     ev_begin(ST_L0);
     int rc = level0_bin();   // also computes the bounding box (converter.rs:96-104)
     if (rc) return rc;
@@ -5251,6 +5260,15 @@ int Engine::build() {
         if (h0_ + i >= kMaxDepth) return fail(-75, "hierarchy depth limit (31) reached: more than cell_point_overflow_limit duplicate points?");
         const auto tl = std::chrono::steady_clock::now();
         rc = run_level(i);
+        if (rc && geom_fault_ && can_replay) {
+            // hexagon or slot indices saturated at a deep level (coordinates far
+            // beyond the cell size, reachable through NaN-collapsed points): the
+            // parallel slot geometry does not hold there, the reference's saturating
+            // casts (hex.rs:67-85) do, so the whole build is replayed sequentially
+            rc = replay_whole(src0, keys0, n0, "saturated hexagon indices");
+            stats_.ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+            return rc;
+        }
         if (rc) return rc;
         stats_.ms_level.push_back(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tl).count());
         if (levels_.size() == i + 1) break;   // no next level
@@ -5266,7 +5284,12 @@ int Engine::build() {
     hierarchies_ = std::max<uint32_t>(hierarchies_, h0_ + (uint32_t)levels_.size());
     stats_.levels = (uint32_t)levels_.size();
     rc = build_infinite();
-    if (rc) return rc;
+    if (rc == kInfSaturated && can_replay) {   // finite cells that could meet the infinite points' ones
+        rc = replay_whole(src0, keys0, n0, "finite coordinates saturating a cell index beside infinite ones");
+        stats_.ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        return rc;
+    }
+    if (rc) return rc == kInfSaturated ? -22 : rc;
     if (profiling_) {
         ev_collect();
         Counters hc;
@@ -5682,7 +5705,6 @@ __global__ __launch_bounds__(1024) void k_nf_scatter(const Point* __restrict__ i
 // Rare by nature (a data error), so no parallel design: one lane, state in HBM.
 constexpr uint32_t kInfNil = 0xFFFFFFFFu;
 constexpr uint64_t kInfMax = 1ull << 18;   // points with an infinite coordinate per build
-constexpr uint64_t kWideMax = 1ull << 24;  // points per build with a sub-grid beyond the dense table (build_wide)
 __global__ void k_iota_u32(uint32_t* k, uint64_t n) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) k[i] = (uint32_t)i;
@@ -5960,8 +5982,11 @@ int Engine::build_infinite() {
         if (nsrc_)
             for (int a = 0; a < 3; a++) m = std::max(m, std::max(std::fabs(gmin_[a]), std::fabs(gmax_[a])));
         const uint32_t hl = h0_ + (uint32_t)std::max<size_t>(std::max<size_t>(levels_.size(), prior_ ? pdev_.size() : 0), 1) - 1;
-        if (!(m / cell_size(cfg_.max_cell_size, hl) < 1.0e9f))
-            return fail(-22, "finite coordinates that saturate a cell index mixed with infinite ones are not supported");
+        if (!(m / cell_size(cfg_.max_cell_size, hl) < 1.0e9f)) {
+            fail(-22, "finite coordinates that saturate a cell index mixed with infinite ones are not supported "
+                      "(in a merge, a level range, or beyond 2^24 points)");
+            return kInfSaturated;
+        }
     }
     return replay_seq(d_inf_pts_, d_inf_keys_, ninf_);
 }
@@ -5972,6 +5997,29 @@ int Engine::build_infinite() {
 // tables in HBM), cells as side cells.  A correctness path, not a fast one:
 // about 1 M arrivals per second.  The bounding box in the reference's form
 // (k_bbox_nf: NaN skipped, infinities kept).
+// The whole build as the sequential replay (k_inf_build over every point),
+// after a parallel attempt that hit geometry it cannot express: the levels and
+// statistics of that attempt are dropped, the input is the one it started from.
+int Engine::replay_whole(const Point* src, const uint32_t* keys, uint64_t n, const char* why) {
+    (void)why;
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    for (Level* l : levels_) delete l;
+    levels_.clear();
+    side_.clear();
+    stats_ = BuildStats();
+    hierarchies_ = nbatches_ > 0 ? 1u : 0u;
+    HIP_CHECK(hipMemsetAsync(dev_->ctr, 0, sizeof(Counters), stream_));
+    src_ = src;
+    src_keys_ = keys;
+    nsrc_ = n;
+    nf_mode_ = false;
+    ninf_ = 0;
+    err_.clear();
+    const int rc = build_wide();
+    stats_.seq_replay = 1;
+    return rc;
+}
+
 int Engine::build_wide() {
     if (nsrc_ > kWideMax) return fail(-22, "sub_grid_dimension > 96: more than 2^24 points per build are not supported");
     const uint32_t nb = (uint32_t)std::min<uint64_t>(std::max<uint64_t>((nsrc_ + 255) / 256, 1), kBBoxBlocks);
@@ -5995,6 +6043,7 @@ int Engine::build_wide() {
     }
     const int rc = replay_seq(src_, keys, nsrc_);
     stats_.levels = hierarchies_;
+    stats_.seq_replay = 1;
     return rc;
 }
 
@@ -6933,6 +6982,7 @@ int Engine::run_level(uint32_t li) {
         return fail(-5, buf);
     }
     if (hc.err) {
+        geom_fault_ = (hc.err & ~(uint32_t)(ERR_SLOT_RANGE | ERR_LAYER | ERR_OCTANT | ERR_SEL)) == 0;
         char buf[200];
         snprintf(buf, sizeof buf,
                  "device error flags 0x%x at level %u (1 slot range, 2 layer, 4 octant, 8 sel, 16 kept cap, 64 capacity, "

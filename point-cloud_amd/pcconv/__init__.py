@@ -54,7 +54,7 @@ class Stats(C.Structure):
                 ("cells", C.c_uint64), ("slabs", C.c_uint64), ("arrivals", C.c_uint64),
                 ("grid_points", C.c_uint64), ("kept_points", C.c_uint64), ("build_ms", C.c_double),
                 ("bbox_min", C.c_float * 3), ("bbox_max", C.c_float * 3), ("level0_early_tiles", C.c_uint64),
-                ("level0_fold", C.c_uint32), ("reserved1", C.c_uint32)]
+                ("level0_fold", C.c_uint32), ("sequential_replay", C.c_uint32)]
 
     def as_dict(self) -> dict:
         d = {k: getattr(self, k) for k, _ in self._fields_ if not k.startswith("bbox")}

@@ -15,9 +15,11 @@ CELL_SIZES = [0.125, 1.0, 7.5, 100.0, 1000.0, 12345.0]
 KINDS = ["uniform", "gauss", "plane", "line", "lattice"]
 
 
-def mid_case(seed: int):
+def mid_case(seed: int, nonfinite: bool = False):
     """(files, cfg, batch, kind) for one seed; at most ~600 000 points and about
-    5 000 cells (each cell is a file the canonical compare reads)."""
+    5 000 cells (each cell is a file the canonical compare reads).  nonfinite:
+    ~0.5 % of the points get NaN / +inf / -inf in one or two coordinates
+    (bounding-volume/src/lib.rs:23-31, metadata.rs:100-102, cell.rs:77-80)."""
     rng = np.random.default_rng(7919 + seed)
     cs = float(rng.choice(CELL_SIZES))
     dim = int(rng.choice(DIMS))
@@ -54,6 +56,15 @@ def mid_case(seed: int):
         dst = rng.integers(1, n, nd)
         src = (rng.uniform(0.0, 1.0, nd) * dst).astype(np.int64)
         xyz[dst] = xyz[src]
+    if nonfinite:
+        m = max(1, n // 200)
+        idx = rng.choice(n, size=m, replace=False)
+        specials = np.array([np.nan, np.inf, -np.inf], dtype=np.float32)
+        for j, i in enumerate(idx):
+            # one or two special axes (all three leave nothing to tell twins
+            # apart: more than the limit of them never terminate in the reference)
+            for a in rng.choice(3, size=1 + (j % 2), replace=False):
+                xyz[i, a] = specials[rng.integers(0, 3)]
     pts = np.zeros(n, dtype=POINT_DTYPE)
     pts["x"], pts["y"], pts["z"] = xyz[:, 0], xyz[:, 1], xyz[:, 2]
     pts["rgba"] = rng.integers(0, 256, (n, 4), dtype=np.uint8)
@@ -62,6 +73,13 @@ def mid_case(seed: int):
     files = [pts[a:b] for a, b in zip([0] + cuts, cuts + [n])]
     cfg = dict(cell_point_overflow_limit=limit, sub_grid_dimension=dim, max_cell_size=cs)
     return files, cfg, batch, kind
+
+
+def halves(files):
+    """(first, second): the case's points cut in two, as two file lists."""
+    allp = np.concatenate(files)
+    h = len(allp) // 2
+    return [allp[:h]], [allp[h:]]
 
 
 def big_case(seed: int):

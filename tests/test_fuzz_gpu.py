@@ -12,7 +12,7 @@ import tempfile
 
 import pytest
 
-from fuzz_cases import big_case, mid_case
+from fuzz_cases import big_case, halves, mid_case
 from gpu_util import compare_dirs, run_gpu, run_oracle  # noqa: E402
 
 pytestmark = pytest.mark.gpu
@@ -20,6 +20,28 @@ pytestmark = pytest.mark.gpu
 
 def _shm():
     return "/dev/shm" if os.path.isdir("/dev/shm") and os.access("/dev/shm", os.W_OK) else None
+
+
+def _explain(files, ga, gb):
+    """For the first cell whose canonical forms differ: its first differing
+    overflow list (or grid) on both sides as input indices (a plain build's keys)."""
+    import numpy as np
+    import canon
+    ca, cb = canon.read_dir_fast(ga)[0], canon.read_dir_fast(gb)[0]
+    allp = np.concatenate(files)
+    index = {}
+    for i in range(len(allp)):
+        index.setdefault(bytes(allp[i].tobytes()), i)
+    ids = lambda blob: [index.get(bytes(blob[j:j + 16]), -1) for j in range(0, len(blob or b""), 16)]
+    for k in sorted(set(ca) & set(cb)):
+        if ca[k] == cb[k]:
+            continue
+        if ca[k][1] != cb[k][1]:
+            return f"cell {k} grid: {sorted(ids(ca[k][1]))[:32]} vs {sorted(ids(cb[k][1]))[:32]}"
+        for (ia, la), (ib, lb) in zip(ca[k][2], cb[k][2]):
+            if la != lb:
+                return f"cell {k} child {ia}: {ids(la)[:64]} vs {ids(lb)[:64]}"
+    return "?"
 
 
 @pytest.mark.parametrize("seed", range(48))
@@ -34,7 +56,7 @@ def test_fuzz_matches_oracle(seed):
             return
         st = run_gpu(tg, files, cfg=cfg, batch=batch)
         d, mg, mo = compare_dirs(tg, to, fast=True)
-        assert d == [], (kind, cfg, batch, d)
+        assert d == [], (kind, cfg, batch, d, _explain(files, to, tg))
         assert mg == mo
         assert st["arrivals"] == arrivals
         assert st["grid_points"] + st["kept_points"] == st["number_of_points"]
@@ -83,23 +105,19 @@ def test_fuzz_big_matches_oracle(seed):
         assert kt["dense_launches"] > 0 and kt["dense_arrivals"] > 0
 
 
-@pytest.mark.parametrize("seed", range(1, 48, 3))
-def test_fuzz_sharded_threads_match_oracle(seed, tmp_path):
-    """The sweep's cases sharded over 2-8 thread ranks on cuda:0 (pcconv.dist:
-    level-0 cells or slabs owned per rank, the exchange in 0 or 2-5 rounds with
-    level-0 pass 1 behind it), merged output against the oracle's one-process run."""
+def _sharded(tmp_path, files, cfg, batch, world, rounds, merge=False, prior=None):
+    """files over `world` thread ranks on cuda:0 (pcconv.dist), written to out;
+    with merge the existing cloud `prior` (file list) is written first by the oracle."""
     import threading
     import numpy as np
     import torch
     from pcconv.dist import HipShardOps, ThreadComm, ThreadGroup, key_range, shard_build
-    from test_dist_cpu import check_against_oracle
     from shard_np import as_tensor
-    files, cfg, batch, kind = mid_case(seed)
-    world = [2, 3, 4, 5, 8][seed % 5]
-    rounds = [0, 2, 3, 5][seed % 4]
     fp = [len(f) for f in files]
     allp = np.concatenate(files)
     out = str(tmp_path / "out")
+    if merge:
+        assert run_oracle(out, prior, cfg=cfg, batch=batch)[0] == 0
     dev = torch.device("cuda", 0)
     grp = ThreadGroup(world)
     res, errs = [None] * world, []
@@ -108,10 +126,10 @@ def test_fuzz_sharded_threads_match_oracle(seed, tmp_path):
         try:
             torch.cuda.set_device(dev)
             a, b = key_range(len(allp), r, world)
-            ops = HipShardOps(0, out_dir=out, batch_size=batch, config=cfg)
+            ops = HipShardOps(0, out_dir=out, batch_size=batch, config=None if merge else cfg, merge=merge)
             ops.landing_rounds = rounds
             t = as_tensor(allp[a:b]).to(dev)
-            res[r] = shard_build(ThreadComm(grp, r, dev), ops, t, a, fp, write=True)
+            res[r] = shard_build(ThreadComm(grp, r, dev), ops, t, a, fp, write=True, merge=merge)
             ops.close()
         except BaseException as e:  # noqa: BLE001
             errs.append(e)
@@ -120,6 +138,99 @@ def test_fuzz_sharded_threads_match_oracle(seed, tmp_path):
     th = [threading.Thread(target=worker, args=(r,)) for r in range(world)]
     [t.start() for t in th]
     [t.join() for t in th]
-    assert not errs, (kind, cfg, batch, world, errs)
+    assert not errs, (cfg, batch, world, errs)
     assert sum(r.recv_points for r in res) == len(allp)
+    return out, res
+
+
+@pytest.mark.parametrize("seed", range(1, 48, 3))
+def test_fuzz_sharded_threads_match_oracle(seed, tmp_path):
+    """The sweep's cases sharded over 2-8 thread ranks on cuda:0 (pcconv.dist:
+    level-0 cells or slabs owned per rank, the exchange in 0 or 2-5 rounds with
+    level-0 pass 1 behind it), merged output against the oracle's one-process run."""
+    from test_dist_cpu import check_against_oracle
+    files, cfg, batch, kind = mid_case(seed)
+    out, res = _sharded(tmp_path, files, cfg, batch, [2, 3, 4, 5, 8][seed % 5], [0, 2, 3, 5][seed % 4])
     check_against_oracle(tmp_path, files, out, res[0].summary, cfg=cfg, batch=batch)
+
+
+@pytest.mark.parametrize("seed", range(2, 48, 4))
+def test_fuzz_sharded_merge_matches_oracle(seed, tmp_path):
+    """Sharded merge (config 5's shape): the first half written by the oracle,
+    the second half merged by 2-5 thread ranks (pcc_open_subtrees per rank)."""
+    from test_dist_cpu import check_against_oracle
+    files, cfg, batch, kind = mid_case(seed)
+    first, second = halves(files)
+    out, res = _sharded(tmp_path, second, cfg, batch, [2, 3, 4, 5][seed % 4], 0, merge=True, prior=first)
+    check_against_oracle(tmp_path, first + second, out, res[0].summary, cfg=cfg, batch=batch)
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_fuzz_nonfinite_matches_oracle(seed):
+    """The sweep's cases with ~0.5 % of the points given NaN / +-inf coordinates."""
+    import pcconv
+    files, cfg, batch, kind = mid_case(seed, nonfinite=True)
+    with tempfile.TemporaryDirectory(dir=_shm()) as tg, tempfile.TemporaryDirectory(dir=_shm()) as to:
+        err, arrivals = run_oracle(to, files, cfg=cfg, batch=batch)
+        assert err == 0
+        st = run_gpu(tg, files, cfg=cfg, batch=batch)
+        d, mg, mo = compare_dirs(tg, to, fast=True)
+        assert d == [], (kind, cfg, batch, d)
+        assert mg == mo
+        assert st["grid_points"] + st["kept_points"] == st["number_of_points"]
+
+
+@pytest.mark.parametrize("seed", range(0, 24, 3))
+def test_fuzz_nonfinite_merge_matches_oracle(seed):
+    """NaN in the existing cloud (its box stays finite: NaN is skipped) and NaN /
+    +-inf in the merged points.  An infinite coordinate in the existing cloud
+    would make its metadata.json box null, which neither the reference's
+    serde_json nor this loader reads back (test_parity_gpu.py)."""
+    import numpy as np
+    files, cfg, batch, kind = mid_case(seed, nonfinite=True)
+    first, second = halves(files)
+    f = first[0]
+    first = [f[~(np.isinf(f["x"]) | np.isinf(f["y"]) | np.isinf(f["z"]))]]   # (the existing cloud: NaN only)
+    with tempfile.TemporaryDirectory(dir=_shm()) as tg, tempfile.TemporaryDirectory(dir=_shm()) as to:
+        assert run_oracle(tg, first, cfg=cfg, batch=batch)[0] == 0
+        st = run_gpu(tg, second, cfg=None, batch=batch)
+        assert run_oracle(to, first + second, cfg=cfg, batch=batch)[0] == 0
+        d, mg, mo = compare_dirs(tg, to, fast=True)
+        assert d == [], (kind, cfg, batch, d)
+        assert mg == mo
+
+
+@pytest.mark.parametrize("seed", range(1, 24, 3))
+def test_fuzz_nonfinite_sharded_matches_oracle(seed, tmp_path):
+    from test_dist_cpu import check_against_oracle
+    files, cfg, batch, kind = mid_case(seed, nonfinite=True)
+    out, res = _sharded(tmp_path, files, cfg, batch, [2, 3, 4][seed % 3], [0, 3][seed % 2])
+    check_against_oracle(tmp_path, files, out, res[0].summary, cfg=cfg, batch=batch)
+
+
+def test_saturated_hexagon_indices_replayed_sequentially():
+    """NaN-collapsed points on a line far from the origin (the sweep's case 8 with
+    non-finite coordinates) recurse to level 24, where x / hex radius no longer
+    fits an i32: the reference saturates (hex.rs:67-85), the parallel slot
+    geometry cannot, so the build is replayed sequentially on the GPU (stats
+    sequential_replay) == the oracle; with the replay disabled it is an error."""
+    import pcconv
+    files, cfg, batch, kind = mid_case(8, nonfinite=True)
+    with tempfile.TemporaryDirectory(dir=_shm()) as tg, tempfile.TemporaryDirectory(dir=_shm()) as to:
+        assert run_oracle(to, files, cfg=cfg, batch=batch)[0] == 0
+        st = run_gpu(tg, files, cfg=cfg, batch=batch)
+        assert st["sequential_replay"] == 1
+        d, mg, mo = compare_dirs(tg, to, fast=True)
+        assert d == [], d
+        assert mg == mo
+        assert mg["hierarchies"] >= 20
+
+
+def test_saturated_hexagon_indices_error_without_replay(monkeypatch):
+    import pcconv
+    monkeypatch.setenv("PCC_NO_REPLAY", "1")
+    files, cfg, batch, kind = mid_case(8, nonfinite=True)
+    with tempfile.TemporaryDirectory(dir=_shm()) as tg:
+        with pytest.raises(pcconv.PccError) as ei:
+            run_gpu(tg, files, cfg=cfg, batch=batch)
+        assert "device error flags" in str(ei.value)
