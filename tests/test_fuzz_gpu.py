@@ -234,3 +234,46 @@ def test_saturated_hexagon_indices_error_without_replay(monkeypatch):
         with pytest.raises(pcconv.PccError) as ei:
             run_gpu(tg, files, cfg=cfg, batch=batch)
         assert "device error flags" in str(ei.value)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_fuzz_big_sharded_matches_oracle(seed, tmp_path):
+    """1-6 M points over 3-8 thread ranks: dense slabs on every rank, heavy cells
+    shared when the clouds are clustered."""
+    from test_dist_cpu import check_against_oracle
+    files, cfg, batch, kind = big_case(seed)
+    out, res = _sharded(tmp_path, files, cfg, batch, [3, 4, 8][seed % 3], [0, 4][seed % 2])
+    check_against_oracle(tmp_path, files, out, res[0].summary, cfg=cfg, batch=batch)
+
+
+@pytest.mark.parametrize("seed", range(6, 10))
+def test_fuzz_big_merge_matches_oracle(seed):
+    files, cfg, batch, kind = big_case(seed)
+    first, second = halves(files)
+    with tempfile.TemporaryDirectory(dir=_shm()) as tg, tempfile.TemporaryDirectory(dir=_shm()) as to:
+        assert run_oracle(tg, first, cfg=cfg, batch=batch)[0] == 0
+        st = run_gpu(tg, second, cfg=None, batch=batch)
+        assert run_oracle(to, first + second, cfg=cfg, batch=batch)[0] == 0
+        d, mg, mo = compare_dirs(tg, to, fast=True)
+        assert d == [], (kind, cfg, batch, d, _explain(first + second, to, tg))
+        assert mg == mo
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_fuzz_wide_subgrid_matches_oracle(seed):
+    """Sub-grids of 97-200 (metadata.rs:67-78 reads any u32): the sequential
+    replay on the GPU, on the sweep's cases cut to 40 000 points."""
+    import numpy as np
+    files, cfg, batch, kind = mid_case(seed)
+    cfg = dict(cfg, sub_grid_dimension=int(np.random.default_rng(seed).integers(97, 201)))
+    left, cut = 40_000, []
+    for f in files:
+        cut.append(f[:max(0, min(len(f), left))])
+        left -= len(cut[-1])
+    with tempfile.TemporaryDirectory(dir=_shm()) as tg, tempfile.TemporaryDirectory(dir=_shm()) as to:
+        assert run_oracle(to, cut, cfg=cfg, batch=batch)[0] == 0
+        st = run_gpu(tg, cut, cfg=cfg, batch=batch)
+        assert st["sequential_replay"] == 1
+        d, mg, mo = compare_dirs(tg, to, fast=True)
+        assert d == [], (kind, cfg, batch, d, _explain(cut, to, tg))
+        assert mg == mo
