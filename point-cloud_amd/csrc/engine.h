@@ -280,6 +280,7 @@ private:
     struct Level;     // device tables of one level
     struct Dev;       // device buffers
     int fail(int code, const std::string& msg);
+    int geom_fail(const char* msg);
     void ev_begin(int stage);
     void ev_end(int stage);
     void ev_collect();

@@ -4817,6 +4817,16 @@ int Engine::fail(int code, const std::string& msg) {
     err_ = msg;
     return code;
 }
+// A point whose level-0 cell, layer or child route disagrees with the grid the
+// parallel binning laid out: at coordinates far from the origin (f32 spacing
+// near the sub-cell size) the separately rounded quotients x / cs and z / r
+// need not nest as they do nearer the origin.  build() replays such an input
+// sequentially (the reference's own per-point arithmetic) when it can.
+int Engine::geom_fail(const char* msg) {
+    geom_fault_ = true;
+    return fail(-34, std::string(msg) + " (coordinates far from the origin: the sequential replay takes inputs of "
+                                        "at most 2^24 points without merge or level range)");
+}
 
 void Engine::reserve(uint64_t n) {
     if (ext_in_) throw std::runtime_error("input added after borrowed keyed input");
@@ -5254,6 +5264,11 @@ int Engine::build() {
     const bool can_replay = !prior_ && !h0_ && !max_levels_ && n0 <= kWideMax && getenv("PCC_NO_REPLAY") == nullptr;
     ev_begin(ST_L0);
     int rc = level0_bin();   // also computes the bounding box (converter.rs:96-104)
+    if (rc && geom_fault_ && can_replay) {   // (see below: a level's geometry fault)
+        rc = replay_whole(src0, keys0, n0, "level-0 cells and layers inconsistent at this magnitude");
+        stats_.ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        return rc;
+    }
     if (rc) return rc;
     stats_.ms_level0_bin = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     for (uint32_t i = 0; !levels_.empty(); i++) {
@@ -6001,7 +6016,7 @@ int Engine::build_infinite() {
 // after a parallel attempt that hit geometry it cannot express: the levels and
 // statistics of that attempt are dropped, the input is the one it started from.
 int Engine::replay_whole(const Point* src, const uint32_t* keys, uint64_t n, const char* why) {
-    (void)why;
+    if (getenv("PCC_VERBOSE")) fprintf(stderr, "[pcc] sequential replay of the whole build: %s\n", why);
     HIP_CHECK(hipStreamSynchronize(stream_));
     for (Level* l : levels_) delete l;
     levels_.clear();
@@ -6299,7 +6314,7 @@ int Engine::level0_bin() {
             rc = enter_nonfinite(bad);
             return rc ? rc : level0_bin();
         }
-        if (bad) return fail(-34, "level-0 binning: layer outside the cell (internal error)");
+        if (bad) return geom_fail("level-0 binning: layer outside the cell (internal error)");
         fold = true;
         for (int a = 0; a < 3; a++) {
             bmin_[a] = bb[a];
@@ -6364,7 +6379,7 @@ int Engine::level0_bin() {
             uint32_t hc2[2];
             HIP_CHECK(hipMemcpyAsync(hc2, cnt, 8, hipMemcpyDeviceToHost, stream_));
             HIP_CHECK(hipStreamSynchronize(stream_));
-            if (hc2[1] & 1u) return fail(-34, "level-0 binning: point outside the bounding grid (internal error)");
+            if (hc2[1] & 1u) return geom_fail("level-0 binning: point outside the bounding grid (internal error)");
             if ((hc2[1] & 2u) || hc2[0] > cap * 6 / 10) continue;   // too full: grow and rebuild
             uint32_t* hcid = static_cast<uint32_t*>(dev_->get(cap * 4));
             k_l0_hash_flags<<<grid_for(cap, 256, 1u << 30), 256, 0, stream_>>>(hk, (uint32_t)cap, hcid);
@@ -6514,7 +6529,7 @@ int Engine::level0_bin() {
         scan_excl_u32(cflag, cscan, (uint32_t)G, d_tot + 2, dev_->scan, stream_);
         if (!defer) {
             readback({{tots, d_tot, 12}, {&hc, dev_->ctr, sizeof hc}});
-            if (hc.err) return fail(-34, "level-0 binning: point outside the bounding grid (internal error)");
+            if (hc.err) return geom_fail("level-0 binning: point outside the bounding grid (internal error)");
         }
     }
     if (defer) {   // upper bounds until the totals are read (below)
@@ -6651,7 +6666,7 @@ int Engine::level0_bin() {
     if (defer) {   // the level's one sync after the bounding box's: totals, lists, errors
         readback({{tots, d_tot, 12}, {&hc, dev_->ctr, sizeof hc}});
         ev_end(ST_L0);
-        if (hc.err) return fail(-34, "level-0 binning: point outside the bounding grid (internal error)");
+        if (hc.err) return geom_fail("level-0 binning: point outside the bounding grid (internal error)");
         if (tots[0] != nsrc_) return fail(-5, "level-0 histogram mismatch");
         L->ncells = tots[2];
         L->nslabs = tots[1];
@@ -6679,7 +6694,7 @@ int Engine::level0_bin() {
     HIP_CHECK(hipGetLastError());
     ev_end(ST_L0);
     readback({{&hc, dev_->ctr, sizeof hc}});
-    if (hc.err) return fail(-34, "level-0 capacities: routing error (internal error)");
+    if (hc.err) return geom_fail("level-0 capacities: routing error (internal error)");
     L->nbig = hc.nbig;
     L->nsmall = hc.nsmall;
     stats_.cells += L->ncells;

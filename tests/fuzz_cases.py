@@ -15,7 +15,7 @@ CELL_SIZES = [0.125, 1.0, 7.5, 100.0, 1000.0, 12345.0]
 KINDS = ["uniform", "gauss", "plane", "line", "lattice"]
 
 
-def mid_case(seed: int, nonfinite: bool = False):
+def mid_case(seed: int, nonfinite: bool = False, far: float = 0.0):
     """(files, cfg, batch, kind) for one seed; at most ~600 000 points and about
     5 000 cells (each cell is a file the canonical compare reads).  nonfinite:
     ~0.5 % of the points get NaN / +inf / -inf in one or two coordinates
@@ -33,6 +33,8 @@ def mid_case(seed: int, nonfinite: bool = False):
     kind = KINDS[seed % len(KINDS)]
     ext = cs * rng.uniform(0.3, 6.5, 3)   # 1-7 level-0 cells per axis
     off = cs * (rng.integers(-3, 4, 3) + rng.uniform(0.0, 1.0, 3))
+    if far:   # the cloud moved far from the origin (far cells: f32 spacing near the sub-cell size)
+        off = off + cs * far * np.sign(rng.uniform(-1.0, 1.0, 3))
     u = rng.uniform(0.0, 1.0, (n, 3))
     if kind == "gauss":
         k = int(rng.integers(1, 9))

@@ -60,6 +60,7 @@ def test_fuzz_matches_oracle(seed):
         assert mg == mo
         assert st["arrivals"] == arrivals
         assert st["grid_points"] + st["kept_points"] == st["number_of_points"]
+        assert st["sequential_replay"] == 0   # (the parallel levels, not the fallback)
 
 
 @pytest.mark.parametrize("seed", range(0, 48, 4))
@@ -277,3 +278,27 @@ def test_fuzz_wide_subgrid_matches_oracle(seed):
         d, mg, mo = compare_dirs(tg, to, fast=True)
         assert d == [], (kind, cfg, batch, d, _explain(cut, to, tg))
         assert mg == mo
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_fuzz_far_from_origin_matches_oracle(seed):
+    """The sweep's cases moved 10^3-10^7 cells from the origin, where the f32
+    spacing of the coordinates reaches the sub-cell size: points collapse onto
+    few slots and recurse deep (metadata.rs:100-102, hex.rs:67-85).  Where the
+    oracle converts, the GPU build equals it; where the reference cannot (the
+    depth limit, metadata.rs:92), the GPU build refuses too."""
+    import pcconv
+    far = [1e3, 1e4, 1e5, 3e5, 1e6, 1e7][seed % 6]
+    files, cfg, batch, kind = mid_case(seed, far=far)
+    with tempfile.TemporaryDirectory(dir=_shm()) as tg, tempfile.TemporaryDirectory(dir=_shm()) as to:
+        err, arrivals = run_oracle(to, files, cfg=cfg, batch=batch)
+        if err:
+            with pytest.raises(pcconv.PccError):
+                run_gpu(tg, files, cfg=cfg, batch=batch)
+            return
+        st = run_gpu(tg, files, cfg=cfg, batch=batch)
+        d, mg, mo = compare_dirs(tg, to, fast=True)
+        assert d == [], (kind, cfg, batch, far, d, _explain(files, to, tg))
+        assert mg == mo
+        if far <= 1e4:
+            assert st["sequential_replay"] == 0
