@@ -61,7 +61,7 @@ typedef struct pcc_stats {
     uint32_t level0_fold;               /* level-0 binning: 0 the three/four-pass path; 3 / 6 the two-pass
                                            fold over cells named by their indices modulo 2 / modulo 4 */
     uint32_t sequential_replay;         /* 1: the whole build ran as the sequential replay on the GPU
-                                           (sub_grid_dimension > 96, or hexagon indices saturated at deep
+                                           (sub_grid_dimension > 97, or hexagon indices saturated at deep
                                            levels, e.g. NaN-collapsed points far from the origin) */
 } pcc_stats;
 

@@ -32,6 +32,12 @@ def _check(files, cfg=None, batch=10_000, fast=False, synth_files=None, base=Non
         assert mg == mo
         assert st["arrivals"] == arrivals
         assert st["grid_points"] + st["kept_points"] == st["number_of_points"]
+        # the parallel levels ran, not the sequential replay (which sub-grids
+        # beyond the dense slot table take, from 97 or a little above)
+        if os.environ.get("PCC_TEST_WIDE"):
+            assert st["sequential_replay"] == 1
+        elif (cfg or {}).get("sub_grid_dimension", 96) <= 96:
+            assert st["sequential_replay"] == 0
         return st
 
 
