@@ -324,10 +324,20 @@ def main_sharded(args, rank, world):
     sys.stdout.flush()
     json_out = os.fdopen(os.dup(1), "w")
     os.dup2(2, 1)
+    # PCC_BENCH_BACKEND=gloo: this path with several ranks on ONE GPU (RCCL refuses
+    # two ranks on one device), collectives through host memory -- a rehearsal of
+    # the N > 1 line, never a measurement of it
+    backend = os.environ.get("PCC_BENCH_BACKEND", "nccl")
+    if backend == "gloo":
+        local %= max(1, torch.cuda.device_count())
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-    dist.init_process_group("nccl", device_id=dev)
-    comm = TorchComm(dev)
+    if backend == "gloo":
+        dist.init_process_group("gloo")
+    else:
+        dist.init_process_group("nccl", device_id=dev)
+    cdev = dev if backend != "gloo" else torch.device("cpu")
+    comm = TorchComm(cdev)
     a, b = key_range(args.points, rank, world)
     pts = torch.empty((b - a, 4), dtype=torch.int32, device=dev)
     pcconv.synth_device(pts.data_ptr(), a, b - a, args.seed, args.kind, -1000.0, 2000.0, local)
@@ -348,12 +358,12 @@ def main_sharded(args, rank, world):
     torch.cuda.synchronize()
     dist.barrier()
     torch.cuda.synchronize()
-    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=cdev)
     dist.all_reduce(el, op=dist.ReduceOp.MAX)
     ms = 1000.0 * float(el.item()) / args.steps
     st = res.local
     tot = torch.tensor([st["levels"], st["cells"], st["slabs"], st["arrivals"], res.recv_points], dtype=torch.int64,
-                       device=dev)
+                       device=cdev)
     per = [torch.zeros_like(tot) for _ in range(world)]
     dist.all_gather(per, tot)
     stage = shard_build(comm, ops, pts, a, files, sync=torch.cuda.synchronize).ms   # untimed split
@@ -363,8 +373,11 @@ def main_sharded(args, rank, world):
         k = prof[-1]
         dense_ms = sum(p["dense_ms"] for p in prof) / len(prof)
         rec = record(args, world, ms, max(p[0] for p in per), sum(p[1] for p in per), sum(p[2] for p in per),
-                     sum(p[3] for p in per), k, dense_ms, f"level-0 cell sharding over {world} ranks (grouped RCCL point-to-point exchange)")
-        rec["sharding"] = {"points_per_rank": [p[4] for p in per], "stage_ms_rank0": stage,
+                     sum(p[3] for p in per), k, dense_ms, f"level-0 cell sharding over {world} ranks ("
+                     + ("grouped RCCL point-to-point exchange)" if backend != "gloo" else "gloo rehearsal on one GPU)"))
+        if backend == "gloo":
+            rec["note"] = "REHEARSAL: ranks share one GPU, collectives over gloo (host); not a multi-GPU measurement"
+        rec["sharding"] = {"points_per_rank": [p[4] for p in per], "stage_ms_rank0": stage, "comm_backend": backend,
                            "hierarchies": res.summary["hierarchies"], "plan": res.plan,
                            "phases_rank0": res.local.get("phases")}
         json_out.write(json.dumps(rec) + "\n")
