@@ -3232,8 +3232,11 @@ __global__ void k_small_desc(const uint32_t* list, uint32_t nlist, const uint32_
     }
     // size class: 0..2 one wave (< 128, < 256, < 512 arrivals), 3 block; the
     // wave classes share wave_out, class c from offset c * nlist.  One global
-    // atomic per block and class.
-    const uint32_t cls = !in ? 4u : (D.n < kWaveMax / 4 ? 0u : (D.n < kWaveMax / 2 ? 1u : (D.n < kWaveMax ? 2u : 3u)));
+    // atomic per block and class.  A destination span of 2^16 points or more
+    // (a merge: child slabs with many seeds in front of their emissions) takes
+    // the block kernel, whose displaced-payload positions are 32-bit (the wave
+    // kernel's are 16-bit: WaveLds::fate)
+    const uint32_t cls = !in ? 4u : (D.dlen > 0xFFFFu ? 3u : (D.n < kWaveMax / 4 ? 0u : (D.n < kWaveMax / 2 ? 1u : (D.n < kWaveMax ? 2u : 3u))));
     const uint64_t lt = lanemask_lt();
     const uint32_t w = threadIdx.x / 64;
     uint32_t rank = 0;
@@ -3613,7 +3616,7 @@ template <int CH>
 struct WaveLds {
     static constexpr int TAB = 128 * CH;
     unsigned long long tab[TAB];
-    uint16_t fate[64 * CH];
+    uint16_t fate[64 * CH];   // displaced occupants' positions in the destination span (< 2^16: k_small_desc)
     uint32_t doff[kDests], dcap[kDests], dcur[kDests];
     uint32_t gcnt[kDests * kDests / 2];   // (child, grandchild) counts, 16 bits each
 };

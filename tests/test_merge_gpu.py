@@ -185,3 +185,24 @@ def test_poisoned_device_cache_parity_and_merge():
         else:
             os.environ["PCC_POISON_CACHE"] = old
         pcconv.release_device_cache()
+
+
+def test_merge_small_slab_with_large_child_rooms():
+    """A merge whose level-0 slabs are small (a dim-8 layer holds <= 196 grid
+    seeds, plus a few new points: the one-wave kernel) while their 24 child
+    slabs hold ~36 000 seeds each (level-1 cells that kept lists of ~94 000
+    points under a limit of 200 000): the slab's destination span is far above
+    2^16, so a displaced seed's position must not pass through a 16-bit field.
+    The new points sit exactly at the slot centres of 400 existing points, so
+    each displaces its slot's grid seed (d^2 = 0, cell.rs:77-80)."""
+    import numpy as np
+    import pyref
+    cfg = dict(sub_grid_dimension=8, cell_point_overflow_limit=200_000, max_cell_size=1000.0)
+    old = synth(71, 0, 6_000_000, lo=0.0, ext=999.0)
+    cr = pyref.sub_cell_size(cfg, pyref.cell_size(cfg, 0)) / np.float32(2.0)
+    pick = old[np.random.default_rng(5).choice(len(old), 400, replace=False)]
+    new = pick.copy()
+    for i, p in enumerate(pick):
+        c = pyref.hex_to_world(pyref.hex_from_world((p["x"], p["y"], p["z"]), cr), cr)
+        new[i]["x"], new[i]["y"], new[i]["z"] = c
+    _merge_check([old], [new], cfg=cfg, fast=True)
