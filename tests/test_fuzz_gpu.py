@@ -302,3 +302,32 @@ def test_fuzz_far_from_origin_matches_oracle(seed):
         assert mg == mo
         if far <= 1e4:
             assert st["sequential_replay"] == 0
+
+
+@pytest.mark.parametrize("seed", range(1, 48, 4))
+def test_fuzz_merge_displacing_seeds(seed):
+    """Merges whose new points sit exactly at the level-0 slot centres of
+    existing points (d^2 = 0: each displaces its slot's grid seed, cell.rs:77-80)
+    plus 2 % random ones, over the sweep's configs."""
+    import numpy as np
+    import pyref
+    files, cfg, batch, kind = mid_case(seed)
+    first, _ = halves(files)
+    old = first[0]
+    rng = np.random.default_rng(seed)
+    cr = pyref.sub_cell_size(cfg, pyref.cell_size(cfg, 0)) / np.float32(2.0)
+    pick = old[rng.choice(len(old), min(len(old), 500), replace=False)]
+    new = pick.copy()
+    for i, p in enumerate(pick):
+        c = pyref.hex_to_world(pyref.hex_from_world((p["x"], p["y"], p["z"]), cr), cr)
+        new[i]["x"], new[i]["y"], new[i]["z"] = c
+    extra = old[rng.choice(len(old), max(1, len(old) // 50), replace=False)].copy()
+    extra["x"] += np.float32(cfg["max_cell_size"] / 1000.0)
+    second = [np.concatenate([new, extra])]
+    with tempfile.TemporaryDirectory(dir=_shm()) as tg, tempfile.TemporaryDirectory(dir=_shm()) as to:
+        assert run_oracle(tg, first, cfg=cfg, batch=batch)[0] == 0
+        st = run_gpu(tg, second, cfg=None, batch=batch)
+        assert run_oracle(to, first + second, cfg=cfg, batch=batch)[0] == 0
+        d, mg, mo = compare_dirs(tg, to, fast=True)
+        assert d == [], (kind, cfg, batch, d, _explain(first + second, to, tg))
+        assert mg == mo
