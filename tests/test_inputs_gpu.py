@@ -351,3 +351,38 @@ def test_laz_cli_equals_las(tmp_path, formats):
     d, ma, mb = compare_dirs(out_las, out_laz, fast=False)
     assert d == [] and ma == mb
     assert ma["number_of_points"] == 165_000
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_las_cli_random_transforms(seed):
+    """Randomised LAS inputs through the CLI: point formats 0-10, LAS 1.2 / 1.4,
+    scales 10^-4..10 with odd mantissas, offsets up to 10^6 with fractions,
+    integer ranges up to the whole i32, 1-3 files (converter/las.rs:23-46:
+    scale * X + offset in f64, then as f32), against the oracle on the numpy
+    decoding."""
+    from las_util import COLOR_OFF, REC
+    rng = np.random.default_rng(900 + seed)
+    with tempfile.TemporaryDirectory() as td:
+        files, decoded = [], []
+        for k in range(int(rng.integers(1, 4))):
+            fmt = int(rng.choice(sorted(REC)))
+            minor = 4 if fmt >= 6 else int(rng.choice([2, 4]))
+            n = int(rng.integers(1, 60_000))
+            scale = tuple(float(np.float64(rng.choice([1, 3, 7, 125, 333])) * 10.0 ** int(rng.integers(-6, 0)))
+                          for _ in range(3))
+            offset = tuple(float(rng.choice([0.0, rng.uniform(-1e6, 1e6), float(rng.integers(-500_000, 500_000)) + 0.5]))
+                           for _ in range(3))
+            span = int(rng.choice([1000, 100_000, 10_000_000, 2**31 - 1]))
+            lim = [min(span, int(1000.0 / s)) + 1 for s in scale]   # (about +-1000 units around the offset)
+            X, Y, Z = (rng.integers(-m, m, n) for m in lim)
+            rgb = rng.integers(0, 65536, (n, 3)) if COLOR_OFF[fmt] is not None else None
+            path = os.path.join(td, f"f{k}.las")
+            write_las(path, X, Y, Z, scale, offset, fmt=fmt, rgb=rgb, minor=minor)
+            files.append(path)
+            decoded.append(decode(X, Y, Z, scale, offset, rgb))
+        out = os.path.join(td, "out")
+        _cli(files, out)
+        ref = os.path.join(td, "ref")
+        _oracle_dir(ref, decoded)
+        d, mg, mo = compare_dirs(out, ref, fast=True)
+        assert d == [] and mg == mo, d
