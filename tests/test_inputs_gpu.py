@@ -386,3 +386,38 @@ def test_las_cli_random_transforms(seed):
         _oracle_dir(ref, decoded)
         d, mg, mo = compare_dirs(out, ref, fast=True)
         assert d == [] and mg == mo, d
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_ply_cli_random_layouts(seed):
+    """Randomised binary PLY vertex layouts through the CLI: x/y/z as float or
+    double, colours as uchar, float or absent, extra properties of other types
+    interleaved in any order, little or big endian, 1-2 files
+    (ply.rs:36-73, point.rs:61-130), against the oracle on the numpy decoding."""
+    rng = np.random.default_rng(700 + seed)
+    with tempfile.TemporaryDirectory() as td:
+        files, expect = [], []
+        for k in range(int(rng.integers(1, 3))):
+            n = int(rng.integers(1, 50_000))
+            lo, ext = float(rng.uniform(-3000, 1000)), float(rng.uniform(10, 4000))
+            cols = [(a, str(rng.choice(["float", "double"])), rng.uniform(lo, lo + ext, n)) for a in "xyz"]
+            for ch in ("red", "green", "blue", "alpha"):
+                t = str(rng.choice(["uchar", "float", "none"]))
+                if t == "uchar":
+                    cols.append((ch, t, rng.integers(0, 256, n)))
+                elif t == "float":
+                    cols.append((ch, t, rng.uniform(-100, 70_000, n).astype(np.float32)))
+            for e in range(int(rng.integers(0, 4))):
+                t = str(rng.choice(["ushort", "int", "uchar", "double"]))
+                cols.append((f"extra{e}", t, rng.integers(0, 200, n)))
+            order = rng.permutation(len(cols))
+            cols = [cols[i] for i in order]
+            path = os.path.join(td, f"f{k}.ply")
+            _write_ply_props(path, cols, enc=str(rng.choice(["binary_little_endian", "binary_big_endian"])))
+            files.append(path)
+            expect.append(_ply_expect(cols))
+        out, ref = os.path.join(td, "out"), os.path.join(td, "ref")
+        _cli(files, out)
+        _oracle_dir(ref, expect)
+        d, mg, mo = compare_dirs(out, ref, fast=True)
+        assert d == [] and mg == mo, d
