@@ -5495,6 +5495,12 @@ bool Engine::pre6_run(uint64_t upto, hipEvent_t after, bool all) {
     if (after) HIP_CHECK(hipStreamWaitEvent(stream_, after, 0));
     const uint32_t ntl = all ? (uint32_t)tl : gend * pre6_tpg_;
     const uint64_t n = all ? upto : (uint64_t)ntl * kL0Tile;
+    // the arenas were sized for the input reserved when pass 1 was decided; a
+    // later file grew the input (reserve) past them: the build runs pass 1
+    if (n > dev_->cap || dev_->ar[1].p != pre6_ar1_) {
+        pre6_ = false;
+        return true;
+    }
     Arena dummy{static_cast<float4*>(d_pre6_dummy_),
                 reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(d_pre6_dummy_) + 256ull * kL0BS * kL0IPT * 16)};
     k_l0_tile6<false><<<gend - pre6_gdone_, kL0BS, 0, stream_>>>(d_in_, nullptr, dev_->ar[1], n, l0_base_params(cfg_, 0),

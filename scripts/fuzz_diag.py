@@ -50,6 +50,13 @@ for rep in range(reps):
         for k in sorted(set(co) & set(cg)):
             if co[k] == cg[k]:
                 continue
+            if co[k][1] != cg[k][1]:
+                ga = sorted(index.get(bytes(co[k][1][j:j + 16]), -1) for j in range(0, len(co[k][1]), 16))
+                gb = sorted(index.get(bytes(cg[k][1][j:j + 16]), -1) for j in range(0, len(cg[k][1]), 16))
+                print(" cell", k, "grid only oracle", sorted(set(ga) - set(gb))[:16], "only gpu",
+                      sorted(set(gb) - set(ga))[:16], flush=True)
+                for i in sorted(set(ga) ^ set(gb))[:8]:
+                    print("   point", i, allp[i], flush=True)
             for (ia, la), (ib, lb) in zip(co[k][2], cg[k][2]):
                 if la != lb:
                     ka = [index.get(bytes(la[j:j + 16]), -1) for j in range(0, len(la or b""), 16)]

@@ -419,3 +419,20 @@ def test_long_kept_lists_radix_sorted(limit):
     p = synth(98, 1, 400_000)
     _check([p[:150_000], p[150_000:151_111], p[151_111:]], cfg=dict(sub_grid_dimension=8, cell_point_overflow_limit=limit),
            batch=6_000, fast=True)
+
+
+def test_upload_growing_past_the_first_reservation():
+    """Files added one by one, each growing the reserved input: level-0 pass 1
+    behind the upload was decided on the first file's reservation, and the
+    second file's tiles reached past the arenas sized for it (found by the
+    bulk sweep, seed 1658: a line of points whose key order the stray stores
+    permuted).  Pass 1 now stops behind the upload when the input outgrows the
+    arenas; == the oracle, and == the build with that pass disabled."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from fuzz_cases import mid_case
+    files, cfg, batch, _ = mid_case(1658)
+    assert [len(f) for f in files] == [4084, 4030, 14950]
+    _check(files, cfg=cfg, batch=batch, fast=True)
+    p = synth(77, 0, 50_000)
+    _check([p[:5000], p[5000:11000], p[11000:]], fast=True)
